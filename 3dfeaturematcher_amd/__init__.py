@@ -1,0 +1,360 @@
+"""3dfeaturematcher_amd -- MI355X-native hot path of caomw/3DFeatureMatcher.
+
+Python mirror of the reference's operator interface for the path
+(``DescriptorsMatcher`` / ``SingleCameraTriangulator`` / ``NormalOptimizer``,
+``main.cpp:91-155``), bound with ctypes to the C ABI of ``libfm3d.so``
+(``include/fm3d.h``).  All compute runs in the HIP kernels of the library; there
+is no CPU fallback -- constructing a context without the library or without a
+GPU raises ``Fm3dError``.
+
+The package directory name starts with a digit, so import it with
+``importlib.import_module("3dfeaturematcher_amd")``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfm3d.so")
+
+FM3D_OK = 0
+ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
+DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
+ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
+
+# every symbol include/fm3d.h declares (tests check the library exports all of them)
+EXPORTS = (
+    "fm3d_settings_default", "fm3d_settings_load", "fm3d_ctx_create", "fm3d_ctx_destroy", "fm3d_last_error",
+    "fm3d_ctx_set_stream", "fm3d_knn2", "fm3d_match_nndr", "fm3d_setg12", "fm3d_g12_from_poses",
+    "fm3d_camera2_from_g12", "fm3d_set_g12", "fm3d_get_camera2", "fm3d_triangulate", "fm3d_set_images",
+    "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",
+    "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
+)
+
+
+class Fm3dError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"fm3d error {code}: {msg}")
+        self.code = code
+
+
+class Settings(ctypes.Structure):
+    """fm3d_settings (the build/settings.yml keys of the path)."""
+    _fields_ = [
+        ("Fx", ctypes.c_double), ("Fy", ctypes.c_double), ("Cx", ctypes.c_double), ("Cy", ctypes.c_double),
+        ("p1", ctypes.c_double), ("p2", ctypes.c_double), ("k0", ctypes.c_double), ("k1", ctypes.c_double),
+        ("k2", ctypes.c_double), ("rodriguesIC", ctypes.c_double * 3), ("translationIC", ctypes.c_double * 3),
+        ("zThresholdMin", ctypes.c_double), ("zThresholdMax", ctypes.c_double), ("epsilonLMMIN", ctypes.c_double),
+        ("pixelsRay", ctypes.c_int), ("pyramids", ctypes.c_int), ("nndrEpsilon", ctypes.c_double),
+        ("pos1", ctypes.c_double * 6), ("pos2", ctypes.c_double * 6), ("boundWidth", ctypes.c_int),
+        ("boundHeight", ctypes.c_int), ("strictNanExit", ctypes.c_int), ("lmWaves", ctypes.c_int),
+    ]
+
+    @staticmethod
+    def default() -> "Settings":
+        s = Settings()
+        _check(lib().fm3d_settings_default(ctypes.byref(s)))
+        return s
+
+    @staticmethod
+    def load(path: str) -> "Settings":
+        s = Settings()
+        _check(lib().fm3d_settings_load(path.encode(), ctypes.byref(s)))
+        return s
+
+    def camera(self):
+        """(fx, fy, cx, cy, (k1, k2, p1, p2, k3)) in OpenCV order."""
+        return self.Fx, self.Fy, self.Cx, self.Cy, (self.k0, self.k1, self.p1, self.p2, self.k2)
+
+    def set_camera(self, cam) -> None:
+        self.Fx, self.Fy, self.Cx, self.Cy = cam.fx, cam.fy, cam.cx, cam.cy
+        self.k0, self.k1, self.p1, self.p2, self.k2 = cam.k
+
+
+DMATCH = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
+RECORD = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("distance", "<f4"), ("status", "<i4"),
+                   ("point", "<f8", (3,)), ("normal", "<f8", (3,))])
+
+
+class LMStats(ctypes.Structure):
+    _fields_ = [("points_in", ctypes.c_int64), ("points_kept", ctypes.c_int64), ("evaluations", ctypes.c_int64),
+                ("pixel_evaluations", ctypes.c_int64), ("drops", ctypes.c_int64 * 8), ("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {"points_in": self.points_in, "points_kept": self.points_kept, "evaluations": self.evaluations,
+                "pixel_evaluations": self.pixel_evaluations, "drops": list(self.drops), "kernel_ms": self.kernel_ms}
+
+
+class PipelineStats(ctypes.Structure):
+    _fields_ = [("queries", ctypes.c_int64), ("trains", ctypes.c_int64), ("matches", ctypes.c_int64),
+                ("inliers", ctypes.c_int64), ("kept", ctypes.c_int64), ("match_ms", ctypes.c_double),
+                ("nndr_ms", ctypes.c_double), ("triangulate_ms", ctypes.c_double), ("pyramid_ms", ctypes.c_double),
+                ("lm_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("lm", LMStats)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "lm"}
+        d["lm"] = self.lm.as_dict()
+        return d
+
+
+_LIB = None
+
+
+def lib():
+    """Load libfm3d.so (built by __graft_entry__.build()); raises if absent."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise Fm3dError(ERR_HIP, f"{LIB_PATH} missing: build it with __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        L.fm3d_last_error.restype = ctypes.c_char_p
+        L.fm3d_version.restype = ctypes.c_char_p
+        _LIB = L
+    return _LIB
+
+
+def _check(code, ctx=None):
+    if code != FM3D_OK:
+        msg = ""
+        if ctx is not None:
+            msg = (lib().fm3d_last_error(ctx) or b"").decode(errors="replace")
+        raise Fm3dError(code, msg)
+
+
+def _ptr(a, t=ctypes.c_double):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _vp(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Context:
+    """One fm3d_ctx: device buffers + a HIP stream on one GPU."""
+
+    def __init__(self, settings: Settings | None = None, device: int = 0):
+        self.settings = settings if settings is not None else Settings.default()
+        self._h = ctypes.c_void_p()
+        rc = lib().fm3d_ctx_create(ctypes.byref(self.settings), ctypes.c_int(device), ctypes.byref(self._h))
+        if rc != FM3D_OK:
+            raise Fm3dError(rc, "fm3d_ctx_create failed (no HIP device / runtime?)")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().fm3d_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, code):
+        _check(code, self._h)
+
+    def set_stream(self, hip_stream: int | None):
+        self.check(lib().fm3d_ctx_set_stream(self._h, ctypes.c_void_p(hip_stream or 0)))
+
+
+def _desc_type(desc: np.ndarray, binary: bool) -> int:
+    if binary:
+        return DESC_BITS
+    if desc.dtype == np.uint8:
+        return DESC_U8
+    if desc.dtype == np.float32:
+        return DESC_F32
+    raise TypeError("descriptors must be uint8 (SIFT-like), float32 or binary uint8 (binary=True)")
+
+
+class DescriptorsMatcher:
+    """DescriptorsMatcher (DescriptorsMatcher/descriptorsmatcher.h:39-111), matcher + NNDR part.
+
+    Feature detection/description (descriptorsmatcher.cpp:110-115) is upstream of
+    the hot path: this class takes the descriptor matrices directly.
+    """
+
+    def __init__(self, ctx: Context, binary: bool = False):
+        self.ctx = ctx
+        self.binary = binary
+
+    def knn_match(self, desc_a: np.ndarray, desc_b: np.ndarray) -> np.ndarray:
+        """knnMatch(A, B, k=2) (descriptorsmatcher.cpp:89-105) -> (nA, 2) DMATCH array."""
+        a = np.ascontiguousarray(desc_a)
+        b = np.ascontiguousarray(desc_b)
+        out = np.zeros((a.shape[0], 2), dtype=DMATCH)
+        self.ctx.check(lib().fm3d_knn2(self.ctx.handle, _vp(a), a.shape[0], _vp(b), b.shape[0], a.shape[1],
+                                       _desc_type(a, self.binary), _vp(out)))
+        return out
+
+    def compareWithNNDR(self, epsilon: float, desc_a: np.ndarray, desc_b: np.ndarray,
+                        matches: np.ndarray | None = None) -> np.ndarray:
+        """compareWithNNDR (descriptorsmatcher.cpp:107-131).  Like the reference, new
+        matches are APPENDED to `matches` (the reference pushes back without clearing)."""
+        a = np.ascontiguousarray(desc_a)
+        b = np.ascontiguousarray(desc_b)
+        out = np.zeros(max(a.shape[0], 1), dtype=DMATCH)
+        n = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_match_nndr(self.ctx.handle, _vp(a), a.shape[0], _vp(b), b.shape[0], a.shape[1],
+                                             _desc_type(a, self.binary), ctypes.c_double(epsilon), _vp(out),
+                                             ctypes.byref(n)))
+        new = out[:n.value].copy()
+        return new if matches is None else np.concatenate([matches, new])
+
+
+class SingleCameraTriangulator:
+    """SingleCameraTriangulator (Triangulator/singlecameratriangulator.h:52-93), hot-path methods."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._kp1 = self._kp2 = self._matches = None
+
+    def setg12(self, T1, T2, r1, r2) -> np.ndarray:
+        g = np.zeros(16)
+        f64 = lambda v: np.ascontiguousarray(v, dtype=np.float64)
+        self.ctx.check(lib().fm3d_setg12(self.ctx.handle, _ptr(f64(T1)), _ptr(f64(T2)), _ptr(f64(r1)),
+                                         _ptr(f64(r2)), _ptr(g)))
+        return g.reshape(4, 4)
+
+    def set_g12(self, g12) -> None:
+        self.ctx.check(lib().fm3d_set_g12(self.ctx.handle, _ptr(np.ascontiguousarray(g12, dtype=np.float64))))
+
+    def camera2(self):
+        R2 = np.zeros(9)
+        t2 = np.zeros(3)
+        self.ctx.check(lib().fm3d_get_camera2(self.ctx.handle, _ptr(R2), _ptr(t2)))
+        return R2.reshape(3, 3), t2
+
+    def setKeypoints(self, kpts1: np.ndarray, kpts2: np.ndarray, matches: np.ndarray) -> None:
+        """setKeypoints (:145-171): keypoint positions (N, 2) float32 + DMATCH array."""
+        self._kp1 = np.ascontiguousarray(kpts1, dtype=np.float32)
+        self._kp2 = np.ascontiguousarray(kpts2, dtype=np.float32)
+        self._matches = np.ascontiguousarray(matches, dtype=DMATCH)
+
+    def triangulate(self):
+        """triangulate (:173-230) -> (points (P, 3) float64, outliersMask (K,) bool)."""
+        K = self._matches.shape[0]
+        pts = np.zeros((max(K, 1), 3))
+        mask = np.zeros(max(K, 1), dtype=np.uint8)
+        n = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_triangulate(self.ctx.handle, _vp(self._kp1), self._kp1.shape[0], _vp(self._kp2),
+                                              self._kp2.shape[0], _vp(self._matches), K, _ptr(pts),
+                                              _ptr(mask, ctypes.c_uint8), ctypes.byref(n)))
+        return pts[:n.value].copy(), mask[:K].astype(bool)
+
+
+class NormalOptimizer:
+    """NormalOptimizer (Triangulator/normaloptimizer.h:43-59), hot-path methods."""
+
+    def __init__(self, ctx: Context, sct: SingleCameraTriangulator | None = None):
+        self.ctx = ctx
+        self.sct = sct
+        self.last_status = self.last_info = self.last_nfev = None
+        self.last_stats = None
+
+    def setImages(self, img1: np.ndarray, img2: np.ndarray) -> None:
+        a = np.ascontiguousarray(img1, dtype=np.uint8)
+        b = np.ascontiguousarray(img2, dtype=np.uint8)
+        if a.shape != b.shape or a.ndim != 2:
+            raise ValueError("two gray images of the same size expected")
+        h, w = a.shape
+        self.ctx.check(lib().fm3d_set_images(self.ctx.handle, _ptr(a, ctypes.c_uint8), _ptr(b, ctypes.c_uint8), w, h, w))
+
+    def pyramid(self, which: int, level: int) -> np.ndarray:
+        w = ctypes.c_int(0)
+        h = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_get_pyramid_level(self.ctx.handle, which, level, None, ctypes.byref(w),
+                                                    ctypes.byref(h)))
+        out = np.zeros((h.value, w.value), dtype=np.uint8)
+        self.ctx.check(lib().fm3d_get_pyramid_level(self.ctx.handle, which, level, _ptr(out, ctypes.c_uint8),
+                                                    ctypes.byref(w), ctypes.byref(h)))
+        return out
+
+    def startVisualizerThread(self):  # PCL viewer: out of scope, no-op
+        pass
+
+    def stopVisualizerThread(self):
+        pass
+
+    def computeOptimizedNormals(self, points3D: np.ndarray):
+        """computeOptimizedNormals (normaloptimizer.cpp:321-452).
+
+        Returns (kept points, normals): failed points are erased (stable order),
+        exactly like the reference mutates its std::vector.  Per-input-point status,
+        lmdif info and evaluation counts are left in last_status / last_info / last_nfev.
+        """
+        P = np.ascontiguousarray(points3D, dtype=np.float64).reshape(-1, 3).copy()
+        n = P.shape[0]
+        normals = np.zeros((max(n, 1), 3))
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        info = np.zeros((max(n, 1), 8), dtype=np.int32)
+        nfev = np.zeros((max(n, 1), 8), dtype=np.int32)
+        kept = ctypes.c_int(0)
+        st = LMStats()
+        self.ctx.check(lib().fm3d_optimize_normals(self.ctx.handle, _ptr(P), n, _ptr(normals),
+                                                   _ptr(status, ctypes.c_int32), _ptr(info, ctypes.c_int32),
+                                                   _ptr(nfev, ctypes.c_int32), ctypes.byref(kept), ctypes.byref(st)))
+        self.last_status, self.last_info, self.last_nfev = status[:n], info[:n], nfev[:n]
+        self.last_stats = st.as_dict()
+        k = kept.value
+        return P[:k].copy(), normals[:k].copy()
+
+
+class Pipeline:
+    """Whole hot path with inputs resident in HBM (bench / multi-GPU shards)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.n_queries = 0
+
+    def upload(self, desc_a, desc_b, kp1, kp2, img1, img2, binary=False, query_offset=0):
+        a = np.ascontiguousarray(desc_a)
+        b = np.ascontiguousarray(desc_b)
+        k1 = np.ascontiguousarray(kp1, dtype=np.float32)
+        k2 = np.ascontiguousarray(kp2, dtype=np.float32)
+        i1 = np.ascontiguousarray(img1, dtype=np.uint8)
+        i2 = np.ascontiguousarray(img2, dtype=np.uint8)
+        h, w = i1.shape
+        self.n_queries = a.shape[0]
+        self.ctx.check(lib().fm3d_pipeline_upload(self.ctx.handle, _vp(a), a.shape[0], _vp(b), b.shape[0],
+                                                  a.shape[1], _desc_type(a, binary), _vp(k1), _vp(k2),
+                                                  _ptr(i1, ctypes.c_uint8), _ptr(i2, ctypes.c_uint8), w, h,
+                                                  query_offset))
+
+    def run(self, records_dev_ptr: int | None = None):
+        """One pass; returns (n_kept, stats dict).  records_dev_ptr: device buffer
+        (e.g. a torch tensor's data_ptr()) with room for n_queries records."""
+        n = ctypes.c_int(0)
+        st = PipelineStats()
+        self.ctx.check(lib().fm3d_pipeline_run(self.ctx.handle, ctypes.c_void_p(records_dev_ptr or 0),
+                                               ctypes.byref(n), ctypes.byref(st)))
+        return n.value, st.as_dict()
+
+    def records(self, n: int, records_dev_ptr: int | None = None) -> np.ndarray:
+        out = np.zeros(max(n, 1), dtype=RECORD)
+        self.ctx.check(lib().fm3d_records_download(self.ctx.handle, ctypes.c_void_p(records_dev_ptr or 0), n,
+                                                   _vp(out)))
+        return out[:n]
+
+
+def g12_from_poses(settings: Settings, T1, T2, r1, r2) -> np.ndarray:
+    """Context-free setg12 algebra (host only)."""
+    g = np.zeros(16)
+    f64 = lambda v: np.ascontiguousarray(v, dtype=np.float64)
+    _check(lib().fm3d_g12_from_poses(ctypes.byref(settings), _ptr(f64(T1)), _ptr(f64(T2)), _ptr(f64(r1)),
+                                     _ptr(f64(r2)), _ptr(g)))
+    return g.reshape(4, 4)
+
+
+def camera2_from_g12(g12):
+    R2 = np.zeros(9)
+    t2 = np.zeros(3)
+    _check(lib().fm3d_camera2_from_g12(_ptr(np.ascontiguousarray(g12, dtype=np.float64).ravel()), _ptr(R2), _ptr(t2)))
+    return R2.reshape(3, 3), t2

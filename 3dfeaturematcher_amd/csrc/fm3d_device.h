@@ -1,0 +1,137 @@
+// fm3d_device.h -- device-side arithmetic shared by the fm3d kernels.
+//
+// Every function restates one reference/OpenCV-2.4 operation with its exact
+// IEEE operation order (the library is compiled with -ffp-contract=off, so no
+// FMA contraction): results are bit-identical to the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fm3d_detmath.h"
+
+namespace fm3d {
+
+struct Camera {
+    double fx, fy, cx, cy;
+    double k[5];  // OpenCV order k1,k2,p1,p2,k3 (settings k0,k1,p1,p2,k2; singlecameratriangulator.cpp:99-105)
+};
+
+// cv::undistortPoints (OpenCV 2.4 cvUndistortPoints), 5 iterations, R = I.
+// Reference call sites: singlecameratriangulator.cpp:169-170 (keypoints), :542 (neighbourhood).
+__host__ __device__ inline void undistort1(const Camera& c, double x, double y, double& ox, double& oy) {
+    const double ifx = 1. / c.fx, ify = 1. / c.fy;
+    double x0, y0;
+    x0 = x = (x - c.cx) * ifx;
+    y0 = y = (y - c.cy) * ify;
+    for (int j = 0; j < 5; j++) {
+        double r2 = x * x + y * y;
+        double icdist = (1 + ((0. * r2 + 0.) * r2 + 0.) * r2) / (1 + ((c.k[4] * r2 + c.k[1]) * r2 + c.k[0]) * r2);
+        double deltaX = 2 * c.k[2] * x * y + c.k[3] * (r2 + 2 * x * x);
+        double deltaY = c.k[2] * (r2 + 2 * y * y) + 2 * c.k[3] * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    double xx = 1. * x + 0. * y + 0.;
+    double yy = 0. * x + 1. * y + 0.;
+    double ww = 1. / (0. * x + 0. * y + 1.);
+    ox = xx * ww;
+    oy = yy * ww;
+}
+
+// cv::projectPoints (OpenCV 2.4 cvProjectPoints2) of one point, rotation matrix R
+// (row-major) and translation t.  Call sites: :388 (R = I, t = 0), :602 (camera 2).
+__host__ __device__ inline void project1(const Camera& c, const double* R, const double* t, double X, double Y,
+                                         double Z, double& u, double& v) {
+    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    z = z ? 1. / z : 1;
+    x *= z;
+    y *= z;
+    double r2 = x * x + y * y;
+    double r4 = r2 * r2;
+    double r6 = r4 * r2;
+    double a1 = 2 * x * y;
+    double a2 = r2 + 2 * x * x;
+    double a3 = r2 + 2 * y * y;
+    double cdist = 1 + c.k[0] * r2 + c.k[1] * r4 + c.k[4] * r6;
+    double icdist2 = 1. / (1 + 0. * r2 + 0. * r4 + 0. * r6);
+    double xd = x * cdist * icdist2 + c.k[2] * a1 + c.k[3] * a2;
+    double yd = y * cdist * icdist2 + c.k[2] * a3 + c.k[3] * a1;
+    u = xd * c.fx + c.cx;
+    v = yd * c.fy + c.cy;
+}
+
+// getBilinearInterpPix32f (tools.cpp:129-142) on a continuous 8-bit image that is
+// followed by >= 2*w+2 zero bytes (the reference reads unchecked one row/col past
+// the image when isPixelGood admits x == cols or y == rows).
+__device__ inline float bilinear(const uint8_t* __restrict__ img, int w, float x, float y) {
+    int x0 = (int)floor((double)x), y0 = (int)floor((double)y);
+    const uint8_t* p0 = img + (long)y0 * w + x0;
+    const uint8_t* p1 = p0 + w;
+    float b00 = (float)p0[0], b10 = (float)p1[0], b01 = (float)p0[1], b11 = (float)p1[1];
+    float xm0 = 1.0f - (x - (float)x0), xm1 = (x - (float)x0);
+    float ym0 = 1.0f - (y - (float)y0), ym1 = (y - (float)y0);
+    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
+}
+
+// isPixelGood (singlecameratriangulator.cpp:657-665).  NaN coordinates are bad
+// (the reference has undefined behaviour for them).
+__host__ __device__ inline bool pixel_good(double x, double y, double scale, int cols, int rows) {
+    if (x != x || y != y) return false;
+    if ((x < 0) || (x > ((1 / scale) * cols)) || (y < 0) || (y > ((1 / scale) * rows))) return false;
+    return true;
+}
+
+// MINPACK enorm, accumulated element by element in index order (lmfit lm_enorm).
+struct Enorm {
+    double s1, s2, s3, x1max, x3max, agiant;
+    __host__ __device__ inline void init(int n) {
+        s1 = s2 = s3 = x1max = x3max = 0.;
+        agiant = 1.304e19 / (double)n;
+    }
+    __host__ __device__ inline void add(double x) {
+        const double rdwarf = 3.834e-20;
+        double xabs = fabs(x), temp;
+        if (xabs > rdwarf && xabs < agiant) {
+            s2 += xabs * xabs;
+        } else if (xabs > rdwarf) {
+            if (xabs > x1max) {
+                temp = x1max / xabs;
+                s1 = 1 + s1 * temp * temp;
+                x1max = xabs;
+            } else {
+                temp = xabs / x1max;
+                s1 += temp * temp;
+            }
+        } else {
+            if (xabs > x3max) {
+                temp = x3max / xabs;
+                s3 = 1 + s3 * temp * temp;
+                x3max = xabs;
+            } else if (xabs != 0.) {
+                temp = xabs / x3max;
+                s3 += temp * temp;
+            }
+        }
+    }
+    __host__ __device__ inline double finish() const {
+        if (s1 != 0) return x1max * sqrt(s1 + (s2 / x1max) / x1max);
+        if (s2 != 0) {
+            if (s2 >= x3max) return sqrt(s2 * (1 + (x3max / s2) * (x3max * s3)));
+            return sqrt(x3max * ((s2 / x3max) + (x3max * s3)));
+        }
+        return x3max * sqrt(s3);
+    }
+};
+
+__host__ __device__ inline double enorm2(const double* x) {
+    Enorm e;
+    e.init(2);
+    e.add(x[0]);
+    e.add(x[1]);
+    return e.finish();
+}
+
+}  // namespace fm3d

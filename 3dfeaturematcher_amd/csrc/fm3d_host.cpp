@@ -1,0 +1,931 @@
+// fm3d_host.cpp -- C ABI (include/fm3d.h): context, host algebra, orchestration.
+//
+// Host-side algebra restates the reference's scalar code (setg12, Rodrigues,
+// Matx44d::inv) with the same operation order as oracle/fm3d_oracle.c; the heavy
+// per-keypoint work runs in the HIP kernels of fm3d_match.hip, fm3d_misc.hip and
+// fm3d_lm.hip.  There is no CPU fallback: without a GPU every compute entry point
+// fails with FM3D_ERR_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fm3d.h"
+#include "fm3d_kernels.h"
+
+using fm3d::Camera;
+using fm3d::LevelDesc;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t alloc = n < 256 ? 256 : n;
+        hipError_t e = hipMalloc(&p, alloc);
+        if (e == hipSuccess) bytes = alloc;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const {
+        return (T*)p;
+    }
+};
+
+constexpr size_t kGuard(int w) { return (size_t)4 * w + 64; }
+
+}  // namespace
+
+struct fm3d_ctx {
+    fm3d_settings s;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool ownStream = false;
+    Camera cam{};
+    double g12[16];
+    double R2[9], t2[3];
+    bool haveG12 = false;
+    // pyramids
+    int w = 0, h = 0;
+    std::vector<int> lw, lh;
+    std::vector<DevBuf> pyr1, pyr2;
+    DevBuf lvlDesc;
+    // circle offsets of pixelsRay
+    DevBuf offsets;
+    int nOff = 0;
+    // work buffers
+    DevBuf A, B, cqA, ctB, idx, key, fkey, knnOut, cand, flag, matches, count, scanTmp;
+    DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
+    DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, slab, slabI1;
+    DevBuf records, recTmp, recFlag;
+    // staged pipeline inputs
+    int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
+    bool staged = false;
+    hipEvent_t ev[8];
+    std::string err;
+};
+
+namespace {
+
+int fail(fm3d_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return fail((ctx), FM3D_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------- host algebra (same operation order as the oracle) ----------------
+void rodrigues_v2m(const double r[3], double R[9]) {
+    double rx = r[0], ry = r[1], rz = r[2];
+    double theta = std::sqrt(rx * rx + ry * ry + rz * rz);
+    if (theta < DBL_EPSILON) {
+        for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? 1. : 0.;
+        return;
+    }
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double c = std::cos(theta), s = std::sin(theta), c1 = 1. - c;
+    double itheta = theta ? 1. / theta : 0.;
+    rx *= itheta;
+    ry *= itheta;
+    rz *= itheta;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rxm[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    for (int k = 0; k < 9; k++) R[k] = c * I[k] + c1 * rrt[k] + s * rxm[k];
+}
+
+void inv_t3(const double A[9], double out[9]) {
+    double c00 = A[4] * A[8] - A[5] * A[7];
+    double c01 = A[5] * A[6] - A[3] * A[8];
+    double c02 = A[3] * A[7] - A[4] * A[6];
+    double c10 = A[2] * A[7] - A[1] * A[8];
+    double c11 = A[0] * A[8] - A[2] * A[6];
+    double c12 = A[1] * A[6] - A[0] * A[7];
+    double c20 = A[1] * A[5] - A[2] * A[4];
+    double c21 = A[2] * A[3] - A[0] * A[5];
+    double c22 = A[0] * A[4] - A[1] * A[3];
+    double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+    double id = 1. / det;
+    out[0] = c00 * id;
+    out[1] = c01 * id;
+    out[2] = c02 * id;
+    out[3] = c10 * id;
+    out[4] = c11 * id;
+    out[5] = c12 * id;
+    out[6] = c20 * id;
+    out[7] = c21 * id;
+    out[8] = c22 * id;
+}
+
+// cvRodrigues2 matrix -> vector; polar factor by three Newton steps (OpenCV: SVD U*V^T)
+void rodrigues_m2v(const double Rin[9], double r[3]) {
+    double R[9], Y[9];
+    std::memcpy(R, Rin, sizeof(R));
+    for (int it = 0; it < 3; it++) {
+        inv_t3(R, Y);
+        for (int k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
+    }
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = std::acos(c);
+    if (s < 1e-5) {
+        double t;
+        if (c > 0)
+            rx = ry = rz = 0;
+        else {
+            t = (R[0] + 1) * 0.5;
+            rx = std::sqrt(t > 0. ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = std::sqrt(t > 0. ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = std::sqrt(t > 0. ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (std::fabs(rx) < std::fabs(ry) && std::fabs(rx) < std::fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            theta /= std::sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta;
+            ry *= theta;
+            rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= theta;
+        rx *= vth;
+        ry *= vth;
+        rz *= vth;
+    }
+    r[0] = rx;
+    r[1] = ry;
+    r[2] = rz;
+}
+
+void compose(const double R[9], const double T[3], double G[16]) {  // tools.cpp:87-99
+    G[0] = R[0]; G[1] = R[1]; G[2] = R[2]; G[3] = T[0];
+    G[4] = R[3]; G[5] = R[4]; G[6] = R[5]; G[7] = T[1];
+    G[8] = R[6]; G[9] = R[7]; G[10] = R[8]; G[11] = T[2];
+    G[12] = 0; G[13] = 0; G[14] = 0; G[15] = 1;
+}
+
+void inv4(const double Ain[16], double B[16]) {  // Matx44d::inv(DECOMP_LU)
+    double A[16];
+    std::memcpy(A, Ain, sizeof(A));
+    for (int i = 0; i < 16; i++) B[i] = (i % 5 == 0) ? 1. : 0.;
+    for (int i = 0; i < 4; i++) {
+        int k = i;
+        for (int j = i + 1; j < 4; j++)
+            if (std::fabs(A[j * 4 + i]) > std::fabs(A[k * 4 + i])) k = j;
+        if (k != i) {
+            for (int j = i; j < 4; j++) std::swap(A[i * 4 + j], A[k * 4 + j]);
+            for (int j = 0; j < 4; j++) std::swap(B[i * 4 + j], B[k * 4 + j]);
+        }
+        double d = -1 / A[i * 4 + i];
+        for (int j = i + 1; j < 4; j++) {
+            double alpha = A[j * 4 + i] * d;
+            for (int kk = i + 1; kk < 4; kk++) A[j * 4 + kk] += alpha * A[i * 4 + kk];
+            for (int kk = 0; kk < 4; kk++) B[j * 4 + kk] += alpha * B[i * 4 + kk];
+        }
+        A[i * 4 + i] = -d;
+    }
+    for (int i = 3; i >= 0; i--)
+        for (int j = 0; j < 4; j++) {
+            double s = B[i * 4 + j];
+            for (int kk = i + 1; kk < 4; kk++) s -= A[i * 4 + kk] * B[kk * 4 + j];
+            B[i * 4 + j] = s * A[i * 4 + i];
+        }
+}
+
+void mul4(const double a[16], const double b[16], double c[16]) {
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double s = 0;
+            for (int k = 0; k < 4; k++) s += a[i * 4 + k] * b[k * 4 + j];
+            c[i * 4 + j] = s;
+        }
+}
+
+void camera2_from_g12(const double g12[16], double R2[9], double t2[3]) {
+    double R[9] = {g12[0], g12[1], g12[2], g12[4], g12[5], g12[6], g12[8], g12[9], g12[10]};
+    double r[3];
+    rodrigues_m2v(R, r);  // decomposeTransformation (tools.cpp:101-114)
+    rodrigues_v2m(r, R2); // cvProjectPoints2 converts r2 back to a matrix
+    t2[0] = g12[3];
+    t2[1] = g12[7];
+    t2[2] = g12[11];
+}
+
+void install_g12(fm3d_ctx* c, const double g[16]) {
+    std::memcpy(c->g12, g, sizeof(c->g12));
+    camera2_from_g12(c->g12, c->R2, c->t2);
+    c->haveG12 = true;
+}
+
+int ensure_offsets(fm3d_ctx* c) {
+    if (c->nOff > 0) return FM3D_OK;
+    const int R = c->s.pixelsRay;
+    std::vector<int2> off;
+    for (int i = -R; i <= R; i++)      // extractPixelsContour (:345-351): i outer (x), j inner (y)
+        for (int j = -R; j <= R; j++)
+            if (i * i + j * j <= R * R) off.push_back(make_int2(i, j));
+    HIPCHK(c, c->offsets.ensure(off.size() * sizeof(int2)));
+    HIPCHK(c, hipMemcpy(c->offsets.p, off.data(), off.size() * sizeof(int2), hipMemcpyHostToDevice));
+    c->nOff = (int)off.size();
+    return FM3D_OK;
+}
+
+int upload(fm3d_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+    HIPCHK(c, b.ensure(bytes));
+    if (bytes) HIPCHK(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return FM3D_OK;
+}
+
+bool f32_is_u8(const float* x, size_t n) {
+    for (size_t i = 0; i < n; i++) {
+        float v = x[i];
+        if (!(v >= 0.f && v <= 255.f) || v != std::floor(v)) return false;
+    }
+    return true;
+}
+
+// pad rows of bytes to dimPad (multiple of 128) with value 128 (x - 128 == 0: no effect on d2)
+std::vector<uint8_t> pad_u8(const uint8_t* x, int n, int dim, int dimPad) {
+    std::vector<uint8_t> o((size_t)n * dimPad, 128);
+    for (int i = 0; i < n; i++) std::memcpy(&o[(size_t)i * dimPad], x + (size_t)i * dim, dim);
+    return o;
+}
+std::vector<uint8_t> f32_to_u8(const float* x, int n, int dim, int dimPad) {
+    std::vector<uint8_t> o((size_t)n * dimPad, 128);
+    for (int i = 0; i < n; i++)
+        for (int d = 0; d < dim; d++) o[(size_t)i * dimPad + d] = (uint8_t)x[(size_t)i * dim + d];
+    return o;
+}
+
+// stage descriptors on the device; returns the effective kernel type
+int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                      int* effType, int* dimPad) {
+    if (dim <= 0 || nA < 0 || nB < 0) return fail(c, FM3D_ERR_INVALID, "bad descriptor shape");
+    int t = type;
+    if (type == FM3D_DESC_F32 && f32_is_u8((const float*)descA, (size_t)nA * dim) &&
+        f32_is_u8((const float*)descB, (size_t)nB * dim))
+        t = FM3D_DESC_U8;  // integer-valued rows: exact, identical ranking and distances
+    if (t == FM3D_DESC_U8) {
+        int dp = ((dim + 127) / 128) * 128;
+        if (dp > 256) return fail(c, FM3D_ERR_UNSUPPORTED, "u8 descriptors longer than 256 bytes");
+        std::vector<uint8_t> a = type == FM3D_DESC_F32 ? f32_to_u8((const float*)descA, nA, dim, dp)
+                                                        : pad_u8((const uint8_t*)descA, nA, dim, dp);
+        std::vector<uint8_t> b = type == FM3D_DESC_F32 ? f32_to_u8((const float*)descB, nB, dim, dp)
+                                                        : pad_u8((const uint8_t*)descB, nB, dim, dp);
+        int r;
+        if ((r = upload(c, c->A, a.data(), a.size()))) return r;
+        if ((r = upload(c, c->B, b.data(), b.size()))) return r;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *dimPad = dp;
+    } else if (t == FM3D_DESC_F32) {
+        int r;
+        if ((r = upload(c, c->A, descA, (size_t)nA * dim * 4))) return r;
+        if ((r = upload(c, c->B, descB, (size_t)nB * dim * 4))) return r;
+        *dimPad = dim;
+    } else if (t == FM3D_DESC_BITS) {
+        int words = (dim + 3) / 4;
+        int wp = (words == 4 || words == 8 || words == 16) ? words : 16;
+        if (words > 16) return fail(c, FM3D_ERR_UNSUPPORTED, "binary descriptors longer than 64 bytes");
+        std::vector<uint8_t> a((size_t)nA * wp * 4, 0), b((size_t)nB * wp * 4, 0);
+        for (int i = 0; i < nA; i++) std::memcpy(&a[(size_t)i * wp * 4], (const uint8_t*)descA + (size_t)i * dim, dim);
+        for (int i = 0; i < nB; i++) std::memcpy(&b[(size_t)i * wp * 4], (const uint8_t*)descB + (size_t)i * dim, dim);
+        int r;
+        if ((r = upload(c, c->A, a.data(), a.size()))) return r;
+        if ((r = upload(c, c->B, b.data(), b.size()))) return r;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *dimPad = wp * 4;
+    } else {
+        return fail(c, FM3D_ERR_INVALID, "unknown descriptor type");
+    }
+    *effType = t;
+    return FM3D_OK;
+}
+
+// knn2 + NNDR flags on staged descriptors (device), results in c->idx/key/fkey/cand/flag
+int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int queryOffset, bool wantKnn) {
+    HIPCHK(c, c->idx.ensure((size_t)nA * 2 * sizeof(int) + 16));
+    HIPCHK(c, c->key.ensure((size_t)nA * 2 * sizeof(int) + 16));
+    HIPCHK(c, c->fkey.ensure((size_t)nA * 2 * sizeof(float) + 16));
+    HIPCHK(c, c->cand.ensure((size_t)nA * sizeof(fm3d_dmatch) + 16));
+    HIPCHK(c, c->flag.ensure((size_t)nA * sizeof(int) + 16));
+    if (wantKnn) HIPCHK(c, c->knnOut.ensure((size_t)nA * 2 * sizeof(fm3d_dmatch) + 16));
+    if (type == FM3D_DESC_U8) {
+        const int nAPad = nA, nBPad = nB;
+        HIPCHK(c, c->cqA.ensure((size_t)(nAPad + 1) * sizeof(int)));
+        HIPCHK(c, c->ctB.ensure((size_t)(nBPad + 1) * sizeof(int)));
+        fm3d::launch_rowconst_u8(c->A.as<uint8_t>(), nA, nAPad, dimPad, c->cqA.as<int>(), c->stream);
+        fm3d::launch_rowconst_u8(c->B.as<uint8_t>(), nB, nBPad, dimPad, c->ctB.as<int>(), c->stream);
+        fm3d::launch_knn2_u8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->cqA.as<int>(),
+                             c->ctB.as<int>(), c->idx.as<int>(), c->key.as<int>(), c->stream);
+    } else if (type == FM3D_DESC_F32) {
+        fm3d::launch_knn2_f32(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, c->idx.as<int>(),
+                              c->fkey.as<float>(), c->stream);
+    } else {
+        fm3d::launch_knn2_bits(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->idx.as<int>(),
+                               c->key.as<int>(), c->stream);
+    }
+    HIPCHK(c, hipGetLastError());
+    fm3d::launch_nndr(type, c->idx.as<int>(), c->key.as<int>(), c->fkey.as<float>(), nA, nB, eps, queryOffset,
+                      wantKnn ? c->knnOut.as<fm3d_dmatch>() : nullptr, c->cand.as<fm3d_dmatch>(), c->flag.as<int>(),
+                      c->stream);
+    HIPCHK(c, hipGetLastError());
+    return FM3D_OK;
+}
+
+int ensure_scan_tmp(fm3d_ctx* c, int n) {
+    HIPCHK(c, c->scanTmp.ensure(fm3d::scan_tmp_bytes(n < 1 ? 1 : n)));
+    HIPCHK(c, c->count.ensure(64));
+    return FM3D_OK;
+}
+
+// LM normals over nPts device points (c->pts), outputs in c->lm*
+int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
+    int r;
+    if ((r = ensure_offsets(c))) return r;
+    if (c->pyr1.empty()) return fail(c, FM3D_ERR_INVALID, "fm3d_set_images (NormalOptimizer::setImages) not called");
+    if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "g12 not set (SingleCameraTriangulator::setg12)");
+    const int levels = c->s.pyramids;
+    HIPCHK(c, c->lmNormals.ensure((size_t)(P + 1) * 3 * sizeof(double)));
+    HIPCHK(c, c->lmStatus.ensure((size_t)(P + 1) * sizeof(int)));
+    HIPCHK(c, c->lmInfo.ensure((size_t)(P + 1) * 8 * sizeof(int)));
+    HIPCHK(c, c->lmNfev.ensure((size_t)(P + 1) * 8 * sizeof(int)));
+    HIPCHK(c, c->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
+    HIPCHK(c, c->lmQueue.ensure(64));
+    HIPCHK(c, c->lmStat.ensure(64));
+    // wavefronts: one lane per point, lanes refill from the queue
+    long waves = c->s.lmWaves > 0 ? c->s.lmWaves : (P + 63) / 64;
+    const size_t perWave = (size_t)c->nOff * 64 * (5 * sizeof(double) + sizeof(float));
+    const size_t budget = (size_t)48 << 30;  // HBM budget for the per-lane pixel slabs
+    long cap = (long)(budget / perWave);
+    if (cap < 1) cap = 1;
+    if (waves > cap) waves = cap;
+    if (waves > 4096) waves = 4096;
+    if (waves < 1) waves = 1;
+    HIPCHK(c, c->slab.ensure(perWave / (5 * sizeof(double) + sizeof(float)) * 5 * sizeof(double) * waves));
+    HIPCHK(c, c->slabI1.ensure(perWave / (5 * sizeof(double) + sizeof(float)) * sizeof(float) * waves));
+    HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 64, c->stream));
+    fm3d::LMParams p{};
+    p.points = c->pts.as<double>();
+    p.P = P;
+    p.cam = c->cam;
+    std::memcpy(p.R2, c->R2, sizeof(p.R2));
+    std::memcpy(p.t2, c->t2, sizeof(p.t2));
+    p.lvl = c->lvlDesc.as<LevelDesc>();
+    p.levels = levels;
+    p.offsets = c->offsets.as<int2>();
+    p.nOff = c->nOff;
+    p.boundW = c->s.boundWidth;
+    p.boundH = c->s.boundHeight;
+    p.epsfcn = c->s.epsilonLMMIN;
+    p.cmax = (int)(2 * c->s.zThresholdMax);  // isInBoundingBox: int cMax = 2*z_threshold_max_ (:648)
+    p.queue = c->lmQueue.as<int>();
+    p.slab = c->slab.as<double>();
+    p.slabI1 = c->slabI1.as<float>();
+    p.nWaves = waves;
+    p.normals = c->lmNormals.as<double>();
+    p.status = c->lmStatus.as<int>();
+    p.info = c->lmInfo.as<int>();
+    p.nfev = c->lmNfev.as<int>();
+    p.mdat = c->lmMdat.as<int>();
+    p.statEval = c->lmStat.as<unsigned long long>();
+    p.statPix = c->lmStat.as<unsigned long long>() + 1;
+    p.overflow = (int*)(c->lmStat.as<unsigned long long>() + 2);
+    {   // per lane: <= points per lane x (levels+1) x (300 evaluations + QR) + slack
+        long long lanes = waves * 64;
+        long long perLane = (P + lanes - 1) / lanes + 1;
+        p.maxIter = perLane * (long long)(levels + 1) * 700 + 1000;
+    }
+    if (P > 0) {
+        const int wavesPerBlock = 4;
+        const int blocks = (int)((waves + wavesPerBlock - 1) / wavesPerBlock);
+        HIPCHK(c, hipEventRecord(e0, c->stream));
+        fm3d::lm_kernel<<<blocks, 64 * wavesPerBlock, 0, c->stream>>>(p);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(e1, c->stream));
+    }
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->points_in = P;
+    }
+    return FM3D_OK;
+}
+
+int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int width, int height, int stride) {
+    if (!img1 || !img2 || width <= 0 || height <= 0 || stride < width)
+        return fail(c, FM3D_ERR_INVALID, "bad image arguments");
+    const int levels = c->s.pyramids;
+    if (levels < 0 || levels > 7) return fail(c, FM3D_ERR_UNSUPPORTED, "pyramids must be in [0, 7]");
+    c->w = width;
+    c->h = height;
+    c->lw.assign(levels + 1, 0);
+    c->lh.assign(levels + 1, 0);
+    c->pyr1.resize(levels + 1);
+    c->pyr2.resize(levels + 1);
+    c->lw[0] = width;
+    c->lh[0] = height;
+    for (int L = 1; L <= levels; L++) {  // cv::pyrDown size ((w+1)/2, (h+1)/2)
+        c->lw[L] = (c->lw[L - 1] + 1) / 2;
+        c->lh[L] = (c->lh[L - 1] + 1) / 2;
+    }
+    for (int L = 0; L <= levels; L++) {
+        size_t bytes = (size_t)c->lw[L] * c->lh[L] + kGuard(c->lw[L]);
+        HIPCHK(c, c->pyr1[L].ensure(bytes));
+        HIPCHK(c, c->pyr2[L].ensure(bytes));
+        HIPCHK(c, hipMemsetAsync(c->pyr1[L].p, 0, bytes, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->pyr2[L].p, 0, bytes, c->stream));
+    }
+    HIPCHK(c, hipMemcpy2DAsync(c->pyr1[0].p, width, img1, stride, width, height, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpy2DAsync(c->pyr2[0].p, width, img2, stride, width, height, hipMemcpyHostToDevice, c->stream));
+    for (int L = 1; L <= levels; L++) {
+        fm3d::launch_pyrdown(c->pyr1[L - 1].as<uint8_t>(), c->lw[L - 1], c->lh[L - 1], c->pyr1[L].as<uint8_t>(),
+                             c->stream);
+        fm3d::launch_pyrdown(c->pyr2[L - 1].as<uint8_t>(), c->lw[L - 1], c->lh[L - 1], c->pyr2[L].as<uint8_t>(),
+                             c->stream);
+    }
+    HIPCHK(c, hipGetLastError());
+    std::vector<LevelDesc> d(levels + 1);
+    for (int L = 0; L <= levels; L++) d[L] = LevelDesc{c->pyr1[L].as<uint8_t>(), c->pyr2[L].as<uint8_t>(), c->lw[L], c->lh[L]};
+    HIPCHK(c, c->lvlDesc.ensure(d.size() * sizeof(LevelDesc)));
+    HIPCHK(c, hipMemcpyAsync(c->lvlDesc.p, d.data(), d.size() * sizeof(LevelDesc), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fm3d_version(void) { return "fm3d 0.1 (gfx950)"; }
+
+int fm3d_ctx_create(const fm3d_settings* s, int device, fm3d_ctx** out) {
+    if (!s || !out) return FM3D_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return FM3D_ERR_HIP;
+    if (device < 0 || device >= n) return FM3D_ERR_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return FM3D_ERR_HIP;
+    fm3d_ctx* c = new fm3d_ctx();
+    c->s = *s;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return FM3D_ERR_HIP;
+    }
+    c->ownStream = true;
+    for (auto& e : c->ev) hipEventCreate(&e);
+    c->cam.fx = s->Fx;
+    c->cam.fy = s->Fy;
+    c->cam.cx = s->Cx;
+    c->cam.cy = s->Cy;
+    c->cam.k[0] = s->k0;
+    c->cam.k[1] = s->k1;
+    c->cam.k[2] = s->p1;
+    c->cam.k[3] = s->p2;
+    c->cam.k[4] = s->k2;
+    *out = c;
+    return FM3D_OK;
+}
+
+void fm3d_ctx_destroy(fm3d_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->lvlDesc, &c->offsets, &c->A, &c->B, &c->cqA, &c->ctB, &c->idx, &c->key, &c->fkey,
+                      &c->knnOut, &c->cand, &c->flag, &c->matches, &c->count, &c->scanTmp, &c->kp1, &c->kp2,
+                      &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
+                      &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat, &c->slab, &c->slabI1,
+                      &c->records, &c->recTmp, &c->recFlag};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& b : c->pyr1) b.release();
+    for (auto& b : c->pyr2) b.release();
+    for (auto& e : c->ev) hipEventDestroy(e);
+    if (c->ownStream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* fm3d_last_error(const fm3d_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int fm3d_ctx_set_stream(fm3d_ctx* c, void* stream) {
+    if (!c) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    if (c->ownStream) hipStreamDestroy(c->stream);
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+        c->ownStream = false;
+    } else {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->ownStream = true;
+    }
+    return FM3D_OK;
+}
+
+int fm3d_knn2(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type, fm3d_dmatch* out) {
+    if (!c || (!descA && nA) || (!descB && nB) || (!out && nA)) return fail(c, FM3D_ERR_INVALID, "null argument");
+    hipSetDevice(c->device);
+    int t, dp, r;
+    if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp))) return r;
+    if ((r = run_match(c, nA, nB, t, dp, 0.0, 0, true))) return r;
+    if (nA) HIPCHK(c, hipMemcpyAsync(out, c->knnOut.p, (size_t)nA * 2 * sizeof(fm3d_dmatch), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+int fm3d_match_nndr(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                    double epsilon, fm3d_dmatch* matches, int* nMatches) {
+    if (!c || !nMatches || (!descA && nA) || (!descB && nB) || (!matches && nA))
+        return fail(c, FM3D_ERR_INVALID, "null argument");
+    hipSetDevice(c->device);
+    int t, dp, r;
+    if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp))) return r;
+    if ((r = run_match(c, nA, nB, t, dp, epsilon, 0, false))) return r;
+    if ((r = ensure_scan_tmp(c, nA))) return r;
+    HIPCHK(c, c->matches.ensure((size_t)(nA + 1) * sizeof(fm3d_dmatch)));
+    fm3d::launch_compact_dmatch(c->cand.as<fm3d_dmatch>(), c->flag.as<int>(), nA, c->matches.as<fm3d_dmatch>(),
+                                c->count.as<int>(), c->scanTmp.p, c->stream);
+    HIPCHK(c, hipGetLastError());
+    int n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (n) HIPCHK(c, hipMemcpy(matches, c->matches.p, (size_t)n * sizeof(fm3d_dmatch), hipMemcpyDeviceToHost));
+    *nMatches = n;
+    return FM3D_OK;
+}
+
+int fm3d_g12_from_poses(const fm3d_settings* s, const double T1[3], const double T2[3], const double r1[3],
+                        const double r2[3], double g[16]) {
+    if (!s || !T1 || !T2 || !r1 || !r2 || !g) return FM3D_ERR_INVALID;
+    double RIC[9], R1[9], R2[9], gIC[16], g1[16], g2[16], a[16], b[16], cc[16], d[16];
+    rodrigues_v2m(s->rodriguesIC, RIC);  // SingleCameraTriangulator ctor (:42-65)
+    compose(RIC, s->translationIC, gIC);
+    rodrigues_v2m(r1, R1);
+    rodrigues_v2m(r2, R2);
+    compose(R1, T1, g1);
+    compose(R2, T2, g2);
+    inv4(gIC, a);
+    inv4(g2, b);
+    mul4(a, b, cc);
+    mul4(cc, g1, d);
+    mul4(d, gIC, g);
+    return FM3D_OK;
+}
+
+int fm3d_camera2_from_g12(const double g12[16], double R2[9], double t2[3]) {
+    if (!g12 || !R2 || !t2) return FM3D_ERR_INVALID;
+    camera2_from_g12(g12, R2, t2);
+    return FM3D_OK;
+}
+
+int fm3d_setg12(fm3d_ctx* c, const double T1[3], const double T2[3], const double r1[3], const double r2[3],
+                double g12[16]) {
+    if (!c || !T1 || !T2 || !r1 || !r2) return fail(c, FM3D_ERR_INVALID, "null argument");
+    double g[16];
+    fm3d_g12_from_poses(&c->s, T1, T2, r1, r2, g);
+    install_g12(c, g);
+    if (g12) std::memcpy(g12, g, sizeof(g));
+    return FM3D_OK;
+}
+
+int fm3d_set_g12(fm3d_ctx* c, const double g12[16]) {
+    if (!c || !g12) return fail(c, FM3D_ERR_INVALID, "null argument");
+    install_g12(c, g12);
+    return FM3D_OK;
+}
+
+int fm3d_get_camera2(const fm3d_ctx* c, double R2[9], double t2[3]) {
+    if (!c || !c->haveG12) return FM3D_ERR_INVALID;
+    std::memcpy(R2, c->R2, sizeof(c->R2));
+    std::memcpy(t2, c->t2, sizeof(c->t2));
+    return FM3D_OK;
+}
+
+int fm3d_triangulate(fm3d_ctx* c, const fm3d_point2f* kpts1, int n1, const fm3d_point2f* kpts2, int n2,
+                     const fm3d_dmatch* matches, int K, double* points, uint8_t* inlierMask, int* nPoints) {
+    if (!c || !nPoints || K < 0) return fail(c, FM3D_ERR_INVALID, "bad argument");
+    if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "g12 not set (SingleCameraTriangulator::setg12)");
+    hipSetDevice(c->device);
+    for (int i = 0; i < K; i++)
+        if (matches[i].queryIdx < 0 || matches[i].queryIdx >= n1 || matches[i].trainIdx < 0 || matches[i].trainIdx >= n2)
+            return fail(c, FM3D_ERR_INVALID, "match index out of range");  // std::vector::at would throw
+    int r;
+    if ((r = upload(c, c->kp1, kpts1, (size_t)n1 * sizeof(fm3d_point2f)))) return r;
+    if ((r = upload(c, c->kp2, kpts2, (size_t)n2 * sizeof(fm3d_point2f)))) return r;
+    if ((r = upload(c, c->matches, matches, (size_t)K * sizeof(fm3d_dmatch)))) return r;
+    HIPCHK(c, c->triPts.ensure((size_t)(K + 1) * 3 * sizeof(double)));
+    HIPCHK(c, c->triMask.ensure((size_t)(K + 1) * sizeof(int)));
+    HIPCHK(c, c->triMask8.ensure((size_t)(K + 1)));
+    HIPCHK(c, c->pts.ensure((size_t)(K + 1) * 3 * sizeof(double)));
+    HIPCHK(c, c->srcIdx.ensure((size_t)(K + 1) * sizeof(int)));
+    if ((r = ensure_scan_tmp(c, K))) return r;
+    fm3d::TriParams p{};
+    p.cam = c->cam;
+    std::memcpy(p.g12, c->g12, sizeof(p.g12));
+    p.zmin = c->s.zThresholdMin;
+    p.zmax = c->s.zThresholdMax;
+    p.kp1 = c->kp1.as<fm3d_point2f>();
+    p.kp2 = c->kp2.as<fm3d_point2f>();
+    p.matches = c->matches.as<fm3d_dmatch>();
+    p.K = K;
+    p.queryOffset = 0;
+    p.pts = c->triPts.as<double>();
+    p.mask = c->triMask.as<int>();
+    p.mask8 = c->triMask8.as<uint8_t>();
+    fm3d::launch_triangulate(p, c->stream);
+    fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), K, c->pts.as<double>(), c->count.as<int>(),
+                                c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
+    HIPCHK(c, hipGetLastError());
+    int n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (inlierMask && K) HIPCHK(c, hipMemcpyAsync(inlierMask, c->triMask8.p, K, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (n && points) HIPCHK(c, hipMemcpy(points, c->pts.p, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    *nPoints = n;
+    return FM3D_OK;
+}
+
+int fm3d_set_images(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int width, int height, int stride) {
+    if (!c) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    return set_images_impl(c, img1, img2, width, height, stride);
+}
+
+int fm3d_get_pyramid_level(const fm3d_ctx* cc, int which, int level, uint8_t* out, int* w, int* h) {
+    fm3d_ctx* c = const_cast<fm3d_ctx*>(cc);
+    if (!c || level < 0 || level >= (int)c->pyr1.size() || (which != 1 && which != 2)) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    if (w) *w = c->lw[level];
+    if (h) *h = c->lh[level];
+    if (out) {
+        const DevBuf& b = which == 1 ? c->pyr1[level] : c->pyr2[level];
+        HIPCHK(c, hipMemcpy(out, b.p, (size_t)c->lw[level] * c->lh[level], hipMemcpyDeviceToHost));
+    }
+    return FM3D_OK;
+}
+
+int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, int32_t* status, int32_t* info,
+                          int32_t* nfev, int* nKept, fm3d_lm_stats* stats) {
+    if (!c || !nKept || P < 0 || (P && (!points || !normals))) return fail(c, FM3D_ERR_INVALID, "bad argument");
+    hipSetDevice(c->device);
+    int r;
+    if ((r = upload(c, c->pts, points, (size_t)P * 3 * sizeof(double)))) return r;
+    if ((r = run_lm(c, P, stats, c->ev[0], c->ev[1]))) return r;
+    std::vector<double> nrm((size_t)P * 3);
+    std::vector<int> st(P), inf((size_t)P * 8), nf((size_t)P * 8);
+    unsigned long long cnt[2] = {0, 0};
+    if (P) {
+        HIPCHK(c, hipMemcpyAsync(nrm.data(), c->lmNormals.p, nrm.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(st.data(), c->lmStatus.p, st.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(inf.data(), c->lmInfo.p, inf.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(nf.data(), c->lmNfev.p, nf.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int overflow = 0;
+    HIPCHK(c, hipMemcpy(&overflow, c->lmStat.as<unsigned long long>() + 2, sizeof(int), hipMemcpyDeviceToHost));
+    if (overflow) return fail(c, FM3D_ERR_HIP, "LM kernel iteration guard tripped (internal error)");
+    float ms = 0.f;
+    if (P) hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+    // erase semantics (normaloptimizer.cpp:366,378): stable compaction, input order kept
+    int kept = 0;
+    bool nanPlane = false;
+    for (int i = 0; i < P; i++) {
+        if (status) status[i] = st[i];
+        if (info) std::memcpy(&info[(size_t)8 * i], &inf[(size_t)8 * i], 8 * sizeof(int));
+        if (nfev) std::memcpy(&nfev[(size_t)8 * i], &nf[(size_t)8 * i], 8 * sizeof(int));
+        if (st[i] == FM3D_ST_NAN_PLANE) nanPlane = true;
+        if (st[i] == FM3D_ST_OK) {
+            for (int k = 0; k < 3; k++) {
+                points[3 * kept + k] = points[3 * i + k];
+                normals[3 * kept + k] = nrm[3 * i + k];
+            }
+            kept++;
+        }
+    }
+    *nKept = kept;
+    if (stats) {
+        stats->points_in = P;
+        stats->points_kept = kept;
+        stats->evaluations = (int64_t)cnt[0];
+        stats->pixel_evaluations = (int64_t)cnt[1];
+        for (int i = 0; i < P; i++)
+            if (st[i] >= 0 && st[i] < 8) stats->drops[st[i]]++;
+        stats->kernel_ms = ms;
+    }
+    if (nanPlane && c->s.strictNanExit)
+        return fail(c, FM3D_ERR_NAN_PLANE, "projectPointToPlane hit NaN (reference: exit(-6))");
+    return FM3D_OK;
+}
+
+// ---------------- whole pipeline, device resident ----------------
+int fm3d_pipeline_upload(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                         const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
+                         int width, int height, int queryOffset) {
+    if (!c || !kpts1 || !kpts2) return fail(c, FM3D_ERR_INVALID, "null argument");
+    hipSetDevice(c->device);
+    int t, dp, r;
+    if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp))) return r;
+    if ((r = upload(c, c->kp1, kpts1, (size_t)nA * sizeof(fm3d_point2f)))) return r;
+    if ((r = upload(c, c->kp2, kpts2, (size_t)nB * sizeof(fm3d_point2f)))) return r;
+    if ((r = set_images_impl(c, img1, img2, width, height, width))) return r;
+    if (!c->haveG12) {
+        double g[16];
+        if ((r = fm3d_setg12(c, c->s.pos1, c->s.pos2, c->s.pos1 + 3, c->s.pos2 + 3, g))) return r;
+    }
+    if ((r = ensure_offsets(c))) return r;
+    c->stNA = nA;
+    c->stNB = nB;
+    c->stDim = dim;
+    c->stType = t;
+    c->stDimPad = dp;
+    c->stQueryOffset = queryOffset;
+    c->staged = true;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pipeline_stats* stats) {
+    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    hipSetDevice(c->device);
+    const int nA = c->stNA, nB = c->stNB;
+    int r;
+    hipEvent_t* ev = c->ev;
+    HIPCHK(c, hipEventRecord(ev[2], c->stream));
+    // a1: match + NNDR
+    if ((r = run_match(c, nA, nB, c->stType, c->stDimPad, c->s.nndrEpsilon, c->stQueryOffset, false))) return r;
+    HIPCHK(c, hipEventRecord(ev[3], c->stream));
+    if ((r = ensure_scan_tmp(c, nA))) return r;
+    HIPCHK(c, c->matches.ensure((size_t)(nA + 1) * sizeof(fm3d_dmatch)));
+    fm3d::launch_compact_dmatch(c->cand.as<fm3d_dmatch>(), c->flag.as<int>(), nA, c->matches.as<fm3d_dmatch>(),
+                                c->count.as<int>(), c->scanTmp.p, c->stream);
+    int K = 0;
+    HIPCHK(c, hipMemcpyAsync(&K, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventRecord(ev[4], c->stream));
+    // a4, a5: triangulate (matches are device resident)
+    HIPCHK(c, c->triPts.ensure((size_t)(K + 1) * 3 * sizeof(double)));
+    HIPCHK(c, c->triMask.ensure((size_t)(K + 1) * sizeof(int)));
+    HIPCHK(c, c->pts.ensure((size_t)(K + 1) * 3 * sizeof(double)));
+    HIPCHK(c, c->srcIdx.ensure((size_t)(K + 1) * sizeof(int)));
+    if ((r = ensure_scan_tmp(c, K > nA ? K : nA))) return r;
+    fm3d::TriParams tp{};
+    tp.cam = c->cam;
+    std::memcpy(tp.g12, c->g12, sizeof(tp.g12));
+    tp.zmin = c->s.zThresholdMin;
+    tp.zmax = c->s.zThresholdMax;
+    tp.kp1 = c->kp1.as<fm3d_point2f>();
+    tp.kp2 = c->kp2.as<fm3d_point2f>();
+    tp.matches = c->matches.as<fm3d_dmatch>();
+    tp.K = K;
+    tp.queryOffset = c->stQueryOffset;
+    tp.pts = c->triPts.as<double>();
+    tp.mask = c->triMask.as<int>();
+    tp.mask8 = nullptr;
+    fm3d::launch_triangulate(tp, c->stream);
+    fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), K, c->pts.as<double>(),
+                                c->count.as<int>(), c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
+    HIPCHK(c, hipGetLastError());
+    int P = 0;
+    HIPCHK(c, hipMemcpyAsync(&P, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventRecord(ev[5], c->stream));
+    // a6-a15: normals (pyramids were built at upload: images are inputs of the path)
+    fm3d_lm_stats ls{};
+    if ((r = run_lm(c, P, &ls, ev[6], ev[7]))) return r;
+    // records of the survivors
+    HIPCHK(c, c->recTmp.ensure((size_t)(P + 1) * sizeof(fm3d_record)));
+    HIPCHK(c, c->recFlag.ensure((size_t)(P + 1) * sizeof(int)));
+    fm3d_record* out = recordsDev;
+    if (!out) {
+        HIPCHK(c, c->records.ensure((size_t)(nA + 1) * sizeof(fm3d_record)));
+        out = c->records.as<fm3d_record>();
+    }
+    if ((r = ensure_scan_tmp(c, P > nA ? P : nA))) return r;
+    fm3d::launch_make_records(c->matches.as<fm3d_dmatch>(), c->srcIdx.as<int>(), P, c->pts.as<double>(),
+                              c->lmNormals.as<double>(), c->lmStatus.as<int>(), c->recTmp.as<fm3d_record>(),
+                              c->recFlag.as<int>(), c->stream);
+    fm3d::launch_compact_records(c->recTmp.as<fm3d_record>(), c->recFlag.as<int>(), P, out, c->count.as<int>(),
+                                 c->scanTmp.p, c->stream);
+    HIPCHK(c, hipGetLastError());
+    int kept = 0;
+    unsigned long long cnt[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(&kept, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nKept) *nKept = kept;
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->queries = nA;
+        stats->trains = nB;
+        stats->matches = K;
+        stats->inliers = P;
+        stats->kept = kept;
+        float ms;
+        hipEventElapsedTime(&ms, ev[2], ev[3]);
+        stats->match_ms = ms;
+        hipEventElapsedTime(&ms, ev[3], ev[4]);
+        stats->nndr_ms = ms;
+        hipEventElapsedTime(&ms, ev[4], ev[5]);
+        stats->triangulate_ms = ms;
+        stats->pyramid_ms = 0;
+        ms = 0;
+        if (P) hipEventElapsedTime(&ms, ev[6], ev[7]);
+        stats->lm_ms = ms;
+        hipEventElapsedTime(&ms, ev[2], ev[1]);
+        stats->total_ms = ms;
+        stats->lm = ls;
+        stats->lm.points_in = P;
+        stats->lm.points_kept = kept;
+        stats->lm.evaluations = (int64_t)cnt[0];
+        stats->lm.pixel_evaluations = (int64_t)cnt[1];
+        stats->lm.kernel_ms = stats->lm_ms;
+    }
+    return FM3D_OK;
+}
+
+int fm3d_records_download(fm3d_ctx* c, const fm3d_record* recordsDev, int n, fm3d_record* out) {
+    if (!c || n < 0 || (n && !out)) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    const void* src = recordsDev ? (const void*)recordsDev : c->records.p;
+    if (n) HIPCHK(c, hipMemcpy(out, src, (size_t)n * sizeof(fm3d_record), hipMemcpyDeviceToHost));
+    return FM3D_OK;
+}
+
+int fm3d_pyrdown(fm3d_ctx* c, const uint8_t* src, int width, int height, uint8_t* dst) {
+    if (!c || !src || !dst || width <= 0 || height <= 0) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    DevBuf a, b;
+    HIPCHK(c, a.ensure((size_t)width * height));
+    const int dw = (width + 1) / 2, dh = (height + 1) / 2;
+    HIPCHK(c, b.ensure((size_t)dw * dh));
+    HIPCHK(c, hipMemcpy(a.p, src, (size_t)width * height, hipMemcpyHostToDevice));
+    fm3d::launch_pyrdown(a.as<uint8_t>(), width, height, b.as<uint8_t>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(dst, b.p, (size_t)dw * dh, hipMemcpyDeviceToHost));
+    a.release();
+    b.release();
+    return FM3D_OK;
+}
+
+int fm3d_neighborhood(fm3d_ctx* c, const double X[3], double* xy, int cap, int* m) {
+    // host restatement of extractPixelsContour (used to cross-check the kernel's own)
+    if (!c || !X || !m) return FM3D_ERR_INVALID;
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Z[3] = {0, 0, 0};
+    double cx, cy;
+    fm3d::project1(c->cam, I, Z, X[0], X[1], X[2], cx, cy);
+    const int R = c->s.pixelsRay;
+    int n = 0;
+    for (int i = -R; i <= R; i++)
+        for (int j = -R; j <= R; j++)
+            if (i * i + j * j <= R * R) {
+                double px = cx + i, py = cy + j;
+                if (px < 0 || py < 0 || px >= c->s.boundWidth || py >= c->s.boundHeight) continue;
+                if (n < cap && xy) {
+                    xy[2 * n] = px;
+                    xy[2 * n + 1] = py;
+                }
+                n++;
+            }
+    *m = n;
+    return FM3D_OK;
+}
+
+int fm3d_undistort(fm3d_ctx* c, const double* xy, int n, double* out) {
+    if (!c || n < 0 || (n && (!xy || !out))) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    DevBuf a, b;
+    HIPCHK(c, a.ensure((size_t)n * 16 + 16));
+    HIPCHK(c, b.ensure((size_t)n * 16 + 16));
+    HIPCHK(c, hipMemcpy(a.p, xy, (size_t)n * 16, hipMemcpyHostToDevice));
+    fm3d::launch_undistort(c->cam, a.as<double>(), n, b.as<double>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, b.p, (size_t)n * 16, hipMemcpyDeviceToHost));
+    a.release();
+    b.release();
+    return FM3D_OK;
+}
+
+}  // extern "C"

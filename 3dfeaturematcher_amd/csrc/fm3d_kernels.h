@@ -1,0 +1,100 @@
+// fm3d_kernels.h -- kernel parameter blocks and host-side launchers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fm3d.h"
+#include "fm3d_device.h"
+
+namespace fm3d {
+
+struct LevelDesc {
+    const uint8_t* img1;  // pyramid level of image 1 (+ zero guard)
+    const uint8_t* img2;
+    int w, h;
+};
+
+struct LMParams {
+    const double* points;  // P x 3
+    int P;
+    Camera cam;
+    double R2[9], t2[3];
+    const LevelDesc* lvl;  // device array, levels+1 entries
+    int levels;
+    const int2* offsets;  // circle offsets (i, j) in reference order
+    int nOff;
+    int boundW, boundH;
+    double epsfcn;
+    int cmax;
+    int* queue;
+    double* slab;    // nWaves * 5 * nOff * 64 doubles
+    float* slabI1;   // nWaves * nOff * 64 floats
+    long nWaves;
+    double* normals;  // P x 3
+    int* status;      // P
+    int* info;        // P x 8
+    int* nfev;        // P x 8
+    int* mdat;        // P
+    unsigned long long* statEval;
+    unsigned long long* statPix;
+    long long maxIter;       // safety bound on main-loop iterations per wave
+    int* overflow;           // set to 1 if a wave hit maxIter
+};
+
+__global__ void lm_kernel(LMParams p);
+
+// ---------------- matching ----------------
+struct KnnOut {
+    int* idx;       // nA x 2 train indices (-1 = none)
+    int* key;       // nA x 2 ranking keys (u8: d2, bits: hamming)
+    float* fkey;    // nA x 2 (f32: FLANN squared distance)
+};
+
+// u8 rows (dim padded to a multiple of 128 with value 128 on both sides -> no effect)
+void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA,
+                    const int* ctB, int* idx, int* key, hipStream_t s);
+void launch_rowconst_u8(const uint8_t* X, int n, int nPad, int dimPad, int* c, hipStream_t s);
+void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, int* idx, float* key, hipStream_t s);
+void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int* idx, int* key,
+                      hipStream_t s);
+// distances + NNDR flag per query; type 0 f32 keys in fkey, 1 u8, 2 bits
+void launch_nndr(int type, const int* idx, const int* key, const float* fkey, int nA, int nB, double eps,
+                 int queryOffset, fm3d_dmatch* knnOut, fm3d_dmatch* cand, int* flag, hipStream_t s);
+
+// ---------------- compaction ----------------
+// out[k] = in[i] for flag[i] != 0, stable; *count (device) = number kept.  tmp >= scan_tmp_bytes(n).
+size_t scan_tmp_bytes(int n);
+void launch_compact_dmatch(const fm3d_dmatch* in, const int* flag, int n, fm3d_dmatch* out, int* count, void* tmp,
+                           hipStream_t s);
+void launch_compact_points(const double* in, const int* flag, int n, double* out, int* count, int* srcIndex,
+                           void* tmp, hipStream_t s);
+void launch_exclusive_scan(const int* flag, int n, int* offsets, int* total, void* tmp, hipStream_t s);
+
+// ---------------- triangulation ----------------
+struct TriParams {
+    Camera cam;
+    double g12[16];
+    double zmin, zmax;
+    const fm3d_point2f* kp1;
+    const fm3d_point2f* kp2;
+    const fm3d_dmatch* matches;
+    int K;
+    int queryOffset;  // matches[].queryIdx - queryOffset indexes kp1
+    double* pts;      // K x 3 (match order, not compacted)
+    int* mask;        // K
+    uint8_t* mask8;   // K (optional)
+};
+void launch_triangulate(const TriParams& p, hipStream_t s);
+
+// ---------------- images ----------------
+void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s);
+void launch_undistort(const Camera& cam, const double* xy, int n, double* out, hipStream_t s);
+
+// ---------------- records ----------------
+void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int nInl, const double* pts,
+                         const double* normals, const int* status, fm3d_record* rec, int* flag, hipStream_t s);
+void launch_compact_records(const fm3d_record* in, const int* flag, int n, fm3d_record* out, int* count, void* tmp,
+                            hipStream_t s);
+
+}  // namespace fm3d

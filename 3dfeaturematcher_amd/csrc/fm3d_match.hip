@@ -1,0 +1,390 @@
+// fm3d_match.hip -- brute-force k=2 matching + NNDR on gfx950.
+//
+// Reference: DescriptorsMatcher::compareWithNNDR (descriptorsmatcher.cpp:107-131)
+// = knnMatch(A, B, matches, 2) then keep m[0] iff m[0].distance <= eps*m[1].distance.
+// The reference's FlannBasedMatcher is approximate (randomised kd-tree / LSH);
+// the parity contract is the exact brute force it approximates, ordered by
+// (distance, trainIdx) -- SURVEY.md §0 D1.
+//
+// Three kernels:
+//   u8   -- SIFT-like byte rows.  d2 = sum (a-b)^2 = |a'|^2 + |b'|^2 - 2 a'.b' with
+//           a' = a - 128 (int8): the dot products run on int8 MFMA
+//           (v_mfma_i32_32x32x32_i8, exact int32), the top-2 on the VALU.
+//   f32  -- float rows in FLANN's L2 accumulation order (groups of four), VALU.
+//   bits -- binary strings, Hamming by popcount, VALU.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "fm3d_kernels.h"
+
+namespace fm3d {
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int kQ = 128;     // queries per workgroup (4 waves x 32)
+constexpr int kT = 128;     // train rows per LDS tile
+constexpr int kThreads = 256;
+
+__device__ inline int swz_chunk(int row, int ch) {
+    // 16-byte chunk XOR swizzle inside each 128-byte segment: rows r..r+15 reading
+    // the same logical chunk hit 16 distinct 16-byte bank slots (ds_read_b128).
+    return (ch & ~7) | ((ch & 7) ^ ((row >> 1) & 7));
+}
+
+// lexicographic (key, idx) top-2 insertion, candidates arriving in increasing idx
+__device__ inline void top2_insert(int s, int j, int& b1, int& i1, int& b2, int& i2) {
+    bool lt1 = s < b1;
+    bool lt2 = s < b2;
+    b2 = lt1 ? b1 : (lt2 ? s : b2);
+    i2 = lt1 ? i1 : (lt2 ? j : i2);
+    b1 = lt1 ? s : b1;
+    i1 = lt1 ? j : i1;
+}
+
+__device__ inline bool lex_lt(int a, int ia, int b, int ib) {
+    return a < b || (a == b && (unsigned)ia < (unsigned)ib);
+}
+
+// merge two sorted top-2 lists (a1 <= a2, c1 <= c2 lexicographically); -1 indices sort last
+__device__ inline void top2_merge(int& b1, int& i1, int& b2, int& i2, int c1, int j1, int c2, int j2) {
+    if (lex_lt(b1, i1, c1, j1)) {
+        // best = b1; second = min(b2, c1)
+        if (!lex_lt(b2, i2, c1, j1)) {
+            b2 = c1;
+            i2 = j1;
+        }
+    } else {
+        // best = c1; second = min(b1, c2)
+        int nb2 = b1, ni2 = i1;
+        if (lex_lt(c2, j2, nb2, ni2)) {
+            nb2 = c2;
+            ni2 = j2;
+        }
+        b1 = c1;
+        i1 = j1;
+        b2 = nb2;
+        i2 = ni2;
+    }
+}
+
+// per-row constant |x'|^2 with x' = x - 128 over the padded row (padding bytes are 128)
+__global__ void rowconst_u8_kernel(const uint8_t* __restrict__ X, int n, int nPad, int dimPad, int* __restrict__ c) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nPad) return;
+    if (r >= n) {
+        c[r] = INT_MAX / 4;  // padding rows: never selected
+        return;
+    }
+    const uint8_t* row = X + (size_t)r * dimPad;
+    int s = 0;
+    for (int d = 0; d < dimPad; d++) {
+        int v = (int)row[d] - 128;
+        s += v * v;
+    }
+    c[r] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __restrict__ A, int nA,
+                                                           const uint8_t* __restrict__ B, int nB, int dimPad,
+                                                           const int* __restrict__ cqA, const int* __restrict__ ctB,
+                                                           int* __restrict__ idxOut, int* __restrict__ keyOut) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tileBytes = kT * dimPad;
+    unsigned char* tiles = smem;                              // 2 x tileBytes
+    int* ctl = (int*)(smem + 2 * (size_t)tileBytes);          // 2 x kT
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int q0 = blockIdx.x * kQ + wave * 32;
+    const int qrow = q0 + (lane & 31);
+    const int half = lane >> 5;
+    const int ksteps = dimPad / 32;
+    const int chunksPerRow = dimPad / 16;
+
+    // B operand: this lane's query bytes as int8 (x ^ 0x80 == x - 128)
+    v4i bq[8];  // up to dimPad = 256
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) {
+        if (kk < ksteps) {
+            v4i v = {0, 0, 0, 0};
+            if (qrow < nA) v = *(const v4i*)(A + (size_t)qrow * dimPad + 32 * kk + 16 * half);
+            bq[kk] = v ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+        }
+    }
+    int b1 = INT_MAX, i1 = -1, b2 = INT_MAX, i2 = -1;
+    const int nTiles = (nB + kT - 1) / kT;
+
+    auto stage = [&](int t, int buf) {
+        unsigned char* dst = tiles + (size_t)buf * tileBytes;
+        const int total = kT * chunksPerRow;
+        for (int c = tid; c < total; c += kThreads) {
+            int row = c / chunksPerRow, ch = c % chunksPerRow;
+            int j = t * kT + row;
+            v4i v = {0, 0, 0, 0};
+            if (j < nB) v = *(const v4i*)(B + (size_t)j * dimPad + 16 * ch);
+            v = v ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+            *(v4i*)(dst + (size_t)row * dimPad + 16 * swz_chunk(row, ch)) = v;
+        }
+        if (tid < kT) {
+            int j = t * kT + tid;
+            ctl[buf * kT + tid] = (j < nB) ? ctB[j] : INT_MAX / 4;
+        }
+    };
+
+    if (nTiles > 0) stage(0, 0);
+    __syncthreads();
+    for (int t = 0; t < nTiles; t++) {
+        const int buf = t & 1;
+        if (t + 1 < nTiles) stage(t + 1, buf ^ 1);
+        const unsigned char* tl = tiles + (size_t)buf * tileBytes;
+        const int* ct = ctl + buf * kT;
+#pragma unroll
+        for (int rb = 0; rb < kT / 32; rb++) {
+            v16i acc = {0};
+            const int arow = rb * 32 + (lane & 31);
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) {
+                if (kk < ksteps) {
+                    v4i a = *(const v4i*)(tl + (size_t)arow * dimPad + 16 * swz_chunk(arow, 2 * kk + half));
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[kk], acc, 0, 0, 0);
+                }
+            }
+            // epilogue: s = |b'|^2 - 2 a'.b' for this lane's 16 train rows (increasing index)
+            int sv[16];
+            int smin = INT_MAX;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const int j = t * kT + row;
+                int s = ct[row] - 2 * acc[r];
+                s = (j < nB) ? s : INT_MAX;
+                sv[r] = s;
+                smin = smin < s ? smin : s;
+            }
+            if (__any(smin < b2)) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    top2_insert(sv[r], t * kT + row, b1, i1, b2, i2);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // lanes l and l+32 hold the same query (different train rows): merge
+    int c1 = __shfl_xor(b1, 32), j1 = __shfl_xor(i1, 32), c2 = __shfl_xor(b2, 32), j2 = __shfl_xor(i2, 32);
+    top2_merge(b1, i1, b2, i2, c1, j1, c2, j2);
+    if (half == 0 && qrow < nA) {
+        const int cq = cqA[qrow];
+        idxOut[2 * qrow] = i1;
+        idxOut[2 * qrow + 1] = i2;
+        keyOut[2 * qrow] = i1 >= 0 ? cq + b1 : INT_MAX;
+        keyOut[2 * qrow + 1] = i2 >= 0 ? cq + b2 : INT_MAX;
+    }
+}
+
+// ---------------- float rows, FLANN L2 order ----------------
+template <int DIM>
+__global__ __launch_bounds__(256) void knn2_f32_kernel(const float* __restrict__ A, int nA, const float* __restrict__ B,
+                                                       int nB, int* __restrict__ idxOut, float* __restrict__ keyOut) {
+    constexpr int TR = 32;  // train rows per tile
+    __shared__ float tile[TR * DIM];
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    float a[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; d++) a[d] = (q < nA) ? A[(size_t)q * DIM + d] : 0.f;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = -1, i2 = -1;
+    for (int t0 = 0; t0 < nB; t0 += TR) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < TR * DIM; e += blockDim.x) {
+            int j = t0 + e / DIM;
+            tile[e] = (j < nB) ? B[(size_t)t0 * DIM + e] : 0.f;
+        }
+        __syncthreads();
+        const int nr = (nB - t0) < TR ? (nB - t0) : TR;
+        for (int r = 0; r < nr; r++) {
+            const float* b = tile + r * DIM;
+            float result = 0.f;
+            int i = 0;
+#pragma unroll
+            for (; i + 3 < DIM; i += 4) {
+                float d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1], d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+                result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+            }
+#pragma unroll
+            for (; i < DIM; i++) {
+                float d0 = a[i] - b[i];
+                result += d0 * d0;
+            }
+            const int j = t0 + r;
+            if (result < b1) {
+                b2 = b1;
+                i2 = i1;
+                b1 = result;
+                i1 = j;
+            } else if (result < b2) {
+                b2 = result;
+                i2 = j;
+            }
+        }
+    }
+    if (q < nA) {
+        idxOut[2 * q] = i1;
+        idxOut[2 * q + 1] = i2;
+        keyOut[2 * q] = b1;
+        keyOut[2 * q + 1] = b2;
+    }
+}
+
+// generic dim: rows read from global memory (any dim, same FLANN order)
+__global__ __launch_bounds__(256) void knn2_f32_generic_kernel(const float* __restrict__ A, int nA,
+                                                               const float* __restrict__ B, int nB, int dim,
+                                                               int* __restrict__ idxOut, float* __restrict__ keyOut) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    const float* a = A + (size_t)q * dim;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = -1, i2 = -1;
+    for (int j = 0; j < nB; j++) {
+        const float* b = B + (size_t)j * dim;
+        float result = 0.f;
+        int i = 0;
+        for (; i + 3 < dim; i += 4) {
+            float d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1], d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+            result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+        }
+        for (; i < dim; i++) {
+            float d0 = a[i] - b[i];
+            result += d0 * d0;
+        }
+        if (result < b1) {
+            b2 = b1;
+            i2 = i1;
+            b1 = result;
+            i1 = j;
+        } else if (result < b2) {
+            b2 = result;
+            i2 = j;
+        }
+    }
+    idxOut[2 * q] = i1;
+    idxOut[2 * q + 1] = i2;
+    keyOut[2 * q] = b1;
+    keyOut[2 * q + 1] = b2;
+}
+
+// ---------------- binary strings, Hamming ----------------
+template <int NW>  // 32-bit words per descriptor
+__global__ __launch_bounds__(256) void knn2_bits_kernel(const uint32_t* __restrict__ A, int nA,
+                                                        const uint32_t* __restrict__ B, int nB,
+                                                        int* __restrict__ idxOut, int* __restrict__ keyOut) {
+    constexpr int TR = 256;
+    __shared__ uint32_t tile[TR * NW];
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t a[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) a[w] = (q < nA) ? A[(size_t)q * NW + w] : 0u;
+    int b1 = INT_MAX, b2 = INT_MAX, i1 = -1, i2 = -1;
+    for (int t0 = 0; t0 < nB; t0 += TR) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < TR * NW; e += blockDim.x) {
+            int j = t0 + e / NW;
+            tile[e] = (j < nB) ? B[(size_t)t0 * NW + e] : 0u;
+        }
+        __syncthreads();
+        const int nr = (nB - t0) < TR ? (nB - t0) : TR;
+        for (int r = 0; r < nr; r++) {
+            int h = 0;
+#pragma unroll
+            for (int w = 0; w < NW; w++) h += __popc(a[w] ^ tile[r * NW + w]);
+            top2_insert(h, t0 + r, b1, i1, b2, i2);
+        }
+    }
+    if (q < nA) {
+        idxOut[2 * q] = i1;
+        idxOut[2 * q + 1] = i2;
+        keyOut[2 * q] = b1;
+        keyOut[2 * q + 1] = b2;
+    }
+}
+
+__global__ void nndr_kernel(int type, const int* __restrict__ idx, const int* __restrict__ key,
+                            const float* __restrict__ fkey, int nA, double eps, int queryOffset,
+                            fm3d_dmatch* __restrict__ knnOut, fm3d_dmatch* __restrict__ cand, int* __restrict__ flag) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    const int i1 = idx[2 * q], i2 = idx[2 * q + 1];
+    float d1, d2;
+    if (type == FM3D_DESC_F32) {
+        // FlannBasedMatcher::convertToDMatches: dist = sqrt(L2sqr) in float
+        d1 = sqrtf(fkey[2 * q]);
+        d2 = sqrtf(fkey[2 * q + 1]);
+    } else if (type == FM3D_DESC_U8) {
+        d1 = sqrtf((float)key[2 * q]);
+        d2 = sqrtf((float)key[2 * q + 1]);
+    } else {
+        d1 = (float)key[2 * q];
+        d2 = (float)key[2 * q + 1];
+    }
+    if (knnOut) {
+        knnOut[2 * q] = fm3d_dmatch{q + queryOffset, i1, 0, d1};
+        knnOut[2 * q + 1] = fm3d_dmatch{q + queryOffset, i2, 0, d2};
+    }
+    // descriptorsmatcher.cpp:121-128: size() >= 2 and distance0 <= epsilon * distance1 (double)
+    const bool keep = (i1 >= 0 && i2 >= 0) && ((double)d1 <= eps * (double)d2);
+    flag[q] = keep ? 1 : 0;
+    cand[q] = fm3d_dmatch{q + queryOffset, i1, 0, d1};
+}
+
+}  // namespace
+
+void launch_rowconst_u8(const uint8_t* X, int n, int nPad, int dimPad, int* c, hipStream_t s) {
+    if (nPad <= 0) return;
+    rowconst_u8_kernel<<<(nPad + 255) / 256, 256, 0, s>>>(X, n, nPad, dimPad, c);
+}
+
+void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA, const int* ctB,
+                    int* idx, int* key, hipStream_t s) {
+    if (nA <= 0) return;
+    size_t lds = 2 * (size_t)kT * dimPad + 2 * kT * sizeof(int);
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)knn2_u8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    knn2_u8_kernel<<<(nA + kQ - 1) / kQ, kThreads, lds, s>>>(A, nA, B, nB, dimPad, cqA, ctB, idx, key);
+}
+
+void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, int* idx, float* key, hipStream_t s) {
+    if (nA <= 0) return;
+    const int grid = (nA + 255) / 256;
+    if (dim == 128)
+        knn2_f32_kernel<128><<<grid, 256, 0, s>>>(A, nA, B, nB, idx, key);
+    else if (dim == 64)
+        knn2_f32_kernel<64><<<grid, 256, 0, s>>>(A, nA, B, nB, idx, key);
+    else
+        knn2_f32_generic_kernel<<<grid, 256, 0, s>>>(A, nA, B, nB, dim, idx, key);
+}
+
+void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int* idx, int* key,
+                      hipStream_t s) {
+    if (nA <= 0) return;
+    const int grid = (nA + 255) / 256;
+    const uint32_t* a = (const uint32_t*)A;
+    const uint32_t* b = (const uint32_t*)B;
+    switch (dimBytes / 4) {
+        case 8: knn2_bits_kernel<8><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;
+        case 16: knn2_bits_kernel<16><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;
+        case 4: knn2_bits_kernel<4><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;
+        default: knn2_bits_kernel<16><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;  // padded to 64 B
+    }
+}
+
+void launch_nndr(int type, const int* idx, const int* key, const float* fkey, int nA, int nB, double eps,
+                 int queryOffset, fm3d_dmatch* knnOut, fm3d_dmatch* cand, int* flag, hipStream_t s) {
+    (void)nB;
+    if (nA <= 0) return;
+    nndr_kernel<<<(nA + 255) / 256, 256, 0, s>>>(type, idx, key, fkey, nA, eps, queryOffset, knnOut, cand, flag);
+}
+
+}  // namespace fm3d

@@ -1,0 +1,308 @@
+// fm3d_misc.hip -- triangulation, pyramids, undistortion and stable compaction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fm3d_kernels.h"
+
+namespace fm3d {
+
+namespace {
+
+// ---------------- DLT triangulation ----------------
+// Null vector of the 4x4 DLT system: one-sided (Hestenes) Jacobi SVD, cyclic pair
+// order, up to 30 sweeps; the same arithmetic as oracle/fm3d_oracle.c
+// (orc_dlt_nullvec).  OpenCV's cvSVD (JacobiSVD) is not reproducible bit for bit;
+// both agree with numpy.linalg.svd to ~1e-12 (tests/golden).
+__device__ inline void dlt_nullvec(double* A, double* v) {
+    double V[16];
+    for (int i = 0; i < 16; i++) V[i] = (i % 5 == 0) ? 1. : 0.;
+    for (int sweep = 0; sweep < 30; sweep++) {
+        bool rotated = false;
+        for (int p = 0; p < 3; p++)
+            for (int q = p + 1; q < 4; q++) {
+                double alpha = 0, beta = 0, gamma = 0;
+                for (int i = 0; i < 4; i++) {
+                    double ap = A[i * 4 + p], aq = A[i * 4 + q];
+                    alpha += ap * ap;
+                    beta += aq * aq;
+                    gamma += ap * aq;
+                }
+                if (gamma != 0. && fabs(gamma) > 1e-15 * sqrt(alpha * beta)) {
+                    double zeta = (beta - alpha) / (2. * gamma);
+                    double t = (zeta >= 0. ? 1. : -1.) / (fabs(zeta) + sqrt(1. + zeta * zeta));
+                    double cs = 1. / sqrt(1. + t * t);
+                    double sn = cs * t;
+                    for (int i = 0; i < 4; i++) {
+                        double ap = A[i * 4 + p], aq = A[i * 4 + q];
+                        A[i * 4 + p] = cs * ap - sn * aq;
+                        A[i * 4 + q] = sn * ap + cs * aq;
+                        ap = V[i * 4 + p];
+                        aq = V[i * 4 + q];
+                        V[i * 4 + p] = cs * ap - sn * aq;
+                        V[i * 4 + q] = sn * ap + cs * aq;
+                    }
+                    rotated = true;
+                }
+            }
+        if (!rotated) break;
+    }
+    double nrm[4];
+    for (int p = 0; p < 4; p++) {
+        double s = 0;
+        for (int i = 0; i < 4; i++) s += A[i * 4 + p] * A[i * 4 + p];
+        nrm[p] = s;
+    }
+    int best = 0;
+    for (int p = 1; p < 4; p++)
+        if (nrm[p] < nrm[best]) best = p;
+    for (int i = 0; i < 4; i++) v[i] = V[i * 4 + best];
+}
+
+// setKeypoints (singlecameratriangulator.cpp:145-171) + triangulate (:173-230), one
+// thread per match: gather, undistortPoints, cvTriangulatePoints, z filter.
+__global__ void triangulate_kernel(TriParams p) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.K) return;
+    const fm3d_dmatch mt = p.matches[i];
+    const fm3d_point2f k1 = p.kp1[mt.queryIdx - p.queryOffset];
+    const fm3d_point2f k2 = p.kp2[mt.trainIdx];
+    double u1x, u1y, u2x, u2y;
+    undistort1(p.cam, (double)k1.x, (double)k1.y, u1x, u1y);
+    undistort1(p.cam, (double)k2.x, (double)k2.y, u2x, u2y);
+    // P1 = [I|0], P2 = [I|0] * g12 (rows 0..2 of g12), A rows x*P.row2 - P.row0, y*P.row2 - P.row1
+    double A[16];
+    const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    for (int k = 0; k < 4; k++) {
+        A[0 * 4 + k] = u1x * P1[8 + k] - P1[0 + k];
+        A[1 * 4 + k] = u1y * P1[8 + k] - P1[4 + k];
+        A[2 * 4 + k] = u2x * p.g12[8 + k] - p.g12[0 + k];
+        A[3 * 4 + k] = u2y * p.g12[8 + k] - p.g12[4 + k];
+    }
+    double X[4];
+    dlt_nullvec(A, X);
+    // Z/W < zThresholdMin || Z/W >= zThresholdMax -> outlier (:200-216)
+    const bool out = (X[2] / X[3] < p.zmin || X[2] / X[3] >= p.zmax);
+    p.mask[i] = out ? 0 : 1;
+    if (p.mask8) p.mask8[i] = out ? 0 : 1;
+    p.pts[3 * i + 0] = X[0] / X[3];
+    p.pts[3 * i + 1] = X[1] / X[3];
+    p.pts[3 * i + 2] = X[2] / X[3];
+}
+
+// ---------------- cv::pyrDown (8U) ----------------
+__device__ inline int reflect101(int q, int len) {
+    if (len == 1) return 0;
+    while (q < 0 || q >= len) q = q < 0 ? -q : 2 * len - q - 2;
+    return q;
+}
+
+__global__ void pyrdown_kernel(const uint8_t* __restrict__ src, int w, int h, uint8_t* __restrict__ dst) {
+    const int dw = (w + 1) / 2, dh = (h + 1) / 2;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= dw || y >= dh) return;
+    const int wt[5] = {1, 4, 6, 4, 1};
+    int sx[5];
+    for (int j = 0; j < 5; j++) sx[j] = reflect101(2 * x + j - 2, w);
+    int s = 0;
+    for (int i = 0; i < 5; i++) {
+        const uint8_t* row = src + (size_t)reflect101(2 * y + i - 2, h) * w;
+        int rs = 0;
+        for (int j = 0; j < 5; j++) rs += wt[j] * row[sx[j]];
+        s += wt[i] * rs;
+    }
+    dst[(size_t)y * dw + x] = (uint8_t)((s + 128) >> 8);
+}
+
+__global__ void undistort_kernel(Camera cam, const double* __restrict__ xy, int n, double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    undistort1(cam, xy[2 * i], xy[2 * i + 1], out[2 * i], out[2 * i + 1]);
+}
+
+// ---------------- stable compaction (three-phase scan) ----------------
+constexpr int kScanBlock = 1024;  // items per block (256 threads x 4)
+
+__global__ void scan_count_kernel(const int* __restrict__ flag, int n, int* __restrict__ blockSums) {
+    __shared__ int red[256];
+    const int base = blockIdx.x * kScanBlock;
+    int c = 0;
+    for (int k = 0; k < 4; k++) {
+        int i = base + threadIdx.x * 4 + k;
+        c += (i < n && flag[i]) ? 1 : 0;
+    }
+    red[threadIdx.x] = c;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) blockSums[blockIdx.x] = red[0];
+}
+
+// exclusive scan of nb block sums in one workgroup of 1024 threads (chunked)
+__global__ void scan_blocks_kernel(int* __restrict__ blockSums, int nb, int* __restrict__ total) {
+    __shared__ int buf[1024];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < nb; c0 += 1024) {
+        const int i = c0 + threadIdx.x;
+        int v = (i < nb) ? blockSums[i] : 0;
+        buf[threadIdx.x] = v;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            int t = (int)threadIdx.x >= off ? buf[threadIdx.x - off] : 0;
+            __syncthreads();
+            buf[threadIdx.x] += t;
+            __syncthreads();
+        }
+        const int incl = buf[threadIdx.x];
+        if (i < nb) blockSums[i] = carry + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+// local exclusive offsets of a 1024-item block; returns the per-thread base
+__device__ inline int block_local_offset(const int* flag, int n, int base, int* sh, int& c4, int f[4]) {
+    c4 = 0;
+    for (int k = 0; k < 4; k++) {
+        int i = base + threadIdx.x * 4 + k;
+        f[k] = (i < n && flag[i]) ? 1 : 0;
+        c4 += f[k];
+    }
+    sh[threadIdx.x] = c4;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        int t = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += t;
+        __syncthreads();
+    }
+    return sh[threadIdx.x] - c4;
+}
+
+template <typename T>
+__global__ void scatter_kernel(const T* __restrict__ in, const int* __restrict__ flag, int n,
+                               const int* __restrict__ blockOff, T* __restrict__ out, int* __restrict__ srcIndex) {
+    __shared__ int sh[256];
+    const int base = blockIdx.x * kScanBlock;
+    int c4, f[4];
+    int o = blockOff[blockIdx.x] + block_local_offset(flag, n, base, sh, c4, f);
+    for (int k = 0; k < 4; k++) {
+        int i = base + threadIdx.x * 4 + k;
+        if (f[k]) {
+            out[o] = in[i];
+            if (srcIndex) srcIndex[o] = i;
+            o++;
+        }
+    }
+}
+
+struct Point3 {
+    double v[3];
+};
+
+__global__ void offsets_kernel(const int* __restrict__ flag, int n, const int* __restrict__ blockOff,
+                               int* __restrict__ offsets) {
+    __shared__ int sh[256];
+    const int base = blockIdx.x * kScanBlock;
+    int c4, f[4];
+    int o = blockOff[blockIdx.x] + block_local_offset(flag, n, base, sh, c4, f);
+    for (int k = 0; k < 4; k++) {
+        int i = base + threadIdx.x * 4 + k;
+        if (i < n) offsets[i] = o;
+        o += f[k];
+    }
+}
+
+template <typename T>
+void compact(const T* in, const int* flag, int n, T* out, int* count, int* srcIndex, void* tmp, hipStream_t s) {
+    const int nb = (n + kScanBlock - 1) / kScanBlock;
+    int* blockSums = (int*)tmp;
+    if (n <= 0) {
+        hipMemsetAsync(count, 0, sizeof(int), s);
+        return;
+    }
+    scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, blockSums);
+    scan_blocks_kernel<<<1, 1024, 0, s>>>(blockSums, nb, count);
+    scatter_kernel<T><<<nb, 256, 0, s>>>(in, flag, n, blockSums, out, srcIndex);
+}
+
+__global__ void make_records_kernel(const fm3d_dmatch* __restrict__ matches, const int* __restrict__ inlierSrc,
+                                    int nInl, const double* __restrict__ pts, const double* __restrict__ normals,
+                                    const int* __restrict__ status, fm3d_record* __restrict__ rec,
+                                    int* __restrict__ flag) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nInl) return;
+    const fm3d_dmatch m = matches[inlierSrc[i]];
+    fm3d_record r;
+    r.queryIdx = m.queryIdx;
+    r.trainIdx = m.trainIdx;
+    r.distance = m.distance;
+    r.status = status[i];
+    for (int k = 0; k < 3; k++) {
+        r.point[k] = pts[3 * i + k];
+        r.normal[k] = normals[3 * i + k];
+    }
+    rec[i] = r;
+    flag[i] = status[i] == FM3D_ST_OK ? 1 : 0;
+}
+
+}  // namespace
+
+void launch_triangulate(const TriParams& p, hipStream_t s) {
+    if (p.K <= 0) return;
+    triangulate_kernel<<<(p.K + 255) / 256, 256, 0, s>>>(p);
+}
+
+void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s) {
+    const int dw = (w + 1) / 2, dh = (h + 1) / 2;
+    dim3 blk(32, 8), grd((dw + 31) / 32, (dh + 7) / 8);
+    pyrdown_kernel<<<grd, blk, 0, s>>>(src, w, h, dst);
+}
+
+void launch_undistort(const Camera& cam, const double* xy, int n, double* out, hipStream_t s) {
+    if (n <= 0) return;
+    undistort_kernel<<<(n + 255) / 256, 256, 0, s>>>(cam, xy, n, out);
+}
+
+size_t scan_tmp_bytes(int n) { return sizeof(int) * ((size_t)(n + kScanBlock - 1) / kScanBlock + 16); }
+
+void launch_compact_dmatch(const fm3d_dmatch* in, const int* flag, int n, fm3d_dmatch* out, int* count, void* tmp,
+                           hipStream_t s) {
+    compact<fm3d_dmatch>(in, flag, n, out, count, nullptr, tmp, s);
+}
+
+void launch_compact_points(const double* in, const int* flag, int n, double* out, int* count, int* srcIndex,
+                           void* tmp, hipStream_t s) {
+    compact<Point3>((const Point3*)in, flag, n, (Point3*)out, count, srcIndex, tmp, s);
+}
+
+void launch_exclusive_scan(const int* flag, int n, int* offsets, int* total, void* tmp, hipStream_t s) {
+    const int nb = (n + kScanBlock - 1) / kScanBlock;
+    int* blockSums = (int*)tmp;
+    if (n <= 0) {
+        hipMemsetAsync(total, 0, sizeof(int), s);
+        return;
+    }
+    scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, blockSums);
+    scan_blocks_kernel<<<1, 1024, 0, s>>>(blockSums, nb, total);
+    offsets_kernel<<<nb, 256, 0, s>>>(flag, n, blockSums, offsets);
+}
+
+void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int nInl, const double* pts,
+                         const double* normals, const int* status, fm3d_record* rec, int* flag, hipStream_t s) {
+    if (nInl <= 0) return;
+    make_records_kernel<<<(nInl + 255) / 256, 256, 0, s>>>(matches, inlierSrc, nInl, pts, normals, status, rec, flag);
+}
+
+void launch_compact_records(const fm3d_record* in, const int* flag, int n, fm3d_record* out, int* count, void* tmp,
+                            hipStream_t s) {
+    compact<fm3d_record>(in, flag, n, out, count, nullptr, tmp, s);
+}
+
+}  // namespace fm3d

@@ -1,0 +1,160 @@
+// fm3d_settings.cpp -- settings.yml reader (cv::FileStorage %YAML:1.0 subset).
+//
+// The reference reads build/settings.yml through cv::FileStorage with ad-hoc keys
+// (main.cpp:62-98, singlecameratriangulator.cpp:45-112, normaloptimizer.cpp:154-164).
+// This parser accepts the subset that file uses: "%YAML:1.0" header, nested maps by
+// indentation, scalars, flow sequences "[a, b, c]", '#' comments.
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "fm3d.h"
+
+namespace {
+
+std::string trim(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) a++;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) b--;
+    return s.substr(a, b - a);
+}
+
+bool parse_yaml(const char* path, std::map<std::string, std::string>& kv) {
+    std::ifstream in(path);
+    if (!in) return false;
+    std::string line;
+    std::vector<std::pair<int, std::string>> stack;  // (indent, key)
+    bool first = true;
+    while (std::getline(in, line)) {
+        if (first) {
+            first = false;
+            if (line.rfind("%YAML", 0) == 0) continue;
+        }
+        // strip comments (not inside quotes; settings.yml has none)
+        size_t hash = line.find('#');
+        if (hash != std::string::npos) line = line.substr(0, hash);
+        if (trim(line).empty()) continue;
+        int indent = 0;
+        while (indent < (int)line.size() && line[indent] == ' ') indent++;
+        std::string body = trim(line);
+        size_t colon = body.find(':');
+        if (colon == std::string::npos) continue;
+        std::string key = trim(body.substr(0, colon));
+        std::string val = trim(body.substr(colon + 1));
+        while (!stack.empty() && stack.back().first >= indent) stack.pop_back();
+        std::string full;
+        for (auto& e : stack) full += e.second + ".";
+        full += key;
+        if (val.empty()) {
+            stack.push_back({indent, key});
+        } else {
+            if (val.size() >= 2 && (val[0] == '"' || val[0] == '\'')) val = val.substr(1, val.size() - 2);
+            kv[full] = val;
+        }
+    }
+    return true;
+}
+
+bool get_d(const std::map<std::string, std::string>& kv, const char* k, double* out) {
+    auto it = kv.find(k);
+    if (it == kv.end()) return false;
+    *out = std::strtod(it->second.c_str(), nullptr);
+    return true;
+}
+
+bool get_i(const std::map<std::string, std::string>& kv, const char* k, int* out) {
+    double d;
+    if (!get_d(kv, k, &d)) return false;
+    *out = (int)d;
+    return true;
+}
+
+bool get_vec(const std::map<std::string, std::string>& kv, const char* k, double* out, int n) {
+    auto it = kv.find(k);
+    if (it == kv.end()) return false;
+    std::string v = it->second;
+    for (char& c : v)
+        if (c == '[' || c == ']' || c == ',') c = ' ';
+    std::istringstream ss(v);
+    for (int i = 0; i < n; i++)
+        if (!(ss >> out[i])) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int fm3d_settings_default(fm3d_settings* s) {
+    if (!s) return FM3D_ERR_INVALID;
+    std::memset(s, 0, sizeof(*s));
+    // build/settings.yml
+    s->Fx = 572.4765;
+    s->Fy = 572.69354;
+    s->Cx = 549.75189;
+    s->Cy = 411.68039;
+    s->p1 = -6.6e-05;
+    s->p2 = 0.000567;
+    s->k0 = -0.299957;
+    s->k1 = 0.124129;
+    s->k2 = -0.028357;
+    s->rodriguesIC[0] = -1.2005;
+    s->rodriguesIC[1] = 1.1981;
+    s->rodriguesIC[2] = -1.2041;
+    s->translationIC[0] = 0.0;
+    s->translationIC[1] = 0.015;
+    s->translationIC[2] = -0.051;
+    s->zThresholdMin = 1.5;
+    s->zThresholdMax = 2.4;
+    s->epsilonLMMIN = 1e-10;
+    s->pixelsRay = 64;
+    s->pyramids = 3;
+    s->nndrEpsilon = 0.55;
+    const double p1[6] = {5.301099, 8.031408, 1.977258, 0.153433, 0.149941, -2.658648};
+    const double p2[6] = {4.735536, 7.691893, 1.913166, 0.252828, 0.048977, -2.676886};
+    for (int i = 0; i < 6; i++) {
+        s->pos1[i] = p1[i];
+        s->pos2[i] = p2[i];
+    }
+    s->boundWidth = 1024;
+    s->boundHeight = 768;
+    s->strictNanExit = 0;
+    s->lmWaves = 0;
+    return FM3D_OK;
+}
+
+extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
+    if (!path || !s) return FM3D_ERR_INVALID;
+    std::map<std::string, std::string> kv;
+    if (!parse_yaml(path, kv)) return FM3D_ERR_PARSE;
+    fm3d_settings_default(s);
+    get_d(kv, "CameraSettings.Fx", &s->Fx);
+    get_d(kv, "CameraSettings.Fy", &s->Fy);
+    get_d(kv, "CameraSettings.Cx", &s->Cx);
+    get_d(kv, "CameraSettings.Cy", &s->Cy);
+    get_d(kv, "CameraSettings.p1", &s->p1);
+    get_d(kv, "CameraSettings.p2", &s->p2);
+    get_d(kv, "CameraSettings.k0", &s->k0);
+    get_d(kv, "CameraSettings.k1", &s->k1);
+    get_d(kv, "CameraSettings.k2", &s->k2);
+    get_vec(kv, "CameraSettings.rodriguesIC", s->rodriguesIC, 3);
+    get_vec(kv, "CameraSettings.translationIC", s->translationIC, 3);
+    get_d(kv, "CameraSettings.zThresholdMin", &s->zThresholdMin);
+    get_d(kv, "CameraSettings.zThresholdMax", &s->zThresholdMax);
+    get_d(kv, "Neighborhoods.epsilonLMMIN", &s->epsilonLMMIN);
+    get_i(kv, "Neighborhoods.pixelsRay", &s->pixelsRay);
+    get_i(kv, "Neighborhoods.pyramids", &s->pyramids);
+    get_d(kv, "NNDR.epsilon", &s->nndrEpsilon);
+    get_vec(kv, "IMAGES.pos1", s->pos1, 6);
+    get_vec(kv, "IMAGES.pos2", s->pos2, 6);
+    // extensions (optional section)
+    get_i(kv, "Fm3d.boundWidth", &s->boundWidth);
+    get_i(kv, "Fm3d.boundHeight", &s->boundHeight);
+    get_i(kv, "Fm3d.strictNanExit", &s->strictNanExit);
+    get_i(kv, "Fm3d.lmWaves", &s->lmWaves);
+    return FM3D_OK;
+}

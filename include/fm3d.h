@@ -1,0 +1,189 @@
+/*
+ * fm3d.h -- C ABI of the MI355X-native 3DFeatureMatcher hot path.
+ *
+ * The reference (caomw/3DFeatureMatcher) exposes this path as three C++ classes
+ * called from main.cpp:91-155.  Every entry point below replaces one of their
+ * methods; the citation names the reference interface it stands in for.  Plain
+ * C types only (no OpenCV / torch types): the C++ shim in
+ * include/fm3d_compat.hpp re-exposes the reference class signatures on top of
+ * this ABI, and INTEGRATION.md shows the bindings.
+ *
+ * Conventions
+ *   - every function returns FM3D_OK (0) or a negative FM3D_ERR_* code; the
+ *     reference's exit() paths become error returns (fm3d_last_error() has the text);
+ *   - host pointers unless the name ends in _dev; the caller owns all buffers;
+ *   - a context owns its device buffers (grown on demand, reused across calls),
+ *     one HIP stream, and is not thread-safe (one host thread per context);
+ *   - the per-point "erase" of the reference (normaloptimizer.cpp:366,378) is a
+ *     stable compaction: survivors keep their input order.
+ */
+#ifndef FM3D_H
+#define FM3D_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FM3D_OK 0
+#define FM3D_ERR_INVALID (-1)     /* bad argument / state (the reference would exit(-1)) */
+#define FM3D_ERR_HIP (-2)         /* HIP runtime error */
+#define FM3D_ERR_UNSUPPORTED (-3) /* e.g. pixelsRay larger than the kernel supports */
+#define FM3D_ERR_NOMEM (-4)
+#define FM3D_ERR_PARSE (-5)       /* settings file could not be read */
+#define FM3D_ERR_NAN_PLANE (-6)   /* strictNanExit: projectPointToPlane exit(-6),
+                                     singlecameratriangulator.cpp:465-469 */
+
+/* per-point outcome of the normal optimisation */
+#define FM3D_ST_OK 0
+#define FM3D_ST_NO_PIXELS 1   /* "Not enough pixels!"  normaloptimizer.cpp:364-369 */
+#define FM3D_ST_ABORT_BBOX 2  /* isInBoundingBox failed, singlecameratriangulator.cpp:557-560 */
+#define FM3D_ST_ABORT_PIX1 3  /* image-1 pixel outside isPixelGood, :580-584 */
+#define FM3D_ST_ABORT_PIX2 4  /* image-2 projection outside isPixelGood, :623-626 */
+#define FM3D_ST_NAN_PLANE 5   /* ray parallel to the plane (reference: exit(-6)) */
+#define FM3D_ST_NAN_NORMAL 6  /* sph2car produced NaN, normaloptimizer.cpp:81-85 */
+
+typedef struct fm3d_ctx fm3d_ctx;
+
+/* Settings: the keys of build/settings.yml the hot path reads. */
+typedef struct fm3d_settings {
+    /* CameraSettings (singlecameratriangulator.cpp:45-109) */
+    double Fx, Fy, Cx, Cy;
+    double p1, p2, k0, k1, k2; /* OpenCV order (k1,k2,p1,p2,k3) = (k0,k1,p1,p2,k2) */
+    double rodriguesIC[3];
+    double translationIC[3];
+    double zThresholdMin, zThresholdMax;
+    /* Neighborhoods (normaloptimizer.cpp:154-156, singlecameratriangulator.cpp:112) */
+    double epsilonLMMIN;
+    int pixelsRay;
+    int pyramids;
+    /* NNDR (main.cpp:94) */
+    double nndrEpsilon;
+    /* IMAGES.pos1 / pos2: T(3) then Rodrigues(3) (main.cpp:96-114) */
+    double pos1[6], pos2[6];
+    /* --- extensions (not in the reference file) --- */
+    int boundWidth, boundHeight; /* literal 1024 x 768 of extractPixelsContour (:359) */
+    int strictNanExit;           /* 1: NaN plane makes fm3d_optimize_normals fail with FM3D_ERR_NAN_PLANE */
+    int lmWaves;                 /* LM kernel wavefronts (0 = auto) */
+} fm3d_settings;
+
+/* cv::DMatch layout */
+typedef struct fm3d_dmatch {
+    int32_t queryIdx, trainIdx, imgIdx;
+    float distance;
+} fm3d_dmatch;
+
+/* cv::KeyPoint::pt */
+typedef struct fm3d_point2f {
+    float x, y;
+} fm3d_point2f;
+
+typedef enum fm3d_desc_type {
+    FM3D_DESC_F32 = 0,  /* float rows (SURF/SIFT): FLANN L2 order, distance = sqrt */
+    FM3D_DESC_U8 = 1,   /* uint8 rows (SIFT saturated to uchar): exact integer L2 */
+    FM3D_DESC_BITS = 2  /* binary strings, dim = bytes (ORB/BRISK/FREAK): Hamming */
+} fm3d_desc_type;
+
+/* one surviving keypoint of the whole hot path (64 bytes) */
+typedef struct fm3d_record {
+    int32_t queryIdx, trainIdx;
+    float distance;
+    int32_t status;
+    double point[3];
+    double normal[3];
+} fm3d_record;
+
+typedef struct fm3d_lm_stats {
+    int64_t points_in;
+    int64_t points_kept;
+    int64_t evaluations;       /* residual evaluations, all points and levels */
+    int64_t pixel_evaluations; /* sum over evaluations of m_dat */
+    int64_t drops[8];          /* points per FM3D_ST_* code */
+    double kernel_ms;          /* LM kernel time (HIP events on the context stream) */
+} fm3d_lm_stats;
+
+typedef struct fm3d_pipeline_stats {
+    int64_t queries, trains, matches, inliers, kept;
+    double match_ms, nndr_ms, triangulate_ms, pyramid_ms, lm_ms, total_ms; /* HIP events */
+    fm3d_lm_stats lm;
+} fm3d_pipeline_stats;
+
+/* ---------------- settings / context ---------------- */
+/* build/settings.yml values (the reference's defaults) */
+int fm3d_settings_default(fm3d_settings *s);
+/* read a %YAML:1.0 cv::FileStorage file (the subset settings.yml uses) */
+int fm3d_settings_load(const char *path, fm3d_settings *s);
+int fm3d_ctx_create(const fm3d_settings *s, int device, fm3d_ctx **out);
+void fm3d_ctx_destroy(fm3d_ctx *ctx);
+const char *fm3d_last_error(const fm3d_ctx *ctx);
+/* use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream */
+int fm3d_ctx_set_stream(fm3d_ctx *ctx, void *hip_stream);
+
+/* ---------------- DescriptorsMatcher ---------------- */
+/* knnMatch(A, B, k=2) of DescriptorsMatcher::compare (descriptorsmatcher.cpp:89-105), exact
+   brute force in (distance, trainIdx) order.  out: nA*2 entries, trainIdx -1 when nB < 2. */
+int fm3d_knn2(fm3d_ctx *ctx, const void *descA, int nA, const void *descB, int nB, int dim, int type,
+              fm3d_dmatch *out);
+/* matcher + NNDR of DescriptorsMatcher::compareWithNNDR (descriptorsmatcher.cpp:117-129):
+   keep m[0] iff two neighbours exist and m[0].distance <= epsilon * m[1].distance.
+   matches: capacity nA, written in query order; *nMatches = count. */
+int fm3d_match_nndr(fm3d_ctx *ctx, const void *descA, int nA, const void *descB, int nB, int dim, int type,
+                    double epsilon, fm3d_dmatch *matches, int *nMatches);
+
+/* ---------------- SingleCameraTriangulator ---------------- */
+/* setg12 (singlecameratriangulator.cpp:123-143): g12 = gIC^-1 g2^-1 g1 gIC, row-major 4x4 */
+int fm3d_setg12(fm3d_ctx *ctx, const double T1[3], const double T2[3], const double r1[3], const double r2[3],
+                double g12[16]);
+/* context-free versions of the two above (pure host algebra, usable without a GPU) */
+int fm3d_g12_from_poses(const fm3d_settings *s, const double T1[3], const double T2[3], const double r1[3],
+                        const double r2[3], double g12[16]);
+int fm3d_camera2_from_g12(const double g12[16], double R2[9], double t2[3]);
+/* install a g12 computed elsewhere */
+int fm3d_set_g12(fm3d_ctx *ctx, const double g12[16]);
+/* R2, t2 that projectPointsToImage2 projects with: Rodrigues(Rodrigues^-1(R12)), t12 (:591-602) */
+int fm3d_get_camera2(const fm3d_ctx *ctx, double R2[9], double t2[3]);
+/* setKeypoints (:145-171) + triangulate (:173-230).  points: capacity 3*nMatches (compacted,
+   match order); inlierMask: nMatches bytes (the outliersMask). */
+int fm3d_triangulate(fm3d_ctx *ctx, const fm3d_point2f *kpts1, int n1, const fm3d_point2f *kpts2, int n2,
+                     const fm3d_dmatch *matches, int nMatches, double *points, uint8_t *inlierMask, int *nPoints);
+
+/* ---------------- NormalOptimizer ---------------- */
+/* setImages (normaloptimizer.cpp:191-221): 8-bit gray images, builds both pyramids */
+int fm3d_set_images(fm3d_ctx *ctx, const uint8_t *img1, const uint8_t *img2, int width, int height, int stride);
+/* copy pyramid level `level` of image `which` (1 or 2) to host; *w,*h receive its size */
+int fm3d_get_pyramid_level(const fm3d_ctx *ctx, int which, int level, uint8_t *out, int *w, int *h);
+/* computeOptimizedNormals (normaloptimizer.cpp:321-452).  points: in/out, 3*P doubles, compacted
+   in place to the kept points (reference erase semantics); normals: capacity 3*P; status: P
+   codes per INPUT point (may be NULL); info/nfev: 8 ints per input point (lmdif info and
+   evaluation count per pyramid level, may be NULL). */
+int fm3d_optimize_normals(fm3d_ctx *ctx, double *points, int P, double *normals, int32_t *status,
+                          int32_t *info, int32_t *nfev, int *nKept, fm3d_lm_stats *stats);
+
+/* ---------------- the whole hot path, device resident ---------------- */
+/* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */
+int fm3d_pipeline_upload(fm3d_ctx *ctx, const void *descA, int nA, const void *descB, int nB, int dim, int type,
+                         const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1,
+                         const uint8_t *img2, int width, int height, int queryOffset);
+/* Run match -> NNDR -> triangulate -> pyramids -> LM normals on the staged inputs.
+   recordsDev: device buffer with capacity nA records (NULL: internal); *nKept: survivors.
+   Synchronises the context stream before returning. */
+int fm3d_pipeline_run(fm3d_ctx *ctx, fm3d_record *recordsDev, int *nKept, fm3d_pipeline_stats *stats);
+/* copy n records from a device record buffer (NULL = internal) to host */
+int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, fm3d_record *out);
+
+/* ---------------- building blocks exposed for tests ---------------- */
+/* cv::pyrDown of one 8-bit image (normaloptimizer.cpp:216-217) */
+int fm3d_pyrdown(fm3d_ctx *ctx, const uint8_t *src, int width, int height, uint8_t *dst);
+/* extractPixelsContour(Vec3d) (:376-397): kept pixel coordinates (2*cap doubles), returns m via *m */
+int fm3d_neighborhood(fm3d_ctx *ctx, const double X[3], double *xy, int cap, int *m);
+/* cv::undistortPoints of n pixel coordinates (device kernel) */
+int fm3d_undistort(fm3d_ctx *ctx, const double *xy, int n, double *out);
+
+/* library version string */
+const char *fm3d_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FM3D_H */

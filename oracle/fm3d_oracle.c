@@ -1,0 +1,1308 @@
+/*
+ * fm3d_oracle.c -- CPU ORACLE for the 3DFeatureMatcher hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * or the timed CPU baseline.  The product (3dfeaturematcher_amd/libfm3d.so)
+ * never links, loads or calls it.
+ *
+ * It is a plain-C restatement of the reference algorithm, following the
+ * reference sources (paths relative to caomw/3DFeatureMatcher):
+ *   DescriptorsMatcher/descriptorsmatcher.cpp:107-131   knnMatch(k=2) + NNDR
+ *   Triangulator/singlecameratriangulator.cpp:123-230   setg12, setKeypoints, triangulate
+ *   Triangulator/singlecameratriangulator.cpp:341-397   extractPixelsContour
+ *   Triangulator/singlecameratriangulator.cpp:421-470   projectPointToPlane
+ *   Triangulator/singlecameratriangulator.cpp:530-665   get3dPoints / intensities / projection / bounds
+ *   Triangulator/normaloptimizer.cpp:65-149             evaluateNormal (LM residual)
+ *   Triangulator/normaloptimizer.cpp:206-292            pyramids, optimize_pyramid, optimize
+ *   Triangulator/normaloptimizer.cpp:321-452            computeOptimizedNormals (erase semantics)
+ *   tools.cpp:87-142, 767-777                           compose/decompose, bilinear, sph<->car
+ * and the third-party arithmetic the reference calls (not vendored in the
+ * reference, versions unpinned; restated from their published algorithms):
+ *   OpenCV 2.4.x: undistortPoints, projectPoints, Rodrigues, triangulatePoints,
+ *                 Matx44d::inv (LU), pyrDown, FLANN L2/Hamming distances
+ *   lmfit ~3.x/4.0 lmmin == MINPACK lmdif/qrfac/lmpar/qrsolv with lmfit defaults
+ *                 (ftol=xtol=gtol=30*DBL_EPSILON, stepbound 100, patience 100)
+ *
+ * Parity pinning: the reference has no tests and no golden
+ * vectors, and cannot be built here (OpenCV/PCL/lmfit absent).  The oracle is
+ * pinned by tests/golden fixtures produced by independent numpy/scipy code
+ * (numpy brute force, numpy.linalg.svd DLT, scipy.optimize.leastsq = MINPACK
+ * lmdif driving a numpy evaluateNormal).  Exact lmfit trajectories are
+ * "parity unpinned".
+ *
+ * Two LM modes:
+ *   ORC_LM_STRICT    : MINPACK Householder QR, index-order sums, libm transcendentals.
+ *   ORC_LM_CANONICAL : the GPU kernel's arithmetic: Gram-sum QR over blocked
+ *                      reductions (nthreads lanes, wave 64 trees) and the
+ *                      deterministic transcendentals of include/fm3d_detmath.h.
+ *                      The GPU kernel must equal this mode bit for bit.
+ * Compiled with -ffp-contract=off (no FMA contraction), like the kernels.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+#include "fm3d_detmath.h"
+
+#define ORC_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------ */
+/* camera model                                                        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    double fx, fy, cx, cy;
+    double k[5]; /* OpenCV order k1,k2,p1,p2,k3 == settings k0,k1,p1,p2,k2
+                    (singlecameratriangulator.cpp:99-105) */
+} orc_camera;
+
+/* cvUndistortPoints (OpenCV 2.4), 5 fixed-point iterations, R = I, P = none.
+   Call sites: singlecameratriangulator.cpp:169-170 and :542. */
+static void orc_undistort1(const orc_camera *c, double x, double y, double *ox, double *oy)
+{
+    const double *k = c->k;
+    double ifx = 1. / c->fx, ify = 1. / c->fy;
+    double x0, y0;
+    int j;
+    x0 = x = (x - c->cx) * ifx;
+    y0 = y = (y - c->cy) * ify;
+    for (j = 0; j < 5; j++) {
+        double r2 = x * x + y * y;
+        /* rational-model numerator with k5..k7 = 0 evaluates to exactly 1 */
+        double icdist = (1 + ((0. * r2 + 0.) * r2 + 0.) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x);
+        double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    {   /* RR = identity */
+        double xx = 1. * x + 0. * y + 0.;
+        double yy = 0. * x + 1. * y + 0.;
+        double ww = 1. / (0. * x + 0. * y + 1.);
+        *ox = xx * ww;
+        *oy = yy * ww;
+    }
+}
+
+/* cvProjectPoints2 (OpenCV 2.4) for one point with rotation matrix R (row-major)
+   and translation t.  Call sites: singlecameratriangulator.cpp:388 (R=I,t=0) and
+   :602 (R = Rodrigues(decompose(g12))). */
+static void orc_project1(const orc_camera *c, const double R[9], const double t[3],
+                         double X, double Y, double Z, double *u, double *v)
+{
+    const double *k = c->k;
+    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    double r2, r4, r6, a1, a2, a3, cdist, icdist2, xd, yd;
+    z = z ? 1. / z : 1;
+    x *= z;
+    y *= z;
+    r2 = x * x + y * y;
+    r4 = r2 * r2;
+    r6 = r4 * r2;
+    a1 = 2 * x * y;
+    a2 = r2 + 2 * x * x;
+    a3 = r2 + 2 * y * y;
+    cdist = 1 + k[0] * r2 + k[1] * r4 + k[4] * r6;
+    icdist2 = 1. / (1 + 0. * r2 + 0. * r4 + 0. * r6);
+    xd = x * cdist * icdist2 + k[2] * a1 + k[3] * a2;
+    yd = y * cdist * icdist2 + k[2] * a3 + k[3] * a1;
+    *u = xd * c->fx + c->cx;
+    *v = yd * c->fy + c->cy;
+}
+
+ORC_API void orc_undistort(const orc_camera *c, const double *xy, int n, double *out)
+{
+    int i;
+    for (i = 0; i < n; i++) orc_undistort1(c, xy[2 * i], xy[2 * i + 1], &out[2 * i], &out[2 * i + 1]);
+}
+
+ORC_API void orc_project(const orc_camera *c, const double R[9], const double t[3],
+                         const double *P, int n, double *out)
+{
+    int i;
+    for (i = 0; i < n; i++)
+        orc_project1(c, R, t, P[3 * i], P[3 * i + 1], P[3 * i + 2], &out[2 * i], &out[2 * i + 1]);
+}
+
+/* ------------------------------------------------------------------ */
+/* Rodrigues / 4x4 transforms (host-side algebra, a3)                  */
+/* ------------------------------------------------------------------ */
+/* cvRodrigues2 vector -> matrix */
+ORC_API void orc_rodrigues_v2m(const double r[3], double R[9])
+{
+    double rx = r[0], ry = r[1], rz = r[2];
+    double theta = sqrt(rx * rx + ry * ry + rz * rz);
+    int k;
+    if (theta < DBL_EPSILON) {
+        for (k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? 1. : 0.;
+        return;
+    }
+    {
+        const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        double c = cos(theta), s = sin(theta), c1 = 1. - c;
+        double itheta = theta ? 1. / theta : 0.;
+        double rrt[9], rxm[9];
+        rx *= itheta; ry *= itheta; rz *= itheta;
+        rrt[0] = rx * rx; rrt[1] = rx * ry; rrt[2] = rx * rz;
+        rrt[3] = rx * ry; rrt[4] = ry * ry; rrt[5] = ry * rz;
+        rrt[6] = rx * rz; rrt[7] = ry * rz; rrt[8] = rz * rz;
+        rxm[0] = 0; rxm[1] = -rz; rxm[2] = ry;
+        rxm[3] = rz; rxm[4] = 0; rxm[5] = -rx;
+        rxm[6] = -ry; rxm[7] = rx; rxm[8] = 0;
+        for (k = 0; k < 9; k++) R[k] = c * I[k] + c1 * rrt[k] + s * rxm[k];
+    }
+}
+
+/* 3x3 inverse transpose via adjugate (for the polar iteration below) */
+static void orc_inv_t3(const double A[9], double out[9])
+{
+    double c00 = A[4] * A[8] - A[5] * A[7];
+    double c01 = A[5] * A[6] - A[3] * A[8];
+    double c02 = A[3] * A[7] - A[4] * A[6];
+    double c10 = A[2] * A[7] - A[1] * A[8];
+    double c11 = A[0] * A[8] - A[2] * A[6];
+    double c12 = A[1] * A[6] - A[0] * A[7];
+    double c20 = A[1] * A[5] - A[2] * A[4];
+    double c21 = A[2] * A[3] - A[0] * A[5];
+    double c22 = A[0] * A[4] - A[1] * A[3];
+    double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+    double id = 1. / det;
+    /* inverse transpose = cofactor matrix / det */
+    out[0] = c00 * id; out[1] = c01 * id; out[2] = c02 * id;
+    out[3] = c10 * id; out[4] = c11 * id; out[5] = c12 * id;
+    out[6] = c20 * id; out[7] = c21 * id; out[8] = c22 * id;
+}
+
+/* cvRodrigues2 matrix -> vector.  OpenCV first replaces R by U*V^T of its SVD
+   (nearest orthonormal matrix); we compute the same polar factor with three
+   Newton steps X <- (X + X^-T)/2 (deterministic; equal to the SVD route within
+   a few ulp for the near-orthonormal inputs this path sees). */
+ORC_API void orc_rodrigues_m2v(const double Rin[9], double r[3])
+{
+    double R[9], Y[9];
+    double rx, ry, rz, s, c, theta;
+    int it, k;
+    memcpy(R, Rin, sizeof(R));
+    for (it = 0; it < 3; it++) {
+        orc_inv_t3(R, Y);
+        for (k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
+    }
+    rx = R[7] - R[5];
+    ry = R[2] - R[6];
+    rz = R[3] - R[1];
+    s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    theta = acos(c);
+    if (s < 1e-5) {
+        double t;
+        if (c > 0)
+            rx = ry = rz = 0;
+        else {
+            t = (R[0] + 1) * 0.5;
+            rx = sqrt(t > 0. ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = sqrt(t > 0. ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = sqrt(t > 0. ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            theta /= sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta; ry *= theta; rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= theta;
+        rx *= vth; ry *= vth; rz *= vth;
+    }
+    r[0] = rx; r[1] = ry; r[2] = rz;
+}
+
+/* composeTransformation, tools.cpp:87-99 */
+static void orc_compose(const double R[9], const double T[3], double G[16])
+{
+    G[0] = R[0]; G[1] = R[1]; G[2] = R[2]; G[3] = T[0];
+    G[4] = R[3]; G[5] = R[4]; G[6] = R[5]; G[7] = T[1];
+    G[8] = R[6]; G[9] = R[7]; G[10] = R[8]; G[11] = T[2];
+    G[12] = 0; G[13] = 0; G[14] = 0; G[15] = 1;
+}
+
+/* Matx44d::inv() == OpenCV LU with partial pivoting (DECOMP_LU) */
+static void orc_inv4(const double Ain[16], double B[16])
+{
+    double A[16];
+    int i, j, k;
+    memcpy(A, Ain, sizeof(A));
+    for (i = 0; i < 16; i++) B[i] = (i % 5 == 0) ? 1. : 0.;
+    for (i = 0; i < 4; i++) {
+        double d;
+        k = i;
+        for (j = i + 1; j < 4; j++)
+            if (fabs(A[j * 4 + i]) > fabs(A[k * 4 + i])) k = j;
+        if (k != i) {
+            for (j = i; j < 4; j++) { double t = A[i * 4 + j]; A[i * 4 + j] = A[k * 4 + j]; A[k * 4 + j] = t; }
+            for (j = 0; j < 4; j++) { double t = B[i * 4 + j]; B[i * 4 + j] = B[k * 4 + j]; B[k * 4 + j] = t; }
+        }
+        d = -1 / A[i * 4 + i];
+        for (j = i + 1; j < 4; j++) {
+            double alpha = A[j * 4 + i] * d;
+            for (k = i + 1; k < 4; k++) A[j * 4 + k] += alpha * A[i * 4 + k];
+            for (k = 0; k < 4; k++) B[j * 4 + k] += alpha * B[i * 4 + k];
+        }
+        A[i * 4 + i] = -d;
+    }
+    for (i = 3; i >= 0; i--)
+        for (j = 0; j < 4; j++) {
+            double s = B[i * 4 + j];
+            for (k = i + 1; k < 4; k++) s -= A[i * 4 + k] * B[k * 4 + j];
+            B[i * 4 + j] = s * A[i * 4 + i];
+        }
+}
+
+static void orc_mul4(const double a[16], const double b[16], double c[16])
+{
+    int i, j, k;
+    for (i = 0; i < 4; i++)
+        for (j = 0; j < 4; j++) {
+            double s = 0;
+            for (k = 0; k < 4; k++) s += a[i * 4 + k] * b[k * 4 + j];
+            c[i * 4 + j] = s;
+        }
+}
+
+/* SingleCameraTriangulator ctor (:42-65) + setg12 (:123-143):
+   g12 = gIC^-1 * g2^-1 * g1 * gIC */
+ORC_API void orc_setg12(const double rIC[3], const double tIC[3], const double T1[3], const double T2[3],
+                        const double r1[3], const double r2[3], double g12[16])
+{
+    double RIC[9], R1[9], R2[9], gIC[16], g1[16], g2[16], a[16], b[16], c[16], d[16];
+    orc_rodrigues_v2m(rIC, RIC);
+    orc_compose(RIC, tIC, gIC);
+    orc_rodrigues_v2m(r1, R1);
+    orc_rodrigues_v2m(r2, R2);
+    orc_compose(R1, T1, g1);
+    orc_compose(R2, T2, g2);
+    orc_inv4(gIC, a);
+    orc_inv4(g2, b);
+    orc_mul4(a, b, c);
+    orc_mul4(c, g1, d);
+    orc_mul4(d, gIC, g12);
+}
+
+/* decomposeTransformation (tools.cpp:101-114) followed by the Rodrigues
+   vector->matrix that cvProjectPoints2 applies to r2: the exact R2,t2 that
+   projectPointsToImage2 (singlecameratriangulator.cpp:591-602) projects with. */
+ORC_API void orc_camera2_from_g12(const double g12[16], double R2[9], double t2[3])
+{
+    double R[9], r[3];
+    R[0] = g12[0]; R[1] = g12[1]; R[2] = g12[2];
+    R[3] = g12[4]; R[4] = g12[5]; R[5] = g12[6];
+    R[6] = g12[8]; R[7] = g12[9]; R[8] = g12[10];
+    orc_rodrigues_m2v(R, r);
+    orc_rodrigues_v2m(r, R2);
+    t2[0] = g12[3]; t2[1] = g12[7]; t2[2] = g12[11];
+}
+
+/* ------------------------------------------------------------------ */
+/* DLT triangulation (a4, a5)                                          */
+/* ------------------------------------------------------------------ */
+/* Null vector of the 4x4 DLT system by one-sided (Hestenes) Jacobi SVD with a
+   fixed cyclic pair order, the same sweep rule as the GPU kernel.  OpenCV's
+   cvSVD (JacobiSVD) is not reproducible bit for bit; the null vector agrees
+   with numpy.linalg.svd to ~1e-12 (tests/golden). */
+static void orc_dlt_nullvec(double A[16], double v[4])
+{
+    double V[16];
+    int sweep, p, q, i, best;
+    for (i = 0; i < 16; i++) V[i] = (i % 5 == 0) ? 1. : 0.;
+    for (sweep = 0; sweep < 30; sweep++) {
+        int rotated = 0;
+        for (p = 0; p < 3; p++)
+            for (q = p + 1; q < 4; q++) {
+                double alpha = 0, beta = 0, gamma = 0;
+                for (i = 0; i < 4; i++) {
+                    double ap = A[i * 4 + p], aq = A[i * 4 + q];
+                    alpha += ap * ap;
+                    beta += aq * aq;
+                    gamma += ap * aq;
+                }
+                if (gamma != 0. && fabs(gamma) > 1e-15 * sqrt(alpha * beta)) {
+                    double zeta = (beta - alpha) / (2. * gamma);
+                    double t = (zeta >= 0. ? 1. : -1.) / (fabs(zeta) + sqrt(1. + zeta * zeta));
+                    double cs = 1. / sqrt(1. + t * t);
+                    double sn = cs * t;
+                    for (i = 0; i < 4; i++) {
+                        double ap = A[i * 4 + p], aq = A[i * 4 + q];
+                        A[i * 4 + p] = cs * ap - sn * aq;
+                        A[i * 4 + q] = sn * ap + cs * aq;
+                        ap = V[i * 4 + p];
+                        aq = V[i * 4 + q];
+                        V[i * 4 + p] = cs * ap - sn * aq;
+                        V[i * 4 + q] = sn * ap + cs * aq;
+                    }
+                    rotated = 1;
+                }
+            }
+        if (!rotated) break;
+    }
+    {
+        double nrm[4];
+        for (p = 0; p < 4; p++) {
+            double s = 0;
+            for (i = 0; i < 4; i++) s += A[i * 4 + p] * A[i * 4 + p];
+            nrm[p] = s;
+        }
+        best = 0;
+        for (p = 1; p < 4; p++)
+            if (nrm[p] < nrm[best]) best = p;
+    }
+    for (i = 0; i < 4; i++) v[i] = V[i * 4 + best];
+}
+
+/* cv::triangulatePoints (OpenCV 2.4 cvTriangulatePoints) for one pair of
+   undistorted points, P1 = [I|0], P2 = first 3 rows of g12
+   (singlecameratriangulator.cpp:179-186). Returns homogeneous X (4). */
+ORC_API void orc_triangulate1(const double g12[16], const double u1[2], const double u2[2], double X[4])
+{
+    double A[16], P1[12], P2[12];
+    int j, k;
+    for (k = 0; k < 12; k++) P1[k] = (k == 0 || k == 5 || k == 10) ? 1. : 0.;
+    for (k = 0; k < 12; k++) P2[k] = g12[k];
+    for (j = 0; j < 2; j++) {
+        const double *P = j == 0 ? P1 : P2;
+        double x = j == 0 ? u1[0] : u2[0];
+        double y = j == 0 ? u1[1] : u2[1];
+        for (k = 0; k < 4; k++) {
+            A[(j * 2 + 0) * 4 + k] = x * P[8 + k] - P[0 + k];
+            A[(j * 2 + 1) * 4 + k] = y * P[8 + k] - P[4 + k];
+        }
+    }
+    orc_dlt_nullvec(A, X);
+}
+
+/* setKeypoints (:145-171) + triangulate (:173-230).
+   kp: float xy per keypoint (cv::KeyPoint::pt).  Outputs: inlier mask per
+   match, compacted points (in match order).  Returns number of inliers. */
+ORC_API int orc_triangulate(const orc_camera *c, const double g12[16], double zmin, double zmax,
+                            const float *kp1, const float *kp2, const int *query, const int *train, int K,
+                            uint8_t *mask, double *points)
+{
+    int i, n = 0;
+    for (i = 0; i < K; i++) {
+        double a1x = (double)kp1[2 * query[i]], a1y = (double)kp1[2 * query[i] + 1];
+        double a2x = (double)kp2[2 * train[i]], a2y = (double)kp2[2 * train[i] + 1];
+        double u1[2], u2[2], X[4];
+        orc_undistort1(c, a1x, a1y, &u1[0], &u1[1]);
+        orc_undistort1(c, a2x, a2y, &u2[0], &u2[1]);
+        orc_triangulate1(g12, u1, u2, X);
+        if (X[2] / X[3] < zmin || X[2] / X[3] >= zmax) {
+            mask[i] = 0;
+        } else {
+            mask[i] = 1;
+            points[3 * n + 0] = X[0] / X[3];
+            points[3 * n + 1] = X[1] / X[3];
+            points[3 * n + 2] = X[2] / X[3];
+            n++;
+        }
+    }
+    return n;
+}
+
+/* ------------------------------------------------------------------ */
+/* descriptor matching (a1)                                            */
+/* ------------------------------------------------------------------ */
+enum { ORC_F32 = 0, ORC_U8 = 1, ORC_BITS = 2 };
+
+/* FLANN L2<float>: groups of 4, result += d0*d0 + d1*d1 + d2*d2 + d3*d3, then tail */
+static float orc_l2_flann(const float *a, const float *b, int n)
+{
+    float result = 0.f;
+    int i = 0;
+    for (; i + 3 < n; i += 4) {
+        float d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1], d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+        result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    for (; i < n; i++) {
+        float d0 = a[i] - b[i];
+        result += d0 * d0;
+    }
+    return result;
+}
+
+/* k=2 brute force with (distance, trainIdx) lexicographic order.  key2 is the
+   ranking value: the squared L2 (float FLANN order or exact integer) or the
+   Hamming count.  dist is what cv::DMatch::distance holds
+   (FlannBasedMatcher::convertToDMatches: sqrt for L2, float(int) for Hamming). */
+ORC_API void orc_knn2(int type, const void *A, int nA, const void *B, int nB, int dim,
+                      int *idx /* nA*2, -1 if absent */, float *dist /* nA*2 */, int nthreads)
+{
+    int i;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+    for (i = 0; i < nA; i++) {
+        double k1 = INFINITY, k2 = INFINITY;
+        int i1 = -1, i2 = -1, j;
+        for (j = 0; j < nB; j++) {
+            double key;
+            if (type == ORC_F32) {
+                key = (double)orc_l2_flann((const float *)A + (size_t)i * dim, (const float *)B + (size_t)j * dim, dim);
+            } else if (type == ORC_U8) {
+                const uint8_t *a = (const uint8_t *)A + (size_t)i * dim, *b = (const uint8_t *)B + (size_t)j * dim;
+                int64_t s = 0;
+                int d;
+                for (d = 0; d < dim; d++) { int df = (int)a[d] - (int)b[d]; s += df * df; }
+                key = (double)s;
+            } else {
+                const uint8_t *a = (const uint8_t *)A + (size_t)i * dim, *b = (const uint8_t *)B + (size_t)j * dim;
+                int s = 0, d;
+                for (d = 0; d < dim; d++) s += __builtin_popcount((unsigned)(a[d] ^ b[d]));
+                key = (double)s;
+            }
+            /* candidates arrive in increasing j: strict < keeps the lowest index on ties */
+            if (key < k1) { k2 = k1; i2 = i1; k1 = key; i1 = j; }
+            else if (key < k2) { k2 = key; i2 = j; }
+        }
+        idx[2 * i] = i1;
+        idx[2 * i + 1] = i2;
+        if (type == ORC_BITS) {
+            dist[2 * i] = (float)k1;
+            dist[2 * i + 1] = (float)k2;
+        } else {
+            dist[2 * i] = sqrtf((float)k1);
+            dist[2 * i + 1] = sqrtf((float)k2);
+        }
+    }
+}
+
+/* compareWithNNDR (descriptorsmatcher.cpp:117-129): keep m[0] iff the query has
+   2 neighbours and m[0].distance <= epsilon * m[1].distance (double compare).
+   Output in query order: (queryIdx, trainIdx, distance). Returns count. */
+ORC_API int orc_nndr(const int *idx, const float *dist, int nA, double eps, int *q_out, int *t_out, float *d_out)
+{
+    int i, n = 0;
+    for (i = 0; i < nA; i++) {
+        if (idx[2 * i] < 0 || idx[2 * i + 1] < 0) continue;
+        if ((double)dist[2 * i] <= eps * (double)dist[2 * i + 1]) {
+            q_out[n] = i;
+            t_out[n] = idx[2 * i];
+            d_out[n] = dist[2 * i];
+            n++;
+        }
+    }
+    return n;
+}
+
+/* ------------------------------------------------------------------ */
+/* images                                                              */
+/* ------------------------------------------------------------------ */
+static int orc_reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) {
+        if (p < 0) p = -p;
+        else p = 2 * len - p - 2;
+    }
+    return p;
+}
+
+/* cv::pyrDown 8U (normaloptimizer.cpp:216-217): 5x5 [1 4 6 4 1]^2 / 256 with
+   BORDER_REFLECT_101, (sum + 128) >> 8, dst size ((w+1)/2, (h+1)/2). */
+ORC_API void orc_pyrdown(const uint8_t *src, int w, int h, uint8_t *dst)
+{
+    static const int wt[5] = {1, 4, 6, 4, 1};
+    int dw = (w + 1) / 2, dh = (h + 1) / 2, x, y, i, j;
+    for (y = 0; y < dh; y++)
+        for (x = 0; x < dw; x++) {
+            int s = 0;
+            for (i = 0; i < 5; i++) {
+                int sy = orc_reflect101(2 * y + i - 2, h);
+                int rs = 0;
+                for (j = 0; j < 5; j++) {
+                    int sx = orc_reflect101(2 * x + j - 2, w);
+                    rs += wt[j] * src[sy * w + sx];
+                }
+                s += wt[i] * rs;
+            }
+            dst[y * dw + x] = (uint8_t)((s + 128) >> 8);
+        }
+}
+
+/* getBilinearInterpPix32f (tools.cpp:129-142).  The reference reads
+   (y0,x0),(y1,x0),(y0,x1),(y1,x1) with no bounds check; isPixelGood admits
+   x == cols and y == rows, so the reference reads one element past a row (which
+   lands in the next row of a continuous cv::Mat) or past the image.  We emulate
+   a continuous buffer followed by zero bytes. */
+static float orc_pix(const uint8_t *img, int w, int h, int y, int x)
+{
+    long idx = (long)y * w + x;
+    if (idx < 0 || idx >= (long)w * h) return 0.f;
+    return (float)img[idx];
+}
+
+static float orc_bilinear(const uint8_t *img, int w, int h, float x, float y)
+{
+    int x0 = (int)floor((double)x), y0 = (int)floor((double)y);
+    int x1 = x0 + 1, y1 = y0 + 1;
+    float b00 = orc_pix(img, w, h, y0, x0), b10 = orc_pix(img, w, h, y1, x0);
+    float b01 = orc_pix(img, w, h, y0, x1), b11 = orc_pix(img, w, h, y1, x1);
+    float xm0 = 1.0f - (x - (float)x0), xm1 = (x - (float)x0);
+    float ym0 = 1.0f - (y - (float)y0), ym1 = (y - (float)y0);
+    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
+}
+
+ORC_API float orc_bilinear_sample(const uint8_t *img, int w, int h, float x, float y)
+{
+    return orc_bilinear(img, w, h, x, y);
+}
+
+/* ------------------------------------------------------------------ */
+/* neighbourhood (a8)                                                  */
+/* ------------------------------------------------------------------ */
+/* extractPixelsContour(Vec3d) (:376-397) -> (Vec2d) (:341-374).  Writes the
+   kept pixel coordinates (double xy) and returns m_dat. */
+ORC_API int orc_neighborhood(const orc_camera *c, const double X[3], int ray, int boundW, int boundH,
+                             double *out_xy, int cap)
+{
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    static const double Z[3] = {0, 0, 0};
+    double cx, cy;
+    int i, j, n = 0;
+    orc_project1(c, I, Z, X[0], X[1], X[2], &cx, &cy);
+    for (i = -ray; i <= ray; i++)
+        for (j = -ray; j <= ray; j++) {
+            if (i * i + j * j <= ray * ray) {
+                double px = cx + i, py = cy + j;
+                if (px < 0 || py < 0 || px >= boundW || py >= boundH) continue;
+                if (n < cap) { out_xy[2 * n] = px; out_xy[2 * n + 1] = py; }
+                n++;
+            }
+        }
+    return n;
+}
+
+/* ------------------------------------------------------------------ */
+/* LM normal optimisation (a7, a9-a15)                                 */
+/* ------------------------------------------------------------------ */
+enum {
+    ORC_ST_OK = 0,
+    ORC_ST_NO_PIXELS = 1,   /* normaloptimizer.cpp:364-369 */
+    ORC_ST_ABORT_BBOX = 2,  /* isInBoundingBox failed (:557-560) */
+    ORC_ST_ABORT_PIX1 = 3,  /* updateImage1PixelsIntensity (:580-584) */
+    ORC_ST_ABORT_PIX2 = 4,  /* projectPointsToImage2 (:623-626) */
+    ORC_ST_NAN_PLANE = 5,   /* projectPointToPlane exit(-6) (:465-469) */
+    ORC_ST_NAN_NORMAL = 6,  /* evaluateNormal NaN normal (:81-85) */
+    ORC_ST_TOO_MANY_PIXELS = 7
+};
+/* mode bits: ORC_LM_GRAM = Gram-sum QR + blocked reductions, ORC_LM_DETMATH =
+   fm3d_detmath transcendentals.  STRICT = 0, CANONICAL = both. */
+enum { ORC_LM_STRICT = 0, ORC_LM_GRAM = 1, ORC_LM_DETMATH = 2, ORC_LM_CANONICAL = 3 };
+
+typedef struct {
+    const uint8_t *img[2][8]; /* pyramid levels of image 1 and 2 */
+    int w[8], h[8];
+} orc_pyramid;
+
+typedef struct {
+    const orc_camera *cam;
+    const double *R2, *t2;
+    const orc_pyramid *pyr;
+    int level;
+    double scale;
+    double X[3];
+    int cmax;           /* int cMax = 2*zThresholdMax (truncating), :648 */
+    int m;
+    const double *ray;  /* m * 2 undistorted (x,y); z = 1 */
+    const double *pix;  /* m * 2 image-1 pixel coordinates */
+    float *I1;          /* m intensities of image 1 at the current level */
+    int I1_ok;
+    int mode;
+    int nthreads;       /* canonical mode: lanes of the GPU workgroup */
+    long nfev;          /* evaluations in the current lmdif call */
+} orc_lmdata;
+
+/* isPixelGood (:657-665); NaN coordinates count as bad (the reference then
+   has undefined behaviour inside getBilinearInterpPix32f). */
+static int orc_pixel_good(double x, double y, double scale, int cols, int rows)
+{
+    if (x != x || y != y) return 0;
+    if ((x < 0) || (x > ((1 / scale) * cols)) || (y < 0) || (y > ((1 / scale) * rows))) return 0;
+    return 1;
+}
+
+/* updateImage1PixelsIntensity (:576-589).  Its inputs do not change inside a
+   pyramid level, so the values (and the abort) are computed once per level. */
+static void orc_update_I1(orc_lmdata *D)
+{
+    int i, L = D->level;
+    D->I1_ok = 1;
+    for (i = 0; i < D->m; i++) {
+        double x = D->pix[2 * i], y = D->pix[2 * i + 1];
+        if (!orc_pixel_good(x, y, D->scale, D->pyr->w[L], D->pyr->h[L])) { D->I1_ok = 0; return; }
+        D->I1[i] = orc_bilinear(D->pyr->img[0][L], D->pyr->w[L], D->pyr->h[L],
+                                (float)(D->scale * x), (float)(D->scale * y));
+    }
+}
+
+static void orc_sph2car(int mode, double phi, double theta, double n[3])
+{   /* tools.cpp:772-777 */
+    if (!(mode & ORC_LM_DETMATH)) {
+        n[0] = cos(theta) * cos(phi);
+        n[1] = cos(theta) * sin(phi);
+        n[2] = sin(theta);
+    } else {
+        n[0] = fm3d_cos(theta) * fm3d_cos(phi);
+        n[1] = fm3d_cos(theta) * fm3d_sin(phi);
+        n[2] = fm3d_sin(theta);
+    }
+}
+
+static void orc_car2sph(int mode, const double v[3], double *phi, double *theta)
+{   /* tools.cpp:767-771 */
+    if (!(mode & ORC_LM_DETMATH)) {
+        *theta = atan2(v[2], sqrt(v[0] * v[0] + v[1] * v[1]));
+        *phi = atan2(v[1], v[0]);
+    } else {
+        *theta = fm3d_atan2(v[2], sqrt(v[0] * v[0] + v[1] * v[1]));
+        *phi = fm3d_atan2(v[1], v[0]);
+    }
+}
+
+/* evaluateNormal (normaloptimizer.cpp:65-149).  Returns 0 or a status code. */
+static int orc_eval(orc_lmdata *D, const double *par, double *fvec)
+{
+    double phi = par[0], theta = par[1];
+    double n[3], mm, w_theta = 1.0, w_phi = 1.0, w;
+    int i, L = D->level;
+    const double cm = (double)D->cmax;
+    D->nfev++;
+    orc_sph2car(D->mode, phi, theta, n);
+    if (n[2] != n[2] || n[1] != n[1] || n[0] != n[0]) return ORC_ST_NAN_NORMAL;
+    /* get3dPointsFromImage1Pixels (:530-574): plane point per pixel, NaN ->
+       exit(-6) (:465-469), outside isInBoundingBox (:646-655) -> abort */
+    mm = n[0] * D->X[0] + n[1] * D->X[1] + n[2] * D->X[2];
+    for (i = 0; i < D->m; i++) {
+        double ux = D->ray[2 * i], uy = D->ray[2 * i + 1];
+        double nn = n[0] * ux + n[1] * uy + n[2] * 1.;
+        double k = mm / nn;
+        double P0 = k * ux, P1 = k * uy, P2 = k * 1.;
+        if (P0 != P0 || P1 != P1 || P2 != P2) return ORC_ST_NAN_PLANE;
+        if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm))) return ORC_ST_ABORT_BBOX;
+    }
+    if (!D->I1_ok) return ORC_ST_ABORT_PIX1;
+    /* weight (:125-142); abs() is std::abs(double) under the reference's <cmath> */
+    if (fabs(theta) - M_PI / 2 > 0 || fabs(phi) - M_PI > 0) {
+        if (!(D->mode & ORC_LM_DETMATH)) {
+            w_theta = exp(fabs(theta) - M_PI / 2) + 1;
+            w_phi = exp(fabs(phi) - M_PI + 1) + 1;
+        } else {
+            w_theta = fm3d_exp(fabs(theta) - M_PI / 2) + 1;
+            w_phi = fm3d_exp(fabs(phi) - M_PI + 1) + 1;
+        }
+    }
+    w = w_phi * w_theta;
+    /* projectPointsToImage2 (:591-644) and the residual (:145-148) */
+    for (i = 0; i < D->m; i++) {
+        double ux = D->ray[2 * i], uy = D->ray[2 * i + 1];
+        double nn = n[0] * ux + n[1] * uy + n[2] * 1.;
+        double k = mm / nn;
+        double u, v;
+        float I2;
+        orc_project1(D->cam, D->R2, D->t2, k * ux, k * uy, k * 1., &u, &v);
+        if (!orc_pixel_good(u, v, D->scale, D->pyr->w[L], D->pyr->h[L])) return ORC_ST_ABORT_PIX2;
+        I2 = orc_bilinear(D->pyr->img[1][L], D->pyr->w[L], D->pyr->h[L], (float)(D->scale * u), (float)(D->scale * v));
+        fvec[i] = w * (D->I1[i] - I2);
+    }
+    return 0;
+}
+
+/* ---- MINPACK building blocks (lmfit's lm_enorm/lm_qrfac/lm_lmpar/lm_qrsolv) ---- */
+#define LM_EPSMCH DBL_EPSILON
+#define LM_DWARF DBL_MIN
+
+/* enorm: scaled Euclidean norm (MINPACK) */
+static double orc_enorm(int n, const double *x)
+{
+    const double rdwarf = 3.834e-20, rgiant = 1.304e19;
+    double s1 = 0, s2 = 0, s3 = 0, x1max = 0, x3max = 0, agiant = rgiant / (double)n, xabs, temp;
+    int i;
+    for (i = 0; i < n; i++) {
+        xabs = fabs(x[i]);
+        if (xabs > rdwarf && xabs < agiant) {
+            s2 += xabs * xabs;
+        } else if (xabs > rdwarf) {
+            if (xabs > x1max) { temp = x1max / xabs; s1 = 1 + s1 * temp * temp; x1max = xabs; }
+            else { temp = xabs / x1max; s1 += temp * temp; }
+        } else {
+            if (xabs > x3max) { temp = x3max / xabs; s3 = 1 + s3 * temp * temp; x3max = xabs; }
+            else if (xabs != 0.) { temp = xabs / x3max; s3 += temp * temp; }
+        }
+    }
+    if (s1 != 0) return x1max * sqrt(s1 + (s2 / x1max) / x1max);
+    if (s2 != 0) {
+        if (s2 >= x3max) return sqrt(s2 * (1 + (x3max / s2) * (x3max * s3)));
+        return sqrt(x3max * ((s2 / x3max) + (x3max * s3)));
+    }
+    return x3max * sqrt(s3);
+}
+
+/* canonical reduction order of the GPU kernel: lane t sums elements
+   t, t+NT, t+2NT, ... in order; 64-lane waves reduce by halving trees
+   (lane l += lane l+s, s = 32..1); wave sums reduce by halving trees. */
+static double orc_blocked_sum(const double *v, int m, int NT)
+{
+    double lane[64], wsum[64];
+    int nw = NT / 64, w, l, s, k;
+    if (NT <= 0) { /* plain index order (diagnostics) */
+        double acc = 0.0;
+        for (k = 0; k < m; k++) acc = acc + v[k];
+        return acc;
+    }
+    for (w = 0; w < nw; w++) {
+        for (l = 0; l < 64; l++) {
+            double acc = 0.0;
+            for (k = w * 64 + l; k < m; k += NT) acc = acc + v[k];
+            lane[l] = acc;
+        }
+        for (s = 32; s >= 1; s >>= 1)
+            for (l = 0; l < s; l++) lane[l] = lane[l] + lane[l + s];
+        wsum[w] = lane[0];
+    }
+    for (s = nw / 2; s >= 1; s >>= 1)
+        for (l = 0; l < s; l++) wsum[l] = wsum[l] + wsum[l + s];
+    return wsum[0];
+}
+
+/* Euclidean norm of an m-vector: MINPACK enorm (strict) or sqrt of the
+   canonical blocked sum of squares (canonical; identical to enorm whenever all
+   |x| lie in (3.8e-20, 1.3e19/m) or are zero, which covers residuals built from
+   8-bit intensities unless the LM weight explodes). */
+static double orc_enorm_m(const orc_lmdata *D, const double *x, double *tmp)
+{
+    int i;
+    if (!(D->mode & ORC_LM_GRAM)) return orc_enorm(D->m, x);
+    for (i = 0; i < D->m; i++) tmp[i] = x[i] * x[i];
+    return sqrt(orc_blocked_sum(tmp, D->m, D->nthreads));
+}
+
+/* qrsolv (MINPACK), r column-major with leading dimension ldr */
+static void orc_qrsolv(int n, double *r, int ldr, const int *ipvt, const double *diag, const double *qtb,
+                       double *x, double *sdiag, double *wa)
+{
+    int i, j, k, l, nsing;
+    double qtbpj, sum, temp, sn, cs, tn, ct;
+#define R_(i, j) r[(j) * ldr + (i)]
+    for (j = 0; j < n; j++) {
+        for (i = j; i < n; i++) R_(i, j) = R_(j, i);
+        x[j] = R_(j, j);
+        wa[j] = qtb[j];
+    }
+    for (j = 0; j < n; j++) {
+        l = ipvt[j];
+        if (diag[l] != 0.) {
+            for (k = j; k < n; k++) sdiag[k] = 0.;
+            sdiag[j] = diag[l];
+            qtbpj = 0.;
+            for (k = j; k < n; k++) {
+                if (sdiag[k] == 0.) continue;
+                if (fabs(R_(k, k)) < fabs(sdiag[k])) {
+                    ct = R_(k, k) / sdiag[k];
+                    sn = 0.5 / sqrt(0.25 + 0.25 * ct * ct);
+                    cs = sn * ct;
+                } else {
+                    tn = sdiag[k] / R_(k, k);
+                    cs = 0.5 / sqrt(0.25 + 0.25 * tn * tn);
+                    sn = cs * tn;
+                }
+                R_(k, k) = cs * R_(k, k) + sn * sdiag[k];
+                temp = cs * wa[k] + sn * qtbpj;
+                qtbpj = -sn * wa[k] + cs * qtbpj;
+                wa[k] = temp;
+                for (i = k + 1; i < n; i++) {
+                    temp = cs * R_(i, k) + sn * sdiag[i];
+                    sdiag[i] = -sn * R_(i, k) + cs * sdiag[i];
+                    R_(i, k) = temp;
+                }
+            }
+        }
+        sdiag[j] = R_(j, j);
+        R_(j, j) = x[j];
+    }
+    nsing = n;
+    for (j = 0; j < n; j++) {
+        if (sdiag[j] == 0. && nsing == n) nsing = j;
+        if (nsing < n) wa[j] = 0.;
+    }
+    for (k = 0; k < nsing; k++) {
+        j = nsing - k - 1;
+        sum = 0.;
+        for (i = j + 1; i < nsing; i++) sum += R_(i, j) * wa[i];
+        wa[j] = (wa[j] - sum) / sdiag[j];
+    }
+    for (j = 0; j < n; j++) x[ipvt[j]] = wa[j];
+#undef R_
+}
+
+/* lmpar (MINPACK) */
+static void orc_lmpar(int n, double *r, int ldr, const int *ipvt, const double *diag, const double *qtb,
+                      double delta, double *par, double *x, double *sdiag, double *wa1, double *wa2)
+{
+    const double p1 = 0.1, p001 = 0.001;
+    int i, iter, j, l, nsing;
+    double dxnorm, fp, gnorm, parc, parl, paru, sum, temp;
+#define R_(i, j) r[(j) * ldr + (i)]
+    nsing = n;
+    for (j = 0; j < n; j++) {
+        wa1[j] = qtb[j];
+        if (R_(j, j) == 0. && nsing == n) nsing = j;
+        if (nsing < n) wa1[j] = 0.;
+    }
+    for (i = 0; i < nsing; i++) {
+        j = nsing - i - 1;
+        wa1[j] = wa1[j] / R_(j, j);
+        temp = wa1[j];
+        for (l = 0; l < j; l++) wa1[l] -= R_(l, j) * temp;
+    }
+    for (j = 0; j < n; j++) x[ipvt[j]] = wa1[j];
+    iter = 0;
+    for (j = 0; j < n; j++) wa2[j] = diag[j] * x[j];
+    dxnorm = orc_enorm(n, wa2);
+    fp = dxnorm - delta;
+    if (fp <= p1 * delta) goto done;
+    parl = 0.;
+    if (nsing >= n) {
+        for (j = 0; j < n; j++) { l = ipvt[j]; wa1[j] = diag[l] * (wa2[l] / dxnorm); }
+        for (j = 0; j < n; j++) {
+            sum = 0.;
+            for (i = 0; i < j; i++) sum += R_(i, j) * wa1[i];
+            wa1[j] = (wa1[j] - sum) / R_(j, j);
+        }
+        temp = orc_enorm(n, wa1);
+        parl = ((fp / delta) / temp) / temp;
+    }
+    for (j = 0; j < n; j++) {
+        sum = 0.;
+        for (i = 0; i <= j; i++) sum += R_(i, j) * qtb[i];
+        l = ipvt[j];
+        wa1[j] = sum / diag[l];
+    }
+    gnorm = orc_enorm(n, wa1);
+    paru = gnorm / delta;
+    if (paru == 0.) paru = LM_DWARF / (delta < p1 ? delta : p1);
+    *par = *par > parl ? *par : parl;
+    *par = *par < paru ? *par : paru;
+    if (*par == 0.) *par = gnorm / dxnorm;
+    for (;;) {
+        iter++;
+        if (*par == 0.) *par = (LM_DWARF > p001 * paru) ? LM_DWARF : p001 * paru;
+        temp = sqrt(*par);
+        for (j = 0; j < n; j++) wa1[j] = temp * diag[j];
+        orc_qrsolv(n, r, ldr, ipvt, wa1, qtb, x, sdiag, wa2);
+        for (j = 0; j < n; j++) wa2[j] = diag[j] * x[j];
+        dxnorm = orc_enorm(n, wa2);
+        temp = fp;
+        fp = dxnorm - delta;
+        if (fabs(fp) <= p1 * delta || (parl == 0. && fp <= temp && temp < 0.) || iter == 10) break;
+        for (j = 0; j < n; j++) { l = ipvt[j]; wa1[j] = diag[l] * (wa2[l] / dxnorm); }
+        for (j = 0; j < n; j++) {
+            wa1[j] = wa1[j] / sdiag[j];
+            temp = wa1[j];
+            for (i = j + 1; i < n; i++) wa1[i] -= R_(i, j) * temp;
+        }
+        temp = orc_enorm(n, wa1);
+        parc = ((fp / delta) / temp) / temp;
+        if (fp > 0.) parl = parl > *par ? parl : *par;
+        if (fp < 0.) paru = paru < *par ? paru : *par;
+        *par = parl > *par + parc ? parl : *par + parc;
+    }
+done:
+    if (iter == 0) *par = 0.;
+#undef R_
+}
+
+/* Jacobian + QR.  Output: r (2x2 column-major upper triangle), qtf, acnorm,
+   ipvt.  Returns 0 or a failure status of one of the two evaluations. */
+static int orc_jac_qr(orc_lmdata *D, double *x, const double *fvec, double eps,
+                      double *fjac, double *wa4, double *tmp, double r[4], double qtf[2],
+                      double acnorm[2], int ipvt[2])
+{
+    int m = D->m, i, j, st;
+    double h[2];
+    /* fdjac2 (MINPACK): forward differences, h = eps*|x_j| (eps if 0) */
+    for (j = 0; j < 2; j++) {
+        double temp = x[j];
+        h[j] = eps * fabs(temp);
+        if (h[j] == 0.) h[j] = eps;
+        x[j] = temp + h[j];
+        st = orc_eval(D, x, wa4);
+        x[j] = temp;
+        if (st) return st;
+        for (i = 0; i < m; i++) fjac[j * m + i] = (wa4[i] - fvec[i]) / h[j];
+    }
+    if (!(D->mode & ORC_LM_GRAM)) {
+        /* qrfac with column pivoting (MINPACK), n = 2 */
+        double rdiag[2], wa[2], ajnorm, sum, temp;
+        int k, kmax;
+        for (j = 0; j < 2; j++) {
+            acnorm[j] = orc_enorm(m, &fjac[j * m]);
+            rdiag[j] = acnorm[j];
+            wa[j] = rdiag[j];
+            ipvt[j] = j;
+        }
+        for (j = 0; j < 2; j++) {
+            kmax = j;
+            for (k = j + 1; k < 2; k++)
+                if (rdiag[k] > rdiag[kmax]) kmax = k;
+            if (kmax != j) {
+                for (i = 0; i < m; i++) { temp = fjac[j * m + i]; fjac[j * m + i] = fjac[kmax * m + i]; fjac[kmax * m + i] = temp; }
+                rdiag[kmax] = rdiag[j];
+                wa[kmax] = wa[j];
+                k = ipvt[j]; ipvt[j] = ipvt[kmax]; ipvt[kmax] = k;
+            }
+            ajnorm = orc_enorm(m - j, &fjac[j * m + j]);
+            if (ajnorm == 0.) { rdiag[j] = 0.; continue; }
+            if (fjac[j * m + j] < 0.) ajnorm = -ajnorm;
+            for (i = j; i < m; i++) fjac[j * m + i] /= ajnorm;
+            fjac[j * m + j] += 1.;
+            for (k = j + 1; k < 2; k++) {
+                sum = 0.;
+                for (i = j; i < m; i++) sum += fjac[j * m + i] * fjac[k * m + i];
+                temp = sum / fjac[j * m + j];
+                for (i = j; i < m; i++) fjac[k * m + i] -= temp * fjac[j * m + i];
+                if (rdiag[k] != 0.) {
+                    temp = fjac[k * m + j] / rdiag[k];
+                    temp = 1. - temp * temp;
+                    rdiag[k] *= sqrt(temp > 0. ? temp : 0.);
+                    temp = rdiag[k] / wa[k];
+                    if (0.05 * temp * temp <= LM_EPSMCH) {
+                        rdiag[k] = orc_enorm(m - j - 1, &fjac[k * m + j + 1]);
+                        wa[k] = rdiag[k];
+                    }
+                }
+            }
+            rdiag[j] = -ajnorm;
+        }
+        /* lmdif: form (q transpose)*fvec, keep the first n components */
+        for (i = 0; i < m; i++) wa4[i] = fvec[i];
+        for (j = 0; j < 2; j++) {
+            if (fjac[j * m + j] != 0.) {
+                sum = 0.;
+                for (i = j; i < m; i++) sum += fjac[j * m + i] * wa4[i];
+                temp = -sum / fjac[j * m + j];
+                for (i = j; i < m; i++) wa4[i] += fjac[j * m + i] * temp;
+            }
+            fjac[j * m + j] = rdiag[j];
+            qtf[j] = wa4[j];
+        }
+        r[0] = fjac[0]; r[1] = 0.; r[2] = fjac[m + 0]; r[3] = fjac[m + 1];
+    } else {
+        /* Gram-sum QR in the kernel's canonical reduction order */
+        double S00, S11, S01, S0f, S1f, Spp, Sqq, Spq, Spf, Sqf, r00, r01, r11, q0, q1, t;
+        int p, q;
+        for (i = 0; i < m; i++) tmp[i] = fjac[i] * fjac[i];
+        S00 = orc_blocked_sum(tmp, m, D->nthreads);
+        for (i = 0; i < m; i++) tmp[i] = fjac[m + i] * fjac[m + i];
+        S11 = orc_blocked_sum(tmp, m, D->nthreads);
+        for (i = 0; i < m; i++) tmp[i] = fjac[i] * fjac[m + i];
+        S01 = orc_blocked_sum(tmp, m, D->nthreads);
+        for (i = 0; i < m; i++) tmp[i] = fjac[i] * fvec[i];
+        S0f = orc_blocked_sum(tmp, m, D->nthreads);
+        for (i = 0; i < m; i++) tmp[i] = fjac[m + i] * fvec[i];
+        S1f = orc_blocked_sum(tmp, m, D->nthreads);
+        acnorm[0] = sqrt(S00);
+        acnorm[1] = sqrt(S11);
+        if (acnorm[1] > acnorm[0]) { p = 1; q = 0; } else { p = 0; q = 1; }
+        ipvt[0] = p; ipvt[1] = q;
+        Spp = p == 0 ? S00 : S11;
+        Sqq = p == 0 ? S11 : S00;
+        Spf = p == 0 ? S0f : S1f;
+        Sqf = p == 0 ? S1f : S0f;
+        Spq = S01;
+        (void)Spp;
+        r00 = acnorm[p];
+        if (r00 == 0.) {
+            r01 = 0.; r11 = 0.; q0 = 0.; q1 = 0.;
+        } else {
+            r01 = Spq / r00;
+            q0 = Spf / r00;
+            t = Sqq - r01 * r01;
+            r11 = t > 0. ? sqrt(t) : 0.;
+            q1 = r11 > 0. ? (Sqf - r01 * q0) / r11 : 0.;
+        }
+        r[0] = r00; r[1] = 0.; r[2] = r01; r[3] = r11;
+        qtf[0] = q0; qtf[1] = q1;
+    }
+    return 0;
+}
+
+/* lmdif (MINPACK) with lmfit's lmmin control (lm_control_double:
+   ftol=xtol=gtol=30*DBL_EPSILON, stepbound(factor)=100, patience=100 ->
+   maxfev = 300, scale_diag = 1 -> mode 1).  Returns the lmdif info (1..8) or,
+   for a user break (evaluateNormal *info = -1, lmmin status.info = 11), the
+   negated failure status. */
+static int orc_lmdif(orc_lmdata *D, double *x, double epsfcn, double *fvec, double *fjac, double *wa4,
+                     double *tmp, int *nfev_out)
+{
+    const int n = 2, maxfev = 100 * (2 + 1);
+    const double ftol = 30 * LM_EPSMCH, xtol = 30 * LM_EPSMCH, gtol = 30 * LM_EPSMCH, factor = 100.;
+    const double p1 = 0.1, p5 = 0.5, p25 = 0.25, p75 = 0.75, p0001 = 1.0e-4;
+    double eps = sqrt(epsfcn > LM_EPSMCH ? epsfcn : LM_EPSMCH);
+    double diag[2], r[4], qtf[2], acnorm[2], wa1[2], wa2[2], wa3[2], sdiag[2], lw[2];
+    double par = 0., delta = 0., xnorm = 0., fnorm, fnorm1, gnorm, pnorm, actred, prered, dirder, ratio, temp, temp1, temp2, sum;
+    int ipvt[2], iter = 1, info = 0, st, i, j, l;
+    D->nfev = 0;
+    /* lmdif input check: m < n is "improper input parameters" (info 0), no evaluation */
+    if (D->m < n) { *nfev_out = 0; return 0; }
+    st = orc_eval(D, x, fvec);
+    if (st) { *nfev_out = (int)D->nfev; return -st; }
+    fnorm = orc_enorm_m(D, fvec, tmp);
+    for (;;) {
+        st = orc_jac_qr(D, x, fvec, eps, fjac, wa4, tmp, r, qtf, acnorm, ipvt);
+        if (st) { *nfev_out = (int)D->nfev; return -st; }
+        if (iter == 1) {
+            for (j = 0; j < n; j++) {
+                diag[j] = acnorm[j];
+                if (acnorm[j] == 0.) diag[j] = 1.;
+            }
+            for (j = 0; j < n; j++) wa3[j] = diag[j] * x[j];
+            xnorm = orc_enorm(n, wa3);
+            delta = factor * xnorm;
+            if (delta == 0.) delta = factor;
+        }
+        gnorm = 0.;
+        if (fnorm != 0.) {
+            for (j = 0; j < n; j++) {
+                l = ipvt[j];
+                if (acnorm[l] == 0.) continue;
+                sum = 0.;
+                for (i = 0; i <= j; i++) sum += r[j * 2 + i] * (qtf[i] / fnorm);
+                temp = fabs(sum / acnorm[l]);
+                gnorm = gnorm > temp ? gnorm : temp;
+            }
+        }
+        if (gnorm <= gtol) info = 4;
+        if (info != 0) break;
+        for (j = 0; j < n; j++) diag[j] = diag[j] > acnorm[j] ? diag[j] : acnorm[j];
+        do {
+            double rr[4];
+            for (j = 0; j < 4; j++) rr[j] = r[j];
+            orc_lmpar(n, rr, 2, ipvt, diag, qtf, delta, &par, wa1, sdiag, lw, wa3);
+            /* the R upper triangle is restored by qrsolv; keep the original */
+            for (j = 0; j < n; j++) {
+                wa1[j] = -wa1[j];
+                wa2[j] = x[j] + wa1[j];
+                wa3[j] = diag[j] * wa1[j];
+            }
+            pnorm = orc_enorm(n, wa3);
+            if (iter == 1) delta = delta < pnorm ? delta : pnorm;
+            st = orc_eval(D, wa2, wa4);
+            if (st) { *nfev_out = (int)D->nfev; return -st; }
+            fnorm1 = orc_enorm_m(D, wa4, tmp);
+            actred = -1.;
+            if (p1 * fnorm1 < fnorm) actred = 1. - (fnorm1 / fnorm) * (fnorm1 / fnorm);
+            for (j = 0; j < n; j++) {
+                wa3[j] = 0.;
+                l = ipvt[j];
+                temp = wa1[l];
+                for (i = 0; i <= j; i++) wa3[i] += r[j * 2 + i] * temp;
+            }
+            temp1 = orc_enorm(n, wa3) / fnorm;
+            temp2 = (sqrt(par) * pnorm) / fnorm;
+            prered = temp1 * temp1 + temp2 * temp2 / p5;
+            dirder = -(temp1 * temp1 + temp2 * temp2);
+            ratio = 0.;
+            if (prered != 0.) ratio = actred / prered;
+            if (ratio <= p25) {
+                if (actred >= 0.) temp = p5;
+                else temp = p5 * dirder / (dirder + p5 * actred);
+                if (p1 * fnorm1 >= fnorm || temp < p1) temp = p1;
+                delta = temp * (delta < pnorm / p1 ? delta : pnorm / p1);
+                par = par / temp;
+            } else if (par == 0. || ratio >= p75) {
+                delta = pnorm / p5;
+                par = p5 * par;
+            }
+            if (ratio >= p0001) {
+                for (j = 0; j < n; j++) {
+                    x[j] = wa2[j];
+                    wa2[j] = diag[j] * x[j];
+                }
+                for (i = 0; i < D->m; i++) fvec[i] = wa4[i];
+                xnorm = orc_enorm(n, wa2);
+                fnorm = fnorm1;
+                iter++;
+            }
+            if (fabs(actred) <= ftol && prered <= ftol && p5 * ratio <= 1.) info = 1;
+            if (delta <= xtol * xnorm) info = 2;
+            if (fabs(actred) <= ftol && prered <= ftol && p5 * ratio <= 1. && info == 2) info = 3;
+            if (info != 0) goto out;
+            if (D->nfev >= maxfev) info = 5;
+            if (fabs(actred) <= LM_EPSMCH && prered <= LM_EPSMCH && p5 * ratio <= 1.) info = 6;
+            if (delta <= LM_EPSMCH * xnorm) info = 7;
+            if (gnorm <= LM_EPSMCH) info = 8;
+            if (info != 0) goto out;
+        } while (ratio < p0001);
+    }
+out:
+    *nfev_out = (int)D->nfev;
+    return info;
+}
+
+/* Standalone LM driver for tests: minimises the evaluateNormal residual of one
+   point at one pyramid level starting from par.  Returns info. */
+
+/* One point: computeOptimizedNormals body (:335-449) with optimize_pyramid
+   (:223-245) and optimize (:247-292).  Returns the status; normal in n_out;
+   per-level lmdif info and evaluation counts (index = level). */
+static int orc_point(const orc_camera *cam, const double R2[9], const double t2[3], const orc_pyramid *pyr,
+                     int levels, const double X[3], int ray, int boundW, int boundH, double epsfcn, int cmax,
+                     int mode, int NT, double n_out[3], int *info_out, int *nfev_out, int *mdat_out)
+{
+    int side = 2 * ray + 1, cap = side * side, m, L, i, status = ORC_ST_OK;
+    double *pix, *rays, *fvec, *fjac, *wa4, *tmp, nrm, norm[3], inv;
+    float *I1;
+    float img_scale;
+    orc_lmdata D;
+    for (L = 0; L <= levels; L++) { info_out[L] = 0; nfev_out[L] = 0; }
+    pix = (double *)malloc(sizeof(double) * 2 * cap);
+    m = orc_neighborhood(cam, X, ray, boundW, boundH, pix, cap);
+    *mdat_out = m;
+    if (m <= 0) { free(pix); return ORC_ST_NO_PIXELS; }
+    if ((mode & ORC_LM_GRAM) && NT > 0 && m > NT * 16) { free(pix); return ORC_ST_TOO_MANY_PIXELS; }
+    rays = (double *)malloc(sizeof(double) * 2 * m);
+    fvec = (double *)malloc(sizeof(double) * m);
+    fjac = (double *)malloc(sizeof(double) * 2 * m);
+    wa4 = (double *)malloc(sizeof(double) * m);
+    tmp = (double *)malloc(sizeof(double) * m);
+    I1 = (float *)malloc(sizeof(float) * m);
+    for (i = 0; i < m; i++) orc_undistort1(cam, pix[2 * i], pix[2 * i + 1], &rays[2 * i], &rays[2 * i + 1]);
+    /* initial guess: viewing ray, Vec3d / norm == multiply by 1/norm (:342-343) */
+    nrm = sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+    inv = 1. / nrm;
+    norm[0] = X[0] * inv; norm[1] = X[1] * inv; norm[2] = X[2] * inv;
+    memset(&D, 0, sizeof(D));
+    D.cam = cam; D.R2 = R2; D.t2 = t2; D.pyr = pyr;
+    D.X[0] = X[0]; D.X[1] = X[1]; D.X[2] = X[2];
+    D.cmax = cmax; D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode; D.nthreads = NT;
+    img_scale = (float)pow(2.0, (double)levels);
+    for (L = levels; L >= 0; L--) {
+        double par[2];
+        int info, nfev;
+        D.level = L;
+        D.scale = 1.0 / img_scale;
+        orc_update_I1(&D);
+        orc_car2sph(mode, norm, &par[0], &par[1]);
+        info = orc_lmdif(&D, par, epsfcn, fvec, fjac, wa4, tmp, &nfev);
+        info_out[L] = info;
+        nfev_out[L] = nfev;
+        if (info < 0) { status = -info; break; }
+        orc_sph2car(mode, par[0], par[1], norm);
+        img_scale /= 2.0f;
+    }
+    n_out[0] = norm[0]; n_out[1] = norm[1]; n_out[2] = norm[2];
+    free(pix); free(rays); free(fvec); free(fjac); free(wa4); free(tmp); free(I1);
+    return status;
+}
+
+/* pyramid storage owned by the caller: levels+1 images of each frame */
+static void orc_build_pyramid(const uint8_t *img1, const uint8_t *img2, int w, int h, int levels,
+                              orc_pyramid *pyr, uint8_t **bufs)
+{
+    int L, f;
+    pyr->w[0] = w; pyr->h[0] = h;
+    pyr->img[0][0] = img1; pyr->img[1][0] = img2;
+    for (L = 1; L <= levels; L++) {
+        pyr->w[L] = (pyr->w[L - 1] + 1) / 2;
+        pyr->h[L] = (pyr->h[L - 1] + 1) / 2;
+        for (f = 0; f < 2; f++) {
+            uint8_t *b = (uint8_t *)malloc((size_t)pyr->w[L] * pyr->h[L]);
+            orc_pyrdown(pyr->img[f][L - 1], pyr->w[L - 1], pyr->h[L - 1], b);
+            pyr->img[f][L] = b;
+            bufs[2 * L + f] = b;
+        }
+    }
+}
+
+/* NormalOptimizer::computeOptimizedNormals over P points.  Per point: normal,
+   status (0 = kept; the reference erases every other point from points3D in
+   place, preserving order), per-level info and nfev (8 slots per point, index
+   = pyramid level), m_dat.  Returns the number of kept points. */
+ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], const double t2[3],
+                                 const uint8_t *img1, const uint8_t *img2, int w, int h, int levels,
+                                 const double *points, int P, int ray, int boundW, int boundH, double epsfcn,
+                                 double zmax, int mode, int NT, double *normals, int *status, int *info,
+                                 int *nfev, int *mdat, int nthreads)
+{
+    orc_pyramid pyr;
+    uint8_t *bufs[16] = {0};
+    int i, kept = 0, cmax = (int)(2 * zmax);
+    if (levels > 7) return -1;
+    orc_build_pyramid(img1, img2, w, h, levels, &pyr, bufs);
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : kept)
+#endif
+    for (i = 0; i < P; i++) {
+        status[i] = orc_point(cam, R2, t2, &pyr, levels, &points[3 * i], ray, boundW, boundH, epsfcn, cmax, mode, NT,
+                              &normals[3 * i], &info[8 * i], &nfev[8 * i], &mdat[i]);
+        if (status[i] == ORC_ST_OK) kept++;
+    }
+    for (i = 0; i < 16; i++) free(bufs[i]);
+    return kept;
+}
+
+/* Single-level LM on one point from a given starting (phi, theta): used by the
+   tests that pin lmdif against scipy.optimize.leastsq on the same residual. */
+ORC_API int orc_lm_single_level(const orc_camera *cam, const double R2[9], const double t2[3],
+                                const uint8_t *img1, const uint8_t *img2, int w, int h, const double X[3],
+                                const double *pix, int m, double epsfcn, double zmax, int mode, int NT,
+                                double par[2], int *nfev_out)
+{
+    orc_pyramid pyr;
+    orc_lmdata D;
+    double *rays = (double *)malloc(sizeof(double) * 2 * m), *fvec = (double *)malloc(sizeof(double) * m);
+    double *fjac = (double *)malloc(sizeof(double) * 2 * m), *wa4 = (double *)malloc(sizeof(double) * m);
+    double *tmp = (double *)malloc(sizeof(double) * m);
+    float *I1 = (float *)malloc(sizeof(float) * m);
+    int i, info;
+    pyr.img[0][0] = img1; pyr.img[1][0] = img2; pyr.w[0] = w; pyr.h[0] = h;
+    for (i = 0; i < m; i++) orc_undistort1(cam, pix[2 * i], pix[2 * i + 1], &rays[2 * i], &rays[2 * i + 1]);
+    memset(&D, 0, sizeof(D));
+    D.cam = cam; D.R2 = R2; D.t2 = t2; D.pyr = &pyr; D.level = 0; D.scale = 1.0;
+    D.X[0] = X[0]; D.X[1] = X[1]; D.X[2] = X[2];
+    D.cmax = (int)(2 * zmax); D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode; D.nthreads = NT;
+    orc_update_I1(&D);
+    info = orc_lmdif(&D, par, epsfcn, fvec, fjac, wa4, tmp, nfev_out);
+    free(rays); free(fvec); free(fjac); free(wa4); free(tmp); free(I1);
+    return info;
+}
+
+/* Residual vector of evaluateNormal at (phi, theta), level 0 (tests). */
+ORC_API int orc_eval_residual(const orc_camera *cam, const double R2[9], const double t2[3],
+                              const uint8_t *img1, const uint8_t *img2, int w, int h, const double X[3],
+                              const double *pix, int m, double zmax, int mode, const double par[2], double *fvec)
+{
+    orc_pyramid pyr;
+    orc_lmdata D;
+    double *rays = (double *)malloc(sizeof(double) * 2 * m);
+    float *I1 = (float *)malloc(sizeof(float) * m);
+    int i, st;
+    pyr.img[0][0] = img1; pyr.img[1][0] = img2; pyr.w[0] = w; pyr.h[0] = h;
+    for (i = 0; i < m; i++) orc_undistort1(cam, pix[2 * i], pix[2 * i + 1], &rays[2 * i], &rays[2 * i + 1]);
+    memset(&D, 0, sizeof(D));
+    D.cam = cam; D.R2 = R2; D.t2 = t2; D.pyr = &pyr; D.level = 0; D.scale = 1.0;
+    D.X[0] = X[0]; D.X[1] = X[1]; D.X[2] = X[2];
+    D.cmax = (int)(2 * zmax); D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode; D.nthreads = 256;
+    orc_update_I1(&D);
+    st = orc_eval(&D, par, fvec);
+    free(rays); free(I1);
+    return st;
+}
+
+ORC_API double orc_blocked_sum_test(const double *v, int m, int NT) { return orc_blocked_sum(v, m, NT); }

@@ -1,0 +1,225 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+F32, U8, BITS = 0, 1, 2
+STRICT, GRAM, DETMATH, CANONICAL = 0, 1, 2, 3
+
+ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL, ST_TOO_MANY = range(8)
+
+
+class OrcCamera(ctypes.Structure):
+    _fields_ = [("fx", ctypes.c_double), ("fy", ctypes.c_double), ("cx", ctypes.c_double),
+                ("cy", ctypes.c_double), ("k", ctypes.c_double * 5)]
+
+    @staticmethod
+    def from_cam(cam) -> "OrcCamera":
+        c = OrcCamera()
+        c.fx, c.fy, c.cx, c.cy = cam.fx, cam.fy, cam.cx, cam.cy
+        for i in range(5):
+            c.k[i] = cam.k[i]
+        return c
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liboracle.so missing: run `make -C oracle` (or __graft_entry__.build())")
+        _LIB = ctypes.CDLL(path)
+    return _LIB
+
+
+def _p(a, t=ctypes.c_double):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def setg12(rIC, tIC, T1, T2, r1, r2):
+    g = np.zeros(16)
+    lib().orc_setg12(_p(_f64(rIC)), _p(_f64(tIC)), _p(_f64(T1)), _p(_f64(T2)), _p(_f64(r1)), _p(_f64(r2)), _p(g))
+    return g.reshape(4, 4)
+
+
+def camera2_from_g12(g12):
+    R2 = np.zeros(9)
+    t2 = np.zeros(3)
+    lib().orc_camera2_from_g12(_p(_f64(np.asarray(g12).ravel())), _p(R2), _p(t2))
+    return R2.reshape(3, 3), t2
+
+
+def rodrigues_v2m(r):
+    R = np.zeros(9)
+    lib().orc_rodrigues_v2m(_p(_f64(r)), _p(R))
+    return R.reshape(3, 3)
+
+
+def rodrigues_m2v(R):
+    r = np.zeros(3)
+    lib().orc_rodrigues_m2v(_p(_f64(np.asarray(R).ravel())), _p(r))
+    return r
+
+
+def undistort(cam, xy):
+    xy = _f64(xy).reshape(-1, 2)
+    out = np.zeros_like(xy)
+    c = OrcCamera.from_cam(cam)
+    lib().orc_undistort(ctypes.byref(c), _p(xy), ctypes.c_int(xy.shape[0]), _p(out))
+    return out
+
+
+def project(cam, R, t, P):
+    P = _f64(P).reshape(-1, 3)
+    out = np.zeros((P.shape[0], 2))
+    c = OrcCamera.from_cam(cam)
+    lib().orc_project(ctypes.byref(c), _p(_f64(np.asarray(R).ravel())), _p(_f64(t)), _p(P),
+                      ctypes.c_int(P.shape[0]), _p(out))
+    return out
+
+
+def knn2(desc_a, desc_b, dtype: int, nthreads: int = 0):
+    a = np.ascontiguousarray(desc_a)
+    b = np.ascontiguousarray(desc_b)
+    n_a, dim = a.shape
+    idx = np.zeros((n_a, 2), dtype=np.int32)
+    dist = np.zeros((n_a, 2), dtype=np.float32)
+    lib().orc_knn2(ctypes.c_int(dtype), a.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(n_a),
+                   b.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(b.shape[0]), ctypes.c_int(dim),
+                   _p(idx, ctypes.c_int), _p(dist, ctypes.c_float), ctypes.c_int(nthreads))
+    return idx, dist
+
+
+def nndr(idx, dist, eps: float):
+    n_a = idx.shape[0]
+    q = np.zeros(n_a, dtype=np.int32)
+    t = np.zeros(n_a, dtype=np.int32)
+    d = np.zeros(n_a, dtype=np.float32)
+    n = lib().orc_nndr(_p(np.ascontiguousarray(idx, dtype=np.int32), ctypes.c_int),
+                       _p(np.ascontiguousarray(dist, dtype=np.float32), ctypes.c_float), ctypes.c_int(n_a),
+                       ctypes.c_double(eps), _p(q, ctypes.c_int), _p(t, ctypes.c_int), _p(d, ctypes.c_float))
+    return q[:n], t[:n], d[:n]
+
+
+def match_nndr(desc_a, desc_b, dtype: int, eps: float, nthreads: int = 0):
+    idx, dist = knn2(desc_a, desc_b, dtype, nthreads)
+    return nndr(idx, dist, eps)
+
+
+def triangulate(cam, g12, zmin, zmax, kp1, kp2, query, train):
+    K = len(query)
+    mask = np.zeros(K, dtype=np.uint8)
+    pts = np.zeros((max(K, 1), 3))
+    c = OrcCamera.from_cam(cam)
+    n = lib().orc_triangulate(ctypes.byref(c), _p(_f64(np.asarray(g12).ravel())), ctypes.c_double(zmin),
+                              ctypes.c_double(zmax), _p(np.ascontiguousarray(kp1, dtype=np.float32), ctypes.c_float),
+                              _p(np.ascontiguousarray(kp2, dtype=np.float32), ctypes.c_float),
+                              _p(np.ascontiguousarray(query, dtype=np.int32), ctypes.c_int),
+                              _p(np.ascontiguousarray(train, dtype=np.int32), ctypes.c_int), ctypes.c_int(K),
+                              _p(mask, ctypes.c_uint8), _p(pts))
+    return pts[:n].copy(), mask.astype(bool)
+
+
+def triangulate1(g12, u1, u2):
+    X = np.zeros(4)
+    lib().orc_triangulate1(_p(_f64(np.asarray(g12).ravel())), _p(_f64(u1)), _p(_f64(u2)), _p(X))
+    return X
+
+
+def pyrdown(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.zeros(((h + 1) // 2, (w + 1) // 2), dtype=np.uint8)
+    lib().orc_pyrdown(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _p(out, ctypes.c_uint8))
+    return out
+
+
+def bilinear(img, x, y):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    f = lib().orc_bilinear_sample
+    f.restype = ctypes.c_float
+    return f(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_float(x), ctypes.c_float(y))
+
+
+def neighborhood(cam, X, ray, bound_w=1024, bound_h=768):
+    cap = (2 * ray + 1) ** 2
+    out = np.zeros((cap, 2))
+    c = OrcCamera.from_cam(cam)
+    n = lib().orc_neighborhood(ctypes.byref(c), _p(_f64(X)), ctypes.c_int(ray), ctypes.c_int(bound_w),
+                               ctypes.c_int(bound_h), _p(out), ctypes.c_int(cap))
+    return out[:n].copy()
+
+
+def optimize_normals(cam, R2, t2, img1, img2, levels, points, ray, bound_w=1024, bound_h=768,
+                     epsfcn=1e-10, zmax=2.4, mode=STRICT, nt=256, nthreads=0):
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    h, w = img1.shape
+    P = _f64(points).reshape(-1, 3)
+    n = P.shape[0]
+    normals = np.zeros((n, 3))
+    status = np.zeros(n, dtype=np.int32)
+    info = np.zeros((n, 8), dtype=np.int32)
+    nfev = np.zeros((n, 8), dtype=np.int32)
+    mdat = np.zeros(n, dtype=np.int32)
+    c = OrcCamera.from_cam(cam)
+    lib().orc_optimize_normals(ctypes.byref(c), _p(_f64(np.asarray(R2).ravel())), _p(_f64(t2)),
+                               _p(img1, ctypes.c_uint8), _p(img2, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h),
+                               ctypes.c_int(levels), _p(P), ctypes.c_int(n), ctypes.c_int(ray), ctypes.c_int(bound_w),
+                               ctypes.c_int(bound_h), ctypes.c_double(epsfcn), ctypes.c_double(zmax),
+                               ctypes.c_int(mode), ctypes.c_int(nt), _p(normals), _p(status, ctypes.c_int),
+                               _p(info, ctypes.c_int), _p(nfev, ctypes.c_int), _p(mdat, ctypes.c_int),
+                               ctypes.c_int(nthreads))
+    return dict(normals=normals, status=status, info=info, nfev=nfev, mdat=mdat)
+
+
+def eval_residual(cam, R2, t2, img1, img2, X, pix, par, zmax=2.4, mode=STRICT):
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    h, w = img1.shape
+    pix = _f64(pix).reshape(-1, 2)
+    f = np.zeros(pix.shape[0])
+    c = OrcCamera.from_cam(cam)
+    st = lib().orc_eval_residual(ctypes.byref(c), _p(_f64(np.asarray(R2).ravel())), _p(_f64(t2)),
+                                 _p(img1, ctypes.c_uint8), _p(img2, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h),
+                                 _p(_f64(X)), _p(pix), ctypes.c_int(pix.shape[0]), ctypes.c_double(zmax),
+                                 ctypes.c_int(mode), _p(_f64(par)), _p(f))
+    return st, f
+
+
+def lm_single_level(cam, R2, t2, img1, img2, X, pix, par0, epsfcn=1e-10, zmax=2.4, mode=STRICT, nt=256):
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    h, w = img1.shape
+    pix = _f64(pix).reshape(-1, 2)
+    par = _f64(par0).copy()
+    nfev = ctypes.c_int(0)
+    c = OrcCamera.from_cam(cam)
+    info = lib().orc_lm_single_level(ctypes.byref(c), _p(_f64(np.asarray(R2).ravel())), _p(_f64(t2)),
+                                     _p(img1, ctypes.c_uint8), _p(img2, ctypes.c_uint8), ctypes.c_int(w),
+                                     ctypes.c_int(h), _p(_f64(X)), _p(pix), ctypes.c_int(pix.shape[0]),
+                                     ctypes.c_double(epsfcn), ctypes.c_double(zmax), ctypes.c_int(mode),
+                                     ctypes.c_int(nt), _p(par), ctypes.byref(nfev))
+    return info, par, nfev.value
+
+
+def blocked_sum(v, nt):
+    v = _f64(v)
+    f = lib().orc_blocked_sum_test
+    f.restype = ctypes.c_double
+    return f(_p(v), ctypes.c_int(v.size), ctypes.c_int(nt))

@@ -1,0 +1,290 @@
+"""GPU parity: libfm3d.so (HIP, gfx950) against the CPU oracle on the same inputs.
+
+Bar (north_star): bit-exact match indices and pixel neighbourhoods; normals
+within 1e-4.  The LM kernel replays the reference's sequential MINPACK sums, so
+it is compared BIT FOR BIT with the oracle run with the same deterministic
+transcendentals (oracle.DETMATH), and at 1e-4 with the libm-based oracle
+(oracle.STRICT).
+"""
+import numpy as np
+import pytest
+
+from conftest import oracle_threads
+
+pytestmark = pytest.mark.gpu
+
+
+def _settings(fm3d, cam, **kw):
+    s = fm3d.Settings.default()
+    s.set_camera(cam)
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+@pytest.fixture(scope="module")
+def pair(synth):
+    return synth.make_frame_pair(3000, seed=11)
+
+
+@pytest.fixture(scope="module")
+def ctx(fm3d, pair):
+    c = fm3d.Context(_settings(fm3d, pair.cam, pixelsRay=16))
+    yield c
+    c.close()
+
+
+# ---------------------------------------------------------------- matching
+@pytest.mark.parametrize("shape", [(3000, 3000), (777, 1500), (1, 5), (130, 1), (0, 10)])
+def test_knn2_u8_exact(fm3d, orc, ctx, pair, shape):
+    nA, nB = shape
+    rng = np.random.default_rng(nA * 7 + nB)
+    A = pair.desc1[:nA] if nA <= len(pair.desc1) else None
+    B = pair.desc2[:nB]
+    if nA <= 1 or nB <= 1:
+        A = rng.integers(0, 256, (nA, 128), dtype=np.uint8)
+        B = rng.integers(0, 256, (nB, 128), dtype=np.uint8)
+    dm = fm3d.DescriptorsMatcher(ctx)
+    if nA == 0:
+        assert len(dm.compareWithNNDR(0.55, A, B)) == 0
+        return
+    got = dm.knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.U8, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    ok = idx >= 0
+    assert np.array_equal(got["distance"][ok], dist[ok])
+    m = dm.compareWithNNDR(0.55, A, B)
+    q, t, d = orc.nndr(idx, dist, 0.55)
+    assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t) and np.array_equal(m["distance"], d)
+
+
+def test_knn2_u8_ties_lowest_index(fm3d, orc, ctx):
+    # duplicated train rows: equal distances must resolve to the lowest trainIdx
+    rng = np.random.default_rng(5)
+    B = rng.integers(0, 256, (300, 128), dtype=np.uint8)
+    B[200] = B[17]
+    B[250] = B[17]
+    A = np.concatenate([B[17:18], B[:40]])
+    got = fm3d.DescriptorsMatcher(ctx).knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.U8, 1)
+    assert np.array_equal(got["trainIdx"], idx)
+    assert got["trainIdx"][0, 0] == 17 and got["trainIdx"][0, 1] == 200
+
+
+def test_knn2_u8_dims(fm3d, orc, ctx):
+    rng = np.random.default_rng(9)
+    for dim in (64, 100, 256):
+        A = rng.integers(0, 256, (500, dim), dtype=np.uint8)
+        B = rng.integers(0, 256, (700, dim), dtype=np.uint8)
+        got = fm3d.DescriptorsMatcher(ctx).knn_match(A, B)
+        idx, dist = orc.knn2(A, B, orc.U8, oracle_threads())
+        assert np.array_equal(got["trainIdx"], idx), dim
+        assert np.array_equal(got["distance"], dist), dim
+
+
+@pytest.mark.parametrize("dim", [128, 64, 36])
+def test_knn2_f32_flann_order(fm3d, orc, ctx, dim):
+    # SURF-like non-integer floats: FLANN L2 accumulation order, float32
+    rng = np.random.default_rng(dim)
+    A = rng.normal(0, 0.1, (1200, dim)).astype(np.float32)
+    B = np.concatenate([A[:900] + rng.normal(0, 0.01, (900, dim)).astype(np.float32),
+                        rng.normal(0, 0.1, (700, dim)).astype(np.float32)])
+    dm = fm3d.DescriptorsMatcher(ctx)
+    got = dm.knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.F32, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    assert np.array_equal(got["distance"], dist)
+    m = dm.compareWithNNDR(0.6, A, B)
+    q, t, d = orc.nndr(idx, dist, 0.6)
+    assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t)
+
+
+def test_knn2_f32_integer_valued_sift(fm3d, orc, ctx, pair):
+    # OpenCV SIFT floats are integer valued: routed to the int8-MFMA kernel, same results
+    A = pair.desc1[:1500].astype(np.float32)
+    B = pair.desc2[:2000].astype(np.float32)
+    got = fm3d.DescriptorsMatcher(ctx).knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.F32, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    assert np.array_equal(got["distance"], dist)
+
+
+def test_knn2_hamming(fm3d, orc, ctx, synth):
+    fp = synth.make_frame_pair(1500, seed=3, desc="orb")
+    dm = fm3d.DescriptorsMatcher(ctx, binary=True)
+    got = dm.knn_match(fp.desc1, fp.desc2)
+    idx, dist = orc.knn2(fp.desc1, fp.desc2, orc.BITS, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    assert np.array_equal(got["distance"], dist)
+    m = dm.compareWithNNDR(0.8, fp.desc1, fp.desc2)
+    q, t, d = orc.nndr(idx, dist, 0.8)
+    assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t)
+    assert np.mean(fp.true_train[m["queryIdx"]] == m["trainIdx"]) > 0.95
+
+
+def test_nndr_appends(fm3d, ctx, pair):
+    dm = fm3d.DescriptorsMatcher(ctx)
+    m1 = dm.compareWithNNDR(0.55, pair.desc1[:500], pair.desc2)
+    m2 = dm.compareWithNNDR(0.55, pair.desc1[:500], pair.desc2, matches=m1)
+    assert len(m2) == 2 * len(m1)
+
+
+# ---------------------------------------------------------------- geometry
+def test_camera2_and_g12(fm3d, orc, ctx, pair):
+    sct = fm3d.SingleCameraTriangulator(ctx)
+    s = ctx.settings
+    g = sct.setg12(s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+    go = orc.setg12(list(s.rodriguesIC), list(s.translationIC), s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+    assert np.array_equal(g, go)
+    R2, t2 = sct.camera2()
+    R2o, t2o = orc.camera2_from_g12(g)
+    assert np.array_equal(R2, R2o) and np.array_equal(t2, t2o)
+
+
+def test_undistort_bitwise(fm3d, orc, ctx):
+    rng = np.random.default_rng(1)
+    xy = np.stack([rng.uniform(-50, 700, 5000), rng.uniform(-50, 530, 5000)], 1)
+    out = np.zeros_like(xy)
+    lib = fm3d.lib()
+    import ctypes
+    ctx.check(lib.fm3d_undistort(ctx.handle, xy.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(xy),
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+    cam = type("C", (), {})()
+    cam.fx, cam.fy, cam.cx, cam.cy, cam.k = ctx.settings.camera()
+    assert np.array_equal(out, orc.undistort(cam, xy))
+
+
+def test_triangulate_bitwise(fm3d, orc, ctx, pair):
+    dm = fm3d.DescriptorsMatcher(ctx)
+    m = dm.compareWithNNDR(0.55, pair.desc1, pair.desc2)
+    sct = fm3d.SingleCameraTriangulator(ctx)
+    sct.set_g12(pair.g12)
+    sct.setKeypoints(pair.kp1, pair.kp2, m)
+    pts, mask = sct.triangulate()
+    pto, masko = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, m["queryIdx"], m["trainIdx"])
+    assert np.array_equal(mask, masko)
+    assert np.array_equal(pts, pto)
+    assert 0 < len(pts) <= len(m)
+
+
+def test_pyramid_bitwise(fm3d, orc, ctx, pair):
+    no = fm3d.NormalOptimizer(ctx)
+    no.setImages(pair.img1, pair.img2)
+    for which, img in ((1, pair.img1), (2, pair.img2)):
+        ref = img
+        for L in range(ctx.settings.pyramids + 1):
+            got = no.pyramid(which, L)
+            assert np.array_equal(got, ref), (which, L)
+            ref = orc.pyrdown(ref)
+    # odd sizes
+    rng = np.random.default_rng(2)
+    for h, w in ((37, 53), (1, 9), (8, 1), (121, 160)):
+        img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        out = np.zeros(((h + 1) // 2, (w + 1) // 2), dtype=np.uint8)
+        import ctypes
+        ctx.check(fm3d.lib().fm3d_pyrdown(ctx.handle, img.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), w, h,
+                                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        assert np.array_equal(out, orc.pyrdown(img)), (h, w)
+
+
+# ---------------------------------------------------------------- normals
+def _normals_case(fm3d, orc, pair, points, ray, bound=(1024, 768), levels=3):
+    s = _settings(fm3d, pair.cam, pixelsRay=ray, boundWidth=bound[0], boundHeight=bound[1], pyramids=levels)
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(pair.g12)
+        R2, t2 = sct.camera2()
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(pair.img1, pair.img2)
+        kept, normals = no.computeOptimizedNormals(points)
+        st, info, nfev = no.last_status, no.last_info, no.last_nfev
+    finally:
+        ctx.close()
+    ref = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, levels, points, ray, bound[0], bound[1],
+                               mode=orc.DETMATH, nthreads=oracle_threads())
+    return kept, normals, st, info, nfev, ref, (R2, t2)
+
+
+@pytest.mark.parametrize("ray", [8, 16])
+def test_normals_bitwise_vs_oracle(fm3d, orc, pair, ray):
+    # triangulated points of the pair (oracle chain), plus border / degenerate cases
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    extra = np.array([[-1.3, -0.95, 2.0],    # projects near the top-left corner: trimmed neighbourhood
+                      [5.0, 5.0, 2.0],       # outside every image: no pixels
+                      [0.0, 0.0, 2.0]])
+    P = np.concatenate([pts[:120], extra])
+    kept, normals, st, info, nfev, ref, _ = _normals_case(fm3d, orc, pair, P, ray)
+    assert np.array_equal(st, ref["status"])
+    assert np.array_equal(info[:, :4], ref["info"][:, :4])
+    assert np.array_equal(nfev[:, :4], ref["nfev"][:, :4])
+    ok = ref["status"] == 0
+    assert np.array_equal(normals, ref["normals"][ok])
+    assert np.array_equal(kept, P[ok])
+    assert ok.sum() > 10
+
+
+def test_normals_vs_strict_oracle_1e4(fm3d, orc, pair):
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    P = pts[:80]
+    kept, normals, st, info, nfev, _, (R2, t2) = _normals_case(fm3d, orc, pair, P, 16)
+    strict = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, 3, P, 16, mode=orc.STRICT,
+                                  nthreads=oracle_threads())
+    assert np.array_equal(st, strict["status"])
+    ok = strict["status"] == 0
+    assert np.abs(normals - strict["normals"][ok]).max() < 1e-4   # north_star tolerance
+
+
+def test_normals_reference_config_ray64(fm3d, orc, pair):
+    # build/settings.yml: pixelsRay 64, pyramids 3 (12,853-pixel residuals)
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    P = pts[:24]
+    kept, normals, st, info, nfev, ref, _ = _normals_case(fm3d, orc, pair, P, 64)
+    assert np.array_equal(st, ref["status"])
+    assert np.array_equal(nfev[:, :4], ref["nfev"][:, :4])
+    ok = ref["status"] == 0
+    assert np.array_equal(normals, ref["normals"][ok])
+
+
+def test_normals_vga_bounds(fm3d, orc, pair):
+    # image bound = the VGA size instead of the reference's literal 1024x768
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    kept, normals, st, info, nfev, ref, _ = _normals_case(fm3d, orc, pair, pts[:60], 12, bound=(640, 480))
+    assert np.array_equal(st, ref["status"])
+    ok = ref["status"] == 0
+    assert np.array_equal(normals, ref["normals"][ok])
+
+
+# ---------------------------------------------------------------- whole path
+def test_pipeline_end_to_end(fm3d, orc, pair):
+    s = _settings(fm3d, pair.cam, pixelsRay=12)
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(pair.g12)
+        R2, t2 = sct.camera2()
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+        n, stats = pipe.run()
+        rec = pipe.records(n)
+        n2, _ = pipe.run()      # idempotent re-run on resident inputs
+        rec2 = pipe.records(n2)
+    finally:
+        ctx.close()
+    assert n == n2 and np.array_equal(rec, rec2)
+    q, t, d = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    assert stats["matches"] == len(q)
+    pts, mask = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    assert stats["inliers"] == len(pts)
+    ref = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, 3, pts, 12, mode=orc.DETMATH,
+                               nthreads=oracle_threads())
+    ok = ref["status"] == 0
+    assert n == ok.sum()
+    assert np.array_equal(rec["queryIdx"], q[mask][ok])
+    assert np.array_equal(rec["trainIdx"], t[mask][ok])
+    assert np.array_equal(rec["point"], pts[ok])
+    assert np.array_equal(rec["normal"], ref["normals"][ok])
