@@ -67,7 +67,7 @@ struct fm3d_ctx {
     DevBuf lvlDesc;
     // circle offsets of pixelsRay
     DevBuf offsets;
-    int nOff = 0;
+    int nOff = 0, nOffPad = 0;
     // work buffers
     DevBuf A, B, cqA, ctB, idx, key, fkey, knnOut, cand, flag, matches, count, scanTmp;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
@@ -244,9 +244,12 @@ int ensure_offsets(fm3d_ctx* c) {
     for (int i = -R; i <= R; i++)      // extractPixelsContour (:345-351): i outer (x), j inner (y)
         for (int j = -R; j <= R; j++)
             if (i * i + j * j <= R * R) off.push_back(make_int2(i, j));
+    c->nOff = (int)off.size();
+    // pad to a multiple of the kernel's pixel chunk with offsets that are never inside the image
+    while (off.size() % 8) off.push_back(make_int2(1 << 20, 1 << 20));
+    c->nOffPad = (int)off.size();
     HIPCHK(c, c->offsets.ensure(off.size() * sizeof(int2)));
     HIPCHK(c, hipMemcpy(c->offsets.p, off.data(), off.size() * sizeof(int2), hipMemcpyHostToDevice));
-    c->nOff = (int)off.size();
     return FM3D_OK;
 }
 
@@ -374,7 +377,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     HIPCHK(c, c->lmStat.ensure(64));
     // wavefronts: one lane per point, lanes refill from the queue
     long waves = c->s.lmWaves > 0 ? c->s.lmWaves : (P + 63) / 64;
-    const size_t perWave = (size_t)c->nOff * 64 * (5 * sizeof(double) + sizeof(float));
+    const size_t perWave = (size_t)c->nOffPad * 64 * (5 * sizeof(double) + sizeof(float));
     const size_t budget = (size_t)48 << 30;  // HBM budget for the per-lane pixel slabs
     long cap = (long)(budget / perWave);
     if (cap < 1) cap = 1;
@@ -395,6 +398,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     p.levels = levels;
     p.offsets = c->offsets.as<int2>();
     p.nOff = c->nOff;
+    p.nOffPad = c->nOffPad;
     p.boundW = c->s.boundWidth;
     p.boundH = c->s.boundHeight;
     p.epsfcn = c->s.epsilonLMMIN;

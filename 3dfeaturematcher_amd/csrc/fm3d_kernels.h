@@ -22,8 +22,8 @@ struct LMParams {
     double R2[9], t2[3];
     const LevelDesc* lvl;  // device array, levels+1 entries
     int levels;
-    const int2* offsets;  // circle offsets (i, j) in reference order
-    int nOff;
+    const int2* offsets;  // circle offsets (i, j) in reference order, padded to nOffPad
+    int nOff, nOffPad;
     int boundW, boundH;
     double epsfcn;
     int cmax;

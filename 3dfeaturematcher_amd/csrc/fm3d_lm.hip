@@ -285,6 +285,15 @@ __device__ inline int lm_after_qr(LM& s) {
     return 0;
 }
 
+// getBilinearInterpPix32f (tools.cpp:129-142) arithmetic on four gathered bytes
+__device__ inline float bilinear4(uint8_t b00_, uint8_t b01_, uint8_t b10_, uint8_t b11_, float x, float y) {
+    float x0 = (float)(int)floor((double)x), y0 = (float)(int)floor((double)y);
+    float b00 = (float)b00_, b10 = (float)b10_, b01 = (float)b01_, b11 = (float)b11_;
+    float xm0 = 1.0f - (x - x0), xm1 = (x - x0);
+    float ym0 = 1.0f - (y - y0), ym1 = (y - y0);
+    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
+}
+
 __device__ inline void sph2car_det(double phi, double theta, double& n0, double& n1, double& n2) {
     // tools.cpp:772-777 with the deterministic transcendentals
     n0 = fm3d_cos(theta) * fm3d_cos(phi);
@@ -294,12 +303,18 @@ __device__ inline void sph2car_det(double phi, double theta, double& n0, double&
 
 }  // namespace
 
+// Pixel loops run in chunks of kCh pixels: all slab loads of a chunk are issued
+// first, then the geometry, then all image gathers, then the in-order
+// accumulation -- so each wave keeps ~3*kCh 512-byte loads and 4*kCh gathers in
+// flight instead of three dependent round trips per pixel.
+constexpr int kCh = 8;
+
 __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
     const int lane = threadIdx.x & (kWave - 1);
     const long wave = (long)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     if (wave >= p.nWaves) return;  // whole wave exits together
-    const int nOff = p.nOff;
-    const size_t plane = (size_t)nOff * kWave;
+    const int nOffPad = p.nOffPad;  // multiple of kCh; padded offsets are never valid pixels
+    const size_t plane = (size_t)nOffPad * kWave;
     double* __restrict__ RX = p.slab + (size_t)wave * 5 * plane;
     double* __restrict__ RY = RX + plane;
     double* __restrict__ F = RY + plane;
@@ -315,9 +330,11 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
     int pidx = -1;
     double X0 = 0, X1 = 0, X2 = 0, ccx = 0, ccy = 0, nrm0 = 0, nrm1 = 0, nrm2 = 0;
     int m = 0, kfirst = 0, ksecond = 0, L = 0;
-    bool full = false, i1ok = true;
+    bool i1ok = true;
     double scale = 1.;
-    LevelDesc lv{};
+    // lanes without a point still execute the (masked-out) gathers of a chunk:
+    // keep their image pointers valid
+    LevelDesc lv = p.lvl[0];
     LM s{};
     int ekind = E_INITIAL;
     double ex0 = 0, ex1 = 0;
@@ -383,24 +400,28 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
         if (__any(st == S_INIT)) {
             const bool act = (st == S_INIT);
             int cnt = 0, kf = -1, ks = -1;
-            for (int k = 0; k < nOff; k++) {
-                const int2 o2 = p.offsets[k];
-                if (act) {
-                    // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH)
-                    double px = ccx + (double)o2.x, py = ccy + (double)o2.y;
-                    const size_t o = (size_t)k * kWave + lane;
-                    if (px < 0 || py < 0 || px >= p.boundW || py >= p.boundH) {
-                        RX[o] = __builtin_nan("");
-                    } else {
-                        double ux, uy;
-                        undistort1(p.cam, px, py, ux, uy);
-                        RX[o] = ux;
-                        RY[o] = uy;
-                        if (kf < 0)
-                            kf = k;
-                        else if (ks < 0)
-                            ks = k;
-                        cnt++;
+            for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
+#pragma unroll
+                for (int c = 0; c < kCh; c++) {
+                    const int k = k0 + c;
+                    const int2 o2 = p.offsets[k];
+                    if (act) {
+                        // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH)
+                        double px = ccx + (double)o2.x, py = ccy + (double)o2.y;
+                        const size_t o = (size_t)k * kWave + lane;
+                        if (px < 0 || py < 0 || px >= p.boundW || py >= p.boundH) {
+                            RX[o] = __builtin_nan("");
+                        } else {
+                            double ux, uy;
+                            undistort1(p.cam, px, py, ux, uy);
+                            RX[o] = ux;
+                            RY[o] = uy;
+                            if (kf < 0)
+                                kf = k;
+                            else if (ks < 0)
+                                ks = k;
+                            cnt++;
+                        }
                     }
                 }
             }
@@ -408,7 +429,6 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
                 m = cnt;
                 kfirst = kf;
                 ksecond = ks;
-                full = (m == nOff);
                 // initial guess: X / norm(X) == X * (1/norm) (Vec3d operator/)
                 double nr = sqrt(X0 * X0 + X1 * X1 + X2 * X2);
                 double inv = 1. / nr;
@@ -432,18 +452,37 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
                 scale = ldexp(1.0, -L);  // 1.0 / float(2^L)  (optimize_pyramid, :225-241)
                 i1ok = true;
             }
-            for (int k = 0; k < nOff; k++) {
-                const int2 o2 = p.offsets[k];
-                if (act && i1ok) {
-                    const size_t o = (size_t)k * kWave + lane;
-                    bool valid = full || (RX[o] == RX[o]);
-                    if (valid) {
-                        double px = ccx + (double)o2.x, py = ccy + (double)o2.y;
-                        if (!pixel_good(px, py, scale, lv.w, lv.h))
-                            i1ok = false;
-                        else
-                            I1[o] = bilinear(lv.img1, lv.w, (float)(scale * px), (float)(scale * py));
-                    }
+            for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
+                double rx[kCh];
+                const uint8_t* g[kCh];
+                float fx[kCh], fy[kCh];
+                bool use[kCh];
+#pragma unroll
+                for (int c = 0; c < kCh; c++) rx[c] = RX[(size_t)(k0 + c) * kWave + lane];
+#pragma unroll
+                for (int c = 0; c < kCh; c++) {
+                    const int2 o2 = p.offsets[k0 + c];
+                    double px = ccx + (double)o2.x, py = ccy + (double)o2.y;
+                    bool valid = act && (rx[c] == rx[c]);
+                    bool good = pixel_good(px, py, scale, lv.w, lv.h);
+                    if (valid && !good) i1ok = false;  // updateImage1PixelsIntensity (:580-584)
+                    use[c] = valid && good;
+                    fx[c] = (float)(scale * px);
+                    fy[c] = (float)(scale * py);
+                    g[c] = use[c] ? lv.img1 + (long)(int)floor((double)fy[c]) * lv.w + (int)floor((double)fx[c])
+                                  : lv.img1;
+                }
+                uint8_t b00[kCh], b01[kCh], b10[kCh], b11[kCh];
+#pragma unroll
+                for (int c = 0; c < kCh; c++) {
+                    b00[c] = g[c][0];
+                    b01[c] = g[c][1];
+                    b10[c] = g[c][lv.w];
+                    b11[c] = g[c][lv.w + 1];
+                }
+#pragma unroll
+                for (int c = 0; c < kCh; c++) {
+                    if (use[c]) I1[(size_t)(k0 + c) * kWave + lane] = bilinear4(b00[c], b01[c], b10[c], b11[c], fx[c], fy[c]);
                 }
             }
             if (act) {
@@ -495,34 +534,72 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
             }
             const bool run = act && fail == 0;
             if (__any(run)) {
-#pragma unroll 2
-                for (int k = 0; k < nOff; k++) {
-                    const size_t o = (size_t)k * kWave + lane;
-                    if (run && ph1 == 0) {
-                        double ux = RX[o];
-                        if (full || ux == ux) {
-                            double uy = RY[o];
-                            // projectPointToPlane (:421-470) + isInBoundingBox (:646-655)
-                            double nn = n0 * ux + n1 * uy + n2 * 1.;
-                            double kk = mm / nn;
-                            double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-                            if (P0 != P0 || P1 != P1 || P2 != P2) {
+                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
+                    double rx[kCh], ry[kCh], fk[kCh];
+                    float i1[kCh];
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        const size_t o = (size_t)(k0 + c) * kWave + lane;
+                        rx[c] = RX[o];
+                        ry[c] = RY[o];
+                        i1[c] = I1[o];
+                        fk[c] = F[o];
+                    }
+                    // geometry: projectPointToPlane (:421-470), isInBoundingBox (:646-655),
+                    // projectPointsToImage2 (:591-644)
+                    unsigned char code1[kCh];  // 0 ok, 1 invalid pixel, 2 NaN plane, 3 bbox
+                    bool good[kCh];
+                    float fx[kCh], fy[kCh];
+                    const uint8_t* g[kCh];
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        const double ux = rx[c], uy = ry[c];
+                        double nn = n0 * ux + n1 * uy + n2 * 1.;
+                        double kk = mm / nn;
+                        double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+                        unsigned char cd = 0;
+                        if (ux != ux)
+                            cd = 1;
+                        else if (P0 != P0 || P1 != P1 || P2 != P2)
+                            cd = 2;
+                        else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
+                            cd = 3;
+                        code1[c] = cd;
+                        double u, v;
+                        project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
+                        bool gd = (cd == 0) && pixel_good(u, v, scale, lv.w, lv.h);
+                        good[c] = gd;
+                        fx[c] = (float)(scale * u);
+                        fy[c] = (float)(scale * v);
+                        g[c] = gd ? lv.img2 + (long)(int)floor((double)fy[c]) * lv.w + (int)floor((double)fx[c])
+                                  : lv.img2;
+                    }
+                    uint8_t b00[kCh], b01[kCh], b10[kCh], b11[kCh];
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        b00[c] = g[c][0];
+                        b01[c] = g[c][1];
+                        b10[c] = g[c][lv.w];
+                        b11[c] = g[c][lv.w + 1];
+                    }
+                    // residuals in pixel order (evaluateNormal :145-148 / fdjac2)
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        if (run && ph1 == 0 && code1[c] != 1) {
+                            if (code1[c] == 2) {
                                 ph1 = FM3D_ST_NAN_PLANE;
-                            } else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm))) {
+                            } else if (code1[c] == 3) {
                                 ph1 = FM3D_ST_ABORT_BBOX;
                             } else if (i1ok && !ph3) {
-                                // projectPointsToImage2 (:591-644)
-                                double u, v;
-                                project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
-                                if (!pixel_good(u, v, scale, lv.w, lv.h)) {
+                                if (!good[c]) {
                                     ph3 = true;
                                 } else {
-                                    float I2 = bilinear(lv.img2, lv.w, (float)(scale * u), (float)(scale * v));
-                                    float dI = I1[o] - I2;
-                                    double r = w * (double)dI;  // evaluateNormal :145-148
+                                    float I2 = bilinear4(b00[c], b01[c], b10[c], b11[c], fx[c], fy[c]);
+                                    float dI = i1[c] - I2;
+                                    double r = w * (double)dI;
                                     double val = r;
-                                    if (isjac) val = (r - F[o]) / hj;  // fdjac2 forward difference
-                                    out[o] = val;
+                                    if (isjac) val = (r - fk[c]) / hj;
+                                    out[(size_t)(k0 + c) * kWave + lane] = val;
                                     en.add(val);
                                 }
                             }
@@ -571,7 +648,7 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
         if (__any(st == S_QR)) {
             const bool act = (st == S_QR);
             int pc = 0;
-            double ajn0 = 0, ajn0s = 0, apf = 0, aqf = 0, ff = 0, aps = 0, fs = 0, vfirst = 0;
+            double ajn0 = 0, ajn0s = 1, apf = 0, aqf = 0, ff = 0, aps = 0, fs = 0, vfirst = 0;
             const double* Jp = J0;
             const double* Jq = J1;
             bool t0 = false;
@@ -590,19 +667,31 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
                 fs = F[os];
                 t0 = (ajn0 != 0.);
                 ajn0s = (t0 && apf < 0.) ? -ajn0 : ajn0;
+                if (!t0) ajn0s = 1.;  // unused
                 vfirst = t0 ? (apf / ajn0s) + 1. : apf;
             }
             // P1: sum_i v_i a_q[i] (qrfac) and sum_i v_i f[i] (lmdif qtf, j = 0)
             double dot = 0., s0 = 0.;
             const bool run1 = act && t0;
             if (__any(run1)) {
-                for (int k = 0; k < nOff; k++) {
-                    const size_t o = (size_t)k * kWave + lane;
-                    if (run1 && (full || RX[o] == RX[o])) {
-                        double v = Jp[o] / ajn0s;
-                        if (k == kfirst) v = v + 1.;
-                        dot += v * Jq[o];
-                        s0 += v * F[o];
+                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
+                    double rx[kCh], ap[kCh], aq[kCh], fk[kCh];
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        const size_t o = (size_t)(k0 + c) * kWave + lane;
+                        rx[c] = RX[o];
+                        ap[c] = Jp[o];
+                        aq[c] = Jq[o];
+                        fk[c] = F[o];
+                    }
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        if (run1 && rx[c] == rx[c]) {
+                            double v = ap[c] / ajn0s;
+                            if (k0 + c == kfirst) v = v + 1.;
+                            dot += v * aq[c];
+                            s0 += v * fk[c];
+                        }
                     }
                 }
             }
@@ -624,42 +713,66 @@ __global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
             e2.init(m > 1 ? m - 1 : 1);
             double aqs1 = 0.;
             if (__any(act)) {
-                for (int k = 0; k < nOff; k++) {
-                    const size_t o = (size_t)k * kWave + lane;
-                    if (act && k > kfirst && (full || RX[o] == RX[o])) {
-                        double aq = Jq[o];
-                        if (t0) {
-                            double v = Jp[o] / ajn0s;
-                            aq = aq - tq * v;
+                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
+                    double rx[kCh], ap[kCh], aq[kCh];
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        const size_t o = (size_t)(k0 + c) * kWave + lane;
+                        rx[c] = RX[o];
+                        ap[c] = Jp[o];
+                        aq[c] = Jq[o];
+                    }
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        const int k = k0 + c;
+                        if (act && k > kfirst && rx[c] == rx[c]) {
+                            double a = aq[c];
+                            if (t0) {
+                                double v = ap[c] / ajn0s;
+                                a = a - tq * v;
+                            }
+                            e2.add(a);
+                            if (k == ksecond) aqs1 = a;
                         }
-                        e2.add(aq);
-                        if (k == ksecond) aqs1 = aq;
                     }
                 }
             }
-            double ajn1 = 0, ajn1s = 0, usecond = 0;
+            double ajn1 = 0, ajn1s = 1, usecond = 0;
             bool t1 = false;
             if (act) {
                 ajn1 = e2.finish();
                 t1 = (ajn1 != 0.);
                 ajn1s = (t1 && aqs1 < 0.) ? -ajn1 : ajn1;
+                if (!t1) ajn1s = 1.;  // unused
                 usecond = t1 ? (aqs1 / ajn1s) + 1. : aqs1;
             }
             // P3: lmdif qtf, j = 1: sum_{i>=1} u_i wa4_i
             double s1 = 0.;
             const bool run3 = act && usecond != 0.;
             if (__any(run3)) {
-                for (int k = 0; k < nOff; k++) {
-                    const size_t o = (size_t)k * kWave + lane;
-                    if (run3 && k > kfirst && (full || RX[o] == RX[o])) {
-                        double v = t0 ? Jp[o] / ajn0s : 0.;
-                        double aq = Jq[o];
-                        if (t0) aq = aq - tq * v;
-                        double u = t1 ? aq / ajn1s : aq;
-                        if (t1 && k == ksecond) u = u + 1.;
-                        double wa = F[o];
-                        if (q0) wa = wa + v * tq0;
-                        s1 += u * wa;
+                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
+                    double rx[kCh], ap[kCh], aq[kCh], fk[kCh];
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        const size_t o = (size_t)(k0 + c) * kWave + lane;
+                        rx[c] = RX[o];
+                        ap[c] = Jp[o];
+                        aq[c] = Jq[o];
+                        fk[c] = F[o];
+                    }
+#pragma unroll
+                    for (int c = 0; c < kCh; c++) {
+                        const int k = k0 + c;
+                        if (run3 && k > kfirst && rx[c] == rx[c]) {
+                            double v = t0 ? ap[c] / ajn0s : 0.;
+                            double a = aq[c];
+                            if (t0) a = a - tq * v;
+                            double u = t1 ? a / ajn1s : a;
+                            if (t1 && k == ksecond) u = u + 1.;
+                            double wa = fk[c];
+                            if (q0) wa = wa + v * tq0;
+                            s1 += u * wa;
+                        }
                     }
                 }
             }

@@ -1,0 +1,110 @@
+"""The C ABI library: loads, exports every symbol include/fm3d.h declares, host-only
+entry points (settings, g12 algebra) -- no GPU compute here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SETTINGS_YML = """%YAML:1.0
+IMAGES:
+   img1: /nonexistent/img_0000007809.pgm
+   img2: /nonexistent/img_0000007825.pgm
+   pos1: [5.301099, 8.031408, 1.977258, 0.153433, 0.149941, -2.658648]
+   pos2: [4.735536, 7.691893, 1.913166, 0.252828, 0.048977, -2.676886]
+NNDR:
+   epsilon: 0.6
+Neighborhoods:
+   #Part for normal optimization: take pixels in the image
+   epsilonLMMIN: 1e-10
+   pixelsRay: 32
+   pyramids: 2
+   method: square
+   cmPerPixel: 0.25
+   epsilon: 0.16
+FeatureOptions:
+   DetectorType: SURF
+   SurfDetector:
+      HessianThreshold: 400
+      Extended: 1
+CameraSettings:
+   rodriguesIC: [-1.2005, 1.1981, -1.2041]
+   translationIC: [0.0, 0.015, -0.051]
+   Fx: 572.4765
+   Fy: 572.69354
+   Cx: 549.75189
+   Cy: 411.68039
+   p1: -6.6e-05
+   p2: 0.000567
+   k0: -0.299957
+   k1: 0.124129
+   k2: -0.028357
+   zThresholdMin: 1.5
+   zThresholdMax: 2.4
+"""
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "fm3d.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(fm3d_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol(fm3d):
+    lib = fm3d.lib()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(fm3d.EXPORTS)
+
+
+def test_struct_layouts(fm3d):
+    assert fm3d.DMATCH.itemsize == 16          # cv::DMatch
+    assert fm3d.RECORD.itemsize == 64
+    assert ctypes.sizeof(fm3d.Settings) == 8 * 9 + 8 * 6 + 8 * 3 + 4 * 2 + 8 + 8 * 12 + 4 * 4
+
+
+def test_settings_default_is_reference_file(fm3d):
+    s = fm3d.Settings.default()
+    assert (s.Fx, s.Fy, s.Cx, s.Cy) == (572.4765, 572.69354, 549.75189, 411.68039)
+    assert (s.pixelsRay, s.pyramids, s.nndrEpsilon, s.epsilonLMMIN) == (64, 3, 0.55, 1e-10)
+    assert (s.boundWidth, s.boundHeight) == (1024, 768)
+
+
+def test_settings_yaml_subset(fm3d, tmp_path):
+    p = tmp_path / "settings.yml"
+    p.write_text(SETTINGS_YML)
+    s = fm3d.Settings.load(str(p))
+    assert s.pixelsRay == 32 and s.pyramids == 2 and s.nndrEpsilon == 0.6
+    assert list(s.pos2) == [4.735536, 7.691893, 1.913166, 0.252828, 0.048977, -2.676886]
+    assert list(s.translationIC) == [0.0, 0.015, -0.051]
+    assert s.k0 == -0.299957 and s.zThresholdMax == 2.4
+    with pytest.raises(fm3d.Fm3dError):
+        fm3d.Settings.load(str(tmp_path / "missing.yml"))
+
+
+def test_g12_host_algebra_bitwise_vs_oracle(fm3d, orc):
+    s = fm3d.Settings.default()
+    g = fm3d.g12_from_poses(s, s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+    go = orc.setg12(list(s.rodriguesIC), list(s.translationIC), s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+    assert np.array_equal(g, go)
+    R2, t2 = fm3d.camera2_from_g12(g)
+    R2o, t2o = orc.camera2_from_g12(go)
+    assert np.array_equal(R2, R2o) and np.array_equal(t2, t2o)
+    # R2 = Rodrigues(Rodrigues^-1(R12)) stays within ulps of the rotation block of g12
+    assert np.abs(R2 - g[:3, :3]).max() < 1e-14
+
+
+def test_compute_without_gpu_fails_loudly(fm3d):
+    """No CPU fallback: without a HIP device the context cannot be created."""
+    import subprocess
+    import sys
+    code = ("import importlib,sys; sys.path.insert(0, %r); f = importlib.import_module('3dfeaturematcher_amd');\n"
+            "try:\n    f.Context()\nexcept f.Fm3dError as e:\n    print('ERR', e.code)\nelse:\n    print('OK')") % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120).stdout
+    has_gpu = os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES", "x") != ""
+    if not has_gpu:
+        assert "ERR" in out
