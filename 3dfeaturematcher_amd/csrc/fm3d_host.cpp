@@ -245,8 +245,9 @@ int ensure_offsets(fm3d_ctx* c) {
         for (int j = -R; j <= R; j++)
             if (i * i + j * j <= R * R) off.push_back(make_int2(i, j));
     c->nOff = (int)off.size();
-    // pad to a multiple of the kernel's pixel chunk with offsets that are never inside the image
-    while (off.size() % 8) off.push_back(make_int2(1 << 20, 1 << 20));
+    // pad to a multiple of the LM kernel's pixel chunk (fm3d::kLMChunk) with offsets that are
+    // never inside the image
+    while (off.size() % fm3d::kLMChunk) off.push_back(make_int2(1 << 20, 1 << 20));
     c->nOffPad = (int)off.size();
     HIPCHK(c, c->offsets.ensure(off.size() * sizeof(int2)));
     HIPCHK(c, hipMemcpy(c->offsets.p, off.data(), off.size() * sizeof(int2), hipMemcpyHostToDevice));
@@ -375,17 +376,28 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     HIPCHK(c, c->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
     HIPCHK(c, c->lmQueue.ensure(64));
     HIPCHK(c, c->lmStat.ensure(64));
-    // wavefronts: one lane per point, lanes refill from the queue
-    long waves = c->s.lmWaves > 0 ? c->s.lmWaves : (P + 63) / 64;
-    const size_t perWave = (size_t)c->nOffPad * 64 * (5 * sizeof(double) + sizeof(float));
-    const size_t budget = (size_t)48 << 30;  // HBM budget for the per-lane pixel slabs
-    long cap = (long)(budget / perWave);
+    // persistent workgroups of fm3d::kLMSlots points each; slots refill from the queue
+    long groups = c->s.lmWaves;
+    if (groups <= 0) {
+        int dev = 0, cus = 0, perCU = 0;
+        HIPCHK(c, hipGetDevice(&dev));
+        HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, reinterpret_cast<const void*>(fm3d::lm_kernel),
+                                                               fm3d::kLMThreads, 0));
+        if (perCU < 1) perCU = 1;
+        groups = (long)cus * perCU;
+    }
+    const long needed = (P + fm3d::kLMSlots - 1) / fm3d::kLMSlots;
+    if (groups > needed) groups = needed;
+    const size_t ents = (size_t)c->nOffPad * fm3d::kLMSlots;
+    const size_t perGroup = ents * (5 * sizeof(double) + sizeof(float));
+    const size_t budget = (size_t)48 << 30;  // HBM budget for the per-group pixel slabs
+    long cap = (long)(budget / perGroup);
     if (cap < 1) cap = 1;
-    if (waves > cap) waves = cap;
-    if (waves > 4096) waves = 4096;
-    if (waves < 1) waves = 1;
-    HIPCHK(c, c->slab.ensure(perWave / (5 * sizeof(double) + sizeof(float)) * 5 * sizeof(double) * waves));
-    HIPCHK(c, c->slabI1.ensure(perWave / (5 * sizeof(double) + sizeof(float)) * sizeof(float) * waves));
+    if (groups > cap) groups = cap;
+    if (groups < 1) groups = 1;
+    HIPCHK(c, c->slab.ensure(ents * 5 * sizeof(double) * groups));
+    HIPCHK(c, c->slabI1.ensure(ents * sizeof(float) * groups));
     HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64, c->stream));
     HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 64, c->stream));
     fm3d::LMParams p{};
@@ -406,7 +418,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     p.queue = c->lmQueue.as<int>();
     p.slab = c->slab.as<double>();
     p.slabI1 = c->slabI1.as<float>();
-    p.nWaves = waves;
+    p.nWaves = groups;
     p.normals = c->lmNormals.as<double>();
     p.status = c->lmStatus.as<int>();
     p.info = c->lmInfo.as<int>();
@@ -415,16 +427,18 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     p.statEval = c->lmStat.as<unsigned long long>();
     p.statPix = c->lmStat.as<unsigned long long>() + 1;
     p.overflow = (int*)(c->lmStat.as<unsigned long long>() + 2);
-    {   // per lane: <= points per lane x (levels+1) x (300 evaluations + QR) + slack
-        long long lanes = waves * 64;
-        long long perLane = (P + lanes - 1) / lanes + 1;
-        p.maxIter = perLane * (long long)(levels + 1) * 700 + 1000;
+    {   // guards against a broken state machine (never expected to trigger): main-loop passes per
+        // group <= its points x levels x (300 evaluations + QR passes), and a wall-clock limit
+        long long perGroup = (P + groups - 1) / groups + 1;
+        p.maxIter = perGroup * (long long)(levels + 1) * 1600 + 10000;
+        int dev = 0, khz = 0;
+        HIPCHK(c, hipGetDevice(&dev));
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+        p.maxTicks = (long long)khz * 1000 * 300;  // 300 s
     }
     if (P > 0) {
-        const int wavesPerBlock = 4;
-        const int blocks = (int)((waves + wavesPerBlock - 1) / wavesPerBlock);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        fm3d::lm_kernel<<<blocks, 64 * wavesPerBlock, 0, c->stream>>>(p);
+        fm3d::lm_kernel<<<(int)groups, fm3d::kLMThreads, 0, c->stream>>>(p);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(e1, c->stream));
     }

@@ -28,9 +28,9 @@ struct LMParams {
     double epsfcn;
     int cmax;
     int* queue;
-    double* slab;    // nWaves * 5 * nOff * 64 doubles
-    float* slabI1;   // nWaves * nOff * 64 floats
-    long nWaves;
+    double* slab;    // nWaves groups x 5 arrays x nOffPad x kLMSlots doubles ([pixel][slot])
+    float* slabI1;   // nWaves groups x nOffPad x kLMSlots floats
+    long nWaves;     // number of workgroups
     double* normals;  // P x 3
     int* status;      // P
     int* info;        // P x 8
@@ -38,9 +38,14 @@ struct LMParams {
     int* mdat;        // P
     unsigned long long* statEval;
     unsigned long long* statPix;
-    long long maxIter;       // safety bound on main-loop iterations per wave
-    int* overflow;           // set to 1 if a wave hit maxIter
+    long long maxIter;       // safety bound on main-loop passes per workgroup
+    long long maxTicks;      // safety bound on wall-clock ticks per workgroup
+    int* overflow;           // set to 1 if a workgroup hit a guard
 };
+
+constexpr int kLMSlots = 4;     // points per LM workgroup
+constexpr int kLMThreads = 256;
+constexpr int kLMChunk = 512;   // pixels per LM chunk (offsets are padded to a multiple)
 
 __global__ void lm_kernel(LMParams p);
 

@@ -5,18 +5,24 @@
 // SingleCameraTriangulator geometry it calls (singlecameratriangulator.cpp:341-665),
 // minimised by lmfit's lmmin (MINPACK lmdif with lmfit's lm_control_double).
 //
-// Design: one LANE per keypoint.  The LM trajectory of a point
-// is decided at the rounding-noise level (ftol = xtol = 30*DBL_EPSILON), so any
-// reordering of the m_dat-long sums (fnorm, column norms, Householder dot
-// products) changes which steps are accepted and moves the final normal by up
-// to 1e-2 on ~15 % of points (measured with the oracle).  Each lane
-// therefore runs the reference's sequential algorithm for its own point: every
-// sum is accumulated in pixel-index order exactly as MINPACK does, so results
-// are bit-identical to the oracle.  The 64 lanes of a wave stream their per-pixel
-// arrays from a slab laid out [pixel][lane] (one 512-byte line per double
-// array and pixel), so every load and store is fully coalesced; the image
-// samples are gathers served from L2.  Lanes fetch new points from a global
-// queue when they finish one, so a wave stays full until the queue drains.
+// Design.  The LM trajectory of a point is decided at the
+// rounding-noise level (ftol = xtol = 30*DBL_EPSILON): any reordering of the
+// m_dat-long sums (fnorm, column norms, Householder dot products) changes which
+// steps are accepted and moves the final normal by up to 1e-2 on ~15 % of
+// points (measured with the oracle).  So every sum is replayed in
+// MINPACK's pixel order, bit for bit -- but only the ADDS are sequential:
+//
+//   * a workgroup (256 threads) serves kG = 4 points ("slots");
+//   * each pass over the neighbourhood runs in chunks of kC pixels: all 256
+//     threads compute the per-(pixel, slot) terms in parallel -- the residual
+//     (plane intersection, distorted projection, bilinear samples), Jacobian
+//     columns, Householder products -- and park them in LDS;
+//   * one "chain" lane per slot (lanes 0..3 of wave 0) then adds the chunk's
+//     terms in pixel order (MINPACK enorm / dot-product order) and runs the
+//     slot's lmdif bookkeeping between passes;
+//   * per-pixel state (undistorted rays, I1, fvec, Jacobian) lives in a
+//     per-workgroup slab laid out [pixel][slot] (coalesced 2 KB per load
+//     instruction); slots fetch new points from a global queue.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
@@ -28,7 +34,6 @@ namespace fm3d {
 
 namespace {
 
-constexpr int kWave = 64;
 
 enum LaneState { S_NEED_POINT = 0, S_INIT, S_LEVEL, S_EVAL, S_QR, S_DONE };
 enum EvalKind { E_INITIAL = 0, E_JAC0, E_JAC1, E_TRIAL };
@@ -303,511 +308,616 @@ __device__ inline void sph2car_det(double phi, double theta, double& n0, double&
 
 }  // namespace
 
-// Pixel loops run in chunks of kCh pixels: all slab loads of a chunk are issued
-// first, then the geometry, then all image gathers, then the in-order
-// accumulation -- so each wave keeps ~3*kCh 512-byte loads and 4*kCh gathers in
-// flight instead of three dependent round trips per pixel.
-constexpr int kCh = 8;
+constexpr int kG = kLMSlots;                  // points (slots) per workgroup
+constexpr int kThreads = kLMThreads;
+constexpr int kC = kLMChunk;                  // pixels per chunk
+constexpr int kPer = kC * kG / kThreads;      // entries per thread per chunk (8)
+constexpr int kSub = 4;                       // entries in flight per thread (register budget)
 
-__global__ __launch_bounds__(256) void lm_kernel(LMParams p) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const long wave = (long)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-    if (wave >= p.nWaves) return;  // whole wave exits together
-    const int nOffPad = p.nOffPad;  // multiple of kCh; padded offsets are never valid pixels
-    const size_t plane = (size_t)nOffPad * kWave;
-    double* __restrict__ RX = p.slab + (size_t)wave * 5 * plane;
-    double* __restrict__ RY = RX + plane;
-    double* __restrict__ F = RY + plane;
-    double* __restrict__ J0 = F + plane;
-    double* __restrict__ J1 = J0 + plane;
-    float* __restrict__ I1 = p.slabI1 + (size_t)wave * plane;
-    const double eps = sqrt(p.epsfcn > kEpsmch ? p.epsfcn : kEpsmch);
-    const double cm = (double)p.cmax;
-    const double Ident[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    const double Zero[3] = {0, 0, 0};
+enum PassKind { P_IDLE = 0, P_INIT, P_LEVEL, P_EVAL, P_QR1, P_QR2, P_QR3, P_DONE };
 
-    int st = S_NEED_POINT;
-    int pidx = -1;
-    double X0 = 0, X1 = 0, X2 = 0, ccx = 0, ccy = 0, nrm0 = 0, nrm1 = 0, nrm2 = 0;
-    int m = 0, kfirst = 0, ksecond = 0, L = 0;
-    bool i1ok = true;
-    double scale = 1.;
-    // lanes without a point still execute the (masked-out) gathers of a chunk:
-    // keep their image pointers valid
-    LevelDesc lv = p.lvl[0];
-    LM s{};
-    int ekind = E_INITIAL;
-    double ex0 = 0, ex1 = 0;
-    long long cnt_eval = 0, cnt_pix = 0;
+// parameters of a slot's current pass (LDS; written by the slot's chain lane)
+struct SlotP {
+    int pass, ekind, kfirst, ksecond, t0, t1, q0, pivot, lw, lh;
+    double n0, n1, n2, mm, w, hj, scale, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant;
+    const uint8_t* img1;
+    const uint8_t* img2;
+};
 
-    auto finish_point = [&](int code) {
-        p.status[pidx] = code;
-        p.normals[3 * pidx + 0] = nrm0;
-        p.normals[3 * pidx + 1] = nrm1;
-        p.normals[3 * pidx + 2] = nrm2;
-        p.mdat[pidx] = m;
-        st = S_NEED_POINT;
-    };
-    auto level_done = [&](int info) {
-        p.info[8 * pidx + L] = info;
-        p.nfev[8 * pidx + L] = s.nfev;
-        sph2car_det(s.x[0], s.x[1], nrm0, nrm1, nrm2);
-        L--;
-        if (L < 0)
-            finish_point(FM3D_ST_OK);
+// persistent state of a slot (LDS; only its chain lane touches it)
+struct SlotS {
+    LM s;
+    double X0, X1, X2, ccx, ccy, nrm0, nrm1, nrm2;
+    double apf, aqf, ff, aps, fs, vfirst, r01, tq0, qtf0, wa4s, usecond, ajn0s, tq, ajn1s;
+    int pidx, m, kfirst, ksecond, L, i1ok, ekind, t0, q0, t1;
+};
+
+// per-pass results the chain lane hands to the bookkeeping
+struct PassOut {
+    double nrm;          // EVAL / QR2: enorm of the pass's values
+    double sumA, sumB;   // QR1 / QR3 dot products
+    double aqs1;         // QR2: transformed a_q at the second kept pixel
+    int cnt, kmin, fail, ph3, i1fail;
+};
+
+// lmdif bookkeeping of one slot (chain lane only).  Kept out of line so that the
+// register budget of the data-parallel part of the kernel is not set by it.
+struct Ctl {
+    const LMParams* p;
+    double* F;
+    double* J0;
+    double* J1;
+    double eps;
+    long long cnt_eval, cnt_pix;
+
+    __device__ void fetch(SlotS& S, SlotP& P) {
+        int pidx = atomicAdd(p->queue, 1);
+        if (pidx >= p->P) {
+            P.pass = P_DONE;
+            return;
+        }
+        S.pidx = pidx;
+        S.X0 = p->points[3 * pidx + 0];
+        S.X1 = p->points[3 * pidx + 1];
+        S.X2 = p->points[3 * pidx + 2];
+        const double Ident[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        const double Zero[3] = {0, 0, 0};
+        double cx, cy;
+        project1(p->cam, Ident, Zero, S.X0, S.X1, S.X2, cx, cy);  // extractPixelsContour(Vec3d) :376-397
+        S.ccx = cx;
+        S.ccy = cy;
+        for (int l = 0; l < 8; l++) {
+            p->info[8 * pidx + l] = 0;
+            p->nfev[8 * pidx + l] = 0;
+        }
+        P.pass = P_INIT;
+        P.ccx = cx;
+        P.ccy = cy;
+    }
+    __device__ void start_level(SlotS& S, SlotP& P) {
+        const LevelDesc lv = p->lvl[S.L];
+        P.pass = P_LEVEL;
+        P.scale = ldexp(1.0, -S.L);  // 1.0 / float(2^L)  (optimize_pyramid, :225-241)
+        P.img1 = lv.img1;
+        P.img2 = lv.img2;
+        P.lw = lv.w;
+        P.lh = lv.h;
+    }
+    __device__ void finish_point(SlotS& S, SlotP& P, int code) {
+        p->status[S.pidx] = code;
+        p->normals[3 * S.pidx + 0] = S.nrm0;
+        p->normals[3 * S.pidx + 1] = S.nrm1;
+        p->normals[3 * S.pidx + 2] = S.nrm2;
+        p->mdat[S.pidx] = S.m;
+        fetch(S, P);
+    }
+    __device__ void level_done(SlotS& S, SlotP& P, int info) {
+        p->info[8 * S.pidx + S.L] = info;
+        p->nfev[8 * S.pidx + S.L] = S.s.nfev;
+        sph2car_det(S.s.x[0], S.s.x[1], S.nrm0, S.nrm1, S.nrm2);
+        S.L--;
+        if (S.L < 0)
+            finish_point(S, P, FM3D_ST_OK);
         else
-            st = S_LEVEL;
-    };
-    auto abort_level = [&](int code) {
-        p.info[8 * pidx + L] = -code;
-        p.nfev[8 * pidx + L] = s.nfev;
-        finish_point(code);
-    };
-    auto request_eval = [&](int kind, double a, double b) {
-        ekind = kind;
-        ex0 = a;
-        ex1 = b;
-        st = S_EVAL;
-    };
+            start_level(S, P);
+    }
+    __device__ void abort_level(SlotS& S, SlotP& P, int code) {
+        p->info[8 * S.pidx + S.L] = -code;
+        p->nfev[8 * S.pidx + S.L] = S.s.nfev;
+        finish_point(S, P, code);
+    }
+    // evaluateNormal (normaloptimizer.cpp:65-149), per-call part
+    __device__ void eval_pass(SlotS& S, SlotP& P, int kind, double a, double b) {
+        S.s.nfev++;
+        cnt_eval++;
+        cnt_pix += S.m;
+        double n0, n1, n2;
+        sph2car_det(a, b, n0, n1, n2);  // par = (phi, theta)
+        if (n2 != n2 || n1 != n1 || n0 != n0) {
+            abort_level(S, P, FM3D_ST_NAN_NORMAL);
+            return;
+        }
+        double w_theta = 1.0, w_phi = 1.0;
+        if (fabs(b) - M_PI / 2 > 0 || fabs(a) - M_PI > 0) {
+            w_theta = fm3d_exp(fabs(b) - M_PI / 2) + 1;
+            w_phi = fm3d_exp(fabs(a) - M_PI + 1) + 1;
+        }
+        S.ekind = kind;
+        P.pass = P_EVAL;
+        P.ekind = kind;
+        P.n0 = n0;
+        P.n1 = n1;
+        P.n2 = n2;
+        P.mm = n0 * S.X0 + n1 * S.X1 + n2 * S.X2;
+        P.w = w_phi * w_theta;
+        P.hj = kind == E_JAC0 ? S.s.h[0] : kind == E_JAC1 ? S.s.h[1] : 1.0;
+        P.agiant = 1.304e19 / (double)S.m;
+    }
+    __device__ void jac0(SlotS& S, SlotP& P) {
+        LM& s = S.s;
+        s.h[0] = eps * fabs(s.x[0]);
+        if (s.h[0] == 0.) s.h[0] = eps;
+        eval_pass(S, P, E_JAC0, s.x[0] + s.h[0], s.x[1]);
+    }
+    __device__ void finalize_qr(SlotS& S, SlotP& P, double qtf1) {
+        S.s.r[0] = S.t0 ? -S.ajn0s : 0.;
+        S.s.r[1] = 0.;
+        S.s.r[2] = S.r01;
+        S.s.r[3] = S.t1 ? -S.ajn1s : 0.;
+        S.s.qtf[0] = S.qtf0;
+        S.s.qtf[1] = qtf1;
+        int info = lm_after_qr(S.s);
+        if (info) {
+            level_done(S, P, info);
+        } else {
+            lm_inner_step(S.s);
+            eval_pass(S, P, E_TRIAL, S.s.wa2[0], S.s.wa2[1]);
+        }
+    }
+    // qrfac with column pivoting for n = 2, on the Jacobian columns left in the slab
+    __device__ void start_qr(SlotS& S, SlotP& P, int slot) {
+        LM& s = S.s;
+        const int pc = (s.acnorm[1] > s.acnorm[0]) ? 1 : 0;  // pivot column = larger norm
+        s.ipvt[0] = pc;
+        s.ipvt[1] = 1 - pc;
+        const double* Jpp = pc ? J1 : J0;
+        const double* Jqq = pc ? J0 : J1;
+        const size_t of = (size_t)S.kfirst * kG + slot, os = (size_t)S.ksecond * kG + slot;
+        S.apf = Jpp[of];
+        S.aqf = Jqq[of];
+        S.ff = F[of];
+        S.aps = Jpp[os];
+        S.fs = F[os];
+        const double ajn0 = s.acnorm[pc];  // == enorm of the pivot column (same elements, same order)
+        S.t0 = ajn0 != 0.;
+        S.ajn0s = (S.t0 && S.apf < 0.) ? -ajn0 : ajn0;
+        if (!S.t0) S.ajn0s = 1.;  // unused
+        S.vfirst = S.t0 ? (S.apf / S.ajn0s) + 1. : S.apf;
+        P.pivot = pc;
+        P.kfirst = S.kfirst;
+        P.ksecond = S.ksecond;
+        P.t0 = S.t0;
+        P.ajn0s = S.ajn0s;
+        if (S.t0) {
+            P.pass = P_QR1;
+        } else {
+            S.tq = 0.;
+            S.r01 = S.aqf;
+            S.q0 = 0;  // vfirst == apf == 0
+            S.tq0 = 0.;
+            S.qtf0 = S.ff;
+            qr2(S, P);
+        }
+    }
+    __device__ void qr2(SlotS& S, SlotP& P) {
+        P.pass = P_QR2;
+        P.tq = S.tq;
+        P.agiant = 1.304e19 / (double)(S.m - 1);
+    }
+
+    __device__ __noinline__ void after_pass(SlotS& S, SlotP& P, const PassOut& o, int slot) {
+        const int ps = P.pass;
+        if (ps == P_INIT) {
+            S.m = o.cnt;
+            S.kfirst = o.kmin;
+            // second kept pixel: next offset after kfirst inside the bounds
+            int ks = -1;
+            for (int k = S.kfirst + 1; S.m > 1 && k < p->nOff; k++) {
+                const int2 o2 = p->offsets[k];
+                const double px = S.ccx + (double)o2.x, py = S.ccy + (double)o2.y;
+                if (!(px < 0 || py < 0 || px >= p->boundW || py >= p->boundH)) {
+                    ks = k;
+                    break;
+                }
+            }
+            S.ksecond = ks;
+            // initial guess: X / norm(X) == X * (1/norm) (Vec3d operator/, :342-343)
+            double nr = sqrt(S.X0 * S.X0 + S.X1 * S.X1 + S.X2 * S.X2);
+            double inv = 1. / nr;
+            S.nrm0 = S.X0 * inv;
+            S.nrm1 = S.X1 * inv;
+            S.nrm2 = S.X2 * inv;
+            if (S.m <= 0) {
+                finish_point(S, P, FM3D_ST_NO_PIXELS);
+            } else {
+                S.L = p->levels;
+                start_level(S, P);
+            }
+        } else if (ps == P_LEVEL) {
+            S.i1ok = o.i1fail ? 0 : 1;
+            // car2sph (tools.cpp:767-771) -> lmdif from the current normal
+            S.s.x[1] = fm3d_atan2(S.nrm2, sqrt(S.nrm0 * S.nrm0 + S.nrm1 * S.nrm1));
+            S.s.x[0] = fm3d_atan2(S.nrm1, S.nrm0);
+            S.s.nfev = 0;
+            S.s.iter = 1;
+            S.s.par = 0.;
+            S.s.delta = 0.;
+            S.s.xnorm = 0.;
+            if (S.m < 2)
+                level_done(S, P, 0);  // lmdif: m < n -> improper input, info 0, no evaluation
+            else
+                eval_pass(S, P, E_INITIAL, S.s.x[0], S.s.x[1]);
+        } else if (ps == P_EVAL) {
+            int code = 0;
+            if (o.fail != 0x7fffffff)  // first failing pixel in index order decides (:455-470, :557-560)
+                code = (o.fail & 3) == 2 ? FM3D_ST_NAN_PLANE : FM3D_ST_ABORT_BBOX;
+            else if (!S.i1ok)
+                code = FM3D_ST_ABORT_PIX1;
+            else if (o.ph3)
+                code = FM3D_ST_ABORT_PIX2;
+            if (code) {
+                abort_level(S, P, code);
+                return;
+            }
+            LM& s = S.s;
+            if (S.ekind == E_INITIAL) {
+                s.fnorm = o.nrm;
+                jac0(S, P);
+            } else if (S.ekind == E_JAC0) {
+                s.acnorm[0] = o.nrm;
+                s.h[1] = eps * fabs(s.x[1]);
+                if (s.h[1] == 0.) s.h[1] = eps;
+                eval_pass(S, P, E_JAC1, s.x[0], s.x[1] + s.h[1]);
+            } else if (S.ekind == E_JAC1) {
+                s.acnorm[1] = o.nrm;
+                start_qr(S, P, slot);
+            } else {
+                bool accepted;
+                int info = lm_after_trial(s, o.nrm, &accepted);
+                if (info) {
+                    level_done(S, P, info);
+                } else if (accepted) {
+                    jac0(S, P);
+                } else {
+                    lm_inner_step(s);
+                    eval_pass(S, P, E_TRIAL, s.wa2[0], s.wa2[1]);
+                }
+            }
+        } else if (ps == P_QR1) {
+            // qrfac j = 0: temp = sum v a_q / v_first; lmdif qtf j = 0: temp = -sum v f / v_first
+            S.tq = o.sumA / S.vfirst;
+            S.r01 = S.aqf - S.tq * S.vfirst;
+            S.q0 = S.vfirst != 0.;
+            S.tq0 = 0.;
+            S.qtf0 = S.ff;
+            if (S.q0) {
+                S.tq0 = -o.sumB / S.vfirst;
+                S.qtf0 = S.ff + S.vfirst * S.tq0;
+            }
+            qr2(S, P);
+        } else if (ps == P_QR2) {
+            const double ajn1 = o.nrm;
+            S.t1 = ajn1 != 0.;
+            S.ajn1s = (S.t1 && o.aqs1 < 0.) ? -ajn1 : ajn1;
+            if (!S.t1) S.ajn1s = 1.;  // unused
+            S.usecond = S.t1 ? (o.aqs1 / S.ajn1s) + 1. : o.aqs1;
+            S.wa4s = S.q0 ? S.fs + (S.aps / S.ajn0s) * S.tq0 : S.fs;
+            if (S.usecond != 0.) {
+                P.pass = P_QR3;
+                P.t1 = S.t1;
+                P.ajn1s = S.ajn1s;
+                P.q0 = S.q0;
+                P.tq0 = S.tq0;
+            } else {
+                finalize_qr(S, P, S.wa4s);
+            }
+        } else if (ps == P_QR3) {
+            const double tq1 = -o.sumA / S.usecond;
+            finalize_qr(S, P, S.wa4s + S.usecond * tq1);
+        }
+    }
+};
+
+__device__ __noinline__ void ctl_fetch(Ctl& c, SlotS& S, SlotP& P) { c.fetch(S, P); }
+
+// enorm terms: x^2 for MINPACK's "intermediate" range (the branch almost every value
+// takes), 0 otherwise; values outside that range raise the chunk's slow flag
+__device__ inline double enorm_term(double x, double agiant, int* slow) {
+    const double xa = fabs(x);
+    if (xa > 3.834e-20 && xa < agiant) return xa * xa;
+    if (xa != 0.) *slow = 1;
+    return 0.;
+}
+
+__global__ __launch_bounds__(kThreads) void lm_kernel(LMParams p) {
+    __shared__ double term[2][kG][kC];
+    __shared__ SlotP sp[kG];
+    __shared__ SlotS ss[kG];
+    __shared__ int shCnt[kG], shKmin[kG], shFail[kG], shPh3[kG], shI1fail[kG], shSlow[kG];
+    __shared__ double shAqs1[kG];
+    __shared__ int shStop;
+
+    const int tid = threadIdx.x;
+    const int slot = tid & (kG - 1);
+    const int prow = tid >> 2;  // pixel row of this thread inside a chunk (+64 i)
+    const size_t ents = (size_t)p.nOffPad * kG;
+    double* __restrict__ RX = p.slab + (size_t)blockIdx.x * 5 * ents;
+    double* __restrict__ RY = RX + ents;
+    double* __restrict__ F = RY + ents;
+    double* __restrict__ J0 = F + ents;
+    double* __restrict__ J1 = J0 + ents;
+    float* __restrict__ I1 = p.slabI1 + (size_t)blockIdx.x * ents;
+    const double cm = (double)p.cmax;
+    const bool chain = tid < kG;  // chain / control lane of slot `tid`
+
+    Ctl ctl;
+    ctl.p = &p;
+    ctl.F = F;
+    ctl.J0 = J0;
+    ctl.J1 = J1;
+    ctl.eps = sqrt(p.epsfcn > kEpsmch ? p.epsfcn : kEpsmch);
+    ctl.cnt_eval = 0;
+    ctl.cnt_pix = 0;
+    if (chain) ctl_fetch(ctl, ss[tid], sp[tid]);
+
+    // chain accumulators (chain lanes)
+    Enorm en;
+    en.init(1);
+    double sumA = 0., sumB = 0.;
 
     long long iterations = 0;
+    const unsigned long long tStart = wall_clock64();
+    if (tid == 0) shStop = 0;
     for (;;) {
-        if (++iterations > p.maxIter) {  // cannot happen for a correct state machine; never hang the GPU
-            if (lane == 0) atomicExch(p.overflow, 1);
-            break;
+        if (tid == 0 && (++iterations > p.maxIter || (long long)(wall_clock64() - tStart) > p.maxTicks)) {
+            // cannot happen for a correct state machine; never hang the GPU
+            shStop = 1;
+            atomicExch(p.overflow, 1);
         }
-        // ---------------- fetch points ----------------
-        if (st == S_NEED_POINT) {
-            pidx = atomicAdd(p.queue, 1);
-            if (pidx >= p.P) {
-                st = S_DONE;
-            } else {
-                X0 = p.points[3 * pidx + 0];
-                X1 = p.points[3 * pidx + 1];
-                X2 = p.points[3 * pidx + 2];
-                // extractPixelsContour(Vec3d) (:376-397): project with r = t = 0
-                project1(p.cam, Ident, Zero, X0, X1, X2, ccx, ccy);
-                for (int l = 0; l < 8; l++) {
-                    p.info[8 * pidx + l] = 0;
-                    p.nfev[8 * pidx + l] = 0;
-                }
-                st = S_INIT;
-            }
+        if (chain) {
+            shCnt[tid] = 0;
+            shKmin[tid] = 0x7fffffff;
+            shFail[tid] = 0x7fffffff;
+            shPh3[tid] = 0;
+            shI1fail[tid] = 0;
+            shSlow[tid] = 0;
+            en.init(1);
+            en.agiant = sp[tid].agiant;
+            sumA = 0.;
+            sumB = 0.;
         }
-        if (__all(st == S_DONE)) break;
+        __syncthreads();
+        bool allDone = true;
+        for (int q = 0; q < kG; q++) allDone = allDone && sp[q].pass == P_DONE;
+        if (shStop || allDone) break;
+        // this thread's slot parameters
+        const SlotP& P = sp[slot];  // read from LDS on use (keeps VGPRs for the pixel data)
+        const bool isjac = (P.ekind == E_JAC0 || P.ekind == E_JAC1);
+        double* __restrict__ outArr = P.ekind == E_JAC0 ? J0 : P.ekind == E_JAC1 ? J1 : F;
+        const double* __restrict__ Jp = P.pivot ? J1 : J0;
+        const double* __restrict__ Jq = P.pivot ? J0 : J1;
+        const bool i1ok = ss[slot].i1ok != 0;
 
-        // ---------------- neighbourhood + undistorted rays (once per point) ----------------
-        if (__any(st == S_INIT)) {
-            const bool act = (st == S_INIT);
-            int cnt = 0, kf = -1, ks = -1;
-            for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
+        for (int k0 = 0; k0 < p.nOffPad; k0 += kC) {
+            // ---------------- parallel terms of this chunk ----------------
+            if (P.pass == P_EVAL) {
+#pragma unroll 1
+                for (int i0 = 0; i0 < kPer; i0 += kSub) {
+                    double rx[kSub], ry[kSub], fk[kSub];
+                    float i1v[kSub];
+                    bool valid[kSub];
 #pragma unroll
-                for (int c = 0; c < kCh; c++) {
-                    const int k = k0 + c;
-                    const int2 o2 = p.offsets[k];
-                    if (act) {
-                        // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH)
-                        double px = ccx + (double)o2.x, py = ccy + (double)o2.y;
-                        const size_t o = (size_t)k * kWave + lane;
-                        if (px < 0 || py < 0 || px >= p.boundW || py >= p.boundH) {
-                            RX[o] = __builtin_nan("");
-                        } else {
-                            double ux, uy;
-                            undistort1(p.cam, px, py, ux, uy);
-                            RX[o] = ux;
-                            RY[o] = uy;
-                            if (kf < 0)
-                                kf = k;
-                            else if (ks < 0)
-                                ks = k;
-                            cnt++;
-                        }
+                    for (int i = 0; i < kSub; i++) {
+                        const int k = k0 + prow + 64 * (i0 + i);
+                        const size_t e = (size_t)k * kG + slot;
+                        const int2 o2 = p.offsets[k];
+                        const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
+                        valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+                        rx[i] = RX[e];
+                        ry[i] = RY[e];
+                        i1v[i] = I1[e];
+                        fk[i] = isjac ? F[e] : 0.;
                     }
-                }
-            }
-            if (act) {
-                m = cnt;
-                kfirst = kf;
-                ksecond = ks;
-                // initial guess: X / norm(X) == X * (1/norm) (Vec3d operator/)
-                double nr = sqrt(X0 * X0 + X1 * X1 + X2 * X2);
-                double inv = 1. / nr;
-                nrm0 = X0 * inv;
-                nrm1 = X1 * inv;
-                nrm2 = X2 * inv;
-                if (m <= 0) {
-                    finish_point(FM3D_ST_NO_PIXELS);
-                } else {
-                    L = p.levels;
-                    st = S_LEVEL;
-                }
-            }
-        }
-
-        // ---------------- level start: image-1 intensities, car2sph, lmdif init ----------------
-        if (__any(st == S_LEVEL)) {
-            const bool act = (st == S_LEVEL);
-            if (act) {
-                lv = p.lvl[L];
-                scale = ldexp(1.0, -L);  // 1.0 / float(2^L)  (optimize_pyramid, :225-241)
-                i1ok = true;
-            }
-            for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
-                double rx[kCh];
-                const uint8_t* g[kCh];
-                float fx[kCh], fy[kCh];
-                bool use[kCh];
+                    unsigned char code1[kSub];
+                    float fx[kSub], fy[kSub];
+                    const uint8_t* g[kSub];
 #pragma unroll
-                for (int c = 0; c < kCh; c++) rx[c] = RX[(size_t)(k0 + c) * kWave + lane];
-#pragma unroll
-                for (int c = 0; c < kCh; c++) {
-                    const int2 o2 = p.offsets[k0 + c];
-                    double px = ccx + (double)o2.x, py = ccy + (double)o2.y;
-                    bool valid = act && (rx[c] == rx[c]);
-                    bool good = pixel_good(px, py, scale, lv.w, lv.h);
-                    if (valid && !good) i1ok = false;  // updateImage1PixelsIntensity (:580-584)
-                    use[c] = valid && good;
-                    fx[c] = (float)(scale * px);
-                    fy[c] = (float)(scale * py);
-                    g[c] = use[c] ? lv.img1 + (long)(int)floor((double)fy[c]) * lv.w + (int)floor((double)fx[c])
-                                  : lv.img1;
-                }
-                uint8_t b00[kCh], b01[kCh], b10[kCh], b11[kCh];
-#pragma unroll
-                for (int c = 0; c < kCh; c++) {
-                    b00[c] = g[c][0];
-                    b01[c] = g[c][1];
-                    b10[c] = g[c][lv.w];
-                    b11[c] = g[c][lv.w + 1];
-                }
-#pragma unroll
-                for (int c = 0; c < kCh; c++) {
-                    if (use[c]) I1[(size_t)(k0 + c) * kWave + lane] = bilinear4(b00[c], b01[c], b10[c], b11[c], fx[c], fy[c]);
-                }
-            }
-            if (act) {
-                // car2sph (tools.cpp:767-771)
-                s.x[1] = fm3d_atan2(nrm2, sqrt(nrm0 * nrm0 + nrm1 * nrm1));
-                s.x[0] = fm3d_atan2(nrm1, nrm0);
-                s.nfev = 0;
-                s.iter = 1;
-                s.par = 0.;
-                s.delta = 0.;
-                s.xnorm = 0.;
-                if (m < 2)
-                    level_done(0);  // lmdif: m < n -> improper input, info 0, no evaluation
-                else
-                    request_eval(E_INITIAL, s.x[0], s.x[1]);
-            }
-        }
-
-        // ---------------- one residual evaluation per lane ----------------
-        if (__any(st == S_EVAL)) {
-            const bool act = (st == S_EVAL);
-            double n0 = 0, n1 = 0, n2 = 0, mm = 0, w = 1.0, hj = 1.0;
-            int fail = 0, ph1 = 0;
-            bool ph3 = false;
-            Enorm en;
-            en.init(m > 0 ? m : 1);
-            double* __restrict__ out = F;
-            const bool isjac = (ekind == E_JAC0 || ekind == E_JAC1);
-            if (act) {
-                s.nfev++;
-                cnt_eval++;
-                cnt_pix += m;
-                sph2car_det(ex0, ex1, n0, n1, n2);  // par = (phi, theta)
-                if (n2 != n2 || n1 != n1 || n0 != n0) fail = FM3D_ST_NAN_NORMAL;
-                mm = n0 * X0 + n1 * X1 + n2 * X2;
-                double w_theta = 1.0, w_phi = 1.0;
-                if (fabs(ex1) - M_PI / 2 > 0 || fabs(ex0) - M_PI > 0) {
-                    w_theta = fm3d_exp(fabs(ex1) - M_PI / 2) + 1;
-                    w_phi = fm3d_exp(fabs(ex0) - M_PI + 1) + 1;
-                }
-                w = w_phi * w_theta;
-                if (ekind == E_JAC0) {
-                    hj = s.h[0];
-                    out = J0;
-                } else if (ekind == E_JAC1) {
-                    hj = s.h[1];
-                    out = J1;
-                }
-            }
-            const bool run = act && fail == 0;
-            if (__any(run)) {
-                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
-                    double rx[kCh], ry[kCh], fk[kCh];
-                    float i1[kCh];
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        const size_t o = (size_t)(k0 + c) * kWave + lane;
-                        rx[c] = RX[o];
-                        ry[c] = RY[o];
-                        i1[c] = I1[o];
-                        fk[c] = F[o];
-                    }
-                    // geometry: projectPointToPlane (:421-470), isInBoundingBox (:646-655),
-                    // projectPointsToImage2 (:591-644)
-                    unsigned char code1[kCh];  // 0 ok, 1 invalid pixel, 2 NaN plane, 3 bbox
-                    bool good[kCh];
-                    float fx[kCh], fy[kCh];
-                    const uint8_t* g[kCh];
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        const double ux = rx[c], uy = ry[c];
-                        double nn = n0 * ux + n1 * uy + n2 * 1.;
-                        double kk = mm / nn;
+                    for (int i = 0; i < kSub; i++) {
+                        // projectPointToPlane (:421-470) + isInBoundingBox (:646-655)
+                        const double ux = rx[i], uy = ry[i];
+                        double nn = P.n0 * ux + P.n1 * uy + P.n2 * 1.;
+                        double kk = P.mm / nn;
                         double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
                         unsigned char cd = 0;
-                        if (ux != ux)
+                        if (!valid[i])
                             cd = 1;
                         else if (P0 != P0 || P1 != P1 || P2 != P2)
                             cd = 2;
                         else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
                             cd = 3;
-                        code1[c] = cd;
+                        // projectPointsToImage2 (:591-644)
                         double u, v;
                         project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
-                        bool gd = (cd == 0) && pixel_good(u, v, scale, lv.w, lv.h);
-                        good[c] = gd;
-                        fx[c] = (float)(scale * u);
-                        fy[c] = (float)(scale * v);
-                        g[c] = gd ? lv.img2 + (long)(int)floor((double)fy[c]) * lv.w + (int)floor((double)fx[c])
-                                  : lv.img2;
+                        if (cd == 0 && !pixel_good(u, v, P.scale, P.lw, P.lh)) cd = 4;
+                        code1[i] = cd;
+                        fx[i] = (float)(P.scale * u);
+                        fy[i] = (float)(P.scale * v);
+                        g[i] = cd == 0 ? P.img2 + (long)(int)floor((double)fy[i]) * P.lw + (int)floor((double)fx[i])
+                                       : P.img2;
                     }
-                    uint8_t b00[kCh], b01[kCh], b10[kCh], b11[kCh];
+                    uint8_t b00[kSub], b01[kSub], b10[kSub], b11[kSub];
 #pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        b00[c] = g[c][0];
-                        b01[c] = g[c][1];
-                        b10[c] = g[c][lv.w];
-                        b11[c] = g[c][lv.w + 1];
+                    for (int i = 0; i < kSub; i++) {
+                        b00[i] = g[i][0];
+                        b01[i] = g[i][1];
+                        b10[i] = g[i][P.lw];
+                        b11[i] = g[i][P.lw + 1];
                     }
-                    // residuals in pixel order (evaluateNormal :145-148 / fdjac2)
 #pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        if (run && ph1 == 0 && code1[c] != 1) {
-                            if (code1[c] == 2) {
-                                ph1 = FM3D_ST_NAN_PLANE;
-                            } else if (code1[c] == 3) {
-                                ph1 = FM3D_ST_ABORT_BBOX;
-                            } else if (i1ok && !ph3) {
-                                if (!good[c]) {
-                                    ph3 = true;
-                                } else {
-                                    float I2 = bilinear4(b00[c], b01[c], b10[c], b11[c], fx[c], fy[c]);
-                                    float dI = i1[c] - I2;
-                                    double r = w * (double)dI;
-                                    double val = r;
-                                    if (isjac) val = (r - fk[c]) / hj;
-                                    out[(size_t)(k0 + c) * kWave + lane] = val;
-                                    en.add(val);
+                    for (int i = 0; i < kSub; i++) {
+                        const int pl = prow + 64 * (i0 + i);
+                        const int k = k0 + pl;
+                        double t1 = 0., t2 = __builtin_nan("");
+                        if (code1[i] == 2 || code1[i] == 3) {
+                            atomicMin(&shFail[slot], k * 4 + code1[i]);  // first failing pixel decides
+                        } else if (code1[i] == 4) {
+                            shPh3[slot] = 1;
+                        } else if (code1[i] == 0 && i1ok) {
+                            float I2 = bilinear4(b00[i], b01[i], b10[i], b11[i], fx[i], fy[i]);
+                            float dI = i1v[i] - I2;
+                            double r = P.w * (double)dI;                    // evaluateNormal :145-148
+                            double val = isjac ? (r - fk[i]) / P.hj : r;  // fdjac2 forward difference
+                            outArr[(size_t)k * kG + slot] = val;
+                            t1 = enorm_term(val, P.agiant, &shSlow[slot]);
+                            t2 = val;
+                        }
+                        term[0][slot][pl] = t1;
+                        term[1][slot][pl] = t2;
+                    }
+                }
+            } else if (P.pass == P_QR1 || P.pass == P_QR2 || P.pass == P_QR3) {
+#pragma unroll 1
+                for (int i0 = 0; i0 < kPer; i0 += kSub) {
+                    double ap[kSub], aq[kSub], fv[kSub];
+                    bool valid[kSub];
+#pragma unroll
+                    for (int i = 0; i < kSub; i++) {
+                        const int k = k0 + prow + 64 * (i0 + i);
+                        const size_t e = (size_t)k * kG + slot;
+                        const int2 o2 = p.offsets[k];
+                        const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
+                        valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+                        ap[i] = Jp[e];
+                        aq[i] = Jq[e];
+                        fv[i] = P.pass == P_QR2 ? 0. : F[e];
+                    }
+#pragma unroll
+                    for (int i = 0; i < kSub; i++) {
+                        const int pl = prow + 64 * (i0 + i);
+                        const int k = k0 + pl;
+                        double t1 = __builtin_nan(""), t2 = __builtin_nan("");
+                        if (P.pass == P_QR1) {
+                            // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); sum v*a_q, sum v*f
+                            if (valid[i]) {
+                                double v = ap[i] / P.ajn0s;
+                                if (k == P.kfirst) v = v + 1.;
+                                t1 = v * aq[i];
+                                t2 = v * fv[i];
+                            }
+                        } else if (P.pass == P_QR2) {
+                            // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
+                            t1 = 0.;
+                            if (valid[i] && k > P.kfirst) {
+                                double a = aq[i];
+                                if (P.t0) {
+                                    double v = ap[i] / P.ajn0s;
+                                    a = a - P.tq * v;
                                 }
+                                if (k == P.ksecond) shAqs1[slot] = a;
+                                t1 = enorm_term(a, P.agiant, &shSlow[slot]);
+                                t2 = a;
                             }
-                        }
-                    }
-                }
-            }
-            if (act) {
-                int code = fail ? fail : ph1 ? ph1 : (!i1ok ? FM3D_ST_ABORT_PIX1 : (ph3 ? FM3D_ST_ABORT_PIX2 : 0));
-                if (code) {
-                    abort_level(code);
-                } else {
-                    double nrm = en.finish();
-                    if (ekind == E_INITIAL) {
-                        s.fnorm = nrm;
-                        s.h[0] = eps * fabs(s.x[0]);
-                        if (s.h[0] == 0.) s.h[0] = eps;
-                        request_eval(E_JAC0, s.x[0] + s.h[0], s.x[1]);
-                    } else if (ekind == E_JAC0) {
-                        s.acnorm[0] = nrm;
-                        s.h[1] = eps * fabs(s.x[1]);
-                        if (s.h[1] == 0.) s.h[1] = eps;
-                        request_eval(E_JAC1, s.x[0], s.x[1] + s.h[1]);
-                    } else if (ekind == E_JAC1) {
-                        s.acnorm[1] = nrm;
-                        st = S_QR;
-                    } else {
-                        bool accepted;
-                        int info = lm_after_trial(s, nrm, &accepted);
-                        if (info) {
-                            level_done(info);
-                        } else if (accepted) {
-                            s.h[0] = eps * fabs(s.x[0]);
-                            if (s.h[0] == 0.) s.h[0] = eps;
-                            request_eval(E_JAC0, s.x[0] + s.h[0], s.x[1]);
                         } else {
-                            lm_inner_step(s);
-                            request_eval(E_TRIAL, s.wa2[0], s.wa2[1]);
-                        }
-                    }
-                }
-            }
-        }
-
-        // ---------------- Householder QR (qrfac, pivoting) + Q^T fvec, n = 2 ----------------
-        if (__any(st == S_QR)) {
-            const bool act = (st == S_QR);
-            int pc = 0;
-            double ajn0 = 0, ajn0s = 1, apf = 0, aqf = 0, ff = 0, aps = 0, fs = 0, vfirst = 0;
-            const double* Jp = J0;
-            const double* Jq = J1;
-            bool t0 = false;
-            if (act) {
-                pc = (s.acnorm[1] > s.acnorm[0]) ? 1 : 0;
-                s.ipvt[0] = pc;
-                s.ipvt[1] = 1 - pc;
-                Jp = pc ? J1 : J0;
-                Jq = pc ? J0 : J1;
-                ajn0 = s.acnorm[pc];  // enorm of the pivot column == its acnorm (same elements, same order)
-                const size_t of = (size_t)kfirst * kWave + lane, os = (size_t)ksecond * kWave + lane;
-                apf = Jp[of];
-                aqf = Jq[of];
-                ff = F[of];
-                aps = Jp[os];
-                fs = F[os];
-                t0 = (ajn0 != 0.);
-                ajn0s = (t0 && apf < 0.) ? -ajn0 : ajn0;
-                if (!t0) ajn0s = 1.;  // unused
-                vfirst = t0 ? (apf / ajn0s) + 1. : apf;
-            }
-            // P1: sum_i v_i a_q[i] (qrfac) and sum_i v_i f[i] (lmdif qtf, j = 0)
-            double dot = 0., s0 = 0.;
-            const bool run1 = act && t0;
-            if (__any(run1)) {
-                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
-                    double rx[kCh], ap[kCh], aq[kCh], fk[kCh];
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        const size_t o = (size_t)(k0 + c) * kWave + lane;
-                        rx[c] = RX[o];
-                        ap[c] = Jp[o];
-                        aq[c] = Jq[o];
-                        fk[c] = F[o];
-                    }
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        if (run1 && rx[c] == rx[c]) {
-                            double v = ap[c] / ajn0s;
-                            if (k0 + c == kfirst) v = v + 1.;
-                            dot += v * aq[c];
-                            s0 += v * fk[c];
-                        }
-                    }
-                }
-            }
-            double tq = 0., r01 = aqf, tq0 = 0., qtf0 = ff;
-            bool q0 = false;
-            if (act) {
-                if (t0) {
-                    tq = dot / vfirst;
-                    r01 = aqf - tq * vfirst;
-                }
-                q0 = (vfirst != 0.);
-                if (q0) {
-                    tq0 = -s0 / vfirst;
-                    qtf0 = ff + vfirst * tq0;
-                }
-            }
-            // P2: ajnorm of the transformed second column, elements 1..m-1
-            Enorm e2;
-            e2.init(m > 1 ? m - 1 : 1);
-            double aqs1 = 0.;
-            if (__any(act)) {
-                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
-                    double rx[kCh], ap[kCh], aq[kCh];
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        const size_t o = (size_t)(k0 + c) * kWave + lane;
-                        rx[c] = RX[o];
-                        ap[c] = Jp[o];
-                        aq[c] = Jq[o];
-                    }
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        const int k = k0 + c;
-                        if (act && k > kfirst && rx[c] == rx[c]) {
-                            double a = aq[c];
-                            if (t0) {
-                                double v = ap[c] / ajn0s;
-                                a = a - tq * v;
+                            // lmdif qtf, j = 1: u_i * wa4_i
+                            if (valid[i] && k > P.kfirst) {
+                                double v = P.t0 ? ap[i] / P.ajn0s : 0.;
+                                double a = aq[i];
+                                if (P.t0) a = a - P.tq * v;
+                                double u = P.t1 ? a / P.ajn1s : a;
+                                if (P.t1 && k == P.ksecond) u = u + 1.;
+                                double wa = fv[i];
+                                if (P.q0) wa = wa + v * P.tq0;
+                                t1 = u * wa;
                             }
-                            e2.add(a);
-                            if (k == ksecond) aqs1 = a;
+                        }
+                        term[0][slot][pl] = t1;
+                        term[1][slot][pl] = t2;
+                    }
+                }
+            } else if (P.pass == P_INIT) {
+#pragma unroll 1
+                for (int i = 0; i < kPer; i++) {
+                    const int k = k0 + prow + 64 * i;
+                    const size_t e = (size_t)k * kG + slot;
+                    const int2 o2 = p.offsets[k];
+                    // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH)
+                    const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
+                    if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
+                        double ux, uy;
+                        undistort1(p.cam, px, py, ux, uy);  // get3dPointsFromImage1Pixels :542
+                        RX[e] = ux;
+                        RY[e] = uy;
+                        atomicAdd(&shCnt[slot], 1);
+                        atomicMin(&shKmin[slot], k);
+                    }
+                }
+            } else if (P.pass == P_LEVEL) {
+#pragma unroll 1
+                for (int i = 0; i < kPer; i++) {
+                    const int k = k0 + prow + 64 * i;
+                    const size_t e = (size_t)k * kG + slot;
+                    const int2 o2 = p.offsets[k];
+                    const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
+                    if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
+                        // updateImage1PixelsIntensity (:576-589)
+                        if (!pixel_good(px, py, P.scale, P.lw, P.lh)) {
+                            shI1fail[slot] = 1;
+                        } else {
+                            const float fx = (float)(P.scale * px), fy = (float)(P.scale * py);
+                            const uint8_t* g = P.img1 + (long)(int)floor((double)fy) * P.lw + (int)floor((double)fx);
+                            I1[e] = bilinear4(g[0], g[1], g[P.lw], g[P.lw + 1], fx, fy);
                         }
                     }
                 }
             }
-            double ajn1 = 0, ajn1s = 1, usecond = 0;
-            bool t1 = false;
-            if (act) {
-                ajn1 = e2.finish();
-                t1 = (ajn1 != 0.);
-                ajn1s = (t1 && aqs1 < 0.) ? -ajn1 : ajn1;
-                if (!t1) ajn1s = 1.;  // unused
-                usecond = t1 ? (aqs1 / ajn1s) + 1. : aqs1;
-            }
-            // P3: lmdif qtf, j = 1: sum_{i>=1} u_i wa4_i
-            double s1 = 0.;
-            const bool run3 = act && usecond != 0.;
-            if (__any(run3)) {
-                for (int k0 = 0; k0 < nOffPad; k0 += kCh) {
-                    double rx[kCh], ap[kCh], aq[kCh], fk[kCh];
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        const size_t o = (size_t)(k0 + c) * kWave + lane;
-                        rx[c] = RX[o];
-                        ap[c] = Jp[o];
-                        aq[c] = Jq[o];
-                        fk[c] = F[o];
-                    }
-#pragma unroll
-                    for (int c = 0; c < kCh; c++) {
-                        const int k = k0 + c;
-                        if (run3 && k > kfirst && rx[c] == rx[c]) {
-                            double v = t0 ? ap[c] / ajn0s : 0.;
-                            double a = aq[c];
-                            if (t0) a = a - tq * v;
-                            double u = t1 ? a / ajn1s : a;
-                            if (t1 && k == ksecond) u = u + 1.;
-                            double wa = fk[c];
-                            if (q0) wa = wa + v * tq0;
-                            s1 += u * wa;
+            __syncthreads();
+            // ---------------- sequential sums in MINPACK's pixel order ----------------
+            if (chain) {
+                const int ps = sp[tid].pass;
+                const double* tA = term[0][tid];
+                const double* tB = term[1][tid];
+                if (ps == P_EVAL || ps == P_QR2) {
+                    if (!shSlow[tid]) {
+                        double s2 = en.s2;
+#pragma unroll 16
+                        for (int q = 0; q < kC; q++) s2 += tA[q];
+                        en.s2 = s2;
+                    } else {
+                        for (int q = 0; q < kC; q++) {
+                            const double x = tB[q];
+                            if (x == x) en.add(x);
                         }
                     }
+                    shSlow[tid] = 0;  // ordered before the next chunk by the barrier below
+                } else if (ps == P_QR1) {
+#pragma unroll 8
+                    for (int q = 0; q < kC; q++) {
+                        const double a = tA[q], b = tB[q];
+                        if (a == a) {
+                            sumA += a;
+                            sumB += b;
+                        }
+                    }
+                } else if (ps == P_QR3) {
+#pragma unroll 8
+                    for (int q = 0; q < kC; q++) {
+                        const double a = tA[q];
+                        if (a == a) sumA += a;
+                    }
                 }
             }
-            if (act) {
-                double wa4s = q0 ? fs + (aps / ajn0s) * tq0 : fs;
-                double qtf1 = wa4s;
-                if (usecond != 0.) {
-                    double tq1 = -s1 / usecond;
-                    qtf1 = wa4s + usecond * tq1;
-                }
-                s.r[0] = t0 ? -ajn0s : 0.;
-                s.r[1] = 0.;
-                s.r[2] = r01;
-                s.r[3] = t1 ? -ajn1s : 0.;
-                s.qtf[0] = qtf0;
-                s.qtf[1] = qtf1;
-                int info = lm_after_qr(s);
-                if (info) {
-                    level_done(info);
-                } else {
-                    lm_inner_step(s);
-                    request_eval(E_TRIAL, s.wa2[0], s.wa2[1]);
-                }
-            }
+            __syncthreads();
+        }
+
+        // ---------------- per-slot lmdif bookkeeping ----------------
+        if (chain) {
+            PassOut o;
+            o.nrm = en.finish();
+            o.sumA = sumA;
+            o.sumB = sumB;
+            o.aqs1 = shAqs1[tid];
+            o.cnt = shCnt[tid];
+            o.kmin = shKmin[tid];
+            o.fail = shFail[tid];
+            o.ph3 = shPh3[tid];
+            o.i1fail = shI1fail[tid];
+            ctl.after_pass(ss[tid], sp[tid], o, tid);
         }
     }
 
-    // statistics: one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) {
-        cnt_eval += __shfl_down(cnt_eval, off);
-        cnt_pix += __shfl_down(cnt_pix, off);
-    }
-    if (lane == 0) {
-        atomicAdd(p.statEval, (unsigned long long)cnt_eval);
-        atomicAdd(p.statPix, (unsigned long long)cnt_pix);
+    if (chain) {
+        atomicAdd(p.statEval, (unsigned long long)ctl.cnt_eval);
+        atomicAdd(p.statPix, (unsigned long long)ctl.cnt_pix);
     }
 }
 
