@@ -81,11 +81,16 @@ RECORD = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("distance", "<f4")
 
 class LMStats(ctypes.Structure):
     _fields_ = [("points_in", ctypes.c_int64), ("points_kept", ctypes.c_int64), ("evaluations", ctypes.c_int64),
-                ("pixel_evaluations", ctypes.c_int64), ("drops", ctypes.c_int64 * 8), ("kernel_ms", ctypes.c_double)]
+                ("pixel_evaluations", ctypes.c_int64), ("drops", ctypes.c_int64 * 8), ("kernel_ms", ctypes.c_double),
+                ("groups", ctypes.c_int64), ("passes", ctypes.c_int64), ("cycles_terms", ctypes.c_int64),
+                ("cycles_chain", ctypes.c_int64), ("cycles_control", ctypes.c_int64), ("cycles_total", ctypes.c_int64),
+                ("wall_ticks_sum", ctypes.c_int64), ("wall_ticks_max", ctypes.c_int64),
+                ("wall_clock_khz", ctypes.c_int64)]
 
     def as_dict(self):
-        return {"points_in": self.points_in, "points_kept": self.points_kept, "evaluations": self.evaluations,
-                "pixel_evaluations": self.pixel_evaluations, "drops": list(self.drops), "kernel_ms": self.kernel_ms}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["drops"] = list(self.drops)
+        return d
 
 
 class PipelineStats(ctypes.Structure):

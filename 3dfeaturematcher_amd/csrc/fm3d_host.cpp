@@ -71,6 +71,8 @@ struct fm3d_ctx {
     // work buffers
     DevBuf A, B, cqA, ctB, idx, key, fkey, knnOut, cand, flag, matches, count, scanTmp;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
+    long lmGroups = 0;
+    int wallKhz = 0;
     DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, slab, slabI1;
     DevBuf records, recTmp, recFlag;
     // staged pipeline inputs
@@ -362,6 +364,18 @@ int ensure_scan_tmp(fm3d_ctx* c, int n) {
     return FM3D_OK;
 }
 
+void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_stats* st) {
+    st->groups = c->lmGroups;
+    st->passes = (int64_t)cnt[3];
+    st->cycles_terms = (int64_t)cnt[4];
+    st->cycles_chain = (int64_t)cnt[5];
+    st->cycles_control = (int64_t)cnt[6];
+    st->cycles_total = (int64_t)cnt[7];
+    st->wall_ticks_sum = (int64_t)cnt[8];
+    st->wall_ticks_max = (int64_t)cnt[9];
+    st->wall_clock_khz = c->wallKhz;
+}
+
 // LM normals over nPts device points (c->pts), outputs in c->lm*
 int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
     int r;
@@ -375,7 +389,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     HIPCHK(c, c->lmNfev.ensure((size_t)(P + 1) * 8 * sizeof(int)));
     HIPCHK(c, c->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
     HIPCHK(c, c->lmQueue.ensure(64));
-    HIPCHK(c, c->lmStat.ensure(64));
+    HIPCHK(c, c->lmStat.ensure(128));
     // persistent workgroups of fm3d::kLMSlots points each; slots refill from the queue
     long groups = c->s.lmWaves;
     if (groups <= 0) {
@@ -399,7 +413,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     HIPCHK(c, c->slab.ensure(ents * 5 * sizeof(double) * groups));
     HIPCHK(c, c->slabI1.ensure(ents * sizeof(float) * groups));
     HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 128, c->stream));
     fm3d::LMParams p{};
     p.points = c->pts.as<double>();
     p.P = P;
@@ -427,6 +441,8 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     p.statEval = c->lmStat.as<unsigned long long>();
     p.statPix = c->lmStat.as<unsigned long long>() + 1;
     p.overflow = (int*)(c->lmStat.as<unsigned long long>() + 2);
+    p.statPass = c->lmStat.as<unsigned long long>() + 3;
+    c->lmGroups = groups;
     {   // guards against a broken state machine (never expected to trigger): main-loop passes per
         // group <= its points x levels x (300 evaluations + QR passes), and a wall-clock limit
         long long perGroup = (P + groups - 1) / groups + 1;
@@ -435,6 +451,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         HIPCHK(c, hipGetDevice(&dev));
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
         p.maxTicks = (long long)khz * 1000 * 300;  // 300 s
+        c->wallKhz = khz;
     }
     if (P > 0) {
         HIPCHK(c, hipEventRecord(e0, c->stream));
@@ -710,7 +727,7 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
     if ((r = run_lm(c, P, stats, c->ev[0], c->ev[1]))) return r;
     std::vector<double> nrm((size_t)P * 3);
     std::vector<int> st(P), inf((size_t)P * 8), nf((size_t)P * 8);
-    unsigned long long cnt[2] = {0, 0};
+    unsigned long long cnt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (P) {
         HIPCHK(c, hipMemcpyAsync(nrm.data(), c->lmNormals.p, nrm.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(st.data(), c->lmStatus.p, st.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -749,6 +766,7 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
         for (int i = 0; i < P; i++)
             if (st[i] >= 0 && st[i] < 8) stats->drops[st[i]]++;
         stats->kernel_ms = ms;
+        fill_lm_cycles(c, cnt, stats);
     }
     if (nanPlane && c->s.strictNanExit)
         return fail(c, FM3D_ERR_NAN_PLANE, "projectPointToPlane hit NaN (reference: exit(-6))");
@@ -846,7 +864,7 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
                                  c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
     int kept = 0;
-    unsigned long long cnt[2] = {0, 0};
+    unsigned long long cnt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     HIPCHK(c, hipMemcpyAsync(&kept, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -878,6 +896,7 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
         stats->lm.evaluations = (int64_t)cnt[0];
         stats->lm.pixel_evaluations = (int64_t)cnt[1];
         stats->lm.kernel_ms = stats->lm_ms;
+        fill_lm_cycles(c, cnt, &stats->lm);
     }
     return FM3D_OK;
 }

@@ -41,10 +41,12 @@ struct LMParams {
     long long maxIter;       // safety bound on main-loop passes per workgroup
     long long maxTicks;      // safety bound on wall-clock ticks per workgroup
     int* overflow;           // set to 1 if a workgroup hit a guard
+    // [passes, cycles terms, cycles chain, cycles control, cycles total, wall ticks sum, wall ticks max]
+    unsigned long long* statPass;
 };
 
 constexpr int kLMSlots = 4;     // points per LM workgroup
-constexpr int kLMThreads = 256;
+constexpr int kLMThreads = 320;  // 4 term waves + 1 chain wave
 constexpr int kLMChunk = 512;   // pixels per LM chunk (offsets are padded to a multiple)
 
 __global__ void lm_kernel(LMParams p);

@@ -12,17 +12,20 @@
 // points (measured with the oracle).  So every sum is replayed in
 // MINPACK's pixel order, bit for bit -- but only the ADDS are sequential:
 //
-//   * a workgroup (256 threads) serves kG = 4 points ("slots");
-//   * each pass over the neighbourhood runs in chunks of kC pixels: all 256
-//     threads compute the per-(pixel, slot) terms in parallel -- the residual
-//     (plane intersection, distorted projection, bilinear samples), Jacobian
-//     columns, Householder products -- and park them in LDS;
-//   * one "chain" lane per slot (lanes 0..3 of wave 0) then adds the chunk's
-//     terms in pixel order (MINPACK enorm / dot-product order) and runs the
-//     slot's lmdif bookkeeping between passes;
+//   * a workgroup serves kG = 4 points ("slots") with 4 "term" waves and one
+//     "chain" wave;
+//   * a pass over the neighbourhood (one residual evaluation, the two-column
+//     forward-difference Jacobian, or one Householder product) runs in chunks
+//     of kC pixels.  The term waves compute every (slot, pixel) term of a chunk
+//     in parallel -- plane intersection, distorted projection, bilinear
+//     samples, Jacobian columns, Householder products -- into a double-buffered
+//     LDS tile, while the chain wave adds the previous chunk's terms in pixel
+//     order (one lane per slot and sum: MINPACK's enorm / dot-product order);
+//   * between passes the chain lanes run the slot's lmdif bookkeeping;
 //   * per-pixel state (undistorted rays, I1, fvec, Jacobian) lives in a
-//     per-workgroup slab laid out [pixel][slot] (coalesced 2 KB per load
-//     instruction); slots fetch new points from a global queue.
+//     per-workgroup slab [array][slot][pixel]; a wave always works on one slot,
+//     so its loads are contiguous 512-byte rows and its branch is uniform, and
+//     idle slots hand their share of the term waves to the busy ones.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
@@ -35,8 +38,9 @@ namespace fm3d {
 namespace {
 
 
-enum LaneState { S_NEED_POINT = 0, S_INIT, S_LEVEL, S_EVAL, S_QR, S_DONE };
-enum EvalKind { E_INITIAL = 0, E_JAC0, E_JAC1, E_TRIAL };
+// E_JAC evaluates both forward-difference columns (fdjac2's j = 0 and j = 1
+// calls) in one pass: they are independent evaluations at (x0+h0, x1), (x0, x1+h1).
+enum EvalKind { E_INITIAL = 0, E_JAC, E_TRIAL };
 
 constexpr double kEpsmch = DBL_EPSILON;
 constexpr double kDwarf = DBL_MIN;
@@ -308,18 +312,24 @@ __device__ inline void sph2car_det(double phi, double theta, double& n0, double&
 
 }  // namespace
 
-constexpr int kG = kLMSlots;                  // points (slots) per workgroup
-constexpr int kThreads = kLMThreads;
-constexpr int kC = kLMChunk;                  // pixels per chunk
-constexpr int kPer = kC * kG / kThreads;      // entries per thread per chunk (8)
-constexpr int kSub = 4;                       // entries in flight per thread (register budget)
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) const long long gi64;  // an int2 offset (x low, y high)
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+
+constexpr int kG = kLMSlots;                   // points (slots) per workgroup
+constexpr int kTermThreads = kLMThreads - 64;  // 4 term waves; the last wave is the chain wave
+constexpr int kC = kLMChunk;                   // pixels per chunk
+constexpr int kPairs = kC / kTermThreads;      // entries per thread per (slot, chunk) (2)
+static_assert(kC % kTermThreads == 0 && kC % 64 == 0, "chunk must tile the term waves");
 
 enum PassKind { P_IDLE = 0, P_INIT, P_LEVEL, P_EVAL, P_QR1, P_QR2, P_QR3, P_DONE };
 
 // parameters of a slot's current pass (LDS; written by the slot's chain lane)
 struct SlotP {
-    int pass, ekind, kfirst, ksecond, t0, t1, q0, pivot, lw, lh;
-    double n0, n1, n2, mm, w, hj, scale, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant;
+    int pass, ekind, nev, kfirst, ksecond, t0, t1, q0, pivot, lw, lh;
+    double n0[2], n1[2], n2[2], mm[2], w[2], hj[2];
+    double scale, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant;
     const uint8_t* img1;
     const uint8_t* img2;
 };
@@ -329,24 +339,24 @@ struct SlotS {
     LM s;
     double X0, X1, X2, ccx, ccy, nrm0, nrm1, nrm2;
     double apf, aqf, ff, aps, fs, vfirst, r01, tq0, qtf0, wa4s, usecond, ajn0s, tq, ajn1s;
-    int pidx, m, kfirst, ksecond, L, i1ok, ekind, t0, q0, t1;
+    int pidx, m, kfirst, ksecond, L, i1ok, ekind, t0, q0, t1, bNaN;
 };
 
-// per-pass results the chain lane hands to the bookkeeping
+// per-pass results the chain lanes hand to the bookkeeping
 struct PassOut {
-    double nrm;          // EVAL / QR2: enorm of the pass's values
-    double sumA, sumB;   // QR1 / QR3 dot products
+    double nrm[2];       // EVAL (per evaluation) / QR2: enorm of the pass's values
+    double sum[2];       // QR1 (a_q and fvec products) / QR3 dot products
     double aqs1;         // QR2: transformed a_q at the second kept pixel
-    int cnt, kmin, fail, ph3, i1fail;
+    int cnt, kmin, fail[2], ph3[2], i1fail;
 };
 
 // lmdif bookkeeping of one slot (chain lane only).  Kept out of line so that the
 // register budget of the data-parallel part of the kernel is not set by it.
 struct Ctl {
-    const LMParams* p;
-    double* F;
-    double* J0;
-    double* J1;
+    const LMParams* p;  // a private copy: the kernel's own accesses stay on the kernarg segment
+    const double* F;
+    const double* J0;
+    const double* J1;
     double eps;
     long long cnt_eval, cnt_pix;
 
@@ -406,38 +416,61 @@ struct Ctl {
         p->nfev[8 * S.pidx + S.L] = S.s.nfev;
         finish_point(S, P, code);
     }
-    // evaluateNormal (normaloptimizer.cpp:65-149), per-call part
-    __device__ void eval_pass(SlotS& S, SlotP& P, int kind, double a, double b) {
-        S.s.nfev++;
-        cnt_eval++;
-        cnt_pix += S.m;
+    // evaluateNormal (normaloptimizer.cpp:65-149), per-call part, for evaluation slot ev.
+    // Returns false if the normal is NaN (the call aborts before touching a pixel).
+    __device__ bool setup_eval(SlotS& S, SlotP& P, int ev, double a, double b, double hj) {
         double n0, n1, n2;
         sph2car_det(a, b, n0, n1, n2);  // par = (phi, theta)
-        if (n2 != n2 || n1 != n1 || n0 != n0) {
-            abort_level(S, P, FM3D_ST_NAN_NORMAL);
-            return;
-        }
+        if (n2 != n2 || n1 != n1 || n0 != n0) return false;
         double w_theta = 1.0, w_phi = 1.0;
         if (fabs(b) - M_PI / 2 > 0 || fabs(a) - M_PI > 0) {
             w_theta = fm3d_exp(fabs(b) - M_PI / 2) + 1;
             w_phi = fm3d_exp(fabs(a) - M_PI + 1) + 1;
         }
+        P.n0[ev] = n0;
+        P.n1[ev] = n1;
+        P.n2[ev] = n2;
+        P.mm[ev] = n0 * S.X0 + n1 * S.X1 + n2 * S.X2;
+        P.w[ev] = w_phi * w_theta;
+        P.hj[ev] = hj;
+        return true;
+    }
+    __device__ void count_eval(SlotS& S) {
+        S.s.nfev++;
+        cnt_eval++;
+        cnt_pix += S.m;
+    }
+    __device__ void eval_pass(SlotS& S, SlotP& P, int kind, double a, double b) {
+        count_eval(S);
+        if (!setup_eval(S, P, 0, a, b, 1.0)) {
+            abort_level(S, P, FM3D_ST_NAN_NORMAL);
+            return;
+        }
         S.ekind = kind;
         P.pass = P_EVAL;
         P.ekind = kind;
-        P.n0 = n0;
-        P.n1 = n1;
-        P.n2 = n2;
-        P.mm = n0 * S.X0 + n1 * S.X1 + n2 * S.X2;
-        P.w = w_phi * w_theta;
-        P.hj = kind == E_JAC0 ? S.s.h[0] : kind == E_JAC1 ? S.s.h[1] : 1.0;
+        P.nev = 1;
         P.agiant = 1.304e19 / (double)S.m;
     }
-    __device__ void jac0(SlotS& S, SlotP& P) {
+    // fdjac2: column j = 0 at (x0 + h0, x1), column j = 1 at (x0, x1 + h1)
+    __device__ void jac_pass(SlotS& S, SlotP& P) {
         LM& s = S.s;
         s.h[0] = eps * fabs(s.x[0]);
         if (s.h[0] == 0.) s.h[0] = eps;
-        eval_pass(S, P, E_JAC0, s.x[0] + s.h[0], s.x[1]);
+        s.h[1] = eps * fabs(s.x[1]);
+        if (s.h[1] == 0.) s.h[1] = eps;
+        count_eval(S);
+        if (!setup_eval(S, P, 0, s.x[0] + s.h[0], s.x[1], s.h[0])) {
+            abort_level(S, P, FM3D_ST_NAN_NORMAL);
+            return;
+        }
+        // column 1's call only happens if column 0's succeeds: counted after the pass
+        S.bNaN = !setup_eval(S, P, 1, s.x[0], s.x[1] + s.h[1], s.h[1]);
+        S.ekind = E_JAC;
+        P.pass = P_EVAL;
+        P.ekind = E_JAC;
+        P.nev = S.bNaN ? 1 : 2;
+        P.agiant = 1.304e19 / (double)S.m;
     }
     __device__ void finalize_qr(SlotS& S, SlotP& P, double qtf1) {
         S.s.r[0] = S.t0 ? -S.ajn0s : 0.;
@@ -460,14 +493,14 @@ struct Ctl {
         const int pc = (s.acnorm[1] > s.acnorm[0]) ? 1 : 0;  // pivot column = larger norm
         s.ipvt[0] = pc;
         s.ipvt[1] = 1 - pc;
-        const double* Jpp = pc ? J1 : J0;
-        const double* Jqq = pc ? J0 : J1;
-        const size_t of = (size_t)S.kfirst * kG + slot, os = (size_t)S.ksecond * kG + slot;
-        S.apf = Jpp[of];
-        S.aqf = Jqq[of];
-        S.ff = F[of];
-        S.aps = Jpp[os];
-        S.fs = F[os];
+        const size_t base = (size_t)slot * p->nOffPad;
+        const double* Jpp = (pc ? J1 : J0) + base;
+        const double* Jqq = (pc ? J0 : J1) + base;
+        S.apf = Jpp[S.kfirst];
+        S.aqf = Jqq[S.kfirst];
+        S.ff = F[base + S.kfirst];
+        S.aps = Jpp[S.ksecond];
+        S.fs = F[base + S.ksecond];
         const double ajn0 = s.acnorm[pc];  // == enorm of the pivot column (same elements, same order)
         S.t0 = ajn0 != 0.;
         S.ajn0s = (S.t0 && S.apf < 0.) ? -ajn0 : ajn0;
@@ -493,6 +526,13 @@ struct Ctl {
         P.pass = P_QR2;
         P.tq = S.tq;
         P.agiant = 1.304e19 / (double)(S.m - 1);
+    }
+    __device__ static int fail_code(int fail, int ph3, int i1ok) {
+        if (fail != 0x7fffffff)  // first failing pixel in index order decides (:455-470, :557-560)
+            return (fail & 3) == 2 ? FM3D_ST_NAN_PLANE : FM3D_ST_ABORT_BBOX;
+        if (!i1ok) return FM3D_ST_ABORT_PIX1;
+        if (ph3) return FM3D_ST_ABORT_PIX2;
+        return 0;
     }
 
     __device__ __noinline__ void after_pass(SlotS& S, SlotP& P, const PassOut& o, int slot) {
@@ -538,36 +578,36 @@ struct Ctl {
             else
                 eval_pass(S, P, E_INITIAL, S.s.x[0], S.s.x[1]);
         } else if (ps == P_EVAL) {
-            int code = 0;
-            if (o.fail != 0x7fffffff)  // first failing pixel in index order decides (:455-470, :557-560)
-                code = (o.fail & 3) == 2 ? FM3D_ST_NAN_PLANE : FM3D_ST_ABORT_BBOX;
-            else if (!S.i1ok)
-                code = FM3D_ST_ABORT_PIX1;
-            else if (o.ph3)
-                code = FM3D_ST_ABORT_PIX2;
+            int code = fail_code(o.fail[0], o.ph3[0], S.i1ok);
             if (code) {
                 abort_level(S, P, code);
                 return;
             }
             LM& s = S.s;
             if (S.ekind == E_INITIAL) {
-                s.fnorm = o.nrm;
-                jac0(S, P);
-            } else if (S.ekind == E_JAC0) {
-                s.acnorm[0] = o.nrm;
-                s.h[1] = eps * fabs(s.x[1]);
-                if (s.h[1] == 0.) s.h[1] = eps;
-                eval_pass(S, P, E_JAC1, s.x[0], s.x[1] + s.h[1]);
-            } else if (S.ekind == E_JAC1) {
-                s.acnorm[1] = o.nrm;
+                s.fnorm = o.nrm[0];
+                jac_pass(S, P);
+            } else if (S.ekind == E_JAC) {
+                s.acnorm[0] = o.nrm[0];
+                count_eval(S);  // fdjac2's call for column 1
+                if (S.bNaN) {
+                    abort_level(S, P, FM3D_ST_NAN_NORMAL);
+                    return;
+                }
+                code = fail_code(o.fail[1], o.ph3[1], S.i1ok);
+                if (code) {
+                    abort_level(S, P, code);
+                    return;
+                }
+                s.acnorm[1] = o.nrm[1];
                 start_qr(S, P, slot);
             } else {
                 bool accepted;
-                int info = lm_after_trial(s, o.nrm, &accepted);
+                int info = lm_after_trial(s, o.nrm[0], &accepted);
                 if (info) {
                     level_done(S, P, info);
                 } else if (accepted) {
-                    jac0(S, P);
+                    jac_pass(S, P);
                 } else {
                     lm_inner_step(s);
                     eval_pass(S, P, E_TRIAL, s.wa2[0], s.wa2[1]);
@@ -575,18 +615,18 @@ struct Ctl {
             }
         } else if (ps == P_QR1) {
             // qrfac j = 0: temp = sum v a_q / v_first; lmdif qtf j = 0: temp = -sum v f / v_first
-            S.tq = o.sumA / S.vfirst;
+            S.tq = o.sum[0] / S.vfirst;
             S.r01 = S.aqf - S.tq * S.vfirst;
             S.q0 = S.vfirst != 0.;
             S.tq0 = 0.;
             S.qtf0 = S.ff;
             if (S.q0) {
-                S.tq0 = -o.sumB / S.vfirst;
+                S.tq0 = -o.sum[1] / S.vfirst;
                 S.qtf0 = S.ff + S.vfirst * S.tq0;
             }
             qr2(S, P);
         } else if (ps == P_QR2) {
-            const double ajn1 = o.nrm;
+            const double ajn1 = o.nrm[0];
             S.t1 = ajn1 != 0.;
             S.ajn1s = (S.t1 && o.aqs1 < 0.) ? -ajn1 : ajn1;
             if (!S.t1) S.ajn1s = 1.;  // unused
@@ -602,8 +642,34 @@ struct Ctl {
                 finalize_qr(S, P, S.wa4s);
             }
         } else if (ps == P_QR3) {
-            const double tq1 = -o.sumA / S.usecond;
+            const double tq1 = -o.sum[0] / S.usecond;
             finalize_qr(S, P, S.wa4s + S.usecond * tq1);
+        }
+    }
+
+    // Slow path of a chunk's enorm (values outside MINPACK's intermediate range
+    // occurred): replay enorm over the chunk's raw values, re-read from the slab
+    // (EVAL) or recomputed with the term waves' exact expression (QR2).
+    __device__ __noinline__ void enorm_slow(Enorm& en, const SlotP& P, int slot, int which, int k0) const {
+        const size_t base = (size_t)slot * p->nOffPad;
+        for (int q = 0; q < kC; q++) {
+            const int k = k0 + q;
+            const int2 o2 = p->offsets[k];
+            const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
+            if (px < 0 || py < 0 || px >= p->boundW || py >= p->boundH) continue;
+            if (P.pass == P_EVAL) {
+                const double* arr = P.ekind == E_JAC ? (which ? J1 : J0) : F;
+                en.add(arr[base + k]);
+            } else if (k > P.kfirst) {  // QR2
+                const double* Jp = P.pivot ? J1 : J0;
+                const double* Jq = P.pivot ? J0 : J1;
+                double a = Jq[base + k];
+                if (P.t0) {
+                    double v = Jp[base + k] / P.ajn0s;
+                    a = a - P.tq * v;
+                }
+                en.add(a);
+            }
         }
     }
 };
@@ -611,7 +677,8 @@ struct Ctl {
 __device__ __noinline__ void ctl_fetch(Ctl& c, SlotS& S, SlotP& P) { c.fetch(S, P); }
 
 // enorm terms: x^2 for MINPACK's "intermediate" range (the branch almost every value
-// takes), 0 otherwise; values outside that range raise the chunk's slow flag
+// takes), +0 otherwise (an exact no-op on the non-negative sum); values outside that
+// range raise the chunk's slow flag and the chain lane replays the chunk with enorm.
 __device__ inline double enorm_term(double x, double agiant, int* slow) {
     const double xa = fabs(x);
     if (xa > 3.834e-20 && xa < agiant) return xa * xa;
@@ -619,44 +686,70 @@ __device__ inline double enorm_term(double x, double agiant, int* slow) {
     return 0.;
 }
 
-__global__ __launch_bounds__(kThreads) void lm_kernel(LMParams p) {
-    __shared__ double term[2][kG][kC];
+// sum += t[0..kC) in index order.  Skipped entries hold +0.0, an exact no-op: a
+// running sum that starts at +0.0 can never become -0.0.
+__device__ inline double chain_sum(double sum, const double* t) {
+    const double2* t2 = reinterpret_cast<const double2*>(t);
+    double2 cur[8], nxt[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) cur[i] = t2[i];
+    for (int q = 16; q < kC; q += 16) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) nxt[i] = t2[q / 2 + i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            sum += cur[i].x;
+            sum += cur[i].y;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) cur[i] = nxt[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        sum += cur[i].x;
+        sum += cur[i].y;
+    }
+    return sum;
+}
+
+__global__ __launch_bounds__(kLMThreads) void lm_kernel(LMParams p) {
+    __shared__ double term[2][2][kG][kC];  // [buffer][sum][slot][pixel]
     __shared__ SlotP sp[kG];
     __shared__ SlotS ss[kG];
-    __shared__ int shCnt[kG], shKmin[kG], shFail[kG], shPh3[kG], shI1fail[kG], shSlow[kG];
+    __shared__ int shCnt[kG], shKmin[kG], shFail[2][kG], shPh3[2][kG], shI1fail[kG], shSlow[2][2][kG];
     __shared__ double shAqs1[kG];
     __shared__ int shStop;
 
     const int tid = threadIdx.x;
-    const int slot = tid & (kG - 1);
-    const int prow = tid >> 2;  // pixel row of this thread inside a chunk (+64 i)
-    const size_t ents = (size_t)p.nOffPad * kG;
-    double* __restrict__ RX = p.slab + (size_t)blockIdx.x * 5 * ents;
-    double* __restrict__ RY = RX + ents;
-    double* __restrict__ F = RY + ents;
-    double* __restrict__ J0 = F + ents;
-    double* __restrict__ J1 = J0 + ents;
-    float* __restrict__ I1 = p.slabI1 + (size_t)blockIdx.x * ents;
+    const bool chainWave = tid >= kTermThreads;
+    const int cl = tid - kTermThreads;  // chain lane: slot cl & 3, sum cl >> 2
+    const bool chain = chainWave && cl < 2 * kG;
+    const int cslot = cl & (kG - 1), cwhich = cl >> 2;
+    const int nOffPad = p.nOffPad;
+    const size_t ents = (size_t)nOffPad * kG;
+    gdouble* __restrict__ RX = (gdouble*)(p.slab + (size_t)blockIdx.x * 5 * ents);
+    gdouble* __restrict__ RY = RX + ents;
+    gdouble* __restrict__ F = RY + ents;
+    gdouble* __restrict__ J0 = F + ents;
+    gdouble* __restrict__ J1 = J0 + ents;
+    gfloat* __restrict__ I1 = (gfloat*)(p.slabI1 + (size_t)blockIdx.x * ents);
+    const gi64* __restrict__ offsets = (const gi64*)p.offsets;
     const double cm = (double)p.cmax;
-    const bool chain = tid < kG;  // chain / control lane of slot `tid`
 
+    const LMParams pc = p;  // the bookkeeping gets its own copy (taking &p would demote every access)
     Ctl ctl;
-    ctl.p = &p;
-    ctl.F = F;
-    ctl.J0 = J0;
-    ctl.J1 = J1;
+    ctl.p = &pc;
+    ctl.F = (const double*)F;
+    ctl.J0 = (const double*)J0;
+    ctl.J1 = (const double*)J1;
     ctl.eps = sqrt(p.epsfcn > kEpsmch ? p.epsfcn : kEpsmch);
     ctl.cnt_eval = 0;
     ctl.cnt_pix = 0;
-    if (chain) ctl_fetch(ctl, ss[tid], sp[tid]);
-
-    // chain accumulators (chain lanes)
-    Enorm en;
-    en.init(1);
-    double sumA = 0., sumB = 0.;
+    if (chain && cwhich == 0) ctl_fetch(ctl, ss[cslot], sp[cslot]);
 
     long long iterations = 0;
-    const unsigned long long tStart = wall_clock64();
+    unsigned long long cyTerms = 0, cyChain = 0, cyCtl = 0;
+    const unsigned long long tStart = wall_clock64(), cyStart = clock64();
     if (tid == 0) shStop = 0;
     for (;;) {
         if (tid == 0 && (++iterations > p.maxIter || (long long)(wall_clock64() - tStart) > p.maxTicks)) {
@@ -664,260 +757,276 @@ __global__ __launch_bounds__(kThreads) void lm_kernel(LMParams p) {
             shStop = 1;
             atomicExch(p.overflow, 1);
         }
-        if (chain) {
-            shCnt[tid] = 0;
-            shKmin[tid] = 0x7fffffff;
-            shFail[tid] = 0x7fffffff;
-            shPh3[tid] = 0;
-            shI1fail[tid] = 0;
-            shSlow[tid] = 0;
-            en.init(1);
-            en.agiant = sp[tid].agiant;
-            sumA = 0.;
-            sumB = 0.;
+        if (chain && cwhich == 0) {
+            shCnt[cslot] = 0;
+            shKmin[cslot] = 0x7fffffff;
+            shFail[0][cslot] = shFail[1][cslot] = 0x7fffffff;
+            shPh3[0][cslot] = shPh3[1][cslot] = 0;
+            shI1fail[cslot] = 0;
+            for (int b = 0; b < 2; b++) shSlow[b][0][cslot] = shSlow[b][1][cslot] = 0;
         }
         __syncthreads();
         bool allDone = true;
-        for (int q = 0; q < kG; q++) allDone = allDone && sp[q].pass == P_DONE;
+        unsigned actMask = 0;
+#pragma unroll
+        for (int q = 0; q < kG; q++) {
+            const int ps = sp[q].pass;
+            allDone = allDone && ps == P_DONE;
+            if (ps != P_DONE && ps != P_IDLE) actMask |= 1u << q;
+        }
         if (shStop || allDone) break;
-        // this thread's slot parameters
-        const SlotP& P = sp[slot];  // read from LDS on use (keeps VGPRs for the pixel data)
-        const bool isjac = (P.ekind == E_JAC0 || P.ekind == E_JAC1);
-        double* __restrict__ outArr = P.ekind == E_JAC0 ? J0 : P.ekind == E_JAC1 ? J1 : F;
-        const double* __restrict__ Jp = P.pivot ? J1 : J0;
-        const double* __restrict__ Jq = P.pivot ? J0 : J1;
-        const bool i1ok = ss[slot].i1ok != 0;
 
-        for (int k0 = 0; k0 < p.nOffPad; k0 += kC) {
-            // ---------------- parallel terms of this chunk ----------------
-            if (P.pass == P_EVAL) {
-#pragma unroll 1
-                for (int i0 = 0; i0 < kPer; i0 += kSub) {
-                    double rx[kSub], ry[kSub], fk[kSub];
-                    float i1v[kSub];
-                    bool valid[kSub];
+        // chain-lane state for this pass
+        const int cps = chain ? sp[cslot].pass : P_IDLE;
+        Enorm en;
+        en.init(1);
+        if (chain) en.agiant = sp[cslot].agiant;
+        double csum = 0.;
+        const bool cActive = chain && (cwhich == 0 ? (cps >= P_EVAL && cps <= P_QR3)
+                                                   : ((cps == P_EVAL && sp[cslot].nev == 2) || cps == P_QR1));
+
+        const int nChunks = nOffPad / kC;
+        for (int c = 0; c <= nChunks; c++) {
+            const unsigned long long tc0 = clock64();
+            if (!chainWave && c < nChunks) {
+                // ---------------- term waves: chunk c into buffer c & 1 ----------------
+                const int k0 = c * kC;
+                const int buf = c & 1;
+                for (int slot = 0; slot < kG; slot++) {
+                    if (!((actMask >> slot) & 1)) continue;  // idle slots cost nothing
+                    const SlotP& P = sp[slot];
+                    const size_t sb = (size_t)slot * nOffPad;
+                    const int pass = P.pass;
+                    if (pass == P_EVAL) {
+                        const int nev = P.nev;
+                        const bool jac = P.ekind == E_JAC;
+                        double rx[kPairs], ry[kPairs], fk[kPairs];
+                        float i1v[kPairs];
+                        bool valid[kPairs];
 #pragma unroll
-                    for (int i = 0; i < kSub; i++) {
-                        const int k = k0 + prow + 64 * (i0 + i);
-                        const size_t e = (size_t)k * kG + slot;
-                        const int2 o2 = p.offsets[k];
-                        const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
-                        valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
-                        rx[i] = RX[e];
-                        ry[i] = RY[e];
-                        i1v[i] = I1[e];
-                        fk[i] = isjac ? F[e] : 0.;
-                    }
-                    unsigned char code1[kSub];
-                    float fx[kSub], fy[kSub];
-                    const uint8_t* g[kSub];
-#pragma unroll
-                    for (int i = 0; i < kSub; i++) {
-                        // projectPointToPlane (:421-470) + isInBoundingBox (:646-655)
-                        const double ux = rx[i], uy = ry[i];
-                        double nn = P.n0 * ux + P.n1 * uy + P.n2 * 1.;
-                        double kk = P.mm / nn;
-                        double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-                        unsigned char cd = 0;
-                        if (!valid[i])
-                            cd = 1;
-                        else if (P0 != P0 || P1 != P1 || P2 != P2)
-                            cd = 2;
-                        else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
-                            cd = 3;
-                        // projectPointsToImage2 (:591-644)
-                        double u, v;
-                        project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
-                        if (cd == 0 && !pixel_good(u, v, P.scale, P.lw, P.lh)) cd = 4;
-                        code1[i] = cd;
-                        fx[i] = (float)(P.scale * u);
-                        fy[i] = (float)(P.scale * v);
-                        g[i] = cd == 0 ? P.img2 + (long)(int)floor((double)fy[i]) * P.lw + (int)floor((double)fx[i])
-                                       : P.img2;
-                    }
-                    uint8_t b00[kSub], b01[kSub], b10[kSub], b11[kSub];
-#pragma unroll
-                    for (int i = 0; i < kSub; i++) {
-                        b00[i] = g[i][0];
-                        b01[i] = g[i][1];
-                        b10[i] = g[i][P.lw];
-                        b11[i] = g[i][P.lw + 1];
-                    }
-#pragma unroll
-                    for (int i = 0; i < kSub; i++) {
-                        const int pl = prow + 64 * (i0 + i);
-                        const int k = k0 + pl;
-                        double t1 = 0., t2 = __builtin_nan("");
-                        if (code1[i] == 2 || code1[i] == 3) {
-                            atomicMin(&shFail[slot], k * 4 + code1[i]);  // first failing pixel decides
-                        } else if (code1[i] == 4) {
-                            shPh3[slot] = 1;
-                        } else if (code1[i] == 0 && i1ok) {
-                            float I2 = bilinear4(b00[i], b01[i], b10[i], b11[i], fx[i], fy[i]);
-                            float dI = i1v[i] - I2;
-                            double r = P.w * (double)dI;                    // evaluateNormal :145-148
-                            double val = isjac ? (r - fk[i]) / P.hj : r;  // fdjac2 forward difference
-                            outArr[(size_t)k * kG + slot] = val;
-                            t1 = enorm_term(val, P.agiant, &shSlow[slot]);
-                            t2 = val;
+                        for (int i = 0; i < kPairs; i++) {
+                            const int k = k0 + tid + kTermThreads * i;
+                            const long long o2 = offsets[k];
+                            const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
+                            valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+                            rx[i] = RX[sb + k];
+                            ry[i] = RY[sb + k];
+                            i1v[i] = I1[sb + k];
+                            fk[i] = jac ? F[sb + k] : 0.;
                         }
-                        term[0][slot][pl] = t1;
-                        term[1][slot][pl] = t2;
-                    }
-                }
-            } else if (P.pass == P_QR1 || P.pass == P_QR2 || P.pass == P_QR3) {
-#pragma unroll 1
-                for (int i0 = 0; i0 < kPer; i0 += kSub) {
-                    double ap[kSub], aq[kSub], fv[kSub];
-                    bool valid[kSub];
+                        for (int ev = 0; ev < nev; ev++) {
+                            unsigned char code1[kPairs];
+                            float fx[kPairs], fy[kPairs];
+                            const gu8* g[kPairs];
+                            const gu8* img2 = (const gu8*)P.img2;
+                            const int lw = P.lw;
 #pragma unroll
-                    for (int i = 0; i < kSub; i++) {
-                        const int k = k0 + prow + 64 * (i0 + i);
-                        const size_t e = (size_t)k * kG + slot;
-                        const int2 o2 = p.offsets[k];
-                        const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
-                        valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
-                        ap[i] = Jp[e];
-                        aq[i] = Jq[e];
-                        fv[i] = P.pass == P_QR2 ? 0. : F[e];
-                    }
-#pragma unroll
-                    for (int i = 0; i < kSub; i++) {
-                        const int pl = prow + 64 * (i0 + i);
-                        const int k = k0 + pl;
-                        double t1 = __builtin_nan(""), t2 = __builtin_nan("");
-                        if (P.pass == P_QR1) {
-                            // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); sum v*a_q, sum v*f
-                            if (valid[i]) {
-                                double v = ap[i] / P.ajn0s;
-                                if (k == P.kfirst) v = v + 1.;
-                                t1 = v * aq[i];
-                                t2 = v * fv[i];
+                            for (int i = 0; i < kPairs; i++) {
+                                // projectPointToPlane (:421-470) + isInBoundingBox (:646-655)
+                                const double ux = rx[i], uy = ry[i];
+                                double nn = P.n0[ev] * ux + P.n1[ev] * uy + P.n2[ev] * 1.;
+                                double kk = P.mm[ev] / nn;
+                                double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+                                unsigned char cd = 0;
+                                if (!valid[i])
+                                    cd = 1;
+                                else if (P0 != P0 || P1 != P1 || P2 != P2)
+                                    cd = 2;
+                                else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
+                                    cd = 3;
+                                // projectPointsToImage2 (:591-644)
+                                double u, v;
+                                project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
+                                if (cd == 0 && !pixel_good(u, v, P.scale, lw, P.lh)) cd = 4;
+                                code1[i] = cd;
+                                fx[i] = (float)(P.scale * u);
+                                fy[i] = (float)(P.scale * v);
+                                g[i] = cd == 0 ? img2 + (long)(int)floor((double)fy[i]) * lw + (int)floor((double)fx[i])
+                                               : img2;
                             }
-                        } else if (P.pass == P_QR2) {
-                            // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
-                            t1 = 0.;
-                            if (valid[i] && k > P.kfirst) {
-                                double a = aq[i];
-                                if (P.t0) {
-                                    double v = ap[i] / P.ajn0s;
-                                    a = a - P.tq * v;
+                            uint8_t b00[kPairs], b01[kPairs], b10[kPairs], b11[kPairs];
+#pragma unroll
+                            for (int i = 0; i < kPairs; i++) {
+                                b00[i] = g[i][0];
+                                b01[i] = g[i][1];
+                                b10[i] = g[i][lw];
+                                b11[i] = g[i][lw + 1];
+                            }
+                            gdouble* __restrict__ outArr = (jac ? (ev ? J1 : J0) : F) + sb;
+                            const double w = P.w[ev], hj = P.hj[ev], agiant = P.agiant;
+                            const bool i1ok = ss[slot].i1ok != 0;
+#pragma unroll
+                            for (int i = 0; i < kPairs; i++) {
+                                const int pl = tid + kTermThreads * i;
+                                const int k = k0 + pl;
+                                double t = 0.;
+                                if (code1[i] == 2 || code1[i] == 3) {
+                                    atomicMin(&shFail[ev][slot], k * 4 + code1[i]);  // first failing pixel decides
+                                } else if (code1[i] == 4) {
+                                    shPh3[ev][slot] = 1;
+                                } else if (code1[i] == 0 && i1ok) {
+                                    float I2 = bilinear4(b00[i], b01[i], b10[i], b11[i], fx[i], fy[i]);
+                                    float dI = i1v[i] - I2;
+                                    double r = w * (double)dI;                  // evaluateNormal :145-148
+                                    double val = jac ? (r - fk[i]) / hj : r;  // fdjac2 forward difference
+                                    outArr[k] = val;
+                                    t = enorm_term(val, agiant, &shSlow[buf][ev][slot]);
                                 }
-                                if (k == P.ksecond) shAqs1[slot] = a;
-                                t1 = enorm_term(a, P.agiant, &shSlow[slot]);
-                                t2 = a;
-                            }
-                        } else {
-                            // lmdif qtf, j = 1: u_i * wa4_i
-                            if (valid[i] && k > P.kfirst) {
-                                double v = P.t0 ? ap[i] / P.ajn0s : 0.;
-                                double a = aq[i];
-                                if (P.t0) a = a - P.tq * v;
-                                double u = P.t1 ? a / P.ajn1s : a;
-                                if (P.t1 && k == P.ksecond) u = u + 1.;
-                                double wa = fv[i];
-                                if (P.q0) wa = wa + v * P.tq0;
-                                t1 = u * wa;
+                                term[buf][ev][slot][pl] = t;
                             }
                         }
-                        term[0][slot][pl] = t1;
-                        term[1][slot][pl] = t2;
-                    }
-                }
-            } else if (P.pass == P_INIT) {
+                    } else if (pass == P_QR1 || pass == P_QR2 || pass == P_QR3) {
+                        const gdouble* __restrict__ Jp = (P.pivot ? J1 : J0) + sb;
+                        const gdouble* __restrict__ Jq = (P.pivot ? J0 : J1) + sb;
+                        double ap[kPairs], aq[kPairs], fv[kPairs];
+                        bool valid[kPairs];
+#pragma unroll
+                        for (int i = 0; i < kPairs; i++) {
+                            const int k = k0 + tid + kTermThreads * i;
+                            const long long o2 = offsets[k];
+                            const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
+                            valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+                            ap[i] = Jp[k];
+                            aq[i] = Jq[k];
+                            fv[i] = pass == P_QR2 ? 0. : F[sb + k];
+                        }
+#pragma unroll
+                        for (int i = 0; i < kPairs; i++) {
+                            const int pl = tid + kTermThreads * i;
+                            const int k = k0 + pl;
+                            double t0 = 0., t1 = 0.;
+                            if (pass == P_QR1) {
+                                // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); v*a_q, v*f
+                                if (valid[i]) {
+                                    double v = ap[i] / P.ajn0s;
+                                    if (k == P.kfirst) v = v + 1.;
+                                    t0 = v * aq[i];
+                                    t1 = v * fv[i];
+                                }
+                            } else if (pass == P_QR2) {
+                                // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
+                                if (valid[i] && k > P.kfirst) {
+                                    double a = aq[i];
+                                    if (P.t0) {
+                                        double v = ap[i] / P.ajn0s;
+                                        a = a - P.tq * v;
+                                    }
+                                    if (k == P.ksecond) shAqs1[slot] = a;
+                                    t0 = enorm_term(a, P.agiant, &shSlow[buf][0][slot]);
+                                }
+                            } else {
+                                // lmdif qtf, j = 1: u_i * wa4_i
+                                if (valid[i] && k > P.kfirst) {
+                                    double v = P.t0 ? ap[i] / P.ajn0s : 0.;
+                                    double a = aq[i];
+                                    if (P.t0) a = a - P.tq * v;
+                                    double u = P.t1 ? a / P.ajn1s : a;
+                                    if (P.t1 && k == P.ksecond) u = u + 1.;
+                                    double wa = fv[i];
+                                    if (P.q0) wa = wa + v * P.tq0;
+                                    t0 = u * wa;
+                                }
+                            }
+                            term[buf][0][slot][pl] = t0;
+                            if (pass == P_QR1) term[buf][1][slot][pl] = t1;
+                        }
+                    } else if (pass == P_INIT) {
 #pragma unroll 1
-                for (int i = 0; i < kPer; i++) {
-                    const int k = k0 + prow + 64 * i;
-                    const size_t e = (size_t)k * kG + slot;
-                    const int2 o2 = p.offsets[k];
-                    // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH)
-                    const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
-                    if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
-                        double ux, uy;
-                        undistort1(p.cam, px, py, ux, uy);  // get3dPointsFromImage1Pixels :542
-                        RX[e] = ux;
-                        RY[e] = uy;
-                        atomicAdd(&shCnt[slot], 1);
-                        atomicMin(&shKmin[slot], k);
-                    }
-                }
-            } else if (P.pass == P_LEVEL) {
+                        for (int i = 0; i < kPairs; i++) {
+                            const int k = k0 + tid + kTermThreads * i;
+                            const long long o2 = offsets[k];
+                            // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH)
+                            const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
+                            if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
+                                double ux, uy;
+                                undistort1(p.cam, px, py, ux, uy);  // get3dPointsFromImage1Pixels :542
+                                RX[sb + k] = ux;
+                                RY[sb + k] = uy;
+                                atomicAdd(&shCnt[slot], 1);
+                                atomicMin(&shKmin[slot], k);
+                            }
+                        }
+                    } else if (pass == P_LEVEL) {
+                        const gu8* img1 = (const gu8*)P.img1;
+                        const int lw = P.lw;
 #pragma unroll 1
-                for (int i = 0; i < kPer; i++) {
-                    const int k = k0 + prow + 64 * i;
-                    const size_t e = (size_t)k * kG + slot;
-                    const int2 o2 = p.offsets[k];
-                    const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
-                    if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
-                        // updateImage1PixelsIntensity (:576-589)
-                        if (!pixel_good(px, py, P.scale, P.lw, P.lh)) {
-                            shI1fail[slot] = 1;
-                        } else {
-                            const float fx = (float)(P.scale * px), fy = (float)(P.scale * py);
-                            const uint8_t* g = P.img1 + (long)(int)floor((double)fy) * P.lw + (int)floor((double)fx);
-                            I1[e] = bilinear4(g[0], g[1], g[P.lw], g[P.lw + 1], fx, fy);
+                        for (int i = 0; i < kPairs; i++) {
+                            const int k = k0 + tid + kTermThreads * i;
+                            const long long o2 = offsets[k];
+                            const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
+                            if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
+                                // updateImage1PixelsIntensity (:576-589)
+                                if (!pixel_good(px, py, P.scale, lw, P.lh)) {
+                                    shI1fail[slot] = 1;
+                                } else {
+                                    const float fx = (float)(P.scale * px), fy = (float)(P.scale * py);
+                                    const gu8* g = img1 + (long)(int)floor((double)fy) * lw + (int)floor((double)fx);
+                                    I1[sb + k] = bilinear4(g[0], g[1], g[lw], g[lw + 1], fx, fy);
+                                }
+                            }
                         }
                     }
                 }
-            }
-            __syncthreads();
-            // ---------------- sequential sums in MINPACK's pixel order ----------------
-            if (chain) {
-                const int ps = sp[tid].pass;
-                const double* tA = term[0][tid];
-                const double* tB = term[1][tid];
-                if (ps == P_EVAL || ps == P_QR2) {
-                    if (!shSlow[tid]) {
-                        double s2 = en.s2;
-#pragma unroll 16
-                        for (int q = 0; q < kC; q++) s2 += tA[q];
-                        en.s2 = s2;
-                    } else {
-                        for (int q = 0; q < kC; q++) {
-                            const double x = tB[q];
-                            if (x == x) en.add(x);
-                        }
-                    }
-                    shSlow[tid] = 0;  // ordered before the next chunk by the barrier below
-                } else if (ps == P_QR1) {
-#pragma unroll 8
-                    for (int q = 0; q < kC; q++) {
-                        const double a = tA[q], b = tB[q];
-                        if (a == a) {
-                            sumA += a;
-                            sumB += b;
-                        }
-                    }
-                } else if (ps == P_QR3) {
-#pragma unroll 8
-                    for (int q = 0; q < kC; q++) {
-                        const double a = tA[q];
-                        if (a == a) sumA += a;
-                    }
+                if (tid == 0) cyTerms += clock64() - tc0;
+            } else if (cActive && c > 0) {
+                // ---------------- chain lanes: chunk c-1, pixel order ----------------
+                const int buf = (c - 1) & 1;
+                const double* t = term[buf][cwhich][cslot];
+                if (cps == P_EVAL || cps == P_QR2) {
+                    if (!shSlow[buf][cwhich][cslot])
+                        en.s2 = chain_sum(en.s2, t);
+                    else
+                        ctl.enorm_slow(en, sp[cslot], cslot, cwhich, (c - 1) * kC);
+                    shSlow[buf][cwhich][cslot] = 0;  // buffer reused two steps later, after a barrier
+                } else {
+                    csum = chain_sum(csum, t);
                 }
+                if (cl == 0) cyChain += clock64() - tc0;
             }
             __syncthreads();
         }
 
         // ---------------- per-slot lmdif bookkeeping ----------------
-        if (chain) {
-            PassOut o;
-            o.nrm = en.finish();
-            o.sumA = sumA;
-            o.sumB = sumB;
-            o.aqs1 = shAqs1[tid];
-            o.cnt = shCnt[tid];
-            o.kmin = shKmin[tid];
-            o.fail = shFail[tid];
-            o.ph3 = shPh3[tid];
-            o.i1fail = shI1fail[tid];
-            ctl.after_pass(ss[tid], sp[tid], o, tid);
+        if (chainWave) {
+            const unsigned long long tc0 = clock64();
+            const double nrm = en.finish();
+            const double nrmB = __shfl(nrm, (cl & (kG - 1)) + kG);
+            const double sumB = __shfl(csum, (cl & (kG - 1)) + kG);
+            if (chain && cwhich == 0 && cps != P_DONE && cps != P_IDLE) {
+                PassOut o;
+                o.nrm[0] = nrm;
+                o.nrm[1] = nrmB;
+                o.sum[0] = csum;
+                o.sum[1] = sumB;
+                o.aqs1 = shAqs1[cslot];
+                o.cnt = shCnt[cslot];
+                o.kmin = shKmin[cslot];
+                o.fail[0] = shFail[0][cslot];
+                o.fail[1] = shFail[1][cslot];
+                o.ph3[0] = shPh3[0][cslot];
+                o.ph3[1] = shPh3[1][cslot];
+                o.i1fail = shI1fail[cslot];
+                ctl.after_pass(ss[cslot], sp[cslot], o, cslot);
+            }
+            if (cl == 0) cyCtl += clock64() - tc0;
         }
     }
 
-    if (chain) {
+    if (chain && cwhich == 0) {
         atomicAdd(p.statEval, (unsigned long long)ctl.cnt_eval);
         atomicAdd(p.statPix, (unsigned long long)ctl.cnt_pix);
+    }
+    if (tid == 0) {
+        atomicAdd(p.statPass + 0, (unsigned long long)iterations);
+        atomicAdd(p.statPass + 1, cyTerms);
+        atomicAdd(p.statPass + 4, clock64() - cyStart);
+        const unsigned long long wt = wall_clock64() - tStart;
+        atomicAdd(p.statPass + 5, wt);
+        atomicMax(p.statPass + 6, wt);
+    }
+    if (cl == 0) {
+        atomicAdd(p.statPass + 2, cyChain);
+        atomicAdd(p.statPass + 3, cyCtl);
     }
 }
 

@@ -175,6 +175,7 @@ def main():
             "cpu_baseline": cpu,
             "stages_ms": {k: last[k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "lm_ms", "total_ms")},
             "counts": {k: last[k] for k in ("queries", "matches", "inliers", "kept")},
+            "lm_profile": lm_profile(last["lm"]),
             "setup_s": {"synthetic_generation": round(t_gen, 2)},
         }
         line = json.dumps(out)
@@ -185,6 +186,21 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def lm_profile(lm):
+    """Where the LM workgroups spend their time (core clocks seen by each group's first wave)."""
+    tot = lm["cycles_total"]
+    return {
+        "groups": lm["groups"], "passes": lm["passes"],
+        "passes_per_group": lm["passes"] / max(lm["groups"], 1),
+        "busy_terms": lm["cycles_terms"] / tot if tot else None,    # first term wave busy / group lifetime
+        "busy_chain": lm["cycles_chain"] / tot if tot else None,    # chain wave summing / group lifetime
+        "busy_control": lm["cycles_control"] / tot if tot else None,
+        "cycles_per_pass": tot / max(lm["passes"], 1),
+        "group_life_mean_over_max": lm["wall_ticks_sum"] / max(lm["groups"], 1) / max(lm["wall_ticks_max"], 1),
+        "clock_ghz": lm["cycles_total"] / max(lm["wall_ticks_sum"], 1) * lm["wall_clock_khz"] * 1e-6,
+    }
 
 
 def cpu_baseline(pair, s, gpu_stats, args):

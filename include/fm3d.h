@@ -101,6 +101,13 @@ typedef struct fm3d_lm_stats {
     int64_t pixel_evaluations; /* sum over evaluations of m_dat */
     int64_t drops[8];          /* points per FM3D_ST_* code */
     double kernel_ms;          /* LM kernel time (HIP events on the context stream) */
+    int64_t groups;            /* LM workgroups launched (kLMSlots points in flight each) */
+    int64_t passes;            /* neighbourhood passes, summed over workgroups */
+    /* core clock cycles seen by each workgroup's first wave, summed over workgroups:
+       parallel term phase, sequential (pixel-order) sum phase, lmdif bookkeeping */
+    int64_t cycles_terms, cycles_chain, cycles_control, cycles_total;
+    /* workgroup lifetimes in constant-rate wall-clock ticks: sum and max over workgroups */
+    int64_t wall_ticks_sum, wall_ticks_max, wall_clock_khz;
 } fm3d_lm_stats;
 
 typedef struct fm3d_pipeline_stats {
