@@ -85,11 +85,14 @@ class LMStats(ctypes.Structure):
                 ("groups", ctypes.c_int64), ("passes", ctypes.c_int64), ("cycles_terms", ctypes.c_int64),
                 ("cycles_chain", ctypes.c_int64), ("cycles_control", ctypes.c_int64), ("cycles_total", ctypes.c_int64),
                 ("wall_ticks_sum", ctypes.c_int64), ("wall_ticks_max", ctypes.c_int64),
-                ("wall_clock_khz", ctypes.c_int64)]
+                ("wall_clock_khz", ctypes.c_int64), ("class_passes", ctypes.c_int64 * 4),
+                ("class_cycles", ctypes.c_int64 * 4), ("last_group_start_ticks", ctypes.c_int64),
+                ("last_group_end_ticks", ctypes.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
-        d["drops"] = list(self.drops)
+        for k in ("drops", "class_passes", "class_cycles"):
+            d[k] = list(d[k])
         return d
 
 

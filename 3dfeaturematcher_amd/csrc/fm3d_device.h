@@ -56,9 +56,12 @@ __host__ __device__ inline void project1(const Camera& c, const double* R, const
     double a2 = r2 + 2 * x * x;
     double a3 = r2 + 2 * y * y;
     double cdist = 1 + c.k[0] * r2 + c.k[1] * r4 + c.k[4] * r6;
-    double icdist2 = 1. / (1 + 0. * r2 + 0. * r4 + 0. * r6);
-    double xd = x * cdist * icdist2 + c.k[2] * a1 + c.k[3] * a2;
-    double yd = y * cdist * icdist2 + c.k[2] * a3 + c.k[3] * a1;
+    // OpenCV's icdist2 = 1 / (1 + 0*r2 + 0*r4 + 0*r6) with k3..k5 = 0: exactly 1 when
+    // r6 (hence r2, r4 >= 0) is finite, NaN otherwise -- x*cdist*icdist2 without the division
+    double xc = x * cdist, yc = y * cdist;
+    if (!(r6 - r6 == 0.)) xc = yc = __builtin_nan("");
+    double xd = xc + c.k[2] * a1 + c.k[3] * a2;
+    double yd = yc + c.k[2] * a3 + c.k[3] * a1;
     u = xd * c.fx + c.cx;
     v = yd * c.fy + c.cy;
 }
@@ -81,6 +84,12 @@ __device__ inline float bilinear(const uint8_t* __restrict__ img, int w, float x
 __host__ __device__ inline bool pixel_good(double x, double y, double scale, int cols, int rows) {
     if (x != x || y != y) return false;
     if ((x < 0) || (x > ((1 / scale) * cols)) || (y < 0) || (y > ((1 / scale) * rows))) return false;
+    return true;
+}
+// the same test with the per-level bounds (1/scale)*cols, (1/scale)*rows precomputed
+__host__ __device__ inline bool pixel_good_b(double x, double y, double xmax, double ymax) {
+    if (x != x || y != y) return false;
+    if ((x < 0) || (x > xmax) || (y < 0) || (y > ymax)) return false;
     return true;
 }
 

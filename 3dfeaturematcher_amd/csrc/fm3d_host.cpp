@@ -11,6 +11,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -73,7 +74,7 @@ struct fm3d_ctx {
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
     long lmGroups = 0;
     int wallKhz = 0;
-    DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, slab, slabI1;
+    DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, lmOrder, lmTrace, slab, slabI1;
     DevBuf records, recTmp, recFlag;
     // staged pipeline inputs
     int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
@@ -364,6 +365,17 @@ int ensure_scan_tmp(fm3d_ctx* c, int n) {
     return FM3D_OK;
 }
 
+// LM kernel register budget: 4 waves/SIMD (3 workgroups per CU) by default;
+// FM3D_LM_WAVES_PER_SIMD=3 selects the 3-wave build (more VGPRs, 2 workgroups per CU)
+const void* lm_kernel_ptr() {
+    static const void* k = [] {
+        const char* e = getenv("FM3D_LM_WAVES_PER_SIMD");
+        if (e && atoi(e) == 3) return reinterpret_cast<const void*>(fm3d::lm_kernel<3>);
+        return reinterpret_cast<const void*>(fm3d::lm_kernel<4>);
+    }();
+    return k;
+}
+
 void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_stats* st) {
     st->groups = c->lmGroups;
     st->passes = (int64_t)cnt[3];
@@ -374,6 +386,12 @@ void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_st
     st->wall_ticks_sum = (int64_t)cnt[8];
     st->wall_ticks_max = (int64_t)cnt[9];
     st->wall_clock_khz = c->wallKhz;
+    for (int k = 0; k < 4; k++) {
+        st->class_passes[k] = (int64_t)cnt[10 + k];
+        st->class_cycles[k] = (int64_t)cnt[14 + k];
+    }
+    st->last_group_start_ticks = (int64_t)(cnt[18] - cnt[20]);
+    st->last_group_end_ticks = (int64_t)(cnt[19] - cnt[20]);
 }
 
 // LM normals over nPts device points (c->pts), outputs in c->lm*
@@ -388,32 +406,30 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     HIPCHK(c, c->lmInfo.ensure((size_t)(P + 1) * 8 * sizeof(int)));
     HIPCHK(c, c->lmNfev.ensure((size_t)(P + 1) * 8 * sizeof(int)));
     HIPCHK(c, c->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
-    HIPCHK(c, c->lmQueue.ensure(64));
-    HIPCHK(c, c->lmStat.ensure(128));
+    HIPCHK(c, c->lmQueue.ensure(64 * sizeof(int)));
+    HIPCHK(c, c->lmStat.ensure(256));
     // persistent workgroups of fm3d::kLMSlots points each; slots refill from the queue
     long groups = c->s.lmWaves;
     if (groups <= 0) {
         int dev = 0, cus = 0, perCU = 0;
         HIPCHK(c, hipGetDevice(&dev));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, reinterpret_cast<const void*>(fm3d::lm_kernel),
-                                                               fm3d::kLMThreads, 0));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lm_kernel_ptr(), fm3d::kLMThreads, 0));
         if (perCU < 1) perCU = 1;
         groups = (long)cus * perCU;
     }
     const long needed = (P + fm3d::kLMSlots - 1) / fm3d::kLMSlots;
     if (groups > needed) groups = needed;
     const size_t ents = (size_t)c->nOffPad * fm3d::kLMSlots;
-    const size_t perGroup = ents * (5 * sizeof(double) + sizeof(float));
+    const size_t perGroup = ents * (5 * sizeof(double) + sizeof(float) + sizeof(int));
     const size_t budget = (size_t)48 << 30;  // HBM budget for the per-group pixel slabs
     long cap = (long)(budget / perGroup);
     if (cap < 1) cap = 1;
     if (groups > cap) groups = cap;
     if (groups < 1) groups = 1;
     HIPCHK(c, c->slab.ensure(ents * 5 * sizeof(double) * groups));
-    HIPCHK(c, c->slabI1.ensure(ents * sizeof(float) * groups));
-    HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 128, c->stream));
+    HIPCHK(c, c->slabI1.ensure(ents * (sizeof(float) + sizeof(int)) * groups));  // I1 + compact index
+    HIPCHK(c, c->lmOrder.ensure((size_t)(P + 1) * sizeof(int)));
     fm3d::LMParams p{};
     p.points = c->pts.as<double>();
     p.P = P;
@@ -455,9 +471,63 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     }
     if (P > 0) {
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        fm3d::lm_kernel<<<(int)groups, fm3d::kLMThreads, 0, c->stream>>>(p);
-        HIPCHK(c, hipGetLastError());
+        // per-launch queues [0..levels], the order count at [16]
+        HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64 * sizeof(int), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 256, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->lmStat.as<unsigned long long>() + 20, 0xff, 8, c->stream));  // min start
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->lmStatus.p, fm3d::kLMRunning, P, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->lmInfo.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->lmNfev.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
+        auto kern = reinterpret_cast<void (*)(fm3d::LMParams)>(const_cast<void*>(lm_kernel_ptr()));
+        // diagnostics: FM3D_LM_TRACE=<file> dumps per-point (fetch tick, finish tick, passes,
+        // workgroup) as int64 after the launch (see tools/lm_trace.py)
+        const char* tr = getenv("FM3D_LM_TRACE");
+        if (tr && *tr) {
+            HIPCHK(c, c->lmTrace.ensure((size_t)P * 4 * sizeof(long long)));
+            HIPCHK(c, hipMemsetAsync(c->lmTrace.p, 0, (size_t)P * 4 * sizeof(long long), c->stream));
+            p.trace = c->lmTrace.as<long long>();
+        }
+        const char* hv = getenv("FM3D_LM_HEAVY");
+        p.heavyPasses = hv ? atoi(hv) : 300;
+        const char* ph = getenv("FM3D_LM_PHASED");
+        if (!(ph && atoi(ph))) {
+            // one launch: every slot runs its point through all levels (coarsest first,
+            // optimize_pyramid :225-241)
+            p.levelHi = levels;
+            p.levelLo = 0;
+            p.queue = c->lmQueue.as<int>();
+            p.order = nullptr;
+            p.nOrder = c->lmQueue.as<int>() + 16;
+            hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(fm3d::kLMThreads), 0, c->stream, p);
+            HIPCHK(c, hipGetLastError());
+        } else {
+            // one launch per pyramid level; between launches the surviving points are
+            // re-queued longest-first by the evaluations of the level just run
+            for (int L = levels; L >= 0; L--) {
+                p.levelHi = p.levelLo = L;
+                p.queue = c->lmQueue.as<int>() + (levels - L);
+                p.order = L == levels ? nullptr : c->lmOrder.as<int>();
+                p.nOrder = c->lmQueue.as<int>() + 16;
+                hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(fm3d::kLMThreads), 0, c->stream, p);
+                HIPCHK(c, hipGetLastError());
+                if (L > 0) {
+                    hipLaunchKernelGGL(fm3d::lm_order_kernel, dim3(1), dim3(1024), 0, c->stream,
+                                       c->lmStatus.as<int>(), c->lmNfev.as<int>(), P, L, c->lmOrder.as<int>(),
+                                       c->lmQueue.as<int>() + 16);
+                    HIPCHK(c, hipGetLastError());
+                }
+            }
+        }
         HIPCHK(c, hipEventRecord(e1, c->stream));
+        if (p.trace) {
+            std::vector<long long> h((size_t)P * 4);
+            HIPCHK(c, hipMemcpyAsync(h.data(), p.trace, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (FILE* f = fopen(tr, "wb")) {
+                fwrite(h.data(), sizeof(long long), h.size(), f);
+                fclose(f);
+            }
+        }
     }
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
@@ -549,7 +619,8 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
     DevBuf* bufs[] = {&c->lvlDesc, &c->offsets, &c->A, &c->B, &c->cqA, &c->ctB, &c->idx, &c->key, &c->fkey,
                       &c->knnOut, &c->cand, &c->flag, &c->matches, &c->count, &c->scanTmp, &c->kp1, &c->kp2,
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
-                      &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat, &c->slab, &c->slabI1,
+                      &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat, &c->lmOrder, &c->lmTrace,
+                      &c->slab, &c->slabI1,
                       &c->records, &c->recTmp, &c->recFlag};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
@@ -727,7 +798,7 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
     if ((r = run_lm(c, P, stats, c->ev[0], c->ev[1]))) return r;
     std::vector<double> nrm((size_t)P * 3);
     std::vector<int> st(P), inf((size_t)P * 8), nf((size_t)P * 8);
-    unsigned long long cnt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long cnt[21] = {};
     if (P) {
         HIPCHK(c, hipMemcpyAsync(nrm.data(), c->lmNormals.p, nrm.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(st.data(), c->lmStatus.p, st.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -864,7 +935,7 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
                                  c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
     int kept = 0;
-    unsigned long long cnt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long cnt[21] = {};
     HIPCHK(c, hipMemcpyAsync(&kept, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));

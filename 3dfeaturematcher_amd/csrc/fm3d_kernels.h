@@ -18,6 +18,11 @@ struct LevelDesc {
 struct LMParams {
     const double* points;  // P x 3
     int P;
+    int levelHi, levelLo;   // pyramid levels this launch runs (levelHi first)
+    int heavyPasses;        // heavy-point scheduling threshold (0 = off)
+    long long* trace;       // optional, P x 4: fetch tick, finish tick, passes, workgroup
+    const int* order;       // points to serve, in order (NULL: 0..P-1)
+    const int* nOrder;      // device count of `order`
     Camera cam;
     double R2[9], t2[3];
     const LevelDesc* lvl;  // device array, levels+1 entries
@@ -45,11 +50,14 @@ struct LMParams {
     unsigned long long* statPass;
 };
 
+constexpr int kLMRunning = 0x100;  // status of a point parked between level launches
 constexpr int kLMSlots = 4;     // points per LM workgroup
-constexpr int kLMThreads = 320;  // 4 term waves + 1 chain wave
-constexpr int kLMChunk = 512;   // pixels per LM chunk (offsets are padded to a multiple)
+constexpr int kLMThreads = 256;  // 3 term waves + 1 chain wave: one wave per SIMD
+constexpr int kLMChunk = 192;   // pixels per LM chunk (offsets are padded to a multiple)
 
+template <int kMinWavesPerSimd>
 __global__ void lm_kernel(LMParams p);
+__global__ void lm_order_kernel(const int* status, const int* nfev, int P, int level, int* order, int* nOrder);
 
 // ---------------- matching ----------------
 struct KnnOut {

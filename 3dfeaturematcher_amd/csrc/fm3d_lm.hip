@@ -12,7 +12,7 @@
 // points (measured with the oracle).  So every sum is replayed in
 // MINPACK's pixel order, bit for bit -- but only the ADDS are sequential:
 //
-//   * a workgroup serves kG = 4 points ("slots") with 4 "term" waves and one
+//   * a workgroup serves kG = 4 points ("slots") with 3 "term" waves and one
 //     "chain" wave;
 //   * a pass over the neighbourhood (one residual evaluation, the two-column
 //     forward-difference Jacobian, or one Householder product) runs in chunks
@@ -22,10 +22,14 @@
 //     LDS tile, while the chain wave adds the previous chunk's terms in pixel
 //     order (one lane per slot and sum: MINPACK's enorm / dot-product order);
 //   * between passes the chain lanes run the slot's lmdif bookkeeping;
-//   * per-pixel state (undistorted rays, I1, fvec, Jacobian) lives in a
-//     per-workgroup slab [array][slot][pixel]; a wave always works on one slot,
-//     so its loads are contiguous 512-byte rows and its branch is uniform, and
-//     idle slots hand their share of the term waves to the busy ones.
+//   * the first pass of a point compacts its neighbourhood: the pixels inside
+//     the image bounds, in reference order, become entries 0..m_dat-1 of the
+//     slot's slab rows (undistorted rays, I1, fvec, Jacobian columns; layout
+//     [array][slot][entry]), so every later pass streams exactly m_dat entries
+//     with contiguous 512-byte wave loads and no bounds tests;
+//   * each term thread owns one entry of every slot per chunk and issues the
+//     loads (then the image gathers) of all slots before consuming any, so a
+//     wave keeps 4 slots' memory traffic in flight.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
@@ -314,22 +318,23 @@ __device__ inline void sph2car_det(double phi, double theta, double& n0, double&
 
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) const long long gi64;  // an int2 offset (x low, y high)
 typedef __attribute__((address_space(1))) const uint8_t gu8;
 
 constexpr int kG = kLMSlots;                   // points (slots) per workgroup
-constexpr int kTermThreads = kLMThreads - 64;  // 4 term waves; the last wave is the chain wave
-constexpr int kC = kLMChunk;                   // pixels per chunk
-constexpr int kPairs = kC / kTermThreads;      // entries per thread per (slot, chunk) (2)
-static_assert(kC % kTermThreads == 0 && kC % 64 == 0, "chunk must tile the term waves");
+constexpr int kTermThreads = kLMThreads - 64;  // term waves; the last wave is the chain wave
+constexpr int kC = kLMChunk;                   // entries per slot per chunk: one per term thread
+static_assert(kC == kTermThreads, "one entry per term thread and slot");
+constexpr int kB = 2;  // slots per batch: a term thread keeps two batches' loads in flight
 
 enum PassKind { P_IDLE = 0, P_INIT, P_LEVEL, P_EVAL, P_QR1, P_QR2, P_QR3, P_DONE };
 
 // parameters of a slot's current pass (LDS; written by the slot's chain lane)
 struct SlotP {
-    int pass, ekind, nev, kfirst, ksecond, t0, t1, q0, pivot, lw, lh;
+    int pass, ekind, nev, len, t0, t1, q0, pivot, lw, lh;
     double n0[2], n1[2], n2[2], mm[2], w[2], hj[2];
-    double scale, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant;
+    double scale, xmax, ymax, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant;  // xmax = (1/scale)*cols (isPixelGood)
     const uint8_t* img1;
     const uint8_t* img2;
 };
@@ -339,19 +344,21 @@ struct SlotS {
     LM s;
     double X0, X1, X2, ccx, ccy, nrm0, nrm1, nrm2;
     double apf, aqf, ff, aps, fs, vfirst, r01, tq0, qtf0, wa4s, usecond, ajn0s, tq, ajn1s;
-    int pidx, m, kfirst, ksecond, L, i1ok, ekind, t0, q0, t1, bNaN;
+    int pidx, m, L, i1ok, ekind, t0, q0, t1, bNaN;
+    int slot, passes;  // passes spent on the current point (heavy-point scheduling)
 };
 
 // per-pass results the chain lanes hand to the bookkeeping
 struct PassOut {
-    double nrm[2];       // EVAL (per evaluation) / QR2: enorm of the pass's values
-    double sum[2];       // QR1 (a_q and fvec products) / QR3 dot products
-    double aqs1;         // QR2: transformed a_q at the second kept pixel
-    int cnt, kmin, fail[2], ph3[2], i1fail;
+    double nrm[2];  // EVAL (per evaluation) / QR2: enorm of the pass's values
+    double sum[2];  // QR1 (a_q and fvec products) / QR3 dot products
+    double aqs1;    // QR2: transformed a_q at the second kept pixel
+    int cnt, fail[2], ph3[2], i1fail;
 };
 
 // lmdif bookkeeping of one slot (chain lane only).  Kept out of line so that the
 // register budget of the data-parallel part of the kernel is not set by it.
+// Entry indices are compact: entry 0 is the first kept pixel, entry 1 the second.
 struct Ctl {
     const LMParams* p;  // a private copy: the kernel's own accesses stay on the kernarg segment
     const double* F;
@@ -359,14 +366,41 @@ struct Ctl {
     const double* J1;
     double eps;
     long long cnt_eval, cnt_pix;
+    int* heavy;  // LDS: passes spent by each slot's current point (0 = none)
 
+    // Heavy-point scheduling: once one slot's point has taken more than heavyPasses
+    // passes, the other slots take no new points until it is done, so the group's
+    // term waves serve that point alone (4 rows per chunk, ~4x shorter passes) and a
+    // long point cannot stretch the end of the launch.  Only the order of work changes.
+    __device__ bool other_heavy(const SlotS& S) const {
+        if (p->heavyPasses <= 0) return false;
+        for (int q = 0; q < kG; q++)
+            if (q != S.slot && heavy[q] > p->heavyPasses) return true;
+        return false;
+    }
+    __device__ void next_point(SlotS& S, SlotP& P) {
+        if (p->trace && S.pidx >= 0 && S.passes > 0) {
+            p->trace[4 * S.pidx + 1] = (long long)wall_clock64();
+            p->trace[4 * S.pidx + 2] += S.passes;
+            p->trace[4 * S.pidx + 3] = blockIdx.x;
+        }
+        heavy[S.slot] = 0;
+        S.passes = 0;
+        if (other_heavy(S)) {
+            P.pass = P_IDLE;
+            return;
+        }
+        fetch(S, P);
+    }
     __device__ void fetch(SlotS& S, SlotP& P) {
-        int pidx = atomicAdd(p->queue, 1);
-        if (pidx >= p->P) {
+        const int q = atomicAdd(p->queue, 1);
+        if (q >= (p->order ? *p->nOrder : p->P)) {
             P.pass = P_DONE;
             return;
         }
+        const int pidx = p->order ? p->order[q] : q;
         S.pidx = pidx;
+        if (p->trace) p->trace[4 * pidx + 0] = (long long)wall_clock64();
         S.X0 = p->points[3 * pidx + 0];
         S.X1 = p->points[3 * pidx + 1];
         S.X2 = p->points[3 * pidx + 2];
@@ -376,18 +410,18 @@ struct Ctl {
         project1(p->cam, Ident, Zero, S.X0, S.X1, S.X2, cx, cy);  // extractPixelsContour(Vec3d) :376-397
         S.ccx = cx;
         S.ccy = cy;
-        for (int l = 0; l < 8; l++) {
-            p->info[8 * pidx + l] = 0;
-            p->nfev[8 * pidx + l] = 0;
-        }
         P.pass = P_INIT;
+        P.len = p->nOffPad;
         P.ccx = cx;
         P.ccy = cy;
     }
     __device__ void start_level(SlotS& S, SlotP& P) {
         const LevelDesc lv = p->lvl[S.L];
         P.pass = P_LEVEL;
+        P.len = S.m;
         P.scale = ldexp(1.0, -S.L);  // 1.0 / float(2^L)  (optimize_pyramid, :225-241)
+        P.xmax = (1 / P.scale) * lv.w;
+        P.ymax = (1 / P.scale) * lv.h;
         P.img1 = lv.img1;
         P.img2 = lv.img2;
         P.lw = lv.w;
@@ -399,17 +433,24 @@ struct Ctl {
         p->normals[3 * S.pidx + 1] = S.nrm1;
         p->normals[3 * S.pidx + 2] = S.nrm2;
         p->mdat[S.pidx] = S.m;
-        fetch(S, P);
+        next_point(S, P);
     }
     __device__ void level_done(SlotS& S, SlotP& P, int info) {
         p->info[8 * S.pidx + S.L] = info;
         p->nfev[8 * S.pidx + S.L] = S.s.nfev;
         sph2car_det(S.s.x[0], S.s.x[1], S.nrm0, S.nrm1, S.nrm2);
         S.L--;
-        if (S.L < 0)
+        if (S.L < 0) {
             finish_point(S, P, FM3D_ST_OK);
-        else
+        } else if (S.L < p->levelLo) {
+            // end of this launch's level range: park the warm-start normal (status stays running)
+            p->normals[3 * S.pidx + 0] = S.nrm0;
+            p->normals[3 * S.pidx + 1] = S.nrm1;
+            p->normals[3 * S.pidx + 2] = S.nrm2;
+            next_point(S, P);
+        } else {
             start_level(S, P);
+        }
     }
     __device__ void abort_level(SlotS& S, SlotP& P, int code) {
         p->info[8 * S.pidx + S.L] = -code;
@@ -448,6 +489,7 @@ struct Ctl {
         }
         S.ekind = kind;
         P.pass = P_EVAL;
+        P.len = S.m;
         P.ekind = kind;
         P.nev = 1;
         P.agiant = 1.304e19 / (double)S.m;
@@ -468,6 +510,7 @@ struct Ctl {
         S.bNaN = !setup_eval(S, P, 1, s.x[0], s.x[1] + s.h[1], s.h[1]);
         S.ekind = E_JAC;
         P.pass = P_EVAL;
+        P.len = S.m;
         P.ekind = E_JAC;
         P.nev = S.bNaN ? 1 : 2;
         P.agiant = 1.304e19 / (double)S.m;
@@ -496,19 +539,18 @@ struct Ctl {
         const size_t base = (size_t)slot * p->nOffPad;
         const double* Jpp = (pc ? J1 : J0) + base;
         const double* Jqq = (pc ? J0 : J1) + base;
-        S.apf = Jpp[S.kfirst];
-        S.aqf = Jqq[S.kfirst];
-        S.ff = F[base + S.kfirst];
-        S.aps = Jpp[S.ksecond];
-        S.fs = F[base + S.ksecond];
+        S.apf = Jpp[0];
+        S.aqf = Jqq[0];
+        S.ff = F[base + 0];
+        S.aps = Jpp[1];
+        S.fs = F[base + 1];
         const double ajn0 = s.acnorm[pc];  // == enorm of the pivot column (same elements, same order)
         S.t0 = ajn0 != 0.;
         S.ajn0s = (S.t0 && S.apf < 0.) ? -ajn0 : ajn0;
         if (!S.t0) S.ajn0s = 1.;  // unused
         S.vfirst = S.t0 ? (S.apf / S.ajn0s) + 1. : S.apf;
         P.pivot = pc;
-        P.kfirst = S.kfirst;
-        P.ksecond = S.ksecond;
+        P.len = S.m;
         P.t0 = S.t0;
         P.ajn0s = S.ajn0s;
         if (S.t0) {
@@ -537,30 +579,25 @@ struct Ctl {
 
     __device__ __noinline__ void after_pass(SlotS& S, SlotP& P, const PassOut& o, int slot) {
         const int ps = P.pass;
+        heavy[slot] = ++S.passes;
         if (ps == P_INIT) {
             S.m = o.cnt;
-            S.kfirst = o.kmin;
-            // second kept pixel: next offset after kfirst inside the bounds
-            int ks = -1;
-            for (int k = S.kfirst + 1; S.m > 1 && k < p->nOff; k++) {
-                const int2 o2 = p->offsets[k];
-                const double px = S.ccx + (double)o2.x, py = S.ccy + (double)o2.y;
-                if (!(px < 0 || py < 0 || px >= p->boundW || py >= p->boundH)) {
-                    ks = k;
-                    break;
-                }
+            if (p->levelHi == p->levels) {
+                // initial guess: X / norm(X) == X * (1/norm) (Vec3d operator/, :342-343)
+                double nr = sqrt(S.X0 * S.X0 + S.X1 * S.X1 + S.X2 * S.X2);
+                double inv = 1. / nr;
+                S.nrm0 = S.X0 * inv;
+                S.nrm1 = S.X1 * inv;
+                S.nrm2 = S.X2 * inv;
+            } else {  // warm start parked by the previous level's launch
+                S.nrm0 = p->normals[3 * S.pidx + 0];
+                S.nrm1 = p->normals[3 * S.pidx + 1];
+                S.nrm2 = p->normals[3 * S.pidx + 2];
             }
-            S.ksecond = ks;
-            // initial guess: X / norm(X) == X * (1/norm) (Vec3d operator/, :342-343)
-            double nr = sqrt(S.X0 * S.X0 + S.X1 * S.X1 + S.X2 * S.X2);
-            double inv = 1. / nr;
-            S.nrm0 = S.X0 * inv;
-            S.nrm1 = S.X1 * inv;
-            S.nrm2 = S.X2 * inv;
             if (S.m <= 0) {
                 finish_point(S, P, FM3D_ST_NO_PIXELS);
             } else {
-                S.L = p->levels;
+                S.L = p->levelHi;
                 start_level(S, P);
             }
         } else if (ps == P_LEVEL) {
@@ -650,22 +687,19 @@ struct Ctl {
     // Slow path of a chunk's enorm (values outside MINPACK's intermediate range
     // occurred): replay enorm over the chunk's raw values, re-read from the slab
     // (EVAL) or recomputed with the term waves' exact expression (QR2).
-    __device__ __noinline__ void enorm_slow(Enorm& en, const SlotP& P, int slot, int which, int k0) const {
+    __device__ __forceinline__ void enorm_slow(Enorm& en, const SlotP& P, int slot, int which, int e0, int n) const {
         const size_t base = (size_t)slot * p->nOffPad;
-        for (int q = 0; q < kC; q++) {
-            const int k = k0 + q;
-            const int2 o2 = p->offsets[k];
-            const double px = P.ccx + (double)o2.x, py = P.ccy + (double)o2.y;
-            if (px < 0 || py < 0 || px >= p->boundW || py >= p->boundH) continue;
+        const int e1 = e0 + n < P.len ? e0 + n : P.len;
+        for (int e = e0; e < e1; e++) {
             if (P.pass == P_EVAL) {
                 const double* arr = P.ekind == E_JAC ? (which ? J1 : J0) : F;
-                en.add(arr[base + k]);
-            } else if (k > P.kfirst) {  // QR2
+                en.add(arr[base + e]);
+            } else if (e > 0) {  // QR2: elements below the diagonal
                 const double* Jp = P.pivot ? J1 : J0;
                 const double* Jq = P.pivot ? J0 : J1;
-                double a = Jq[base + k];
+                double a = Jq[base + e];
                 if (P.t0) {
-                    double v = Jp[base + k] / P.ajn0s;
+                    double v = Jp[base + e] / P.ajn0s;
                     a = a - P.tq * v;
                 }
                 en.add(a);
@@ -674,7 +708,7 @@ struct Ctl {
     }
 };
 
-__device__ __noinline__ void ctl_fetch(Ctl& c, SlotS& S, SlotP& P) { c.fetch(S, P); }
+__device__ __noinline__ void ctl_fetch(Ctl& c, SlotS& S, SlotP& P) { c.next_point(S, P); }
 
 // enorm terms: x^2 for MINPACK's "intermediate" range (the branch almost every value
 // takes), +0 otherwise (an exact no-op on the non-negative sum); values outside that
@@ -712,15 +746,20 @@ __device__ inline double chain_sum(double sum, const double* t) {
     return sum;
 }
 
-__global__ __launch_bounds__(kLMThreads) void lm_kernel(LMParams p) {
-    __shared__ double term[2][2][kG][kC];  // [buffer][sum][slot][pixel]
+template <int kMinWavesPerSimd>
+__global__ __launch_bounds__(kLMThreads, kMinWavesPerSimd) void lm_kernel(LMParams p) {
+    __shared__ double term[2][2][kG][kC];  // [buffer][sum][row][entry]
     __shared__ SlotP sp[kG];
     __shared__ SlotS ss[kG];
-    __shared__ int shCnt[kG], shKmin[kG], shFail[2][kG], shPh3[2][kG], shI1fail[kG], shSlow[2][2][kG];
+    __shared__ int shCnt[kG], shFail[2][kG], shPh3[2][kG], shI1fail[kG], shSlow[2][2][kG];
     __shared__ double shAqs1[kG];
-    __shared__ int shStop;
+    __shared__ int shStop, shHeavy[kG];
+    __shared__ LMParams shP;
+    __shared__ Ctl shCtl[kG];
+    __shared__ PassOut shOut[kG];
 
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
     const bool chainWave = tid >= kTermThreads;
     const int cl = tid - kTermThreads;  // chain lane: slot cl & 3, sum cl >> 2
     const bool chain = chainWave && cl < 2 * kG;
@@ -732,25 +771,209 @@ __global__ __launch_bounds__(kLMThreads) void lm_kernel(LMParams p) {
     gdouble* __restrict__ F = RY + ents;
     gdouble* __restrict__ J0 = F + ents;
     gdouble* __restrict__ J1 = J0 + ents;
-    gfloat* __restrict__ I1 = (gfloat*)(p.slabI1 + (size_t)blockIdx.x * ents);
+    gfloat* __restrict__ I1 = (gfloat*)(p.slabI1 + (size_t)blockIdx.x * 2 * ents);
+    gint* __restrict__ KI = (gint*)(I1 + ents);  // compact entry -> neighbourhood offset index
     const gi64* __restrict__ offsets = (const gi64*)p.offsets;
     const double cm = (double)p.cmax;
+    const unsigned long long ltMask = (1ull << lane) - 1;
 
-    const LMParams pc = p;  // the bookkeeping gets its own copy (taking &p would demote every access)
-    Ctl ctl;
-    ctl.p = &pc;
-    ctl.F = (const double*)F;
-    ctl.J0 = (const double*)J0;
-    ctl.J1 = (const double*)J1;
-    ctl.eps = sqrt(p.epsfcn > kEpsmch ? p.epsfcn : kEpsmch);
-    ctl.cnt_eval = 0;
-    ctl.cnt_pix = 0;
-    if (chain && cwhich == 0) ctl_fetch(ctl, ss[cslot], sp[cslot]);
+    // The bookkeeping works on LDS copies of the parameters and of its own state: taking
+    // the address of a private object would put it in scratch (and a kernel with a large
+    // scratch footprint gets fewer resident waves), taking &p would demote every access.
+    if (tid == 0) shP = p;
+    __syncthreads();
+    Ctl& ctl = shCtl[cslot];
+    if (chain && cwhich == 0) {
+        ctl.p = &shP;
+        ctl.F = (const double*)F;
+        ctl.J0 = (const double*)J0;
+        ctl.J1 = (const double*)J1;
+        ctl.eps = sqrt(p.epsfcn > kEpsmch ? p.epsfcn : kEpsmch);
+        ctl.cnt_eval = 0;
+        ctl.cnt_pix = 0;
+        ctl.heavy = shHeavy;
+        shHeavy[cslot] = 0;
+        ss[cslot].slot = cslot;
+        ss[cslot].passes = 0;
+        ss[cslot].pidx = -1;
+        ctl_fetch(ctl, ss[cslot], sp[cslot]);
+    }
+    // the chain wave's dependent adds bound a pass once few slots are left: let it issue first
+    if (chainWave) __builtin_amdgcn_s_setprio(3);
+
+    // residual / Householder passes: a batch of kB slots' slab entries (loaded one
+    // batch ahead), then their geometry, gathers and terms
+    struct Ld {
+        double a[kB], b[kB], c[kB];
+        float i[kB];
+    };
+    // term rows of a chunk: row r holds kC consecutive entries of one slot.  With one or
+    // two busy slots each gets 4 or 2 rows, so a lone point's pass takes 4x fewer steps.
+    struct Rows {
+        int slot[kG];  // -1: unused row (wave-uniform)
+        int e0, rps;   // this thread's entry in row r: e0 + (r % rps) * kC
+    };
+    auto load_batch = [&](Ld& L, const int h, const Rows& R) {
+#pragma unroll
+        for (int s = 0; s < kB; s++) {
+            L.a[s] = L.b[s] = L.c[s] = 0.;
+            L.i[s] = 0.f;
+            const int slot = R.slot[h + s], e = R.e0 + ((h + s) % R.rps) * kC;
+            if (slot < 0) continue;
+            const SlotP& P = sp[slot];
+            const int ps = P.pass;
+            if (ps < P_EVAL || ps > P_QR3 || e >= P.len) continue;
+            const size_t sb = (size_t)slot * nOffPad;
+            if (ps == P_EVAL) {
+                L.a[s] = RX[sb + e];
+                L.b[s] = RY[sb + e];
+                L.i[s] = I1[sb + e];
+                if (P.ekind == E_JAC) L.c[s] = F[sb + e];
+            } else {
+                const gdouble* Jp = P.pivot ? J1 : J0;
+                const gdouble* Jq = P.pivot ? J0 : J1;
+                L.a[s] = Jp[sb + e];
+                L.b[s] = Jq[sb + e];
+                if (ps != P_QR2) L.c[s] = F[sb + e];
+            }
+        }
+    };
+    auto process_batch = [&](const Ld& L, const int h, const Rows& R, const int buf) {
+        // geometry of every evaluation: projectPointToPlane (:421-470), isInBoundingBox
+        // (:646-655), projectPointsToImage2 (:591-644) -> gather addresses
+        unsigned char code[kB][2];
+        float fx[kB][2], fy[kB][2];
+        const gu8* g[kB][2];
+#pragma unroll
+        for (int s = 0; s < kB; s++) {
+#pragma unroll
+            for (int ev = 0; ev < 2; ev++) {
+                const int slot = R.slot[h + s], e = R.e0 + ((h + s) % R.rps) * kC;
+                const SlotP& P = sp[slot < 0 ? 0 : slot];
+                code[s][ev] = 1;
+                fx[s][ev] = fy[s][ev] = 0.f;
+                g[s][ev] = (const gu8*)P.img2;
+                if (slot < 0 || P.pass != P_EVAL || ev >= P.nev || e >= P.len) continue;
+                const double ux = L.a[s], uy = L.b[s];
+                double nn = P.n0[ev] * ux + P.n1[ev] * uy + P.n2[ev] * 1.;
+                double kk = P.mm[ev] / nn;
+                double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+                unsigned char cd = 0;
+                if (P0 != P0 || P1 != P1 || P2 != P2)
+                    cd = 2;
+                else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
+                    cd = 3;
+                double u, v;
+                project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
+                if (cd == 0 && !pixel_good_b(u, v, P.xmax, P.ymax)) cd = 4;
+                code[s][ev] = cd;
+                fx[s][ev] = (float)(P.scale * u);
+                fy[s][ev] = (float)(P.scale * v);
+                if (cd == 0)
+                    g[s][ev] += (long)(int)floor((double)fy[s][ev]) * P.lw + (int)floor((double)fx[s][ev]);
+            }
+        }
+        uint8_t b00[kB][2], b01[kB][2], b10[kB][2], b11[kB][2];
+#pragma unroll
+        for (int s = 0; s < kB; s++) {
+#pragma unroll
+            for (int ev = 0; ev < 2; ev++) {
+                b00[s][ev] = b01[s][ev] = b10[s][ev] = b11[s][ev] = 0;
+                if (code[s][ev] != 0) continue;
+                const int lw = sp[R.slot[h + s]].lw;
+                b00[s][ev] = g[s][ev][0];
+                b01[s][ev] = g[s][ev][1];
+                b10[s][ev] = g[s][ev][lw];
+                b11[s][ev] = g[s][ev][lw + 1];
+            }
+        }
+        // ---- terms ----
+#pragma unroll
+        for (int s = 0; s < kB; s++) {
+            const int slot = R.slot[h + s], e = R.e0 + ((h + s) % R.rps) * kC, row = h + s;
+            if (slot < 0) continue;
+            const SlotP& P = sp[slot];
+            const int ps = P.pass;
+            if (ps < P_EVAL || ps > P_QR3) continue;
+            const size_t sb = (size_t)slot * nOffPad;
+            const bool in = e < P.len;
+            if (ps == P_EVAL) {
+                const bool jac = P.ekind == E_JAC;
+                const bool i1ok = ss[slot].i1ok != 0;
+#pragma unroll
+                for (int ev = 0; ev < 2; ev++) {
+                    if (ev >= P.nev) continue;
+                    const unsigned char cd = code[s][ev];
+                    double t = 0.;
+                    if (!in) {
+                    } else if (cd == 2 || cd == 3) {
+                        atomicMin(&shFail[ev][slot], e * 4 + cd);  // first failing pixel decides
+                    } else if (cd == 4) {
+                        shPh3[ev][slot] = 1;
+                    } else if (i1ok) {
+                        float I2 = bilinear4(b00[s][ev], b01[s][ev], b10[s][ev], b11[s][ev], fx[s][ev],
+                                             fy[s][ev]);
+                        float dI = L.i[s] - I2;
+                        double r = P.w[ev] * (double)dI;                   // evaluateNormal :145-148
+                        double val = jac ? (r - L.c[s]) / P.hj[ev] : r;  // fdjac2 forward difference
+                        (jac ? (ev ? J1 : J0) : F)[sb + e] = val;
+                        t = enorm_term(val, P.agiant, &shSlow[buf][ev][slot]);
+                    }
+                    term[buf][ev][row][tid] = t;
+                }
+            } else {
+                const double ap = L.a[s], aq = L.b[s], fv = L.c[s];
+                double t0 = 0., t1 = 0.;
+                if (ps == P_QR1) {
+                    // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); v*a_q, v*f
+                    if (in) {
+                        double v = ap / P.ajn0s;
+                        if (e == 0) v = v + 1.;
+                        t0 = v * aq;
+                        t1 = v * fv;
+                    }
+                    term[buf][1][row][tid] = t1;
+                } else if (ps == P_QR2) {
+                    // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
+                    if (in && e > 0) {
+                        double a = aq;
+                        if (P.t0) {
+                            double v = ap / P.ajn0s;
+                            a = a - P.tq * v;
+                        }
+                        if (e == 1) shAqs1[slot] = a;
+                        t0 = enorm_term(a, P.agiant, &shSlow[buf][0][slot]);
+                    }
+                } else {
+                    // lmdif qtf, j = 1: u_i * wa4_i
+                    if (in && e > 0) {
+                        double v = P.t0 ? ap / P.ajn0s : 0.;
+                        double a = aq;
+                        if (P.t0) a = a - P.tq * v;
+                        double u = P.t1 ? a / P.ajn1s : a;
+                        if (P.t1 && e == 1) u = u + 1.;
+                        double wa = fv;
+                        if (P.q0) wa = wa + v * P.tq0;
+                        t0 = u * wa;
+                    }
+                }
+                term[buf][0][row][tid] = t0;
+            }
+        }
+    };
 
     long long iterations = 0;
     unsigned long long cyTerms = 0, cyChain = 0, cyCtl = 0;
     const unsigned long long tStart = wall_clock64(), cyStart = clock64();
-    if (tid == 0) shStop = 0;
+    // per pass class (any JAC / any other evaluation / Householder only / once-per-point):
+    // group passes and cycles, counted by thread 0
+    unsigned long long clsCnt[4] = {0, 0, 0, 0}, clsCyc[4] = {0, 0, 0, 0};
+    unsigned long long passStart = 0;
+    int passCls = 0;
+    if (tid == 0) {
+        shStop = 0;
+        atomicMin(p.statPass + 17, tStart);
+    }
     for (;;) {
         if (tid == 0 && (++iterations > p.maxIter || (long long)(wall_clock64() - tStart) > p.maxTicks)) {
             // cannot happen for a correct state machine; never hang the GPU
@@ -758,249 +981,186 @@ __global__ __launch_bounds__(kLMThreads) void lm_kernel(LMParams p) {
             atomicExch(p.overflow, 1);
         }
         if (chain && cwhich == 0) {
+            if (sp[cslot].pass == P_IDLE) ctl_fetch(ctl, ss[cslot], sp[cslot]);  // waiting on a heavy point
             shCnt[cslot] = 0;
-            shKmin[cslot] = 0x7fffffff;
             shFail[0][cslot] = shFail[1][cslot] = 0x7fffffff;
             shPh3[0][cslot] = shPh3[1][cslot] = 0;
             shI1fail[cslot] = 0;
             for (int b = 0; b < 2; b++) shSlow[b][0][cslot] = shSlow[b][1][cslot] = 0;
         }
         __syncthreads();
-        bool allDone = true;
+        bool allDone = true, rare = false;
         unsigned actMask = 0;
 #pragma unroll
         for (int q = 0; q < kG; q++) {
             const int ps = sp[q].pass;
             allDone = allDone && ps == P_DONE;
             if (ps != P_DONE && ps != P_IDLE) actMask |= 1u << q;
+            rare = rare || ps == P_INIT || ps == P_LEVEL;
+        }
+        if (tid == 0 && iterations > 1) {
+            clsCnt[passCls]++;
+            clsCyc[passCls] += clock64() - passStart;
         }
         if (shStop || allDone) break;
+        if (tid == 0) {
+            passStart = clock64();
+            bool jac = false, ev = false, qr = false;
+            for (int q = 0; q < kG; q++) {
+                const int ps = sp[q].pass;
+                jac = jac || (ps == P_EVAL && sp[q].ekind == E_JAC);
+                ev = ev || ps == P_EVAL;
+                qr = qr || (ps >= P_QR1 && ps <= P_QR3);
+            }
+            passCls = jac ? 0 : ev ? 1 : qr ? 2 : 3;
+        }
+        // rows per busy slot (once-per-point/level passes keep one row per slot)
+        const int nA = __popc(actMask);
+        const int rps = (rare || nA > 2) ? 1 : (nA == 1 ? 4 : 2);
+        int rowSlot[kG];
+        int nSteps = 0;
+#pragma unroll
+        for (int r = 0; r < kG; r++) {
+            const int k = r / rps;  // k-th busy slot
+            int sl = -1, seen = 0;
+#pragma unroll
+            for (int q = 0; q < kG; q++)
+                if ((actMask >> q) & 1) {
+                    if (seen == k) sl = q;
+                    seen++;
+                }
+            rowSlot[r] = sl;
+        }
+#pragma unroll
+        for (int q = 0; q < kG; q++)
+            if ((actMask >> q) & 1) {
+                const int ns = (sp[q].len + rps * kC - 1) / (rps * kC);
+                nSteps = ns > nSteps ? ns : nSteps;
+            }
 
-        // chain-lane state for this pass
-        const int cps = chain ? sp[cslot].pass : P_IDLE;
-        Enorm en;
-        en.init(1);
-        if (chain) en.agiant = sp[cslot].agiant;
-        double csum = 0.;
-        const bool cActive = chain && (cwhich == 0 ? (cps >= P_EVAL && cps <= P_QR3)
-                                                   : ((cps == P_EVAL && sp[cslot].nev == 2) || cps == P_QR1));
-
-        const int nChunks = nOffPad / kC;
-        for (int c = 0; c <= nChunks; c++) {
-            const unsigned long long tc0 = clock64();
-            if (!chainWave && c < nChunks) {
-                // ---------------- term waves: chunk c into buffer c & 1 ----------------
-                const int k0 = c * kC;
-                const int buf = c & 1;
-                for (int slot = 0; slot < kG; slot++) {
-                    if (!((actMask >> slot) & 1)) continue;  // idle slots cost nothing
-                    const SlotP& P = sp[slot];
-                    const size_t sb = (size_t)slot * nOffPad;
-                    const int pass = P.pass;
-                    if (pass == P_EVAL) {
-                        const int nev = P.nev;
-                        const bool jac = P.ekind == E_JAC;
-                        double rx[kPairs], ry[kPairs], fk[kPairs];
-                        float i1v[kPairs];
-                        bool valid[kPairs];
-#pragma unroll
-                        for (int i = 0; i < kPairs; i++) {
-                            const int k = k0 + tid + kTermThreads * i;
-                            const long long o2 = offsets[k];
-                            const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
-                            valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
-                            rx[i] = RX[sb + k];
-                            ry[i] = RY[sb + k];
-                            i1v[i] = I1[sb + k];
-                            fk[i] = jac ? F[sb + k] : 0.;
-                        }
-                        for (int ev = 0; ev < nev; ev++) {
-                            unsigned char code1[kPairs];
-                            float fx[kPairs], fy[kPairs];
-                            const gu8* g[kPairs];
-                            const gu8* img2 = (const gu8*)P.img2;
-                            const int lw = P.lw;
-#pragma unroll
-                            for (int i = 0; i < kPairs; i++) {
-                                // projectPointToPlane (:421-470) + isInBoundingBox (:646-655)
-                                const double ux = rx[i], uy = ry[i];
-                                double nn = P.n0[ev] * ux + P.n1[ev] * uy + P.n2[ev] * 1.;
-                                double kk = P.mm[ev] / nn;
-                                double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-                                unsigned char cd = 0;
-                                if (!valid[i])
-                                    cd = 1;
-                                else if (P0 != P0 || P1 != P1 || P2 != P2)
-                                    cd = 2;
-                                else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
-                                    cd = 3;
-                                // projectPointsToImage2 (:591-644)
-                                double u, v;
-                                project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
-                                if (cd == 0 && !pixel_good(u, v, P.scale, lw, P.lh)) cd = 4;
-                                code1[i] = cd;
-                                fx[i] = (float)(P.scale * u);
-                                fy[i] = (float)(P.scale * v);
-                                g[i] = cd == 0 ? img2 + (long)(int)floor((double)fy[i]) * lw + (int)floor((double)fx[i])
-                                               : img2;
-                            }
-                            uint8_t b00[kPairs], b01[kPairs], b10[kPairs], b11[kPairs];
-#pragma unroll
-                            for (int i = 0; i < kPairs; i++) {
-                                b00[i] = g[i][0];
-                                b01[i] = g[i][1];
-                                b10[i] = g[i][lw];
-                                b11[i] = g[i][lw + 1];
-                            }
-                            gdouble* __restrict__ outArr = (jac ? (ev ? J1 : J0) : F) + sb;
-                            const double w = P.w[ev], hj = P.hj[ev], agiant = P.agiant;
-                            const bool i1ok = ss[slot].i1ok != 0;
-#pragma unroll
-                            for (int i = 0; i < kPairs; i++) {
-                                const int pl = tid + kTermThreads * i;
-                                const int k = k0 + pl;
-                                double t = 0.;
-                                if (code1[i] == 2 || code1[i] == 3) {
-                                    atomicMin(&shFail[ev][slot], k * 4 + code1[i]);  // first failing pixel decides
-                                } else if (code1[i] == 4) {
-                                    shPh3[ev][slot] = 1;
-                                } else if (code1[i] == 0 && i1ok) {
-                                    float I2 = bilinear4(b00[i], b01[i], b10[i], b11[i], fx[i], fy[i]);
-                                    float dI = i1v[i] - I2;
-                                    double r = w * (double)dI;                  // evaluateNormal :145-148
-                                    double val = jac ? (r - fk[i]) / hj : r;  // fdjac2 forward difference
-                                    outArr[k] = val;
-                                    t = enorm_term(val, agiant, &shSlow[buf][ev][slot]);
+        // Term waves and the chain wave run separate step loops with the same number of
+        // barriers (wave-uniform branches), so neither side's registers are live in the other.
+        if (!chainWave) {
+            int runBase[kG] = {0, 0, 0, 0};  // INIT: kept pixels before this chunk (same in every term thread)
+            Ld L0, L1;
+            for (int c = 0; c <= nSteps; c++) {
+                if (c < nSteps) {
+                    const unsigned long long tc0 = clock64();
+                    // ---------------- term waves: chunk c into buffer c & 1 ----------------
+                    const int e = c * kC + tid;  // this thread's entry of every slot
+                    const int buf = c & 1;
+                    // ---- once per point / level: neighbourhood compaction, image-1 samples ----
+    #pragma unroll
+                    for (int s = 0; s < kG; s++) {
+                        const SlotP& P = sp[s];
+                        if (!((actMask >> s) & 1) || c * kC >= P.len) continue;
+                        const size_t sb = (size_t)s * nOffPad;
+                        if (P.pass == P_INIT) {
+                            // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH), in
+                            // offset order -> entries runBase + (kept pixels before this one in the chunk)
+                            int before = 0, total = 0, rank = 0;
+                            bool mine = false;
+                            double mx = 0, my = 0;
+    #pragma unroll
+                            for (int b = 0; b < kC / 64; b++) {
+                                const long long o2 = offsets[c * kC + 64 * b + lane];
+                                const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
+                                const bool v = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+                                const unsigned long long bm = __ballot(v);
+                                const int n = __popcll(bm);
+                                if (b < wave) before += n;
+                                if (b == wave) {
+                                    mine = v;
+                                    rank = __popcll(bm & ltMask);
+                                    mx = px;
+                                    my = py;
                                 }
-                                term[buf][ev][slot][pl] = t;
+                                total += n;
                             }
-                        }
-                    } else if (pass == P_QR1 || pass == P_QR2 || pass == P_QR3) {
-                        const gdouble* __restrict__ Jp = (P.pivot ? J1 : J0) + sb;
-                        const gdouble* __restrict__ Jq = (P.pivot ? J0 : J1) + sb;
-                        double ap[kPairs], aq[kPairs], fv[kPairs];
-                        bool valid[kPairs];
-#pragma unroll
-                        for (int i = 0; i < kPairs; i++) {
-                            const int k = k0 + tid + kTermThreads * i;
-                            const long long o2 = offsets[k];
-                            const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
-                            valid[i] = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
-                            ap[i] = Jp[k];
-                            aq[i] = Jq[k];
-                            fv[i] = pass == P_QR2 ? 0. : F[sb + k];
-                        }
-#pragma unroll
-                        for (int i = 0; i < kPairs; i++) {
-                            const int pl = tid + kTermThreads * i;
-                            const int k = k0 + pl;
-                            double t0 = 0., t1 = 0.;
-                            if (pass == P_QR1) {
-                                // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); v*a_q, v*f
-                                if (valid[i]) {
-                                    double v = ap[i] / P.ajn0s;
-                                    if (k == P.kfirst) v = v + 1.;
-                                    t0 = v * aq[i];
-                                    t1 = v * fv[i];
-                                }
-                            } else if (pass == P_QR2) {
-                                // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
-                                if (valid[i] && k > P.kfirst) {
-                                    double a = aq[i];
-                                    if (P.t0) {
-                                        double v = ap[i] / P.ajn0s;
-                                        a = a - P.tq * v;
-                                    }
-                                    if (k == P.ksecond) shAqs1[slot] = a;
-                                    t0 = enorm_term(a, P.agiant, &shSlow[buf][0][slot]);
-                                }
-                            } else {
-                                // lmdif qtf, j = 1: u_i * wa4_i
-                                if (valid[i] && k > P.kfirst) {
-                                    double v = P.t0 ? ap[i] / P.ajn0s : 0.;
-                                    double a = aq[i];
-                                    if (P.t0) a = a - P.tq * v;
-                                    double u = P.t1 ? a / P.ajn1s : a;
-                                    if (P.t1 && k == P.ksecond) u = u + 1.;
-                                    double wa = fv[i];
-                                    if (P.q0) wa = wa + v * P.tq0;
-                                    t0 = u * wa;
-                                }
-                            }
-                            term[buf][0][slot][pl] = t0;
-                            if (pass == P_QR1) term[buf][1][slot][pl] = t1;
-                        }
-                    } else if (pass == P_INIT) {
-#pragma unroll 1
-                        for (int i = 0; i < kPairs; i++) {
-                            const int k = k0 + tid + kTermThreads * i;
-                            const long long o2 = offsets[k];
-                            // extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH)
-                            const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
-                            if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
+                            if (mine) {
+                                const int pos = runBase[s] + before + rank;
                                 double ux, uy;
-                                undistort1(p.cam, px, py, ux, uy);  // get3dPointsFromImage1Pixels :542
-                                RX[sb + k] = ux;
-                                RY[sb + k] = uy;
-                                atomicAdd(&shCnt[slot], 1);
-                                atomicMin(&shKmin[slot], k);
+                                undistort1(p.cam, mx, my, ux, uy);  // get3dPointsFromImage1Pixels :542
+                                RX[sb + pos] = ux;
+                                RY[sb + pos] = uy;
+                                KI[sb + pos] = e;
                             }
-                        }
-                    } else if (pass == P_LEVEL) {
-                        const gu8* img1 = (const gu8*)P.img1;
-                        const int lw = P.lw;
-#pragma unroll 1
-                        for (int i = 0; i < kPairs; i++) {
-                            const int k = k0 + tid + kTermThreads * i;
-                            const long long o2 = offsets[k];
+                            runBase[s] += total;
+                            if (tid == 0) shCnt[s] = runBase[s];
+                        } else if (P.pass == P_LEVEL && e < P.len) {
+                            // updateImage1PixelsIntensity (:576-589)
+                            const long long o2 = offsets[KI[sb + e]];
                             const double px = P.ccx + (double)(int)o2, py = P.ccy + (double)(int)(o2 >> 32);
-                            if (!(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH)) {
-                                // updateImage1PixelsIntensity (:576-589)
-                                if (!pixel_good(px, py, P.scale, lw, P.lh)) {
-                                    shI1fail[slot] = 1;
-                                } else {
-                                    const float fx = (float)(P.scale * px), fy = (float)(P.scale * py);
-                                    const gu8* g = img1 + (long)(int)floor((double)fy) * lw + (int)floor((double)fx);
-                                    I1[sb + k] = bilinear4(g[0], g[1], g[lw], g[lw + 1], fx, fy);
-                                }
+                            if (!pixel_good_b(px, py, P.xmax, P.ymax)) {
+                                shI1fail[s] = 1;
+                            } else {
+                                const gu8* img1 = (const gu8*)P.img1;
+                                const float fx = (float)(P.scale * px), fy = (float)(P.scale * py);
+                                const gu8* g = img1 + (long)(int)floor((double)fy) * P.lw + (int)floor((double)fx);
+                                I1[sb + e] = bilinear4(g[0], g[1], g[P.lw], g[P.lw + 1], fx, fy);
                             }
                         }
                     }
+                    // residual / Householder passes, software-pipelined by batch: the loads of
+                    // the next batch are in flight while the current one is processed
+                    Rows R, Rn;
+    #pragma unroll
+                    for (int r = 0; r < kG; r++) R.slot[r] = Rn.slot[r] = rowSlot[r];
+                    R.rps = Rn.rps = rps;
+                    R.e0 = c * rps * kC + tid;
+                    Rn.e0 = R.e0 + rps * kC;
+                    if (c == 0) load_batch(L0, 0, R);
+                    load_batch(L1, kB, R);
+                    process_batch(L0, 0, R, buf);
+                    if (c + 1 < nSteps) load_batch(L0, 0, Rn);
+                    process_batch(L1, kB, R, buf);
+                    if (tid == 0) cyTerms += clock64() - tc0;
                 }
-                if (tid == 0) cyTerms += clock64() - tc0;
-            } else if (cActive && c > 0) {
-                // ---------------- chain lanes: chunk c-1, pixel order ----------------
-                const int buf = (c - 1) & 1;
-                const double* t = term[buf][cwhich][cslot];
-                if (cps == P_EVAL || cps == P_QR2) {
-                    if (!shSlow[buf][cwhich][cslot])
-                        en.s2 = chain_sum(en.s2, t);
-                    else
-                        ctl.enorm_slow(en, sp[cslot], cslot, cwhich, (c - 1) * kC);
-                    shSlow[buf][cwhich][cslot] = 0;  // buffer reused two steps later, after a barrier
-                } else {
-                    csum = chain_sum(csum, t);
-                }
-                if (cl == 0) cyChain += clock64() - tc0;
+                __syncthreads();
             }
-            __syncthreads();
-        }
-
-        // ---------------- per-slot lmdif bookkeeping ----------------
-        if (chainWave) {
+        } else {
+            // chain-lane state for this pass
+            const int cps = chain ? sp[cslot].pass : P_IDLE;
+            const int cSteps = chain ? (sp[cslot].len + rps * kC - 1) / (rps * kC) : 0;
+            const int cRow0 = __popc(actMask & ((1u << cslot) - 1)) * rps;  // first row of my slot
+            Enorm en;
+            en.init(1);
+            if (chain) en.agiant = sp[cslot].agiant;
+            double csum = 0.;
+            const bool cActive = chain && (cwhich == 0 ? (cps >= P_EVAL && cps <= P_QR3)
+                                                       : ((cps == P_EVAL && sp[cslot].nev == 2) || cps == P_QR1));
+            for (int c = 0; c <= nSteps; c++) {
+                if (cActive && c > 0 && c - 1 < cSteps) {
+                    const unsigned long long tc0 = clock64();
+                    // ---------------- chain lanes: chunk c-1, entry order ----------------
+                    const int buf = (c - 1) & 1;
+                    if (cps == P_EVAL || cps == P_QR2) {
+                        if (!shSlow[buf][cwhich][cslot]) {
+                            for (int r = 0; r < rps; r++) en.s2 = chain_sum(en.s2, term[buf][cwhich][cRow0 + r]);
+                        } else {
+                            ctl.enorm_slow(en, sp[cslot], cslot, cwhich, (c - 1) * rps * kC, rps * kC);
+                        }
+                        shSlow[buf][cwhich][cslot] = 0;  // buffer reused two steps later, after a barrier
+                    } else {
+                        for (int r = 0; r < rps; r++) csum = chain_sum(csum, term[buf][cwhich][cRow0 + r]);
+                    }
+                    if (cl == 0) cyChain += clock64() - tc0;
+                }
+                __syncthreads();
+            }
+            // ---------------- per-slot lmdif bookkeeping ----------------
             const unsigned long long tc0 = clock64();
             const double nrm = en.finish();
             const double nrmB = __shfl(nrm, (cl & (kG - 1)) + kG);
             const double sumB = __shfl(csum, (cl & (kG - 1)) + kG);
             if (chain && cwhich == 0 && cps != P_DONE && cps != P_IDLE) {
-                PassOut o;
+                PassOut& o = shOut[cslot];
                 o.nrm[0] = nrm;
                 o.nrm[1] = nrmB;
                 o.sum[0] = csum;
                 o.sum[1] = sumB;
                 o.aqs1 = shAqs1[cslot];
                 o.cnt = shCnt[cslot];
-                o.kmin = shKmin[cslot];
                 o.fail[0] = shFail[0][cslot];
                 o.fail[1] = shFail[1][cslot];
                 o.ph3[0] = shPh3[0][cslot];
@@ -1023,11 +1183,53 @@ __global__ __launch_bounds__(kLMThreads) void lm_kernel(LMParams p) {
         const unsigned long long wt = wall_clock64() - tStart;
         atomicAdd(p.statPass + 5, wt);
         atomicMax(p.statPass + 6, wt);
+        for (int k = 0; k < 4; k++) {
+            atomicAdd(p.statPass + 7 + k, clsCnt[k]);
+            atomicAdd(p.statPass + 11 + k, clsCyc[k]);
+        }
+        atomicMax(p.statPass + 15, tStart);  // latest workgroup start: late starts = grid > residency
+        atomicMax(p.statPass + 16, wall_clock64());
     }
     if (cl == 0) {
         atomicAdd(p.statPass + 2, cyChain);
         atomicAdd(p.statPass + 3, cyCtl);
     }
 }
+
+// Between level launches: the points still running, ordered by the evaluations the
+// level just finished took, most first (a longest-first schedule for the next level:
+// per-point cost is strongly correlated across pyramid levels).  Counting sort, one
+// workgroup; the order inside a bin does not matter (points are independent).
+__global__ __launch_bounds__(1024) void lm_order_kernel(const int* __restrict__ status, const int* __restrict__ nfev,
+                                                      int P, int level, int* __restrict__ order, int* nOrder) {
+    constexpr int kBins = 512;
+    __shared__ int hist[kBins];
+    for (int b = threadIdx.x; b < kBins; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        if (status[i] != kLMRunning) continue;
+        const int n = nfev[8 * i + level];
+        atomicAdd(&hist[kBins - 1 - (n < kBins - 1 ? n : kBins - 1)], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int b = 0; b < kBins; b++) {
+            const int c = hist[b];
+            hist[b] = run;
+            run += c;
+        }
+        *nOrder = run;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        if (status[i] != kLMRunning) continue;
+        const int n = nfev[8 * i + level];
+        order[atomicAdd(&hist[kBins - 1 - (n < kBins - 1 ? n : kBins - 1)], 1)] = i;
+    }
+}
+
+template __global__ void lm_kernel<3>(LMParams);
+template __global__ void lm_kernel<4>(LMParams);
 
 }  // namespace fm3d

@@ -200,6 +200,11 @@ def lm_profile(lm):
         "cycles_per_pass": tot / max(lm["passes"], 1),
         "group_life_mean_over_max": lm["wall_ticks_sum"] / max(lm["groups"], 1) / max(lm["wall_ticks_max"], 1),
         "clock_ghz": lm["cycles_total"] / max(lm["wall_ticks_sum"], 1) * lm["wall_clock_khz"] * 1e-6,
+        "kcycles_per_pass_by_class": {n: round(cy / max(c, 1) / 1e3, 1) for n, c, cy in
+                                      zip(("jac", "eval", "qr", "once"), lm["class_passes"], lm["class_cycles"])},
+        "passes_by_class": dict(zip(("jac", "eval", "qr", "once"), lm["class_passes"])),
+        "last_group_start_ms": lm["last_group_start_ticks"] / max(lm["wall_clock_khz"], 1),
+        "last_group_end_ms": lm["last_group_end_ticks"] / max(lm["wall_clock_khz"], 1),
     }
 
 

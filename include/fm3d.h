@@ -108,6 +108,11 @@ typedef struct fm3d_lm_stats {
     int64_t cycles_terms, cycles_chain, cycles_control, cycles_total;
     /* workgroup lifetimes in constant-rate wall-clock ticks: sum and max over workgroups */
     int64_t wall_ticks_sum, wall_ticks_max, wall_clock_khz;
+    /* workgroup passes and cycles by class: [0] with a Jacobian evaluation, [1] with another
+       residual evaluation, [2] Householder products only, [3] once-per-point/level passes */
+    int64_t class_passes[4], class_cycles[4];
+    /* wall-clock ticks from the first workgroup start to the last start / the last end */
+    int64_t last_group_start_ticks, last_group_end_ticks;
 } fm3d_lm_stats;
 
 typedef struct fm3d_pipeline_stats {
