@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", type=str, default="")
+    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "r01_pmc_c4.json"),
+                    help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()
 
 
@@ -131,6 +133,7 @@ def main():
         all_kept = int(k.item())
 
     lm_ms = float(np.mean([st["lm_ms"] for st in stats]))
+    traffic = pmc_traffic(args)
     pix = float(np.mean([st["lm"]["pixel_evaluations"] for st in stats]))
     evals = float(np.mean([st["lm"]["evaluations"] for st in stats]))
     last = stats[-1]
@@ -162,12 +165,16 @@ def main():
             },
             "roofline": {
                 "kernel": "fm3d::lm_kernel (LM normal refinement)",
-                "bound": "fp64",
+                "bound": "mfma",
+                "compute": "fp64 (issued on the VALU; MI355X fp64 matrix and vector peaks coincide at 78.6 TFLOP/s)",
                 "achieved": achieved_tflops,
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_tflops / FP64_PEAK_TFLOPS,
-                "traffic": None,
+                "traffic": traffic["bytes"] if traffic else None,
+                "traffic_unit": "bytes per launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_GBps": traffic["bytes"] / (lm_ms * 1e6) if traffic and lm_ms > 0 else None,
+                "traffic_source": traffic["source"] if traffic else None,
                 "algorithmic": f"{FLOPS_PER_PIXEL_EVAL} flop per pixel evaluation x {pix:.4g} pixel evaluations "
                                f"({evals:.4g} residual evaluations) per launch",
                 "avg_launch_ms": lm_ms,
@@ -186,6 +193,20 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args):
+    """HBM bytes per LM launch from the committed rocprofv3 PMC summary of this workload
+    (separate --pmc passes; rocprofv3 cannot run inside the timed process)."""
+    try:
+        with open(args.pmc_json) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    w = d.get("workload", {})
+    if (w.get("keypoints"), w.get("ray"), w.get("levels")) != (args.keypoints, args.ray, args.levels):
+        return None
+    return {"bytes": d["hbm_bytes_per_launch"], "source": os.path.relpath(args.pmc_json, ROOT)}
 
 
 def lm_profile(lm):

@@ -1,0 +1,196 @@
+/*
+ * fm3d_compat.hpp -- header-only C++ shim that re-exposes the reference's class
+ * interface for the hot path on top of the C ABI (fm3d.h).
+ *
+ * The reference calls its three classes from main.cpp:91-155:
+ *   DescriptorsMatcher        DescriptorsMatcher/descriptorsmatcher.h:39-111
+ *   SingleCameraTriangulator  Triangulator/singlecameratriangulator.h:52-93
+ *   NormalOptimizer           Triangulator/normaloptimizer.h:43-59
+ * The classes below keep those names, method names, argument order, argument meaning
+ * and out-parameter semantics (appended matches, erased points, appended normals).
+ * Two deliberate differences, both outside the hot path:
+ *   - compareWithNNDR takes the descriptor matrices: feature detection/description
+ *     (descriptorsmatcher.cpp:110-115) is upstream and out of scope;
+ *   - the OpenCV value types are replaced by the small PODs below (Mat8u, DescMat,
+ *     KeyPoint, DMatch, Vec3d, Matx44d) with the same fields the path reads, and
+ *     cv::FileStorage by the settings.yml reader fm3d_settings_load.
+ * Errors: every ABI failure throws fm3d::compat::Error (the reference exit()s).
+ */
+#ifndef FM3D_COMPAT_HPP
+#define FM3D_COMPAT_HPP
+
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fm3d.h"
+
+namespace fm3d {
+namespace compat {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+struct Point2f {
+    float x, y;
+};
+struct KeyPoint {  // cv::KeyPoint: the path reads .pt only (singlecameratriangulator.cpp:152-164)
+    Point2f pt;
+    float size, angle, response;
+    int octave, class_id;
+};
+typedef fm3d_dmatch DMatch;  // cv::DMatch field layout: queryIdx, trainIdx, imgIdx, distance
+typedef std::array<double, 3> Vec3d;
+typedef std::array<double, 16> Matx44d;  // row major
+
+struct Mat8u {  // CV_8UC1 image (rows x cols, row stride `step` bytes)
+    int rows, cols;
+    const uint8_t* data;
+    int step;
+};
+struct DescMat {  // descriptor matrix: CV_32F rows, CV_8U rows, or binary strings
+    int rows, cols;
+    fm3d_desc_type type;  // FM3D_DESC_F32 / FM3D_DESC_U8 / FM3D_DESC_BITS (cols = bytes)
+    const void* data;
+};
+
+inline void check(fm3d_ctx* ctx, int rc) {
+    if (rc != FM3D_OK) throw Error(rc, ctx ? fm3d_last_error(ctx) : "fm3d error");
+}
+
+// Owns the device context (settings + one HIP stream on one GPU).
+class Device {
+public:
+    explicit Device(const fm3d_settings& s, int device = 0) { check(nullptr, fm3d_ctx_create(&s, device, &ctx_)); }
+    // cv::FileStorage fs(path) stand-in: the %YAML:1.0 subset build/settings.yml uses
+    static fm3d_settings load_settings(const std::string& path) {
+        fm3d_settings s;
+        check(nullptr, fm3d_settings_load(path.c_str(), &s));
+        return s;
+    }
+    ~Device() { fm3d_ctx_destroy(ctx_); }
+    Device(const Device&) = delete;
+    Device& operator=(const Device&) = delete;
+    fm3d_ctx* ctx() const { return ctx_; }
+
+private:
+    fm3d_ctx* ctx_ = nullptr;
+};
+
+// DescriptorsMatcher (descriptorsmatcher.h:39-111)
+class DescriptorsMatcher {
+public:
+    explicit DescriptorsMatcher(Device& d) : d_(d) {}
+    // knnMatch(k=2) of compare (descriptorsmatcher.cpp:89-105): nA x 2 neighbours
+    void knnMatch(const DescMat& A, const DescMat& B, std::vector<std::array<DMatch, 2> >& out) {
+        require_same(A, B);
+        out.resize(A.rows);
+        check(d_.ctx(), fm3d_knn2(d_.ctx(), A.data, A.rows, B.data, B.rows, A.cols, A.type,
+                                  reinterpret_cast<fm3d_dmatch*>(out.data())));
+    }
+    // compareWithNNDR (descriptorsmatcher.cpp:107-131): matches are APPENDED, in query order
+    void compareWithNNDR(double epsilon, std::vector<DMatch>& matches, const DescMat& A, const DescMat& B) {
+        require_same(A, B);
+        std::vector<DMatch> tmp(A.rows > 0 ? A.rows : 1);
+        int n = 0;
+        check(d_.ctx(), fm3d_match_nndr(d_.ctx(), A.data, A.rows, B.data, B.rows, A.cols, A.type, epsilon,
+                                        tmp.data(), &n));
+        matches.insert(matches.end(), tmp.begin(), tmp.begin() + n);
+    }
+
+private:
+    static void require_same(const DescMat& A, const DescMat& B) {
+        if (A.cols != B.cols || A.type != B.type) throw Error(FM3D_ERR_INVALID, "descriptor matrices differ");
+    }
+    Device& d_;
+};
+
+// SingleCameraTriangulator (singlecameratriangulator.h:52-93), hot-path methods
+class SingleCameraTriangulator {
+public:
+    explicit SingleCameraTriangulator(Device& d) : d_(d) {}
+    // setg12 (:123-143): g12 = gIC^-1 g2^-1 g1 gIC, also installed for triangulation
+    void setg12(const Vec3d& T1, const Vec3d& T2, const Vec3d& r1, const Vec3d& r2, Matx44d& g12) {
+        check(d_.ctx(), fm3d_setg12(d_.ctx(), T1.data(), T2.data(), r1.data(), r2.data(), g12.data()));
+    }
+    void setg12(const Matx44d& g12) { check(d_.ctx(), fm3d_set_g12(d_.ctx(), g12.data())); }
+    // setKeypoints (:145-171)
+    void setKeypoints(const std::vector<KeyPoint>& k1, const std::vector<KeyPoint>& k2,
+                      const std::vector<DMatch>& matches) {
+        kp1_.resize(k1.size());
+        kp2_.resize(k2.size());
+        for (size_t i = 0; i < k1.size(); i++) kp1_[i] = fm3d_point2f{k1[i].pt.x, k1[i].pt.y};
+        for (size_t i = 0; i < k2.size(); i++) kp2_[i] = fm3d_point2f{k2[i].pt.x, k2[i].pt.y};
+        matches_ = matches;
+    }
+    // triangulate (:173-230): points3D is cleared then filled (inliers, match order);
+    // outliersMask is APPENDED (one flag per match, true = kept), as in the reference
+    void triangulate(std::vector<Vec3d>& points3D, std::vector<bool>& outliersMask) {
+        const int K = (int)matches_.size();
+        std::vector<double> pts((size_t)3 * (K > 0 ? K : 1));
+        std::vector<uint8_t> mask(K > 0 ? K : 1);
+        int n = 0;
+        check(d_.ctx(), fm3d_triangulate(d_.ctx(), kp1_.data(), (int)kp1_.size(), kp2_.data(), (int)kp2_.size(),
+                                         matches_.data(), K, pts.data(), mask.data(), &n));
+        points3D.clear();
+        for (int i = 0; i < n; i++) points3D.push_back(Vec3d{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]});
+        for (int i = 0; i < K; i++) outliersMask.push_back(mask[i] != 0);
+    }
+    Device& device() const { return d_; }
+
+private:
+    Device& d_;
+    std::vector<fm3d_point2f> kp1_, kp2_;
+    std::vector<DMatch> matches_;
+};
+
+// NormalOptimizer (normaloptimizer.h:43-59), hot-path methods
+class NormalOptimizer {
+public:
+    NormalOptimizer(Device& d, SingleCameraTriangulator* sct) : d_(d), sct_(sct) {}
+    // setImages (normaloptimizer.cpp:191-221): both gray images, builds the pyramids
+    void setImages(const Mat8u& img1, const Mat8u& img2) {
+        if (img1.rows != img2.rows || img1.cols != img2.cols || img1.step != img2.step)
+            throw Error(FM3D_ERR_INVALID, "images differ in size");
+        check(d_.ctx(), fm3d_set_images(d_.ctx(), img1.data, img2.data, img1.cols, img1.rows, img1.step));
+    }
+    // computeOptimizedNormals (:321-452): failed points are ERASED from points3D (order
+    // kept); one normal per kept point is APPENDED to normalsVector
+    void computeOptimizedNormals(std::vector<Vec3d>& points3D, std::vector<Vec3d>& normalsVector) {
+        const int P = (int)points3D.size();
+        std::vector<double> pts((size_t)3 * (P > 0 ? P : 1)), nrm((size_t)3 * (P > 0 ? P : 1));
+        for (int i = 0; i < P; i++)
+            for (int k = 0; k < 3; k++) pts[3 * i + k] = points3D[i][k];
+        status_.assign(P > 0 ? P : 1, 0);
+        int kept = 0;
+        check(d_.ctx(), fm3d_optimize_normals(d_.ctx(), pts.data(), P, nrm.data(), status_.data(), nullptr, nullptr,
+                                              &kept, &stats_));
+        status_.resize(P);
+        points3D.resize(kept);
+        for (int i = 0; i < kept; i++) {
+            points3D[i] = Vec3d{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+            normalsVector.push_back(Vec3d{nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]});
+        }
+    }
+    // the PCL viewer thread (pclvisualizerthread.cpp) is visual only: no-ops
+    void startVisualizerThread() {}
+    void stopVisualizerThread() {}
+    // per input point outcome of the last call (FM3D_ST_*) and its counters
+    const std::vector<int32_t>& lastStatus() const { return status_; }
+    const fm3d_lm_stats& lastStats() const { return stats_; }
+
+private:
+    Device& d_;
+    SingleCameraTriangulator* sct_;
+    std::vector<int32_t> status_;
+    fm3d_lm_stats stats_{};
+};
+
+}  // namespace compat
+}  // namespace fm3d
+
+#endif  // FM3D_COMPAT_HPP

@@ -1,0 +1,100 @@
+"""The C++ compat shim (include/fm3d_compat.hpp) and the drop-in consumer
+examples/fm3d_main.cpp that mirrors main.cpp:91-155: settings.yml + PGM images +
+keypoint/descriptor side files in, matches / points / normals out."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, oracle_threads
+
+EXE = os.path.join(ROOT, "examples", "fm3d_main")
+
+
+def test_compat_header_compiles():
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "examples", "fm3d_main.cpp")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_example_binary_built_and_usage():
+    assert os.path.exists(EXE), "run __graft_entry__.build() (make -C examples)"
+    r = subprocess.run([EXE], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "usage" in r.stderr
+
+
+def write_pgm(path, img):
+    h, w = img.shape
+    with open(path, "wb") as f:
+        f.write(b"P5\n# fm3d test\n%d %d\n255\n" % (w, h))
+        f.write(np.ascontiguousarray(img, dtype=np.uint8).tobytes())
+
+
+def settings_yml(cam, pos1, pos2, ray, levels, eps):
+    k0, k1, p1, p2, k2 = cam.k
+    f = lambda v: repr(float(v))
+    return f"""%YAML:1.0
+IMAGES:
+   img1: img1.pgm
+   img2: img2.pgm
+   pos1: [{', '.join(f(v) for v in pos1)}]
+   pos2: [{', '.join(f(v) for v in pos2)}]
+NNDR:
+   epsilon: {f(eps)}
+Neighborhoods:
+   epsilonLMMIN: 1e-10
+   pixelsRay: {ray}
+   pyramids: {levels}
+CameraSettings:
+   rodriguesIC: [-1.2005, 1.1981, -1.2041]
+   translationIC: [0.0, 0.015, -0.051]
+   Fx: {f(cam.fx)}
+   Fy: {f(cam.fy)}
+   Cx: {f(cam.cx)}
+   Cy: {f(cam.cy)}
+   p1: {f(p1)}
+   p2: {f(p2)}
+   k0: {f(k0)}
+   k1: {f(k1)}
+   k2: {f(k2)}
+   zThresholdMin: 1.5
+   zThresholdMax: 2.4
+"""
+
+
+@pytest.mark.gpu
+def test_example_main_matches_python_api(fm3d, synth, orc, tmp_path):
+    pair = synth.make_frame_pair(1500, seed=21)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    pair.kp1.astype(np.float32).tofile(d / "kp1.f32")
+    pair.kp2.astype(np.float32).tofile(d / "kp2.f32")
+    pair.desc1.tofile(d / "desc1.u8")
+    pair.desc2.tofile(d / "desc2.u8")
+    (d / "settings.yml").write_text(settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.55))
+    r = subprocess.run([EXE, "-s", str(d / "settings.yml"), "-d", str(d)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    matches = np.fromfile(d / "out_matches.bin", dtype=fm3d.DMATCH)
+    pts = np.fromfile(d / "out_points.f64").reshape(-1, 3)
+    nrm = np.fromfile(d / "out_normals.f64").reshape(-1, 3)
+    # the same calls through the Python mirror of the reference classes
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    ctx = fm3d.Context(s)
+    try:
+        m = fm3d.DescriptorsMatcher(ctx).compareWithNNDR(s.nndrEpsilon, pair.desc1, pair.desc2)
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.setg12(s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+        sct.setKeypoints(pair.kp1, pair.kp2, m)
+        P, _ = sct.triangulate()
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(pair.img1, pair.img2)
+        kept, normals = no.computeOptimizedNormals(P)
+    finally:
+        ctx.close()
+    assert matches.tobytes() == m.tobytes()
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, s.nndrEpsilon, oracle_threads())
+    assert np.array_equal(matches["queryIdx"], q) and np.array_equal(matches["trainIdx"], t)
+    assert len(kept) > 10
+    assert np.array_equal(pts, kept) and np.array_equal(nrm, normals)

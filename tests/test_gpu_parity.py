@@ -288,3 +288,16 @@ def test_pipeline_end_to_end(fm3d, orc, pair):
     assert np.array_equal(rec["trainIdx"], t[mask][ok])
     assert np.array_equal(rec["point"], pts[ok])
     assert np.array_equal(rec["normal"], ref["normals"][ok])
+
+
+def test_sharded_blocks_equal_single_run(fm3d, pair):
+    """Contiguous query blocks with queryOffset (multi-GPU partition, run here one block
+    after the other on one GPU) concatenate to the single-run records byte for byte."""
+    import importlib
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    s = _settings(fm3d, pair.cam, pixelsRay=10, pyramids=2)
+    full = shard.run_shard(pair, s, 0, len(pair.desc1))
+    parts = [shard.run_shard(pair, s, *shard.partition(len(pair.desc1), 3, r)) for r in range(3)]
+    merged = np.concatenate(parts)
+    assert len(full) > 100
+    assert merged.tobytes() == full.tobytes()

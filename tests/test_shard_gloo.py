@@ -1,0 +1,101 @@
+"""Multi-rank sharding of one frame pair on CPU: world size 2 with
+the gloo backend.  Each rank computes its contiguous query block with the CPU oracle
+standing in for the device (tests may call the oracle; the product's shard_fn is the
+GPU path), the records are all-gathered and merged in rank order, and the merge must
+equal the single-process result byte for byte."""
+import importlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def oracle_records(pair, s, lo, hi):
+    """The whole path for queries [lo, hi) on the CPU oracle, as fm3d records."""
+    import oracle as orc
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    q, t, d = orc.match_nndr(pair.desc1[lo:hi], pair.desc2, orc.U8, s.nndrEpsilon, 2)
+    pts, mask = orc.triangulate(pair.cam, pair.g12, s.zThresholdMin, s.zThresholdMax, pair.kp1[lo:hi], pair.kp2,
+                                q, t)
+    R2, t2 = fm3d.camera2_from_g12(pair.g12)
+    r = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts, s.pixelsRay,
+                             mode=orc.DETMATH, nthreads=2)
+    ok = r["status"] == 0
+    rec = np.zeros(int(ok.sum()), dtype=fm3d.RECORD)
+    rec["queryIdx"] = q[mask][ok] + lo
+    rec["trainIdx"] = t[mask][ok]
+    rec["distance"] = d[mask][ok]
+    rec["point"] = pts[ok]
+    rec["normal"] = r["normals"][ok]
+    return rec
+
+
+def _settings(pair):
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.pixelsRay = 6
+    s.pyramids = 1
+    return s
+
+
+def _worker(rank, world, port, q):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        synth = importlib.import_module("3dfeaturematcher_amd.synth")
+        shard = importlib.import_module("3dfeaturematcher_amd.shard")
+        pair = synth.make_frame_pair(301, 160, 120, seed=4)
+        merged = shard.run_sharded(pair, _settings(pair), shard_fn=oracle_records)
+        q.put((rank, merged.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_partition_covers_in_order():
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    for n in (0, 1, 7, 100, 1001):
+        for w in (1, 2, 3, 8):
+            blocks = [shard.partition(n, w, r) for r in range(w)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+            sizes = [hi - lo for lo, hi in blocks]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard.partition(10, 2, 2)
+
+
+def test_sharded_merge_equals_single_run_gloo(synth, fm3d):
+    pair = synth.make_frame_pair(301, 160, 120, seed=4)
+    full = oracle_records(pair, _settings(pair), 0, len(pair.desc1))
+    assert len(full) > 10
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        merged = np.frombuffer(got[r], dtype=fm3d.RECORD)
+        assert merged.tobytes() == full.tobytes(), r
