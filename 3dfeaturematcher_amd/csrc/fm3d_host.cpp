@@ -367,6 +367,11 @@ int ensure_scan_tmp(fm3d_ctx* c, int n) {
 
 // LM kernel register budget: 4 waves/SIMD (3 workgroups per CU) by default;
 // FM3D_LM_WAVES_PER_SIMD=3 selects the 3-wave build (more VGPRs, 2 workgroups per CU)
+bool lm_use_v1() {
+    const char* e = getenv("FM3D_LM_V1");
+    return e && atoi(e) != 0;
+}
+
 const void* lm_kernel_ptr() {
     static const void* k = [] {
         const char* e = getenv("FM3D_LM_WAVES_PER_SIMD");
@@ -392,6 +397,7 @@ void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_st
     }
     st->last_group_start_ticks = (int64_t)(cnt[18] - cnt[20]);
     st->last_group_end_ticks = (int64_t)(cnt[19] - cnt[20]);
+    st->cycles_wait = (int64_t)cnt[24];
 }
 
 // LM normals over nPts device points (c->pts), outputs in c->lm*
@@ -408,27 +414,35 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     HIPCHK(c, c->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
     HIPCHK(c, c->lmQueue.ensure(64 * sizeof(int)));
     HIPCHK(c, c->lmStat.ensure(256));
-    // persistent workgroups of fm3d::kLMSlots points each; slots refill from the queue
+    // persistent workgroups; slots refill from the queue.  Default: the wave-per-point
+    // kernel (fm3d_lm2.hip); FM3D_LM_V1=1 selects the lockstep 4-slot kernel (fm3d_lm.hip).
+    const bool v1 = lm_use_v1();
+    const int slots = v1 ? fm3d::kLMSlots : fm3d::kLM2Slots;
+    const int threads = v1 ? fm3d::kLMThreads : fm3d::kLM2Threads;
+    const void* kptr = v1 ? lm_kernel_ptr() : reinterpret_cast<const void*>(fm3d::lm2_kernel);
     long groups = c->s.lmWaves;
     if (groups <= 0) {
         int dev = 0, cus = 0, perCU = 0;
         HIPCHK(c, hipGetDevice(&dev));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lm_kernel_ptr(), fm3d::kLMThreads, 0));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kptr, threads, 0));
         if (perCU < 1) perCU = 1;
         groups = (long)cus * perCU;
     }
-    const long needed = (P + fm3d::kLMSlots - 1) / fm3d::kLMSlots;
+    const long needed = (P + slots - 1) / slots;
     if (groups > needed) groups = needed;
-    const size_t ents = (size_t)c->nOffPad * fm3d::kLMSlots;
-    const size_t perGroup = ents * (5 * sizeof(double) + sizeof(float) + sizeof(int));
+    const size_t ents = (size_t)c->nOffPad * slots;
+    // v1: 5 double + float + int arrays; v2: 2 double (rays) + 5 32-bit arrays (I1, fvec and
+    // Jacobian dI as float, compact index)
+    const size_t perGroup = v1 ? ents * (5 * sizeof(double) + 2 * sizeof(float)) : ents * (2 * sizeof(double) + 5 * 4);
     const size_t budget = (size_t)48 << 30;  // HBM budget for the per-group pixel slabs
     long cap = (long)(budget / perGroup);
     if (cap < 1) cap = 1;
     if (groups > cap) groups = cap;
     if (groups < 1) groups = 1;
-    HIPCHK(c, c->slab.ensure(ents * 5 * sizeof(double) * groups));
-    HIPCHK(c, c->slabI1.ensure(ents * (sizeof(float) + sizeof(int)) * groups));  // I1 + compact index
+    // +4 KiB: the v2 passes prefetch up to two 64-entry chunks past a slot's last entry
+    HIPCHK(c, c->slab.ensure(ents * (v1 ? 5 : 2) * sizeof(double) * groups + 4096));
+    HIPCHK(c, c->slabI1.ensure(ents * (v1 ? 2 : 5) * 4 * groups + 4096));  // v1: I1 + compact index
     HIPCHK(c, c->lmOrder.ensure((size_t)(P + 1) * sizeof(int)));
     fm3d::LMParams p{};
     p.points = c->pts.as<double>();
@@ -461,12 +475,15 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     c->lmGroups = groups;
     {   // guards against a broken state machine (never expected to trigger): main-loop passes per
         // group <= its points x levels x (300 evaluations + QR passes), and a wall-clock limit
-        long long perGroup = (P + groups - 1) / groups + 1;
+        long long perGroup = (P + groups * slots - 1) / (groups * slots) + 1;
+        if (v1) perGroup = (P + groups - 1) / groups + 1;
         p.maxIter = perGroup * (long long)(levels + 1) * 1600 + 10000;
         int dev = 0, khz = 0;
         HIPCHK(c, hipGetDevice(&dev));
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
-        p.maxTicks = (long long)khz * 1000 * 300;  // 300 s
+        const char* ms = getenv("FM3D_LM_MAX_SECONDS");  // watchdog (tests lower it)
+        const long long secs = ms && atoll(ms) > 0 ? atoll(ms) : 300;
+        p.maxTicks = (long long)khz * 1000 * secs;
         c->wallKhz = khz;
     }
     if (P > 0) {
@@ -478,7 +495,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->lmStatus.p, fm3d::kLMRunning, P, c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmInfo.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmNfev.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
-        auto kern = reinterpret_cast<void (*)(fm3d::LMParams)>(const_cast<void*>(lm_kernel_ptr()));
+        auto kern = reinterpret_cast<void (*)(fm3d::LMParams)>(const_cast<void*>(kptr));
         // diagnostics: FM3D_LM_TRACE=<file> dumps per-point (fetch tick, finish tick, passes,
         // workgroup) as int64 after the launch (see tools/lm_trace.py)
         const char* tr = getenv("FM3D_LM_TRACE");
@@ -490,7 +507,12 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         const char* hv = getenv("FM3D_LM_HEAVY");
         p.heavyPasses = hv ? atoi(hv) : 300;
         const char* ph = getenv("FM3D_LM_PHASED");
-        if (!(ph && atoi(ph))) {
+        if (!v1) {
+            p.levelHi = levels;
+            p.levelLo = 0;
+            hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(threads), 0, c->stream, p);
+            HIPCHK(c, hipGetLastError());
+        } else if (!(ph && atoi(ph))) {
             // one launch: every slot runs its point through all levels (coarsest first,
             // optimize_pyramid :225-241)
             p.levelHi = levels;
@@ -798,7 +820,7 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
     if ((r = run_lm(c, P, stats, c->ev[0], c->ev[1]))) return r;
     std::vector<double> nrm((size_t)P * 3);
     std::vector<int> st(P), inf((size_t)P * 8), nf((size_t)P * 8);
-    unsigned long long cnt[21] = {};
+    unsigned long long cnt[25] = {};
     if (P) {
         HIPCHK(c, hipMemcpyAsync(nrm.data(), c->lmNormals.p, nrm.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(st.data(), c->lmStatus.p, st.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -935,7 +957,7 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
                                  c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
     int kept = 0;
-    unsigned long long cnt[21] = {};
+    unsigned long long cnt[25] = {};
     HIPCHK(c, hipMemcpyAsync(&kept, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));

@@ -1,0 +1,966 @@
+// fm3d_lm2.hip -- NormalOptimizer::computeOptimizedNormals on gfx950: one wavefront per point.
+//
+// Reference: Triangulator/normaloptimizer.cpp:223-452 (optimize_pyramid, optimize,
+// computeOptimizedNormals), the residual evaluateNormal (:65-149) and the
+// SingleCameraTriangulator geometry it calls (singlecameratriangulator.cpp:341-665),
+// minimised by lmfit's lmmin (MINPACK lmdif; fm3d_lmdif.h).
+//
+// Why the sums are sequential: lmdif decides every step at rounding-noise level
+// (ftol = xtol = 30*DBL_EPSILON), so every m_dat-long sum (enorm of fvec, the Jacobian
+// column norms, the Householder dot products) is replayed in MINPACK's pixel order,
+// bit for bit.  Only the ADDS are sequential; everything feeding
+// them is data parallel.
+//
+// Design:
+//   * a workgroup = kW "term" wavefronts + one "chain" wavefront.  Term wave w owns one
+//     point ("slot") at a time, pulls the next point from a global queue when its
+//     point is done, and runs every pass over the point's neighbourhood itself, 64
+//     entries (one per lane) per chunk, with all pass parameters wave-uniform;
+//   * the chain wave's lane 2s+k adds slot s's k-th sum of the current pass in entry
+//     order, fed through a per-slot LDS ring of kR chunks (producer/consumer counters
+//     in LDS, workgroup-scope release/acquire).  Slots never wait for each other: there
+//     is no workgroup barrier in the main loop;
+//   * between passes, lane 0 of the term wave runs the slot's lmdif bookkeeping;
+//   * the first pass of a point compacts its neighbourhood (pixels inside the image
+//     bounds, reference order) and precomputes the undistorted rays, so later passes
+//     stream exactly m_dat entries;
+//   * residuals and Jacobian columns are stored as the float intensity differences
+//     dI they are computed from (4 bytes instead of 8): fvec = w*(double)dI and
+//     J = (w_j*(double)dI_j - fvec)/h_j are recomputed from them with the same IEEE
+//     operations, hence the same bits;
+//   * divisions by a pass-uniform denominator (h_j, the Householder norms) use the
+//     correctly rounded reciprocal and one Markstein correction (two FMAs), which is
+//     exactly IEEE division in the guarded range (mdiv below).
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "fm3d_device.h"
+#include "fm3d_kernels.h"
+#include "fm3d_lmdif.h"
+
+namespace fm3d {
+
+namespace {
+
+using namespace lmdif;
+
+constexpr int kW = kLM2Slots;  // term waves (slots) per workgroup
+constexpr int kE = 64;         // entries per chunk: one per lane
+constexpr int kR = kLM2Ring;   // chunks in flight per slot (LDS ring depth)
+constexpr int kRow = kE + 2;   // padded ring row: consecutive rows start 4 banks apart
+
+enum PassKind2 { Q_IDLE = 0, Q_INIT, Q_LEVEL, Q_EVAL, Q_QR1, Q_QR2, Q_QR3, Q_DONE };
+enum SumKind { S_NONE = 0, S_ENORM, S_DOT };
+
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) int gint;
+typedef __attribute__((address_space(1))) const long long gi64;  // an int2 offset (x low, y high)
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+
+// a / d with y = RN(1/d): q0 = RN(a*y) is within one ulp of a/d, and one Markstein step
+// q0 + (a - d*q0)*y (residual exact by FMA) rounds correctly (round to nearest, no
+// overflow/underflow).  Guarded: mok (pass-uniform) requires 1e-200 < |d| < 1e200, and
+// |a| < 1e100 keeps the quotient normal; outside that, IEEE division.
+__device__ __forceinline__ double mdiv(double a, double d, double y, bool mok) {
+    if (mok && fabs(a) < 1e100) {
+        const double q0 = a * y;
+        const double r = __builtin_fma(-d, q0, a);
+        return __builtin_fma(r, y, q0);
+    }
+    return a / d;
+}
+__device__ __forceinline__ bool mdiv_ok(double d) { return fabs(d) > 1e-200 && fabs(d) < 1e200; }
+
+// enorm terms: x^2 in MINPACK's intermediate range (the branch almost every value
+// takes), +0 otherwise -- an exact no-op on the non-negative running sum.  Values outside
+// the range raise `slow` and the chain lane replays the chunk with the full enorm.
+__device__ __forceinline__ double enorm_term(double x, double agiant, bool& slow) {
+    const double xa = fabs(x);
+    if (xa > 3.834e-20 && xa < agiant) return xa * xa;
+    if (xa != 0.) slow = true;
+    return 0.;
+}
+
+// ---------------------------------------------------------------- LDS state
+// the slot's current pass, written by lane 0 of the slot's term wave
+struct SlotP2 {
+    int pass, ekind, nev, len, pivot, t0, t1, q0, lw;
+    double n0[2], n1[2], n2[2], mm[2], w[2], hj[2];
+    double scale, xmax, ymax, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant, wF;
+    const uint8_t* img1;
+    const uint8_t* img2;
+};
+
+// persistent bookkeeping state of a slot (lane 0 of its term wave only)
+struct SlotS2 {
+    LM s;
+    double X0, X1, X2, ccx, ccy, nrm0, nrm1, nrm2;
+    double apf, aqf, ff, aps, fs, vfirst, r01, tq0, qtf0, wa4s, usecond, ajn0s, tq, ajn1s;
+    double wF, wJ[2];  // weights of the evaluations behind the stored fvec / Jacobian dI values
+    int pidx, m, L, i1ok, ekind, t0, q0, t1, bNaN;
+};
+
+// per-pass results handed to the bookkeeping
+struct PassOut2 {
+    double nrm[2];  // EVAL (per evaluation) / QR2: enorm of the pass's values
+    double sum[2];  // QR1 (a_q and fvec products) / QR3 dot products
+    double aqs1;    // QR2: transformed a_q at the second kept pixel
+    int cnt, fail[2], ph3[2], i1fail;
+};
+
+// what the chain lanes need to know about a pass (written before its first chunk)
+struct PassDesc {
+    int nChunks, id;
+    int kind[2];  // SumKind per chain lane (which = 0, 1)
+    double agiant;
+};
+
+// per-slot views of the slabs: [array][global slot][entry]
+struct Slab {
+    gdouble* RX;
+    gdouble* RY;
+    gfloat* I1;
+    gfloat* DF;  // fvec as float dI (of the last residual evaluation)
+    gfloat* DJ0;
+    gfloat* DJ1;
+    gint* KI;  // compact entry -> neighbourhood offset index
+};
+__device__ inline Slab slab_of(const LMParams& p, long gslot) {
+    const size_t n = (size_t)p.nOffPad, G = (size_t)p.nWaves * kW;
+    Slab s;
+    s.RX = (gdouble*)p.slab + gslot * n;
+    s.RY = s.RX + G * n;
+    s.I1 = (gfloat*)p.slabI1 + gslot * n;
+    s.DF = s.I1 + G * n;
+    s.DJ0 = s.DF + G * n;
+    s.DJ1 = s.DJ0 + G * n;
+    s.KI = (gint*)(s.DJ1 + G * n);
+    return s;
+}
+
+// ---------------------------------------------------------------- bookkeeping
+// lmdif bookkeeping of one slot, run by lane 0 of its term wave between passes.  Lives
+// in LDS: a private object whose address is taken would go to scratch.
+struct Ctl2 {
+    const LMParams* p;
+    Slab sl;
+    double eps;
+    long long cnt_eval, cnt_pix;
+
+    __device__ void fetch(SlotS2& S, SlotP2& P) {
+        const int q = atomicAdd(p->queue, 1);
+        if (q >= p->P) {
+            P.pass = Q_DONE;
+            return;
+        }
+        S.pidx = q;
+        S.X0 = p->points[3 * q + 0];
+        S.X1 = p->points[3 * q + 1];
+        S.X2 = p->points[3 * q + 2];
+        const double Ident[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        const double Zero[3] = {0, 0, 0};
+        double cx, cy;
+        project1(p->cam, Ident, Zero, S.X0, S.X1, S.X2, cx, cy);  // extractPixelsContour(Vec3d) :376-397
+        S.ccx = cx;
+        S.ccy = cy;
+        P.pass = Q_INIT;
+        P.len = p->nOffPad;
+        P.ccx = cx;
+        P.ccy = cy;
+    }
+    __device__ void start_level(SlotS2& S, SlotP2& P) {
+        const LevelDesc lv = p->lvl[S.L];
+        P.pass = Q_LEVEL;
+        P.len = S.m;
+        P.scale = ldexp(1.0, -S.L);  // 1.0 / float(2^L)  (optimize_pyramid, :225-241)
+        P.xmax = (1 / P.scale) * lv.w;
+        P.ymax = (1 / P.scale) * lv.h;
+        P.img1 = lv.img1;
+        P.img2 = lv.img2;
+        P.lw = lv.w;
+        P.ccx = S.ccx;
+        P.ccy = S.ccy;
+    }
+    __device__ void finish_point(SlotS2& S, SlotP2& P, int code) {
+        p->status[S.pidx] = code;
+        p->normals[3 * S.pidx + 0] = S.nrm0;
+        p->normals[3 * S.pidx + 1] = S.nrm1;
+        p->normals[3 * S.pidx + 2] = S.nrm2;
+        p->mdat[S.pidx] = S.m;
+        fetch(S, P);
+    }
+    __device__ void level_done(SlotS2& S, SlotP2& P, int info) {
+        p->info[8 * S.pidx + S.L] = info;
+        p->nfev[8 * S.pidx + S.L] = S.s.nfev;
+        sph2car_det(S.s.x[0], S.s.x[1], S.nrm0, S.nrm1, S.nrm2);
+        S.L--;
+        if (S.L < 0)
+            finish_point(S, P, FM3D_ST_OK);
+        else
+            start_level(S, P);
+    }
+    __device__ void abort_level(SlotS2& S, SlotP2& P, int code) {
+        p->info[8 * S.pidx + S.L] = -code;
+        p->nfev[8 * S.pidx + S.L] = S.s.nfev;
+        finish_point(S, P, code);
+    }
+    // evaluateNormal (normaloptimizer.cpp:65-149), per-call part, for evaluation ev.
+    // Returns false if the normal is NaN (the call aborts before touching a pixel).
+    __device__ bool setup_eval(SlotS2& S, SlotP2& P, int ev, double a, double b, double hj) {
+        double n0, n1, n2;
+        sph2car_det(a, b, n0, n1, n2);  // par = (phi, theta)
+        if (n2 != n2 || n1 != n1 || n0 != n0) return false;
+        double w_theta = 1.0, w_phi = 1.0;
+        if (fabs(b) - M_PI / 2 > 0 || fabs(a) - M_PI > 0) {
+            w_theta = fm3d_exp(fabs(b) - M_PI / 2) + 1;
+            w_phi = fm3d_exp(fabs(a) - M_PI + 1) + 1;
+        }
+        P.n0[ev] = n0;
+        P.n1[ev] = n1;
+        P.n2[ev] = n2;
+        P.mm[ev] = n0 * S.X0 + n1 * S.X1 + n2 * S.X2;
+        P.w[ev] = w_phi * w_theta;
+        P.hj[ev] = hj;
+        return true;
+    }
+    __device__ void count_eval(SlotS2& S) {
+        S.s.nfev++;
+        cnt_eval++;
+        cnt_pix += S.m;
+    }
+    __device__ void eval_pass(SlotS2& S, SlotP2& P, int kind, double a, double b) {
+        count_eval(S);
+        if (!setup_eval(S, P, 0, a, b, 1.0)) {
+            abort_level(S, P, FM3D_ST_NAN_NORMAL);
+            return;
+        }
+        S.ekind = kind;
+        S.wF = P.w[0];  // this pass rewrites the stored fvec
+        P.pass = Q_EVAL;
+        P.len = S.m;
+        P.ekind = kind;
+        P.nev = 1;
+        P.agiant = 1.304e19 / (double)S.m;
+    }
+    // fdjac2: column j = 0 at (x0 + h0, x1), column j = 1 at (x0, x1 + h1)
+    __device__ void jac_pass(SlotS2& S, SlotP2& P) {
+        LM& s = S.s;
+        s.h[0] = eps * fabs(s.x[0]);
+        if (s.h[0] == 0.) s.h[0] = eps;
+        s.h[1] = eps * fabs(s.x[1]);
+        if (s.h[1] == 0.) s.h[1] = eps;
+        count_eval(S);
+        if (!setup_eval(S, P, 0, s.x[0] + s.h[0], s.x[1], s.h[0])) {
+            abort_level(S, P, FM3D_ST_NAN_NORMAL);
+            return;
+        }
+        // column 1's call only happens if column 0's succeeds: counted after the pass
+        S.bNaN = !setup_eval(S, P, 1, s.x[0], s.x[1] + s.h[1], s.h[1]);
+        S.wJ[0] = P.w[0];
+        S.wJ[1] = P.w[1];
+        S.ekind = E_JAC;
+        P.pass = Q_EVAL;
+        P.len = S.m;
+        P.ekind = E_JAC;
+        P.nev = S.bNaN ? 1 : 2;
+        P.agiant = 1.304e19 / (double)S.m;
+        P.wF = S.wF;
+    }
+    // stored fvec / Jacobian column values at entry e (the passes' own operations)
+    __device__ double fvec_at(const SlotS2& S, int e) const { return S.wF * (double)sl.DF[e]; }
+    __device__ double jcol_at(const SlotS2& S, int j, int e) const {
+        const double F = fvec_at(S, e);
+        const double r = S.wJ[j] * (double)(j ? sl.DJ1 : sl.DJ0)[e];
+        return (r - F) / S.s.h[j];
+    }
+    __device__ void finalize_qr(SlotS2& S, SlotP2& P, double qtf1) {
+        S.s.r[0] = S.t0 ? -S.ajn0s : 0.;
+        S.s.r[1] = 0.;
+        S.s.r[2] = S.r01;
+        S.s.r[3] = S.t1 ? -S.ajn1s : 0.;
+        S.s.qtf[0] = S.qtf0;
+        S.s.qtf[1] = qtf1;
+        int info = lm_after_qr(S.s);
+        if (info) {
+            level_done(S, P, info);
+        } else {
+            lm_inner_step(S.s);
+            eval_pass(S, P, E_TRIAL, S.s.wa2[0], S.s.wa2[1]);
+        }
+    }
+    // qrfac with column pivoting for n = 2, on the Jacobian columns of the slab
+    __device__ void start_qr(SlotS2& S, SlotP2& P) {
+        LM& s = S.s;
+        const int pc = (s.acnorm[1] > s.acnorm[0]) ? 1 : 0;  // pivot column = larger norm
+        s.ipvt[0] = pc;
+        s.ipvt[1] = 1 - pc;
+        S.apf = jcol_at(S, pc, 0);
+        S.aqf = jcol_at(S, 1 - pc, 0);
+        S.ff = fvec_at(S, 0);
+        S.aps = jcol_at(S, pc, 1);
+        S.fs = fvec_at(S, 1);
+        const double ajn0 = s.acnorm[pc];  // == enorm of the pivot column (same elements, same order)
+        S.t0 = ajn0 != 0.;
+        S.ajn0s = (S.t0 && S.apf < 0.) ? -ajn0 : ajn0;
+        if (!S.t0) S.ajn0s = 1.;  // unused
+        S.vfirst = S.t0 ? (S.apf / S.ajn0s) + 1. : S.apf;
+        P.pivot = pc;
+        P.len = S.m;
+        P.t0 = S.t0;
+        P.ajn0s = S.ajn0s;
+        P.wF = S.wF;
+        P.w[0] = S.wJ[0];
+        P.w[1] = S.wJ[1];
+        P.hj[0] = s.h[0];
+        P.hj[1] = s.h[1];
+        if (S.t0) {
+            P.pass = Q_QR1;
+        } else {
+            S.tq = 0.;
+            S.r01 = S.aqf;
+            S.q0 = 0;  // vfirst == apf == 0
+            S.tq0 = 0.;
+            S.qtf0 = S.ff;
+            qr2(S, P);
+        }
+    }
+    __device__ void qr2(SlotS2& S, SlotP2& P) {
+        P.pass = Q_QR2;
+        P.tq = S.tq;
+        P.agiant = 1.304e19 / (double)(S.m - 1);
+    }
+    __device__ static int fail_code(int fail, int ph3, int i1ok) {
+        if (fail != 0x7fffffff)  // first failing pixel in index order decides (:455-470, :557-560)
+            return (fail & 3) == 2 ? FM3D_ST_NAN_PLANE : FM3D_ST_ABORT_BBOX;
+        if (!i1ok) return FM3D_ST_ABORT_PIX1;
+        if (ph3) return FM3D_ST_ABORT_PIX2;
+        return 0;
+    }
+
+    __device__ __noinline__ void after_pass(SlotS2& S, SlotP2& P, const PassOut2& o) {
+        const int ps = P.pass;
+        if (ps == Q_INIT) {
+            S.m = o.cnt;
+            // initial guess: X / norm(X) == X * (1/norm) (Vec3d operator/, :342-343)
+            double nr = sqrt(S.X0 * S.X0 + S.X1 * S.X1 + S.X2 * S.X2);
+            double inv = 1. / nr;
+            S.nrm0 = S.X0 * inv;
+            S.nrm1 = S.X1 * inv;
+            S.nrm2 = S.X2 * inv;
+            if (S.m <= 0) {
+                finish_point(S, P, FM3D_ST_NO_PIXELS);
+            } else {
+                S.L = p->levels;
+                start_level(S, P);
+            }
+        } else if (ps == Q_LEVEL) {
+            S.i1ok = o.i1fail ? 0 : 1;
+            // car2sph (tools.cpp:767-771) -> lmdif from the current normal
+            S.s.x[1] = fm3d_atan2(S.nrm2, sqrt(S.nrm0 * S.nrm0 + S.nrm1 * S.nrm1));
+            S.s.x[0] = fm3d_atan2(S.nrm1, S.nrm0);
+            S.s.nfev = 0;
+            S.s.iter = 1;
+            S.s.par = 0.;
+            S.s.delta = 0.;
+            S.s.xnorm = 0.;
+            if (S.m < 2)
+                level_done(S, P, 0);  // lmdif: m < n -> improper input, info 0, no evaluation
+            else
+                eval_pass(S, P, E_INITIAL, S.s.x[0], S.s.x[1]);
+        } else if (ps == Q_EVAL) {
+            int code = fail_code(o.fail[0], o.ph3[0], S.i1ok);
+            if (code) {
+                abort_level(S, P, code);
+                return;
+            }
+            LM& s = S.s;
+            if (S.ekind == E_INITIAL) {
+                s.fnorm = o.nrm[0];
+                jac_pass(S, P);
+            } else if (S.ekind == E_JAC) {
+                s.acnorm[0] = o.nrm[0];
+                count_eval(S);  // fdjac2's call for column 1
+                if (S.bNaN) {
+                    abort_level(S, P, FM3D_ST_NAN_NORMAL);
+                    return;
+                }
+                code = fail_code(o.fail[1], o.ph3[1], S.i1ok);
+                if (code) {
+                    abort_level(S, P, code);
+                    return;
+                }
+                s.acnorm[1] = o.nrm[1];
+                start_qr(S, P);
+            } else {
+                bool accepted;
+                int info = lm_after_trial(s, o.nrm[0], &accepted);
+                if (info) {
+                    level_done(S, P, info);
+                } else if (accepted) {
+                    jac_pass(S, P);
+                } else {
+                    lm_inner_step(s);
+                    eval_pass(S, P, E_TRIAL, s.wa2[0], s.wa2[1]);
+                }
+            }
+        } else if (ps == Q_QR1) {
+            // qrfac j = 0: temp = sum v a_q / v_first; lmdif qtf j = 0: temp = -sum v f / v_first
+            S.tq = o.sum[0] / S.vfirst;
+            S.r01 = S.aqf - S.tq * S.vfirst;
+            S.q0 = S.vfirst != 0.;
+            S.tq0 = 0.;
+            S.qtf0 = S.ff;
+            if (S.q0) {
+                S.tq0 = -o.sum[1] / S.vfirst;
+                S.qtf0 = S.ff + S.vfirst * S.tq0;
+            }
+            qr2(S, P);
+        } else if (ps == Q_QR2) {
+            const double ajn1 = o.nrm[0];
+            S.t1 = ajn1 != 0.;
+            S.ajn1s = (S.t1 && o.aqs1 < 0.) ? -ajn1 : ajn1;
+            if (!S.t1) S.ajn1s = 1.;  // unused
+            S.usecond = S.t1 ? (o.aqs1 / S.ajn1s) + 1. : o.aqs1;
+            S.wa4s = S.q0 ? S.fs + (S.aps / S.ajn0s) * S.tq0 : S.fs;
+            if (S.usecond != 0.) {
+                P.pass = Q_QR3;
+                P.t1 = S.t1;
+                P.ajn1s = S.ajn1s;
+                P.q0 = S.q0;
+                P.tq0 = S.tq0;
+            } else {
+                finalize_qr(S, P, S.wa4s);
+            }
+        } else if (ps == Q_QR3) {
+            const double tq1 = -o.sum[0] / S.usecond;
+            finalize_qr(S, P, S.wa4s + S.usecond * tq1);
+        }
+    }
+};
+
+struct Shared {
+    double ring[kW][kR][2][kRow];  // chunk terms [slot][ring position][sum][entry]
+    int chunkSlow[kW][kR];         // bit k: sum k of that chunk holds raw values (enorm slow path)
+    int produced[kW];              // chunks produced, per slot (monotonic)
+    int consumed[kW][2];           // chunks consumed, per chain lane (monotonic)
+    int resultId[kW][2];           // id of the last pass whose result is published
+    double result[kW][2];
+    int done[kW];
+    PassDesc pd[kW];
+    SlotP2 sp[kW];
+    SlotS2 ss[kW];
+    PassOut2 out[kW];
+    Ctl2 ctl[kW];
+    LMParams P;
+};
+
+__device__ __forceinline__ int lds_load_acq(int* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// sum += t[0..64) in index order: 64 dependent adds fed by ds_read_b128 one batch ahead
+__device__ __forceinline__ double chain_sum64(double sum, const double* t) {
+    const double2* t2 = reinterpret_cast<const double2*>(t);
+    double2 cur[8], nxt[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) cur[i] = t2[i];
+#pragma unroll
+    for (int q = 16; q < kE; q += 16) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) nxt[i] = t2[q / 2 + i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            sum += cur[i].x;
+            sum += cur[i].y;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) cur[i] = nxt[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        sum += cur[i].x;
+        sum += cur[i].y;
+    }
+    return sum;
+}
+
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---------------------------------------------------------------- term wave
+// Publishes chunk `seq` of slot w: waits for ring space, writes the two term rows,
+// releases the produced counter.
+struct Producer {
+    Shared* sh;
+    int w, lane;
+    int seq;
+    long long waitCycles;
+
+    __device__ __forceinline__ void put(double t0, double t1, int slowBits) {
+        double* row0 = &sh->ring[w][seq % kR][0][0];
+        if (seq >= kR) {
+            // ring space: both chain lanes of the slot have consumed chunk seq - kR
+            const long long c0 = clock64();
+            while (min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])) <= seq - kR)
+                __builtin_amdgcn_s_sleep(1);
+            waitCycles += clock64() - c0;
+        }
+        row0[lane] = t0;
+        row0[kRow + lane] = t1;
+        if (lane == 0) sh->chunkSlow[w][seq % kR] = slowBits;
+        // every lane's ring stores are done before lane 0 publishes (lgkmcnt is per wave)
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        if (lane == 0) lds_store_rel(&sh->produced[w], seq + 1);
+        seq++;
+    }
+};
+
+// one residual evaluation of a neighbourhood entry: projectPointToPlane (:421-470),
+// isInBoundingBox (:646-655), projectPointsToImage2 (:591-644) -> gather address
+struct Geo {
+    float fx, fy;
+    const gu8* g;
+    int code;  // 0 ok, 2 NaN plane, 3 bounding box, 4 image-2 pixel outside
+};
+
+__device__ __forceinline__ Geo geometry(const LMParams& p, double ux, double uy, double n0, double n1, double n2,
+                                        double mm, double scale, double xmax, double ymax, const uint8_t* img2,
+                                        int lw, double cm) {
+    Geo r;
+    double nn = n0 * ux + n1 * uy + n2 * 1.;
+    double kk = mm / nn;
+    double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+    int cd = 0;
+    if (P0 != P0 || P1 != P1 || P2 != P2)
+        cd = 2;
+    else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
+        cd = 3;
+    double u, v;
+    project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
+    if (cd == 0 && !pixel_good_b(u, v, xmax, ymax)) cd = 4;
+    r.code = cd;
+    r.fx = (float)(scale * u);
+    r.fy = (float)(scale * v);
+    r.g = (const gu8*)img2;
+    if (cd == 0) r.g += (long)(int)floorf(r.fy) * lw + (int)floorf(r.fx);
+    return r;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel(LMParams p) {
+    __shared__ Shared sh;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long tStart = wall_clock64(), cyStart = clock64();
+    if (tid == 0) sh.P = p;
+    if (tid < kW) {
+        sh.produced[tid] = 0;
+        sh.consumed[tid][0] = sh.consumed[tid][1] = 0;
+        sh.resultId[tid][0] = sh.resultId[tid][1] = 0;
+        sh.done[tid] = 0;
+    }
+    __syncthreads();
+
+    if (wave < kW) {
+        // ======================= term wave: slot w =======================
+        const int w = wave;
+        const long gslot = (long)blockIdx.x * kW + w;
+        Ctl2& ctl = sh.ctl[w];
+        const Slab sl = slab_of(p, gslot);
+        if (lane == 0) {
+            ctl.p = &sh.P;
+            ctl.sl = sl;
+            ctl.eps = sqrt(p.epsfcn > DBL_EPSILON ? p.epsfcn : DBL_EPSILON);
+            ctl.cnt_eval = 0;
+            ctl.cnt_pix = 0;
+        }
+        SlotP2& SP = sh.sp[w];
+        SlotS2& SS = sh.ss[w];
+        PassOut2& OUT = sh.out[w];
+        Producer prod{&sh, w, lane, 0, 0};
+        const double cm = (double)p.cmax;
+        const gi64* __restrict__ offsets = (const gi64*)p.offsets;
+        const unsigned long long ltMask = (1ull << lane) - 1;
+        int passId = 0;
+        long long nPass = 0, iterations = 0;
+        unsigned long long cyCtl = 0, cyTerms = 0, clsCnt[4] = {0, 0, 0, 0}, clsCyc[4] = {0, 0, 0, 0};
+        if (lane == 0) ctl.fetch(SS, SP);
+        for (;;) {
+            if (++iterations > p.maxIter || (long long)(wall_clock64() - tStart) > p.maxTicks) {
+                if (lane == 0) atomicExch(p.overflow, 1);  // cannot happen for a correct state machine
+                break;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const int pass = rfl(SP.pass);
+            if (pass == Q_DONE) break;
+            const unsigned long long tp0 = clock64();
+            const int len = rfl(SP.len);
+            const int nCh = (len + kE - 1) / kE;
+            int cls = 3;
+            if (pass == Q_INIT) {
+                // ---- extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH) in
+                // offset order -> compact entries; undistorted rays (get3dPointsFromImage1Pixels :542)
+                const double ccx = SP.ccx, ccy = SP.ccy;
+                int base = 0;
+                for (int k = 0; k < nCh; k++) {
+                    const int e = k * kE + lane;
+                    const long long o2 = offsets[e];
+                    const double px = ccx + (double)(int)o2, py = ccy + (double)(int)(o2 >> 32);
+                    const bool v = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+                    const unsigned long long bm = __ballot(v);
+                    if (v) {
+                        const int pos = base + __popcll(bm & ltMask);
+                        double ux, uy;
+                        undistort1(p.cam, px, py, ux, uy);
+                        sl.RX[pos] = ux;
+                        sl.RY[pos] = uy;
+                        sl.KI[pos] = e;
+                    }
+                    base += __popcll(bm);
+                }
+                if (lane == 0) OUT.cnt = base;
+            } else if (pass == Q_LEVEL) {
+                // ---- updateImage1PixelsIntensity (:576-589)
+                const double ccx = SP.ccx, ccy = SP.ccy, scale = SP.scale, xmax = SP.xmax, ymax = SP.ymax;
+                const gu8* img1 = (const gu8*)SP.img1;
+                const int lw = rfl(SP.lw);
+                bool bad = false;
+                for (int k = 0; k < nCh; k++) {
+                    const int e = k * kE + lane;
+                    if (e < len) {
+                        const long long o2 = offsets[sl.KI[e]];
+                        const double px = ccx + (double)(int)o2, py = ccy + (double)(int)(o2 >> 32);
+                        if (!pixel_good_b(px, py, xmax, ymax)) {
+                            bad = true;
+                        } else {
+                            const float fx = (float)(scale * px), fy = (float)(scale * py);
+                            const gu8* g = img1 + (long)(int)floorf(fy) * lw + (int)floorf(fx);
+                            sl.I1[e] = bilinear4(g[0], g[1], g[lw], g[lw + 1], fx, fy);
+                        }
+                    }
+                }
+                const bool anyBad = __ballot(bad) != 0;
+                if (lane == 0) OUT.i1fail = anyBad ? 1 : 0;
+            } else {
+                // ---- a summed pass: terms here, sums by the chain lanes
+                passId++;
+                nPass++;
+                const int ekind = rfl(SP.ekind);
+                const int nev = rfl(SP.nev);
+                const bool jac = pass == Q_EVAL && ekind == E_JAC;
+                cls = jac ? 0 : (pass == Q_EVAL ? 1 : 2);
+                const double agiant = SP.agiant;
+                if (lane == 0) {
+                    PassDesc& d = sh.pd[w];
+                    d.nChunks = nCh;
+                    d.id = passId;
+                    d.agiant = agiant;
+                    d.kind[0] = (pass == Q_QR1 || pass == Q_QR3) ? S_DOT : S_ENORM;
+                    d.kind[1] = pass == Q_QR1 ? S_DOT : ((pass == Q_EVAL && nev == 2) ? S_ENORM : S_NONE);
+                }
+                int fail0 = 0x7fffffff, fail1 = 0x7fffffff, ph30 = 0, ph31 = 0;
+                double aqs1 = 0.;
+                if (pass == Q_EVAL) {
+                    const double n00 = SP.n0[0], n10 = SP.n1[0], n20 = SP.n2[0], mm0 = SP.mm[0], w0 = SP.w[0];
+                    const double n01 = SP.n0[1], n11 = SP.n1[1], n21 = SP.n2[1], mm1 = SP.mm[1], w1 = SP.w[1];
+                    const double h0 = SP.hj[0], h1 = SP.hj[1], wF = SP.wF;
+                    const double y0 = 1. / h0, y1 = 1. / h1;
+                    const bool mok0 = mdiv_ok(h0), mok1 = mdiv_ok(h1);
+                    const double scale = SP.scale, xmax = SP.xmax, ymax = SP.ymax;
+                    const uint8_t* img2 = SP.img2;
+                    const int lw = rfl(SP.lw);
+                    const bool i1ok = rfl(SS.i1ok) != 0;
+                    // NEV evaluations per entry (2: both forward-difference columns); JAC: the
+                    // values are Jacobian columns (r - fvec)/h_j, else the residual fvec itself
+                    auto run = [&](auto nevc, auto jacc) {
+                        constexpr int NEV = decltype(nevc)::value;
+                        constexpr bool JAC = decltype(jacc)::value;
+                        struct Ld {
+                            double ux, uy, dF;
+                            float i1;
+                        };
+                        // entries past len (up to two chunks past the pass) read slab padding
+                        auto load = [&](int k) {
+                            Ld L;
+                            const int e = k * kE + lane;
+                            L.ux = sl.RX[e];
+                            L.uy = sl.RY[e];
+                            L.i1 = sl.I1[e];
+                            L.dF = JAC ? (double)sl.DF[e] : 0.;
+                            return L;
+                        };
+                        auto chunk = [&](const Ld& L, int k) {
+                            const int e = k * kE + lane;
+                            const bool in = e < len;
+                            const Geo g0 = geometry(p, L.ux, L.uy, n00, n10, n20, mm0, scale, xmax, ymax, img2, lw, cm);
+                            Geo g1;
+                            if (NEV == 2)
+                                g1 = geometry(p, L.ux, L.uy, n01, n11, n21, mm1, scale, xmax, ymax, img2, lw, cm);
+                            // gathers for every lane: a failed entry's address is the image base
+                            const uint8_t a00 = g0.g[0], a01 = g0.g[1], a10 = g0.g[lw], a11 = g0.g[lw + 1];
+                            uint8_t c00 = 0, c01 = 0, c10 = 0, c11 = 0;
+                            if (NEV == 2) {
+                                c00 = g1.g[0];
+                                c01 = g1.g[1];
+                                c10 = g1.g[lw];
+                                c11 = g1.g[lw + 1];
+                            }
+                            // failures: first NaN-plane / bounding-box pixel in index order; image-2 flags
+                            {
+                                const unsigned long long b0 = __ballot(in && (g0.code == 2 || g0.code == 3));
+                                if (b0 && fail0 == 0x7fffffff) {
+                                    const int l = __ffsll((long long)b0) - 1;
+                                    fail0 = (k * kE + l) * 4 + __shfl(g0.code, l);
+                                }
+                                ph30 |= __ballot(in && g0.code == 4) != 0;
+                                if (NEV == 2) {
+                                    const unsigned long long b1 = __ballot(in && (g1.code == 2 || g1.code == 3));
+                                    if (b1 && fail1 == 0x7fffffff) {
+                                        const int l = __ffsll((long long)b1) - 1;
+                                        fail1 = (k * kE + l) * 4 + __shfl(g1.code, l);
+                                    }
+                                    ph31 |= __ballot(in && g1.code == 4) != 0;
+                                }
+                            }
+                            // evaluateNormal :145-148 (fvec), fdjac2 forward differences (JAC)
+                            const float dI0 = L.i1 - bilinear4(a00, a01, a10, a11, g0.fx, g0.fy);
+                            const double r0 = w0 * (double)dI0;
+                            double v0 = JAC ? mdiv(r0 - wF * L.dF, h0, y0, mok0) : r0;
+                            v0 = (in && i1ok && g0.code == 0) ? v0 : 0.;
+                            if (JAC)
+                                sl.DJ0[e] = dI0;
+                            else
+                                sl.DF[e] = dI0;
+                            bool slow0 = false, slow1 = false;
+                            const double t0 = enorm_term(v0, agiant, slow0);
+                            double v1 = 0., t1 = 0.;
+                            if (NEV == 2) {
+                                const float dI1 = L.i1 - bilinear4(c00, c01, c10, c11, g1.fx, g1.fy);
+                                const double r1 = w1 * (double)dI1;
+                                v1 = mdiv(r1 - wF * L.dF, h1, y1, mok1);
+                                v1 = (in && i1ok && g1.code == 0) ? v1 : 0.;
+                                sl.DJ1[e] = dI1;
+                                t1 = enorm_term(v1, agiant, slow1);
+                            }
+                            const bool s0 = __ballot(slow0) != 0, s1 = __ballot(slow1) != 0;
+                            prod.put(s0 ? v0 : t0, s1 ? v1 : t1, (s0 ? 1 : 0) | (s1 ? 2 : 0));
+                        };
+                        // two chunks of slab loads in flight ahead of the one being computed
+                        Ld A = load(0), B = load(1);
+                        for (int k = 0; k < nCh; k += 2) {
+                            const Ld C = load(k + 2);
+                            chunk(A, k);
+                            A = C;
+                            if (k + 1 < nCh) {
+                                const Ld D = load(k + 3);
+                                chunk(B, k + 1);
+                                B = D;
+                            }
+                        }
+                    };
+                    if (nev == 2)
+                        run(std::integral_constant<int, 2>(), std::true_type());
+                    else if (jac)
+                        run(std::integral_constant<int, 1>(), std::true_type());
+                    else
+                        run(std::integral_constant<int, 1>(), std::false_type());
+                } else {
+                    // ---- Householder passes (qrfac / lmdif qtf for n = 2) on the stored columns
+                    const int pc = rfl(SP.pivot), t0f = rfl(SP.t0), t1f = rfl(SP.t1), q0f = rfl(SP.q0);
+                    const double wF = SP.wF, wp = SP.w[pc], wq = SP.w[1 - pc], hp = SP.hj[pc], hq = SP.hj[1 - pc];
+                    const double yp = 1. / hp, yq = 1. / hq;
+                    const bool mokp = mdiv_ok(hp), mokq = mdiv_ok(hq);
+                    const double ajn0s = SP.ajn0s, ya0 = 1. / ajn0s, tq = SP.tq;
+                    const bool moka0 = mdiv_ok(ajn0s);
+                    const double ajn1s = SP.ajn1s, ya1 = 1. / ajn1s, tq0 = SP.tq0;
+                    const bool moka1 = mdiv_ok(ajn1s);
+                    const gfloat* Dp = pc ? sl.DJ1 : sl.DJ0;
+                    const gfloat* Dq = pc ? sl.DJ0 : sl.DJ1;
+                    auto run = [&](auto kindc) {
+                        constexpr int KIND = decltype(kindc)::value;
+                        struct Ld {
+                            float p, q, f;
+                        };
+                        auto load = [&](int k) {
+                            Ld L;
+                            const int e = k * kE + lane;
+                            L.p = Dp[e];
+                            L.q = Dq[e];
+                            L.f = sl.DF[e];
+                            return L;
+                        };
+                        auto chunk = [&](const Ld& L, int k) {
+                            const int e = k * kE + lane;
+                            const bool in = e < len;
+                            // the stored columns: F = wF*dI_F, J_j = (w_j*dI_j - F)/h_j (as the JAC pass)
+                            const double F = wF * (double)L.f;
+                            const double ap = mdiv(wp * (double)L.p - F, hp, yp, mokp);
+                            const double aq = mdiv(wq * (double)L.q - F, hq, yq, mokq);
+                            double t0 = 0., t1 = 0., a = 0.;
+                            bool slow = false;
+                            if (KIND == Q_QR1) {
+                                // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); v*a_q, v*f
+                                double v = mdiv(ap, ajn0s, ya0, moka0);
+                                if (e == 0) v = v + 1.;
+                                t0 = in ? v * aq : 0.;
+                                t1 = in ? v * F : 0.;
+                            } else if (KIND == Q_QR2) {
+                                // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
+                                a = aq;
+                                if (t0f) a = a - tq * mdiv(ap, ajn0s, ya0, moka0);
+                                a = (in && e > 0) ? a : 0.;
+                                if (e == 1) aqs1 = a;
+                                t0 = enorm_term(a, agiant, slow);
+                            } else {
+                                // lmdif qtf, j = 1: u_i * wa4_i
+                                const double v = t0f ? mdiv(ap, ajn0s, ya0, moka0) : 0.;
+                                double b = aq;
+                                if (t0f) b = b - tq * v;
+                                double u = t1f ? mdiv(b, ajn1s, ya1, moka1) : b;
+                                if (t1f && e == 1) u = u + 1.;
+                                double wa = F;
+                                if (q0f) wa = wa + v * tq0;
+                                t0 = (in && e > 0) ? u * wa : 0.;
+                            }
+                            const bool sl0 = __ballot(slow) != 0;
+                            prod.put(sl0 ? a : t0, t1, sl0 ? 1 : 0);
+                        };
+                        Ld A = load(0), B = load(1);
+                        for (int k = 0; k < nCh; k += 2) {
+                            const Ld C = load(k + 2);
+                            chunk(A, k);
+                            A = C;
+                            if (k + 1 < nCh) {
+                                const Ld D = load(k + 3);
+                                chunk(B, k + 1);
+                                B = D;
+                            }
+                        }
+                    };
+                    if (pass == Q_QR1)
+                        run(std::integral_constant<int, Q_QR1>());
+                    else if (pass == Q_QR2)
+                        run(std::integral_constant<int, Q_QR2>());
+                    else
+                        run(std::integral_constant<int, Q_QR3>());
+                    aqs1 = __shfl(aqs1, 1);  // QR2: entry 1 lives in lane 1 of chunk 0
+                }
+                // ---- the chain lanes' results of this pass
+                {
+                    const long long c0 = clock64();
+                    while (lds_load_acq(&sh.resultId[w][0]) != passId || lds_load_acq(&sh.resultId[w][1]) != passId)
+                        __builtin_amdgcn_s_sleep(1);
+                    prod.waitCycles += clock64() - c0;
+                }
+                if (lane == 0) {
+                    OUT.nrm[0] = OUT.sum[0] = sh.result[w][0];
+                    OUT.nrm[1] = OUT.sum[1] = sh.result[w][1];
+                    OUT.fail[0] = fail0;
+                    OUT.fail[1] = fail1;
+                    OUT.ph3[0] = ph30;
+                    OUT.ph3[1] = ph31;
+                    OUT.aqs1 = aqs1;
+                }
+            }
+            // every lane's slab and LDS stores are done before the bookkeeping reads them
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const unsigned long long tp1 = clock64();
+            if (lane == 0) ctl.after_pass(SS, SP, OUT);
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long tp2 = clock64();
+            cyTerms += tp1 - tp0;
+            cyCtl += tp2 - tp1;
+            clsCnt[cls]++;
+            clsCyc[cls] += tp2 - tp0;
+        }
+        if (lane == 0) {
+            lds_store_rel(&sh.done[w], 1);
+            atomicAdd(p.statEval, (unsigned long long)ctl.cnt_eval);
+            atomicAdd(p.statPix, (unsigned long long)ctl.cnt_pix);
+            atomicAdd(p.statPass + 0, (unsigned long long)nPass);
+            atomicAdd(p.statPass + 1, cyTerms);
+            atomicAdd(p.statPass + 3, cyCtl);
+            for (int k = 0; k < 4; k++) {
+                atomicAdd(p.statPass + 7 + k, clsCnt[k]);
+                atomicAdd(p.statPass + 11 + k, clsCyc[k]);
+            }
+            atomicAdd(p.statPass + 21, (unsigned long long)prod.waitCycles);
+        }
+    } else {
+        // ======================= chain wave =======================
+        // the chain's dependent adds bound a pass's last chunk: let it issue first
+        __builtin_amdgcn_s_setprio(3);
+        const int s = lane >> 1, which = lane & 1;
+        bool alive = s < kW;
+        const int ss_ = alive ? s : 0;
+        int cur = 0, rem = 0, kind = S_NONE, pid = 0;
+        bool inPass = false;
+        Enorm en;
+        en.init(1);
+        double dsum = 0.;
+        unsigned long long busy = 0;
+        for (;;) {
+            if ((long long)(wall_clock64() - tStart) > p.maxTicks) break;
+            if (!__any(alive)) break;
+            const int pr = alive ? lds_load_acq(&sh.produced[ss_]) : 0;
+            const bool have = alive && pr > cur;
+            if (have && !inPass) {
+                const PassDesc& d = sh.pd[ss_];
+                rem = d.nChunks;
+                kind = d.kind[which];
+                pid = d.id;
+                en.init(1);
+                en.agiant = d.agiant;
+                dsum = 0.;
+                inPass = true;
+            }
+            if (__any(have)) {
+                const unsigned long long c0 = clock64();
+                if (have) {
+                    const int pos = cur % kR;
+                    const double* row = &sh.ring[ss_][pos][which][0];
+                    if (kind == S_ENORM) {
+                        if ((sh.chunkSlow[ss_][pos] >> which) & 1) {
+                            for (int i = 0; i < kE; i++) en.add(row[i]);
+                        } else {
+                            en.s2 = chain_sum64(en.s2, row);
+                        }
+                    } else if (kind == S_DOT) {
+                        dsum = chain_sum64(dsum, row);
+                    }
+                    cur++;
+                    lds_store_rel(&sh.consumed[ss_][which], cur);
+                    if (--rem == 0) {
+                        sh.result[ss_][which] = kind == S_ENORM ? en.finish() : dsum;
+                        lds_store_rel(&sh.resultId[ss_][which], pid);
+                        inPass = false;
+                    }
+                }
+                busy += clock64() - c0;
+            } else {
+                if (alive && !inPass && lds_load_acq(&sh.done[ss_]) && lds_load_acq(&sh.produced[ss_]) == cur)
+                    alive = false;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (lane == 0) atomicAdd(p.statPass + 2, busy);
+    }
+    if (tid == 0) {
+        atomicAdd(p.statPass + 4, clock64() - cyStart);
+        const unsigned long long wt = wall_clock64() - tStart;
+        atomicAdd(p.statPass + 5, wt);
+        atomicMax(p.statPass + 6, wt);
+        atomicMax(p.statPass + 15, tStart);
+        atomicMax(p.statPass + 16, wall_clock64());
+        atomicMin(p.statPass + 17, tStart);
+    }
+}
+
+}  // namespace fm3d

@@ -224,6 +224,7 @@ def lm_profile(lm):
         "kcycles_per_pass_by_class": {n: round(cy / max(c, 1) / 1e3, 1) for n, c, cy in
                                       zip(("jac", "eval", "qr", "once"), lm["class_passes"], lm["class_cycles"])},
         "passes_by_class": dict(zip(("jac", "eval", "qr", "once"), lm["class_passes"])),
+        "wait_over_terms": lm["cycles_wait"] / max(lm["cycles_terms"], 1),  # wave-per-point kernel
         "last_group_start_ms": lm["last_group_start_ticks"] / max(lm["wall_clock_khz"], 1),
         "last_group_end_ms": lm["last_group_end_ticks"] / max(lm["wall_clock_khz"], 1),
     }

@@ -113,6 +113,9 @@ typedef struct fm3d_lm_stats {
     int64_t class_passes[4], class_cycles[4];
     /* wall-clock ticks from the first workgroup start to the last start / the last end */
     int64_t last_group_start_ticks, last_group_end_ticks;
+    /* wave-per-point kernel: term-wave cycles spent waiting on the chain lanes
+       (ring full, pass results), summed over term waves */
+    int64_t cycles_wait;
 } fm3d_lm_stats;
 
 typedef struct fm3d_pipeline_stats {
