@@ -440,9 +440,9 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     if (cap < 1) cap = 1;
     if (groups > cap) groups = cap;
     if (groups < 1) groups = 1;
-    // +4 KiB: the v2 passes prefetch up to two 64-entry chunks past a slot's last entry
-    HIPCHK(c, c->slab.ensure(ents * (v1 ? 5 : 2) * sizeof(double) * groups + 4096));
-    HIPCHK(c, c->slabI1.ensure(ents * (v1 ? 2 : 5) * 4 * groups + 4096));  // v1: I1 + compact index
+    // +8 KiB: the v2 passes prefetch up to four 64-entry chunks past a slot's last entry
+    HIPCHK(c, c->slab.ensure(ents * (v1 ? 5 : 2) * sizeof(double) * groups + 8192));
+    HIPCHK(c, c->slabI1.ensure(ents * (v1 ? 2 : 5) * 4 * groups + 8192));  // v1: I1 + compact index
     HIPCHK(c, c->lmOrder.ensure((size_t)(P + 1) * sizeof(int)));
     fm3d::LMParams p{};
     p.points = c->pts.as<double>();

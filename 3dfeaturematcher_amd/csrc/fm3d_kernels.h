@@ -60,7 +60,7 @@ __global__ void lm_kernel(LMParams p);
 
 // wave-per-point LM kernel (fm3d_lm2.hip): kLM2Slots term waves + 1 chain wave
 constexpr int kLM2Slots = 7;
-constexpr int kLM2Ring = 4;  // chunks of 64 entries in flight per slot
+constexpr int kLM2Ring = 8;  // chunks of 64 entries in flight per slot
 constexpr int kLM2Threads = 64 * (kLM2Slots + 1);
 __global__ void lm2_kernel(LMParams p);
 __global__ void lm_order_kernel(const int* status, const int* nfev, int P, int level, int* order, int* nOrder);

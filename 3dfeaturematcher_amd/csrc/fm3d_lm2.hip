@@ -458,6 +458,10 @@ struct Shared {
     LMParams P;
 };
 
+// the workgroup's LDS state, at namespace scope so that the wave-role functions below
+// address it directly (ds_* instructions) without a generic pointer
+__shared__ Shared g_sh;
+
 __device__ __forceinline__ int lds_load_acq(int* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -465,28 +469,35 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// sum += t[0..64) in index order: 64 dependent adds fed by ds_read_b128 one batch ahead
+// sum += t[0..64) in index order: 64 dependent adds, fed by ds_read_b128 into two
+// alternating register sets of 16 values (no register copies inside the chain)
 __device__ __forceinline__ double chain_sum64(double sum, const double* t) {
     const double2* t2 = reinterpret_cast<const double2*>(t);
-    double2 cur[8], nxt[8];
+    double2 a[8], b[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) cur[i] = t2[i];
+    for (int i = 0; i < 8; i++) a[i] = t2[i];
 #pragma unroll
-    for (int q = 16; q < kE; q += 16) {
+    for (int i = 0; i < 8; i++) b[i] = t2[8 + i];
 #pragma unroll
-        for (int i = 0; i < 8; i++) nxt[i] = t2[q / 2 + i];
+    for (int h = 0; h < 2; h++) {
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            sum += cur[i].x;
-            sum += cur[i].y;
+            sum += a[i].x;
+            sum += a[i].y;
+        }
+        if (h == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) a[i] = t2[16 + i];
         }
 #pragma unroll
-        for (int i = 0; i < 8; i++) cur[i] = nxt[i];
-    }
+        for (int i = 0; i < 8; i++) {
+            sum += b[i].x;
+            sum += b[i].y;
+        }
+        if (h == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        sum += cur[i].x;
-        sum += cur[i].y;
+            for (int i = 0; i < 8; i++) b[i] = t2[24 + i];
+        }
     }
     return sum;
 }
@@ -552,10 +563,80 @@ __device__ __forceinline__ Geo geometry(const LMParams& p, double ux, double uy,
     return r;
 }
 
+// ======================= chain wave =======================
+// Lane 2s+k adds sum k of slot s's current pass, chunk by chunk in entry order.  A
+// function of its own (not inlined) so that its registers are allocated apart from the
+// term waves' code.
+__device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, long long maxTicks,
+                                        unsigned long long* statBusy) {
+    // the chain's dependent adds bound a pass's last chunk: let it issue first
+    __builtin_amdgcn_s_setprio(3);
+    const int s = lane >> 1, which = lane & 1;
+    bool alive = s < kW;
+    const int ss_ = alive ? s : 0;
+    int cur = 0, rem = 0, kind = S_NONE, pid = 0;
+    bool inPass = false;
+    Enorm en;  // MINPACK enorm state; s2 lives in acc on the fast path
+    en.init(1);
+    double acc = 0.;  // running sum: enorm s2 (S_ENORM) or the dot product (S_DOT)
+    unsigned long long busy = 0;
+    for (;;) {
+        if ((long long)(wall_clock64() - tStart) > maxTicks) break;
+        if (!__any(alive)) break;
+        const int pr = alive ? lds_load_acq(&g_sh.produced[ss_]) : 0;
+        const bool have = alive && pr > cur;
+        if (have && !inPass) {
+            const PassDesc& d = g_sh.pd[ss_];
+            rem = d.nChunks;
+            kind = d.kind[which];
+            pid = d.id;
+            en.init(1);
+            en.agiant = d.agiant;
+            acc = 0.;
+            inPass = true;
+        }
+        if (__any(have)) {
+            const unsigned long long c0 = clock64();
+            // up to two chunks per lane per round, never past the pass's last chunk; every
+            // lane runs the same add chain (S_NONE lanes sum zeros they never publish)
+            const int nb = have ? min(min(pr - cur, rem), 2) : 0;
+#pragma nounroll
+            for (int b = 0; b < 2; b++) {
+                if (b < nb) {
+                    const int pos = cur % kR;
+                    const double* row = &g_sh.ring[ss_][pos][which][0];
+                    if (kind == S_ENORM && ((g_sh.chunkSlow[ss_][pos] >> which) & 1)) {
+                        en.s2 = acc;
+                        for (int i = 0; i < kE; i++) en.add(row[i]);
+                        acc = en.s2;
+                    } else {
+                        acc = chain_sum64(acc, row);
+                    }
+                    cur++;
+                    rem--;
+                }
+            }
+            if (nb > 0) lds_store_rel(&g_sh.consumed[ss_][which], cur);
+            if (have && rem == 0) {
+                en.s2 = acc;
+                g_sh.result[ss_][which] = kind == S_ENORM ? en.finish() : acc;
+                lds_store_rel(&g_sh.resultId[ss_][which], pid);
+                inPass = false;
+            }
+            busy += clock64() - c0;
+        } else {
+            if (alive && !inPass && lds_load_acq(&g_sh.done[ss_]) && lds_load_acq(&g_sh.produced[ss_]) == cur)
+                alive = false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (lane == 0) atomicAdd(statBusy, busy);
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel(LMParams p) {
-    __shared__ Shared sh;
+    Shared& sh = g_sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long tStart = wall_clock64(), cyStart = clock64();
     if (tid == 0) sh.P = p;
@@ -792,7 +873,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                             const int e = k * kE + lane;
                             L.p = Dp[e];
                             L.q = Dq[e];
-                            L.f = sl.DF[e];
+                            L.f = sl.DF[e];  // QR2 needs F too: J = (w_j dI_j - F) / h_j
                             return L;
                         };
                         auto chunk = [&](const Ld& L, int k) {
@@ -831,15 +912,19 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                             const bool sl0 = __ballot(slow) != 0;
                             prod.put(sl0 ? a : t0, t1, sl0 ? 1 : 0);
                         };
-                        Ld A = load(0), B = load(1);
-                        for (int k = 0; k < nCh; k += 2) {
-                            const Ld C = load(k + 2);
-                            chunk(A, k);
-                            A = C;
-                            if (k + 1 < nCh) {
-                                const Ld D = load(k + 3);
-                                chunk(B, k + 1);
-                                B = D;
+                        // kQD chunks of loads in flight: this pass computes little per entry
+                        constexpr int kQD = 4;
+                        Ld buf[kQD];
+#pragma unroll
+                        for (int j = 0; j < kQD; j++) buf[j] = load(j);
+                        for (int k = 0; k < nCh; k += kQD) {
+#pragma unroll
+                            for (int j = 0; j < kQD; j++) {
+                                if (k + j < nCh) {
+                                    const Ld nx = load(k + j + kQD);
+                                    chunk(buf[j], k + j);
+                                    buf[j] = nx;
+                                }
                             }
                         }
                     };
@@ -894,63 +979,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
             atomicAdd(p.statPass + 21, (unsigned long long)prod.waitCycles);
         }
     } else {
-        // ======================= chain wave =======================
-        // the chain's dependent adds bound a pass's last chunk: let it issue first
-        __builtin_amdgcn_s_setprio(3);
-        const int s = lane >> 1, which = lane & 1;
-        bool alive = s < kW;
-        const int ss_ = alive ? s : 0;
-        int cur = 0, rem = 0, kind = S_NONE, pid = 0;
-        bool inPass = false;
-        Enorm en;
-        en.init(1);
-        double dsum = 0.;
-        unsigned long long busy = 0;
-        for (;;) {
-            if ((long long)(wall_clock64() - tStart) > p.maxTicks) break;
-            if (!__any(alive)) break;
-            const int pr = alive ? lds_load_acq(&sh.produced[ss_]) : 0;
-            const bool have = alive && pr > cur;
-            if (have && !inPass) {
-                const PassDesc& d = sh.pd[ss_];
-                rem = d.nChunks;
-                kind = d.kind[which];
-                pid = d.id;
-                en.init(1);
-                en.agiant = d.agiant;
-                dsum = 0.;
-                inPass = true;
-            }
-            if (__any(have)) {
-                const unsigned long long c0 = clock64();
-                if (have) {
-                    const int pos = cur % kR;
-                    const double* row = &sh.ring[ss_][pos][which][0];
-                    if (kind == S_ENORM) {
-                        if ((sh.chunkSlow[ss_][pos] >> which) & 1) {
-                            for (int i = 0; i < kE; i++) en.add(row[i]);
-                        } else {
-                            en.s2 = chain_sum64(en.s2, row);
-                        }
-                    } else if (kind == S_DOT) {
-                        dsum = chain_sum64(dsum, row);
-                    }
-                    cur++;
-                    lds_store_rel(&sh.consumed[ss_][which], cur);
-                    if (--rem == 0) {
-                        sh.result[ss_][which] = kind == S_ENORM ? en.finish() : dsum;
-                        lds_store_rel(&sh.resultId[ss_][which], pid);
-                        inPass = false;
-                    }
-                }
-                busy += clock64() - c0;
-            } else {
-                if (alive && !inPass && lds_load_acq(&sh.done[ss_]) && lds_load_acq(&sh.produced[ss_]) == cur)
-                    alive = false;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        if (lane == 0) atomicAdd(p.statPass + 2, busy);
+        chain_wave(lane, tStart, p.maxTicks, p.statPass + 2);
     }
     if (tid == 0) {
         atomicAdd(p.statPass + 4, clock64() - cyStart);
