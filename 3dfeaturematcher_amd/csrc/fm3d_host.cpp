@@ -76,6 +76,7 @@ struct fm3d_ctx {
     int wallKhz = 0;
     DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, lmOrder, lmTrace, slab, slabI1;
     DevBuf records, recTmp, recFlag;
+    DevBuf lmProj;  // camera-2 projection constants for the LM kernel (fm3d::ProjConst)
     // staged pipeline inputs
     int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
     bool staged = false;
@@ -450,6 +451,15 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     p.cam = c->cam;
     std::memcpy(p.R2, c->R2, sizeof(p.R2));
     std::memcpy(p.t2, c->t2, sizeof(p.t2));
+    {   // the same constants as a small global table (re-read per chunk by the LM kernel)
+        fm3d::ProjConst pc;
+        std::memcpy(pc.R, c->R2, sizeof(pc.R));
+        std::memcpy(pc.t, c->t2, sizeof(pc.t));
+        pc.cam = c->cam;
+        HIPCHK(c, c->lmProj.ensure(sizeof(pc)));
+        HIPCHK(c, hipMemcpyAsync(c->lmProj.p, &pc, sizeof(pc), hipMemcpyHostToDevice, c->stream));
+        p.proj = c->lmProj.as<fm3d::ProjConst>();
+    }
     p.lvl = c->lvlDesc.as<LevelDesc>();
     p.levels = levels;
     p.offsets = c->offsets.as<int2>();
@@ -643,7 +653,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
                       &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat, &c->lmOrder, &c->lmTrace,
                       &c->slab, &c->slabI1,
-                      &c->records, &c->recTmp, &c->recFlag};
+                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();

@@ -15,6 +15,12 @@ struct LevelDesc {
     int w, h;
 };
 
+// camera-2 projection constants (projectPointsToImage2, singlecameratriangulator.cpp:591-644)
+struct ProjConst {
+    double R[9], t[3];
+    Camera cam;
+};
+
 struct LMParams {
     const double* points;  // P x 3
     int P;
@@ -25,6 +31,7 @@ struct LMParams {
     const int* nOrder;      // device count of `order`
     Camera cam;
     double R2[9], t2[3];
+    const ProjConst* proj;  // the same R2, t2, cam in global memory
     const LevelDesc* lvl;  // device array, levels+1 entries
     int levels;
     const int2* offsets;  // circle offsets (i, j) in reference order, padded to nOffPad

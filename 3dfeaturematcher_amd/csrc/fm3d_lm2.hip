@@ -540,9 +540,22 @@ struct Geo {
     int code;  // 0 ok, 2 NaN plane, 3 bounding box, 4 image-2 pixel outside
 };
 
+typedef __attribute__((address_space(4))) const ProjConst cProjConst;
+
+// The projection constants re-read (scalar loads, scalar cache) at every use: 21 uniform
+// doubles kept live across the pass loops would not fit the SGPR budget and get spilled
+// to VGPR lanes (a v_readlane per use).  The zero is opaque to the compiler, so the loads
+// are not hoisted out of the loop.
+__device__ __forceinline__ const cProjConst* proj_consts(const ProjConst* p) {
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return (const cProjConst*)((const __attribute__((address_space(4))) char*)p + z);
+}
+
 __device__ __forceinline__ Geo geometry(const LMParams& p, double ux, double uy, double n0, double n1, double n2,
                                         double mm, double scale, double xmax, double ymax, const uint8_t* img2,
                                         int lw, double cm) {
+    const cProjConst* pc = proj_consts(p.proj);
     Geo r;
     double nn = n0 * ux + n1 * uy + n2 * 1.;
     double kk = mm / nn;
@@ -553,7 +566,17 @@ __device__ __forceinline__ Geo geometry(const LMParams& p, double ux, double uy,
     else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
         cd = 3;
     double u, v;
-    project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
+    {
+        const double R[9] = {pc->R[0], pc->R[1], pc->R[2], pc->R[3], pc->R[4], pc->R[5], pc->R[6], pc->R[7], pc->R[8]};
+        const double t[3] = {pc->t[0], pc->t[1], pc->t[2]};
+        Camera cam;
+        cam.fx = pc->cam.fx;
+        cam.fy = pc->cam.fy;
+        cam.cx = pc->cam.cx;
+        cam.cy = pc->cam.cy;
+        for (int i = 0; i < 5; i++) cam.k[i] = pc->cam.k[i];
+        project1(cam, R, t, P0, P1, P2, u, v);
+    }
     if (cd == 0 && !pixel_good_b(u, v, xmax, ymax)) cd = 4;
     r.code = cd;
     r.fx = (float)(scale * u);
