@@ -511,17 +511,24 @@ struct Producer {
     Shared* sh;
     int w, lane;
     int seq;
+    int room;  // chunks known to be free in the ring (from the last read of the consumed counters)
     long long waitCycles;
 
     __device__ __forceinline__ void put(double t0, double t1, int slowBits) {
         double* row0 = &sh->ring[w][seq % kR][0][0];
-        if (seq >= kR) {
-            // ring space: both chain lanes of the slot have consumed chunk seq - kR
+        if (room == 0) {
+            // ring space: both chain lanes of the slot have consumed chunk seq - kR.  The
+            // counters are read only when the space seen last time is used up.
             const long long c0 = clock64();
-            while (min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])) <= seq - kR)
+            for (;;) {
+                const int c = min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1]));
+                room = c + kR - seq;
+                if (room > 0) break;
                 __builtin_amdgcn_s_sleep(1);
+            }
             waitCycles += clock64() - c0;
         }
+        room--;
         row0[lane] = t0;
         row0[kRow + lane] = t1;
         if (lane == 0) sh->chunkSlow[w][seq % kR] = slowBits;
@@ -687,7 +694,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
         SlotP2& SP = sh.sp[w];
         SlotS2& SS = sh.ss[w];
         PassOut2& OUT = sh.out[w];
-        Producer prod{&sh, w, lane, 0, 0};
+        Producer prod{&sh, w, lane, 0, kR, 0};
         const double cm = (double)p.cmax;
         const gi64* __restrict__ offsets = (const gi64*)p.offsets;
         const unsigned long long ltMask = (1ull << lane) - 1;
