@@ -74,7 +74,7 @@ struct fm3d_ctx {
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
     long lmGroups = 0;
     int wallKhz = 0;
-    DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, lmOrder, lmTrace, slab, slabI1;
+    DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, slab, slabI1;
     DevBuf records, recTmp, recFlag;
     DevBuf lmProj;  // camera-2 projection constants for the LM kernel (fm3d::ProjConst)
     // staged pipeline inputs
@@ -249,9 +249,9 @@ int ensure_offsets(fm3d_ctx* c) {
         for (int j = -R; j <= R; j++)
             if (i * i + j * j <= R * R) off.push_back(make_int2(i, j));
     c->nOff = (int)off.size();
-    // pad to a multiple of the LM kernel's pixel chunk (fm3d::kLMChunk) with offsets that are
-    // never inside the image
-    while (off.size() % fm3d::kLMChunk) off.push_back(make_int2(1 << 20, 1 << 20));
+    // pad to a multiple of the LM kernel's 64-entry chunk with offsets that are never
+    // inside the image
+    while (off.size() % 64) off.push_back(make_int2(1 << 20, 1 << 20));
     c->nOffPad = (int)off.size();
     HIPCHK(c, c->offsets.ensure(off.size() * sizeof(int2)));
     HIPCHK(c, hipMemcpy(c->offsets.p, off.data(), off.size() * sizeof(int2), hipMemcpyHostToDevice));
@@ -366,22 +366,6 @@ int ensure_scan_tmp(fm3d_ctx* c, int n) {
     return FM3D_OK;
 }
 
-// LM kernel register budget: 4 waves/SIMD (3 workgroups per CU) by default;
-// FM3D_LM_WAVES_PER_SIMD=3 selects the 3-wave build (more VGPRs, 2 workgroups per CU)
-bool lm_use_v1() {
-    const char* e = getenv("FM3D_LM_V1");
-    return e && atoi(e) != 0;
-}
-
-const void* lm_kernel_ptr() {
-    static const void* k = [] {
-        const char* e = getenv("FM3D_LM_WAVES_PER_SIMD");
-        if (e && atoi(e) == 3) return reinterpret_cast<const void*>(fm3d::lm_kernel<3>);
-        return reinterpret_cast<const void*>(fm3d::lm_kernel<4>);
-    }();
-    return k;
-}
-
 void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_stats* st) {
     st->groups = c->lmGroups;
     st->passes = (int64_t)cnt[3];
@@ -415,36 +399,32 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     HIPCHK(c, c->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
     HIPCHK(c, c->lmQueue.ensure(64 * sizeof(int)));
     HIPCHK(c, c->lmStat.ensure(256));
-    // persistent workgroups; slots refill from the queue.  Default: the wave-per-point
-    // kernel (fm3d_lm2.hip); FM3D_LM_V1=1 selects the lockstep 4-slot kernel (fm3d_lm.hip).
-    const bool v1 = lm_use_v1();
-    const int slots = v1 ? fm3d::kLMSlots : fm3d::kLM2Slots;
-    const int threads = v1 ? fm3d::kLMThreads : fm3d::kLM2Threads;
-    const void* kptr = v1 ? lm_kernel_ptr() : reinterpret_cast<const void*>(fm3d::lm2_kernel);
+    // persistent workgroups of fm3d::kLM2Slots term waves (one point each) + a chain wave;
+    // slots refill from the queue (fm3d_lm2.hip)
+    const int slots = fm3d::kLM2Slots;
+    const void* kptr = reinterpret_cast<const void*>(fm3d::lm2_kernel);
     long groups = c->s.lmWaves;
     if (groups <= 0) {
         int dev = 0, cus = 0, perCU = 0;
         HIPCHK(c, hipGetDevice(&dev));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kptr, threads, 0));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kptr, fm3d::kLM2Threads, 0));
         if (perCU < 1) perCU = 1;
         groups = (long)cus * perCU;
     }
     const long needed = (P + slots - 1) / slots;
     if (groups > needed) groups = needed;
     const size_t ents = (size_t)c->nOffPad * slots;
-    // v1: 5 double + float + int arrays; v2: 2 double (rays) + 5 32-bit arrays (I1, fvec and
-    // Jacobian dI as float, compact index)
-    const size_t perGroup = v1 ? ents * (5 * sizeof(double) + 2 * sizeof(float)) : ents * (2 * sizeof(double) + 5 * 4);
-    const size_t budget = (size_t)48 << 30;  // HBM budget for the per-group pixel slabs
+    // per slot and entry: rays (2 doubles) + I1, fvec dI, two Jacobian dI (float) + compact index
+    const size_t perGroup = ents * (2 * sizeof(double) + 5 * 4);
+    const size_t budget = (size_t)48 << 30;  // HBM budget for the per-slot pixel slabs
     long cap = (long)(budget / perGroup);
     if (cap < 1) cap = 1;
     if (groups > cap) groups = cap;
     if (groups < 1) groups = 1;
-    // +8 KiB: the v2 passes prefetch up to four 64-entry chunks past a slot's last entry
-    HIPCHK(c, c->slab.ensure(ents * (v1 ? 5 : 2) * sizeof(double) * groups + 8192));
-    HIPCHK(c, c->slabI1.ensure(ents * (v1 ? 2 : 5) * 4 * groups + 8192));  // v1: I1 + compact index
-    HIPCHK(c, c->lmOrder.ensure((size_t)(P + 1) * sizeof(int)));
+    // +8 KiB: the passes prefetch up to four 64-entry chunks past a slot's last entry
+    HIPCHK(c, c->slab.ensure(ents * 2 * sizeof(double) * groups + 8192));
+    HIPCHK(c, c->slabI1.ensure(ents * 5 * 4 * groups + 8192));
     fm3d::LMParams p{};
     p.points = c->pts.as<double>();
     p.P = P;
@@ -483,11 +463,10 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     p.overflow = (int*)(c->lmStat.as<unsigned long long>() + 2);
     p.statPass = c->lmStat.as<unsigned long long>() + 3;
     c->lmGroups = groups;
-    {   // guards against a broken state machine (never expected to trigger): main-loop passes per
-        // group <= its points x levels x (300 evaluations + QR passes), and a wall-clock limit
-        long long perGroup = (P + groups * slots - 1) / (groups * slots) + 1;
-        if (v1) perGroup = (P + groups - 1) / groups + 1;
-        p.maxIter = perGroup * (long long)(levels + 1) * 1600 + 10000;
+    {   // guards against a broken state machine (never expected to trigger): passes per slot
+        // <= its points x levels x (300 evaluations + QR passes), and a wall-clock limit
+        const long long perSlot = (P + groups * slots - 1) / (groups * slots) + 1;
+        p.maxIter = perSlot * (long long)(levels + 1) * 1600 + 10000;
         int dev = 0, khz = 0;
         HIPCHK(c, hipGetDevice(&dev));
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
@@ -498,68 +477,17 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     }
     if (P > 0) {
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        // per-launch queues [0..levels], the order count at [16]
         HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64 * sizeof(int), c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 256, c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmStat.as<unsigned long long>() + 20, 0xff, 8, c->stream));  // min start
         HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->lmStatus.p, fm3d::kLMRunning, P, c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmInfo.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmNfev.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
-        auto kern = reinterpret_cast<void (*)(fm3d::LMParams)>(const_cast<void*>(kptr));
-        // diagnostics: FM3D_LM_TRACE=<file> dumps per-point (fetch tick, finish tick, passes,
-        // workgroup) as int64 after the launch (see tools/lm_trace.py)
-        const char* tr = getenv("FM3D_LM_TRACE");
-        if (tr && *tr) {
-            HIPCHK(c, c->lmTrace.ensure((size_t)P * 4 * sizeof(long long)));
-            HIPCHK(c, hipMemsetAsync(c->lmTrace.p, 0, (size_t)P * 4 * sizeof(long long), c->stream));
-            p.trace = c->lmTrace.as<long long>();
-        }
-        const char* hv = getenv("FM3D_LM_HEAVY");
-        p.heavyPasses = hv ? atoi(hv) : 300;
-        const char* ph = getenv("FM3D_LM_PHASED");
-        if (!v1) {
-            p.levelHi = levels;
-            p.levelLo = 0;
-            hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(threads), 0, c->stream, p);
-            HIPCHK(c, hipGetLastError());
-        } else if (!(ph && atoi(ph))) {
-            // one launch: every slot runs its point through all levels (coarsest first,
-            // optimize_pyramid :225-241)
-            p.levelHi = levels;
-            p.levelLo = 0;
-            p.queue = c->lmQueue.as<int>();
-            p.order = nullptr;
-            p.nOrder = c->lmQueue.as<int>() + 16;
-            hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(fm3d::kLMThreads), 0, c->stream, p);
-            HIPCHK(c, hipGetLastError());
-        } else {
-            // one launch per pyramid level; between launches the surviving points are
-            // re-queued longest-first by the evaluations of the level just run
-            for (int L = levels; L >= 0; L--) {
-                p.levelHi = p.levelLo = L;
-                p.queue = c->lmQueue.as<int>() + (levels - L);
-                p.order = L == levels ? nullptr : c->lmOrder.as<int>();
-                p.nOrder = c->lmQueue.as<int>() + 16;
-                hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(fm3d::kLMThreads), 0, c->stream, p);
-                HIPCHK(c, hipGetLastError());
-                if (L > 0) {
-                    hipLaunchKernelGGL(fm3d::lm_order_kernel, dim3(1), dim3(1024), 0, c->stream,
-                                       c->lmStatus.as<int>(), c->lmNfev.as<int>(), P, L, c->lmOrder.as<int>(),
-                                       c->lmQueue.as<int>() + 16);
-                    HIPCHK(c, hipGetLastError());
-                }
-            }
-        }
+        // one launch: every slot runs its point through all levels, coarsest first
+        // (optimize_pyramid :225-241)
+        hipLaunchKernelGGL(fm3d::lm2_kernel, dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream, p);
+        HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(e1, c->stream));
-        if (p.trace) {
-            std::vector<long long> h((size_t)P * 4);
-            HIPCHK(c, hipMemcpyAsync(h.data(), p.trace, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            if (FILE* f = fopen(tr, "wb")) {
-                fwrite(h.data(), sizeof(long long), h.size(), f);
-                fclose(f);
-            }
-        }
     }
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
@@ -651,7 +579,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
     DevBuf* bufs[] = {&c->lvlDesc, &c->offsets, &c->A, &c->B, &c->cqA, &c->ctB, &c->idx, &c->key, &c->fkey,
                       &c->knnOut, &c->cand, &c->flag, &c->matches, &c->count, &c->scanTmp, &c->kp1, &c->kp2,
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
-                      &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat, &c->lmOrder, &c->lmTrace,
+                      &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat,
                       &c->slab, &c->slabI1,
                       &c->records, &c->recTmp, &c->recFlag, &c->lmProj};
     for (DevBuf* b : bufs) b->release();

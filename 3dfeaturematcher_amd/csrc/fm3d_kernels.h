@@ -24,15 +24,10 @@ struct ProjConst {
 struct LMParams {
     const double* points;  // P x 3
     int P;
-    int levelHi, levelLo;   // pyramid levels this launch runs (levelHi first)
-    int heavyPasses;        // heavy-point scheduling threshold (0 = off)
-    long long* trace;       // optional, P x 4: fetch tick, finish tick, passes, workgroup
-    const int* order;       // points to serve, in order (NULL: 0..P-1)
-    const int* nOrder;      // device count of `order`
     Camera cam;
     double R2[9], t2[3];
     const ProjConst* proj;  // the same R2, t2, cam in global memory
-    const LevelDesc* lvl;  // device array, levels+1 entries
+    const LevelDesc* lvl;   // device array, levels+1 entries
     int levels;
     const int2* offsets;  // circle offsets (i, j) in reference order, padded to nOffPad
     int nOff, nOffPad;
@@ -40,8 +35,8 @@ struct LMParams {
     double epsfcn;
     int cmax;
     int* queue;
-    double* slab;    // nWaves groups x 5 arrays x nOffPad x kLMSlots doubles ([pixel][slot])
-    float* slabI1;   // nWaves groups x nOffPad x kLMSlots floats
+    double* slab;    // rays: 2 arrays x (groups*kLM2Slots) slots x nOffPad entries
+    float* slabI1;   // I1, fvec dI, 2 Jacobian dI, compact index: 5 arrays, same shape
     long nWaves;     // number of workgroups
     double* normals;  // P x 3
     int* status;      // P
@@ -50,27 +45,21 @@ struct LMParams {
     int* mdat;        // P
     unsigned long long* statEval;
     unsigned long long* statPix;
-    long long maxIter;       // safety bound on main-loop passes per workgroup
+    long long maxIter;       // safety bound on passes per slot
     long long maxTicks;      // safety bound on wall-clock ticks per workgroup
     int* overflow;           // set to 1 if a workgroup hit a guard
-    // [passes, cycles terms, cycles chain, cycles control, cycles total, wall ticks sum, wall ticks max]
+    // [passes, cycles terms, cycles chain, cycles control, cycles total, wall ticks sum, wall ticks
+    //  max, class passes x4, class cycles x4, max start, max end, min start, ..., producer waits]
     unsigned long long* statPass;
 };
 
-constexpr int kLMRunning = 0x100;  // status of a point parked between level launches
-constexpr int kLMSlots = 4;     // points per LM workgroup
-constexpr int kLMThreads = 256;  // 3 term waves + 1 chain wave: one wave per SIMD
-constexpr int kLMChunk = 192;   // pixels per LM chunk (offsets are padded to a multiple)
-
-template <int kMinWavesPerSimd>
-__global__ void lm_kernel(LMParams p);
+constexpr int kLMRunning = 0x100;  // status of a point still in flight
 
 // wave-per-point LM kernel (fm3d_lm2.hip): kLM2Slots term waves + 1 chain wave
 constexpr int kLM2Slots = 7;
 constexpr int kLM2Ring = 8;  // chunks of 64 entries in flight per slot
 constexpr int kLM2Threads = 64 * (kLM2Slots + 1);
 __global__ void lm2_kernel(LMParams p);
-__global__ void lm_order_kernel(const int* status, const int* nfev, int P, int level, int* order, int* nOrder);
 
 // ---------------- matching ----------------
 struct KnnOut {

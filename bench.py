@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", type=str, default="")
-    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "r01_pmc_c4.json"),
+    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "r01_pmc_c4_lm2.json"),
                     help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()
 
@@ -164,7 +164,7 @@ def main():
                 "parallelism": f"dp{world}: one frame pair per rank, RCCL all-gather of survivor records",
             },
             "roofline": {
-                "kernel": "fm3d::lm_kernel (LM normal refinement)",
+                "kernel": "fm3d::lm2_kernel (LM normal refinement)",
                 "bound": "mfma",
                 "compute": "fp64 (issued on the VALU; MI355X fp64 matrix and vector peaks coincide at 78.6 TFLOP/s)",
                 "achieved": achieved_tflops,
@@ -210,22 +210,18 @@ def pmc_traffic(args):
 
 
 def lm_profile(lm):
-    """Where the LM workgroups spend their time (core clocks seen by each group's first wave)."""
+    """Where the LM kernel's time goes (in-kernel clock counters, fm3d_lm_stats)."""
     tot = lm["cycles_total"]
     return {
         "groups": lm["groups"], "passes": lm["passes"],
-        "passes_per_group": lm["passes"] / max(lm["groups"], 1),
-        "busy_terms": lm["cycles_terms"] / tot if tot else None,    # first term wave busy / group lifetime
-        "busy_chain": lm["cycles_chain"] / tot if tot else None,    # chain wave summing / group lifetime
-        "busy_control": lm["cycles_control"] / tot if tot else None,
-        "cycles_per_pass": tot / max(lm["passes"], 1),
+        "chain_busy": lm["cycles_chain"] / tot if tot else None,    # chain wave adding / group lifetime
+        "control_over_terms": lm["cycles_control"] / max(lm["cycles_terms"], 1),  # lmdif bookkeeping
+        "wait_over_terms": lm["cycles_wait"] / max(lm["cycles_terms"], 1),        # term waves waiting on the chain
         "group_life_mean_over_max": lm["wall_ticks_sum"] / max(lm["groups"], 1) / max(lm["wall_ticks_max"], 1),
         "clock_ghz": lm["cycles_total"] / max(lm["wall_ticks_sum"], 1) * lm["wall_clock_khz"] * 1e-6,
         "kcycles_per_pass_by_class": {n: round(cy / max(c, 1) / 1e3, 1) for n, c, cy in
                                       zip(("jac", "eval", "qr", "once"), lm["class_passes"], lm["class_cycles"])},
         "passes_by_class": dict(zip(("jac", "eval", "qr", "once"), lm["class_passes"])),
-        "wait_over_terms": lm["cycles_wait"] / max(lm["cycles_terms"], 1),  # wave-per-point kernel
-        "last_group_start_ms": lm["last_group_start_ticks"] / max(lm["wall_clock_khz"], 1),
         "last_group_end_ms": lm["last_group_end_ticks"] / max(lm["wall_clock_khz"], 1),
     }
 

@@ -65,7 +65,7 @@ typedef struct fm3d_settings {
     /* --- extensions (not in the reference file) --- */
     int boundWidth, boundHeight; /* literal 1024 x 768 of extractPixelsContour (:359) */
     int strictNanExit;           /* 1: NaN plane makes fm3d_optimize_normals fail with FM3D_ERR_NAN_PLANE */
-    int lmWaves;                 /* LM kernel wavefronts (0 = auto) */
+    int lmWaves;                 /* LM workgroups to launch (0 = fill the GPU) */
 } fm3d_settings;
 
 /* cv::DMatch layout */
@@ -101,20 +101,20 @@ typedef struct fm3d_lm_stats {
     int64_t pixel_evaluations; /* sum over evaluations of m_dat */
     int64_t drops[8];          /* points per FM3D_ST_* code */
     double kernel_ms;          /* LM kernel time (HIP events on the context stream) */
-    int64_t groups;            /* LM workgroups launched (kLMSlots points in flight each) */
-    int64_t passes;            /* neighbourhood passes, summed over workgroups */
-    /* core clock cycles seen by each workgroup's first wave, summed over workgroups:
-       parallel term phase, sequential (pixel-order) sum phase, lmdif bookkeeping */
+    int64_t groups;            /* LM workgroups launched (7 points in flight each, one per term wave) */
+    int64_t passes;            /* summed neighbourhood passes (residual, Jacobian, Householder), all points */
+    /* core clock cycles, summed over workgroups or waves: term waves inside passes
+       (including waits), the chain wave busy adding, term waves in the lmdif bookkeeping,
+       workgroup 0-th wave lifetime */
     int64_t cycles_terms, cycles_chain, cycles_control, cycles_total;
     /* workgroup lifetimes in constant-rate wall-clock ticks: sum and max over workgroups */
     int64_t wall_ticks_sum, wall_ticks_max, wall_clock_khz;
-    /* workgroup passes and cycles by class: [0] with a Jacobian evaluation, [1] with another
-       residual evaluation, [2] Householder products only, [3] once-per-point/level passes */
+    /* passes and term-wave cycles by class: [0] Jacobian (two residual evaluations),
+       [1] one residual evaluation, [2] Householder products, [3] once per point / level */
     int64_t class_passes[4], class_cycles[4];
     /* wall-clock ticks from the first workgroup start to the last start / the last end */
     int64_t last_group_start_ticks, last_group_end_ticks;
-    /* wave-per-point kernel: term-wave cycles spent waiting on the chain lanes
-       (ring full, pass results), summed over term waves */
+    /* term-wave cycles spent waiting on the chain lanes (ring full, pass results) */
     int64_t cycles_wait;
 } fm3d_lm_stats;
 

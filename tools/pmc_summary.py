@@ -15,16 +15,20 @@ def main():
     d = sys.argv[1]
     kname = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "lm2_kernel"
     out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None
-    agg = {}
+    agg, n = {}, {}
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             if kname in r["Kernel_Name"]:
-                agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                c = r["Counter_Name"]
+                agg[c] = agg.get(c, 0.0) + float(r["Counter_Value"])
+                n.setdefault(c, set()).add(r["Dispatch_Id"])
+    agg = {c: v / len(n[c]) for c, v in agg.items()}  # per launch
     dur = None
     for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))):
         if kname in r["Name"]:
             dur = float(r["AverageNs"])
-    res = {"kernel": kname, "trace_avg_ns": dur, "counters": agg}
+    res = {"kernel": kname, "trace_avg_ns": dur, "counters_per_launch": agg,
+           "launches": max((len(v) for v in n.values()), default=0)}
     if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
         rd, wr = 2 * agg["FETCH_SIZE"] * 1024, agg["WRITE_SIZE"] * 1024
         res.update(hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes_per_launch=rd + wr,
