@@ -32,6 +32,7 @@ EXPORTS = (
     "fm3d_camera2_from_g12", "fm3d_set_g12", "fm3d_get_camera2", "fm3d_triangulate", "fm3d_set_images",
     "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
+    "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches",
 )
 
 
@@ -51,6 +52,7 @@ class Settings(ctypes.Structure):
         ("pixelsRay", ctypes.c_int), ("pyramids", ctypes.c_int), ("nndrEpsilon", ctypes.c_double),
         ("pos1", ctypes.c_double * 6), ("pos2", ctypes.c_double * 6), ("boundWidth", ctypes.c_int),
         ("boundHeight", ctypes.c_int), ("strictNanExit", ctypes.c_int), ("lmWaves", ctypes.c_int),
+        ("neighEpsilon", ctypes.c_double), ("cmPerPixel", ctypes.c_double),
     ]
 
     @staticmethod
@@ -257,6 +259,42 @@ class SingleCameraTriangulator:
                                               _ptr(mask, ctypes.c_uint8), ctypes.byref(n)))
         return pts[:n.value].copy(), mask[:K].astype(bool)
 
+    def projectReferencePointsToImageWithFrames(self, referenceNeighborhood, featuresFrames, image_points=False):
+        """singlecameratriangulator.cpp:769-849 on image 1 of setImages: (P, size, size) uint8 patches,
+        patch[j, i] = sample of reference point (i, j); optionally the (P, size*size, 2) projections.
+        The reference neighbourhood must be the square one of the settings (it is rebuilt on the GPU)."""
+        F = np.ascontiguousarray(featuresFrames, dtype=np.float64).reshape(-1, 16)
+        size = lib().fm3d_patch_size(ctypes.byref(self.ctx.settings))
+        if referenceNeighborhood is not None and len(referenceNeighborhood) != size * size:
+            raise ValueError(f"reference neighbourhood has {len(referenceNeighborhood)} points, settings give {size}^2")
+        n = F.shape[0]
+        patches = np.zeros((max(n, 1), size, size), dtype=np.uint8)
+        pts = np.zeros((max(n, 1), size * size, 2)) if image_points else None
+        self.ctx.check(lib().fm3d_export_patches(self.ctx.handle, _ptr(F), n, _ptr(patches, ctypes.c_uint8),
+                                                 _ptr(pts) if pts is not None else None))
+        return (patches[:n], pts[:n]) if image_points else patches[:n]
+
+
+class NeighborhoodsGenerator:
+    """NeighborhoodsGenerator (Triangulator/neighborhoodsgenerator.h:78-97), the square method."""
+
+    def __init__(self, settings: Settings):
+        self.settings = settings
+
+    def size(self) -> int:
+        return lib().fm3d_patch_size(ctypes.byref(self.settings))
+
+    def getReferenceSquaredNeighborhood(self) -> np.ndarray:
+        """neighborhoodsgenerator.cpp:134-158: (size*size, 3) points (-eps + inc*i, -eps + inc*j, 0),
+        i outer."""
+        eps, inc, n = self.settings.neighEpsilon, self.settings.cmPerPixel * 0.01, self.size()
+        out = np.zeros((n * n, 3))
+        for i in range(n):
+            for j in range(n):
+                out[i * n + j, 0] = -eps + inc * i
+                out[i * n + j, 1] = -eps + inc * j
+        return out
+
 
 class NormalOptimizer:
     """NormalOptimizer (Triangulator/normaloptimizer.h:43-59), hot-path methods."""
@@ -284,6 +322,21 @@ class NormalOptimizer:
         self.ctx.check(lib().fm3d_get_pyramid_level(self.ctx.handle, which, level, _ptr(out, ctypes.c_uint8),
                                                     ctypes.byref(w), ctypes.byref(h)))
         return out
+
+    def getGravity(self) -> np.ndarray:
+        """getGravity (normaloptimizer.cpp:185-188): Rodrigues(rodriguesIC)^-1 (0, 0, -1)."""
+        g = np.zeros(3)
+        _check(lib().fm3d_gravity(ctypes.byref(self.ctx.settings), _ptr(g)))
+        return g
+
+    def computeFeaturesFrames(self, points3D: np.ndarray, normals: np.ndarray) -> np.ndarray:
+        """computeFeaturesFrames (normaloptimizer.cpp:454-504): (P, 4, 4) frames, on the GPU."""
+        P = np.ascontiguousarray(points3D, dtype=np.float64).reshape(-1, 3)
+        N = np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 3)
+        n = min(P.shape[0], N.shape[0])  # the reference walks both vectors together
+        frames = np.zeros((max(n, 1), 4, 4))
+        self.ctx.check(lib().fm3d_features_frames(self.ctx.handle, _ptr(P), _ptr(N), n, _ptr(frames)))
+        return frames[:n]
 
     def startVisualizerThread(self):  # PCL viewer: out of scope, no-op
         pass

@@ -940,6 +940,88 @@ int fm3d_records_download(fm3d_ctx* c, const fm3d_record* recordsDev, int n, fm3
     return FM3D_OK;
 }
 
+int fm3d_gravity(const fm3d_settings* s, double g[3]) {
+    // NormalOptimizer ctor (normaloptimizer.cpp:160-178): Rodrigues(rodriguesIC).inv() * (0,0,-1),
+    // OpenCV 2.4's closed-form 3x3 Matx inverse, Matx * Vec accumulated from 0 in index order
+    if (!s || !g) return FM3D_ERR_INVALID;
+    double a[9], b[9];
+    rodrigues_v2m(s->rodriguesIC, a);
+#define A(i, j) a[(i)*3 + (j)]
+    double d = A(0, 0) * (A(1, 1) * A(2, 2) - A(2, 1) * A(1, 2)) - A(0, 1) * (A(1, 0) * A(2, 2) - A(2, 0) * A(1, 2)) +
+               A(0, 2) * (A(1, 0) * A(2, 1) - A(2, 0) * A(1, 1));
+    if (d == 0) return FM3D_ERR_INVALID;
+    d = 1 / d;
+    b[0] = (A(1, 1) * A(2, 2) - A(1, 2) * A(2, 1)) * d;
+    b[1] = (A(0, 2) * A(2, 1) - A(0, 1) * A(2, 2)) * d;
+    b[2] = (A(0, 1) * A(1, 2) - A(0, 2) * A(1, 1)) * d;
+    b[3] = (A(1, 2) * A(2, 0) - A(1, 0) * A(2, 2)) * d;
+    b[4] = (A(0, 0) * A(2, 2) - A(0, 2) * A(2, 0)) * d;
+    b[5] = (A(0, 2) * A(1, 0) - A(0, 0) * A(1, 2)) * d;
+    b[6] = (A(1, 0) * A(2, 1) - A(1, 1) * A(2, 0)) * d;
+    b[7] = (A(0, 1) * A(2, 0) - A(0, 0) * A(2, 1)) * d;
+    b[8] = (A(0, 0) * A(1, 1) - A(0, 1) * A(1, 0)) * d;
+#undef A
+    const double v[3] = {0, 0, -1};
+    for (int i = 0; i < 3; i++) {
+        double acc = 0;
+        for (int k = 0; k < 3; k++) acc += b[i * 3 + k] * v[k];
+        g[i] = acc;
+    }
+    return FM3D_OK;
+}
+
+int fm3d_features_frames(fm3d_ctx* c, const double* points, const double* normals, int P, double* frames) {
+    if (!c || P < 0 || (P && (!points || !normals || !frames))) return FM3D_ERR_INVALID;
+    if (P == 0) return FM3D_OK;
+    hipSetDevice(c->device);
+    double g[3];
+    int r;
+    if ((r = fm3d_gravity(&c->s, g))) return fail(c, r, "gravity: singular rodriguesIC rotation");
+    DevBuf a, b, f;
+    HIPCHK(c, a.ensure((size_t)P * 3 * sizeof(double)));
+    HIPCHK(c, b.ensure((size_t)P * 3 * sizeof(double)));
+    HIPCHK(c, f.ensure((size_t)P * 16 * sizeof(double)));
+    HIPCHK(c, hipMemcpyAsync(a.p, points, (size_t)P * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(b.p, normals, (size_t)P * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_features_frames(a.as<double>(), b.as<double>(), P, g, f.as<double>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(frames, f.p, (size_t)P * 16 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+int fm3d_patch_size(const fm3d_settings* s) {
+    if (!s) return FM3D_ERR_INVALID;
+    // numberOfPointsPerEdge (neighborhoodsgenerator.cpp:136-137)
+    return 2 * ((int)floor(s->neighEpsilon / (0.01 * s->cmPerPixel)));
+}
+
+int fm3d_export_patches(fm3d_ctx* c, const double* frames, int P, uint8_t* patches, double* imagePoints) {
+    if (!c || P < 0 || (P && (!frames || !patches))) return FM3D_ERR_INVALID;
+    if (c->pyr1.empty()) return fail(c, FM3D_ERR_INVALID, "fm3d_set_images not called");
+    const int size = fm3d_patch_size(&c->s);
+    if (size <= 0) return fail(c, FM3D_ERR_INVALID, "patch size <= 0 (Neighborhoods.epsilon / cmPerPixel)");
+    if (P == 0) return FM3D_OK;
+    hipSetDevice(c->device);
+    const size_t per = (size_t)size * size;
+    DevBuf f, rt, out, pts;
+    HIPCHK(c, f.ensure((size_t)P * 16 * sizeof(double)));
+    HIPCHK(c, rt.ensure((size_t)P * 12 * sizeof(double)));
+    HIPCHK(c, out.ensure((size_t)P * per));
+    if (imagePoints) HIPCHK(c, pts.ensure((size_t)P * per * 2 * sizeof(double)));
+    HIPCHK(c, hipMemcpyAsync(f.p, frames, (size_t)P * 16 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_export_patches(f.as<double>(), P, size, c->s.neighEpsilon, c->s.cmPerPixel * 0.01, c->cam,
+                                c->pyr1[0].as<uint8_t>(), c->lw[0], c->lh[0], rt.as<double>(), out.as<uint8_t>(),
+                                imagePoints ? pts.as<double>() : nullptr, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(patches, out.p, (size_t)P * per, hipMemcpyDeviceToHost, c->stream));
+    if (imagePoints)
+        HIPCHK(c, hipMemcpyAsync(imagePoints, pts.p, (size_t)P * per * 2 * sizeof(double), hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
 int fm3d_pyrdown(fm3d_ctx* c, const uint8_t* src, int width, int height, uint8_t* dst) {
     if (!c || !src || !dst || width <= 0 || height <= 0) return FM3D_ERR_INVALID;
     hipSetDevice(c->device);

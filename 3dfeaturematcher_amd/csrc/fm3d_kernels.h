@@ -108,6 +108,14 @@ void launch_triangulate(const TriParams& p, hipStream_t s);
 void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s);
 void launch_undistort(const Camera& cam, const double* xy, int n, double* out, hipStream_t s);
 
+// ---------------- feature frames + patch export (fm3d_patch.hip) ----------------
+void launch_features_frames(const double* pts, const double* nrm, int P, const double g[3], double* frames,
+                            hipStream_t s);
+// RT: 12 doubles of scratch per frame
+void launch_export_patches(const double* frames, int P, int size, double eps, double inc, const Camera& cam,
+                           const uint8_t* img, int w, int h, double* RT, uint8_t* patches, double* imagePoints,
+                           hipStream_t s);
+
 // ---------------- records ----------------
 void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int nInl, const double* pts,
                          const double* normals, const int* status, fm3d_record* rec, int* flag, hipStream_t s);

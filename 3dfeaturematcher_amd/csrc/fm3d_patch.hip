@@ -1,0 +1,194 @@
+// fm3d_patch.hip -- feature frames and normal-rectified patch export.
+//
+// Reference: NormalOptimizer::computeFeaturesFrames (Triangulator/normaloptimizer.cpp:454-504),
+// NeighborhoodsGenerator::getReferenceSquaredNeighborhood (neighborhoodsgenerator.cpp:134-158) and
+// SingleCameraTriangulator::projectReferencePointsToImageWithFrame(s)
+// (singlecameratriangulator.cpp:769-849).  main.cpp:157-180 runs them after the normals.
+//
+// Three kernels, all bit-exact against oracle/fm3d_oracle.c (deterministic-math mode):
+//   frames_kernel        one thread per point: z = n, x = g x z, y = z x x, cv::normalize(x), (y),
+//                        columns through Vec::dot, translation = the point;
+//   frame_camera_kernel  one thread per frame: decomposeTransformation + the cvRodrigues2 round trip
+//                        cvProjectPoints2 applies (matrix -> vector -> matrix);
+//   patch_kernel         one thread per (reference point, frame): projectPoints, isPixelGood(p, 1.0)
+//                        of image 1, (uchar) bilinear sample, written transposed (patch.at(col, row)).
+// Every output byte depends on one projected sample; the patch kernel is a projection + gather
+// bound by the fp64 VALU (≈60 fp64 ops per sample) -- there is no reduction and no data reuse
+// beyond the image in L2.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "fm3d_device.h"
+#include "fm3d_kernels.h"
+
+namespace fm3d {
+
+namespace {
+
+// cv::normalize(v, v) of a Vec3d: 1/||v|| (squares summed from 0 in index order; 0 if the norm is
+// <= DBL_EPSILON), then v*scale + 0 (convertTo with scale, shift 0)
+__device__ inline void normalize3(double v[3]) {
+    double s = 0;
+    for (int i = 0; i < 3; i++) s += v[i] * v[i];
+    s = sqrt(s);
+    const double scale = s > DBL_EPSILON ? 1 / s : 0.;
+    for (int i = 0; i < 3; i++) v[i] = v[i] * scale + 0.;
+}
+
+__global__ void frames_kernel(const double* __restrict__ pts, const double* __restrict__ nrm, int P, double g0,
+                              double g1, double g2, double* __restrict__ frames) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const double z[3] = {nrm[3 * p], nrm[3 * p + 1], nrm[3 * p + 2]};
+    // x = gravity.cross(z), y = z.cross(x) (cv::Vec3d::cross), normalised afterwards (:476-481)
+    double x[3] = {g1 * z[2] - g2 * z[1], g2 * z[0] - g0 * z[2], g0 * z[1] - g1 * z[0]};
+    double y[3] = {z[1] * x[2] - z[2] * x[1], z[2] * x[0] - z[0] * x[2], z[0] * x[1] - z[1] * x[0]};
+    normalize3(x);
+    normalize3(y);
+    double* F = frames + 16 * (size_t)p;
+    for (int r = 0; r < 3; r++) {
+        // actualFrame(r, c) = e_r.dot(c-th basis vector) (:484-486)
+        const double e[3] = {(double)(r == 0), (double)(r == 1), (double)(r == 2)};
+        F[4 * r + 0] = ((0 + e[0] * x[0]) + e[1] * x[1]) + e[2] * x[2];
+        F[4 * r + 1] = ((0 + e[0] * y[0]) + e[1] * y[1]) + e[2] * y[2];
+        F[4 * r + 2] = ((0 + e[0] * z[0]) + e[1] * z[1]) + e[2] * z[2];
+        F[4 * r + 3] = pts[3 * p + r];
+    }
+    F[12] = 0;
+    F[13] = 0;
+    F[14] = 0;
+    F[15] = 1;
+}
+
+// 3x3 inverse transpose via the adjugate (one Newton step of the polar decomposition below)
+__device__ inline void inv_t3(const double A[9], double out[9]) {
+    const double c00 = A[4] * A[8] - A[5] * A[7];
+    const double c01 = A[5] * A[6] - A[3] * A[8];
+    const double c02 = A[3] * A[7] - A[4] * A[6];
+    const double c10 = A[2] * A[7] - A[1] * A[8];
+    const double c11 = A[0] * A[8] - A[2] * A[6];
+    const double c12 = A[1] * A[6] - A[0] * A[7];
+    const double c20 = A[1] * A[5] - A[2] * A[4];
+    const double c21 = A[2] * A[3] - A[0] * A[5];
+    const double c22 = A[0] * A[4] - A[1] * A[3];
+    const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+    const double id = 1. / det;
+    out[0] = c00 * id;
+    out[1] = c01 * id;
+    out[2] = c02 * id;
+    out[3] = c10 * id;
+    out[4] = c11 * id;
+    out[5] = c12 * id;
+    out[6] = c20 * id;
+    out[7] = c21 * id;
+    out[8] = c22 * id;
+}
+
+// decomposeTransformation (tools.cpp:101-114) then cvProjectPoints2's Rodrigues: the R, t that
+// projectReferencePointsToImageWithFrame projects with.  cvRodrigues2 (matrix -> vector) first
+// replaces R by its nearest orthonormal matrix (polar factor, three Newton steps X <- (X + X^-T)/2).
+__global__ void frame_camera_kernel(const double* __restrict__ frames, int P, double* __restrict__ RT) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const double* F = frames + 16 * (size_t)p;
+    double R[9] = {F[0], F[1], F[2], F[4], F[5], F[6], F[8], F[9], F[10]}, Y[9];
+    for (int it = 0; it < 3; it++) {
+        inv_t3(R, Y);
+        for (int k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
+    }
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = fm3d_acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t = (R[0] + 1) * 0.5;
+            rx = sqrt(t > 0. ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = sqrt(t > 0. ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = sqrt(t > 0. ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            theta /= sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta;
+            ry *= theta;
+            rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= theta;
+        rx *= vth;
+        ry *= vth;
+        rz *= vth;
+    }
+    // vector -> matrix
+    double* out = RT + 12 * (size_t)p;
+    theta = sqrt(rx * rx + ry * ry + rz * rz);
+    if (theta < DBL_EPSILON) {
+        for (int k = 0; k < 9; k++) out[k] = (k % 4 == 0) ? 1. : 0.;
+    } else {
+        const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        const double cc = fm3d_cos(theta), ss = fm3d_sin(theta), c1 = 1. - cc;
+        const double itheta = theta ? 1. / theta : 0.;
+        rx *= itheta;
+        ry *= itheta;
+        rz *= itheta;
+        const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+        const double rxm[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+        for (int k = 0; k < 9; k++) out[k] = cc * I[k] + c1 * rrt[k] + ss * rxm[k];
+    }
+    out[9] = F[3];
+    out[10] = F[7];
+    out[11] = F[11];
+}
+
+__global__ __launch_bounds__(256) void patch_kernel(const double* __restrict__ RT, int P, int size, double eps,
+                                                    double inc, Camera cam, const uint8_t* __restrict__ img, int w,
+                                                    int h, uint8_t* __restrict__ patches,
+                                                    double* __restrict__ imagePoints) {
+    const int p = blockIdx.y;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;  // reference point i*size + j
+    if (p >= P || k >= size * size) return;
+    const int i = k / size, j = k - i * size;
+    const double* rt = RT + 12 * (size_t)p;
+    const double R[9] = {rt[0], rt[1], rt[2], rt[3], rt[4], rt[5], rt[6], rt[7], rt[8]};
+    const double t[3] = {rt[9], rt[10], rt[11]};
+    double u, v;
+    project1(cam, R, t, -eps + inc * i, -eps + inc * j, 0, u, v);
+    const size_t base = (size_t)p * size * size;
+    if (imagePoints) {
+        imagePoints[(base + k) * 2] = u;
+        imagePoints[(base + k) * 2 + 1] = v;
+    }
+    uint8_t val = 0;
+    if (pixel_good(u, v, 1.0, w, h)) val = (uint8_t)bilinear(img, w, (float)u, (float)v);
+    patches[base + (size_t)j * size + i] = val;  // patch.at<uchar>(col, row), :842-846
+}
+
+}  // namespace
+
+void launch_features_frames(const double* pts, const double* nrm, int P, const double g[3], double* frames,
+                            hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(frames_kernel, dim3((P + 255) / 256), dim3(256), 0, s, pts, nrm, P, g[0], g[1], g[2], frames);
+}
+
+void launch_export_patches(const double* frames, int P, int size, double eps, double inc, const Camera& cam,
+                           const uint8_t* img, int w, int h, double* RT, uint8_t* patches, double* imagePoints,
+                           hipStream_t s) {
+    if (P <= 0 || size <= 0) return;
+    hipLaunchKernelGGL(frame_camera_kernel, dim3((P + 255) / 256), dim3(256), 0, s, frames, P, RT);
+    const size_t per = (size_t)size * size;
+    for (int p0 = 0; p0 < P; p0 += 65535) {  // grid.y limit
+        const int n = P - p0 < 65535 ? P - p0 : 65535;
+        dim3 grid((unsigned)((per + 255) / 256), (unsigned)n);
+        hipLaunchKernelGGL(patch_kernel, grid, dim3(256), 0, s, RT + 12 * (size_t)p0, n, size, eps, inc, cam, img, w,
+                           h, patches + per * p0, imagePoints ? imagePoints + 2 * per * p0 : nullptr);
+    }
+}
+
+}  // namespace fm3d

@@ -124,6 +124,8 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->boundHeight = 768;
     s->strictNanExit = 0;
     s->lmWaves = 0;
+    s->neighEpsilon = 0.16;  // build/settings.yml Neighborhoods
+    s->cmPerPixel = 0.25;
     return FM3D_OK;
 }
 
@@ -149,6 +151,8 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
     get_i(kv, "Neighborhoods.pixelsRay", &s->pixelsRay);
     get_i(kv, "Neighborhoods.pyramids", &s->pyramids);
     get_d(kv, "NNDR.epsilon", &s->nndrEpsilon);
+    get_d(kv, "Neighborhoods.epsilon", &s->neighEpsilon);
+    get_d(kv, "Neighborhoods.cmPerPixel", &s->cmPerPixel);
     get_vec(kv, "IMAGES.pos1", s->pos1, 6);
     get_vec(kv, "IMAGES.pos2", s->pos2, 6);
     // extensions (optional section)

@@ -7,7 +7,8 @@
 //   <dir>/img1.pgm img2.pgm   8-bit P5 images
 //   <dir>/kp1.f32 kp2.f32     N x 2 float32 keypoint positions
 //   <dir>/desc1.u8 desc2.u8   N x 128 uint8 descriptors (SIFT saturated to uchar)
-// Writes <dir>/out_matches.bin (DMatch), out_points.f64, out_normals.f64.
+// Writes <dir>/out_matches.bin (DMatch), out_points.f64, out_normals.f64 and, like main.cpp:160-180,
+// the normal-rectified patches of the first 16 points as patch_<i>.pgm.
 // Usage: fm3d_main -s settings.yml -d <dir>
 #include <cstdio>
 #include <cstring>
@@ -62,6 +63,13 @@ static std::vector<T> read_raw(const std::string& path) {
     return v;
 }
 
+// P5 writer (cv::imwrite of the patches, singlecameratriangulator.cpp:799-802)
+static void write_pgm(const std::string& path, const Patch8u& m) {
+    std::ofstream f(path, std::ios::binary);
+    f << "P5\n" << m.cols << " " << m.rows << "\n255\n";
+    f.write(reinterpret_cast<const char*>(m.data.data()), (std::streamsize)m.data.size());
+}
+
 template <class T>
 static void write_raw(const std::string& path, const T* p, size_t n) {
     std::ofstream f(path, std::ios::binary);
@@ -111,6 +119,19 @@ int main(int argc, char** argv) {
         std::vector<Vec3d> normals;
         no.computeOptimizedNormals(points3D, normals);
         no.stopVisualizerThread();
+
+        // main.cpp:157-180: feature frames, reference neighbourhood, normal-rectified patches
+        std::vector<Matx44d> featuresFrames;
+        no.computeFeaturesFrames(points3D, normals, featuresFrames);
+        NeighborhoodsGenerator ng(s);
+        std::vector<Vec3d> referenceNeighborhood;
+        ng.getReferenceSquaredNeighborhood(referenceNeighborhood);
+        std::vector<Patch8u> patchesVector;
+        std::vector<std::vector<double> > imagePointsVector;
+        sct.projectReferencePointsToImageWithFrames(referenceNeighborhood, featuresFrames, patchesVector,
+                                                    imagePointsVector);
+        for (size_t i = 0; i < patchesVector.size() && i < 16; i++)
+            write_pgm(dir + "/patch_" + std::to_string(i) + ".pgm", patchesVector[i]);
 
         write_raw(dir + "/out_matches.bin", matches.data(), matches.size());
         write_raw(dir + "/out_points.f64", points3D.data()->data(), points3D.size() * 3);

@@ -66,6 +66,8 @@ typedef struct fm3d_settings {
     int boundWidth, boundHeight; /* literal 1024 x 768 of extractPixelsContour (:359) */
     int strictNanExit;           /* 1: NaN plane makes fm3d_optimize_normals fail with FM3D_ERR_NAN_PLANE */
     int lmWaves;                 /* LM workgroups to launch (0 = fill the GPU) */
+    /* Neighborhoods.epsilon / cmPerPixel (neighborhoodsgenerator.cpp:43-44): patch export */
+    double neighEpsilon, cmPerPixel;
 } fm3d_settings;
 
 /* cv::DMatch layout */
@@ -174,6 +176,23 @@ int fm3d_get_pyramid_level(const fm3d_ctx *ctx, int which, int level, uint8_t *o
    evaluation count per pyramid level, may be NULL). */
 int fm3d_optimize_normals(fm3d_ctx *ctx, double *points, int P, double *normals, int32_t *status,
                           int32_t *info, int32_t *nfev, int *nKept, fm3d_lm_stats *stats);
+
+/* ---------------- feature frames + patch export (after the hot path) ---------------- */
+/* gravity_ of the NormalOptimizer ctor (normaloptimizer.cpp:160-178):
+   Rodrigues(rodriguesIC).inv() * (0, 0, -1) */
+int fm3d_gravity(const fm3d_settings *s, double g[3]);
+/* computeFeaturesFrames (normaloptimizer.cpp:454-504): one row-major 4x4 frame per (point, normal),
+   frames: 16*P doubles */
+int fm3d_features_frames(fm3d_ctx *ctx, const double *points, const double *normals, int P, double *frames);
+/* numberOfPointsPerEdge of getReferenceSquaredNeighborhood (neighborhoodsgenerator.cpp:134-158):
+   2*floor(epsilon / (0.01*cmPerPixel)) -- 128 with build/settings.yml */
+int fm3d_patch_size(const fm3d_settings *s);
+/* getReferenceSquaredNeighborhood + projectReferencePointsToImageWithFrames
+   (singlecameratriangulator.cpp:769-849) on image 1 of fm3d_set_images: per frame a size x size
+   8-bit patch, patches[f][j][i] = sample of reference point (i, j) (the reference's transposed
+   patch.at<uchar>(col, row)); imagePoints (may be NULL): 2*size*size doubles per frame, point order
+   i*size + j.  patches: P*size*size bytes. */
+int fm3d_export_patches(fm3d_ctx *ctx, const double *frames, int P, uint8_t *patches, double *imagePoints);
 
 /* ---------------- the whole hot path, device resident ---------------- */
 /* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */

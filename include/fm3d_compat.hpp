@@ -20,6 +20,7 @@
 #define FM3D_COMPAT_HPP
 
 #include <array>
+#include <cmath>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -52,6 +53,10 @@ struct Mat8u {  // CV_8UC1 image (rows x cols, row stride `step` bytes)
     const uint8_t* data;
     int step;
 };
+struct Patch8u {  // an owned CV_8UC1 patch (rows x cols, continuous)
+    int rows = 0, cols = 0;
+    std::vector<uint8_t> data;
+};
 struct DescMat {  // descriptor matrix: CV_32F rows, CV_8U rows, or binary strings
     int rows, cols;
     fm3d_desc_type type;  // FM3D_DESC_F32 / FM3D_DESC_U8 / FM3D_DESC_BITS (cols = bytes)
@@ -65,7 +70,9 @@ inline void check(fm3d_ctx* ctx, int rc) {
 // Owns the device context (settings + one HIP stream on one GPU).
 class Device {
 public:
-    explicit Device(const fm3d_settings& s, int device = 0) { check(nullptr, fm3d_ctx_create(&s, device, &ctx_)); }
+    explicit Device(const fm3d_settings& s, int device = 0) : settings_(s) {
+        check(nullptr, fm3d_ctx_create(&s, device, &ctx_));
+    }
     // cv::FileStorage fs(path) stand-in: the %YAML:1.0 subset build/settings.yml uses
     static fm3d_settings load_settings(const std::string& path) {
         fm3d_settings s;
@@ -76,9 +83,29 @@ public:
     Device(const Device&) = delete;
     Device& operator=(const Device&) = delete;
     fm3d_ctx* ctx() const { return ctx_; }
+    const fm3d_settings& settings() const { return settings_; }
 
 private:
     fm3d_ctx* ctx_ = nullptr;
+    fm3d_settings settings_;
+};
+
+// NeighborhoodsGenerator (neighborhoodsgenerator.h:78-97), the square method
+class NeighborhoodsGenerator {
+public:
+    explicit NeighborhoodsGenerator(const fm3d_settings& s) : s_(s) {}
+    // getReferenceSquaredNeighborhood (neighborhoodsgenerator.cpp:134-158): cleared, then size^2
+    // points (-epsilon + inc*i, -epsilon + inc*j, 0), i outer
+    void getReferenceSquaredNeighborhood(std::vector<Vec3d>& neighborhood) const {
+        const int n = fm3d_patch_size(&s_);
+        const double inc = s_.cmPerPixel * 0.01;
+        neighborhood.clear();
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) neighborhood.push_back(Vec3d{-s_.neighEpsilon + inc * i, -s_.neighEpsilon + inc * j, 0});
+    }
+
+private:
+    fm3d_settings s_;
 };
 
 // DescriptorsMatcher (descriptorsmatcher.h:39-111)
@@ -118,6 +145,32 @@ public:
         check(d_.ctx(), fm3d_setg12(d_.ctx(), T1.data(), T2.data(), r1.data(), r2.data(), g12.data()));
     }
     void setg12(const Matx44d& g12) { check(d_.ctx(), fm3d_set_g12(d_.ctx(), g12.data())); }
+    // projectReferencePointsToImageWithFrames (:769-849) on image 1 of NormalOptimizer::setImages:
+    // patchesVector / imagePointsVector are cleared, then one size x size patch (and its 2*size*size
+    // projected coordinates) per frame; patch row j, column i = reference point (i, j)
+    void projectReferencePointsToImageWithFrames(const std::vector<Vec3d>& referenceNeighborhood,
+                                                 const std::vector<Matx44d>& featuresFrames,
+                                                 std::vector<Patch8u>& patchesVector,
+                                                 std::vector<std::vector<double> >& imagePointsVector) {
+        patchesVector.clear();
+        imagePointsVector.clear();
+        const int P = (int)featuresFrames.size();
+        const int size = fm3d_patch_size(&d_.settings());  // the square neighbourhood the ABI rebuilds
+        if ((size_t)size * size != referenceNeighborhood.size())
+            throw Error(FM3D_ERR_INVALID, "reference neighbourhood is not the square one of the settings");
+        if (P == 0 || size == 0) return;
+        std::vector<uint8_t> patches((size_t)P * size * size);
+        std::vector<double> pts((size_t)P * size * size * 2);
+        check(d_.ctx(), fm3d_export_patches(d_.ctx(), featuresFrames.data()->data(), P, patches.data(), pts.data()));
+        for (int p = 0; p < P; p++) {
+            Patch8u m;
+            m.rows = m.cols = size;
+            m.data.assign(patches.begin() + (size_t)p * size * size, patches.begin() + (size_t)(p + 1) * size * size);
+            patchesVector.push_back(m);
+            imagePointsVector.push_back(std::vector<double>(pts.begin() + (size_t)p * size * size * 2,
+                                                            pts.begin() + (size_t)(p + 1) * size * size * 2));
+        }
+    }
     // setKeypoints (:145-171)
     void setKeypoints(const std::vector<KeyPoint>& k1, const std::vector<KeyPoint>& k2,
                       const std::vector<DMatch>& matches) {
@@ -151,7 +204,7 @@ private:
 // NormalOptimizer (normaloptimizer.h:43-59), hot-path methods
 class NormalOptimizer {
 public:
-    NormalOptimizer(Device& d, SingleCameraTriangulator* sct) : d_(d), sct_(sct) {}
+    NormalOptimizer(Device& d, SingleCameraTriangulator* sct) : d_(d), sct_(sct), settings_(d.settings()) {}
     // setImages (normaloptimizer.cpp:191-221): both gray images, builds the pyramids
     void setImages(const Mat8u& img1, const Mat8u& img2) {
         if (img1.rows != img2.rows || img1.cols != img2.cols || img1.step != img2.step)
@@ -176,6 +229,24 @@ public:
             normalsVector.push_back(Vec3d{nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]});
         }
     }
+    // getGravity (normaloptimizer.cpp:185-188)
+    Vec3d getGravity() const {
+        fm3d_settings s;
+        settings(s);
+        Vec3d g;
+        check(d_.ctx(), fm3d_gravity(&s, g.data()));
+        return g;
+    }
+    // computeFeaturesFrames (normaloptimizer.cpp:454-504): one frame per (point, normal), APPENDED
+    void computeFeaturesFrames(const std::vector<Vec3d>& points3D, const std::vector<Vec3d>& normalsVector,
+                               std::vector<Matx44d>& featuresFrames) {
+        const size_t n = points3D.size() < normalsVector.size() ? points3D.size() : normalsVector.size();
+        if (n == 0) return;
+        std::vector<Matx44d> f(n);
+        check(d_.ctx(), fm3d_features_frames(d_.ctx(), points3D.data()->data(), normalsVector.data()->data(), (int)n,
+                                             f.data()->data()));
+        featuresFrames.insert(featuresFrames.end(), f.begin(), f.end());
+    }
     // the PCL viewer thread (pclvisualizerthread.cpp) is visual only: no-ops
     void startVisualizerThread() {}
     void stopVisualizerThread() {}
@@ -184,8 +255,10 @@ public:
     const fm3d_lm_stats& lastStats() const { return stats_; }
 
 private:
+    void settings(fm3d_settings& s) const { s = settings_; }
     Device& d_;
     SingleCameraTriangulator* sct_;
+    fm3d_settings settings_;
     std::vector<int32_t> status_;
     fm3d_lm_stats stats_{};
 };

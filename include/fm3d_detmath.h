@@ -181,6 +181,12 @@ FM3D_HD double fm3d_atan2(double y, double x)
     return y < 0.0 ? -a : a;
 }
 
+/* acos(c) for c in [-1, 1] (cvRodrigues2, matrix -> vector) */
+FM3D_HD double fm3d_acos(double c)
+{
+    return fm3d_atan2(sqrt((1.0 - c) * (1.0 + c)), c);
+}
+
 FM3D_HD double fm3d_exp(double x)
 {
     double k, r, p;

@@ -1306,3 +1306,185 @@ ORC_API int orc_eval_residual(const orc_camera *cam, const double R2[9], const d
 }
 
 ORC_API double orc_blocked_sum_test(const double *v, int m, int NT) { return orc_blocked_sum(v, m, NT); }
+
+/* ------------------------------------------------------------------ */
+/* Feature frames + patch export              */
+/* ------------------------------------------------------------------ */
+/* NormalOptimizer ctor (normaloptimizer.cpp:160-178): gravity = Rodrigues(rodriguesIC).inv() *
+   (0,0,-1), with OpenCV 2.4's closed-form 3x3 Matx inverse (Matx_FastInvOp<_Tp,3>, determinant by
+   cofactors of the first row) and Matx * Vec accumulating from 0 in index order. */
+ORC_API void orc_gravity(const double rIC[3], double g[3])
+{
+    double a[9], b[9], d;
+    const double v[3] = {0, 0, -1};
+    int i, k;
+    orc_rodrigues_v2m(rIC, a);
+#define A(i, j) a[(i)*3 + (j)]
+    d = A(0, 0) * (A(1, 1) * A(2, 2) - A(2, 1) * A(1, 2)) - A(0, 1) * (A(1, 0) * A(2, 2) - A(2, 0) * A(1, 2)) +
+        A(0, 2) * (A(1, 0) * A(2, 1) - A(2, 0) * A(1, 1));
+    d = 1 / d;
+    b[0] = (A(1, 1) * A(2, 2) - A(1, 2) * A(2, 1)) * d;
+    b[1] = (A(0, 2) * A(2, 1) - A(0, 1) * A(2, 2)) * d;
+    b[2] = (A(0, 1) * A(1, 2) - A(0, 2) * A(1, 1)) * d;
+    b[3] = (A(1, 2) * A(2, 0) - A(1, 0) * A(2, 2)) * d;
+    b[4] = (A(0, 0) * A(2, 2) - A(0, 2) * A(2, 0)) * d;
+    b[5] = (A(0, 2) * A(1, 0) - A(0, 0) * A(1, 2)) * d;
+    b[6] = (A(1, 0) * A(2, 1) - A(1, 1) * A(2, 0)) * d;
+    b[7] = (A(0, 1) * A(2, 0) - A(0, 0) * A(2, 1)) * d;
+    b[8] = (A(0, 0) * A(1, 1) - A(0, 1) * A(1, 0)) * d;
+#undef A
+    for (i = 0; i < 3; i++) {
+        double s = 0;
+        for (k = 0; k < 3; k++) s += b[i * 3 + k] * v[k];
+        g[i] = s;
+    }
+}
+
+/* cv::normalize(v, v) of a Vec3d: scale = 1/||v|| (sum of squares from 0 in index order),
+   0 if ||v|| <= DBL_EPSILON; then v*scale + 0 (convertTo with scale and shift 0). */
+static void orc_normalize3(double v[3])
+{
+    double s = 0, scale;
+    int i;
+    for (i = 0; i < 3; i++) s += v[i] * v[i];
+    s = sqrt(s);
+    scale = s > DBL_EPSILON ? 1 / s : 0.;
+    for (i = 0; i < 3; i++) v[i] = v[i] * scale + 0.;
+}
+
+/* computeFeaturesFrames (normaloptimizer.cpp:454-504): z = n, x = g x z, y = z x x (before
+   normalisation), normalise x and y, columns (e.x, e.y, e.z) with Vec::dot accumulating from 0,
+   translation = the point.  frames: 16 doubles per point, row major. */
+ORC_API void orc_features_frames(const double *pts, const double *nrm, int P, const double g[3], double *frames)
+{
+    int p, r;
+    for (p = 0; p < P; p++) {
+        const double *z = nrm + 3 * p;
+        double x[3], y[3], *F = frames + 16 * p;
+        x[0] = g[1] * z[2] - g[2] * z[1];
+        x[1] = g[2] * z[0] - g[0] * z[2];
+        x[2] = g[0] * z[1] - g[1] * z[0];
+        y[0] = z[1] * x[2] - z[2] * x[1];
+        y[1] = z[2] * x[0] - z[0] * x[2];
+        y[2] = z[0] * x[1] - z[1] * x[0];
+        orc_normalize3(x);
+        orc_normalize3(y);
+        for (r = 0; r < 3; r++) {
+            const double e[3] = {r == 0, r == 1, r == 2};
+            F[4 * r + 0] = ((0 + e[0] * x[0]) + e[1] * x[1]) + e[2] * x[2];
+            F[4 * r + 1] = ((0 + e[0] * y[0]) + e[1] * y[1]) + e[2] * y[2];
+            F[4 * r + 2] = ((0 + e[0] * z[0]) + e[1] * z[1]) + e[2] * z[2];
+            F[4 * r + 3] = pts[3 * p + r];
+        }
+        F[12] = 0; F[13] = 0; F[14] = 0; F[15] = 1;
+    }
+}
+
+/* numberOfPointsPerEdge of getReferenceSquaredNeighborhood (neighborhoodsgenerator.cpp:136-137) */
+ORC_API int orc_patch_size(double eps, double cmpp)
+{
+    return 2 * ((int)floor(eps / (0.01 * cmpp)));
+}
+
+/* cvRodrigues2 round trip of decomposeTransformation + cvProjectPoints2, with libm (mode 0) or
+   the deterministic transcendentals (mode ORC_LM_DETMATH; acos(c) = atan2(sqrt((1-c)(1+c)), c)). */
+static void orc_frame_camera(const double F[16], int mode, double R2[9], double t2[3])
+{
+    double R[9], Y[9], r[3], rx, ry, rz, s, c, theta;
+    int it, k;
+    R[0] = F[0]; R[1] = F[1]; R[2] = F[2];
+    R[3] = F[4]; R[4] = F[5]; R[5] = F[6];
+    R[6] = F[8]; R[7] = F[9]; R[8] = F[10];
+    t2[0] = F[3]; t2[1] = F[7]; t2[2] = F[11];
+    if (!(mode & ORC_LM_DETMATH)) {
+        orc_rodrigues_m2v(R, r);
+        orc_rodrigues_v2m(r, R2);
+        return;
+    }
+    /* orc_rodrigues_m2v with fm3d_acos */
+    for (it = 0; it < 3; it++) {
+        orc_inv_t3(R, Y);
+        for (k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
+    }
+    rx = R[7] - R[5];
+    ry = R[2] - R[6];
+    rz = R[3] - R[1];
+    s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    theta = fm3d_acos(c);
+    if (s < 1e-5) {
+        double t;
+        if (c > 0)
+            rx = ry = rz = 0;
+        else {
+            t = (R[0] + 1) * 0.5;
+            rx = sqrt(t > 0. ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = sqrt(t > 0. ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = sqrt(t > 0. ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            theta /= sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta; ry *= theta; rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= theta;
+        rx *= vth; ry *= vth; rz *= vth;
+    }
+    /* orc_rodrigues_v2m with fm3d_cos / fm3d_sin */
+    theta = sqrt(rx * rx + ry * ry + rz * rz);
+    if (theta < DBL_EPSILON) {
+        for (k = 0; k < 9; k++) R2[k] = (k % 4 == 0) ? 1. : 0.;
+        return;
+    }
+    {
+        const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        double cc = fm3d_cos(theta), ss = fm3d_sin(theta), c1 = 1. - cc;
+        double itheta = theta ? 1. / theta : 0.;
+        double rrt[9], rxm[9];
+        rx *= itheta; ry *= itheta; rz *= itheta;
+        rrt[0] = rx * rx; rrt[1] = rx * ry; rrt[2] = rx * rz;
+        rrt[3] = rx * ry; rrt[4] = ry * ry; rrt[5] = ry * rz;
+        rrt[6] = rx * rz; rrt[7] = ry * rz; rrt[8] = rz * rz;
+        rxm[0] = 0; rxm[1] = -rz; rxm[2] = ry;
+        rxm[3] = rz; rxm[4] = 0; rxm[5] = -rx;
+        rxm[6] = -ry; rxm[7] = rx; rxm[8] = 0;
+        for (k = 0; k < 9; k++) R2[k] = cc * I[k] + c1 * rrt[k] + ss * rxm[k];
+    }
+}
+
+/* getReferenceSquaredNeighborhood (neighborhoodsgenerator.cpp:134-158) projected with every frame
+   (projectReferencePointsToImageWithFrame, singlecameratriangulator.cpp:805-849): point (i, j) =
+   (-eps + inc*i, -eps + inc*j, 0), inc = cmPerPixel*0.01; pixel outside isPixelGood(p, 1.0) of
+   image 1 (or NaN) -> 0, else (uchar) of the bilinear sample; written to patch row j, column i
+   (the reference's patch.at<uchar>(col, row)).  patches: P*size*size; imagePoints (may be NULL):
+   P*size*size*2 in point order i*size + j. */
+ORC_API int orc_export_patches(const orc_camera *cam, const uint8_t *img, int w, int h, const double *frames,
+                               int P, double eps, double cmpp, int mode, uint8_t *patches, double *imagePoints)
+{
+    const int size = orc_patch_size(eps, cmpp);
+    const double inc = cmpp * 0.01;
+    int p;
+    if (size <= 0) return 0;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (p = 0; p < P; p++) {
+        double R2[9], t2[3];
+        int i, j;
+        orc_frame_camera(frames + 16 * (size_t)p, mode, R2, t2);
+        for (i = 0; i < size; i++)
+            for (j = 0; j < size; j++) {
+                double u, v;
+                uint8_t val = 0;
+                orc_project1(cam, R2, t2, -eps + inc * i, -eps + inc * j, 0, &u, &v);
+                if (imagePoints) {
+                    imagePoints[((size_t)p * size * size + (size_t)i * size + j) * 2] = u;
+                    imagePoints[((size_t)p * size * size + (size_t)i * size + j) * 2 + 1] = v;
+                }
+                if (orc_pixel_good(u, v, 1.0, w, h)) val = (uint8_t)orc_bilinear(img, w, h, (float)u, (float)v);
+                patches[(size_t)p * size * size + (size_t)j * size + i] = val;
+            }
+    }
+    return size;
+}

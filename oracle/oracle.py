@@ -223,3 +223,36 @@ def blocked_sum(v, nt):
     f = lib().orc_blocked_sum_test
     f.restype = ctypes.c_double
     return f(_p(v), ctypes.c_int(v.size), ctypes.c_int(nt))
+
+
+def gravity(rIC):
+    g = np.zeros(3)
+    lib().orc_gravity(_p(_f64(rIC)), _p(g))
+    return g
+
+
+def features_frames(points, normals, g):
+    P = _f64(points).reshape(-1, 3)
+    N = _f64(normals).reshape(-1, 3)
+    frames = np.zeros((P.shape[0], 4, 4))
+    lib().orc_features_frames(_p(P), _p(N), ctypes.c_int(P.shape[0]), _p(_f64(g)), _p(frames))
+    return frames
+
+
+def patch_size(eps, cmpp):
+    return lib().orc_patch_size(ctypes.c_double(eps), ctypes.c_double(cmpp))
+
+
+def export_patches(cam, img1, frames, eps=0.16, cmpp=0.25, mode=STRICT, image_points=False):
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    h, w = img1.shape
+    F = _f64(frames).reshape(-1, 16)
+    n = F.shape[0]
+    size = patch_size(eps, cmpp)
+    patches = np.zeros((n, size, size), dtype=np.uint8)
+    pts = np.zeros((n, size * size, 2)) if image_points else None
+    c = OrcCamera.from_cam(cam)
+    lib().orc_export_patches(ctypes.byref(c), _p(img1, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _p(F),
+                             ctypes.c_int(n), ctypes.c_double(eps), ctypes.c_double(cmpp), ctypes.c_int(mode),
+                             _p(patches, ctypes.c_uint8), _p(pts) if pts is not None else None)
+    return (patches, pts) if image_points else patches

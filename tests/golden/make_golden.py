@@ -10,6 +10,9 @@ ships no test vectors):
                 operation order -> bit-exact targets), setg12 with numpy.linalg.inv
   dlt.npz       DLT triangulation with numpy.linalg.svd null vectors
   pyr.npz       cv::pyrDown via scipy.ndimage.correlate1d(mode="mirror") = reflect-101
+  patches.npz   computeFeaturesFrames + getReferenceSquaredNeighborhood +
+                projectReferencePointsToImageWithFrames (numpy: SVD polar factor, libm
+                acos/cos/sin, float32 bilinear, uint8 truncation, transposed write)
   lm.npz        NormalOptimizer::computeOptimizedNormals on a 160x120 pair with
                 pixelsRay 6: per level scipy.optimize.leastsq (MINPACK lmdif, lmfit's
                 tolerances) on a numpy evaluateNormal; aborts end the point (erase).
@@ -356,10 +359,70 @@ def make_lm():
     print("lm fixture:", np.bincount(status), "kept", int(np.sum(np.array(status) == 0)))
 
 
+# ---------------------------------------------------------------- patch export
+def make_patches():
+    """Feature frames (normaloptimizer.cpp:454-504) and normal-rectified patches
+    (neighborhoodsgenerator.cpp:134-158, singlecameratriangulator.cpp:769-849)."""
+    lm = np.load(os.path.join(HERE, "lm.npz"))
+    ok = lm["status"] == 0
+    pts, nrm = lm["points"][ok][:12], lm["normals"][ok][:12]
+    cam = synth.Camera.reference(160)
+    img1 = lm["img1"]
+    h, w = img1.shape
+    rIC = np.array([-1.2005, 1.1981, -1.2041])
+    g = np.linalg.inv(rodrigues_np(rIC)) @ np.array([0., 0., -1.])  # gravity, normaloptimizer.cpp:160-176
+    frames = np.zeros((len(pts), 4, 4))
+    for p in range(len(pts)):  # scalar float ops, the reference's order
+        z = [float(v) for v in nrm[p]]
+        x = [g[1] * z[2] - g[2] * z[1], g[2] * z[0] - g[0] * z[2], g[0] * z[1] - g[1] * z[0]]
+        y = [z[1] * x[2] - z[2] * x[1], z[2] * x[0] - z[0] * x[2], z[0] * x[1] - z[1] * x[0]]
+        for v in (x, y):  # cv::normalize: v * (1/||v||) + 0
+            s = 0.
+            for c in v:
+                s += c * c
+            s = math.sqrt(s)
+            sc = 1 / s if s > EPS else 0.
+            v[:] = [c * sc + 0. for c in v]
+        for r in range(3):
+            e = [float(r == 0), float(r == 1), float(r == 2)]
+            frames[p, r, :3] = [((0 + e[0] * b[0]) + e[1] * b[1]) + e[2] * b[2] for b in (x, y, z)]
+            frames[p, r, 3] = pts[p, r]
+        frames[p, 3] = [0, 0, 0, 1]
+    eps, cmpp = 0.04, 0.25
+    size = 2 * int(math.floor(eps / (0.01 * cmpp)))
+    inc = cmpp * 0.01
+    ref = np.array([(-eps + inc * i, -eps + inc * j, 0.) for i in range(size) for j in range(size)])
+    patches = np.zeros((len(pts), size, size), np.uint8)
+    imgpts = np.zeros((len(pts), size * size, 2))
+    for p in range(len(pts)):
+        R = frames[p, :3, :3]
+        U, _, Vt = np.linalg.svd(R)  # cvRodrigues2 matrix -> vector: nearest rotation U V^T
+        Q = U @ Vt
+        rx, ry, rz = Q[2, 1] - Q[1, 2], Q[0, 2] - Q[2, 0], Q[1, 0] - Q[0, 1]
+        s = math.sqrt((rx * rx + ry * ry + rz * rz) * 0.25)
+        c = min(1., max(-1., (Q[0, 0] + Q[1, 1] + Q[2, 2] - 1) * 0.5))
+        theta = math.acos(c)
+        vth = theta / (2 * s)
+        R2 = rodrigues_np(np.array([rx * vth, ry * vth, rz * vth]))
+        uv = project_np(cam, R2, frames[p, :3, 3], ref)
+        imgpts[p] = uv
+        good = pixel_good_np(uv[:, 0], uv[:, 1], 1.0, w, h)
+        val = np.zeros(len(ref), np.uint8)
+        u32, v32 = uv[:, 0].astype(np.float32), uv[:, 1].astype(np.float32)
+        val[good] = bilinear_np(img1, u32[good], v32[good]).astype(np.uint8)
+        patches[p] = val.reshape(size, size).T  # patch.at<uchar>(col, row): row j, column i
+    np.savez_compressed(os.path.join(HERE, "patches.npz"), img1=img1,
+                        cam=np.array([cam.fx, cam.fy, cam.cx, cam.cy, *cam.k]), rIC=rIC, g=g, points=pts,
+                        normals=nrm, frames=frames, eps=eps, cmpp=cmpp, size=size, patches=patches,
+                        image_points=imgpts)
+    print("patch fixture:", len(pts), "patches of", size, "x", size)
+
+
 if __name__ == "__main__":
     make_match()
     make_camera()
     make_dlt()
     make_pyr()
     make_lm()
+    make_patches()
     print("golden fixtures written to", HERE)

@@ -64,7 +64,7 @@ def test_library_exports_every_header_symbol(fm3d):
 def test_struct_layouts(fm3d):
     assert fm3d.DMATCH.itemsize == 16          # cv::DMatch
     assert fm3d.RECORD.itemsize == 64
-    assert ctypes.sizeof(fm3d.Settings) == 8 * 9 + 8 * 6 + 8 * 3 + 4 * 2 + 8 + 8 * 12 + 4 * 4
+    assert ctypes.sizeof(fm3d.Settings) == 8 * 9 + 8 * 6 + 8 * 3 + 4 * 2 + 8 + 8 * 12 + 4 * 4 + 8 * 2
 
 
 def test_settings_default_is_reference_file(fm3d):
@@ -108,3 +108,12 @@ def test_compute_without_gpu_fails_loudly(fm3d):
     has_gpu = os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES", "x") != ""
     if not has_gpu:
         assert "ERR" in out
+
+
+def test_gravity_and_patch_size_host(fm3d, orc):
+    s = fm3d.Settings.default()
+    g = np.zeros(3)
+    assert fm3d.lib().fm3d_gravity(ctypes.byref(s), g.ctypes.data_as(ctypes.POINTER(ctypes.c_double))) == 0
+    assert np.array_equal(g, orc.gravity(list(s.rodriguesIC)))  # same operations, bit for bit
+    assert fm3d.lib().fm3d_patch_size(ctypes.byref(s)) == 128
+    assert fm3d.NeighborhoodsGenerator(s).getReferenceSquaredNeighborhood().shape == (128 * 128, 3)

@@ -98,3 +98,17 @@ def test_example_main_matches_python_api(fm3d, synth, orc, tmp_path):
     assert np.array_equal(matches["queryIdx"], q) and np.array_equal(matches["trainIdx"], t)
     assert len(kept) > 10
     assert np.array_equal(pts, kept) and np.array_equal(nrm, normals)
+    # main.cpp:157-180: patch_<i>.pgm of the normal-rectified patches (P5 128 128, like results/)
+    s2 = fm3d.Settings.load(str(d / "settings.yml"))
+    ctx = fm3d.Context(s2)
+    try:
+        no = fm3d.NormalOptimizer(ctx)
+        no.setImages(pair.img1, pair.img2)
+        frames = no.computeFeaturesFrames(kept, normals)
+        patches = fm3d.SingleCameraTriangulator(ctx).projectReferencePointsToImageWithFrames(None, frames)
+    finally:
+        ctx.close()
+    for i in range(min(16, len(kept))):
+        raw = (d / f"patch_{i}.pgm").read_bytes()
+        assert raw.startswith(b"P5\n128 128\n255\n")
+        assert raw[len(b"P5\n128 128\n255\n"):] == patches[i].tobytes()

@@ -301,3 +301,37 @@ def test_sharded_blocks_equal_single_run(fm3d, pair):
     merged = np.concatenate(parts)
     assert len(full) > 100
     assert merged.tobytes() == full.tobytes()
+
+
+# ---------------------------------------------------------------- patch export (§8(f))
+def test_features_frames_and_patches_bitwise(fm3d, orc, pair):
+    """computeFeaturesFrames + getReferenceSquaredNeighborhood + projectReferencePointsToImageWithFrames
+    on the GPU: frames bit-exact, 128x128 patches and projected points bit-exact against the oracle's
+    deterministic-math mode, and within the truncation flips of the libm oracle."""
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    kept, normals, st, info, nfev, ref, _ = _normals_case(fm3d, orc, pair, pts[:60], 12)
+    assert len(kept) > 20
+    s = _settings(fm3d, pair.cam)
+    ctx = fm3d.Context(s)
+    try:
+        no = fm3d.NormalOptimizer(ctx)
+        no.setImages(pair.img1, pair.img2)
+        g = no.getGravity()
+        frames = no.computeFeaturesFrames(kept, normals)
+        ng = fm3d.NeighborhoodsGenerator(s)
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        patches, ipts = sct.projectReferencePointsToImageWithFrames(ng.getReferenceSquaredNeighborhood(), frames,
+                                                                    image_points=True)
+    finally:
+        ctx.close()
+    assert np.array_equal(g, orc.gravity(list(s.rodriguesIC)))
+    assert np.array_equal(frames, orc.features_frames(kept, normals, g))
+    assert patches.shape == (len(kept), 128, 128)
+    ref_p, ref_pts = orc.export_patches(pair.cam, pair.img1, frames, mode=orc.DETMATH, image_points=True)
+    assert np.array_equal(ipts, ref_pts)
+    assert np.array_equal(patches, ref_p)
+    strict = orc.export_patches(pair.cam, pair.img1, frames, mode=orc.STRICT)
+    d = np.abs(patches.astype(int) - strict.astype(int))
+    assert d.max() <= 1 and (d == 0).mean() > 0.999
+    assert (patches > 0).mean() > 0.5  # the patches see the textured scene

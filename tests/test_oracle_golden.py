@@ -116,3 +116,31 @@ def test_blocked_sum_order(orc):
         seq = seq + x
     assert orc.blocked_sum(v, 0) == seq
     assert abs(orc.blocked_sum(v, 256) - seq) < 1e-12
+
+
+def test_features_frames_and_patches_vs_numpy(orc):
+    """computeFeaturesFrames + patch export: the oracle against the numpy restatement
+    (tests/golden/make_golden.py make_patches): frames bit for bit (same scalar operations),
+    gravity to 1e-15 (numpy inverts by LU), patches allowing the rare 1-level truncation flip
+    that the SVD-vs-Newton polar factor and libm ulps can cause."""
+    g = load("patches.npz")
+    cam = Cam(g["cam"])
+    assert np.abs(orc.gravity(g["rIC"]) - g["g"]).max() < 1e-15
+    frames = orc.features_frames(g["points"], g["normals"], g["g"])
+    assert np.array_equal(frames, g["frames"])
+    eps, cmpp = float(g["eps"]), float(g["cmpp"])
+    assert orc.patch_size(eps, cmpp) == int(g["size"])
+    patches, pts = orc.export_patches(cam, g["img1"], frames, eps, cmpp, mode=orc.STRICT, image_points=True)
+    assert np.abs(pts - g["image_points"]).max() < 1e-9
+    d = np.abs(patches.astype(int) - g["patches"].astype(int))
+    assert d.max() <= 1 and (d == 0).mean() > 0.99
+    # DETMATH (the GPU's transcendentals) moves nothing here beyond the same truncation flips
+    p2 = orc.export_patches(cam, g["img1"], frames, eps, cmpp, mode=orc.DETMATH)
+    assert np.abs(p2.astype(int) - patches.astype(int)).max() <= 1
+
+
+def test_reference_patch_size():
+    """build/settings.yml (Neighborhoods epsilon 0.16, cmPerPixel 0.25) gives the 128x128 patches
+    of the reference's results/*/patch_*.pgm (P5 128 128)."""
+    import oracle
+    assert oracle.patch_size(0.16, 0.25) == 128
