@@ -422,9 +422,9 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     if (cap < 1) cap = 1;
     if (groups > cap) groups = cap;
     if (groups < 1) groups = 1;
-    // +8 KiB: the passes prefetch up to four 64-entry chunks past a slot's last entry
-    HIPCHK(c, c->slab.ensure(ents * 2 * sizeof(double) * groups + 8192));
-    HIPCHK(c, c->slabI1.ensure(ents * 5 * 4 * groups + 8192));
+    // +8 KiB: the passes prefetch up to eight 64-entry chunks past a slot's last entry
+    HIPCHK(c, c->slab.ensure(ents * 2 * sizeof(double) * groups + 16384));
+    HIPCHK(c, c->slabI1.ensure(ents * 5 * 4 * groups + 16384));
     fm3d::LMParams p{};
     p.points = c->pts.as<double>();
     p.P = P;

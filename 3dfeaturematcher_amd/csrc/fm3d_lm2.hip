@@ -943,7 +943,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                             prod.put(sl0 ? a : t0, t1, sl0 ? 1 : 0);
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry
-                        constexpr int kQD = 4;
+                        constexpr int kQD = 8;
                         Ld buf[kQD];
 #pragma unroll
                         for (int j = 0; j < kQD; j++) buf[j] = load(j);
