@@ -18,7 +18,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfm3d.so")
+# FM3D_LIB selects another in-tree build of the same library (A/B performance experiments)
+LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
