@@ -335,3 +335,57 @@ def test_features_frames_and_patches_bitwise(fm3d, orc, pair):
     d = np.abs(patches.astype(int) - strict.astype(int))
     assert d.max() <= 1 and (d == 0).mean() > 0.999
     assert (patches > 0).mean() > 0.5  # the patches see the textured scene
+
+
+# ---------------------------------------------------------------- BASELINE configs as parity cases
+def test_c2_sift10k_match_and_dlt(fm3d, orc, synth):
+    """BASELINE configs[1] (C2): 10k SIFT-128 per frame, brute-force L2 match + NNDR + DLT --
+    match indices, distances, inlier mask and points bit-exact against the oracle."""
+    fp = synth.make_frame_pair(10_000, seed=101)
+    ctx = fm3d.Context(_settings(fm3d, fp.cam))
+    try:
+        m = fm3d.DescriptorsMatcher(ctx).compareWithNNDR(0.55, fp.desc1, fp.desc2)
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(fp.g12)
+        sct.setKeypoints(fp.kp1, fp.kp2, m)
+        pts, mask = sct.triangulate()
+    finally:
+        ctx.close()
+    q, t, d = orc.match_nndr(fp.desc1, fp.desc2, orc.U8, 0.55, oracle_threads())
+    assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t) and np.array_equal(m["distance"], d)
+    pto, masko = orc.triangulate(fp.cam, fp.g12, 1.5, 2.4, fp.kp1, fp.kp2, q, t)
+    assert np.array_equal(mask, masko) and np.array_equal(pts, pto)
+    assert len(q) > 8000 and np.mean(fp.true_train[q] == t) > 0.99
+
+
+def test_c3_orb10k_pipeline_ray32(fm3d, orc, synth):
+    """BASELINE configs[2] (C3): 10k ORB-256 (Hamming) + normals on 64x64-pixel neighbourhoods
+    (pixelsRay 32), through the device-resident pipeline.  Matching and DLT are checked in full;
+    the LM on the records of the first 150 triangulated points (the oracle's CPU time bound)."""
+    fp = synth.make_frame_pair(10_000, seed=102, desc="orb")
+    s = _settings(fm3d, fp.cam, pixelsRay=32, nndrEpsilon=0.8)
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(fp.g12)
+        R2, t2 = sct.camera2()
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2, binary=True)
+        n, stats = pipe.run()
+        rec = pipe.records(n)
+    finally:
+        ctx.close()
+    q, t, _ = orc.match_nndr(fp.desc1, fp.desc2, orc.BITS, 0.8, oracle_threads())
+    assert stats["matches"] == len(q)
+    pts, mask = orc.triangulate(fp.cam, fp.g12, 1.5, 2.4, fp.kp1, fp.kp2, q, t)
+    assert stats["inliers"] == len(pts)
+    k = 150
+    ref = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, 3, pts[:k], 32, mode=orc.DETMATH,
+                               nthreads=oracle_threads())
+    ok = ref["status"] == 0
+    qi = q[mask][:k]
+    sub = rec[np.isin(rec["queryIdx"], qi)]
+    assert np.array_equal(sub["queryIdx"], qi[ok])
+    assert np.array_equal(sub["point"], pts[:k][ok])
+    assert np.array_equal(sub["normal"], ref["normals"][ok])
+    assert n > 0.3 * len(pts)
