@@ -1,0 +1,64 @@
+// fm3d_fastdiv.h -- divisions with IEEE results at fewer VALU instructions (gfx950).
+//
+// The compiler's fp64 division is v_div_scale x2, v_rcp, two Newton steps, a multiply,
+// one Markstein correction, v_div_fmas and v_div_fixup (11 instructions).  Where the
+// operands need no scaling and no special-case fix-up, the same steps without
+// v_div_scale / v_div_fmas / v_div_fixup produce the same bits; outside the guarded
+// ranges these helpers fall back to the division operator.  tools/micro/div_check.hip
+// compares every helper with the division operator on random operands.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace fm3d {
+
+// a / d with y = RN(1/d) precomputed (pass-uniform d): q0 = RN(a*y) is within one ulp of
+// a/d, and one Markstein step q0 + (a - d*q0)*y (residual exact by FMA) rounds correctly.
+// mok (pass-uniform) requires 1e-200 < |d| < 1e200; |a| < 1e100 keeps the quotient normal
+// for the operands the LM passes divide (|a| is 0 or above 1e-60: products of float
+// intensity differences and O(1) weights).  a = -0 with d > 0 gives +0 (IEEE: -0); the
+// passes never divide -0: their numerators are differences, +0 when the operands are equal.
+__device__ __forceinline__ double mdiv(double a, double d, double y, bool mok) {
+    if (mok && fabs(a) < 1e100) {
+        const double q0 = a * y;
+        const double r = __builtin_fma(-d, q0, a);
+        return __builtin_fma(r, y, q0);
+    }
+    return a / d;
+}
+__device__ __forceinline__ bool mdiv_ok(double d) { return fabs(d) > 1e-200 && fabs(d) < 1e200; }
+
+// z ? 1/z : 1 (cvProjectPoints2).  For 2^-700 <= |z| <= 2^700 the hardware sequence
+// scales nothing (exponent gap < 768, 1/z normal) and fixes nothing up.
+__device__ __forceinline__ double recip_z(double z) {
+    const double az = fabs(z);
+    if (az >= 0x1p-700 && az <= 0x1p700) {
+        double r = __builtin_amdgcn_rcp(z);
+        double e = __builtin_fma(-z, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        e = __builtin_fma(-z, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        const double rem = __builtin_fma(-z, r, 1.0);
+        return __builtin_fma(rem, r, r);
+    }
+    return z ? 1. / z : 1.;
+}
+
+// mm / nn with a pass-uniform numerator: mok = 2^-600 <= |mm| <= 2^60 (div_nn_ok), and
+// 2^-600 <= |nn| <= 2^60 per lane -- exponent gap < 768, quotient and remainder normal.
+__device__ __forceinline__ bool div_nn_ok(double mm) { return fabs(mm) >= 0x1p-600 && fabs(mm) <= 0x1p60; }
+__device__ __forceinline__ double div_nn(double mm, double nn, bool mok) {
+    const double an = fabs(nn);
+    if (mok && an >= 0x1p-600 && an <= 0x1p60) {
+        double r = __builtin_amdgcn_rcp(nn);
+        double e = __builtin_fma(-nn, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        e = __builtin_fma(-nn, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        const double q = mm * r;
+        const double rem = __builtin_fma(-nn, q, mm);
+        return __builtin_fma(rem, r, q);
+    }
+    return mm / nn;
+}
+
+}  // namespace fm3d

@@ -421,6 +421,9 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     long cap = (long)(budget / perGroup);
     if (cap < 1) cap = 1;
     if (groups > cap) groups = cap;
+    // the summed passes address a slab array with a 32-bit byte offset
+    const long cap32 = (long)((((size_t)1 << 32) - ((size_t)1 << 20)) / (ents * sizeof(double)));
+    if (groups > cap32) groups = cap32;
     if (groups < 1) groups = 1;
     // +8 KiB: the passes prefetch up to eight 64-entry chunks past a slot's last entry
     HIPCHK(c, c->slab.ensure(ents * 2 * sizeof(double) * groups + 16384));
@@ -436,6 +439,13 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         std::memcpy(pc.R, c->R2, sizeof(pc.R));
         std::memcpy(pc.t, c->t2, sizeof(pc.t));
         pc.cam = c->cam;
+        const size_t Gn = (size_t)groups * slots * c->nOffPad;  // entries per slab array
+        pc.slabRX = (const char*)c->slab.p;
+        pc.slabRY = pc.slabRX + Gn * sizeof(double);
+        pc.slabI1 = (const char*)c->slabI1.p;
+        pc.slabDF = (char*)c->slabI1.p + Gn * 4;
+        pc.slabDJ0 = pc.slabDF + Gn * 4;
+        pc.slabDJ1 = pc.slabDJ0 + Gn * 4;
         HIPCHK(c, c->lmProj.ensure(sizeof(pc)));
         HIPCHK(c, hipMemcpyAsync(c->lmProj.p, &pc, sizeof(pc), hipMemcpyHostToDevice, c->stream));
         p.proj = c->lmProj.as<fm3d::ProjConst>();

@@ -19,6 +19,10 @@ struct LevelDesc {
 struct ProjConst {
     double R[9], t[3];
     Camera cam;
+    // LM slab array bases (grid-uniform): the summed passes re-read them per chunk
+    // with scalar loads and address entries by one 32-bit byte offset
+    const char *slabRX, *slabRY, *slabI1;
+    char *slabDF, *slabDJ0, *slabDJ1;
 };
 
 struct LMParams {

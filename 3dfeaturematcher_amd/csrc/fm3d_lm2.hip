@@ -38,6 +38,7 @@
 #include <type_traits>
 
 #include "fm3d_device.h"
+#include "fm3d_fastdiv.h"
 #include "fm3d_kernels.h"
 #include "fm3d_lmdif.h"
 
@@ -50,6 +51,7 @@ using namespace lmdif;
 constexpr int kW = kLM2Slots;  // term waves (slots) per workgroup
 constexpr int kE = 64;         // entries per chunk: one per lane
 constexpr int kR = kLM2Ring;   // chunks in flight per slot (LDS ring depth)
+static_assert((kR & (kR - 1)) == 0, "ring depth: a power of two");
 constexpr int kRow = kE + 2;   // padded ring row: consecutive rows start 4 banks apart
 
 enum PassKind2 { Q_IDLE = 0, Q_INIT, Q_LEVEL, Q_EVAL, Q_QR1, Q_QR2, Q_QR3, Q_DONE };
@@ -60,20 +62,8 @@ typedef __attribute__((address_space(1))) float gfloat;
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) const long long gi64;  // an int2 offset (x low, y high)
 typedef __attribute__((address_space(1))) const uint8_t gu8;
+typedef __attribute__((address_space(1), aligned(1))) const uint16_t gu16u;  // a byte pair at any address
 
-// a / d with y = RN(1/d): q0 = RN(a*y) is within one ulp of a/d, and one Markstein step
-// q0 + (a - d*q0)*y (residual exact by FMA) rounds correctly (round to nearest, no
-// overflow/underflow).  Guarded: mok (pass-uniform) requires 1e-200 < |d| < 1e200, and
-// |a| < 1e100 keeps the quotient normal; outside that, IEEE division.
-__device__ __forceinline__ double mdiv(double a, double d, double y, bool mok) {
-    if (mok && fabs(a) < 1e100) {
-        const double q0 = a * y;
-        const double r = __builtin_fma(-d, q0, a);
-        return __builtin_fma(r, y, q0);
-    }
-    return a / d;
-}
-__device__ __forceinline__ bool mdiv_ok(double d) { return fabs(d) > 1e-200 && fabs(d) < 1e200; }
 
 // enorm terms: x^2 in MINPACK's intermediate range (the branch almost every value
 // takes), +0 otherwise -- an exact no-op on the non-negative running sum.  Values outside
@@ -503,6 +493,10 @@ __device__ __forceinline__ double chain_sum64(double sum, const double* t) {
 }
 
 __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ const uint8_t* rfl_ptr(const uint8_t* q) {
+    const unsigned long long v = (unsigned long long)q;
+    return (const uint8_t*)(((unsigned long long)(unsigned)rfl((int)(v >> 32)) << 32) | (unsigned)rfl((int)v));
+}
 
 // ---------------------------------------------------------------- term wave
 // Publishes chunk `seq` of slot w: waits for ring space, writes the two term rows,
@@ -515,13 +509,13 @@ struct Producer {
     long long waitCycles;
 
     __device__ __forceinline__ void put(double t0, double t1, int slowBits) {
-        double* row0 = &sh->ring[w][seq % kR][0][0];
+        // seq and room are wave-uniform: kept in SGPRs (readfirstlane on every LDS read)
         if (room == 0) {
             // ring space: both chain lanes of the slot have consumed chunk seq - kR.  The
             // counters are read only when the space seen last time is used up.
             const long long c0 = clock64();
             for (;;) {
-                const int c = min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1]));
+                const int c = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])));
                 room = c + kR - seq;
                 if (room > 0) break;
                 __builtin_amdgcn_s_sleep(1);
@@ -529,9 +523,12 @@ struct Producer {
             waitCycles += clock64() - c0;
         }
         room--;
+        seq = rfl(seq);
+        const int pos = seq & (kR - 1);
+        double* row0 = &sh->ring[w][pos][0][0];
         row0[lane] = t0;
         row0[kRow + lane] = t1;
-        if (lane == 0) sh->chunkSlow[w][seq % kR] = slowBits;
+        if (lane == 0) sh->chunkSlow[w][pos] = slowBits;
         // every lane's ring stores are done before lane 0 publishes (lgkmcnt is per wave)
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         if (lane == 0) lds_store_rel(&sh->produced[w], seq + 1);
@@ -591,6 +588,78 @@ __device__ __forceinline__ Geo geometry(const LMParams& p, double ux, double uy,
     r.g = (const gu8*)img2;
     if (cd == 0) r.g += (long)(int)floorf(r.fy) * lw + (int)floorf(r.fx);
     return r;
+}
+
+// geometry() for the summed passes: the same arithmetic, reduced to what they consume.
+//  * inbox: isInBoundingBox of the plane point; false for a NaN coordinate too (the
+//    NaN-plane / bounding-box distinction is recomputed for the rare failing lane);
+//  * good: inbox and isPixelGood of the camera-2 pixel (NaN -> false).  u, v are only
+//    used when good, so the r6 NaN propagation of project1 is not needed: an infinite or
+//    NaN r6 makes u or v infinite or NaN either way;
+//  * off: byte offset of the bilinear window in image 2 (0 when not good).
+struct Geo2 {
+    float fx, fy;
+    unsigned off;
+    bool inbox, good;
+};
+__device__ __forceinline__ Geo2 geometry2(const LMParams& p, double ux, double uy, double n0, double n1, double n2,
+                                          double mm, bool mmok, double scale, double xmax, double ymax, int lw,
+                                          double cm) {
+    const cProjConst* pc = proj_consts(p.proj);
+    Geo2 r;
+    const double nn = n0 * ux + n1 * uy + n2 * 1.;
+    const double kk = div_nn(mm, nn, mmok);
+    const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+    r.inbox = fabs(P0) < cm && fabs(P1) < cm && P2 > 0. && P2 < cm;
+    double x = pc->R[0] * P0 + pc->R[1] * P1 + pc->R[2] * P2 + pc->t[0];
+    double y = pc->R[3] * P0 + pc->R[4] * P1 + pc->R[5] * P2 + pc->t[1];
+    const double z = recip_z(pc->R[6] * P0 + pc->R[7] * P1 + pc->R[8] * P2 + pc->t[2]);
+    x *= z;
+    y *= z;
+    const double r2 = x * x + y * y;
+    const double r4 = r2 * r2;
+    const double r6 = r4 * r2;
+    const double a1 = 2 * x * y;
+    const double a2 = r2 + 2 * x * x;
+    const double a3 = r2 + 2 * y * y;
+    const double cdist = 1 + pc->cam.k[0] * r2 + pc->cam.k[1] * r4 + pc->cam.k[4] * r6;
+    const double xd = x * cdist + pc->cam.k[2] * a1 + pc->cam.k[3] * a2;
+    const double yd = y * cdist + pc->cam.k[2] * a3 + pc->cam.k[3] * a1;
+    const double u = xd * pc->cam.fx + pc->cam.cx;
+    const double v = yd * pc->cam.fy + pc->cam.cy;
+    r.good = r.inbox && u >= 0 && u <= xmax && v >= 0 && v <= ymax;
+    r.fx = (float)(scale * u);
+    r.fy = (float)(scale * v);
+    r.off = r.good ? (unsigned)((int)floorf(r.fy) * lw + (int)floorf(r.fx)) : 0u;
+    return r;
+}
+
+// failure code of geometry() (2 NaN plane point, 3 outside the bounding box) for an entry
+// whose inbox is false: the rare path of the summed passes
+__device__ __noinline__ int plane_code(double ux, double uy, double n0, double n1, double n2, double mm) {
+    const double nn = n0 * ux + n1 * uy + n2 * 1.;
+    const double kk = mm / nn;
+    const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+    return (P0 != P0 || P1 != P1 || P2 != P2) ? 2 : 3;
+}
+
+// getBilinearInterpPix32f on the gathered window, the floors taken from the sample
+// coordinates (exact: |x| < 2^24 wherever the value is used)
+__device__ __forceinline__ float bilinear_w(unsigned lo, unsigned hi, float x, float y) {
+    const float x0 = floorf(x), y0 = floorf(y);
+    const float b00 = (float)(lo & 0xff), b01 = (float)((lo >> 8) & 0xff);
+    const float b10 = (float)(hi & 0xff), b11 = (float)((hi >> 8) & 0xff);
+    const float xm0 = 1.0f - (x - x0), xm1 = (x - x0);
+    const float ym0 = 1.0f - (y - y0), ym1 = (y - y0);
+    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
+}
+
+// enorm term with the slow-path flag: x^2 is the term whenever no lane of the chunk needs
+// MINPACK's small/large component handling (x = 0 adds +0, as enorm does)
+__device__ __forceinline__ double enorm_term2(double x, double agiant, bool& slow) {
+    const double xa = fabs(x);
+    slow = !(xa < agiant) || (xa <= 3.834e-20 && xa != 0.);
+    return x * x;
 }
 
 // ======================= chain wave =======================
@@ -680,10 +749,13 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
 
     if (wave < kW) {
         // ======================= term wave: slot w =======================
-        const int w = wave;
+        const int w = rfl(wave);
         const long gslot = (long)blockIdx.x * kW + w;
         Ctl2& ctl = sh.ctl[w];
         const Slab sl = slab_of(p, gslot);
+        // the summed passes address the slabs as grid-uniform array bases (ProjConst, scalar
+        // loads) + one 32-bit byte offset per entry (global_load ... vOffset, sBase)
+        const unsigned slot8 = (unsigned)((size_t)gslot * p.nOffPad * 8);  // < 2^32 (host-checked)
         if (lane == 0) {
             ctl.p = &sh.P;
             ctl.sl = sl;
@@ -789,6 +861,11 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                     const bool i1ok = rfl(SS.i1ok) != 0;
                     // NEV evaluations per entry (2: both forward-difference columns); JAC: the
                     // values are Jacobian columns (r - fvec)/h_j, else the residual fvec itself
+                    const bool mmok0 = div_nn_ok(mm0);
+                    const bool mmok1 = div_nn_ok(mm1);
+                    const gu8* img2b = (const gu8*)rfl_ptr(img2);
+                    // NEV evaluations per entry (2: both forward-difference columns); JAC: the
+                    // values are Jacobian columns (r - fvec)/h_j, else the residual fvec itself
                     auto run = [&](auto nevc, auto jacc) {
                         constexpr int NEV = decltype(nevc)::value;
                         constexpr bool JAC = decltype(jacc)::value;
@@ -796,83 +873,86 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                             double ux, uy, dF;
                             float i1;
                         };
-                        // entries past len (up to two chunks past the pass) read slab padding
-                        auto load = [&](int k) {
+                        // o8 / o4: byte offsets of the chunk's entries in the 8- / 4-byte slab arrays.
+                        // Entries past len (up to three chunks past the pass) read slab padding.
+                        auto load = [&](unsigned o8, unsigned o4) {
+                            const cProjConst* pc = proj_consts(p.proj);
                             Ld L;
-                            const int e = k * kE + lane;
-                            L.ux = sl.RX[e];
-                            L.uy = sl.RY[e];
-                            L.i1 = sl.I1[e];
-                            L.dF = JAC ? (double)sl.DF[e] : 0.;
+                            L.ux = *(const gdouble*)(pc->slabRX + o8);
+                            L.uy = *(const gdouble*)(pc->slabRY + o8);
+                            L.i1 = *(const gfloat*)(pc->slabI1 + o4);
+                            L.dF = JAC ? (double)*(const gfloat*)(pc->slabDF + o4) : 0.;
                             return L;
                         };
-                        auto chunk = [&](const Ld& L, int k) {
-                            const int e = k * kE + lane;
-                            const bool in = e < len;
-                            const Geo g0 = geometry(p, L.ux, L.uy, n00, n10, n20, mm0, scale, xmax, ymax, img2, lw, cm);
-                            Geo g1;
+                        auto gather = [&](unsigned off) {  // two byte pairs: (y0, x0..x0+1), (y0+1, ...)
+                            return make_uint2(*(const gu16u*)(img2b + off), *(const gu16u*)(img2b + (off + lw)));
+                        };
+                        auto chunk = [&](const Ld& L, int k, unsigned o4) {
+                            const bool in = k * kE + lane < len;
+                            const Geo2 g0 = geometry2(p, L.ux, L.uy, n00, n10, n20, mm0, mmok0, scale, xmax, ymax, lw, cm);
+                            Geo2 g1;
                             if (NEV == 2)
-                                g1 = geometry(p, L.ux, L.uy, n01, n11, n21, mm1, scale, xmax, ymax, img2, lw, cm);
-                            // gathers for every lane: a failed entry's address is the image base
-                            const uint8_t a00 = g0.g[0], a01 = g0.g[1], a10 = g0.g[lw], a11 = g0.g[lw + 1];
-                            uint8_t c00 = 0, c01 = 0, c10 = 0, c11 = 0;
-                            if (NEV == 2) {
-                                c00 = g1.g[0];
-                                c01 = g1.g[1];
-                                c10 = g1.g[lw];
-                                c11 = g1.g[lw + 1];
-                            }
+                                g1 = geometry2(p, L.ux, L.uy, n01, n11, n21, mm1, mmok1, scale, xmax, ymax, lw, cm);
+                            // gathers for every lane: a failed entry reads the image's first bytes
+                            const uint2 a = gather(g0.off);
+                            uint2 c;
+                            if (NEV == 2) c = gather(g1.off);
                             // failures: first NaN-plane / bounding-box pixel in index order; image-2 flags
                             {
-                                const unsigned long long b0 = __ballot(in && (g0.code == 2 || g0.code == 3));
+                                const unsigned long long b0 = __ballot(in && !g0.inbox);
                                 if (b0 && fail0 == 0x7fffffff) {
                                     const int l = __ffsll((long long)b0) - 1;
-                                    fail0 = (k * kE + l) * 4 + __shfl(g0.code, l);
+                                    const int cd = plane_code(L.ux, L.uy, n00, n10, n20, mm0);
+                                    fail0 = (k * kE + l) * 4 + __shfl(cd, l);
                                 }
-                                ph30 |= __ballot(in && g0.code == 4) != 0;
+                                ph30 |= __ballot(in && g0.inbox && !g0.good) != 0;
                                 if (NEV == 2) {
-                                    const unsigned long long b1 = __ballot(in && (g1.code == 2 || g1.code == 3));
+                                    const unsigned long long b1 = __ballot(in && !g1.inbox);
                                     if (b1 && fail1 == 0x7fffffff) {
                                         const int l = __ffsll((long long)b1) - 1;
-                                        fail1 = (k * kE + l) * 4 + __shfl(g1.code, l);
+                                        const int cd = plane_code(L.ux, L.uy, n01, n11, n21, mm1);
+                                        fail1 = (k * kE + l) * 4 + __shfl(cd, l);
                                     }
-                                    ph31 |= __ballot(in && g1.code == 4) != 0;
+                                    ph31 |= __ballot(in && g1.inbox && !g1.good) != 0;
                                 }
                             }
                             // evaluateNormal :145-148 (fvec), fdjac2 forward differences (JAC)
-                            const float dI0 = L.i1 - bilinear4(a00, a01, a10, a11, g0.fx, g0.fy);
+                            const float dI0 = L.i1 - bilinear_w(a.x, a.y, g0.fx, g0.fy);
                             const double r0 = w0 * (double)dI0;
                             double v0 = JAC ? mdiv(r0 - wF * L.dF, h0, y0, mok0) : r0;
-                            v0 = (in && i1ok && g0.code == 0) ? v0 : 0.;
-                            if (JAC)
-                                sl.DJ0[e] = dI0;
-                            else
-                                sl.DF[e] = dI0;
+                            v0 = (in && i1ok && g0.good) ? v0 : 0.;
+                            {
+                                const cProjConst* pc = proj_consts(p.proj);
+                                *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + o4) = dI0;
+                            }
                             bool slow0 = false, slow1 = false;
-                            const double t0 = enorm_term(v0, agiant, slow0);
+                            const double t0 = enorm_term2(v0, agiant, slow0);
                             double v1 = 0., t1 = 0.;
                             if (NEV == 2) {
-                                const float dI1 = L.i1 - bilinear4(c00, c01, c10, c11, g1.fx, g1.fy);
+                                const float dI1 = L.i1 - bilinear_w(c.x, c.y, g1.fx, g1.fy);
                                 const double r1 = w1 * (double)dI1;
                                 v1 = mdiv(r1 - wF * L.dF, h1, y1, mok1);
-                                v1 = (in && i1ok && g1.code == 0) ? v1 : 0.;
-                                sl.DJ1[e] = dI1;
-                                t1 = enorm_term(v1, agiant, slow1);
+                                v1 = (in && i1ok && g1.good) ? v1 : 0.;
+                                *(gfloat*)(proj_consts(p.proj)->slabDJ1 + o4) = dI1;
+                                t1 = enorm_term2(v1, agiant, slow1);
                             }
                             const bool s0 = __ballot(slow0) != 0, s1 = __ballot(slow1) != 0;
                             prod.put(s0 ? v0 : t0, s1 ? v1 : t1, (s0 ? 1 : 0) | (s1 ? 2 : 0));
                         };
                         // two chunks of slab loads in flight ahead of the one being computed
-                        Ld A = load(0), B = load(1);
+                        unsigned o8 = slot8 + lane * 8u, o4 = o8 >> 1;
+                        Ld A = load(o8, o4), B = load(o8 + 512u, o4 + 256u);
                         for (int k = 0; k < nCh; k += 2) {
-                            const Ld C = load(k + 2);
-                            chunk(A, k);
+                            const Ld C = load(o8 + 1024u, o4 + 512u);
+                            chunk(A, k, o4);
                             A = C;
                             if (k + 1 < nCh) {
-                                const Ld D = load(k + 3);
-                                chunk(B, k + 1);
+                                const Ld D = load(o8 + 1536u, o4 + 768u);
+                                chunk(B, k + 1, o4 + 256u);
                                 B = D;
                             }
+                            o8 += 1024u;
+                            o4 += 512u;
                         }
                     };
                     if (nev == 2)

@@ -226,6 +226,17 @@ def lm_profile(lm):
     }
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(pair, s, gpu_stats, args):
     """Time the CPU oracle (reference algorithm, C + OpenMP) on a bounded sample of the
     same workload and extrapolate to the full frame pair."""
@@ -259,11 +270,24 @@ def cpu_baseline(pair, s, gpu_stats, args):
     dt = time.perf_counter() - t
     t_lm = dt / npts * gpu_stats["inliers"]
     total = t_match + t_tri + t_lm
+    # the same stages on one core (both 1-thread and all-cores figures)
+    t = time.perf_counter()
+    orc.knn2(pair.desc1[:256], pair.desc2, orc.U8, 1)
+    t1_match = (time.perf_counter() - t) / 256 * nA
+    t = time.perf_counter()
+    orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts[:2], s.pixelsRay,
+                         mode=orc.STRICT, nthreads=1)
+    t1_lm = (time.perf_counter() - t) / 2 * gpu_stats["inliers"]
+    total1 = t1_match + t_tri + t1_lm
     return {
         "value": gpu_stats["kept"] / total,
         "unit": "keypoints/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": cpu_model(),
+        "single_thread": {"value": gpu_stats["kept"] / total1, "unit": "keypoints/s", "cores": 1,
+                          "sample": f"knn2 of 256 queries, LM normals of 2 points, 1 thread (est. {total1:.0f} s "
+                                    f"per frame pair: match {t1_match:.1f}, LM {t1_lm:.1f})"},
         "sample": f"oracle (C, OpenMP {threads} threads): knn2 of {qs} queries x {len(pair.desc2)} train, "
                   f"DLT of {len(q)} matches, LM normals of {npts} points (pixelsRay {s.pixelsRay}); "
                   f"extrapolated to {nA} queries / {gpu_stats['matches']} matches / {gpu_stats['inliers']} points "
