@@ -523,16 +523,17 @@ struct Producer {
             waitCycles += clock64() - c0;
         }
         room--;
-        seq = rfl(seq);
         const int pos = seq & (kR - 1);
         double* row0 = &sh->ring[w][pos][0][0];
         row0[lane] = t0;
         row0[kRow + lane] = t1;
-        if (lane == 0) sh->chunkSlow[w][pos] = slowBits;
-        // every lane's ring stores are done before lane 0 publishes (lgkmcnt is per wave)
+        // the flags and the counter are written by every lane (same address, same value): no
+        // lane-0 branch, so seq stays a scalar
+        sh->chunkSlow[w][pos] = slowBits;
+        // every lane's ring stores are done before the counter is published (lgkmcnt is per wave)
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        if (lane == 0) lds_store_rel(&sh->produced[w], seq + 1);
         seq++;
+        lds_store_rel(&sh->produced[w], seq);
     }
 };
 
@@ -971,22 +972,25 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                     const bool moka0 = mdiv_ok(ajn0s);
                     const double ajn1s = SP.ajn1s, ya1 = 1. / ajn1s, tq0 = SP.tq0;
                     const bool moka1 = mdiv_ok(ajn1s);
-                    const gfloat* Dp = pc ? sl.DJ1 : sl.DJ0;
-                    const gfloat* Dq = pc ? sl.DJ0 : sl.DJ1;
                     auto run = [&](auto kindc) {
                         constexpr int KIND = decltype(kindc)::value;
                         struct Ld {
                             float p, q, f;
                         };
-                        auto load = [&](int k) {
+                        // o4: byte offset of the chunk's entries in the 4-byte slab arrays
+                        auto load = [&](unsigned o4) {
+                            const cProjConst* pcs = proj_consts(p.proj);
+                            const char* Dp = pc ? pcs->slabDJ1 : pcs->slabDJ0;
+                            const char* Dq = pc ? pcs->slabDJ0 : pcs->slabDJ1;
                             Ld L;
-                            const int e = k * kE + lane;
-                            L.p = Dp[e];
-                            L.q = Dq[e];
-                            L.f = sl.DF[e];  // QR2 needs F too: J = (w_j dI_j - F) / h_j
+                            L.p = *(const gfloat*)(Dp + o4);
+                            L.q = *(const gfloat*)(Dq + o4);
+                            L.f = *(const gfloat*)(pcs->slabDF + o4);  // J = (w_j dI_j - F) / h_j needs F
                             return L;
                         };
-                        auto chunk = [&](const Ld& L, int k) {
+                        // edge: the first or the last chunk (the diagonal entries 0 and 1, entries
+                        // past len); every other chunk skips those tests
+                        auto chunk = [&](const Ld& L, int k, bool edge) {
                             const int e = k * kE + lane;
                             const bool in = e < len;
                             // the stored columns: F = wF*dI_F, J_j = (w_j*dI_j - F)/h_j (as the JAC pass)
@@ -998,44 +1002,50 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                             if (KIND == Q_QR1) {
                                 // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); v*a_q, v*f
                                 double v = mdiv(ap, ajn0s, ya0, moka0);
-                                if (e == 0) v = v + 1.;
-                                t0 = in ? v * aq : 0.;
-                                t1 = in ? v * F : 0.;
+                                if (edge && e == 0) v = v + 1.;
+                                t0 = v * aq;
+                                t1 = v * F;
+                                if (edge && !in) t0 = t1 = 0.;
                             } else if (KIND == Q_QR2) {
                                 // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
                                 a = aq;
                                 if (t0f) a = a - tq * mdiv(ap, ajn0s, ya0, moka0);
-                                a = (in && e > 0) ? a : 0.;
-                                if (e == 1) aqs1 = a;
-                                t0 = enorm_term(a, agiant, slow);
+                                if (edge) {
+                                    a = (in && e > 0) ? a : 0.;
+                                    if (e == 1) aqs1 = a;
+                                }
+                                t0 = enorm_term2(a, agiant, slow);
                             } else {
                                 // lmdif qtf, j = 1: u_i * wa4_i
                                 const double v = t0f ? mdiv(ap, ajn0s, ya0, moka0) : 0.;
                                 double b = aq;
                                 if (t0f) b = b - tq * v;
                                 double u = t1f ? mdiv(b, ajn1s, ya1, moka1) : b;
-                                if (t1f && e == 1) u = u + 1.;
+                                if (edge && t1f && e == 1) u = u + 1.;
                                 double wa = F;
                                 if (q0f) wa = wa + v * tq0;
-                                t0 = (in && e > 0) ? u * wa : 0.;
+                                t0 = u * wa;
+                                if (edge && !(in && e > 0)) t0 = 0.;
                             }
                             const bool sl0 = __ballot(slow) != 0;
                             prod.put(sl0 ? a : t0, t1, sl0 ? 1 : 0);
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry
                         constexpr int kQD = 8;
+                        unsigned o4 = (slot8 >> 1) + lane * 4u;
                         Ld buf[kQD];
 #pragma unroll
-                        for (int j = 0; j < kQD; j++) buf[j] = load(j);
+                        for (int j = 0; j < kQD; j++) buf[j] = load(o4 + j * 256u);
                         for (int k = 0; k < nCh; k += kQD) {
 #pragma unroll
                             for (int j = 0; j < kQD; j++) {
                                 if (k + j < nCh) {
-                                    const Ld nx = load(k + j + kQD);
-                                    chunk(buf[j], k + j);
+                                    const Ld nx = load(o4 + (j + kQD) * 256u);
+                                    chunk(buf[j], k + j, k + j == 0 || k + j == nCh - 1);
                                     buf[j] = nx;
                                 }
                             }
+                            o4 += kQD * 256u;
                         }
                     };
                     if (pass == Q_QR1)
