@@ -28,27 +28,37 @@ __device__ __forceinline__ double mdiv(double a, double d, double y, bool mok) {
 __device__ __forceinline__ bool mdiv_ok(double d) { return fabs(d) > 1e-200 && fabs(d) < 1e200; }
 
 // z ? 1/z : 1 (cvProjectPoints2).  For 2^-700 <= |z| <= 2^700 the hardware sequence
-// scales nothing (exponent gap < 768, 1/z normal) and fixes nothing up.
+// scales nothing (exponent gap < 768, 1/z normal) and fixes nothing up.  recip_z_lo
+// tests only the lower bound: for plane points inside the bounding box |z| is far below
+// 2^700, and the other entries do not use the value.
+__device__ __forceinline__ double recip_fast(double z) {
+    double r = __builtin_amdgcn_rcp(z);
+    double e = __builtin_fma(-z, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-z, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double rem = __builtin_fma(-z, r, 1.0);
+    return __builtin_fma(rem, r, r);
+}
 __device__ __forceinline__ double recip_z(double z) {
     const double az = fabs(z);
-    if (az >= 0x1p-700 && az <= 0x1p700) {
-        double r = __builtin_amdgcn_rcp(z);
-        double e = __builtin_fma(-z, r, 1.0);
-        r = __builtin_fma(r, e, r);
-        e = __builtin_fma(-z, r, 1.0);
-        r = __builtin_fma(r, e, r);
-        const double rem = __builtin_fma(-z, r, 1.0);
-        return __builtin_fma(rem, r, r);
-    }
+    if (az >= 0x1p-700 && az <= 0x1p700) return recip_fast(z);
+    return z ? 1. / z : 1.;
+}
+__device__ __forceinline__ double recip_z_lo(double z) {
+    if (fabs(z) >= 0x1p-700) return recip_fast(z);
     return z ? 1. / z : 1.;
 }
 
-// mm / nn with a pass-uniform numerator: mok = 2^-600 <= |mm| <= 2^60 (div_nn_ok), and
-// 2^-600 <= |nn| <= 2^60 per lane -- exponent gap < 768, quotient and remainder normal.
+// mm / nn with a numerator in [2^-600, 2^60] (mok = div_nn_ok(mm), pass-uniform) and
+// |nn| <= 2^60 (a unit normal times a ray (x, y, 1) of bounded x, y).  The sequence
+// scales nothing unless |nn| < 2^-600, and the exponent gap reaches 768, or nn is
+// denormal, only when |mm / nn| > 2^400.  So the result equals mm / nn whenever
+// |mm / nn| < 2^100, and is NaN or at least 2^100 in magnitude otherwise: the ray-plane
+// point falls outside the bounding box (|P| < 4) exactly when it does for the IEEE quotient.
 __device__ __forceinline__ bool div_nn_ok(double mm) { return fabs(mm) >= 0x1p-600 && fabs(mm) <= 0x1p60; }
 __device__ __forceinline__ double div_nn(double mm, double nn, bool mok) {
-    const double an = fabs(nn);
-    if (mok && an >= 0x1p-600 && an <= 0x1p60) {
+    if (mok) {
         double r = __builtin_amdgcn_rcp(nn);
         double e = __builtin_fma(-nn, r, 1.0);
         r = __builtin_fma(r, e, r);

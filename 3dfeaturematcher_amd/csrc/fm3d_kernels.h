@@ -59,8 +59,9 @@ struct LMParams {
 
 constexpr int kLMRunning = 0x100;  // status of a point still in flight
 
-// wave-per-point LM kernel (fm3d_lm2.hip): kLM2Slots term waves + 1 chain wave
-constexpr int kLM2Slots = 7;
+// wave-per-point LM kernel (fm3d_lm2.hip): kLM2Slots term waves + 1 chain wave, one
+// 1024-thread workgroup per CU (4 waves per SIMD; 141 KB of LDS)
+constexpr int kLM2Slots = 15;
 constexpr int kLM2Ring = 8;  // chunks of 64 entries in flight per slot
 constexpr int kLM2Threads = 64 * (kLM2Slots + 1);
 __global__ void lm2_kernel(LMParams p);

@@ -614,7 +614,7 @@ __device__ __forceinline__ Geo2 geometry2(const LMParams& p, double ux, double u
     r.inbox = fabs(P0) < cm && fabs(P1) < cm && P2 > 0. && P2 < cm;
     double x = pc->R[0] * P0 + pc->R[1] * P1 + pc->R[2] * P2 + pc->t[0];
     double y = pc->R[3] * P0 + pc->R[4] * P1 + pc->R[5] * P2 + pc->t[1];
-    const double z = recip_z(pc->R[6] * P0 + pc->R[7] * P1 + pc->R[8] * P2 + pc->t[2]);
+    const double z = recip_z_lo(pc->R[6] * P0 + pc->R[7] * P1 + pc->R[8] * P2 + pc->t[2]);
     x *= z;
     y *= z;
     const double r2 = x * x + y * y;
@@ -656,10 +656,11 @@ __device__ __forceinline__ float bilinear_w(unsigned lo, unsigned hi, float x, f
 }
 
 // enorm term with the slow-path flag: x^2 is the term whenever no lane of the chunk needs
-// MINPACK's small/large component handling (x = 0 adds +0, as enorm does)
+// MINPACK's small/large component handling (x = 0 adds +0, as enorm does).  slow: whether
+// any lane of the wave does (a wave-uniform ballot of the lane tests).
 __device__ __forceinline__ double enorm_term2(double x, double agiant, bool& slow) {
     const double xa = fabs(x);
-    slow = !(xa < agiant) || (xa <= 3.834e-20 && xa != 0.);
+    slow = __ballot(!(xa < agiant) || (xa <= 3.834e-20 && xa != 0.)) != 0;
     return x * x;
 }
 
@@ -735,7 +736,8 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
 
 }  // namespace
 
-__global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel(LMParams p) {
+// 4 waves per SIMD: one workgroup of 16 waves per CU (128 VGPRs)
+__global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     Shared& sh = g_sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long tStart = wall_clock64(), cyStart = clock64();
@@ -848,7 +850,8 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                     d.kind[0] = (pass == Q_QR1 || pass == Q_QR3) ? S_DOT : S_ENORM;
                     d.kind[1] = pass == Q_QR1 ? S_DOT : ((pass == Q_EVAL && nev == 2) ? S_ENORM : S_NONE);
                 }
-                int fail0 = 0x7fffffff, fail1 = 0x7fffffff, ph30 = 0, ph31 = 0;
+                int fail0 = 0x7fffffff, fail1 = 0x7fffffff;
+                unsigned long long ph30 = 0, ph31 = 0;  // image-2 failures seen (lane masks)
                 double aqs1 = 0.;
                 if (pass == Q_EVAL) {
                     const double n00 = SP.n0[0], n10 = SP.n1[0], n20 = SP.n2[0], mm0 = SP.mm[0], w0 = SP.w[0];
@@ -865,8 +868,6 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                     const bool mmok0 = div_nn_ok(mm0);
                     const bool mmok1 = div_nn_ok(mm1);
                     const gu8* img2b = (const gu8*)rfl_ptr(img2);
-                    // NEV evaluations per entry (2: both forward-difference columns); JAC: the
-                    // values are Jacobian columns (r - fvec)/h_j, else the residual fvec itself
                     auto run = [&](auto nevc, auto jacc) {
                         constexpr int NEV = decltype(nevc)::value;
                         constexpr bool JAC = decltype(jacc)::value;
@@ -906,7 +907,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                                     const int cd = plane_code(L.ux, L.uy, n00, n10, n20, mm0);
                                     fail0 = (k * kE + l) * 4 + __shfl(cd, l);
                                 }
-                                ph30 |= __ballot(in && g0.inbox && !g0.good) != 0;
+                                ph30 |= __ballot(in && g0.inbox && !g0.good);
                                 if (NEV == 2) {
                                     const unsigned long long b1 = __ballot(in && !g1.inbox);
                                     if (b1 && fail1 == 0x7fffffff) {
@@ -914,7 +915,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                                         const int cd = plane_code(L.ux, L.uy, n01, n11, n21, mm1);
                                         fail1 = (k * kE + l) * 4 + __shfl(cd, l);
                                     }
-                                    ph31 |= __ballot(in && g1.inbox && !g1.good) != 0;
+                                    ph31 |= __ballot(in && g1.inbox && !g1.good);
                                 }
                             }
                             // evaluateNormal :145-148 (fvec), fdjac2 forward differences (JAC)
@@ -937,8 +938,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                                 *(gfloat*)(proj_consts(p.proj)->slabDJ1 + o4) = dI1;
                                 t1 = enorm_term2(v1, agiant, slow1);
                             }
-                            const bool s0 = __ballot(slow0) != 0, s1 = __ballot(slow1) != 0;
-                            prod.put(s0 ? v0 : t0, s1 ? v1 : t1, (s0 ? 1 : 0) | (s1 ? 2 : 0));
+                            prod.put(slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
                         };
                         // two chunks of slab loads in flight ahead of the one being computed
                         unsigned o8 = slot8 + lane * 8u, o4 = o8 >> 1;
@@ -1027,8 +1027,7 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                                 t0 = u * wa;
                                 if (edge && !(in && e > 0)) t0 = 0.;
                             }
-                            const bool sl0 = __ballot(slow) != 0;
-                            prod.put(sl0 ? a : t0, t1, sl0 ? 1 : 0);
+                            prod.put(slow ? a : t0, t1, slow ? 1 : 0);
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry
                         constexpr int kQD = 8;
@@ -1068,8 +1067,8 @@ __global__ __launch_bounds__(kLM2Threads, 2 * kLM2Threads / 256) void lm2_kernel
                     OUT.nrm[1] = OUT.sum[1] = sh.result[w][1];
                     OUT.fail[0] = fail0;
                     OUT.fail[1] = fail1;
-                    OUT.ph3[0] = ph30;
-                    OUT.ph3[1] = ph31;
+                    OUT.ph3[0] = ph30 != 0;
+                    OUT.ph3[1] = ph31 != 0;
                     OUT.aqs1 = aqs1;
                 }
             }

@@ -217,6 +217,8 @@ def lm_profile(lm):
         "chain_busy": lm["cycles_chain"] / tot if tot else None,    # chain wave adding / group lifetime
         "control_over_terms": lm["cycles_control"] / max(lm["cycles_terms"], 1),  # lmdif bookkeeping
         "wait_over_terms": lm["cycles_wait"] / max(lm["cycles_terms"], 1),        # term waves waiting on the chain
+        # mean number of term waves inside a pass over the lifetime of a workgroup's first wave
+        "busy_slots_per_group": lm["cycles_terms"] / tot if tot else None,
         "group_life_mean_over_max": lm["wall_ticks_sum"] / max(lm["groups"], 1) / max(lm["wall_ticks_max"], 1),
         "clock_ghz": lm["cycles_total"] / max(lm["wall_ticks_sum"], 1) * lm["wall_clock_khz"] * 1e-6,
         "kcycles_per_pass_by_class": {n: round(cy / max(c, 1) / 1e3, 1) for n, c, cy in

@@ -103,7 +103,7 @@ typedef struct fm3d_lm_stats {
     int64_t pixel_evaluations; /* sum over evaluations of m_dat */
     int64_t drops[8];          /* points per FM3D_ST_* code */
     double kernel_ms;          /* LM kernel time (HIP events on the context stream) */
-    int64_t groups;            /* LM workgroups launched (7 points in flight each, one per term wave) */
+    int64_t groups;            /* LM workgroups launched (15 points in flight each, one per term wave) */
     int64_t passes;            /* summed neighbourhood passes (residual, Jacobian, Householder), all points */
     /* core clock cycles, summed over workgroups or waves: term waves inside passes
        (including waits), the chain wave busy adding, term waves in the lmdif bookkeeping,

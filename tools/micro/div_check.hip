@@ -35,25 +35,41 @@ __device__ inline bool same(double a, double b) {
 }
 
 __device__ double g_fail[64][3];  // first failing mdiv operands: a, d, fast result
+__device__ double g_fail2[8][3];  // first failing div_nn operands: mm, nn, fast result
+__device__ unsigned long long bad_[2];
 
 __global__ void check(uint64_t seed, int iters, unsigned long long* bad, unsigned long long* fast) {
     const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     unsigned long long nb[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
     for (int i = 0; i < iters; i++) {
         const uint64_t r0 = mix(seed ^ (t * 0x100000001B3ull + i)), r1 = mix(r0), r2 = mix(r1);
-        // recip_z
+        // recip_z; recip_z_lo where |z| <= 2^700
         {
-            const double z = draw(r0, -760, 760);
+            const double z = draw(r0, -1100, 760);
             const double ref = z ? 1. / z : 1.;
             nb[0] += !same(recip_z(z), ref);
+            if (!(fabs(z) > 0x1p700)) nb[0] += !same(recip_z_lo(z), ref);
             nf[0] += fabs(z) >= 0x1p-700 && fabs(z) <= 0x1p700;
         }
-        // div_nn (the numerator is pass-uniform in the kernel; any value here)
+        // div_nn (the numerator is pass-uniform in the kernel; any value here; |nn| <= 2^60):
+        // the IEEE quotient where that is below 2^100, NaN or >= 2^100 where it is not
         {
-            const double mm = draw(r1, -640, 80), nn = draw(r2, -640, 80);
+            const double mm = draw(r1, -640, 80);
+            double nn = draw(r2, -1100, 60);
+            if (__builtin_isinf(nn)) nn = 0x1p60;  // outside the precondition
             const bool ok = div_nn_ok(mm);
-            nb[1] += !same(div_nn(mm, nn, ok), mm / nn);
-            nf[1] += ok && fabs(nn) >= 0x1p-600 && fabs(nn) <= 0x1p60;
+            const double f = div_nn(mm, nn, ok), x = mm / nn;
+            const bool bad = fabs(x) < 0x1p100 ? !same(f, x) : !(f != f || !(fabs(f) < 0x1p100));
+            nb[1] += bad;
+            nf[1] += ok;
+            if (bad) {
+                const unsigned long long slot = atomicAdd(&bad_[1], 1ull);
+                if (slot < 8) {
+                    g_fail2[slot][0] = mm;
+                    g_fail2[slot][1] = nn;
+                    g_fail2[slot][2] = f;
+                }
+            }
         }
         // mdiv on its operand domain: |a| = 0 or in [2^-200, 2^370], any d
         {
@@ -95,6 +111,11 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(hf, fast, 24, hipMemcpyDeviceToHost);
     const char* names[3] = {"recip_z", "div_nn", "mdiv"};
     const unsigned long long n = (unsigned long long)blocks * threads * iters;
+    double hfail2[8][3];
+    (void)hipMemcpyFromSymbol(hfail2, HIP_SYMBOL(g_fail2), sizeof(hfail2));
+    for (int i = 0; i < (hb[1] < 8 ? (int)hb[1] : 8); i++)
+        printf("div_nn mismatch: mm=%a nn=%a fast=%a ieee=%a\n", hfail2[i][0], hfail2[i][1], hfail2[i][2],
+               hfail2[i][0] / hfail2[i][1]);
     double hfail[64][3];
     (void)hipMemcpyFromSymbol(hfail, HIP_SYMBOL(g_fail), sizeof(hfail));
     for (int i = 0; i < (hb[2] < 8 ? (int)hb[2] : 8); i++)
