@@ -433,12 +433,14 @@ struct Ctl2 {
 };
 
 struct Shared {
-    double ring[kW][kR][2][kRow];  // chunk terms [slot][ring position][sum][entry]
-    int chunkSlow[kW][kR];         // bit k: sum k of that chunk holds raw values (enorm slow path)
+    // chunk terms [slot][ring position][sum][entry]; entry kE holds the chunk's slow flag for
+    // that sum (nonzero: raw values for MINPACK's full enorm instead of squares)
+    double ring[kW][kR][2][kRow];
     int produced[kW];              // chunks produced, per slot (monotonic)
     int consumed[kW][2];           // chunks consumed, per chain lane (monotonic)
     int resultId[kW][2];           // id of the last pass whose result is published
     double result[kW][2];
+    Enorm chainEn[64];  // MINPACK enorm state of each chain lane (s2 lives in its register)
     int done[kW];
     PassDesc pd[kW];
     SlotP2 sp[kW];
@@ -459,36 +461,45 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// sum += t[0..64) in index order: 64 dependent adds, fed by ds_read_b128 into two
-// alternating register sets of 16 values (no register copies inside the chain)
-__device__ __forceinline__ double chain_sum64(double sum, const double* t) {
-    const double2* t2 = reinterpret_cast<const double2*>(t);
-    double2 a[8], b[8];
+// sum += row[0..64) in index order: 64 dependent adds, fed by ds_read_b128 into four
+// register sets of 8 values in rotation, so three sets (24 values) are in flight while one is
+// added.  Compiler barriers keep the reads in that order.  slow: the row's slow flag (entry
+// kE), read with the data and tested by the caller after the sum.
+__device__ __forceinline__ double chain_sum64(double sum, const double* row, double& slow) {
+    const double2* R = reinterpret_cast<const double2*>(row);
+    double2 v0[4], v1[4], v2[4], v3[4];
+    auto ld = [&](double2 (&v)[4], int k) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) a[i] = t2[i];
+        for (int i = 0; i < 4; i++) v[i] = R[4 * k + i];
+        __asm__ __volatile__("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto add = [&](const double2 (&v)[4]) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) b[i] = t2[8 + i];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            sum += a[i].x;
-            sum += a[i].y;
+        for (int i = 0; i < 4; i++) {
+            sum += v[i].x;
+            sum += v[i].y;
         }
-        if (h == 0) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) a[i] = t2[16 + i];
-        }
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            sum += b[i].x;
-            sum += b[i].y;
-        }
-        if (h == 0) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) b[i] = t2[24 + i];
-        }
-    }
+        __asm__ __volatile__("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    ld(v0, 0);
+    ld(v1, 1);
+    ld(v2, 2);
+    slow = row[kE];
+    ld(v3, 3);
+    add(v0);
+    ld(v0, 4);
+    add(v1);
+    ld(v1, 5);
+    add(v2);
+    ld(v2, 6);
+    add(v3);
+    ld(v3, 7);
+    add(v0);
+    add(v1);
+    add(v2);
+    add(v3);
     return sum;
 }
 
@@ -512,15 +523,17 @@ struct Producer {
         // seq and room are wave-uniform: kept in SGPRs (readfirstlane on every LDS read)
         if (room == 0) {
             // ring space: both chain lanes of the slot have consumed chunk seq - kR.  The
-            // counters are read only when the space seen last time is used up.
-            const long long c0 = clock64();
-            for (;;) {
-                const int c = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])));
-                room = c + kR - seq;
-                if (room > 0) break;
-                __builtin_amdgcn_s_sleep(1);
+            // counters are read only when the space seen last time is used up, and the
+            // clock only when that space is still zero.
+            room = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1]))) + kR - seq;
+            if (room <= 0) {
+                const long long c0 = clock64();
+                do {
+                    __builtin_amdgcn_s_sleep(1);
+                    room = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1]))) + kR - seq;
+                } while (room <= 0);
+                waitCycles += clock64() - c0;
             }
-            waitCycles += clock64() - c0;
         }
         room--;
         const int pos = seq & (kR - 1);
@@ -529,7 +542,8 @@ struct Producer {
         row0[kRow + lane] = t1;
         // the flags and the counter are written by every lane (same address, same value): no
         // lane-0 branch, so seq stays a scalar
-        sh->chunkSlow[w][pos] = slowBits;
+        row0[kE] = (slowBits & 1) ? 1. : 0.;
+        row0[kRow + kE] = (slowBits & 2) ? 1. : 0.;
         // every lane's ring stores are done before the counter is published (lgkmcnt is per wave)
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         seq++;
@@ -667,7 +681,23 @@ __device__ __forceinline__ double enorm_term2(double x, double agiant, bool& slo
 // ======================= chain wave =======================
 // Lane 2s+k adds sum k of slot s's current pass, chunk by chunk in entry order.  A
 // function of its own (not inlined) so that its registers are allocated apart from the
-// term waves' code.
+// term waves' code.  MINPACK's enorm state beyond the running s2 lives in LDS
+// (g_sh.chainEn): only chunks with raw values (chain_slow) and the pass result touch it.
+
+// a chunk of raw values again from acc0 (the running s2 before it), with MINPACK's full enorm
+__device__ __forceinline__ double chain_slow(int lane, double acc0, const double* row) {
+    Enorm en = g_sh.chainEn[lane];
+    en.s2 = acc0;
+    for (int i = 0; i < kE; i++) en.add(row[i]);
+    g_sh.chainEn[lane] = en;
+    return en.s2;
+}
+__device__ __forceinline__ double chain_finish(int lane, double acc) {
+    Enorm en = g_sh.chainEn[lane];
+    en.s2 = acc;
+    return en.finish();
+}
+
 __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, long long maxTicks,
                                         unsigned long long* statBusy) {
     // the chain's dependent adds bound a pass's last chunk: let it issue first
@@ -677,10 +707,10 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
     const int ss_ = alive ? s : 0;
     int cur = 0, rem = 0, kind = S_NONE, pid = 0;
     bool inPass = false;
-    Enorm en;  // MINPACK enorm state; s2 lives in acc on the fast path
-    en.init(1);
     double acc = 0.;  // running sum: enorm s2 (S_ENORM) or the dot product (S_DOT)
-    unsigned long long busy = 0;
+    // busy time: one clock read per busy round (the span to the next round's read)
+    unsigned long long busy = 0, tLast = 0;
+    bool wasBusy = false;
     for (;;) {
         if ((long long)(wall_clock64() - tStart) > maxTicks) break;
         if (!__any(alive)) break;
@@ -691,41 +721,44 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
             rem = d.nChunks;
             kind = d.kind[which];
             pid = d.id;
+            Enorm& en = g_sh.chainEn[lane];
             en.init(1);
             en.agiant = d.agiant;
             acc = 0.;
             inPass = true;
         }
         if (__any(have)) {
-            const unsigned long long c0 = clock64();
+            const unsigned long long t = clock64();
+            if (wasBusy) busy += t - tLast;
+            tLast = t;
+            wasBusy = true;
             // up to two chunks per lane per round, never past the pass's last chunk; every
             // lane runs the same add chain (S_NONE lanes sum zeros they never publish)
             const int nb = have ? min(min(pr - cur, rem), 2) : 0;
 #pragma nounroll
             for (int b = 0; b < 2; b++) {
                 if (b < nb) {
-                    const int pos = cur % kR;
-                    const double* row = &g_sh.ring[ss_][pos][which][0];
-                    if (kind == S_ENORM && ((g_sh.chunkSlow[ss_][pos] >> which) & 1)) {
-                        en.s2 = acc;
-                        for (int i = 0; i < kE; i++) en.add(row[i]);
-                        acc = en.s2;
-                    } else {
-                        acc = chain_sum64(acc, row);
-                    }
+                    const double* row = &g_sh.ring[ss_][cur & (kR - 1)][which][0];
+                    double slow;
+                    const double acc0 = acc;
+                    acc = chain_sum64(acc, row, slow);
+                    // a chunk of raw values (rare): again, with MINPACK's full enorm
+                    if (kind == S_ENORM && slow != 0.) acc = chain_slow(lane, acc0, row);
                     cur++;
                     rem--;
                 }
             }
             if (nb > 0) lds_store_rel(&g_sh.consumed[ss_][which], cur);
             if (have && rem == 0) {
-                en.s2 = acc;
-                g_sh.result[ss_][which] = kind == S_ENORM ? en.finish() : acc;
+                g_sh.result[ss_][which] = kind == S_ENORM ? chain_finish(lane, acc) : acc;
                 lds_store_rel(&g_sh.resultId[ss_][which], pid);
                 inPass = false;
             }
-            busy += clock64() - c0;
         } else {
+            if (wasBusy) {
+                busy += clock64() - tLast;
+                wasBusy = false;
+            }
             if (alive && !inPass && lds_load_acq(&g_sh.done[ss_]) && lds_load_acq(&g_sh.produced[ss_]) == cur)
                 alive = false;
             __builtin_amdgcn_s_sleep(1);
