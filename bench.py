@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", type=str, default="")
-    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "r01_pmc_c4_lm2.json"),
+    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "r01_pmc_c4_final.json"),
                     help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()
 
@@ -265,9 +265,12 @@ def cpu_baseline(pair, s, gpu_stats, args):
     # LM normals: sample of points
     fm3d = importlib.import_module("3dfeaturematcher_amd")
     R2, t2 = fm3d.camera2_from_g12(pair.g12)
-    npts = min(len(pts), max(threads, 16))
+    # a seeded random subset (per-point LM cost varies by orders of magnitude), 16 points per
+    # thread so the dynamic schedule balances
+    sub = np.random.default_rng(7).permutation(len(pts))
+    npts = min(len(pts), 16 * threads)
     t = time.perf_counter()
-    r = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts[:npts], s.pixelsRay,
+    r = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts[sub[:npts]], s.pixelsRay,
                              mode=orc.STRICT, nthreads=threads)
     dt = time.perf_counter() - t
     t_lm = dt / npts * gpu_stats["inliers"]
@@ -277,9 +280,10 @@ def cpu_baseline(pair, s, gpu_stats, args):
     orc.knn2(pair.desc1[:256], pair.desc2, orc.U8, 1)
     t1_match = (time.perf_counter() - t) / 256 * nA
     t = time.perf_counter()
-    orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts[:2], s.pixelsRay,
+    n1 = min(len(pts), 16)
+    orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts[sub[:n1]], s.pixelsRay,
                          mode=orc.STRICT, nthreads=1)
-    t1_lm = (time.perf_counter() - t) / 2 * gpu_stats["inliers"]
+    t1_lm = (time.perf_counter() - t) / n1 * gpu_stats["inliers"]
     total1 = t1_match + t_tri + t1_lm
     return {
         "value": gpu_stats["kept"] / total,
@@ -288,10 +292,10 @@ def cpu_baseline(pair, s, gpu_stats, args):
         "kind": "port",
         "cpu_model": cpu_model(),
         "single_thread": {"value": gpu_stats["kept"] / total1, "unit": "keypoints/s", "cores": 1,
-                          "sample": f"knn2 of 256 queries, LM normals of 2 points, 1 thread (est. {total1:.0f} s "
+                          "sample": f"knn2 of 256 queries, LM normals of {n1} points, 1 thread (est. {total1:.0f} s "
                                     f"per frame pair: match {t1_match:.1f}, LM {t1_lm:.1f})"},
         "sample": f"oracle (C, OpenMP {threads} threads): knn2 of {qs} queries x {len(pair.desc2)} train, "
-                  f"DLT of {len(q)} matches, LM normals of {npts} points (pixelsRay {s.pixelsRay}); "
+                  f"DLT of {len(q)} matches, LM normals of {npts} random points (pixelsRay {s.pixelsRay}); "
                   f"extrapolated to {nA} queries / {gpu_stats['matches']} matches / {gpu_stats['inliers']} points "
                   f"(est. {total:.1f} s per frame pair: match {t_match:.1f}, DLT {t_tri:.3f}, LM {t_lm:.1f})",
     }

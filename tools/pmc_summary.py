@@ -45,6 +45,11 @@ def main():
             simd_cycles = 1024 * dur * 1e-9 * (agg["SQ_BUSY_CYCLES"] / 32 / (dur * 1e-9))
             res["valu_busy_per_simd"] = 4 * agg["SQ_ACTIVE_INST_VALU"] / simd_cycles
             res["busy_clock_ghz"] = agg["SQ_BUSY_CYCLES"] / 32 / dur
+    if "SQ_LDS_IDX_ACTIVE" in agg:
+        # LDS: extra cycles from bank conflicts per LDS-array cycle; instructions per wave-cycle
+        res["lds_bank_conflict_frac"] = agg.get("SQ_LDS_BANK_CONFLICT", 0.) / max(agg["SQ_LDS_IDX_ACTIVE"], 1)
+        res["lds_addr_conflict_frac"] = agg.get("SQ_LDS_ADDR_CONFLICT", 0.) / max(agg["SQ_LDS_IDX_ACTIVE"], 1)
+        res["lds_unaligned_stall_frac"] = agg.get("SQ_LDS_UNALIGNED_STALL", 0.) / max(agg["SQ_LDS_IDX_ACTIVE"], 1)
     res["note"] = ("FETCH_SIZE/WRITE_SIZE in KiB; gfx950 FETCH_SIZE reads half the bytes of wide streaming loads "
                    "(doubled here); each counter group measured in its own rocprofv3 --pmc pass")
     print(json.dumps(res, indent=1))
