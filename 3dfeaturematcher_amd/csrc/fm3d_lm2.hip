@@ -973,20 +973,69 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             }
                             prod.put(slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
                         };
-                        // two chunks of slab loads in flight ahead of the one being computed
                         unsigned o8 = slot8 + lane * 8u, o4 = o8 >> 1;
-                        Ld A = load(o8, o4), B = load(o8 + 512u, o4 + 256u);
-                        for (int k = 0; k < nCh; k += 2) {
-                            const Ld C = load(o8 + 1024u, o4 + 512u);
-                            chunk(A, k, o4);
-                            A = C;
-                            if (k + 1 < nCh) {
-                                const Ld D = load(o8 + 1536u, o4 + 768u);
-                                chunk(B, k + 1, o4 + 256u);
-                                B = D;
+                        if (NEV == 2) {
+                            // two chunks of slab loads in flight ahead of the one being computed
+                            Ld A = load(o8, o4), B = load(o8 + 512u, o4 + 256u);
+                            for (int k = 0; k < nCh; k += 2) {
+                                const Ld C = load(o8 + 1024u, o4 + 512u);
+                                chunk(A, k, o4);
+                                A = C;
+                                if (k + 1 < nCh) {
+                                    const Ld D = load(o8 + 1536u, o4 + 768u);
+                                    chunk(B, k + 1, o4 + 256u);
+                                    B = D;
+                                }
+                                o8 += 1024u;
+                                o4 += 512u;
                             }
-                            o8 += 1024u;
-                            o4 += 512u;
+                        } else {
+                            // one evaluation per entry: two chunks side by side, so the two
+                            // independent geometries interleave (as the two columns of a Jacobian
+                            // pass do); the slab loads of the next pair are issued once the pair's
+                            // geometry has consumed its own
+                            Ld A = load(o8, o4), B = load(o8 + 512u, o4 + 256u);
+                            for (int k = 0; k < nCh; k += 2) {
+                                const bool two = k + 1 < nCh;  // wave-uniform
+                                const bool inA = k * kE + lane < len, inB = (k + 1) * kE + lane < len;
+                                const Geo2 gA = geometry2(p, A.ux, A.uy, n00, n10, n20, mm0, mmok0, scale, xmax, ymax, lw, cm);
+                                // past the last chunk B holds slab padding: its entries are not
+                                // `in`, its gathers read the image's first bytes, nothing is stored
+                                const Geo2 gB = geometry2(p, B.ux, B.uy, n00, n10, n20, mm0, mmok0, scale, xmax, ymax, lw, cm);
+                                const uint2 a = gather(gA.off), b = gather(gB.off);
+                                const float i1A = A.i1, i1B = B.i1;
+                                const double dFA = A.dF, dFB = B.dF;
+                                // failures in entry order: chunk k before chunk k + 1
+                                const unsigned long long bA = __ballot(inA && !gA.inbox);
+                                const unsigned long long bB = __ballot(inB && !gB.inbox);
+                                if ((bA | bB) && fail0 == 0x7fffffff) {
+                                    const bool first = bA != 0;
+                                    const int l = __ffsll((long long)(first ? bA : bB)) - 1;
+                                    const int cd = first ? plane_code(A.ux, A.uy, n00, n10, n20, mm0)
+                                                         : plane_code(B.ux, B.uy, n00, n10, n20, mm0);
+                                    fail0 = ((first ? k : k + 1) * kE + l) * 4 + __shfl(cd, l);
+                                }
+                                ph30 |= __ballot(inA && gA.inbox && !gA.good) | __ballot(inB && gB.inbox && !gB.good);
+                                A = load(o8 + 1024u, o4 + 512u);
+                                B = load(o8 + 1536u, o4 + 768u);
+                                auto back1 = [&](const Geo2& g, uint2 w, float i1, double dF, bool in, unsigned oo) {
+                                    const float dI = i1 - bilinear_w(w.x, w.y, g.fx, g.fy);
+                                    const double r = w0 * (double)dI;
+                                    double v = JAC ? mdiv(r - wF * dF, h0, y0, mok0) : r;
+                                    v = (in && i1ok && g.good) ? v : 0.;
+                                    {
+                                        const cProjConst* pc = proj_consts(p.proj);
+                                        *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + oo) = dI;
+                                    }
+                                    bool slow;
+                                    const double t = enorm_term2(v, agiant, slow);
+                                    prod.put(slow ? v : t, 0., slow ? 1 : 0);
+                                };
+                                back1(gA, a, i1A, dFA, inA, o4);
+                                if (two) back1(gB, b, i1B, dFB, inB, o4 + 256u);
+                                o8 += 1024u;
+                                o4 += 512u;
+                            }
                         }
                     };
                     if (nev == 2)
