@@ -17,13 +17,18 @@ namespace fm3d {
 // for the operands the LM passes divide (|a| is 0 or above 1e-60: products of float
 // intensity differences and O(1) weights).  a = -0 with d > 0 gives +0 (IEEE: -0); the
 // passes never divide -0: their numerators are differences, +0 when the operands are equal.
+// The fast sequence runs on every lane; the division operator only on the lanes outside the
+// guard, inside a branch taken when any lane of the wave is (rare): no exec-mask juggling on
+// the common path.
 __device__ __forceinline__ double mdiv(double a, double d, double y, bool mok) {
-    if (mok && fabs(a) < 1e100) {
-        const double q0 = a * y;
-        const double r = __builtin_fma(-d, q0, a);
-        return __builtin_fma(r, y, q0);
+    const double q0 = a * y;
+    const double r = __builtin_fma(-d, q0, a);
+    double q = __builtin_fma(r, y, q0);
+    const bool ok = mok && fabs(a) < 1e100;
+    if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+        if (!ok) q = a / d;
     }
-    return a / d;
+    return q;
 }
 __device__ __forceinline__ bool mdiv_ok(double d) { return fabs(d) > 1e-200 && fabs(d) < 1e200; }
 
@@ -46,8 +51,12 @@ __device__ __forceinline__ double recip_z(double z) {
     return z ? 1. / z : 1.;
 }
 __device__ __forceinline__ double recip_z_lo(double z) {
-    if (fabs(z) >= 0x1p-700) return recip_fast(z);
-    return z ? 1. / z : 1.;
+    double q = recip_fast(z);
+    const bool ok = fabs(z) >= 0x1p-700;
+    if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+        if (!ok) q = z ? 1. / z : 1.;
+    }
+    return q;
 }
 
 // mm / nn with a numerator in [2^-600, 2^60] (mok = div_nn_ok(mm), pass-uniform) and
