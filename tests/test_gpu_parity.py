@@ -249,6 +249,31 @@ def test_normals_reference_config_ray64(fm3d, orc, pair):
     assert np.array_equal(normals, ref["normals"][ok])
 
 
+def test_normals_ray128_largest_neighbourhood(fm3d, orc, pair):
+    # pixelsRay 128: 51,445-pixel residuals (4x the reference's), the largest slab rows
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    P = pts[:12]
+    kept, normals, st, info, nfev, ref, _ = _normals_case(fm3d, orc, pair, P, 128)
+    assert np.array_equal(st, ref["status"])
+    assert np.array_equal(nfev[:, :4], ref["nfev"][:, :4])
+    ok = ref["status"] == 0
+    assert np.array_equal(normals, ref["normals"][ok])
+
+
+@pytest.mark.parametrize("levels", [0, 1])
+def test_normals_pyramid_depths(fm3d, orc, pair, levels):
+    # no pyramid (level 0 only) and one pyramid level
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    kept, normals, st, info, nfev, ref, _ = _normals_case(fm3d, orc, pair, pts[:40], 16, levels=levels)
+    assert np.array_equal(st, ref["status"])
+    assert np.array_equal(nfev[:, :levels + 1], ref["nfev"][:, :levels + 1])
+    ok = ref["status"] == 0
+    assert np.array_equal(normals, ref["normals"][ok])
+    assert ok.sum() > 5
+
+
 def test_normals_vga_bounds(fm3d, orc, pair):
     # image bound = the VGA size instead of the reference's literal 1024x768
     q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
