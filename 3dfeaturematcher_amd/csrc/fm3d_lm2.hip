@@ -28,9 +28,12 @@
 //     dI they are computed from (4 bytes instead of 8): fvec = w*(double)dI and
 //     J = (w_j*(double)dI_j - fvec)/h_j are recomputed from them with the same IEEE
 //     operations, hence the same bits;
-//   * divisions by a pass-uniform denominator (h_j, the Householder norms) use the
-//     correctly rounded reciprocal and one Markstein correction (two FMAs), which is
-//     exactly IEEE division in the guarded range (mdiv below).
+//   * divisions are the hardware sequence without its scaling / fix-up wrappers where the
+//     operands need none (fm3d_fastdiv.h: the same bits, checked by
+//     tools/micro/div_check.hip); by a pass-uniform denominator (h_j, the Householder
+//     norms) they are one multiply by the correctly rounded reciprocal and one Markstein
+//     correction;
+//   * one workgroup of kW = 15 term waves + the chain wave per CU (4 waves per SIMD).
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
@@ -64,16 +67,6 @@ typedef __attribute__((address_space(1))) const long long gi64;  // an int2 offs
 typedef __attribute__((address_space(1))) const uint8_t gu8;
 typedef __attribute__((address_space(1), aligned(1))) const uint16_t gu16u;  // a byte pair at any address
 
-
-// enorm terms: x^2 in MINPACK's intermediate range (the branch almost every value
-// takes), +0 otherwise -- an exact no-op on the non-negative running sum.  Values outside
-// the range raise `slow` and the chain lane replays the chunk with the full enorm.
-__device__ __forceinline__ double enorm_term(double x, double agiant, bool& slow) {
-    const double xa = fabs(x);
-    if (xa > 3.834e-20 && xa < agiant) return xa * xa;
-    if (xa != 0.) slow = true;
-    return 0.;
-}
 
 // ---------------------------------------------------------------- LDS state
 // the slot's current pass, written by lane 0 of the slot's term wave
@@ -551,14 +544,6 @@ struct Producer {
     }
 };
 
-// one residual evaluation of a neighbourhood entry: projectPointToPlane (:421-470),
-// isInBoundingBox (:646-655), projectPointsToImage2 (:591-644) -> gather address
-struct Geo {
-    float fx, fy;
-    const gu8* g;
-    int code;  // 0 ok, 2 NaN plane, 3 bounding box, 4 image-2 pixel outside
-};
-
 typedef __attribute__((address_space(4))) const ProjConst cProjConst;
 
 // The projection constants re-read (scalar loads, scalar cache) at every use: 21 uniform
@@ -571,43 +556,12 @@ __device__ __forceinline__ const cProjConst* proj_consts(const ProjConst* p) {
     return (const cProjConst*)((const __attribute__((address_space(4))) char*)p + z);
 }
 
-__device__ __forceinline__ Geo geometry(const LMParams& p, double ux, double uy, double n0, double n1, double n2,
-                                        double mm, double scale, double xmax, double ymax, const uint8_t* img2,
-                                        int lw, double cm) {
-    const cProjConst* pc = proj_consts(p.proj);
-    Geo r;
-    double nn = n0 * ux + n1 * uy + n2 * 1.;
-    double kk = mm / nn;
-    double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-    int cd = 0;
-    if (P0 != P0 || P1 != P1 || P2 != P2)
-        cd = 2;
-    else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm)))
-        cd = 3;
-    double u, v;
-    {
-        const double R[9] = {pc->R[0], pc->R[1], pc->R[2], pc->R[3], pc->R[4], pc->R[5], pc->R[6], pc->R[7], pc->R[8]};
-        const double t[3] = {pc->t[0], pc->t[1], pc->t[2]};
-        Camera cam;
-        cam.fx = pc->cam.fx;
-        cam.fy = pc->cam.fy;
-        cam.cx = pc->cam.cx;
-        cam.cy = pc->cam.cy;
-        for (int i = 0; i < 5; i++) cam.k[i] = pc->cam.k[i];
-        project1(cam, R, t, P0, P1, P2, u, v);
-    }
-    if (cd == 0 && !pixel_good_b(u, v, xmax, ymax)) cd = 4;
-    r.code = cd;
-    r.fx = (float)(scale * u);
-    r.fy = (float)(scale * v);
-    r.g = (const gu8*)img2;
-    if (cd == 0) r.g += (long)(int)floorf(r.fy) * lw + (int)floorf(r.fx);
-    return r;
-}
-
-// geometry() for the summed passes: the same arithmetic, reduced to what they consume.
+// One residual evaluation of a neighbourhood entry: projectPointToPlane (:421-470),
+// isInBoundingBox (:646-655), projectPointsToImage2 (:591-644) and the gather address,
+// reduced to what the summed passes consume:
 //  * inbox: isInBoundingBox of the plane point; false for a NaN coordinate too (the
-//    NaN-plane / bounding-box distinction is recomputed for the rare failing lane);
+//    NaN-plane / bounding-box distinction, failure codes 2 / 3, is recomputed for the rare
+//    failing lane by plane_code);
 //  * good: inbox and isPixelGood of the camera-2 pixel (NaN -> false).  u, v are only
 //    used when good, so the r6 NaN propagation of project1 is not needed: an infinite or
 //    NaN r6 makes u or v infinite or NaN either way;
@@ -649,8 +603,8 @@ __device__ __forceinline__ Geo2 geometry2(const LMParams& p, double ux, double u
     return r;
 }
 
-// failure code of geometry() (2 NaN plane point, 3 outside the bounding box) for an entry
-// whose inbox is false: the rare path of the summed passes
+// failure code (2 NaN plane point, 3 outside the bounding box) of an entry whose inbox is
+// false: the rare path of the summed passes
 __device__ __noinline__ int plane_code(double ux, double uy, double n0, double n1, double n2, double mm) {
     const double nn = n0 * ux + n1 * uy + n2 * 1.;
     const double kk = mm / nn;
