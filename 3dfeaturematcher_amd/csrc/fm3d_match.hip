@@ -13,6 +13,8 @@
 //   f32  -- float rows in FLANN's L2 accumulation order (groups of four), VALU.
 //   bits -- binary strings, Hamming by popcount, VALU.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <limits.h>
 #include <stdint.h>
 
@@ -88,6 +90,9 @@ __global__ void rowconst_u8_kernel(const uint8_t* __restrict__ X, int n, int nPa
     c[r] = s;
 }
 
+// KS: dimPad / 32 when it is 4 (128-byte rows) or 8 (256), so the MFMA chain is straight-line
+// code; 0 reads it from dimPad
+template <int KS>
 __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __restrict__ A, int nA,
                                                            const uint8_t* __restrict__ B, int nB, int dimPad,
                                                            const int* __restrict__ cqA, const int* __restrict__ ctB,
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     const int q0 = blockIdx.x * kQ + wave * 32;
     const int qrow = q0 + (lane & 31);
     const int half = lane >> 5;
-    const int ksteps = dimPad / 32;
+    const int ksteps = KS ? KS : dimPad / 32;
     const int chunksPerRow = dimPad / 16;
 
     // B operand: this lane's query bytes as int8 (x ^ 0x80 == x - 128)
@@ -151,18 +156,24 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
                     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[kk], acc, 0, 0, 0);
                 }
             }
-            // epilogue: s = |b'|^2 - 2 a'.b' for this lane's 16 train rows (increasing index)
+            // epilogue: s = |b'|^2 - 2 a'.b' for this lane's 16 train rows (increasing index);
+            // rows past nB exist only in the last tile, which alone runs the bounds test
             int sv[16];
             int smin = INT_MAX;
+            auto dists = [&](auto fullc) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                const int j = t * kT + row;
-                int s = ct[row] - 2 * acc[r];
-                s = (j < nB) ? s : INT_MAX;
-                sv[r] = s;
-                smin = smin < s ? smin : s;
-            }
+                for (int r = 0; r < 16; r++) {
+                    const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    int s = ct[row] - (acc[r] + acc[r]);
+                    if (!decltype(fullc)::value) s = (t * kT + row < nB) ? s : INT_MAX;
+                    sv[r] = s;
+                    smin = min(smin, s);
+                }
+            };
+            if ((t + 1) * kT <= nB)
+                dists(std::true_type());
+            else
+                dists(std::false_type());
             if (__any(smin < b2)) {
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
@@ -350,9 +361,17 @@ void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
                     int* idx, int* key, hipStream_t s) {
     if (nA <= 0) return;
     size_t lds = 2 * (size_t)kT * dimPad + 2 * kT * sizeof(int);
-    if (lds > 65536)
-        (void)hipFuncSetAttribute((const void*)knn2_u8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    knn2_u8_kernel<<<(nA + kQ - 1) / kQ, kThreads, lds, s>>>(A, nA, B, nB, dimPad, cqA, ctB, idx, key);
+    auto go = [&](auto kernel) {
+        if (lds > 65536)
+            (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        kernel<<<(nA + kQ - 1) / kQ, kThreads, lds, s>>>(A, nA, B, nB, dimPad, cqA, ctB, idx, key);
+    };
+    if (dimPad == 128)
+        go(knn2_u8_kernel<4>);
+    else if (dimPad == 256)
+        go(knn2_u8_kernel<8>);
+    else
+        go(knn2_u8_kernel<0>);
 }
 
 void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, int* idx, float* key, hipStream_t s) {
