@@ -863,14 +863,16 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             float i1;
                         };
                         // o8 / o4: byte offsets of the chunk's entries in the 8- / 4-byte slab arrays.
-                        // Entries past len (up to three chunks past the pass) read slab padding.
+                        // Entries past len (up to three chunks past the pass) read slab padding.  The
+                        // slab streams are read once per pass (nontemporal: they leave L2 to the
+                        // image gathers).
                         auto load = [&](unsigned o8, unsigned o4) {
                             const cProjConst* pc = proj_consts(p.proj);
                             Ld L;
-                            L.ux = *(const gdouble*)(pc->slabRX + o8);
-                            L.uy = *(const gdouble*)(pc->slabRY + o8);
-                            L.i1 = *(const gfloat*)(pc->slabI1 + o4);
-                            L.dF = JAC ? (double)*(const gfloat*)(pc->slabDF + o4) : 0.;
+                            L.ux = __builtin_nontemporal_load((const gdouble*)(pc->slabRX + o8));
+                            L.uy = __builtin_nontemporal_load((const gdouble*)(pc->slabRY + o8));
+                            L.i1 = __builtin_nontemporal_load((const gfloat*)(pc->slabI1 + o4));
+                            L.dF = JAC ? (double)__builtin_nontemporal_load((const gfloat*)(pc->slabDF + o4)) : 0.;
                             return L;
                         };
                         auto gather = [&](unsigned off) {  // two byte pairs: (y0, x0..x0+1), (y0+1, ...)
@@ -1019,9 +1021,9 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             const char* Dp = pc ? pcs->slabDJ1 : pcs->slabDJ0;
                             const char* Dq = pc ? pcs->slabDJ0 : pcs->slabDJ1;
                             Ld L;
-                            L.p = *(const gfloat*)(Dp + o4);
-                            L.q = *(const gfloat*)(Dq + o4);
-                            L.f = *(const gfloat*)(pcs->slabDF + o4);  // J = (w_j dI_j - F) / h_j needs F
+                            L.p = __builtin_nontemporal_load((const gfloat*)(Dp + o4));
+                            L.q = __builtin_nontemporal_load((const gfloat*)(Dq + o4));
+                            L.f = __builtin_nontemporal_load((const gfloat*)(pcs->slabDF + o4));  // J = (w_j dI_j - F) / h_j needs F
                             return L;
                         };
                         // edge: the first or the last chunk (the diagonal entries 0 and 1, entries
