@@ -429,7 +429,7 @@ struct Shared {
     // chunk terms [slot][ring position][sum][entry]; entry kE holds the chunk's slow flag for
     // that sum (nonzero: raw values for MINPACK's full enorm instead of squares)
     double ring[kW][kR][2][kRow];
-    int produced[kW];              // chunks produced, per slot (monotonic)
+    int rowTag[kW][kR];            // chunk index whose terms a ring position holds (published last)
     int consumed[kW][2];           // chunks consumed, per chain lane (monotonic)
     int resultId[kW][2];           // id of the last pass whose result is published
     double result[kW][2];
@@ -503,44 +503,40 @@ __device__ __forceinline__ const uint8_t* rfl_ptr(const uint8_t* q) {
 }
 
 // ---------------------------------------------------------------- term wave
-// Publishes chunk `seq` of slot w: waits for ring space, writes the two term rows,
-// releases the produced counter.
+// Publishes chunk c (slot w's running chunk index) into ring position c % kR: waits for ring
+// space, writes the two term rows and their slow flags, then releases the position's tag.
 struct Producer {
     Shared* sh;
     int w, lane;
-    int seq;
-    int room;  // chunks known to be free in the ring (from the last read of the consumed counters)
+    int cmin;  // chunks both chain lanes had consumed at the last read of their counters
     long long waitCycles;
 
-    __device__ __forceinline__ void put(double t0, double t1, int slowBits) {
-        // seq and room are wave-uniform: kept in SGPRs (readfirstlane on every LDS read)
-        if (room == 0) {
-            // ring space: both chain lanes of the slot have consumed chunk seq - kR.  The
-            // counters are read only when the space seen last time is used up, and the
-            // clock only when that space is still zero.
-            room = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1]))) + kR - seq;
-            if (room <= 0) {
+    __device__ __forceinline__ void put(int c, double t0, double t1, int slowBits) {
+        // c and cmin are wave-uniform: kept in SGPRs (readfirstlane on every LDS read)
+        if (c >= cmin + kR) {
+            // ring space: both chain lanes have consumed chunk c - kR.  The counters are read
+            // only when the space seen last time is used up, the clock only when still full.
+            cmin = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])));
+            if (c >= cmin + kR) {
                 const long long c0 = clock64();
                 do {
                     __builtin_amdgcn_s_sleep(1);
-                    room = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1]))) + kR - seq;
-                } while (room <= 0);
+                    cmin = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])));
+                } while (c >= cmin + kR);
                 waitCycles += clock64() - c0;
             }
         }
-        room--;
-        const int pos = seq & (kR - 1);
+        const int pos = c & (kR - 1);
         double* row0 = &sh->ring[w][pos][0][0];
         row0[lane] = t0;
         row0[kRow + lane] = t1;
-        // the flags and the counter are written by every lane (same address, same value): no
-        // lane-0 branch, so seq stays a scalar
+        // the flags and the tag are written by every lane (same address, same value): no
+        // lane-0 branch, so c stays a scalar
         row0[kE] = (slowBits & 1) ? 1. : 0.;
         row0[kRow + kE] = (slowBits & 2) ? 1. : 0.;
-        // every lane's ring stores are done before the counter is published (lgkmcnt is per wave)
+        // every lane's ring stores are done before the tag is published (lgkmcnt is per wave)
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        seq++;
-        lds_store_rel(&sh->produced[w], seq);
+        lds_store_rel(&sh->rowTag[w][pos], c);
     }
 };
 
@@ -668,8 +664,7 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
     for (;;) {
         if ((long long)(wall_clock64() - tStart) > maxTicks) break;
         if (!__any(alive)) break;
-        const int pr = alive ? lds_load_acq(&g_sh.produced[ss_]) : 0;
-        const bool have = alive && pr > cur;
+        const bool have = alive && lds_load_acq(&g_sh.rowTag[ss_][cur & (kR - 1)]) == cur;
         if (have && !inPass) {
             const PassDesc& d = g_sh.pd[ss_];
             rem = d.nChunks;
@@ -688,7 +683,8 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
             wasBusy = true;
             // up to two chunks per lane per round, never past the pass's last chunk; every
             // lane runs the same add chain (S_NONE lanes sum zeros they never publish)
-            const int nb = have ? min(min(pr - cur, rem), 2) : 0;
+            const int nb =
+                have ? ((rem >= 2 && lds_load_acq(&g_sh.rowTag[ss_][(cur + 1) & (kR - 1)]) == cur + 1) ? 2 : 1) : 0;
 #pragma nounroll
             for (int b = 0; b < 2; b++) {
                 if (b < nb) {
@@ -713,8 +709,8 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
                 busy += clock64() - tLast;
                 wasBusy = false;
             }
-            if (alive && !inPass && lds_load_acq(&g_sh.done[ss_]) && lds_load_acq(&g_sh.produced[ss_]) == cur)
-                alive = false;
+            // done is set after the slot's last pass completed: every chunk was consumed
+            if (alive && !inPass && lds_load_acq(&g_sh.done[ss_])) alive = false;
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -730,7 +726,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     const unsigned long long tStart = wall_clock64(), cyStart = clock64();
     if (tid == 0) sh.P = p;
     if (tid < kW) {
-        sh.produced[tid] = 0;
+        for (int k = 0; k < kR; k++) sh.rowTag[tid][k] = -1;
         sh.consumed[tid][0] = sh.consumed[tid][1] = 0;
         sh.resultId[tid][0] = sh.resultId[tid][1] = 0;
         sh.done[tid] = 0;
@@ -756,7 +752,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
         SlotP2& SP = sh.sp[w];
         SlotS2& SS = sh.ss[w];
         PassOut2& OUT = sh.out[w];
-        Producer prod{&sh, w, lane, 0, kR, 0};
+        Producer prod{&sh, w, lane, 0, 0};
+        int chunkSeq = 0;  // chunks of this slot published so far (all passes)
         const double cm = (double)p.cmax;
         const gi64* __restrict__ offsets = (const gi64*)p.offsets;
         const unsigned long long ltMask = (1ull << lane) - 1;
@@ -824,6 +821,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 // ---- a summed pass: terms here, sums by the chain lanes
                 passId++;
                 nPass++;
+                const int cbase = chunkSeq;  // chunk k of the pass is the slot's chunk cbase + k
+                chunkSeq = cbase + nCh;
                 const int ekind = rfl(SP.ekind);
                 const int nev = rfl(SP.nev);
                 const bool jac = pass == Q_EVAL && ekind == E_JAC;
@@ -927,7 +926,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 *(gfloat*)(proj_consts(p.proj)->slabDJ1 + o4) = dI1;
                                 t1 = enorm_term2(v1, agiant, slow1);
                             }
-                            prod.put(slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
+                            prod.put(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
                         };
                         unsigned o8 = slot8 + lane * 8u, o4 = o8 >> 1;
                         if (NEV == 2) {
@@ -974,7 +973,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 ph30 |= __ballot(inA && gA.inbox && !gA.good) | __ballot(inB && gB.inbox && !gB.good);
                                 A = load(o8 + 1024u, o4 + 512u);
                                 B = load(o8 + 1536u, o4 + 768u);
-                                auto back1 = [&](const Geo2& g, uint2 w, float i1, double dF, bool in, unsigned oo) {
+                                auto back1 = [&](const Geo2& g, uint2 w, float i1, double dF, bool in, unsigned oo, int kk) {
                                     const float dI = i1 - bilinear_w(w.x, w.y, g.fx, g.fy);
                                     const double r = w0 * (double)dI;
                                     double v = JAC ? mdiv(r - wF * dF, h0, y0, mok0) : r;
@@ -985,10 +984,10 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                     }
                                     bool slow;
                                     const double t = enorm_term2(v, agiant, slow);
-                                    prod.put(slow ? v : t, 0., slow ? 1 : 0);
+                                    prod.put(cbase + kk, slow ? v : t, 0., slow ? 1 : 0);
                                 };
-                                back1(gA, a, i1A, dFA, inA, o4);
-                                if (two) back1(gB, b, i1B, dFB, inB, o4 + 256u);
+                                back1(gA, a, i1A, dFA, inA, o4, k);
+                                if (two) back1(gB, b, i1B, dFB, inB, o4 + 256u, k + 1);
                                 o8 += 1024u;
                                 o4 += 512u;
                             }
@@ -1065,7 +1064,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 t0 = u * wa;
                                 if (edge && !(in && e > 0)) t0 = 0.;
                             }
-                            prod.put(slow ? a : t0, t1, slow ? 1 : 0);
+                            prod.put(cbase + k, slow ? a : t0, t1, slow ? 1 : 0);
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry
                         constexpr int kQD = 8;
