@@ -484,6 +484,8 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         const long long secs = ms && atoll(ms) > 0 ? atoll(ms) : 300;
         p.maxTicks = (long long)khz * 1000 * secs;
         c->wallKhz = khz;
+        const char* co = getenv("FM3D_LM_COOP");  // A/B switch for the tail help
+        p.coop = co ? atoi(co) : 1;
     }
     if (P > 0) {
         HIPCHK(c, hipEventRecord(e0, c->stream));

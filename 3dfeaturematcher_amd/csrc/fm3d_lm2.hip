@@ -435,6 +435,14 @@ struct Shared {
     double result[kW][2];
     Enorm chainEn[64];  // MINPACK enorm state of each chain lane (s2 lives in its register)
     int done[kW];
+    // tail help: a wave whose slot has no more points takes every other chunk of a busy slot's
+    // summed passes (one helper per slot, attached for good)
+    int helper[kW];                // 1 once a helper is attached
+    int annSeq[kW];                // passes announced to the helper (monotonic)
+    int annBase[kW], annId[kW];    // the announced pass: first chunk index, pass id
+    int helpDone[kW];              // id of the last announced pass whose helper share is complete
+    int hfail[kW][2], hph3[kW][2]; // the helper share's failures (as fail0/fail1, ph30/ph31 != 0)
+    int hAtt[kW], hSeen[kW], hAnn[kW];  // per wave (lane 0): attached slot, passes taken, passes announced
     PassDesc pd[kW];
     SlotP2 sp[kW];
     SlotS2 ss[kW];
@@ -510,6 +518,7 @@ struct Producer {
     int w, lane;
     int cmin;  // chunks both chain lanes had consumed at the last read of their counters
     long long waitCycles;
+    unsigned long long deadline;  // wall clock: the watchdog ends a wait that a broken chain never releases
 
     __device__ __forceinline__ void put(int c, double t0, double t1, int slowBits) {
         // c and cmin are wave-uniform: kept in SGPRs (readfirstlane on every LDS read)
@@ -522,7 +531,7 @@ struct Producer {
                 do {
                     __builtin_amdgcn_s_sleep(1);
                     cmin = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])));
-                } while (c >= cmin + kR);
+                } while (c >= cmin + kR && wall_clock64() < deadline);
                 waitCycles += clock64() - c0;
             }
         }
@@ -730,6 +739,9 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
         sh.consumed[tid][0] = sh.consumed[tid][1] = 0;
         sh.resultId[tid][0] = sh.resultId[tid][1] = 0;
         sh.done[tid] = 0;
+        sh.helper[tid] = sh.annSeq[tid] = sh.helpDone[tid] = 0;
+        sh.hAtt[tid] = -2;  // -2: the wave runs its own slot; -1: helper, not attached
+        sh.hSeen[tid] = sh.hAnn[tid] = 0;
     }
     __syncthreads();
 
@@ -741,7 +753,6 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
         const Slab sl = slab_of(p, gslot);
         // the summed passes address the slabs as grid-uniform array bases (ProjConst, scalar
         // loads) + one 32-bit byte offset per entry (global_load ... vOffset, sBase)
-        const unsigned slot8 = (unsigned)((size_t)gslot * p.nOffPad * 8);  // < 2^32 (host-checked)
         if (lane == 0) {
             ctl.p = &sh.P;
             ctl.sl = sl;
@@ -749,26 +760,81 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
             ctl.cnt_eval = 0;
             ctl.cnt_pix = 0;
         }
-        SlotP2& SP = sh.sp[w];
-        SlotS2& SS = sh.ss[w];
         PassOut2& OUT = sh.out[w];
-        Producer prod{&sh, w, lane, 0, 0};
+        Producer prod{&sh, w, lane, 0, 0, tStart + (unsigned long long)p.maxTicks};  // publishes into slot prod.w's ring
         int chunkSeq = 0;  // chunks of this slot published so far (all passes)
+        // sh.hAtt[w] != -2: no points left for slot w; the wave helps slot prod.w
         const double cm = (double)p.cmax;
         const gi64* __restrict__ offsets = (const gi64*)p.offsets;
         const unsigned long long ltMask = (1ull << lane) - 1;
         int passId = 0;
         long long nPass = 0, iterations = 0;
         unsigned long long cyCtl = 0, cyTerms = 0, clsCnt[4] = {0, 0, 0, 0}, clsCyc[4] = {0, 0, 0, 0};
-        if (lane == 0) ctl.fetch(SS, SP);
+        if (lane == 0) ctl.fetch(sh.ss[w], sh.sp[w]);
         for (;;) {
             if (++iterations > p.maxIter || (long long)(wall_clock64() - tStart) > p.maxTicks) {
                 if (lane == 0) atomicExch(p.overflow, 1);  // cannot happen for a correct state machine
                 break;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            bool own = true;
+            int hBase = 0;
+            if (rfl(sh.hAtt[w]) != -2) {
+                // helper: the attached slot's next announced pass; else attach to a busy slot
+                // without a helper; else leave.  A slot's owner announces its passes while the
+                // slot is not done and waits for each share, so a detach never strands a pass.
+                int go = 0, att = 0;
+                if (lane == 0) {
+                    att = sh.hAtt[w];
+                    int seen = sh.hSeen[w];
+                    for (;;) {
+                        if (att >= 0) {
+                            if (lds_load_acq(&sh.annSeq[att]) > seen) {
+                                seen++;
+                                hBase = sh.annBase[att];
+                                go = 1;
+                                break;
+                            }
+                            if (lds_load_acq(&sh.done[att])) {
+                                att = -1;
+                                continue;
+                            }
+                            if ((long long)(wall_clock64() - tStart) > p.maxTicks) break;
+                            __builtin_amdgcn_s_sleep(2);
+                            continue;
+                        }
+                        for (int s = 0; s < kW && att < 0; s++)
+                            if (s != w && !lds_load_acq(&sh.done[s]) && lds_load_acq(&sh.helper[s]) == 0 &&
+                                atomicCAS(&sh.helper[s], 0, 1) == 0) {
+                                att = s;
+                                seen = 0;  // a slot announces to its first and only helper
+                            }
+                        if (att < 0) break;
+                    }
+                    sh.hAtt[w] = att;
+                    sh.hSeen[w] = seen;
+                }
+                if (!rfl(go)) break;
+                att = rfl(att);
+                hBase = rfl(hBase);
+                own = false;
+                if (prod.w != att) {
+                    prod.w = att;
+                    prod.cmin = 0;
+                }
+            }
+            const int tw = prod.w;
+            SlotP2& SP = sh.sp[tw];
+            SlotS2& SS = sh.ss[tw];
             const int pass = rfl(SP.pass);
-            if (pass == Q_DONE) break;
+            if (own && pass == Q_DONE) {
+                if (!p.coop) break;
+                if (lane == 0) {
+                    lds_store_rel(&sh.done[w], 1);
+                    sh.hAtt[w] = -1;  // enter the helper branch above
+                }
+                continue;
+            }
             const unsigned long long tp0 = clock64();
             const int len = rfl(SP.len);
             const int nCh = (len + kE - 1) / kE;
@@ -819,22 +885,35 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 if (lane == 0) OUT.i1fail = anyBad ? 1 : 0;
             } else {
                 // ---- a summed pass: terms here, sums by the chain lanes
-                passId++;
-                nPass++;
-                const int cbase = chunkSeq;  // chunk k of the pass is the slot's chunk cbase + k
-                chunkSeq = cbase + nCh;
+                // chunk k of the pass is the slot's chunk cbase + k.  Split with a helper: the
+                // owner computes chunks 0, 2, 4, ..., the helper 1, 3, 5, ... (k0, kS)
+                int cbase = hBase, k0 = 1, kS = 2;
+                if (own) {
+                    passId++;
+                    nPass++;
+                    cbase = chunkSeq;
+                    chunkSeq = cbase + nCh;
+                    k0 = 0;
+                    kS = (p.coop && rfl(lds_load_acq(&sh.helper[w])) != 0) ? 2 : 1;  // 2: split
+                }
+                const unsigned s8 = (unsigned)(((size_t)blockIdx.x * kW + tw) * p.nOffPad * 8);  // slot tw's, < 2^32 (host-checked)
                 const int ekind = rfl(SP.ekind);
                 const int nev = rfl(SP.nev);
                 const bool jac = pass == Q_EVAL && ekind == E_JAC;
                 cls = jac ? 0 : (pass == Q_EVAL ? 1 : 2);
                 const double agiant = SP.agiant;
-                if (lane == 0) {
+                if (own && lane == 0) {
                     PassDesc& d = sh.pd[w];
                     d.nChunks = nCh;
                     d.id = passId;
                     d.agiant = agiant;
                     d.kind[0] = (pass == Q_QR1 || pass == Q_QR3) ? S_DOT : S_ENORM;
                     d.kind[1] = pass == Q_QR1 ? S_DOT : ((pass == Q_EVAL && nev == 2) ? S_ENORM : S_NONE);
+                    if (kS == 2) {  // SP, SS and the pass descriptor are written: announce
+                        sh.annBase[w] = cbase;
+                        sh.annId[w] = passId;
+                        lds_store_rel(&sh.annSeq[w], ++sh.hAnn[w]);
+                    }
                 }
                 int fail0 = 0x7fffffff, fail1 = 0x7fffffff;
                 unsigned long long ph30 = 0, ph31 = 0;  // image-2 failures seen (lane masks)
@@ -928,31 +1007,34 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             }
                             prod.put(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
                         };
-                        unsigned o8 = slot8 + lane * 8u, o4 = o8 >> 1;
+                        // this wave's chunks: k0, k0 + kS, ...; st8 / st4: the offset step between them
+                        unsigned o8 = s8 + lane * 8u + (unsigned)k0 * 512u, o4 = o8 >> 1;
+                        const unsigned st8 = (unsigned)kS * 512u, st4 = st8 >> 1;
                         if (NEV == 2) {
                             // two chunks of slab loads in flight ahead of the one being computed
-                            Ld A = load(o8, o4), B = load(o8 + 512u, o4 + 256u);
-                            for (int k = 0; k < nCh; k += 2) {
-                                const Ld C = load(o8 + 1024u, o4 + 512u);
+                            Ld A = load(o8, o4), B = load(o8 + st8, o4 + st4);
+                            for (int k = k0; k < nCh; k += 2 * kS) {
+                                const Ld C = load(o8 + 2 * st8, o4 + 2 * st4);
                                 chunk(A, k, o4);
                                 A = C;
-                                if (k + 1 < nCh) {
-                                    const Ld D = load(o8 + 1536u, o4 + 768u);
-                                    chunk(B, k + 1, o4 + 256u);
+                                if (k + kS < nCh) {
+                                    const Ld D = load(o8 + 3 * st8, o4 + 3 * st4);
+                                    chunk(B, k + kS, o4 + st4);
                                     B = D;
                                 }
-                                o8 += 1024u;
-                                o4 += 512u;
+                                o8 += 2 * st8;
+                                o4 += 2 * st4;
                             }
                         } else {
                             // one evaluation per entry: two chunks side by side, so the two
                             // independent geometries interleave (as the two columns of a Jacobian
                             // pass do); the slab loads of the next pair are issued once the pair's
                             // geometry has consumed its own
-                            Ld A = load(o8, o4), B = load(o8 + 512u, o4 + 256u);
-                            for (int k = 0; k < nCh; k += 2) {
-                                const bool two = k + 1 < nCh;  // wave-uniform
-                                const bool inA = k * kE + lane < len, inB = (k + 1) * kE + lane < len;
+                            Ld A = load(o8, o4), B = load(o8 + st8, o4 + st4);
+                            for (int k = k0; k < nCh; k += 2 * kS) {
+                                const int kB = k + kS;
+                                const bool two = kB < nCh;  // wave-uniform
+                                const bool inA = k * kE + lane < len, inB = kB * kE + lane < len;
                                 const Geo2 gA = geometry2(p, A.ux, A.uy, n00, n10, n20, mm0, mmok0, scale, xmax, ymax, lw, cm);
                                 // past the last chunk B holds slab padding: its entries are not
                                 // `in`, its gathers read the image's first bytes, nothing is stored
@@ -968,11 +1050,11 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                     const int l = __ffsll((long long)(first ? bA : bB)) - 1;
                                     const int cd = first ? plane_code(A.ux, A.uy, n00, n10, n20, mm0)
                                                          : plane_code(B.ux, B.uy, n00, n10, n20, mm0);
-                                    fail0 = ((first ? k : k + 1) * kE + l) * 4 + __shfl(cd, l);
+                                    fail0 = ((first ? k : kB) * kE + l) * 4 + __shfl(cd, l);
                                 }
                                 ph30 |= __ballot(inA && gA.inbox && !gA.good) | __ballot(inB && gB.inbox && !gB.good);
-                                A = load(o8 + 1024u, o4 + 512u);
-                                B = load(o8 + 1536u, o4 + 768u);
+                                A = load(o8 + 2 * st8, o4 + 2 * st4);
+                                B = load(o8 + 3 * st8, o4 + 3 * st4);
                                 auto back1 = [&](const Geo2& g, uint2 w, float i1, double dF, bool in, unsigned oo, int kk) {
                                     const float dI = i1 - bilinear_w(w.x, w.y, g.fx, g.fy);
                                     const double r = w0 * (double)dI;
@@ -987,9 +1069,9 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                     prod.put(cbase + kk, slow ? v : t, 0., slow ? 1 : 0);
                                 };
                                 back1(gA, a, i1A, dFA, inA, o4, k);
-                                if (two) back1(gB, b, i1B, dFB, inB, o4 + 256u, k + 1);
-                                o8 += 1024u;
-                                o4 += 512u;
+                                if (two) back1(gB, b, i1B, dFB, inB, o4 + st4, kB);
+                                o8 += 2 * st8;
+                                o4 += 2 * st4;
                             }
                         }
                     };
@@ -1068,20 +1150,27 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry
                         constexpr int kQD = 8;
-                        unsigned o4 = (slot8 >> 1) + lane * 4u;
+                        unsigned o4 = (s8 >> 1) + lane * 4u + (unsigned)k0 * 256u;
+                        const unsigned st4 = (unsigned)kS * 256u;
                         Ld buf[kQD];
 #pragma unroll
-                        for (int j = 0; j < kQD; j++) buf[j] = load(o4 + j * 256u);
-                        for (int k = 0; k < nCh; k += kQD) {
+                        for (int j = 0; j < kQD; j++) {
+                            buf[j] = load(o4);
+                            o4 += st4;
+                        }
+                        // o4: the prefetch offset, kQD chunks ahead (one running offset keeps the
+                        // per-chunk offsets out of the scalar registers)
+                        for (int k = k0; k < nCh; k += kQD * kS) {
 #pragma unroll
                             for (int j = 0; j < kQD; j++) {
-                                if (k + j < nCh) {
-                                    const Ld nx = load(o4 + (j + kQD) * 256u);
-                                    chunk(buf[j], k + j, k + j == 0 || k + j == nCh - 1);
+                                const int kc = k + j * kS;
+                                if (kc < nCh) {
+                                    const Ld nx = load(o4);
+                                    chunk(buf[j], kc, kc == 0 || kc == nCh - 1);
                                     buf[j] = nx;
                                 }
+                                o4 += st4;
                             }
-                            o4 += kQD * 256u;
                         }
                     };
                     if (pass == Q_QR1)
@@ -1092,28 +1181,48 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         run(std::integral_constant<int, Q_QR3>());
                     aqs1 = __shfl(aqs1, 1);  // QR2: entry 1 lives in lane 1 of chunk 0
                 }
-                // ---- the chain lanes' results of this pass
-                {
+                if (!own) {
+                    // the helper share is complete: its slab stores, then its failures
+                    __builtin_amdgcn_s_waitcnt(0);
+                    if (lane == 0) {
+                        sh.hfail[tw][0] = fail0;
+                        sh.hfail[tw][1] = fail1;
+                        sh.hph3[tw][0] = ph30 != 0;
+                        sh.hph3[tw][1] = ph31 != 0;
+                        lds_store_rel(&sh.helpDone[tw], sh.annId[tw]);
+                    }
+                } else {
+                    // ---- the chain lanes' results of this pass (and the helper share)
                     const long long c0 = clock64();
-                    while (lds_load_acq(&sh.resultId[w][0]) != passId || lds_load_acq(&sh.resultId[w][1]) != passId)
+                    while ((lds_load_acq(&sh.resultId[w][0]) != passId || lds_load_acq(&sh.resultId[w][1]) != passId) &&
+                           wall_clock64() < prod.deadline)
                         __builtin_amdgcn_s_sleep(1);
+                    bool hp0 = false, hp1 = false;
+                    if (kS == 2) {
+                        while (lds_load_acq(&sh.helpDone[w]) != passId && wall_clock64() < prod.deadline)
+                            __builtin_amdgcn_s_sleep(1);
+                        fail0 = min(fail0, sh.hfail[w][0]);
+                        fail1 = min(fail1, sh.hfail[w][1]);
+                        hp0 = sh.hph3[w][0] != 0;
+                        hp1 = sh.hph3[w][1] != 0;
+                    }
                     prod.waitCycles += clock64() - c0;
-                }
-                if (lane == 0) {
-                    OUT.nrm[0] = OUT.sum[0] = sh.result[w][0];
-                    OUT.nrm[1] = OUT.sum[1] = sh.result[w][1];
-                    OUT.fail[0] = fail0;
-                    OUT.fail[1] = fail1;
-                    OUT.ph3[0] = ph30 != 0;
-                    OUT.ph3[1] = ph31 != 0;
-                    OUT.aqs1 = aqs1;
+                    if (lane == 0) {
+                        OUT.nrm[0] = OUT.sum[0] = sh.result[w][0];
+                        OUT.nrm[1] = OUT.sum[1] = sh.result[w][1];
+                        OUT.fail[0] = fail0;
+                        OUT.fail[1] = fail1;
+                        OUT.ph3[0] = ph30 != 0 || hp0;
+                        OUT.ph3[1] = ph31 != 0 || hp1;
+                        OUT.aqs1 = aqs1;
+                    }
                 }
             }
             // every lane's slab and LDS stores are done before the bookkeeping reads them
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             const unsigned long long tp1 = clock64();
-            if (lane == 0) ctl.after_pass(SS, SP, OUT);
+            if (own && lane == 0) ctl.after_pass(SS, SP, OUT);
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long tp2 = clock64();
             cyTerms += tp1 - tp0;
