@@ -274,6 +274,24 @@ def test_normals_pyramid_depths(fm3d, orc, pair, levels):
     assert ok.sum() > 5
 
 
+@pytest.mark.parametrize("coop", ["0", "1"])
+def test_normals_more_points_than_slots(fm3d, orc, pair, coop, monkeypatch):
+    # 6,000 points > 3,840 slots: slots pull second points from the queue while idle slots help
+    # busy ones (FM3D_LM_COOP=1, the default) or leave (0); both must give the oracle's bits
+    monkeypatch.setenv("FM3D_LM_COOP", coop)
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    reps = -(-6000 // len(pts))
+    P = np.concatenate([pts * (1.0 + 2e-3 * r) for r in range(reps)])[:6000]
+    kept, normals, st, info, nfev, ref, _ = _normals_case(fm3d, orc, pair, P, 6)
+    assert np.array_equal(st, ref["status"])
+    assert np.array_equal(nfev[:, :4], ref["nfev"][:, :4])
+    ok = ref["status"] == 0
+    assert np.array_equal(normals, ref["normals"][ok])
+    assert np.array_equal(kept, P[ok])
+    assert ok.sum() > 1000
+
+
 def test_normals_vga_bounds(fm3d, orc, pair):
     # image bound = the VGA size instead of the reference's literal 1024x768
     q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
