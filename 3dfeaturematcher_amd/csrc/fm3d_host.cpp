@@ -71,6 +71,9 @@ struct fm3d_ctx {
     int nOff = 0, nOffPad = 0;
     // work buffers
     DevBuf A, B, cqA, ctB, idx, key, fkey, knnOut, cand, flag, matches, count, scanTmp;
+    DevBuf partIdx, partKey;  // per-part top-2 lists of the f32 matcher
+    DevBuf bPairs;            // the f32 train rows in interleaved pairs
+    int nCU = 0;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
     long lmGroups = 0;
     int wallKhz = 0;
@@ -346,8 +349,20 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         fm3d::launch_knn2_u8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->cqA.as<int>(),
                              c->ctB.as<int>(), c->idx.as<int>(), c->key.as<int>(), c->stream);
     } else if (type == FM3D_DESC_F32) {
-        fm3d::launch_knn2_f32(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, c->idx.as<int>(),
-                              c->fkey.as<float>(), c->stream);
+        if (c->nCU <= 0) {
+            int n = 0;
+            HIPCHK(c, hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, c->device));
+            c->nCU = n > 0 ? n : 1;
+        }
+        const int parts = fm3d::knn2_f32_parts(nA, nB, dimPad, c->nCU);
+        if (parts > 1) {
+            HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
+            HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(float) + 16));
+        }
+        HIPCHK(c, c->bPairs.ensure(fm3d::knn2_f32_pairs_bytes(nB, dimPad) + 16));
+        fm3d::launch_knn2_f32(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, parts, c->partIdx.as<int>(),
+                              c->partKey.as<float>(), c->bPairs.as<float>(), c->idx.as<int>(), c->fkey.as<float>(),
+                              c->stream);
     } else {
         fm3d::launch_knn2_bits(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->idx.as<int>(),
                                c->key.as<int>(), c->stream);
@@ -593,7 +608,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
                       &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat,
                       &c->slab, &c->slabI1,
-                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj};
+                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();

@@ -197,57 +197,140 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
 }
 
 // ---------------- float rows, FLANN L2 order ----------------
+// One query per thread, a[DIM] in registers.  The train rows are copied once into pairs,
+// interleaved element by element, and read through scalar loads (every lane needs the same
+// values), so one packed f32 instruction (v_pk_add / v_pk_mul, SGPR-pair operand) advances the
+// distances to two rows: per lane the arithmetic is exactly FLANN's L2 order (groups of four,
+// result += ((d0*d0 + d1*d1) + d2*d2) + d3*d3), just two rows at a time.  blockIdx.y selects a
+// contiguous range of train rows (a part); the parts' top-2 lists are merged by knn2_f32_merge.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ inline void top2_insert_f(float s, int j, float& b1, int& i1, float& b2, int& i2) {
+    // the scan order's rule: strictly smaller replaces (ties keep the lower train index; NaN and
+    // +inf never enter)
+    const bool lt1 = s < b1, lt2 = s < b2;
+    b2 = lt1 ? b1 : (lt2 ? s : b2);
+    i2 = lt1 ? i1 : (lt2 ? j : i2);
+    b1 = lt1 ? s : b1;
+    i1 = lt1 ? j : i1;
+}
+
+// B in row pairs, interleaved element by element: P[(pr*DIM + d)*2 + k] = B[2pr + k][d] (zero
+// past nB, nPairs rounded up to even so that the kernel may read pair pr + 1 unconditionally)
+__global__ void f32_row_pairs_kernel(const float* __restrict__ B, int nB, int dim, int nPairs, float* __restrict__ P) {
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (size_t)nPairs * dim * 2) return;
+    const int k = (int)(e & 1);
+    const size_t pd = e >> 1;
+    const int pr = (int)(pd / dim), d = (int)(pd - (size_t)pr * dim);
+    const int j = 2 * pr + k;
+    P[e] = j < nB ? B[(size_t)j * dim + d] : 0.f;
+}
+
+// (a.lo - b.lo, a.lo - b.hi) and (a.hi - b.lo, a.hi - b.hi) with b in an SGPR pair: one
+// v_pk_add_f32 with src0's half broadcast by op_sel (the query row stays packed two elements
+// per register pair)
+__device__ inline f32x2 pk_sub_lo_s(f32x2 a, f32x2 b) {
+    f32x2 d;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(a), "s"(b));
+    return d;
+}
+__device__ inline f32x2 pk_sub_hi_s(f32x2 a, f32x2 b) {
+    f32x2 d;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(a), "s"(b));
+    return d;
+}
+
+// the same scan with the train row pairs read through scalar loads (every lane of a wave needs
+// the same train values): no LDS traffic, the SGPR pair is the packed instruction's operand
 template <int DIM>
-__global__ __launch_bounds__(256) void knn2_f32_kernel(const float* __restrict__ A, int nA, const float* __restrict__ B,
-                                                       int nB, int* __restrict__ idxOut, float* __restrict__ keyOut) {
-    constexpr int TR = 32;  // train rows per tile
-    __shared__ float tile[TR * DIM];
+__global__ __launch_bounds__(256) void knn2_f32_sgpr_kernel(const float* __restrict__ A, int nA,
+                                                            const float* __restrict__ P, int nB, int rowsPerPart,
+                                                            int* __restrict__ idxOut, float* __restrict__ keyOut) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    float a[DIM];
+    const int jBeg = blockIdx.y * rowsPerPart;
+    const int jEnd = min(nB, jBeg + rowsPerPart);
+    f32x2 a[DIM / 2];
+    {
+        const float4* ap = reinterpret_cast<const float4*>(A + (size_t)min(q, nA - 1) * DIM);
 #pragma unroll
-    for (int d = 0; d < DIM; d++) a[d] = (q < nA) ? A[(size_t)q * DIM + d] : 0.f;
+        for (int k = 0; k < DIM / 4; k++) {
+            const float4 v = ap[k];
+            a[2 * k] = f32x2{v.x, v.y};
+            a[2 * k + 1] = f32x2{v.z, v.w};
+        }
+    }
     float b1 = __builtin_inff(), b2 = __builtin_inff();
     int i1 = -1, i2 = -1;
-    for (int t0 = 0; t0 < nB; t0 += TR) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < TR * DIM; e += blockDim.x) {
-            int j = t0 + e / DIM;
-            tile[e] = (j < nB) ? B[(size_t)t0 * DIM + e] : 0.f;
-        }
-        __syncthreads();
-        const int nr = (nB - t0) < TR ? (nB - t0) : TR;
-        for (int r = 0; r < nr; r++) {
-            const float* b = tile + r * DIM;
-            float result = 0.f;
-            int i = 0;
+    const float inf = __builtin_inff();
+    for (int j = jBeg; j < jEnd; j += 4) {  // jBeg even: rows j..j+3 are pairs j/2, j/2 + 1
+        const f32x2* b = reinterpret_cast<const f32x2*>(P) + (size_t)(j >> 1) * DIM;
+        const f32x2* c = b + DIM;
+        f32x2 res = {0.f, 0.f}, rec = {0.f, 0.f};
+        // software pipeline: the scalar loads of group g + kAhead are issued before group g is used
+        constexpr int kG = DIM / 4, kAhead = 3;
+        f32x2 vb[kG][4], vc[kG][4];
 #pragma unroll
-            for (; i + 3 < DIM; i += 4) {
-                float d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1], d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
-                result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+        for (int g = 0; g < kAhead; g++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                vb[g][t] = b[4 * g + t];
+                vc[g][t] = c[4 * g + t];
             }
 #pragma unroll
-            for (; i < DIM; i++) {
-                float d0 = a[i] - b[i];
-                result += d0 * d0;
+        for (int g = 0; g < kG; g++) {
+            if (g + kAhead < kG) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    vb[g + kAhead][t] = b[4 * (g + kAhead) + t];
+                    vc[g + kAhead][t] = c[4 * (g + kAhead) + t];
+                }
             }
-            const int j = t0 + r;
-            if (result < b1) {
-                b2 = b1;
-                i2 = i1;
-                b1 = result;
-                i1 = j;
-            } else if (result < b2) {
-                b2 = result;
-                i2 = j;
-            }
+            __builtin_amdgcn_sched_barrier(0);
+            const int i = 4 * g;
+            const f32x2 d0 = pk_sub_lo_s(a[i / 2], vb[g][0]), d1 = pk_sub_hi_s(a[i / 2], vb[g][1]);
+            const f32x2 d2 = pk_sub_lo_s(a[i / 2 + 1], vb[g][2]), d3 = pk_sub_hi_s(a[i / 2 + 1], vb[g][3]);
+            const f32x2 e0 = pk_sub_lo_s(a[i / 2], vc[g][0]), e1 = pk_sub_hi_s(a[i / 2], vc[g][1]);
+            const f32x2 e2 = pk_sub_lo_s(a[i / 2 + 1], vc[g][2]), e3 = pk_sub_hi_s(a[i / 2 + 1], vc[g][3]);
+            res += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+            rec += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
         }
+        top2_insert_f(res.x, j, b1, i1, b2, i2);
+        top2_insert_f(j + 1 < jEnd ? res.y : inf, j + 1, b1, i1, b2, i2);
+        top2_insert_f(j + 2 < jEnd ? rec.x : inf, j + 2, b1, i1, b2, i2);
+        top2_insert_f(j + 3 < jEnd ? rec.y : inf, j + 3, b1, i1, b2, i2);
     }
     if (q < nA) {
-        idxOut[2 * q] = i1;
-        idxOut[2 * q + 1] = i2;
-        keyOut[2 * q] = b1;
-        keyOut[2 * q + 1] = b2;
+        const size_t o = ((size_t)blockIdx.y * nA + q) * 2;
+        idxOut[o] = i1;
+        idxOut[o + 1] = i2;
+        keyOut[o] = b1;
+        keyOut[o + 1] = b2;
     }
+}
+
+// merges the parts' top-2 lists in part order (= train index order), with the scan's rule
+__global__ void knn2_f32_merge(const int* __restrict__ pIdx, const float* __restrict__ pKey, int nA, int parts,
+                               int* __restrict__ idxOut, float* __restrict__ keyOut) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = -1, i2 = -1;
+    for (int s = 0; s < parts; s++) {
+        const size_t o = ((size_t)s * nA + q) * 2;
+        int j0 = pIdx[o], j1 = pIdx[o + 1];
+        float k0 = pKey[o], k1 = pKey[o + 1];
+        if (j1 >= 0 && j1 < j0) {  // visit the part's two candidates in train index order
+            const int tj = j0; j0 = j1; j1 = tj;
+            const float tk = k0; k0 = k1; k1 = tk;
+        }
+        if (j0 >= 0) top2_insert_f(k0, j0, b1, i1, b2, i2);
+        if (j1 >= 0) top2_insert_f(k1, j1, b1, i1, b2, i2);
+    }
+    idxOut[2 * q] = i1;
+    idxOut[2 * q + 1] = i2;
+    keyOut[2 * q] = b1;
+    keyOut[2 * q + 1] = b2;
 }
 
 // generic dim: rows read from global memory (any dim, same FLANN order)
@@ -374,15 +457,49 @@ void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
         go(knn2_u8_kernel<0>);
 }
 
-void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, int* idx, float* key, hipStream_t s) {
+int knn2_f32_parts(int nA, int nB, int dim, int nCU) {
+    // train-range parts: spread the query blocks evenly over the CUs (the kernel is VALU-bound,
+    // one CU's time is its share of blocks); each part keeps >= 2048 rows
+    if (dim != 128 && dim != 64) return 1;
+    const int nBlk = (nA + 255) / 256;
+    int best = 1;
+    double bestT = 1e30;
+    for (int s = 1; s <= 8; s++) {
+        if (s > 1 && nB / s < 2048) break;
+        const double t = (double)((nBlk * s + nCU - 1) / nCU) / s;
+        if (t < bestT - 1e-9) {
+            bestT = t;
+            best = s;
+        }
+    }
+    return best;
+}
+
+size_t knn2_f32_pairs_bytes(int nB, int dim) {
+    const size_t nPairs = ((size_t)(nB + 1) / 2 + 1) & ~(size_t)1;
+    return nPairs * dim * 2 * sizeof(float);
+}
+
+void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, int parts, int* partIdx,
+                     float* partKey, float* pairs, int* idx, float* key, hipStream_t s) {
     if (nA <= 0) return;
     const int grid = (nA + 255) / 256;
-    if (dim == 128)
-        knn2_f32_kernel<128><<<grid, 256, 0, s>>>(A, nA, B, nB, idx, key);
-    else if (dim == 64)
-        knn2_f32_kernel<64><<<grid, 256, 0, s>>>(A, nA, B, nB, idx, key);
-    else
+    if (dim != 128 && dim != 64) {
         knn2_f32_generic_kernel<<<grid, 256, 0, s>>>(A, nA, B, nB, dim, idx, key);
+        return;
+    }
+    const int rowsPerPart = parts > 1 ? ((nB + parts - 1) / parts + 1) & ~1 : (nB > 0 ? nB : 1);
+    const dim3 g(grid, parts);
+    int* oi = parts > 1 ? partIdx : idx;
+    float* ok = parts > 1 ? partKey : key;
+    const int nPairs = (int)(knn2_f32_pairs_bytes(nB, dim) / (dim * 2 * sizeof(float)));
+    const size_t n = (size_t)nPairs * dim * 2;
+    f32_row_pairs_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(B, nB, dim, nPairs, pairs);
+    if (dim == 128)
+        knn2_f32_sgpr_kernel<128><<<g, 256, 0, s>>>(A, nA, pairs, nB, rowsPerPart, oi, ok);
+    else
+        knn2_f32_sgpr_kernel<64><<<g, 256, 0, s>>>(A, nA, pairs, nB, rowsPerPart, oi, ok);
+    if (parts > 1) knn2_f32_merge<<<grid, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
 }
 
 void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int* idx, int* key,

@@ -99,6 +99,25 @@ def test_knn2_f32_flann_order(fm3d, orc, ctx, dim):
     assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t)
 
 
+@pytest.mark.parametrize("dim", [128, 64])
+def test_knn2_f32_train_parts_and_ties(fm3d, orc, ctx, dim):
+    # a train set large enough to be split into parts (merged afterwards), an odd row count (the
+    # last row pair has one row) and exact duplicates across parts (ties: lower train index first)
+    rng = np.random.default_rng(100 + dim)
+    nB = 20001
+    B = rng.normal(0, 0.1, (nB, dim)).astype(np.float32)
+    B[15000:15400] = B[100:500]          # duplicates in a later part
+    B[nB - 1] = B[7]                     # and in the last, single-row pair
+    A = np.concatenate([B[:600] + rng.normal(0, 0.01, (600, dim)).astype(np.float32),
+                        B[100:300], B[[7, 7]],  # zero distances, tied twice
+                        rng.normal(0, 0.1, (2200, dim)).astype(np.float32)])
+    got = fm3d.DescriptorsMatcher(ctx).knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.F32, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    assert np.array_equal(got["distance"], dist)
+    assert (idx[600:800, 0] == np.arange(100, 300)).all() and (idx[600:800, 1] == np.arange(15000, 15200)).all()
+
+
 def test_knn2_f32_integer_valued_sift(fm3d, orc, ctx, pair):
     # OpenCV SIFT floats are integer valued: routed to the int8-MFMA kernel, same results
     A = pair.desc1[:1500].astype(np.float32)
