@@ -340,6 +340,11 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
     HIPCHK(c, c->cand.ensure((size_t)nA * sizeof(fm3d_dmatch) + 16));
     HIPCHK(c, c->flag.ensure((size_t)nA * sizeof(int) + 16));
     if (wantKnn) HIPCHK(c, c->knnOut.ensure((size_t)nA * 2 * sizeof(fm3d_dmatch) + 16));
+    if (c->nCU <= 0) {
+        int n = 0;
+        HIPCHK(c, hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, c->device));
+        c->nCU = n > 0 ? n : 1;
+    }
     if (type == FM3D_DESC_U8) {
         const int nAPad = nA, nBPad = nB;
         HIPCHK(c, c->cqA.ensure((size_t)(nAPad + 1) * sizeof(int)));
@@ -349,12 +354,7 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         fm3d::launch_knn2_u8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->cqA.as<int>(),
                              c->ctB.as<int>(), c->idx.as<int>(), c->key.as<int>(), c->stream);
     } else if (type == FM3D_DESC_F32) {
-        if (c->nCU <= 0) {
-            int n = 0;
-            HIPCHK(c, hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, c->device));
-            c->nCU = n > 0 ? n : 1;
-        }
-        const int parts = fm3d::knn2_f32_parts(nA, nB, dimPad, c->nCU);
+        const int parts = (dimPad == 64 || dimPad == 128) ? fm3d::knn2_parts(nA, nB, dimPad, c->nCU) : 1;
         if (parts > 1) {
             HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
             HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(float) + 16));
@@ -364,8 +364,13 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
                               c->partKey.as<float>(), c->bPairs.as<float>(), c->idx.as<int>(), c->fkey.as<float>(),
                               c->stream);
     } else {
-        fm3d::launch_knn2_bits(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->idx.as<int>(),
-                               c->key.as<int>(), c->stream);
+        const int parts = fm3d::knn2_parts(nA, nB, dimPad, c->nCU);
+        if (parts > 1) {
+            HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
+            HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
+        }
+        fm3d::launch_knn2_bits(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, parts, c->partIdx.as<int>(),
+                               c->partKey.as<int>(), c->idx.as<int>(), c->key.as<int>(), c->stream);
     }
     HIPCHK(c, hipGetLastError());
     fm3d::launch_nndr(type, c->idx.as<int>(), c->key.as<int>(), c->fkey.as<float>(), nA, nB, eps, queryOffset,

@@ -78,13 +78,14 @@ struct KnnOut {
 void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA,
                     const int* ctB, int* idx, int* key, hipStream_t s);
 void launch_rowconst_u8(const uint8_t* X, int n, int nPad, int dimPad, int* c, hipStream_t s);
-// f32 rows: `parts` train ranges (knn2_f32_parts), merged through partIdx/partKey (parts*nA*2 each)
-int knn2_f32_parts(int nA, int nB, int dim, int nCU);
+// f32 rows (dim 64 / 128): `parts` train ranges (knn2_parts), merged through partIdx/partKey (parts*nA*2 each)
+int knn2_parts(int nA, int nB, int dim, int nCU);
 size_t knn2_f32_pairs_bytes(int nB, int dim);  // the row-pair copy of B (dim 64 / 128)
 void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, int parts, int* partIdx,
                      float* partKey, float* pairs, int* idx, float* key, hipStream_t s);
-void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int* idx, int* key,
-                      hipStream_t s);
+// binary rows: `parts` train ranges (knn2_parts), merged through partIdx/partKey
+void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int parts, int* partIdx,
+                      int* partKey, int* idx, int* key, hipStream_t s);
 // distances + NNDR flag per query; type 0 f32 keys in fkey, 1 u8, 2 bits
 void launch_nndr(int type, const int* idx, const int* key, const float* fkey, int nA, int nB, double eps,
                  int queryOffset, fm3d_dmatch* knnOut, fm3d_dmatch* cand, int* flag, hipStream_t s);

@@ -371,38 +371,69 @@ __global__ __launch_bounds__(256) void knn2_f32_generic_kernel(const float* __re
 }
 
 // ---------------- binary strings, Hamming ----------------
-template <int NW>  // 32-bit words per descriptor
-__global__ __launch_bounds__(256) void knn2_bits_kernel(const uint32_t* __restrict__ A, int nA,
-                                                        const uint32_t* __restrict__ B, int nB,
-                                                        int* __restrict__ idxOut, int* __restrict__ keyOut) {
-    constexpr int TR = 256;
-    __shared__ uint32_t tile[TR * NW];
+// One query per thread; the train rows are read through scalar loads (uniform across the wave:
+// the words are SGPR operands of v_xor / v_bcnt, no LDS), over a train range (blockIdx.y, parts
+// merged by knn2_int_merge); four rows per iteration
+template <int NW>
+__global__ __launch_bounds__(256) void knn2_bits_sgpr_kernel(const uint32_t* __restrict__ A, int nA,
+                                                             const uint32_t* __restrict__ B, int nB, int rowsPerPart,
+                                                             int* __restrict__ idxOut, int* __restrict__ keyOut) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int jBeg = blockIdx.y * rowsPerPart;
+    const int jEnd = min(nB, jBeg + rowsPerPart);
     uint32_t a[NW];
+    const uint32_t* ap = A + (size_t)min(q, nA - 1) * NW;
 #pragma unroll
-    for (int w = 0; w < NW; w++) a[w] = (q < nA) ? A[(size_t)q * NW + w] : 0u;
+    for (int w = 0; w < NW; w++) a[w] = ap[w];
     int b1 = INT_MAX, b2 = INT_MAX, i1 = -1, i2 = -1;
-    for (int t0 = 0; t0 < nB; t0 += TR) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < TR * NW; e += blockDim.x) {
-            int j = t0 + e / NW;
-            tile[e] = (j < nB) ? B[(size_t)t0 * NW + e] : 0u;
-        }
-        __syncthreads();
-        const int nr = (nB - t0) < TR ? (nB - t0) : TR;
-        for (int r = 0; r < nr; r++) {
-            int h = 0;
+    int j = jBeg;
+    for (; j + 3 < jEnd; j += 4) {
+        const uint32_t* r = B + (size_t)j * NW;
+        int h[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int w = 0; w < NW; w++) h += __popc(a[w] ^ tile[r * NW + w]);
-            top2_insert(h, t0 + r, b1, i1, b2, i2);
-        }
+        for (int w = 0; w < NW; w++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) h[t] += __popc(a[w] ^ r[t * NW + w]);
+#pragma unroll
+        for (int t = 0; t < 4; t++) top2_insert(h[t], j + t, b1, i1, b2, i2);
+    }
+    for (; j < jEnd; j++) {
+        const uint32_t* r = B + (size_t)j * NW;
+        int h = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) h += __popc(a[w] ^ r[w]);
+        top2_insert(h, j, b1, i1, b2, i2);
     }
     if (q < nA) {
-        idxOut[2 * q] = i1;
-        idxOut[2 * q + 1] = i2;
-        keyOut[2 * q] = b1;
-        keyOut[2 * q + 1] = b2;
+        const size_t o = ((size_t)blockIdx.y * nA + q) * 2;
+        idxOut[o] = i1;
+        idxOut[o + 1] = i2;
+        keyOut[o] = b1;
+        keyOut[o + 1] = b2;
     }
+}
+
+// merges the parts' top-2 lists (int keys) in part order with the scan's rule
+__global__ void knn2_int_merge(const int* __restrict__ pIdx, const int* __restrict__ pKey, int nA, int parts,
+                               int* __restrict__ idxOut, int* __restrict__ keyOut) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    int b1 = INT_MAX, b2 = INT_MAX, i1 = -1, i2 = -1;
+    for (int s = 0; s < parts; s++) {
+        const size_t o = ((size_t)s * nA + q) * 2;
+        int j0 = pIdx[o], j1 = pIdx[o + 1];
+        int k0 = pKey[o], k1 = pKey[o + 1];
+        if (j1 >= 0 && j1 < j0) {  // visit the part's two candidates in train index order
+            const int tj = j0; j0 = j1; j1 = tj;
+            const int tk = k0; k0 = k1; k1 = tk;
+        }
+        if (j0 >= 0) top2_insert(k0, j0, b1, i1, b2, i2);
+        if (j1 >= 0) top2_insert(k1, j1, b1, i1, b2, i2);
+    }
+    idxOut[2 * q] = i1;
+    idxOut[2 * q + 1] = i2;
+    keyOut[2 * q] = b1;
+    keyOut[2 * q + 1] = b2;
 }
 
 __global__ void nndr_kernel(int type, const int* __restrict__ idx, const int* __restrict__ key,
@@ -457,10 +488,10 @@ void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
         go(knn2_u8_kernel<0>);
 }
 
-int knn2_f32_parts(int nA, int nB, int dim, int nCU) {
+int knn2_parts(int nA, int nB, int dim, int nCU) {
     // train-range parts: spread the query blocks evenly over the CUs (the kernel is VALU-bound,
     // one CU's time is its share of blocks); each part keeps >= 2048 rows
-    if (dim != 128 && dim != 64) return 1;
+    (void)dim;
     const int nBlk = (nA + 255) / 256;
     int best = 1;
     double bestT = 1e30;
@@ -502,18 +533,22 @@ void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, in
     if (parts > 1) knn2_f32_merge<<<grid, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
 }
 
-void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int* idx, int* key,
-                      hipStream_t s) {
+void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int parts, int* partIdx,
+                      int* partKey, int* idx, int* key, hipStream_t s) {
     if (nA <= 0) return;
     const int grid = (nA + 255) / 256;
     const uint32_t* a = (const uint32_t*)A;
     const uint32_t* b = (const uint32_t*)B;
+    const int rowsPerPart = parts > 1 ? (nB + parts - 1) / parts : (nB > 0 ? nB : 1);
+    const dim3 g(grid, parts);
+    int* oi = parts > 1 ? partIdx : idx;
+    int* ok = parts > 1 ? partKey : key;
     switch (dimBytes / 4) {
-        case 8: knn2_bits_kernel<8><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;
-        case 16: knn2_bits_kernel<16><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;
-        case 4: knn2_bits_kernel<4><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;
-        default: knn2_bits_kernel<16><<<grid, 256, 0, s>>>(a, nA, b, nB, idx, key); break;  // padded to 64 B
+        case 8: knn2_bits_sgpr_kernel<8><<<g, 256, 0, s>>>(a, nA, b, nB, rowsPerPart, oi, ok); break;
+        case 4: knn2_bits_sgpr_kernel<4><<<g, 256, 0, s>>>(a, nA, b, nB, rowsPerPart, oi, ok); break;
+        default: knn2_bits_sgpr_kernel<16><<<g, 256, 0, s>>>(a, nA, b, nB, rowsPerPart, oi, ok); break;  // 64 B
     }
+    if (parts > 1) knn2_int_merge<<<grid, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
 }
 
 void launch_nndr(int type, const int* idx, const int* key, const float* fkey, int nA, int nB, double eps,
