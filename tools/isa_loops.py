@@ -16,7 +16,10 @@ def main():
     start = next(i for i, l in enumerate(text) if re.match(r"^_Z\w*" + key + r"\w*:", l))
     end = next(i for i in range(start, len(text)) if text[i].startswith(".Lfunc_end"))
     lines = text[start:end]
-    heads = [(i, l.split(":")[0]) for i, l in enumerate(lines) if "Loop Header" in l and l.startswith(".LBB")]
+    # the "Loop Header" note is on the label's line, or on the next one for nested loops
+    heads = [(i, l.split(":")[0]) for i, l in enumerate(lines) if l.startswith(".LBB") and
+             ("Loop Header" in l or (i + 1 < len(lines) and "Loop Header" in lines[i + 1] and
+                                     not lines[i + 1].startswith(".LBB")))]
     for i, h in heads:
         ends = [j for j, l in enumerate(lines) if re.search(r"s_c?branch\w* " + re.escape(h) + r"$", l)]
         if not ends:
