@@ -507,7 +507,8 @@ int knn2_parts(int nA, int nB, int dim, int nCU) {
 }
 
 size_t knn2_f32_pairs_bytes(int nB, int dim) {
-    const size_t nPairs = ((size_t)(nB + 1) / 2 + 1) & ~(size_t)1;
+    size_t nPairs = ((size_t)(nB + 1) / 2 + 1) & ~(size_t)1;
+    if (nPairs < 2) nPairs = 2;  // nB = 0: still a (zero) launch grid
     return nPairs * dim * 2 * sizeof(float);
 }
 

@@ -118,6 +118,29 @@ def test_knn2_f32_train_parts_and_ties(fm3d, orc, ctx, dim):
     assert (idx[600:800, 0] == np.arange(100, 300)).all() and (idx[600:800, 1] == np.arange(15000, 15200)).all()
 
 
+@pytest.mark.parametrize("kind", ["f32_128", "f32_64", "bits"])
+@pytest.mark.parametrize("shape", [(1, 5), (130, 1), (5, 2), (40, 0), (300, 4099)])
+def test_knn2_ragged_f32_and_bits(fm3d, orc, ctx, kind, shape):
+    # one query, one or two train rows, no train rows (trainIdx -1), odd sizes past a part
+    nA, nB = shape
+    rng = np.random.default_rng(nA * 13 + nB)
+    if kind == "bits":
+        A = rng.integers(0, 256, (nA, 32), dtype=np.uint8)
+        B = rng.integers(0, 256, (nB, 32), dtype=np.uint8)
+        ty = orc.BITS
+    else:
+        d = int(kind.split("_")[1])
+        A = rng.normal(0, 0.1, (nA, d)).astype(np.float32)
+        B = rng.normal(0, 0.1, (nB, d)).astype(np.float32)
+        ty = orc.F32
+    got = fm3d.DescriptorsMatcher(ctx, binary=kind == "bits").knn_match(A, B)
+    idx, dist = orc.knn2(A, B, ty, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    ok = idx >= 0
+    assert np.array_equal(got["distance"][ok], dist[ok])
+    assert (idx[:, 0] >= 0).all() == (nB >= 1) and (idx[:, 1] >= 0).all() == (nB >= 2)
+
+
 def test_knn2_f32_integer_valued_sift(fm3d, orc, ctx, pair):
     # OpenCV SIFT floats are integer valued: routed to the int8-MFMA kernel, same results
     A = pair.desc1[:1500].astype(np.float32)
