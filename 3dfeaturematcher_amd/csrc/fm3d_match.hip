@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
                                                            const int* __restrict__ cqA, const int* __restrict__ ctB,
                                                            int* __restrict__ idxOut, int* __restrict__ keyOut) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tileBytes = kT * dimPad;
+    const int tileBytes = kT * (KS ? 32 * KS : dimPad);
     unsigned char* tiles = smem;                              // 2 x tileBytes
     int* ctl = (int*)(smem + 2 * (size_t)tileBytes);          // 2 x kT
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -106,7 +106,8 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     const int qrow = q0 + (lane & 31);
     const int half = lane >> 5;
     const int ksteps = KS ? KS : dimPad / 32;
-    const int chunksPerRow = dimPad / 16;
+    const int rowBytes = KS ? 32 * KS : dimPad;  // = dimPad (compile-time for KS != 0)
+    const int chunksPerRow = rowBytes / 16;
 
     // B operand: this lane's query bytes as int8 (x ^ 0x80 == x - 128)
     v4i bq[8];  // up to dimPad = 256
@@ -121,28 +122,51 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     int b1 = INT_MAX, i1 = -1, b2 = INT_MAX, i2 = -1;
     const int nTiles = (nB + kT - 1) / kT;
 
-    auto stage = [&](int t, int buf) {
-        unsigned char* dst = tiles + (size_t)buf * tileBytes;
-        const int total = kT * chunksPerRow;
-        for (int c = tid; c < total; c += kThreads) {
-            int row = c / chunksPerRow, ch = c % chunksPerRow;
-            int j = t * kT + row;
+    // train tiles: the global loads of tile t + 1 are issued into registers before tile t is
+    // computed and written to LDS after it, so their latency overlaps the MFMA work
+    constexpr int kPre = 8;  // 16-byte chunks per thread and tile (kT * 256 / 16 / kThreads at most)
+    const int total = kT * chunksPerRow;
+    v4i pre[kPre];
+    int preCt = INT_MAX / 4;
+    auto load_tile = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < kPre; i++) {
+            const int c = tid + i * kThreads;
             v4i v = {0, 0, 0, 0};
-            if (j < nB) v = *(const v4i*)(B + (size_t)j * dimPad + 16 * ch);
-            v = v ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
-            *(v4i*)(dst + (size_t)row * dimPad + 16 * swz_chunk(row, ch)) = v;
+            if (c < total) {
+                const int row = c / chunksPerRow, ch = c - row * chunksPerRow;
+                const int j = t * kT + row;
+                if (j < nB) v = *(const v4i*)(B + (size_t)j * rowBytes + 16 * ch);
+            }
+            pre[i] = v;
         }
         if (tid < kT) {
-            int j = t * kT + tid;
-            ctl[buf * kT + tid] = (j < nB) ? ctB[j] : INT_MAX / 4;
+            const int j = t * kT + tid;
+            preCt = (j < nB) ? ctB[j] : INT_MAX / 4;
         }
     };
+    auto store_tile = [&](int buf) {
+        unsigned char* dst = tiles + (size_t)buf * tileBytes;
+#pragma unroll
+        for (int i = 0; i < kPre; i++) {
+            const int c = tid + i * kThreads;
+            if (c < total) {
+                const int row = c / chunksPerRow, ch = c - row * chunksPerRow;
+                *(v4i*)(dst + (size_t)row * rowBytes + 16 * swz_chunk(row, ch)) =
+                    pre[i] ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+            }
+        }
+        if (tid < kT) ctl[buf * kT + tid] = preCt;
+    };
 
-    if (nTiles > 0) stage(0, 0);
+    if (nTiles > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
     __syncthreads();
     for (int t = 0; t < nTiles; t++) {
         const int buf = t & 1;
-        if (t + 1 < nTiles) stage(t + 1, buf ^ 1);
+        if (t + 1 < nTiles) load_tile(t + 1);
         const unsigned char* tl = tiles + (size_t)buf * tileBytes;
         const int* ct = ctl + buf * kT;
 #pragma unroll
@@ -152,7 +176,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
 #pragma unroll
             for (int kk = 0; kk < 8; kk++) {
                 if (kk < ksteps) {
-                    v4i a = *(const v4i*)(tl + (size_t)arow * dimPad + 16 * swz_chunk(arow, 2 * kk + half));
+                    v4i a = *(const v4i*)(tl + (size_t)arow * rowBytes + 16 * swz_chunk(arow, 2 * kk + half));
                     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[kk], acc, 0, 0, 0);
                 }
             }
@@ -182,6 +206,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
                 }
             }
         }
+        if (t + 1 < nTiles) store_tile(buf ^ 1);
         __syncthreads();
     }
     // lanes l and l+32 hold the same query (different train rows): merge
