@@ -33,7 +33,7 @@ EXPORTS = (
     "fm3d_camera2_from_g12", "fm3d_set_g12", "fm3d_get_camera2", "fm3d_triangulate", "fm3d_set_images",
     "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
-    "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches",
+    "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
 )
 
 
@@ -284,6 +284,15 @@ class NeighborhoodsGenerator:
 
     def size(self) -> int:
         return lib().fm3d_patch_size(ctypes.byref(self.settings))
+
+    def computeSquareNeighborhoodsByNormals(self, ctx: "Context", featuresFrames) -> np.ndarray:
+        """neighborhoodsgenerator.cpp:76-132 (main.cpp:187): (P, size*size, 3) points of the square
+        grid transformed by each feature frame, point order i*size + j; computed on the GPU of ctx."""
+        F = np.ascontiguousarray(featuresFrames, dtype=np.float64).reshape(-1, 16)
+        n, size = F.shape[0], self.size()
+        out = np.zeros((max(n, 1), size * size, 3))
+        ctx.check(lib().fm3d_square_neighborhoods(ctx.handle, _ptr(F), n, _ptr(out)))
+        return out[:n]
 
     def getReferenceSquaredNeighborhood(self) -> np.ndarray:
         """neighborhoodsgenerator.cpp:134-158: (size*size, 3) points (-eps + inc*i, -eps + inc*j, 0),

@@ -1054,6 +1054,33 @@ int fm3d_export_patches(fm3d_ctx* c, const double* frames, int P, uint8_t* patch
     return FM3D_OK;
 }
 
+int fm3d_square_neighborhoods(fm3d_ctx* c, const double* frames, int P, double* out) {
+    if (!c || P < 0 || (P && (!frames || !out))) return FM3D_ERR_INVALID;
+    const int size = fm3d_patch_size(&c->s);
+    if (size <= 0) return fail(c, FM3D_ERR_INVALID, "neighbourhood size <= 0 (Neighborhoods.epsilon / cmPerPixel)");
+    if (P == 0) return FM3D_OK;
+    hipSetDevice(c->device);
+    // chunks of frames bound the device buffer (~512 MB of points); the copy of chunk k overlaps
+    // nothing here -- the host buffer is the boundary
+    const size_t perFrame = (size_t)size * size * 3 * sizeof(double);
+    const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)P, ((size_t)512 << 20) / perFrame));
+    DevBuf f, o;
+    HIPCHK(c, f.ensure((size_t)chunk * 16 * sizeof(double)));
+    HIPCHK(c, o.ensure((size_t)chunk * perFrame));
+    for (int p0 = 0; p0 < P; p0 += chunk) {
+        const int n = std::min(chunk, P - p0);
+        HIPCHK(c, hipMemcpyAsync(f.p, frames + (size_t)16 * p0, (size_t)n * 16 * sizeof(double),
+                                 hipMemcpyHostToDevice, c->stream));
+        fm3d::launch_square_neighborhoods(f.as<double>(), n, size, c->s.neighEpsilon, c->s.cmPerPixel * 0.01,
+                                          o.as<double>(), c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(out + (size_t)p0 * size * size * 3, o.p, (size_t)n * perFrame,
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return FM3D_OK;
+}
+
 int fm3d_pyrdown(fm3d_ctx* c, const uint8_t* src, int width, int height, uint8_t* dst) {
     if (!c || !src || !dst || width <= 0 || height <= 0) return FM3D_ERR_INVALID;
     hipSetDevice(c->device);

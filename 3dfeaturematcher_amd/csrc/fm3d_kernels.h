@@ -122,6 +122,9 @@ void launch_undistort(const Camera& cam, const double* xy, int n, double* out, h
 // ---------------- feature frames + patch export (fm3d_patch.hip) ----------------
 void launch_features_frames(const double* pts, const double* nrm, int P, const double g[3], double* frames,
                             hipStream_t s);
+// computeSquareNeighborhoodsByNormals: out P*size*size*3 doubles (device)
+void launch_square_neighborhoods(const double* frames, int P, int size, double eps, double inc, double* out,
+                                 hipStream_t s);
 // RT: 12 doubles of scratch per frame
 void launch_export_patches(const double* frames, int P, int size, double eps, double inc, const Camera& cam,
                            const uint8_t* img, int w, int h, double* RT, uint8_t* patches, double* imagePoints,

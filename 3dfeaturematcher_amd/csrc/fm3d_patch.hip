@@ -5,13 +5,16 @@
 // SingleCameraTriangulator::projectReferencePointsToImageWithFrame(s)
 // (singlecameratriangulator.cpp:769-849).  main.cpp:157-180 runs them after the normals.
 //
-// Three kernels, all bit-exact against oracle/fm3d_oracle.c (deterministic-math mode):
+// Four kernels, all bit-exact against oracle/fm3d_oracle.c (deterministic-math mode):
 //   frames_kernel        one thread per point: z = n, x = g x z, y = z x x, cv::normalize(x), (y),
 //                        columns through Vec::dot, translation = the point;
 //   frame_camera_kernel  one thread per frame: decomposeTransformation + the cvRodrigues2 round trip
 //                        cvProjectPoints2 applies (matrix -> vector -> matrix);
 //   patch_kernel         one thread per (reference point, frame): projectPoints, isPixelGood(p, 1.0)
-//                        of image 1, (uchar) bilinear sample, written transposed (patch.at(col, row)).
+//                        of image 1, (uchar) bilinear sample, written transposed (patch.at(col, row));
+//   square_neighborhoods_kernel  NeighborhoodsGenerator::computeSquareNeighborhoodsByNormals
+//                        (neighborhoodsgenerator.cpp:76-132, main.cpp:187): the square grid through
+//                        every frame, 24 B written per point (HBM-bound).
 // Every output byte depends on one projected sample; the patch kernel is a projection + gather
 // bound by the fp64 VALU (≈60 fp64 ops per sample) -- there is no reduction and no data reuse
 // beyond the image in L2.
@@ -169,7 +172,61 @@ __global__ __launch_bounds__(256) void patch_kernel(const double* __restrict__ R
     patches[base + (size_t)j * size + i] = val;  // patch.at<uchar>(col, row), :842-846
 }
 
+// computeSquareNeighborhoodByNormal (neighborhoodsgenerator.cpp:92-132) of every frame: point
+// (i, j) = frame * (-eps + inc*i, -eps + inc*j, 0, 1) in Matx44d * Vec4d's order (s = 0, then
+// += m(r,k) v(k) for k = 0..3), scaled by 1/w when w != 1.  One thread per output point, a block =
+// 256 consecutive points; the 24-byte records go through LDS and leave as coalesced 16-byte
+// nontemporal stores (the kernel is bound by the HBM writes, 24 B per point).
+constexpr int kSqThreads = 256;
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(kSqThreads) void square_neighborhoods_kernel(const double* __restrict__ frames,
+                                                                           long long total, int size, double eps,
+                                                                           double inc, double* __restrict__ out) {
+    __shared__ double rec[kSqThreads * 3];
+    const long long base = (long long)blockIdx.x * kSqThreads;
+    const long long idx = base + threadIdx.x;
+    if (idx < total) {
+        const long long per = (long long)size * size;
+        const long long f = idx / per;
+        const int ij = (int)(idx - f * per);
+        const int i = ij / size, j = ij - (ij / size) * size;
+        const double* F = frames + 16 * f;
+        const double v0 = -eps + inc * i, v1 = -eps + inc * j, v2 = 0, v3 = 1;
+        double h[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            h[r] = (((0 + F[4 * r] * v0) + F[4 * r + 1] * v1) + F[4 * r + 2] * v2) + F[4 * r + 3] * v3;
+        if (h[3] != 1) {
+            const double a = 1. / h[3];
+            h[0] = h[0] * a;
+            h[1] = h[1] * a;
+            h[2] = h[2] * a;
+        }
+        rec[3 * threadIdx.x] = h[0];
+        rec[3 * threadIdx.x + 1] = h[1];
+        rec[3 * threadIdx.x + 2] = h[2];
+    }
+    __syncthreads();
+    const long long n = total - base < kSqThreads ? total - base : kSqThreads;  // points of this block
+    const int nd = (int)(3 * n);                                                  // doubles (even unless n odd)
+    double* o = out + 3 * base;
+    for (int k = threadIdx.x; 2 * k < nd; k += kSqThreads) {
+        if (2 * k + 1 < nd)
+            __builtin_nontemporal_store(*(const f64x2*)&rec[2 * k], (f64x2*)(o + 2 * k));
+        else
+            __builtin_nontemporal_store(rec[2 * k], o + 2 * k);
+    }
+}
+
 }  // namespace
+
+void launch_square_neighborhoods(const double* frames, int P, int size, double eps, double inc, double* out,
+                                 hipStream_t s) {
+    const long long total = (long long)P * size * size;
+    if (total <= 0) return;
+    square_neighborhoods_kernel<<<(unsigned)((total + kSqThreads - 1) / kSqThreads), kSqThreads, 0, s>>>(
+        frames, total, size, eps, inc, out);
+}
 
 void launch_features_frames(const double* pts, const double* nrm, int P, const double g[3], double* frames,
                             hipStream_t s) {

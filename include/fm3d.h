@@ -193,6 +193,11 @@ int fm3d_patch_size(const fm3d_settings *s);
    patch.at<uchar>(col, row)); imagePoints (may be NULL): 2*size*size doubles per frame, point order
    i*size + j.  patches: P*size*size bytes. */
 int fm3d_export_patches(fm3d_ctx *ctx, const double *frames, int P, uint8_t *patches, double *imagePoints);
+/* NeighborhoodsGenerator::computeSquareNeighborhoodsByNormals (neighborhoodsgenerator.cpp:76-132,
+   called at main.cpp:187): per frame the size x size square grid (-eps + inc*i, -eps + inc*j, 0),
+   inc = 0.01*cmPerPixel, transformed by the frame (Matx44d * Vec4d; scaled by 1/w when w != 1).
+   out: P*size*size*3 doubles, point order i*size + j (host buffer; computed in HBM in chunks). */
+int fm3d_square_neighborhoods(fm3d_ctx *ctx, const double *frames, int P, double *out);
 
 /* ---------------- the whole hot path, device resident ---------------- */
 /* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */

@@ -103,6 +103,19 @@ public:
         for (int i = 0; i < n; i++)
             for (int j = 0; j < n; j++) neighborhood.push_back(Vec3d{-s_.neighEpsilon + inc * i, -s_.neighEpsilon + inc * j, 0});
     }
+    // computeSquareNeighborhoodsByNormals (neighborhoodsgenerator.cpp:76-132, main.cpp:187): cleared,
+    // then per frame the size^2 grid points moved by the frame, computed on d's GPU
+    void computeSquareNeighborhoodsByNormals(Device& d, const std::vector<Matx44d>& featuresFrames,
+                                             std::vector<std::vector<Vec3d> >& neighborhoodsVector) const {
+        const size_t per = (size_t)fm3d_patch_size(&s_) * fm3d_patch_size(&s_);
+        std::vector<Vec3d> all(featuresFrames.size() * per);
+        neighborhoodsVector.clear();
+        if (featuresFrames.empty()) return;
+        check(d.ctx(), fm3d_square_neighborhoods(d.ctx(), featuresFrames.data()->data(), (int)featuresFrames.size(),
+                                                 all.data()->data()));
+        for (size_t f = 0; f < featuresFrames.size(); f++)
+            neighborhoodsVector.emplace_back(all.begin() + f * per, all.begin() + (f + 1) * per);
+    }
 
 private:
     fm3d_settings s_;

@@ -1386,6 +1386,38 @@ ORC_API int orc_patch_size(double eps, double cmpp)
     return 2 * ((int)floor(eps / (0.01 * cmpp)));
 }
 
+/* computeSquareNeighborhoodsByNormals (neighborhoodsgenerator.cpp:76-90) ->
+   computeSquareNeighborhoodByNormal (:92-132) for every frame: point (i, j), i outer, =
+   featureFrame * (-eps + inc*i, -eps + inc*j, 0, 1) with Matx44d * Vec4d's sum order
+   (s = 0; s += m(r,k) * v(k), k = 0..3); when the w component != 1 the point is scaled by 1/w
+   (OpenCV Vec / double), then (x, y, z) kept.  out: P*size*size*3, point order i*size + j. */
+ORC_API int orc_square_neighborhoods(const double *frames, int P, double eps, double cmpp, double *out)
+{
+    const int size = orc_patch_size(eps, cmpp);
+    const double inc = cmpp * 0.01;
+    int p;
+    if (size <= 0) return 0;
+    #pragma omp parallel for schedule(static)
+    for (p = 0; p < P; p++) {
+        const double *F = frames + (size_t)16 * p;
+        int i, j, r;
+        for (i = 0; i < size; i++)
+            for (j = 0; j < size; j++) {
+                const double v[4] = {-eps + inc * i, -eps + inc * j, 0, 1};
+                double h[4];
+                double *o = out + ((size_t)p * size * size + (size_t)i * size + j) * 3;
+                for (r = 0; r < 4; r++)
+                    h[r] = (((0 + F[4 * r] * v[0]) + F[4 * r + 1] * v[1]) + F[4 * r + 2] * v[2]) + F[4 * r + 3] * v[3];
+                if (h[3] != 1) {
+                    const double a = 1. / h[3];
+                    h[0] = h[0] * a; h[1] = h[1] * a; h[2] = h[2] * a;
+                }
+                o[0] = h[0]; o[1] = h[1]; o[2] = h[2];
+            }
+    }
+    return size;
+}
+
 /* cvRodrigues2 round trip of decomposeTransformation + cvProjectPoints2, with libm (mode 0) or
    the deterministic transcendentals (mode ORC_LM_DETMATH; acos(c) = atan2(sqrt((1-c)(1+c)), c)). */
 static void orc_frame_camera(const double F[16], int mode, double R2[9], double t2[3])

@@ -243,6 +243,16 @@ def patch_size(eps, cmpp):
     return lib().orc_patch_size(ctypes.c_double(eps), ctypes.c_double(cmpp))
 
 
+def square_neighborhoods(frames, eps=0.16, cmpp=0.25):
+    """computeSquareNeighborhoodsByNormals (neighborhoodsgenerator.cpp:76-132): (P, size*size, 3)."""
+    F = _f64(frames).reshape(-1, 16)
+    n = F.shape[0]
+    size = patch_size(eps, cmpp)
+    out = np.zeros((n, max(size, 0) ** 2, 3))
+    lib().orc_square_neighborhoods(_p(F), ctypes.c_int(n), ctypes.c_double(eps), ctypes.c_double(cmpp), _p(out))
+    return out
+
+
 def export_patches(cam, img1, frames, eps=0.16, cmpp=0.25, mode=STRICT, image_points=False):
     img1 = np.ascontiguousarray(img1, dtype=np.uint8)
     h, w = img1.shape

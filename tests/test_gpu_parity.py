@@ -422,6 +422,27 @@ def test_features_frames_and_patches_bitwise(fm3d, orc, pair):
     assert (patches > 0).mean() > 0.5  # the patches see the textured scene
 
 
+def test_square_neighborhoods_bitwise(fm3d, orc, pair):
+    """computeSquareNeighborhoodsByNormals (main.cpp:187) on the GPU: every frame's 128x128 grid
+    bit-exact against the oracle, plus a non-rigid frame (the 1/w branch) and a small grid whose
+    point count is not a multiple of the block."""
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    normals = pts / np.linalg.norm(pts, axis=1, keepdims=True)
+    frames = orc.features_frames(pts[:50], normals[:50], orc.gravity([0.1, -0.2, 0.05])).reshape(-1, 16)
+    frames = np.concatenate([frames, [[1, 0.5, 0.25, 0.1, 0, 1, 0, 0.2, 0.3, 0, 1, 2.0, 0.01, -0.02, 0.5, 0.9]]])
+    for eps, cmpp in ((0.16, 0.25), (0.0151, 0.25)):
+        s = _settings(fm3d, pair.cam, neighEpsilon=eps, cmPerPixel=cmpp)
+        ctx = fm3d.Context(s)
+        try:
+            got = fm3d.NeighborhoodsGenerator(s).computeSquareNeighborhoodsByNormals(ctx, frames)
+        finally:
+            ctx.close()
+        ref = orc.square_neighborhoods(frames, eps, cmpp)
+        assert got.shape == ref.shape and got.shape[1] == orc.patch_size(eps, cmpp) ** 2
+        assert np.array_equal(got, ref), (eps, cmpp)
+
+
 # ---------------------------------------------------------------- BASELINE configs as parity cases
 def test_c2_sift10k_match_and_dlt(fm3d, orc, synth):
     """BASELINE configs[1] (C2): 10k SIFT-128 per frame, brute-force L2 match + NNDR + DLT --

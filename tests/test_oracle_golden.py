@@ -139,6 +139,30 @@ def test_features_frames_and_patches_vs_numpy(orc):
     assert np.abs(p2.astype(int) - patches.astype(int)).max() <= 1
 
 
+def test_square_neighborhoods_vs_numpy(orc):
+    """computeSquareNeighborhoodsByNormals (neighborhoodsgenerator.cpp:76-132): the oracle against
+    a numpy restatement with the same scalar operations (Matx44d * Vec4d summed from 0 in k order),
+    on the golden frames plus a non-rigid frame (w != 1: scaled by 1/w)."""
+    g = load("patches.npz")
+    frames = np.concatenate([g["frames"].reshape(-1, 16), [[1, 0.5, 0.25, 0.1, 0, 1, 0, 0.2, 0.3, 0, 1, 2.0,
+                                                              0.01, -0.02, 0.5, 0.9]]])
+    eps, cmpp = 0.016, 0.025
+    size = orc.patch_size(eps, cmpp)
+    out = orc.square_neighborhoods(frames, eps, cmpp)
+    assert out.shape == (len(frames), size * size, 3)
+    inc = cmpp * 0.01
+    i, j = np.meshgrid(np.arange(size), np.arange(size), indexing="ij")
+    v = [(-eps + inc * i.astype(np.float64)).ravel(), (-eps + inc * j.astype(np.float64)).ravel(),
+         np.zeros(size * size), np.ones(size * size)]
+    for p, F in enumerate(frames):
+        h = [(((0.0 + F[4 * r] * v[0]) + F[4 * r + 1] * v[1]) + F[4 * r + 2] * v[2]) + F[4 * r + 3] * v[3]
+             for r in range(4)]
+        a = np.where(h[3] != 1, 1.0 / h[3], 1.0)
+        ref = np.stack([np.where(h[3] != 1, h[k] * a, h[k]) for k in range(3)], axis=1)
+        assert np.array_equal(out[p], ref), p
+    assert not np.array_equal(out[-1][:, :3], out[-1][:, :3] * 0)  # the w != 1 frame produced points
+
+
 def test_reference_patch_size():
     """build/settings.yml (Neighborhoods epsilon 0.16, cmPerPixel 0.25) gives the 128x128 patches
     of the reference's results/*/patch_*.pgm (P5 128 128)."""
