@@ -14,7 +14,7 @@
 //                        of image 1, (uchar) bilinear sample, written transposed (patch.at(col, row));
 //   square_neighborhoods_kernel  NeighborhoodsGenerator::computeSquareNeighborhoodsByNormals
 //                        (neighborhoodsgenerator.cpp:76-132, main.cpp:187): the square grid through
-//                        every frame, 24 B written per point (HBM-bound).
+//                        every frame, 24 B written per point (HBM-bound, 5.3 TB/s).
 // Every output byte depends on one projected sample; the patch kernel is a projection + gather
 // bound by the fp64 VALU (≈60 fp64 ops per sample) -- there is no reduction and no data reuse
 // beyond the image in L2.
@@ -185,12 +185,10 @@ __global__ __launch_bounds__(kSqThreads) void square_neighborhoods_kernel(const 
     __shared__ double rec[kSqThreads * 3];
     const long long base = (long long)blockIdx.x * kSqThreads;
     const long long idx = base + threadIdx.x;
-    if (idx < total) {
-        const long long per = (long long)size * size;
-        const long long f = idx / per;
+    const long long per = (long long)size * size;
+    auto point = [&](const double* F, long long f) {
         const int ij = (int)(idx - f * per);
         const int i = ij / size, j = ij - (ij / size) * size;
-        const double* F = frames + 16 * f;
         const double v0 = -eps + inc * i, v1 = -eps + inc * j, v2 = 0, v3 = 1;
         double h[4];
 #pragma unroll
@@ -205,6 +203,14 @@ __global__ __launch_bounds__(kSqThreads) void square_neighborhoods_kernel(const 
         rec[3 * threadIdx.x] = h[0];
         rec[3 * threadIdx.x + 1] = h[1];
         rec[3 * threadIdx.x + 2] = h[2];
+    };
+    if (per % kSqThreads == 0) {
+        // the block lies inside one frame: its index is uniform, the 16 values come through scalar loads
+        const long long f = base / per;
+        if (idx < total) point(frames + 16 * f, f);
+    } else if (idx < total) {
+        const long long f = idx / per;
+        point(frames + 16 * f, f);
     }
     __syncthreads();
     const long long n = total - base < kSqThreads ? total - base : kSqThreads;  // points of this block
