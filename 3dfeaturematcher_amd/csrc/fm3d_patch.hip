@@ -154,9 +154,12 @@ __global__ __launch_bounds__(256) void patch_kernel(const double* __restrict__ R
                                                     int h, uint8_t* __restrict__ patches,
                                                     double* __restrict__ imagePoints) {
     const int p = blockIdx.y;
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;  // reference point i*size + j
-    if (p >= P || k >= size * size) return;
-    const int i = k / size, j = k - i * size;
+    // threads run over the patch bytes (row j, column i), so a wave's byte stores are contiguous;
+    // the reference point is i*size + j
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P || o >= size * size) return;
+    const int j = o / size, i = o - j * size;
+    const int k = i * size + j;
     const double* rt = RT + 12 * (size_t)p;
     const double R[9] = {rt[0], rt[1], rt[2], rt[3], rt[4], rt[5], rt[6], rt[7], rt[8]};
     const double t[3] = {rt[9], rt[10], rt[11]};
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256) void patch_kernel(const double* __restrict__ R
     }
     uint8_t val = 0;
     if (pixel_good(u, v, 1.0, w, h)) val = (uint8_t)bilinear(img, w, (float)u, (float)v);
-    patches[base + (size_t)j * size + i] = val;  // patch.at<uchar>(col, row), :842-846
+    patches[base + o] = val;  // o = j*size + i: patch.at<uchar>(col, row), :842-846
 }
 
 // computeSquareNeighborhoodByNormal (neighborhoodsgenerator.cpp:92-132) of every frame: point

@@ -1,4 +1,4 @@
-"""Times computeSquareNeighborhoodsByNormals on the GPU (build/settings.yml grid: 128 x 128 points
+"""Times computeSquareNeighborhoodsByNormals and the patch export on the GPU (build/settings.yml grid: 128 x 128 points
 per frame, 24 B written per point).  Run under rocprofv3 --kernel-trace --stats for the kernel's
 own time (the call itself includes the D2H copy of the host output buffer).
 
@@ -36,6 +36,18 @@ def main():
             dt = time.perf_counter() - t0
             print(f"frames {args.frames}: {out.shape[1]} points each, {out.nbytes / 1e6:.0f} MB, "
                   f"call {1e3 * dt:.1f} ms (incl. D2H)", flush=True)
+        # projectReferencePointsToImageWithFrames on a synthetic image (128x128 8-bit patches)
+        no = fm3d.NormalOptimizer(ctx)
+        img = rng.integers(0, 256, (480, 640), dtype=np.uint8)
+        no.setImages(img, img)
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        fr = frames.copy()
+        fr[:, :3, 3] = np.array([0.0, 0.0, 2.0]) + rng.normal(0, 0.3, (args.frames, 3))
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            patches = sct.projectReferencePointsToImageWithFrames(None, fr)
+            dt = time.perf_counter() - t0
+            print(f"patches {args.frames}: {patches.nbytes / 1e6:.0f} MB, call {1e3 * dt:.1f} ms", flush=True)
     finally:
         ctx.close()
 
