@@ -351,8 +351,14 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         HIPCHK(c, c->ctB.ensure((size_t)(nBPad + 1) * sizeof(int)));
         fm3d::launch_rowconst_u8(c->A.as<uint8_t>(), nA, nAPad, dimPad, c->cqA.as<int>(), c->stream);
         fm3d::launch_rowconst_u8(c->B.as<uint8_t>(), nB, nBPad, dimPad, c->ctB.as<int>(), c->stream);
+        const int parts = fm3d::knn2_u8_parts(nA, nB, c->nCU);
+        if (parts > 1) {
+            HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
+            HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
+        }
         fm3d::launch_knn2_u8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->cqA.as<int>(),
-                             c->ctB.as<int>(), c->idx.as<int>(), c->key.as<int>(), c->stream);
+                             c->ctB.as<int>(), parts, c->partIdx.as<int>(), c->partKey.as<int>(), c->idx.as<int>(),
+                             c->key.as<int>(), c->stream);
     } else if (type == FM3D_DESC_F32) {
         const int parts = (dimPad == 64 || dimPad == 128) ? fm3d::knn2_parts(nA, nB, dimPad, c->nCU) : 1;
         if (parts > 1) {

@@ -75,8 +75,10 @@ struct KnnOut {
 };
 
 // u8 rows (dim padded to a multiple of 128 with value 128 on both sides -> no effect)
-void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA,
-                    const int* ctB, int* idx, int* key, hipStream_t s);
+// u8 rows: `parts` train-tile ranges (knn2_u8_parts), merged through partIdx/partKey
+int knn2_u8_parts(int nA, int nB, int nCU);
+void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA, const int* ctB,
+                    int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s);
 void launch_rowconst_u8(const uint8_t* X, int n, int nPad, int dimPad, int* c, hipStream_t s);
 // f32 rows (dim 64 / 128): `parts` train ranges (knn2_parts), merged through partIdx/partKey (parts*nA*2 each)
 int knn2_parts(int nA, int nB, int dim, int nCU);

@@ -96,7 +96,8 @@ template <int KS>
 __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __restrict__ A, int nA,
                                                            const uint8_t* __restrict__ B, int nB, int dimPad,
                                                            const int* __restrict__ cqA, const int* __restrict__ ctB,
-                                                           int* __restrict__ idxOut, int* __restrict__ keyOut) {
+                                                           int tilesPerPart, int* __restrict__ idxOut,
+                                                           int* __restrict__ keyOut) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tileBytes = kT * (KS ? 32 * KS : dimPad);
     unsigned char* tiles = smem;                              // 2 x tileBytes
@@ -120,7 +121,9 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
         }
     }
     int b1 = INT_MAX, i1 = -1, b2 = INT_MAX, i2 = -1;
-    const int nTiles = (nB + kT - 1) / kT;
+    // train tiles of this part (blockIdx.y): [tBeg, tEnd); the parts' lists are merged by knn2_int_merge
+    const int tBeg = blockIdx.y * tilesPerPart;
+    const int tEnd = min((nB + kT - 1) / kT, tBeg + tilesPerPart);
 
     // train tiles: the global loads of tile t + 1 are issued into registers before tile t is
     // computed and written to LDS after it, so their latency overlaps the MFMA work
@@ -159,14 +162,14 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
         if (tid < kT) ctl[buf * kT + tid] = preCt;
     };
 
-    if (nTiles > 0) {
-        load_tile(0);
+    if (tBeg < tEnd) {
+        load_tile(tBeg);
         store_tile(0);
     }
     __syncthreads();
-    for (int t = 0; t < nTiles; t++) {
-        const int buf = t & 1;
-        if (t + 1 < nTiles) load_tile(t + 1);
+    for (int t = tBeg; t < tEnd; t++) {
+        const int buf = (t - tBeg) & 1;
+        if (t + 1 < tEnd) load_tile(t + 1);
         const unsigned char* tl = tiles + (size_t)buf * tileBytes;
         const int* ct = ctl + buf * kT;
 #pragma unroll
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
                 }
             }
         }
-        if (t + 1 < nTiles) store_tile(buf ^ 1);
+        if (t + 1 < tEnd) store_tile(buf ^ 1);
         __syncthreads();
     }
     // lanes l and l+32 hold the same query (different train rows): merge
@@ -214,10 +217,11 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     top2_merge(b1, i1, b2, i2, c1, j1, c2, j2);
     if (half == 0 && qrow < nA) {
         const int cq = cqA[qrow];
-        idxOut[2 * qrow] = i1;
-        idxOut[2 * qrow + 1] = i2;
-        keyOut[2 * qrow] = i1 >= 0 ? cq + b1 : INT_MAX;
-        keyOut[2 * qrow + 1] = i2 >= 0 ? cq + b2 : INT_MAX;
+        const size_t o = ((size_t)blockIdx.y * nA + qrow) * 2;
+        idxOut[o] = i1;
+        idxOut[o + 1] = i2;
+        keyOut[o] = i1 >= 0 ? cq + b1 : INT_MAX;
+        keyOut[o + 1] = i2 >= 0 ? cq + b2 : INT_MAX;
     }
 }
 
@@ -497,13 +501,18 @@ void launch_rowconst_u8(const uint8_t* X, int n, int nPad, int dimPad, int* c, h
 }
 
 void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA, const int* ctB,
-                    int* idx, int* key, hipStream_t s) {
+                    int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s) {
     if (nA <= 0) return;
     size_t lds = 2 * (size_t)kT * dimPad + 2 * kT * sizeof(int);
+    const int nTiles = (nB + kT - 1) / kT;
+    const int tilesPerPart = parts > 1 ? (nTiles + parts - 1) / parts : (nTiles > 0 ? nTiles : 1);
+    const dim3 g((nA + kQ - 1) / kQ, parts);
+    int* oi = parts > 1 ? partIdx : idx;
+    int* ok = parts > 1 ? partKey : key;
     auto go = [&](auto kernel) {
         if (lds > 65536)
             (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        kernel<<<(nA + kQ - 1) / kQ, kThreads, lds, s>>>(A, nA, B, nB, dimPad, cqA, ctB, idx, key);
+        kernel<<<g, kThreads, lds, s>>>(A, nA, B, nB, dimPad, cqA, ctB, tilesPerPart, oi, ok);
     };
     if (dimPad == 128)
         go(knn2_u8_kernel<4>);
@@ -511,6 +520,20 @@ void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
         go(knn2_u8_kernel<8>);
     else
         go(knn2_u8_kernel<0>);
+    if (parts > 1) knn2_int_merge<<<(nA + 255) / 256, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
+}
+
+int knn2_u8_parts(int nA, int nB, int nCU) {
+    // split the train tiles only when the query blocks alone leave CUs idle (at 100k queries the
+    // extra staging of more, shorter blocks costs more than the balance gains: 3.96 vs 3.57 ms);
+    // each part keeps >= 16 tiles (2048 rows)
+    const int nBlk = (nA + kQ - 1) / kQ;
+    const int nTiles = (nB + kT - 1) / kT;
+    if (nBlk <= 0 || nCU <= 0 || nBlk >= nCU) return 1;
+    int p = (nCU + nBlk - 1) / nBlk;
+    if (p > 8) p = 8;
+    while (p > 1 && nTiles / p < 16) p--;
+    return p;
 }
 
 int knn2_parts(int nA, int nB, int dim, int nCU) {
