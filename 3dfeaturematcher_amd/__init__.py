@@ -28,7 +28,7 @@ ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, 
 
 # every symbol include/fm3d.h declares (tests check the library exports all of them)
 EXPORTS = (
-    "fm3d_settings_default", "fm3d_settings_load", "fm3d_ctx_create", "fm3d_ctx_destroy", "fm3d_last_error",
+    "fm3d_settings_default", "fm3d_settings_load", "fm3d_settings_lookup", "fm3d_ctx_create", "fm3d_ctx_destroy", "fm3d_last_error",
     "fm3d_ctx_set_stream", "fm3d_knn2", "fm3d_match_nndr", "fm3d_setg12", "fm3d_g12_from_poses",
     "fm3d_camera2_from_g12", "fm3d_set_g12", "fm3d_get_camera2", "fm3d_triangulate", "fm3d_set_images",
     "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",

@@ -293,7 +293,8 @@ int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB,
                       int* effType, int* dimPad) {
     if (dim <= 0 || nA < 0 || nB < 0) return fail(c, FM3D_ERR_INVALID, "bad descriptor shape");
     int t = type;
-    if (type == FM3D_DESC_F32 && f32_is_u8((const float*)descA, (size_t)nA * dim) &&
+    // integer-valued f32 rows take the u8 kernel only where it supports the width (padded <= 256)
+    if (type == FM3D_DESC_F32 && ((dim + 127) / 128) * 128 <= 256 && f32_is_u8((const float*)descA, (size_t)nA * dim) &&
         f32_is_u8((const float*)descB, (size_t)nB * dim))
         t = FM3D_DESC_U8;  // integer-valued rows: exact, identical ranking and distances
     if (t == FM3D_DESC_U8) {
@@ -506,17 +507,18 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         int dev = 0, khz = 0;
         HIPCHK(c, hipGetDevice(&dev));
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
-        const char* ms = getenv("FM3D_LM_MAX_SECONDS");  // watchdog (tests lower it)
-        const long long secs = ms && atoll(ms) > 0 ? atoll(ms) : 300;
-        p.maxTicks = (long long)khz * 1000 * secs;
+        const char* ms = getenv("FM3D_LM_MAX_SECONDS");  // watchdog (tests lower it; fractions allowed)
+        const double secs = ms && atof(ms) > 0 ? atof(ms) : 300.;
+        p.maxTicks = (long long)((double)khz * 1000. * secs);
         c->wallKhz = khz;
         const char* co = getenv("FM3D_LM_COOP");  // A/B switch for the tail help
         p.coop = co ? atoi(co) : 1;
     }
+    // the counters (incl. the overflow word) are reset for every call, also for P == 0
+    HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 256, c->stream));
     if (P > 0) {
         HIPCHK(c, hipEventRecord(e0, c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64 * sizeof(int), c->stream));
-        HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 256, c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmStat.as<unsigned long long>() + 20, 0xff, 8, c->stream));  // min start
         HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->lmStatus.p, fm3d::kLMRunning, P, c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmInfo.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
@@ -805,7 +807,7 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
         HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    int overflow = 0;
+    int overflow = 0;  // lmStat is reset by run_lm for every call (P == 0 included)
     HIPCHK(c, hipMemcpy(&overflow, c->lmStat.as<unsigned long long>() + 2, sizeof(int), hipMemcpyDeviceToHost));
     if (overflow) return fail(c, FM3D_ERR_HIP, "LM kernel iteration guard tripped (internal error)");
     float ms = 0.f;
@@ -938,6 +940,15 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
     HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    // the LM watchdog (maxIter / FM3D_LM_MAX_SECONDS) leaves points in kLMRunning: an error, not drops
+    if (cnt[2]) return fail(c, FM3D_ERR_HIP, "LM kernel iteration guard tripped (internal error)");
+    if (c->s.strictNanExit && P > 0) {  // reference exit(-6) on a NaN plane hit (:465-469)
+        std::vector<int> st(P);
+        HIPCHK(c, hipMemcpy(st.data(), c->lmStatus.p, (size_t)P * sizeof(int), hipMemcpyDeviceToHost));
+        for (int i = 0; i < P; i++)
+            if (st[i] == FM3D_ST_NAN_PLANE)
+                return fail(c, FM3D_ERR_NAN_PLANE, "projectPointToPlane hit NaN (reference: exit(-6))");
+    }
     if (nKept) *nKept = kept;
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));

@@ -1246,7 +1246,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     } else {
         chain_wave(lane, tStart, p.maxTicks, p.statPass + 2);
     }
-    if (tid == 0) {
+    // the group's lifetime: the chain wave leaves last (once every slot is done)
+    if (wave == kW && lane == 0) {
         atomicAdd(p.statPass + 4, clock64() - cyStart);
         const unsigned long long wt = wall_clock64() - tStart;
         atomicAdd(p.statPass + 5, wt);

@@ -4,6 +4,7 @@
 // (main.cpp:62-98, singlecameratriangulator.cpp:45-112, normaloptimizer.cpp:154-164).
 // This parser accepts the subset that file uses: "%YAML:1.0" header, nested maps by
 // indentation, scalars, flow sequences "[a, b, c]", '#' comments.
+#include <algorithm>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -160,5 +161,20 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
     get_i(kv, "Fm3d.boundHeight", &s->boundHeight);
     get_i(kv, "Fm3d.strictNanExit", &s->strictNanExit);
     get_i(kv, "Fm3d.lmWaves", &s->lmWaves);
+    return FM3D_OK;
+}
+
+extern "C" int fm3d_settings_lookup(const char* path, const char* key, char* out, int cap, int* len) {
+    if (!path || !key || !len || cap < 0 || (cap > 0 && !out)) return FM3D_ERR_INVALID;
+    std::map<std::string, std::string> kv;
+    if (!parse_yaml(path, kv)) return FM3D_ERR_PARSE;
+    auto it = kv.find(key);
+    if (it == kv.end()) return FM3D_ERR_INVALID;
+    *len = (int)it->second.size();
+    if (cap > 0) {
+        const size_t n = std::min((size_t)cap - 1, it->second.size());
+        std::memcpy(out, it->second.data(), n);
+        out[n] = 0;
+    }
     return FM3D_OK;
 }

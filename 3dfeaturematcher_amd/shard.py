@@ -7,8 +7,9 @@ splits into contiguous query blocks, one per rank:
   rank r takes queries [lo_r, hi_r) of frame A against ALL of frame B, runs the
   whole path on its device (fm3d_pipeline_upload with queryOffset = lo_r, so
   queryIdx stays global), and the per-rank survivor records are all-gathered
-  (count first, then fixed-capacity 64-byte records) and concatenated in rank
-  order.
+  (count first, then fixed-capacity 64-byte records, all_gather_device) and
+  concatenated in rank order (merge_gathered).  bench.py --gpus N runs exactly
+  this on one 1M-keypoint frame pair (C5) with the record buffers on the GPUs.
 
 Rank order x query order inside a shard == query order, so the merged list is
 byte-identical to the single-GPU run.  The collective is torch.distributed's
@@ -35,6 +36,41 @@ def partition(n: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def shard_capacity(n: int, world: int) -> int:
+    """Records per rank buffer: the largest block's query count (>= 1)."""
+    return max(1, max(hi - lo for lo, hi in (partition(n, world, r) for r in range(world))))
+
+
+def all_gather_device(rec_buf, n_kept: int, group=None):
+    """The collective of one step: every rank's survivor count, then its fixed-capacity
+    record buffer (rec_buf: (capacity, 64) uint8 tensor, records [0, n_kept) valid), all-
+    gathered with all_gather_into_tensor (RCCL over xGMI for cuda tensors, gloo on CPU).
+    Returns (gathered (world, capacity, 64) uint8, counts (world,) int32), on rec_buf's device."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    mine = torch.tensor([n_kept], dtype=torch.int32, device=rec_buf.device)
+    counts = torch.empty(world, dtype=torch.int32, device=rec_buf.device)
+    dist.all_gather_into_tensor(counts, mine, group=group)
+    gathered = torch.empty((world,) + tuple(rec_buf.shape), dtype=torch.uint8, device=rec_buf.device)
+    dist.all_gather_into_tensor(gathered.view(-1), rec_buf.reshape(-1), group=group)
+    return gathered, counts
+
+
+def merge_gathered(gathered, counts) -> np.ndarray:
+    """Rank-order concatenation of the valid records of every rank's buffer: the single-
+    device record list (rank order x query order inside a shard == query order)."""
+    rec_dtype = importlib.import_module("3dfeaturematcher_amd").RECORD
+    g = np.ascontiguousarray(gathered.cpu().numpy() if hasattr(gathered, "cpu") else gathered, dtype=np.uint8)
+    c = np.asarray(counts.cpu().numpy() if hasattr(counts, "cpu") else counts).astype(np.int64)
+    cap = g.shape[1]
+    if g.ndim != 3 or g.shape[2] != RECORD_BYTES or (c < 0).any() or (c > cap).any():
+        raise ValueError("gathered record buffers of an unexpected shape or count")
+    parts = [g[r, : c[r]].reshape(-1).view(rec_dtype) for r in range(g.shape[0])]
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=rec_dtype)
+
+
 def gather_records(records: np.ndarray, capacity: int, group=None, device=None) -> np.ndarray:
     """All-gather every rank's survivor records (fm3d RECORD dtype) and merge them in
     rank order.  `capacity` = the largest shard's query count (fixed-size buffers)."""
@@ -46,21 +82,13 @@ def gather_records(records: np.ndarray, capacity: int, group=None, device=None) 
     n = len(records)
     if n > capacity:
         raise ValueError("more records than the shard capacity")
-    buf = np.zeros(capacity * RECORD_BYTES, dtype=np.uint8)
-    buf[: n * RECORD_BYTES] = np.ascontiguousarray(records, dtype=rec_dtype).view(np.uint8)
+    buf = np.zeros((capacity, RECORD_BYTES), dtype=np.uint8)
+    buf[:n] = np.ascontiguousarray(records, dtype=rec_dtype).view(np.uint8).reshape(n, RECORD_BYTES)
     mine = torch.from_numpy(buf)
-    cnt = torch.tensor([n], dtype=torch.int64)
     if device is not None:
-        mine, cnt = mine.to(device), cnt.to(device)
-    counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    parts = [torch.zeros_like(mine) for _ in range(world)]
-    dist.all_gather(parts, mine, group=group)
-    out = []
-    for c, p in zip(counts, parts):
-        k = int(c.item())
-        out.append(p.cpu().numpy()[: k * RECORD_BYTES].view(rec_dtype))
-    return np.concatenate(out) if out else np.zeros(0, dtype=rec_dtype)
+        mine = mine.to(device)
+    gathered, counts = all_gather_device(mine, n, group=group)
+    return merge_gathered(gathered, counts)
 
 
 def run_shard(pair, settings, lo: int, hi: int, device: int = 0) -> np.ndarray:
@@ -89,7 +117,6 @@ def run_sharded(pair, settings, group=None, device=None,
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     n = len(pair.desc1)
     lo, hi = partition(n, world, rank)
-    cap = max(partition(n, world, r)[1] - partition(n, world, r)[0] for r in range(world))
     fn = shard_fn or (lambda p, s, a, b: run_shard(p, s, a, b, device=device.index if device is not None else 0))
     rec = fn(pair, settings, lo, hi)
-    return gather_records(rec, max(cap, 1), group=group, device=device)
+    return gather_records(rec, shard_capacity(n, world), group=group, device=device)

@@ -1,23 +1,35 @@
 """bench.py -- headline benchmark of the 3DFeatureMatcher hot path on MI355X.
 
 Metric (BASELINE.json): matched + triangulated + normal-optimised keypoints/s.
-Workload (BASELINE.json configs[3], "C4"): 100k SIFT-128 keypoints per 640x480
-frame pair, full pipeline (exact brute-force match + NNDR -> DLT triangulation ->
-LM normal refinement with pixelsRay 64 over 3+1 pyramid levels), synthetic data
-(3dfeaturematcher_amd/synth.py).  One step = one frame pair through the whole
-path with its inputs already resident in HBM.
 
-Multi-GPU (one process per GPU, launched by torch.distributed.run): every rank
-processes its own frame pair (weak scaling) and the per-rank survivor records
-(queryIdx, trainIdx, distance, 3D point, normal) are all-gathered over RCCL.
-value = keypoints kept by all ranks / max-over-ranks time.
+Workloads (BASELINE.json configs):
+  * C4 (configs[3], the default at one GPU): 100k SIFT-128 keypoints per 640x480 frame
+    pair, full pipeline (exact brute-force match + NNDR -> DLT triangulation -> LM normal
+    refinement with pixelsRay 64 over 3+1 pyramid levels).
+  * C5 (configs[4], the default at N > 1 GPUs): ONE 1M-keypoint frame pair (the C4 scene and
+    settings, 1M sub-pixel keypoints per 640x480 frame), sharded over the N
+    ranks: rank r takes the contiguous query block shard.partition(1M, N, r)
+    against all of frame B (replicated), runs the whole path on its GPU, and the per-rank
+    survivor records (queryIdx, trainIdx, distance, 3D point, normal) are all-gathered over
+    RCCL (counts, then fixed-capacity record buffers) every step.  value = kept keypoints of
+    the frame pair / max-over-ranks time (strong scaling).  After the timed steps rank 0 runs
+    the same frame pair unsharded on its GPU and checks that the rank-order merge of the
+    gathered records is byte-identical to it.
+  * --weak: the round-1 mode, every rank its own C4 frame pair (weak scaling), labelled weak.
 
-Rank 0 at N=1 also times the CPU oracle (the reference algorithm restated in C,
-OpenMP over queries/points) on a bounded sample and extrapolates (cpu_baseline).
+One step = one frame pair (or one shard of it) through the path with its inputs already
+resident in HBM: descriptors, keypoints and the image pyramids are uploaded / built before
+the timed region (upload_ms in the line), the survivor records stay in HBM (or go to the
+all-gather).  Synthetic data: 3dfeaturematcher_amd/synth.py (seeded ray-cast facet scene).
+
+Rank 0 at N=1 also times the CPU oracle (the reference algorithm restated in C, OpenMP over
+queries/points, on every CPU the process may run on) on a bounded sample and extrapolates
+(cpu_baseline).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import importlib
 import json
 import os
@@ -30,9 +42,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "matched+triangulated+normal-optimised keypoints/sec; HBM GB/s vs roofline"
-FLOPS_PER_PIXEL_EVAL = 91   # restated evaluateNormal per pixel (DESIGN.md §Measurement)
-FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 (vector == matrix) peak
+FLOPS_PER_PIXEL_EVAL = 91   # restated evaluateNormal per pixel (DESIGN.md §3.4)
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector peak, an FMA counted as 2 flops
+FP64_PEAK_NO_FMA = 39.3     # the same issue rate for 1-flop instructions (-ffp-contract=off: no FMA)
 HBM_PEAK_GBS = 8000.0
+WORKLOADS = {"c4": dict(keypoints=100_000, width=640, height=480),
+             "c5": dict(keypoints=1_000_000, width=640, height=480)}
 
 
 def parse():
@@ -40,19 +55,27 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--keypoints", type=int, default=100_000)
+    ap.add_argument("--workload", choices=("auto", "c4", "c5"), default="auto",
+                    help="auto: C4 at one GPU, C5 (one sharded 1M-keypoint frame pair) at N > 1")
+    ap.add_argument("--weak", action="store_true", help="every rank its own C4 frame pair (weak scaling)")
+    ap.add_argument("--keypoints", type=int, default=0)
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--ray", type=int, default=64)
     ap.add_argument("--levels", type=int, default=3)
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--lm-waves", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the C5 byte-identity check against one GPU")
     ap.add_argument("--out", type=str, default="")
-    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "r01_pmc_c4_final.json"),
+    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "r02_pmc_c4.json"),
                     help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()
+
+
+def records_digest(rec_bytes: bytes) -> str:
+    return hashlib.sha256(rec_bytes).hexdigest()[:16]
 
 
 def main():
@@ -60,7 +83,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    workload = args.workload
+    if workload == "auto":
+        workload = "c5" if world > 1 and not args.weak else "c4"
+    if args.weak:
+        workload = "c4"
+    wl = dict(WORKLOADS[workload])
+    for k in ("keypoints", "width", "height"):
+        if getattr(args, k):
+            wl[k] = getattr(args, k)
+    sharded = not args.weak and world > 1
+    dist = torch = None
     if world > 1:
         import torch
         import torch.distributed as tdist
@@ -70,43 +103,44 @@ def main():
 
     fm3d = importlib.import_module("3dfeaturematcher_amd")
     synth = importlib.import_module("3dfeaturematcher_amd.synth")
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
 
     t_gen = time.time()
-    pair = synth.make_frame_pair(args.keypoints, args.width, args.height, seed=args.seed + 1000 * rank)
+    seed = args.seed + (1000 * rank if args.weak else 0)
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=seed)
     t_gen = time.time() - t_gen
     s = fm3d.Settings.default()
     s.set_camera(pair.cam)
     s.pixelsRay = args.ray
     s.pyramids = args.levels
     s.lmWaves = args.lm_waves
+    n = len(pair.desc1)
+    lo, hi = shard.partition(n, world, rank) if sharded else (0, n)
     ctx = fm3d.Context(s, device=local if world > 1 else 0)
     sct = fm3d.SingleCameraTriangulator(ctx)
     sct.set_g12(pair.g12)
     pipe = fm3d.Pipeline(ctx)
-    pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+    t_up = time.perf_counter()
+    pipe.upload(pair.desc1[lo:hi], pair.desc2, pair.kp1[lo:hi], pair.kp2, pair.img1, pair.img2, query_offset=lo)
+    upload_ms = (time.perf_counter() - t_up) * 1e3
 
     rec_buf = None
     if dist is not None:
-        import torch
-        rec_buf = torch.empty((args.keypoints, 64), dtype=torch.uint8, device=f"cuda:{local}")
-        gathered = torch.empty((world, args.keypoints, 64), dtype=torch.uint8, device=f"cuda:{local}")
-        counts = torch.zeros(world, dtype=torch.int32, device=f"cuda:{local}")
+        cap = shard.shard_capacity(n, world) if sharded else n
+        rec_buf = torch.empty((cap, shard.RECORD_BYTES), dtype=torch.uint8, device=f"cuda:{local}")
+    last = {}
 
     def step():
-        n, st = pipe.run(rec_buf.data_ptr() if rec_buf is not None else None)
+        k, st = pipe.run(rec_buf.data_ptr() if rec_buf is not None else None)
         if dist is not None:
-            import torch
-            mine = torch.tensor([n], dtype=torch.int32, device=rec_buf.device)
-            dist.all_gather_into_tensor(counts, mine)
-            dist.all_gather_into_tensor(gathered.view(-1), rec_buf.view(-1))
-        return n, st
+            last["gathered"], last["counts"] = shard.all_gather_device(rec_buf, k)
+        return k, st
 
     for _ in range(args.warmup):
         step()
 
     def sync():
         if dist is not None:
-            import torch
             torch.cuda.synchronize()
             dist.barrier()
             torch.cuda.synchronize()
@@ -116,34 +150,51 @@ def main():
     kept_total = 0
     stats = []
     for _ in range(args.steps):
-        n, st = step()
-        kept_total += n
+        k, st = step()
+        kept_total += k
         stats.append(st)
     sync()
     elapsed = time.perf_counter() - t0
 
     all_kept = kept_total
     if dist is not None:
-        import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=rec_buf.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        k = torch.tensor([kept_total], dtype=torch.int64, device=rec_buf.device)
-        dist.all_reduce(k, op=dist.ReduceOp.SUM)
-        all_kept = int(k.item())
+        kk = torch.tensor([kept_total], dtype=torch.int64, device=rec_buf.device)
+        dist.all_reduce(kk, op=dist.ReduceOp.SUM)
+        all_kept = int(kk.item())
+
+    # D2H of the survivor records (outside the timed region; reported beside it)
+    t_dl = time.perf_counter()
+    if dist is None:
+        mine = pipe.records(stats[-1]["kept"])
+    else:
+        merged = shard.merge_gathered(last["gathered"], last["counts"])
+    download_ms = (time.perf_counter() - t_dl) * 1e3
+
+    check = None
+    if sharded:
+        check = check_against_one_gpu(args, fm3d, pair, s, merged, local, rank, dist, torch)
 
     lm_ms = float(np.mean([st["lm_ms"] for st in stats]))
-    traffic = pmc_traffic(args)
     pix = float(np.mean([st["lm"]["pixel_evaluations"] for st in stats]))
     evals = float(np.mean([st["lm"]["evaluations"] for st in stats]))
-    last = stats[-1]
-    achieved_tflops = FLOPS_PER_PIXEL_EVAL * pix / (lm_ms * 1e-3) / 1e12 if lm_ms > 0 else 0.0
-
+    last_st = stats[-1]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(pair, s, last, args)
+        cpu = cpu_baseline(pair, s, last_st, args)
 
     if rank == 0:
+        kp_k = wl["keypoints"] // 1000
+        if workload == "c5":
+            desc = (f"C5: one {kp_k}k-keypoint SIFT-128 (u8) 640x480-class frame pair ({wl['width']}x{wl['height']}), "
+                    f"full pipeline, pixelsRay {args.ray}, pyramids {args.levels}, query blocks sharded over "
+                    f"{world} GPU(s), RCCL all-gather of survivor records")
+        else:
+            desc = (f"C4: {kp_k}k SIFT-128 (u8) keypoints per {wl['width']}x{wl['height']} frame pair, full "
+                    f"pipeline, pixelsRay {args.ray}, pyramids {args.levels}")
+        frame_s = elapsed / args.steps
         out = {
             "metric": METRIC,
             "value": all_kept / elapsed,
@@ -151,40 +202,35 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": frame_s * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (ray-cast facet scene, seeded; 3dfeaturematcher_amd/synth.py)",
             "config": {
-                "workload": f"C4: {args.keypoints // 1000}k SIFT-128 (u8) keypoints per {args.width}x{args.height} "
-                            f"frame pair, full pipeline, pixelsRay {args.ray}, pyramids {args.levels}",
-                "keypoints_per_frame": args.keypoints, "pixelsRay": args.ray, "pyramids": args.levels,
-                "parallelism": f"dp{world}: one frame pair per rank, RCCL all-gather of survivor records",
+                "workload": desc,
+                "keypoints_per_frame": wl["keypoints"], "width": wl["width"], "height": wl["height"],
+                "pixelsRay": args.ray, "pyramids": args.levels,
+                "parallelism": (f"dp{world}: contiguous query blocks of one frame pair, frame B replicated, "
+                                f"RCCL all-gather of counts + 64-B survivor records each step") if sharded else
+                               (f"dp{world}: one frame pair per rank (weak)" if world > 1 else "1 GPU"),
+                "timed": ("match -> NNDR -> DLT -> LM -> survivor records on HBM-resident inputs (descriptors, "
+                          "keypoints, image pyramids uploaded/built before the timed region: upload_ms; record "
+                          "D2H after it: download_ms)"),
             },
-            "roofline": {
-                "kernel": "fm3d::lm2_kernel (LM normal refinement)",
-                "bound": "mfma",
-                "compute": "fp64 (issued on the VALU; MI355X fp64 matrix and vector peaks coincide at 78.6 TFLOP/s)",
-                "achieved": achieved_tflops,
-                "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved_tflops / FP64_PEAK_TFLOPS,
-                "traffic": traffic["bytes"] if traffic else None,
-                "traffic_unit": "bytes per launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-                "traffic_GBps": traffic["bytes"] / (lm_ms * 1e6) if traffic and lm_ms > 0 else None,
-                "traffic_source": traffic["source"] if traffic else None,
-                "algorithmic": f"{FLOPS_PER_PIXEL_EVAL} flop per pixel evaluation x {pix:.4g} pixel evaluations "
-                               f"({evals:.4g} residual evaluations) per launch",
-                "avg_launch_ms": lm_ms,
-            },
+            "upload_ms": upload_ms,
+            "download_ms": download_ms,
+            "pcie_inclusive_value": all_kept / args.steps / (frame_s + (upload_ms + download_ms) * 1e-3),
+            "roofline": roofline(stats, lm_ms, pix, evals, args, pair, s),
             "cpu_baseline": cpu,
-            "stages_ms": {k: last[k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "lm_ms", "total_ms")},
-            "counts": {k: last[k] for k in ("queries", "matches", "inliers", "kept")},
-            "lm_profile": lm_profile(last["lm"]),
+            "stages_ms": {k: last_st[k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "lm_ms", "total_ms")},
+            "counts": {k: last_st[k] for k in ("queries", "matches", "inliers", "kept")},
+            "lm_profile": lm_profile(last_st["lm"]),
             "setup_s": {"synthetic_generation": round(t_gen, 2)},
         }
+        if check is not None:
+            out["sharding_check"] = check
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:
@@ -192,7 +238,39 @@ def main():
                 f.write(line + "\n")
     ctx.close()
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def check_against_one_gpu(args, fm3d, pair, s, merged, local, rank, dist, torch):
+    """Rank 0: the unsharded frame pair on its own GPU (one run, untimed by the metric), byte
+    for byte against the rank-order merge of the last step's gathered records."""
+    res = None
+    if rank == 0 and not args.no_check:
+        ctx = fm3d.Context(s, device=local)
+        try:
+            sct = fm3d.SingleCameraTriangulator(ctx)
+            sct.set_g12(pair.g12)
+            pipe = fm3d.Pipeline(ctx)
+            pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+            t = time.perf_counter()
+            k, st = pipe.run()
+            one_s = time.perf_counter() - t
+            full = pipe.records(k)
+        finally:
+            ctx.close()
+        same = full.tobytes() == merged.tobytes()
+        res = {"identical_to_1gpu": bool(same), "records": int(len(merged)),
+               "digest_sharded": records_digest(merged.tobytes()), "digest_1gpu": records_digest(full.tobytes()),
+               "one_gpu_run": {"ms": one_s * 1e3, "kept_per_s": k / one_s,
+                               "note": "the same frame pair unsharded on rank 0's GPU, one run after the timed "
+                                       "steps (no warmup of its own)"}}
+    ok = torch.tensor([0 if (res is not None and not res["identical_to_1gpu"]) else 1], dtype=torch.int32,
+                      device=f"cuda:{local}")
+    dist.broadcast(ok, 0)
+    if not int(ok.item()):
+        raise SystemExit("sharded records differ from the single-GPU run")
+    return res
 
 
 def pmc_traffic(args):
@@ -204,20 +282,59 @@ def pmc_traffic(args):
     except (OSError, ValueError):
         return None
     w = d.get("workload", {})
-    if (w.get("keypoints"), w.get("ray"), w.get("levels")) != (args.keypoints, args.ray, args.levels):
+    if (w.get("keypoints"), w.get("ray"), w.get("levels")) != (args.keypoints or 100_000, args.ray, args.levels):
         return None
-    return {"bytes": d["hbm_bytes_per_launch"], "source": os.path.relpath(args.pmc_json, ROOT)}
+    return {"bytes": d["hbm_bytes_per_launch"], "source": os.path.relpath(args.pmc_json, ROOT),
+            "calibration": d.get("calibration")}
+
+
+def roofline(stats, lm_ms, pix, evals, args, pair, s):
+    """The dominant kernel (lm2_kernel) against its fp64 issue ceiling; HBM traffic beside it."""
+    traffic = pmc_traffic(args)
+    achieved = FLOPS_PER_PIXEL_EVAL * pix / (lm_ms * 1e-3) / 1e12 if lm_ms > 0 else 0.0
+    inliers = float(np.mean([st["inliers"] for st in stats]))
+    pyr = 0
+    w, h = pair.img1.shape[1], pair.img1.shape[0]
+    for _ in range(args.levels + 1):
+        pyr += w * h
+        w, h = (w + 1) // 2, (h + 1) // 2
+    alg_bytes = inliers * (24 + 24 + 4) + 2 * pyr  # point in, normal out, status; both pyramids once
+    r = {
+        "kernel": "fm3d::lm2_kernel (LM normal refinement)",
+        "bound": "fp64-valu",
+        "compute": "fp64 VALU (no MFMA); -ffp-contract=off, so every flop is its own instruction",
+        "achieved": achieved,
+        "peak": FP64_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": achieved / FP64_PEAK_TFLOPS,
+        "peak_no_fma": FP64_PEAK_NO_FMA,
+        "frac_no_fma": achieved / FP64_PEAK_NO_FMA,
+        "traffic": traffic["bytes"] if traffic else None,
+        "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes)",
+        "traffic_source": traffic["source"] if traffic else None,
+        "traffic_calibration": traffic["calibration"] if traffic else None,
+        "traffic_per_pixel_eval": traffic["bytes"] / pix if traffic and pix else None,
+        "algorithmic_bytes": alg_bytes,
+        "traffic_over_algorithmic": traffic["bytes"] / alg_bytes if traffic else None,
+        "traffic_GBps": traffic["bytes"] / (lm_ms * 1e6) if traffic and lm_ms > 0 else None,
+        "algorithmic": f"{FLOPS_PER_PIXEL_EVAL} flop per pixel evaluation x {pix:.4g} pixel evaluations "
+                       f"({evals:.4g} residual evaluations) per launch; bytes: {inliers:.0f} points x 52 B + "
+                       f"2 pyramids of {pyr} B",
+        "avg_launch_ms": lm_ms,
+    }
+    return r
 
 
 def lm_profile(lm):
-    """Where the LM kernel's time goes (in-kernel clock counters, fm3d_lm_stats)."""
+    """Where the LM kernel's time goes (in-kernel clock counters, fm3d_lm_stats).  Per-group
+    lifetimes are the chain wave's (it leaves last)."""
     tot = lm["cycles_total"]
     return {
         "groups": lm["groups"], "passes": lm["passes"],
         "chain_busy": lm["cycles_chain"] / tot if tot else None,    # chain wave adding / group lifetime
         "control_over_terms": lm["cycles_control"] / max(lm["cycles_terms"], 1),  # lmdif bookkeeping
         "wait_over_terms": lm["cycles_wait"] / max(lm["cycles_terms"], 1),        # term waves waiting on the chain
-        # mean number of term waves inside a pass over the lifetime of a workgroup's first wave
+        # mean number of term waves inside a pass over the group lifetime
         "busy_slots_per_group": lm["cycles_terms"] / tot if tot else None,
         "group_life_mean_over_max": lm["wall_ticks_sum"] / max(lm["groups"], 1) / max(lm["wall_ticks_max"], 1),
         "clock_ghz": lm["cycles_total"] / max(lm["wall_ticks_sum"], 1) * lm["wall_clock_khz"] * 1e-6,
@@ -239,12 +356,28 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_quota():
+    """CPUs the cgroup grants this process (cpu.max), None if unlimited / unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(pair, s, gpu_stats, args):
     """Time the CPU oracle (reference algorithm, C + OpenMP) on a bounded sample of the
-    same workload and extrapolate to the full frame pair."""
+    same workload, on every CPU this process may run on, and extrapolate to the frame pair."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    # every CPU the process may run on: its affinity set, capped by the cgroup quota (on the GPU
+    # box 256 CPUs are visible and 16 granted; 256 threads on a 16-CPU quota run slower)
+    quota = cpu_quota()
+    threads = len(os.sched_getaffinity(0))
+    if quota:
+        threads = max(1, min(threads, int(quota)))
+    threads = int(os.environ.get("FM3D_CPU_THREADS", "0") or 0) or threads
     budget = args.cpu_budget_s
     nA = len(pair.desc1)
     # match: sample of queries against the full train set
@@ -257,21 +390,20 @@ def cpu_baseline(pair, s, gpu_stats, args):
             break
         qs = min(nA, qs * 4)
     t_match = dt / qs * nA
-    # triangulation on the GPU's matches (full set)
+    # triangulation on the oracle's matches of a query sample
     q, tr, _ = orc.match_nndr(pair.desc1[:2000], pair.desc2, orc.U8, s.nndrEpsilon, threads)
     t = time.perf_counter()
     pts, _ = orc.triangulate(pair.cam, pair.g12, s.zThresholdMin, s.zThresholdMax, pair.kp1, pair.kp2, q, tr)
     t_tri = (time.perf_counter() - t) / max(len(q), 1) * gpu_stats["matches"]
-    # LM normals: sample of points
+    # LM normals: a seeded random subset (per-point LM cost varies by orders of magnitude), 16
+    # points per thread so the dynamic schedule balances
     fm3d = importlib.import_module("3dfeaturematcher_amd")
     R2, t2 = fm3d.camera2_from_g12(pair.g12)
-    # a seeded random subset (per-point LM cost varies by orders of magnitude), 16 points per
-    # thread so the dynamic schedule balances
     sub = np.random.default_rng(7).permutation(len(pts))
     npts = min(len(pts), 16 * threads)
     t = time.perf_counter()
-    r = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts[sub[:npts]], s.pixelsRay,
-                             mode=orc.STRICT, nthreads=threads)
+    orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts[sub[:npts]], s.pixelsRay,
+                         mode=orc.STRICT, nthreads=threads)
     dt = time.perf_counter() - t
     t_lm = dt / npts * gpu_stats["inliers"]
     total = t_match + t_tri + t_lm
@@ -289,15 +421,19 @@ def cpu_baseline(pair, s, gpu_stats, args):
         "value": gpu_stats["kept"] / total,
         "unit": "keypoints/s",
         "cores": threads,
+        "nproc": os.cpu_count(),
+        "cpu_quota_cores": cpu_quota(),
         "kind": "port",
         "cpu_model": cpu_model(),
         "single_thread": {"value": gpu_stats["kept"] / total1, "unit": "keypoints/s", "cores": 1,
                           "sample": f"knn2 of 256 queries, LM normals of {n1} points, 1 thread (est. {total1:.0f} s "
                                     f"per frame pair: match {t1_match:.1f}, LM {t1_lm:.1f})"},
-        "sample": f"oracle (C, OpenMP {threads} threads): knn2 of {qs} queries x {len(pair.desc2)} train, "
-                  f"DLT of {len(q)} matches, LM normals of {npts} random points (pixelsRay {s.pixelsRay}); "
-                  f"extrapolated to {nA} queries / {gpu_stats['matches']} matches / {gpu_stats['inliers']} points "
-                  f"(est. {total:.1f} s per frame pair: match {t_match:.1f}, DLT {t_tri:.3f}, LM {t_lm:.1f})",
+        "affinity_cpus": len(os.sched_getaffinity(0)),
+        "sample": f"oracle (C, OpenMP {threads} threads = the CPUs granted to the process): knn2 of {qs} queries x "
+                  f"{len(pair.desc2)} train, DLT of {len(q)} matches, LM normals of {npts} random points "
+                  f"(pixelsRay {s.pixelsRay}); extrapolated to {nA} queries / {gpu_stats['matches']} matches / "
+                  f"{gpu_stats['inliers']} points (est. {total:.1f} s per frame pair: match {t_match:.1f}, "
+                  f"DLT {t_tri:.3f}, LM {t_lm:.1f})",
     }
 
 

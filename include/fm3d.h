@@ -131,6 +131,11 @@ typedef struct fm3d_pipeline_stats {
 int fm3d_settings_default(fm3d_settings *s);
 /* read a %YAML:1.0 cv::FileStorage file (the subset settings.yml uses) */
 int fm3d_settings_load(const char *path, fm3d_settings *s);
+/* cv::FileStorage node lookup (fs["IMAGES"]["img1"] >> ..., main.cpp:74-98): the raw text of the
+   dotted key "IMAGES.img1" in a %YAML:1.0 file -- a scalar or a flow sequence "[a, b]", quotes
+   removed.  out: cap bytes, NUL-terminated (may be NULL to ask for *len); *len = text length.
+   FM3D_ERR_PARSE: the file cannot be read; FM3D_ERR_INVALID: no such key (or a map node). */
+int fm3d_settings_lookup(const char *path, const char *key, char *out, int cap, int *len);
 int fm3d_ctx_create(const fm3d_settings *s, int device, fm3d_ctx **out);
 void fm3d_ctx_destroy(fm3d_ctx *ctx);
 const char *fm3d_last_error(const fm3d_ctx *ctx);

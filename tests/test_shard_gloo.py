@@ -99,3 +99,25 @@ def test_sharded_merge_equals_single_run_gloo(synth, fm3d):
     for r in range(2):
         merged = np.frombuffer(got[r], dtype=fm3d.RECORD)
         assert merged.tobytes() == full.tobytes(), r
+
+
+def test_merge_gathered_ragged_counts(fm3d):
+    """The merge of the bench's C5 step: fixed-capacity per-rank buffers whose tails hold stale
+    bytes; only the first counts[r] records of rank r, in rank order, survive."""
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    rng = np.random.default_rng(0)
+    cap, counts = 6, [5, 0, 3, 6]
+    recs = []
+    for r, c in enumerate(counts):
+        rec = np.zeros(c, dtype=fm3d.RECORD)
+        rec["queryIdx"] = 100 * r + np.arange(c)
+        rec["point"] = rng.normal(size=(c, 3))
+        recs.append(rec)
+    g = rng.integers(0, 256, (len(counts), cap, shard.RECORD_BYTES), dtype=np.uint8)  # stale bytes
+    for r, rec in enumerate(recs):
+        g[r, :len(rec)] = rec.view(np.uint8).reshape(len(rec), shard.RECORD_BYTES)
+    merged = shard.merge_gathered(g, np.array(counts, dtype=np.int32))
+    assert merged.tobytes() == np.concatenate(recs).tobytes()
+    with pytest.raises(ValueError):
+        shard.merge_gathered(g, np.array([7, 0, 0, 0]))
+    assert shard.shard_capacity(10, 4) == 3 and shard.shard_capacity(0, 2) == 1

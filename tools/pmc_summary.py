@@ -50,6 +50,14 @@ def main():
         res["lds_bank_conflict_frac"] = agg.get("SQ_LDS_BANK_CONFLICT", 0.) / max(agg["SQ_LDS_IDX_ACTIVE"], 1)
         res["lds_addr_conflict_frac"] = agg.get("SQ_LDS_ADDR_CONFLICT", 0.) / max(agg["SQ_LDS_IDX_ACTIVE"], 1)
         res["lds_unaligned_stall_frac"] = agg.get("SQ_LDS_UNALIGNED_STALL", 0.) / max(agg["SQ_LDS_IDX_ACTIVE"], 1)
+    if "--workload" in sys.argv:  # keypoints,ray,levels of the bench command profiled
+        k, r, l = (int(x) for x in sys.argv[sys.argv.index("--workload") + 1].split(","))
+        res["workload"] = {"keypoints": k, "ray": r, "levels": l}
+    if "--command" in sys.argv:
+        res["command"] = sys.argv[sys.argv.index("--command") + 1]
+    calib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r02_fetch_calibration.json")
+    if os.path.exists(calib):
+        res["calibration"] = os.path.relpath(os.path.abspath(calib), os.path.join(os.path.dirname(calib), ".."))
     res["note"] = ("FETCH_SIZE/WRITE_SIZE in KiB; gfx950 FETCH_SIZE reads half the bytes of wide streaming loads "
                    "(doubled here); each counter group measured in its own rocprofv3 --pmc pass")
     print(json.dumps(res, indent=1))
