@@ -31,12 +31,13 @@
  * lmdif driving a numpy evaluateNormal).  Exact lmfit trajectories are
  * "parity unpinned".
  *
- * Two LM modes:
- *   ORC_LM_STRICT    : MINPACK Householder QR, index-order sums, libm transcendentals.
- *   ORC_LM_CANONICAL : the GPU kernel's arithmetic: Gram-sum QR over blocked
- *                      reductions (nthreads lanes, wave 64 trees) and the
- *                      deterministic transcendentals of include/fm3d_detmath.h.
- *                      The GPU kernel must equal this mode bit for bit.
+ * Two LM modes, both MINPACK lmdif with Householder qrfac and every m_dat-long
+ * sum in pixel (index) order:
+ *   ORC_LM_STRICT  : libm transcendentals (sin/cos/atan2/exp) -- the reference's;
+ *   ORC_LM_DETMATH : the deterministic transcendentals of include/fm3d_detmath.h.
+ *                    THE GPU CONTRACT: the LM kernel (csrc/fm3d_lm2.hip) equals this
+ *                    mode bit for bit (statuses, lmdif info / nfev per level, normals);
+ *                    STRICT is the north_star's 1e-4 comparison.
  * Compiled with -ffp-contract=off (no FMA contraction), like the kernels.
  */
 #include <math.h>
@@ -597,12 +598,10 @@ enum {
     ORC_ST_ABORT_PIX1 = 3,  /* updateImage1PixelsIntensity (:580-584) */
     ORC_ST_ABORT_PIX2 = 4,  /* projectPointsToImage2 (:623-626) */
     ORC_ST_NAN_PLANE = 5,   /* projectPointToPlane exit(-6) (:465-469) */
-    ORC_ST_NAN_NORMAL = 6,  /* evaluateNormal NaN normal (:81-85) */
-    ORC_ST_TOO_MANY_PIXELS = 7
+    ORC_ST_NAN_NORMAL = 6   /* evaluateNormal NaN normal (:81-85) */
 };
-/* mode bits: ORC_LM_GRAM = Gram-sum QR + blocked reductions, ORC_LM_DETMATH =
-   fm3d_detmath transcendentals.  STRICT = 0, CANONICAL = both. */
-enum { ORC_LM_STRICT = 0, ORC_LM_GRAM = 1, ORC_LM_DETMATH = 2, ORC_LM_CANONICAL = 3 };
+/* LM modes (mode bit 2: fm3d_detmath transcendentals instead of libm) */
+enum { ORC_LM_STRICT = 0, ORC_LM_DETMATH = 2 };
 
 typedef struct {
     const uint8_t *img[2][8]; /* pyramid levels of image 1 and 2 */
@@ -623,7 +622,6 @@ typedef struct {
     float *I1;          /* m intensities of image 1 at the current level */
     int I1_ok;
     int mode;
-    int nthreads;       /* canonical mode: lanes of the GPU workgroup */
     long nfev;          /* evaluations in the current lmdif call */
 } orc_lmdata;
 
@@ -750,45 +748,6 @@ static double orc_enorm(int n, const double *x)
         return sqrt(x3max * ((s2 / x3max) + (x3max * s3)));
     }
     return x3max * sqrt(s3);
-}
-
-/* canonical reduction order of the GPU kernel: lane t sums elements
-   t, t+NT, t+2NT, ... in order; 64-lane waves reduce by halving trees
-   (lane l += lane l+s, s = 32..1); wave sums reduce by halving trees. */
-static double orc_blocked_sum(const double *v, int m, int NT)
-{
-    double lane[64], wsum[64];
-    int nw = NT / 64, w, l, s, k;
-    if (NT <= 0) { /* plain index order (diagnostics) */
-        double acc = 0.0;
-        for (k = 0; k < m; k++) acc = acc + v[k];
-        return acc;
-    }
-    for (w = 0; w < nw; w++) {
-        for (l = 0; l < 64; l++) {
-            double acc = 0.0;
-            for (k = w * 64 + l; k < m; k += NT) acc = acc + v[k];
-            lane[l] = acc;
-        }
-        for (s = 32; s >= 1; s >>= 1)
-            for (l = 0; l < s; l++) lane[l] = lane[l] + lane[l + s];
-        wsum[w] = lane[0];
-    }
-    for (s = nw / 2; s >= 1; s >>= 1)
-        for (l = 0; l < s; l++) wsum[l] = wsum[l] + wsum[l + s];
-    return wsum[0];
-}
-
-/* Euclidean norm of an m-vector: MINPACK enorm (strict) or sqrt of the
-   canonical blocked sum of squares (canonical; identical to enorm whenever all
-   |x| lie in (3.8e-20, 1.3e19/m) or are zero, which covers residuals built from
-   8-bit intensities unless the LM weight explodes). */
-static double orc_enorm_m(const orc_lmdata *D, const double *x, double *tmp)
-{
-    int i;
-    if (!(D->mode & ORC_LM_GRAM)) return orc_enorm(D->m, x);
-    for (i = 0; i < D->m; i++) tmp[i] = x[i] * x[i];
-    return sqrt(orc_blocked_sum(tmp, D->m, D->nthreads));
 }
 
 /* qrsolv (MINPACK), r column-major with leading dimension ldr */
@@ -945,7 +904,7 @@ static int orc_jac_qr(orc_lmdata *D, double *x, const double *fvec, double eps,
         if (st) return st;
         for (i = 0; i < m; i++) fjac[j * m + i] = (wa4[i] - fvec[i]) / h[j];
     }
-    if (!(D->mode & ORC_LM_GRAM)) {
+    {
         /* qrfac with column pivoting (MINPACK), n = 2 */
         double rdiag[2], wa[2], ajnorm, sum, temp;
         int k, kmax;
@@ -1001,42 +960,6 @@ static int orc_jac_qr(orc_lmdata *D, double *x, const double *fvec, double eps,
             qtf[j] = wa4[j];
         }
         r[0] = fjac[0]; r[1] = 0.; r[2] = fjac[m + 0]; r[3] = fjac[m + 1];
-    } else {
-        /* Gram-sum QR in the kernel's canonical reduction order */
-        double S00, S11, S01, S0f, S1f, Spp, Sqq, Spq, Spf, Sqf, r00, r01, r11, q0, q1, t;
-        int p, q;
-        for (i = 0; i < m; i++) tmp[i] = fjac[i] * fjac[i];
-        S00 = orc_blocked_sum(tmp, m, D->nthreads);
-        for (i = 0; i < m; i++) tmp[i] = fjac[m + i] * fjac[m + i];
-        S11 = orc_blocked_sum(tmp, m, D->nthreads);
-        for (i = 0; i < m; i++) tmp[i] = fjac[i] * fjac[m + i];
-        S01 = orc_blocked_sum(tmp, m, D->nthreads);
-        for (i = 0; i < m; i++) tmp[i] = fjac[i] * fvec[i];
-        S0f = orc_blocked_sum(tmp, m, D->nthreads);
-        for (i = 0; i < m; i++) tmp[i] = fjac[m + i] * fvec[i];
-        S1f = orc_blocked_sum(tmp, m, D->nthreads);
-        acnorm[0] = sqrt(S00);
-        acnorm[1] = sqrt(S11);
-        if (acnorm[1] > acnorm[0]) { p = 1; q = 0; } else { p = 0; q = 1; }
-        ipvt[0] = p; ipvt[1] = q;
-        Spp = p == 0 ? S00 : S11;
-        Sqq = p == 0 ? S11 : S00;
-        Spf = p == 0 ? S0f : S1f;
-        Sqf = p == 0 ? S1f : S0f;
-        Spq = S01;
-        (void)Spp;
-        r00 = acnorm[p];
-        if (r00 == 0.) {
-            r01 = 0.; r11 = 0.; q0 = 0.; q1 = 0.;
-        } else {
-            r01 = Spq / r00;
-            q0 = Spf / r00;
-            t = Sqq - r01 * r01;
-            r11 = t > 0. ? sqrt(t) : 0.;
-            q1 = r11 > 0. ? (Sqf - r01 * q0) / r11 : 0.;
-        }
-        r[0] = r00; r[1] = 0.; r[2] = r01; r[3] = r11;
-        qtf[0] = q0; qtf[1] = q1;
     }
     return 0;
 }
@@ -1061,7 +984,7 @@ static int orc_lmdif(orc_lmdata *D, double *x, double epsfcn, double *fvec, doub
     if (D->m < n) { *nfev_out = 0; return 0; }
     st = orc_eval(D, x, fvec);
     if (st) { *nfev_out = (int)D->nfev; return -st; }
-    fnorm = orc_enorm_m(D, fvec, tmp);
+    fnorm = orc_enorm(D->m, fvec);
     for (;;) {
         st = orc_jac_qr(D, x, fvec, eps, fjac, wa4, tmp, r, qtf, acnorm, ipvt);
         if (st) { *nfev_out = (int)D->nfev; return -st; }
@@ -1103,7 +1026,7 @@ static int orc_lmdif(orc_lmdata *D, double *x, double epsfcn, double *fvec, doub
             if (iter == 1) delta = delta < pnorm ? delta : pnorm;
             st = orc_eval(D, wa2, wa4);
             if (st) { *nfev_out = (int)D->nfev; return -st; }
-            fnorm1 = orc_enorm_m(D, wa4, tmp);
+            fnorm1 = orc_enorm(D->m, wa4);
             actred = -1.;
             if (p1 * fnorm1 < fnorm) actred = 1. - (fnorm1 / fnorm) * (fnorm1 / fnorm);
             for (j = 0; j < n; j++) {
@@ -1162,7 +1085,7 @@ out:
    per-level lmdif info and evaluation counts (index = level). */
 static int orc_point(const orc_camera *cam, const double R2[9], const double t2[3], const orc_pyramid *pyr,
                      int levels, const double X[3], int ray, int boundW, int boundH, double epsfcn, int cmax,
-                     int mode, int NT, double n_out[3], int *info_out, int *nfev_out, int *mdat_out)
+                     int mode, double n_out[3], int *info_out, int *nfev_out, int *mdat_out)
 {
     int side = 2 * ray + 1, cap = side * side, m, L, i, status = ORC_ST_OK;
     double *pix, *rays, *fvec, *fjac, *wa4, *tmp, nrm, norm[3], inv;
@@ -1174,7 +1097,6 @@ static int orc_point(const orc_camera *cam, const double R2[9], const double t2[
     m = orc_neighborhood(cam, X, ray, boundW, boundH, pix, cap);
     *mdat_out = m;
     if (m <= 0) { free(pix); return ORC_ST_NO_PIXELS; }
-    if ((mode & ORC_LM_GRAM) && NT > 0 && m > NT * 16) { free(pix); return ORC_ST_TOO_MANY_PIXELS; }
     rays = (double *)malloc(sizeof(double) * 2 * m);
     fvec = (double *)malloc(sizeof(double) * m);
     fjac = (double *)malloc(sizeof(double) * 2 * m);
@@ -1189,7 +1111,7 @@ static int orc_point(const orc_camera *cam, const double R2[9], const double t2[
     memset(&D, 0, sizeof(D));
     D.cam = cam; D.R2 = R2; D.t2 = t2; D.pyr = pyr;
     D.X[0] = X[0]; D.X[1] = X[1]; D.X[2] = X[2];
-    D.cmax = cmax; D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode; D.nthreads = NT;
+    D.cmax = cmax; D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode;
     img_scale = (float)pow(2.0, (double)levels);
     for (L = levels; L >= 0; L--) {
         double par[2];
@@ -1236,7 +1158,7 @@ static void orc_build_pyramid(const uint8_t *img1, const uint8_t *img2, int w, i
 ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], const double t2[3],
                                  const uint8_t *img1, const uint8_t *img2, int w, int h, int levels,
                                  const double *points, int P, int ray, int boundW, int boundH, double epsfcn,
-                                 double zmax, int mode, int NT, double *normals, int *status, int *info,
+                                 double zmax, int mode, double *normals, int *status, int *info,
                                  int *nfev, int *mdat, int nthreads)
 {
     orc_pyramid pyr;
@@ -1249,7 +1171,7 @@ ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], cons
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : kept)
 #endif
     for (i = 0; i < P; i++) {
-        status[i] = orc_point(cam, R2, t2, &pyr, levels, &points[3 * i], ray, boundW, boundH, epsfcn, cmax, mode, NT,
+        status[i] = orc_point(cam, R2, t2, &pyr, levels, &points[3 * i], ray, boundW, boundH, epsfcn, cmax, mode,
                               &normals[3 * i], &info[8 * i], &nfev[8 * i], &mdat[i]);
         if (status[i] == ORC_ST_OK) kept++;
     }
@@ -1261,7 +1183,7 @@ ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], cons
    tests that pin lmdif against scipy.optimize.leastsq on the same residual. */
 ORC_API int orc_lm_single_level(const orc_camera *cam, const double R2[9], const double t2[3],
                                 const uint8_t *img1, const uint8_t *img2, int w, int h, const double X[3],
-                                const double *pix, int m, double epsfcn, double zmax, int mode, int NT,
+                                const double *pix, int m, double epsfcn, double zmax, int mode,
                                 double par[2], int *nfev_out)
 {
     orc_pyramid pyr;
@@ -1276,7 +1198,7 @@ ORC_API int orc_lm_single_level(const orc_camera *cam, const double R2[9], const
     memset(&D, 0, sizeof(D));
     D.cam = cam; D.R2 = R2; D.t2 = t2; D.pyr = &pyr; D.level = 0; D.scale = 1.0;
     D.X[0] = X[0]; D.X[1] = X[1]; D.X[2] = X[2];
-    D.cmax = (int)(2 * zmax); D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode; D.nthreads = NT;
+    D.cmax = (int)(2 * zmax); D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode;
     orc_update_I1(&D);
     info = orc_lmdif(&D, par, epsfcn, fvec, fjac, wa4, tmp, nfev_out);
     free(rays); free(fvec); free(fjac); free(wa4); free(tmp); free(I1);
@@ -1298,14 +1220,13 @@ ORC_API int orc_eval_residual(const orc_camera *cam, const double R2[9], const d
     memset(&D, 0, sizeof(D));
     D.cam = cam; D.R2 = R2; D.t2 = t2; D.pyr = &pyr; D.level = 0; D.scale = 1.0;
     D.X[0] = X[0]; D.X[1] = X[1]; D.X[2] = X[2];
-    D.cmax = (int)(2 * zmax); D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode; D.nthreads = 256;
+    D.cmax = (int)(2 * zmax); D.m = m; D.ray = rays; D.pix = pix; D.I1 = I1; D.mode = mode;
     orc_update_I1(&D);
     st = orc_eval(&D, par, fvec);
     free(rays); free(I1);
     return st;
 }
 
-ORC_API double orc_blocked_sum_test(const double *v, int m, int NT) { return orc_blocked_sum(v, m, NT); }
 
 /* ------------------------------------------------------------------ */
 /* Feature frames + patch export              */

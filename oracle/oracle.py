@@ -14,9 +14,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
 F32, U8, BITS = 0, 1, 2
-STRICT, GRAM, DETMATH, CANONICAL = 0, 1, 2, 3
+STRICT, DETMATH = 0, 2  # libm transcendentals / fm3d_detmath.h (the GPU contract)
 
-ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL, ST_TOO_MANY = range(8)
+ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
 
 class OrcCamera(ctypes.Structure):
@@ -166,7 +166,7 @@ def neighborhood(cam, X, ray, bound_w=1024, bound_h=768):
 
 
 def optimize_normals(cam, R2, t2, img1, img2, levels, points, ray, bound_w=1024, bound_h=768,
-                     epsfcn=1e-10, zmax=2.4, mode=STRICT, nt=256, nthreads=0):
+                     epsfcn=1e-10, zmax=2.4, mode=STRICT, nthreads=0):
     img1 = np.ascontiguousarray(img1, dtype=np.uint8)
     img2 = np.ascontiguousarray(img2, dtype=np.uint8)
     h, w = img1.shape
@@ -182,7 +182,7 @@ def optimize_normals(cam, R2, t2, img1, img2, levels, points, ray, bound_w=1024,
                                _p(img1, ctypes.c_uint8), _p(img2, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h),
                                ctypes.c_int(levels), _p(P), ctypes.c_int(n), ctypes.c_int(ray), ctypes.c_int(bound_w),
                                ctypes.c_int(bound_h), ctypes.c_double(epsfcn), ctypes.c_double(zmax),
-                               ctypes.c_int(mode), ctypes.c_int(nt), _p(normals), _p(status, ctypes.c_int),
+                               ctypes.c_int(mode), _p(normals), _p(status, ctypes.c_int),
                                _p(info, ctypes.c_int), _p(nfev, ctypes.c_int), _p(mdat, ctypes.c_int),
                                ctypes.c_int(nthreads))
     return dict(normals=normals, status=status, info=info, nfev=nfev, mdat=mdat)
@@ -202,7 +202,7 @@ def eval_residual(cam, R2, t2, img1, img2, X, pix, par, zmax=2.4, mode=STRICT):
     return st, f
 
 
-def lm_single_level(cam, R2, t2, img1, img2, X, pix, par0, epsfcn=1e-10, zmax=2.4, mode=STRICT, nt=256):
+def lm_single_level(cam, R2, t2, img1, img2, X, pix, par0, epsfcn=1e-10, zmax=2.4, mode=STRICT):
     img1 = np.ascontiguousarray(img1, dtype=np.uint8)
     img2 = np.ascontiguousarray(img2, dtype=np.uint8)
     h, w = img1.shape
@@ -214,15 +214,8 @@ def lm_single_level(cam, R2, t2, img1, img2, X, pix, par0, epsfcn=1e-10, zmax=2.
                                      _p(img1, ctypes.c_uint8), _p(img2, ctypes.c_uint8), ctypes.c_int(w),
                                      ctypes.c_int(h), _p(_f64(X)), _p(pix), ctypes.c_int(pix.shape[0]),
                                      ctypes.c_double(epsfcn), ctypes.c_double(zmax), ctypes.c_int(mode),
-                                     ctypes.c_int(nt), _p(par), ctypes.byref(nfev))
+                                     _p(par), ctypes.byref(nfev))
     return info, par, nfev.value
-
-
-def blocked_sum(v, nt):
-    v = _f64(v)
-    f = lib().orc_blocked_sum_test
-    f.restype = ctypes.c_double
-    return f(_p(v), ctypes.c_int(v.size), ctypes.c_int(nt))
 
 
 def gravity(rIC):

@@ -112,3 +112,95 @@ def test_example_main_matches_python_api(fm3d, synth, orc, tmp_path):
         raw = (d / f"patch_{i}.pgm").read_bytes()
         assert raw.startswith(b"P5\n128 128\n255\n")
         assert raw[len(b"P5\n128 128\n255\n"):] == patches[i].tobytes()
+
+
+DROPIN = os.path.join(ROOT, "examples", "main_dropin")
+
+
+def test_dropin_main_compiles_against_cv_standins():
+    """examples/main_dropin.cpp (main.cpp's call sequence with only the includes replaced by
+    include/fm3d_cv.hpp) compiles warning-free."""
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I",
+                        os.path.join(ROOT, "include"), os.path.join(ROOT, "examples", "main_dropin.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([DROPIN], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "Usage" in r.stdout
+
+
+def test_settings_lookup_filestorage_nodes(fm3d, tmp_path):
+    """fm3d_settings_lookup (cv::FileNode of the stand-ins) on the reference's settings layout."""
+    import ctypes
+    p = tmp_path / "s.yml"
+    p.write_text("%YAML:1.0\nIMAGES:\n#TIME : 1 POS : 1 2 3\n\n   img1: /data/img_7809.pgm\n"
+                 "   pos1: [5.301099, 8.031408, 1.977258, 0.153433, 0.149941, -2.658648]\n"
+                 "NNDR:\n   epsilon: 0.55\nFeatureOptions:\n   SurfDetector:\n      Extended: 1\n"
+                 "   ExtractorType: SURF\n")
+    lib = fm3d.lib()
+
+    def look(key):
+        n = ctypes.c_int(0)
+        buf = ctypes.create_string_buffer(256)
+        rc = lib.fm3d_settings_lookup(str(p).encode(), key.encode(), buf, 256, ctypes.byref(n))
+        return rc, buf.value.decode(), n.value
+
+    assert look("IMAGES.img1") == (0, "/data/img_7809.pgm", len("/data/img_7809.pgm"))
+    assert look("NNDR.epsilon")[1] == "0.55"
+    assert look("IMAGES.pos1")[1].startswith("[5.301099,")
+    assert look("FeatureOptions.SurfDetector.Extended")[1] == "1"
+    assert look("FeatureOptions.ExtractorType")[1] == "SURF"
+    assert look("FeatureOptions.Missing")[0] == fm3d.ERR_INVALID
+    n = ctypes.c_int(0)
+    assert lib.fm3d_settings_lookup(str(tmp_path / "nope.yml").encode(), b"A", None, 0, ctypes.byref(n)) == fm3d.ERR_PARSE
+
+
+@pytest.mark.gpu
+def test_dropin_main_matches_python_api(fm3d, synth, orc, tmp_path):
+    """main_dropin -s settings.yml (the reference command line): matches, triangulated points and
+    normals equal the Python mirror's on the same inputs; patch_<i>.pgm of every kept point equal
+    the patch export; the square neighbourhood of frame 0 equals the oracle's."""
+    pair = synth.make_frame_pair(1500, seed=23)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    # the upstream detector's output, as the images' feature side files
+    pair.kp1.astype(np.float32).tofile(d / "img1.pgm.kpts.f32")
+    pair.kp2.astype(np.float32).tofile(d / "img2.pgm.kpts.f32")
+    pair.desc1.tofile(d / "img1.pgm.desc.u8")
+    pair.desc2.tofile(d / "img2.pgm.desc.u8")
+    yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.55)
+    yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
+    yml += "FeatureOptions:\n   DetectorType: SIFT\n   ExtractorType: SIFT\n"
+    (d / "settings.yml").write_text(yml)
+    r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
+    assert r.returncode == 0, r.stderr + r.stdout
+    matches = np.fromfile(d / "out_matches.bin", dtype=fm3d.DMATCH)
+    pts = np.fromfile(d / "out_points.f64").reshape(-1, 3)
+    nrm = np.fromfile(d / "out_normals.f64").reshape(-1, 3)
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    ctx = fm3d.Context(s)
+    try:
+        m = fm3d.DescriptorsMatcher(ctx).compareWithNNDR(s.nndrEpsilon, pair.desc1, pair.desc2)
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.setg12(s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+        sct.setKeypoints(pair.kp1, pair.kp2, m)
+        P, _ = sct.triangulate()
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(pair.img1, pair.img2)
+        kept, normals = no.computeOptimizedNormals(P)
+        frames = no.computeFeaturesFrames(kept, normals)
+        patches = sct.projectReferencePointsToImageWithFrames(None, frames)
+    finally:
+        ctx.close()
+    assert matches.tobytes() == m.tobytes()
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, s.nndrEpsilon, oracle_threads())
+    assert np.array_equal(matches["queryIdx"], q) and np.array_equal(matches["trainIdx"], t)
+    assert len(kept) > 10
+    assert np.array_equal(pts, kept) and np.array_equal(nrm, normals)
+    for i in range(len(kept)):
+        raw = (d / f"patch_{i}.pgm").read_bytes()
+        assert raw == b"P5\n128 128\n255\n" + patches[i].tobytes()
+    nb0 = np.fromfile(d / "out_neighborhoods.f64").reshape(-1, 3)
+    assert np.array_equal(nb0, orc.square_neighborhoods(frames[:1])[0])
+    for f in ("matches.pgm", "projectedPatches.pgm"):
+        assert (d / f).read_bytes().startswith(b"P6\n")

@@ -107,17 +107,6 @@ def test_detmath_does_not_move_lm(orc):
     assert np.abs(a["normals"][ok] - b["normals"][ok]).max() < 1e-12
 
 
-def test_blocked_sum_order(orc):
-    rng = np.random.default_rng(1)
-    v = rng.normal(size=3000)
-    # NT = 0 is plain index order
-    seq = 0.0
-    for x in v:
-        seq = seq + x
-    assert orc.blocked_sum(v, 0) == seq
-    assert abs(orc.blocked_sum(v, 256) - seq) < 1e-12
-
-
 def test_features_frames_and_patches_vs_numpy(orc):
     """computeFeaturesFrames + patch export: the oracle against the numpy restatement
     (tests/golden/make_golden.py make_patches): frames bit for bit (same scalar operations),
