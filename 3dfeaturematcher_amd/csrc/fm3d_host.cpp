@@ -71,7 +71,8 @@ struct fm3d_ctx {
     int nOff = 0, nOffPad = 0;
     // work buffers
     DevBuf A, B, cqA, ctB, idx, key, fkey, knnOut, cand, flag, matches, count, scanTmp;
-    DevBuf partIdx, partKey;  // per-part top-2 lists of the f32 matcher
+    DevBuf partIdx, partKey;  // per-part top-2 lists of the split matchers
+    DevBuf A8, B8;            // binary rows unpacked to int8 for the MFMA matcher
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     int nCU = 0;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
@@ -333,6 +334,12 @@ int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB,
     return FM3D_OK;
 }
 
+// FM3D_BITS_MFMA=0 keeps 256-bit binary rows on the popcount kernel (A/B comparisons)
+bool bits_mfma() {
+    const char* e = getenv("FM3D_BITS_MFMA");
+    return !(e && e[0] == '0');
+}
+
 // knn2 + NNDR flags on staged descriptors (device), results in c->idx/key/fkey/cand/flag
 int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int queryOffset, bool wantKnn) {
     HIPCHK(c, c->idx.ensure((size_t)nA * 2 * sizeof(int) + 16));
@@ -350,14 +357,14 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         const int nAPad = nA, nBPad = nB;
         HIPCHK(c, c->cqA.ensure((size_t)(nAPad + 1) * sizeof(int)));
         HIPCHK(c, c->ctB.ensure((size_t)(nBPad + 1) * sizeof(int)));
-        fm3d::launch_rowconst_u8(c->A.as<uint8_t>(), nA, nAPad, dimPad, c->cqA.as<int>(), c->stream);
-        fm3d::launch_rowconst_u8(c->B.as<uint8_t>(), nB, nBPad, dimPad, c->ctB.as<int>(), c->stream);
+        fm3d::launch_rowconst_u8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->cqA.as<int>(),
+                                 c->ctB.as<int>(), c->stream);
         const int parts = fm3d::knn2_u8_parts(nA, nB, c->nCU);
         if (parts > 1) {
             HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
             HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
         }
-        fm3d::launch_knn2_u8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->cqA.as<int>(),
+        fm3d::launch_knn2_i8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, 0, c->cqA.as<int>(),
                              c->ctB.as<int>(), parts, c->partIdx.as<int>(), c->partKey.as<int>(), c->idx.as<int>(),
                              c->key.as<int>(), c->stream);
     } else if (type == FM3D_DESC_F32) {
@@ -370,6 +377,22 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         fm3d::launch_knn2_f32(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, parts, c->partIdx.as<int>(),
                               c->partKey.as<float>(), c->bPairs.as<float>(), c->idx.as<int>(), c->fkey.as<float>(),
                               c->stream);
+    } else if (dimPad == 32 && bits_mfma()) {
+        // 256-bit rows (ORB): unpacked to int8 and matched on the int8 MFMA kernel (exact integer
+        // Hamming distances popc(b) - a.b', same ranking rule)
+        HIPCHK(c, c->A8.ensure((size_t)nA * 256 + 16));
+        HIPCHK(c, c->B8.ensure((size_t)nB * 256 + 16));
+        HIPCHK(c, c->ctB.ensure((size_t)(nB + 1) * sizeof(int)));
+        fm3d::launch_unpack_bits(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, c->A8.as<uint8_t>(),
+                                 c->B8.as<uint8_t>(), c->ctB.as<int>(), c->stream);
+        const int parts = fm3d::knn2_u8_parts(nA, nB, c->nCU);
+        if (parts > 1) {
+            HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
+            HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
+        }
+        fm3d::launch_knn2_i8(c->A8.as<uint8_t>(), nA, c->B8.as<uint8_t>(), nB, 256, 1, nullptr, c->ctB.as<int>(),
+                             parts, c->partIdx.as<int>(), c->partKey.as<int>(), c->idx.as<int>(), c->key.as<int>(),
+                             c->stream);
     } else {
         const int parts = fm3d::knn2_parts(nA, nB, dimPad, c->nCU);
         if (parts > 1) {
@@ -621,7 +644,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
                       &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat,
                       &c->slab, &c->slabI1,
-                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs};
+                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->A8, &c->B8};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();

@@ -77,9 +77,16 @@ struct KnnOut {
 // u8 rows (dim padded to a multiple of 128 with value 128 on both sides -> no effect)
 // u8 rows: `parts` train-tile ranges (knn2_u8_parts), merged through partIdx/partKey
 int knn2_u8_parts(int nA, int nB, int nCU);
-void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA, const int* ctB,
-                    int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s);
-void launch_rowconst_u8(const uint8_t* X, int n, int nPad, int dimPad, int* c, hipStream_t s);
+// int8-MFMA matcher for u8 rows (bits = 0) and for 32-byte binary rows unpacked by
+// launch_unpack_bits (bits = 1, dimPad 256); ctB = packed train row constants
+void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int bits, const int* cqA,
+                    const int* ctB, int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s);
+// row constants of both sides: cq = |a'|^2 per query row, ctp = packed train constants
+void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int* cq, int* ctp,
+                        hipStream_t s);
+// 32-byte binary rows -> 256 int8 (query 0/1, train -1/+1) + packed train constants popc(b)
+void launch_unpack_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, uint8_t* outA, uint8_t* outB, int* ctp,
+                        hipStream_t s);
 // f32 rows (dim 64 / 128): `parts` train ranges (knn2_parts), merged through partIdx/partKey (parts*nA*2 each)
 int knn2_parts(int nA, int nB, int dim, int nCU);
 size_t knn2_f32_pairs_bytes(int nB, int dim);  // the row-pair copy of B (dim 64 / 128)

@@ -16,6 +16,7 @@
 
 #include <type_traits>
 #include <limits.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include "fm3d_kernels.h"
@@ -73,27 +74,78 @@ __device__ inline void top2_merge(int& b1, int& i1, int& b2, int& i2, int c1, in
     }
 }
 
-// per-row constant |x'|^2 with x' = x - 128 over the padded row (padding bytes are 128)
-__global__ void rowconst_u8_kernel(const uint8_t* __restrict__ X, int n, int nPad, int dimPad, int* __restrict__ c) {
-    int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nPad) return;
-    if (r >= n) {
-        c[r] = INT_MAX / 4;  // padding rows: never selected
-        return;
-    }
-    const uint8_t* row = X + (size_t)r * dimPad;
+// Ranking keys of the int8 kernel are packed per train tile into one u32 so that the top-2 of a
+// tile costs three VALU operations per distance (v_lshl_add_u32, v_max_u32, v_med3_u32).  The
+// kernel keeps the LARGEST packed values:
+//   bits 31..7: X = kKeyBias - s, s = |b'|^2 - 2 a'.b' (u8) or popc(b) - a.b' (bits); 1 <= X < 2^25
+//   bits  6..0: 127 - (row inside its 128-row tile)   (equal s -> the lower row wins)
+// The packed row constant ctq = ((kKeyBias - c) << 7) | (127 - row) is formed once per train row;
+// the epilogue adds acc << 8 (u8: 2 a'.b') or acc << 7 (bits) to it.  0 marks "no row".
+constexpr uint32_t kKeyBias = (1u << 24) + (1u << 22) + 1;  // s in [-2^22, 2^24 + 2^22)
+
+__device__ inline uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ inline uint32_t umax(uint32_t a, uint32_t b) { return a < b ? b : a; }
+// (plain C, not inline asm, where it reads an MFMA result: the hazard recognizer does not pad
+// reads inside asm)
+__device__ inline uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) { return umax(umin(a, b), umin(umax(a, b), c)); }
+__device__ inline uint32_t pack_row(uint32_t c, int r) { return ((kKeyBias - c) << 7) | (uint32_t)(127 - (r & 127)); }
+
+// per-row constants of both sides in one launch, 16 bytes per lane (v_dot4_i32_i8 of x' = x - 128
+// with itself), lanes of a row summed by shuffles: |x'|^2 for the query rows (cq), the packed
+// ranking constant for the train rows (ctp).  Padding bytes are 128 (x' = 0).
+__global__ void rowconst_u8_kernel(const uint8_t* __restrict__ A, int nA, const uint8_t* __restrict__ B, int nB,
+                                   int dimPad, int* __restrict__ cq, int* __restrict__ ctp) {
+    const int cpr = dimPad / 16;  // 8 or 16 lanes per row (power of two)
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = t / cpr, k = t - r * cpr;
+    const bool isA = r < nA;
+    const int rr = isA ? r : r - nA;
     int s = 0;
-    for (int d = 0; d < dimPad; d++) {
-        int v = (int)row[d] - 128;
-        s += v * v;
+    if (r < nA + nB) {
+        const v4i x = *(const v4i*)((isA ? A : B) + (size_t)rr * dimPad + 16 * k) ^
+                      (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+#pragma unroll
+        for (int w = 0; w < 4; w++) s = __builtin_amdgcn_sdot4(x[w], x[w], s, false);
     }
-    c[r] = s;
+    for (int o = 1; o < cpr; o <<= 1) s += __shfl_xor(s, o);
+    if (k == 0 && r < nA + nB) {
+        if (isA)
+            cq[rr] = s;
+        else
+            ctp[rr] = (int)pack_row((uint32_t)s, rr);
+    }
+}
+
+// binary rows (32 bytes) of both sides unpacked in one launch to int8 rows of 256 bits for the
+// MFMA kernel: the query side as 0/1, the train side as -1/+1 (so that popc(b) - a.b' is the Hamming
+// distance) with the packed ranking constant popc(b)
+__global__ void unpack_bits_kernel(const uint32_t* __restrict__ A, int nA, const uint32_t* __restrict__ B, int nB,
+                                   int8_t* __restrict__ outA, int8_t* __restrict__ outB, int* __restrict__ ctp) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;  // one 32-bit word per thread, 8 per row
+    const int r = t >> 3, w = t & 7;
+    if (r >= nA + nB) return;
+    const bool train = r >= nA;
+    const int rr = train ? r - nA : r;
+    const uint32_t x = (train ? B : A)[(size_t)rr * 8 + w];
+    const int lo = train ? -1 : 0;
+    int8_t b[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) b[k] = ((x >> k) & 1u) ? 1 : lo;
+    v4i* o = (v4i*)((train ? outB : outA) + (size_t)rr * 256 + 32 * w);
+    o[0] = *(const v4i*)&b[0];
+    o[1] = *(const v4i*)&b[16];
+    int pc = __popc(x);
+    pc += __shfl_xor(pc, 1);
+    pc += __shfl_xor(pc, 2);
+    pc += __shfl_xor(pc, 4);
+    if (train && w == 0) ctp[rr] = (int)pack_row((uint32_t)pc, rr);
 }
 
 // KS: dimPad / 32 when it is 4 (128-byte rows) or 8 (256), so the MFMA chain is straight-line
-// code; 0 reads it from dimPad
-template <int KS>
-__global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __restrict__ A, int nA,
+// code; 0 reads it from dimPad.  BITS: rows are pre-unpacked int8 bits (no -128 offset, key
+// popc(b) - a.b', no query constant).
+template <int KS, bool BITS>
+__global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __restrict__ A, int nA,
                                                            const uint8_t* __restrict__ B, int nB, int dimPad,
                                                            const int* __restrict__ cqA, const int* __restrict__ ctB,
                                                            int tilesPerPart, int* __restrict__ idxOut,
@@ -101,7 +153,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tileBytes = kT * (KS ? 32 * KS : dimPad);
     unsigned char* tiles = smem;                              // 2 x tileBytes
-    int* ctl = (int*)(smem + 2 * (size_t)tileBytes);          // 2 x kT
+    uint32_t* ctl = (uint32_t*)(smem + 2 * (size_t)tileBytes);  // 2 x kT packed row constants
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int q0 = blockIdx.x * kQ + wave * 32;
     const int qrow = q0 + (lane & 31);
@@ -109,15 +161,17 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     const int ksteps = KS ? KS : dimPad / 32;
     const int rowBytes = KS ? 32 * KS : dimPad;  // = dimPad (compile-time for KS != 0)
     const int chunksPerRow = rowBytes / 16;
+    constexpr int kFlip = BITS ? 0 : (int)0x80808080;  // x ^ 0x80 == x - 128
+    constexpr int kShift = BITS ? 7 : 8;                 // acc * MUL * 128 (key bits start at bit 7)
 
-    // B operand: this lane's query bytes as int8 (x ^ 0x80 == x - 128)
+    // B operand: this lane's query bytes as int8
     v4i bq[8];  // up to dimPad = 256
 #pragma unroll
     for (int kk = 0; kk < 8; kk++) {
         if (kk < ksteps) {
             v4i v = {0, 0, 0, 0};
             if (qrow < nA) v = *(const v4i*)(A + (size_t)qrow * dimPad + 32 * kk + 16 * half);
-            bq[kk] = v ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+            bq[kk] = v ^ (v4i){kFlip, kFlip, kFlip, kFlip};
         }
     }
     int b1 = INT_MAX, i1 = -1, b2 = INT_MAX, i2 = -1;
@@ -130,7 +184,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     constexpr int kPre = 8;  // 16-byte chunks per thread and tile (kT * 256 / 16 / kThreads at most)
     const int total = kT * chunksPerRow;
     v4i pre[kPre];
-    int preCt = INT_MAX / 4;
+    uint32_t preCt = 0;
     auto load_tile = [&](int t) {
 #pragma unroll
         for (int i = 0; i < kPre; i++) {
@@ -145,7 +199,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
         }
         if (tid < kT) {
             const int j = t * kT + tid;
-            preCt = (j < nB) ? ctB[j] : INT_MAX / 4;
+            preCt = (j < nB) ? (uint32_t)ctB[j] : 0u;
         }
     };
     auto store_tile = [&](int buf) {
@@ -156,7 +210,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
             if (c < total) {
                 const int row = c / chunksPerRow, ch = c - row * chunksPerRow;
                 *(v4i*)(dst + (size_t)row * rowBytes + 16 * swz_chunk(row, ch)) =
-                    pre[i] ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+                    pre[i] ^ (v4i){kFlip, kFlip, kFlip, kFlip};
             }
         }
         if (tid < kT) ctl[buf * kT + tid] = preCt;
@@ -171,9 +225,12 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
         const int buf = (t - tBeg) & 1;
         if (t + 1 < tEnd) load_tile(t + 1);
         const unsigned char* tl = tiles + (size_t)buf * tileBytes;
-        const int* ct = ctl + buf * kT;
-#pragma unroll
-        for (int rb = 0; rb < kT / 32; rb++) {
+        const uint32_t* ct = ctl + buf * kT;
+        // packed top-2 (largest) of this tile, two chains (even / odd row blocks) merged after the tile
+        uint32_t p1[2] = {0, 0}, p2[2] = {0, 0};
+        // software pipeline over the four 32-row blocks: the MFMA chain of block rb + 1 is issued
+        // between the epilogue instructions of block rb (both in flight in one wave)
+        auto mma = [&](int rb) {
             v16i acc = {0};
             const int arow = rb * 32 + (lane & 31);
 #pragma unroll
@@ -183,32 +240,46 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
                     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[kk], acc, 0, 0, 0);
                 }
             }
-            // epilogue: s = |b'|^2 - 2 a'.b' for this lane's 16 train rows (increasing index);
-            // rows past nB exist only in the last tile, which alone runs the bounds test
-            int sv[16];
-            int smin = INT_MAX;
-            auto dists = [&](auto fullc) {
+            return acc;
+        };
+        auto epi = [&](const v16i& acc, int rb, auto fullc) {
+            // this lane's 16 train rows of the block; rows past nB exist only in the last tile,
+            // tested against one per-lane limit (the row offsets stay compile-time constants)
+            const int c = rb & 1;
+            const int lim = nB - t * kT - 4 * half;
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                    int s = ct[row] - (acc[r] + acc[r]);
-                    if (!decltype(fullc)::value) s = (t * kT + row < nB) ? s : INT_MAX;
-                    sv[r] = s;
-                    smin = min(smin, s);
-                }
-            };
-            if ((t + 1) * kT <= nB)
-                dists(std::true_type());
-            else
-                dists(std::false_type());
-            if (__any(smin < b2)) {
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                    top2_insert(sv[r], t * kT + row, b1, i1, b2, i2);
-                }
+            for (int r = 0; r < 16; r++) {
+                const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                uint32_t v = ((uint32_t)acc[r] << kShift) + ct[row];
+                if (!decltype(fullc)::value) v = (rb * 32 + (r & 3) + 8 * (r >> 2) < lim) ? v : 0u;
+                p2[c] = med3u(p1[c], p2[c], v);
+                p1[c] = umax(p1[c], v);
             }
-        }
+        };
+        auto blocks = [&](auto fullc) {
+            v16i accCur = mma(0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int rb = 0; rb < kT / 32; rb++) {
+                v16i accNext;
+                if (rb + 1 < kT / 32) accNext = mma(rb + 1);
+                epi(accCur, rb, fullc);
+                // one scheduling region per block: at most two accumulators live (without the
+                // barriers the compiler hoists all sixteen MFMAs: 194 VGPRs instead of 150)
+                __builtin_amdgcn_sched_barrier(0);
+                if (rb + 1 < kT / 32) accCur = accNext;
+            }
+        };
+        if ((t + 1) * kT <= nB)
+            blocks(std::true_type());
+        else
+            blocks(std::false_type());
+        // merge the chains, then fold the tile's two best into the running (key, index) list:
+        // earlier tiles hold lower indices, and top2_insert keeps them on equal keys
+        const uint32_t m1 = umax(p1[0], p1[1]);
+        const uint32_t m2 = umax(umin(p1[0], p1[1]), umax(p2[0], p2[1]));
+        if (m1) top2_insert((int)kKeyBias - (int)(m1 >> 7), t * kT + 127 - (int)(m1 & 127), b1, i1, b2, i2);
+        if (m2) top2_insert((int)kKeyBias - (int)(m2 >> 7), t * kT + 127 - (int)(m2 & 127), b1, i1, b2, i2);
         if (t + 1 < tEnd) store_tile(buf ^ 1);
         __syncthreads();
     }
@@ -216,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void knn2_u8_kernel(const uint8_t* __rest
     int c1 = __shfl_xor(b1, 32), j1 = __shfl_xor(i1, 32), c2 = __shfl_xor(b2, 32), j2 = __shfl_xor(i2, 32);
     top2_merge(b1, i1, b2, i2, c1, j1, c2, j2);
     if (half == 0 && qrow < nA) {
-        const int cq = cqA[qrow];
+        const int cq = BITS ? 0 : cqA[qrow];
         const size_t o = ((size_t)blockIdx.y * nA + qrow) * 2;
         idxOut[o] = i1;
         idxOut[o + 1] = i2;
@@ -495,13 +566,22 @@ __global__ void nndr_kernel(int type, const int* __restrict__ idx, const int* __
 
 }  // namespace
 
-void launch_rowconst_u8(const uint8_t* X, int n, int nPad, int dimPad, int* c, hipStream_t s) {
-    if (nPad <= 0) return;
-    rowconst_u8_kernel<<<(nPad + 255) / 256, 256, 0, s>>>(X, n, nPad, dimPad, c);
+void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int* cq, int* ctp,
+                        hipStream_t s) {
+    const size_t threads = (size_t)(nA + nB) * (dimPad / 16);
+    if (threads == 0) return;
+    rowconst_u8_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(A, nA, B, nB, dimPad, cq, ctp);
 }
 
-void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, const int* cqA, const int* ctB,
-                    int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s) {
+void launch_unpack_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, uint8_t* outA, uint8_t* outB, int* ctp,
+                        hipStream_t s) {
+    if (nA + nB <= 0) return;
+    unpack_bits_kernel<<<((nA + nB) * 8 + 255) / 256, 256, 0, s>>>((const uint32_t*)A, nA, (const uint32_t*)B, nB,
+                                                                (int8_t*)outA, (int8_t*)outB, ctp);
+}
+
+void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int bits, const int* cqA,
+                    const int* ctB, int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s) {
     if (nA <= 0) return;
     size_t lds = 2 * (size_t)kT * dimPad + 2 * kT * sizeof(int);
     const int nTiles = (nB + kT - 1) / kT;
@@ -514,25 +594,34 @@ void launch_knn2_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
             (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         kernel<<<g, kThreads, lds, s>>>(A, nA, B, nB, dimPad, cqA, ctB, tilesPerPart, oi, ok);
     };
-    if (dimPad == 128)
-        go(knn2_u8_kernel<4>);
+    if (bits)
+        go(knn2_i8_kernel<8, true>);  // 32-byte binary rows unpacked to 256 int8
+    else if (dimPad == 128)
+        go(knn2_i8_kernel<4, false>);
     else if (dimPad == 256)
-        go(knn2_u8_kernel<8>);
+        go(knn2_i8_kernel<8, false>);
     else
-        go(knn2_u8_kernel<0>);
+        go(knn2_i8_kernel<0, false>);
     if (parts > 1) knn2_int_merge<<<(nA + 255) / 256, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
 }
 
 int knn2_u8_parts(int nA, int nB, int nCU) {
-    // split the train tiles only when the query blocks alone leave CUs idle (at 100k queries the
-    // extra staging of more, shorter blocks costs more than the balance gains: 3.96 vs 3.57 ms);
-    // each part keeps >= 16 tiles (2048 rows)
+    // Split the train tiles only when the 128-query blocks alone leave CUs idle (at 100k queries
+    // the extra staging of more, shorter blocks costs more than the balance gains).  Then aim at
+    // four blocks per CU, each part keeping >= 4 tiles: at 10k x 10k (79 query blocks) 16 parts
+    // take the u8 kernel 63 -> 29 us and the bits kernel 56 -> 43 us (rocprofv3, MI355X).
+    // FM3D_I8_PARTS overrides (tuning).
+    static const int forced = [] {
+        const char* e = getenv("FM3D_I8_PARTS");
+        return e ? atoi(e) : 0;
+    }();
     const int nBlk = (nA + kQ - 1) / kQ;
     const int nTiles = (nB + kT - 1) / kT;
+    if (forced > 0) return forced;
     if (nBlk <= 0 || nCU <= 0 || nBlk >= nCU) return 1;
-    int p = (nCU + nBlk - 1) / nBlk;
-    if (p > 8) p = 8;
-    while (p > 1 && nTiles / p < 16) p--;
+    int p = (4 * nCU + nBlk - 1) / nBlk;
+    if (p > 16) p = 16;
+    while (p > 1 && nTiles / p < 4) p--;
     return p;
 }
 

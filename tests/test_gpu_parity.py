@@ -520,6 +520,44 @@ def test_knn2_u8_train_parts_ties(fm3d, orc, ctx):
     assert idx[100, 0] == 3 and idx[100, 1] == 2304
 
 
+@pytest.mark.parametrize("mfma", ["1", "0"])
+@pytest.mark.parametrize("nA", [402, 3000])
+def test_knn2_bits_parts_and_ties(fm3d, orc, ctx, mfma, nA, monkeypatch):
+    """256-bit rows on the int8-MFMA kernel (unpacked bits, packed per-tile keys) and on the
+    popcount kernel: duplicated train rows inside one tile (different 32-row blocks), across tiles
+    and across parts, plus the many natural Hamming ties of random strings, must all resolve to the
+    lowest trainIdx for both neighbours."""
+    monkeypatch.setenv("FM3D_BITS_MFMA", mfma)
+    rng = np.random.default_rng(23 + nA)
+    nB = 9001
+    B = rng.integers(0, 256, (nB, 32), dtype=np.uint8)
+    B[115] = B[3]; B[125] = B[3]        # same tile, other row blocks (other chain)
+    B[5000:5100] = B[10:110]            # later tile / part
+    B[nB - 1] = B[3]; B[2304] = B[3]    # last partial tile, first row of a part
+    A = np.concatenate([B[10:110], B[[3, 3]], rng.integers(0, 256, (nA - 102, 32), dtype=np.uint8)])
+    got = fm3d.DescriptorsMatcher(ctx, binary=True).knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.BITS, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    assert np.array_equal(got["distance"], dist)
+    assert (idx[:100, 0] == np.arange(10, 110)).all() and (idx[:100, 1] == np.arange(5000, 5100)).all()
+    assert idx[100, 0] == 3 and idx[100, 1] == 115
+
+
+def test_knn2_u8_ties_inside_tile_chains(fm3d, orc, ctx):
+    """Equal distances at rows of the same 128-row tile held by the two epilogue chains (even and
+    odd 32-row blocks) and by the two lane halves: the packed per-tile key orders them by row."""
+    rng = np.random.default_rng(24)
+    B = rng.integers(0, 256, (700, 128), dtype=np.uint8)
+    for r in (36, 68, 100, 133, 165, 4, 5):
+        B[r] = B[1]
+    A = np.concatenate([B[[1, 36, 133]], rng.integers(0, 256, (200, 128), dtype=np.uint8)])
+    got = fm3d.DescriptorsMatcher(ctx).knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.U8, 1)
+    assert np.array_equal(got["trainIdx"], idx)
+    assert np.array_equal(got["distance"], dist)
+    assert list(got["trainIdx"][0]) == [1, 4]
+
+
 def test_knn2_integer_valued_f32_wider_than_u8_kernel(fm3d, orc, ctx):
     """Integer-valued f32 rows longer than the u8 kernel's 256 bytes stay on the f32 kernel."""
     rng = np.random.default_rng(22)

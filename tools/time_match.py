@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--kinds", default="surf64_f32,sift128_f32,sift128_u8,orb256_bits")
     args = ap.parse_args()
     rng = np.random.default_rng(3)
     n = args.n
@@ -31,6 +32,8 @@ def main():
     ctx = fm3d.Context(fm3d.Settings.default())
     try:
         for name, d in cases.items():
+            if name not in args.kinds.split(","):
+                continue
             m = fm3d.DescriptorsMatcher(ctx, binary=name.endswith("bits"))
             ts = []
             for _ in range(args.reps):
