@@ -433,6 +433,8 @@ void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_st
     st->last_group_start_ticks = (int64_t)(cnt[18] - cnt[20]);
     st->last_group_end_ticks = (int64_t)(cnt[19] - cnt[20]);
     st->cycles_wait = (int64_t)cnt[24];
+    st->chain_rounds = (int64_t)cnt[21];
+    st->chain_chunks = (int64_t)cnt[22];
 }
 
 // LM normals over nPts device points (c->pts), outputs in c->lm*

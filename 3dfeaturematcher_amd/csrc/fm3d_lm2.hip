@@ -467,6 +467,11 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
 // added.  Compiler barriers keep the reads in that order.  slow: the row's slow flag (entry
 // kE), read with the data and tested by the caller after the sum.
 __device__ __forceinline__ double chain_sum64(double sum, const double* row, double& slow) {
+#if FM3D_ABL_CHAIN
+    // ablation (timing experiments only, wrong sums): one add per chunk
+    slow = 0.;
+    return sum + row[0];
+#endif
     const double2* R = reinterpret_cast<const double2*>(row);
     double2 v0[4], v1[4], v2[4], v3[4];
     auto ld = [&](double2 (&v)[4], int k) {
@@ -658,7 +663,7 @@ __device__ __forceinline__ double chain_finish(int lane, double acc) {
 }
 
 __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, long long maxTicks,
-                                        unsigned long long* statBusy) {
+                                        unsigned long long* statBusy, unsigned long long* statRounds) {
     // the chain's dependent adds bound a pass's last chunk: let it issue first
     __builtin_amdgcn_s_setprio(3);
     const int s = lane >> 1, which = lane & 1;
@@ -668,7 +673,7 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
     bool inPass = false;
     double acc = 0.;  // running sum: enorm s2 (S_ENORM) or the dot product (S_DOT)
     // busy time: one clock read per busy round (the span to the next round's read)
-    unsigned long long busy = 0, tLast = 0;
+    unsigned long long busy = 0, tLast = 0, rounds = 0, chunks = 0;
     bool wasBusy = false;
     for (;;) {
         if ((long long)(wall_clock64() - tStart) > maxTicks) break;
@@ -694,6 +699,8 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
             // lane runs the same add chain (S_NONE lanes sum zeros they never publish)
             const int nb =
                 have ? ((rem >= 2 && lds_load_acq(&g_sh.rowTag[ss_][(cur + 1) & (kR - 1)]) == cur + 1) ? 2 : 1) : 0;
+            rounds++;
+            chunks += nb;
 #pragma nounroll
             for (int b = 0; b < 2; b++) {
                 if (b < nb) {
@@ -723,7 +730,12 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    if (lane == 0) atomicAdd(statBusy, busy);
+    if (lane == 0) {
+        atomicAdd(statBusy, busy);
+        atomicAdd(statRounds, rounds);
+    }
+    for (int o = 32; o > 0; o >>= 1) chunks += __shfl_xor(chunks, o);
+    if (lane == 0) atomicAdd(statRounds + 1, chunks);
 }
 
 }  // namespace
@@ -1244,7 +1256,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
             atomicAdd(p.statPass + 21, (unsigned long long)prod.waitCycles);
         }
     } else {
-        chain_wave(lane, tStart, p.maxTicks, p.statPass + 2);
+        chain_wave(lane, tStart, p.maxTicks, p.statPass + 2, p.statPass + 18);
     }
     // the group's lifetime: the chain wave leaves last (once every slot is done)
     if (wave == kW && lane == 0) {

@@ -118,6 +118,9 @@ typedef struct fm3d_lm_stats {
     int64_t last_group_start_ticks, last_group_end_ticks;
     /* term-wave cycles spent waiting on the chain lanes (ring full, pass results) */
     int64_t cycles_wait;
+    /* chain wave: busy rounds (each adds up to two chunks per lane) and chunks added, summed
+       over workgroups and lanes */
+    int64_t chain_rounds, chain_chunks;
 } fm3d_lm_stats;
 
 typedef struct fm3d_pipeline_stats {
