@@ -34,6 +34,7 @@ EXPORTS = (
     "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
+    "fm3d_circular_neighborhoods",
 )
 
 
@@ -54,6 +55,7 @@ class Settings(ctypes.Structure):
         ("pos1", ctypes.c_double * 6), ("pos2", ctypes.c_double * 6), ("boundWidth", ctypes.c_int),
         ("boundHeight", ctypes.c_int), ("strictNanExit", ctypes.c_int), ("lmWaves", ctypes.c_int),
         ("neighEpsilon", ctypes.c_double), ("cmPerPixel", ctypes.c_double),
+        ("neighMethod", ctypes.c_int), ("neighThetas", ctypes.c_int), ("neighRays", ctypes.c_int),
     ]
 
     @staticmethod
@@ -278,10 +280,34 @@ class SingleCameraTriangulator:
 
 
 class NeighborhoodsGenerator:
-    """NeighborhoodsGenerator (Triangulator/neighborhoodsgenerator.h:78-97), the square method."""
+    """NeighborhoodsGenerator (Triangulator/neighborhoodsgenerator.h:78-97): the square method and the
+    circular one (Neighborhoods.method; the reference constructor exits with -10 on anything else,
+    here ValueError)."""
 
     def __init__(self, settings: Settings):
+        if settings.neighMethod not in (0, 1):
+            raise ValueError("Unsupported method for plane neighborhood extraction")  # :69-73 exit(-10)
         self.settings = settings
+
+    def computeCircularNeighborhoodsByNormals(self, ctx: "Context", points, normals=None) -> np.ndarray:
+        """neighborhoodsgenerator.cpp:160-224: (P, thetas*rays, 3) samples on concentric circles in the
+        tangent plane of every point, ray outer / angle inner; normals None -> the initial guess X/|X|
+        (the reference fills its empty normals Mat the same way).  points / normals: (P, 3) (the
+        reference's 3 x N Mats, transposed).  Computed on the GPU of ctx."""
+        X = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        N = None if normals is None or len(normals) == 0 else np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 3)
+        if N is not None and N.shape != X.shape:
+            raise ValueError("normals and points differ in shape")
+        n, S = X.shape[0], self.settings.neighThetas * self.settings.neighRays
+        out = np.zeros((max(n, 1), max(S, 1), 3))
+        ctx.check(lib().fm3d_circular_neighborhoods(ctx.handle, _ptr(X), _ptr(N) if N is not None else None, n,
+                                                    _ptr(out)))
+        return out[:n, :S]
+
+    def computeCircularNeighborhoodByNormal(self, ctx: "Context", point, normal=(0.0, 0.0, 0.0)) -> np.ndarray:
+        """neighborhoodsgenerator.cpp:226-277 (one point; a zero normal -> X/|X|): (thetas*rays, 3)."""
+        nz = not any(float(v) != 0.0 for v in normal)
+        return self.computeCircularNeighborhoodsByNormals(ctx, [point], None if nz else [normal])[0]
 
     def size(self) -> int:
         return lib().fm3d_patch_size(ctypes.byref(self.settings))

@@ -1123,6 +1123,52 @@ int fm3d_square_neighborhoods(fm3d_ctx* c, const double* frames, int P, double* 
     return FM3D_OK;
 }
 
+int fm3d_circular_neighborhoods(fm3d_ctx* c, const double* points, const double* normals, int P, double* out) {
+    if (!c || P < 0 || (P && (!points || !out))) return FM3D_ERR_INVALID;
+    if (c->s.neighMethod != 1) return fail(c, FM3D_ERR_INVALID, "Neighborhoods.method is not circular");
+    const int T = c->s.neighThetas, Rn = c->s.neighRays;
+    if (T <= 0 || Rn <= 0) return fail(c, FM3D_ERR_INVALID, "Neighborhoods.thetas / rays <= 0");
+    if (P == 0) return FM3D_OK;
+    hipSetDevice(c->device);
+    // the constructor's lookup table (neighborhoodsgenerator.cpp:50-64), libm sin as the reference
+    const double eps = c->s.neighEpsilon;
+    const double rayIncrement = eps / Rn, thetaIncrement = 2 * M_PI / T;
+    const int S = T * Rn;
+    std::vector<double> lut((size_t)S * 3);
+    for (int i = 1; i <= Rn; i++)
+        for (int j = 0; j < T; j++) {
+            const double t = j * thetaIncrement;
+            double* e = &lut[3 * ((size_t)(i - 1) * T + j)];
+            e[0] = (double)i * rayIncrement;
+            e[1] = std::sin(t);
+            e[2] = 2 * (std::sin(t / 2)) * (std::sin(t / 2));
+        }
+    // chunks of points bound the device buffer (~512 MB of samples)
+    const size_t perPoint = (size_t)S * 3 * sizeof(double);
+    const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)P, ((size_t)512 << 20) / perPoint));
+    DevBuf L, X, N, O;
+    HIPCHK(c, L.ensure(lut.size() * sizeof(double)));
+    HIPCHK(c, X.ensure((size_t)chunk * 3 * sizeof(double)));
+    if (normals) HIPCHK(c, N.ensure((size_t)chunk * 3 * sizeof(double)));
+    HIPCHK(c, O.ensure((size_t)chunk * perPoint));
+    HIPCHK(c, hipMemcpyAsync(L.p, lut.data(), lut.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    for (int p0 = 0; p0 < P; p0 += chunk) {
+        const int n = std::min(chunk, P - p0);
+        HIPCHK(c, hipMemcpyAsync(X.p, points + (size_t)3 * p0, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice,
+                                 c->stream));
+        if (normals)
+            HIPCHK(c, hipMemcpyAsync(N.p, normals + (size_t)3 * p0, (size_t)n * 3 * sizeof(double),
+                                     hipMemcpyHostToDevice, c->stream));
+        fm3d::launch_circular_neighborhoods(X.as<double>(), normals ? N.as<double>() : nullptr, n, S, L.as<double>(),
+                                            eps, O.as<double>(), c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(out + (size_t)p0 * S * 3, O.p, (size_t)n * perPoint, hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return FM3D_OK;
+}
+
 int fm3d_pyrdown(fm3d_ctx* c, const uint8_t* src, int width, int height, uint8_t* dst) {
     if (!c || !src || !dst || width <= 0 || height <= 0) return FM3D_ERR_INVALID;
     hipSetDevice(c->device);

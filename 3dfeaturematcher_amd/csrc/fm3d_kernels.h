@@ -132,6 +132,10 @@ void launch_undistort(const Camera& cam, const double* xy, int n, double* out, h
 void launch_features_frames(const double* pts, const double* nrm, int P, const double g[3], double* frames,
                             hipStream_t s);
 // computeSquareNeighborhoodsByNormals: out P*size*size*3 doubles (device)
+// computeCircularNeighborhoodsByNormals: P points (P*3), normals (P*3 or NULL: X/|X|), S samples per
+// point from lut (S*3: r, sin t, 2 sin^2(t/2)) -> out P*S*3
+void launch_circular_neighborhoods(const double* pts, const double* nrm, int P, int S, const double* lut, double eps,
+                                   double* out, hipStream_t s);
 void launch_square_neighborhoods(const double* frames, int P, int size, double eps, double inc, double* out,
                                  hipStream_t s);
 // RT: 12 doubles of scratch per frame

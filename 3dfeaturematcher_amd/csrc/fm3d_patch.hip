@@ -14,7 +14,9 @@
 //                        of image 1, (uchar) bilinear sample, written transposed (patch.at(col, row));
 //   square_neighborhoods_kernel  NeighborhoodsGenerator::computeSquareNeighborhoodsByNormals
 //                        (neighborhoodsgenerator.cpp:76-132, main.cpp:187): the square grid through
-//                        every frame, 24 B written per point (HBM-bound, 5.3 TB/s).
+//                        every frame, 24 B written per point (HBM-bound, 5.3 TB/s);
+//   circular_neighborhoods_kernel  NeighborhoodsGenerator::computeCircularNeighborhoodsByNormals
+//                        (neighborhoodsgenerator.cpp:160-224): one thread per (point, sample).
 // Every output byte depends on one projected sample; the patch kernel is a projection + gather
 // bound by the fp64 VALU (≈60 fp64 ops per sample) -- there is no reduction and no data reuse
 // beyond the image in L2.
@@ -227,7 +229,73 @@ __global__ __launch_bounds__(kSqThreads) void square_neighborhoods_kernel(const 
     }
 }
 
+// ---------------- circular neighbourhoods (neighborhoodsgenerator.cpp:160-277)
+// Matx33d * Vec3d / Matx33d * Matx33d as OpenCV's Matx_MatMulOp: s = 0; s += a(i,k)*b(k,j) in k order
+__device__ inline void matvec3(const double A[9], const double v[3], double o[3]) {
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += A[3 * i + k] * v[k];
+        o[i] = s;
+    }
+}
+
+// one thread per (point, sample): the spanner, W = skew(n) (tools.cpp:122-127) and the sample
+// X + r*((s + (W*s)*st) + ((st2*W)*W)*s), each operation in the reference's Matx / Vec order.  lut:
+// (r, sin t, 2 sin^2(t/2)) per sample, built on the host by the constructor's formulas (:50-64).
+__global__ __launch_bounds__(256) void circular_neighborhoods_kernel(const double* __restrict__ pts,
+                                                                     const double* __restrict__ nrm, long long total,
+                                                                     int S, const double* __restrict__ lut, double eps,
+                                                                     double* __restrict__ out) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    const long long p = t / S;
+    const int k = (int)(t - p * S);
+    const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
+    double n[3];
+    if (nrm) {
+        n[0] = nrm[3 * p];
+        n[1] = nrm[3 * p + 1];
+        n[2] = nrm[3 * p + 2];
+    } else {
+        // normal = point / cv::norm(point): Vec / double multiplies by the reciprocal
+        double q = 0;
+        for (int i = 0; i < 3; i++) q += X[i] * X[i];
+        const double inv = 1. / sqrt(q);
+        for (int i = 0; i < 3; i++) n[i] = X[i] * inv;
+    }
+    // spanner(0, 1, -n1/n2); spanner / cv::norm(spanner) * epsilon
+    double sp[3] = {0., 1., -n[1] / n[2]};
+    double q = 0;
+    for (int i = 0; i < 3; i++) q += sp[i] * sp[i];
+    const double inv = 1. / sqrt(q);
+    for (int i = 0; i < 3; i++) sp[i] = sp[i] * inv * eps;
+    const double W[9] = {0, -n[2], n[1], n[2], 0, -n[0], -n[1], n[0], 0};
+    const double r = lut[3 * k], st = lut[3 * k + 1], st2 = lut[3 * k + 2];
+    double Ws[3], sW[9], M[9], B[3];
+    matvec3(W, sp, Ws);
+    for (int i = 0; i < 9; i++) sW[i] = W[i] * st2;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int l = 0; l < 3; l++) s += sW[3 * i + l] * W[3 * l + j];
+            M[3 * i + j] = s;
+        }
+    matvec3(M, sp, B);
+    double* o = out + 3 * t;
+    for (int i = 0; i < 3; i++) {
+        const double v = (sp[i] + Ws[i] * st) + B[i];
+        o[i] = X[i] + v * r;
+    }
+}
+
 }  // namespace
+
+void launch_circular_neighborhoods(const double* pts, const double* nrm, int P, int S, const double* lut, double eps,
+                                   double* out, hipStream_t s) {
+    const long long total = (long long)P * S;
+    if (total <= 0) return;
+    circular_neighborhoods_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(pts, nrm, total, S, lut, eps, out);
+}
 
 void launch_square_neighborhoods(const double* frames, int P, int size, double eps, double inc, double* out,
                                  hipStream_t s) {

@@ -127,6 +127,9 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->lmWaves = 0;
     s->neighEpsilon = 0.16;  // build/settings.yml Neighborhoods
     s->cmPerPixel = 0.25;
+    s->neighMethod = 0;      // method: square
+    s->neighThetas = 15;     // the commented-out circular values of build/settings.yml
+    s->neighRays = 5;
     return FM3D_OK;
 }
 
@@ -154,6 +157,16 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
     get_d(kv, "NNDR.epsilon", &s->nndrEpsilon);
     get_d(kv, "Neighborhoods.epsilon", &s->neighEpsilon);
     get_d(kv, "Neighborhoods.cmPerPixel", &s->cmPerPixel);
+    {
+        auto it = kv.find("Neighborhoods.method");
+        if (it != kv.end()) {
+            std::string m = it->second;
+            if (m.size() >= 2 && (m[0] == '"' || m[0] == '\'') && m.back() == m[0]) m = m.substr(1, m.size() - 2);
+            s->neighMethod = m == "square" ? 0 : (m == "circular" ? 1 : -1);
+        }
+    }
+    get_i(kv, "Neighborhoods.thetas", &s->neighThetas);
+    get_i(kv, "Neighborhoods.rays", &s->neighRays);
     get_vec(kv, "IMAGES.pos1", s->pos1, 6);
     get_vec(kv, "IMAGES.pos2", s->pos2, 6);
     // extensions (optional section)

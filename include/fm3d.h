@@ -68,6 +68,9 @@ typedef struct fm3d_settings {
     int lmWaves;                 /* LM workgroups to launch (0 = fill the GPU) */
     /* Neighborhoods.epsilon / cmPerPixel (neighborhoodsgenerator.cpp:43-44): patch export */
     double neighEpsilon, cmPerPixel;
+    /* Neighborhoods.method (neighborhoodsgenerator.cpp:38-73): 0 square, 1 circular, -1 anything
+       else (the reference's exit(-10)); thetas / rays of the circular method (:47-48) */
+    int neighMethod, neighThetas, neighRays;
 } fm3d_settings;
 
 /* cv::DMatch layout */
@@ -206,6 +209,15 @@ int fm3d_export_patches(fm3d_ctx *ctx, const double *frames, int P, uint8_t *pat
    inc = 0.01*cmPerPixel, transformed by the frame (Matx44d * Vec4d; scaled by 1/w when w != 1).
    out: P*size*size*3 doubles, point order i*size + j (host buffer; computed in HBM in chunks). */
 int fm3d_square_neighborhoods(fm3d_ctx *ctx, const double *frames, int P, double *out);
+/* NeighborhoodsGenerator::computeCircularNeighborhoodsByNormals (neighborhoodsgenerator.cpp:160-224;
+   the single-point computeCircularNeighborhoodByNormal :226-277 is P = 1): per point thetas*rays
+   samples X + r_i*(s + (W s) sin t_j + 2 sin^2(t_j/2) (W W s)) with the constructor's lookup table
+   (:50-64), s = epsilon*(0, 1, -n1/n2)/|(0, 1, -n1/n2)|, W = skew(n), in Matx / Vec operation order.
+   points: P*3 doubles (the reference's 3 x N Mat, transposed); normals: P*3 doubles, or NULL for the
+   initial guess X/|X| (the reference's empty-normals branch, :167-183).  out: P*thetas*rays*3
+   doubles, sample order (ray outer, angle inner).  FM3D_ERR_INVALID unless neighMethod is circular
+   (the reference constructor reads thetas / rays only then). */
+int fm3d_circular_neighborhoods(fm3d_ctx *ctx, const double *points, const double *normals, int P, double *out);
 
 /* ---------------- the whole hot path, device resident ---------------- */
 /* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */

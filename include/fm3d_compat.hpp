@@ -24,6 +24,8 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <cstdlib>
+#include <cstdio>
 #include <vector>
 
 #include "fm3d.h"
@@ -90,10 +92,47 @@ private:
     fm3d_settings settings_;
 };
 
-// NeighborhoodsGenerator (neighborhoodsgenerator.h:78-97), the square method
+// NeighborhoodsGenerator (neighborhoodsgenerator.h:78-97), the square and the circular methods
 class NeighborhoodsGenerator {
 public:
-    explicit NeighborhoodsGenerator(const fm3d_settings& s) : s_(s) {}
+    // neighborhoodsgenerator.cpp:36-74: an unsupported Neighborhoods.method ends the program with -10
+    explicit NeighborhoodsGenerator(const fm3d_settings& s) : s_(s) {
+        if (s_.neighMethod != 0 && s_.neighMethod != 1) {
+            std::fprintf(stderr, "Unsupported method for plane neighborhood extraction\n");
+            std::exit(-10);
+        }
+    }
+    // computeCircularNeighborhoodsByNormals (neighborhoodsgenerator.cpp:160-224): per point
+    // thetas*rays samples (ray outer, angle inner) on d's GPU; empty normals are filled with the
+    // initial guess X/|X| as the reference does (its normals Mat is an in/out parameter)
+    void computeCircularNeighborhoodsByNormals(Device& d, const std::vector<Vec3d>& points, std::vector<Vec3d>& normals,
+                                               std::vector<std::vector<Vec3d> >& neighborhoodsVector) const {
+        const size_t S = (size_t)s_.neighThetas * s_.neighRays;
+        if (normals.empty())
+            for (const Vec3d& X : points) {
+                double q = 0;
+                for (int i = 0; i < 3; i++) q += X[i] * X[i];
+                const double inv = 1. / std::sqrt(q);
+                normals.push_back(Vec3d{X[0] * inv, X[1] * inv, X[2] * inv});
+            }
+        std::vector<Vec3d> all(points.size() * S);
+        if (!points.empty())
+            check(d.ctx(), fm3d_circular_neighborhoods(d.ctx(), points.data()->data(), normals.data()->data(),
+                                                       (int)points.size(), all.data()->data()));
+        for (size_t p = 0; p < points.size(); p++)  // appended, as the reference push_backs
+            neighborhoodsVector.emplace_back(all.begin() + p * S, all.begin() + (p + 1) * S);
+    }
+    // computeCircularNeighborhoodByNormal (neighborhoodsgenerator.cpp:226-277): a zero normal is
+    // replaced by X/|X| (in/out), then the samples of that one point
+    void computeCircularNeighborhoodByNormal(Device& d, const Vec3d& point, Vec3d& normal,
+                                             std::vector<Vec3d>& neighborhood) const {
+        std::vector<Vec3d> pts{point}, nrm;
+        if (!(normal[0] == 0 && normal[1] == 0 && normal[2] == 0)) nrm.push_back(normal);
+        std::vector<std::vector<Vec3d> > out;
+        computeCircularNeighborhoodsByNormals(d, pts, nrm, out);
+        normal = nrm[0];
+        neighborhood = out[0];
+    }
     // getReferenceSquaredNeighborhood (neighborhoodsgenerator.cpp:134-158): cleared, then size^2
     // points (-epsilon + inc*i, -epsilon + inc*j, 0), i outer
     void getReferenceSquaredNeighborhood(std::vector<Vec3d>& neighborhood) const {

@@ -19,7 +19,7 @@
  *                                                             compareWithNNDR :55-77)
  *   SingleCameraTriangulator  singlecameratriangulator.h:52-93
  *   NormalOptimizer           normaloptimizer.h:43-59
- *   NeighborhoodsGenerator    neighborhoodsgenerator.h:78-97 (square method)
+ *   NeighborhoodsGenerator    neighborhoodsgenerator.h:78-97 (square and circular methods)
  *
  * What differs, and why:
  *   - feature detection/description (descriptorsmatcher.cpp:110-115) is upstream of the GPU path
@@ -60,6 +60,7 @@
 #define CV_32FC1 5
 #define CV_64FC1 6
 #define CV_64FC2 14
+#define CV_64FC3 22
 #endif
 #ifndef CV_LOAD_IMAGE_GRAYSCALE
 #define CV_LOAD_IMAGE_GRAYSCALE 0
@@ -634,7 +635,7 @@ private:
     fm3d::compat::NormalOptimizer no_;
 };
 
-// ---------------------------------------------------------------- NeighborhoodsGenerator (square)
+// ---------------------------------------------------------------- NeighborhoodsGenerator
 class NeighborhoodsGenerator {
 public:
     explicit NeighborhoodsGenerator(cv::FileStorage settings) : s_(settings.settings()), ng_(s_) {}
@@ -662,7 +663,45 @@ public:
         }
     }
 
+    // neighborhoodsgenerator.cpp:160-224: points / normals are 3 x N CV_64F Mats (column = point);
+    // an empty normals Mat is filled with the initial guess; one 1 x (thetas*rays) CV_64FC3 Mat per
+    // point is appended
+    void computeCircularNeighborhoodsByNormals(const cv::Mat& points, cv::Mat& normals,
+                                               std::vector<cv::Mat>& neighborhoodsVector) {
+        const int n = points.cols;
+        std::vector<fm3d::compat::Vec3d> P(n), N;
+        for (int i = 0; i < n; i++)
+            for (int k = 0; k < 3; k++) P[i][k] = points.at<double>(k, i);
+        if (!normals.empty()) {
+            N.resize(n);
+            for (int i = 0; i < n; i++)
+                for (int k = 0; k < 3; k++) N[i][k] = normals.at<double>(k, i);
+        }
+        std::vector<std::vector<fm3d::compat::Vec3d> > out;
+        ng_.computeCircularNeighborhoodsByNormals(fm3d::cvshim::device(s_), P, N, out);
+        if (normals.empty()) {
+            normals = cv::Mat::zeros(cv::Size(n, 3), CV_64FC1);
+            for (int i = 0; i < n; i++)
+                for (int k = 0; k < 3; k++) normals.at<double>(k, i) = N[i][k];
+        }
+        for (const auto& nb : out) neighborhoodsVector.push_back(to_mat(nb));
+    }
+    // neighborhoodsgenerator.cpp:226-277
+    void computeCircularNeighborhoodByNormal(const cv::Vec3d& point, cv::Vec3d& normal, cv::Mat& neighborhood) {
+        fm3d::compat::Vec3d X{point[0], point[1], point[2]}, nn{normal[0], normal[1], normal[2]};
+        std::vector<fm3d::compat::Vec3d> nb;
+        ng_.computeCircularNeighborhoodByNormal(fm3d::cvshim::device(s_), X, nn, nb);
+        normal = cv::Vec3d(nn[0], nn[1], nn[2]);
+        neighborhood = to_mat(nb);
+    }
+
 private:
+    static cv::Mat to_mat(const std::vector<fm3d::compat::Vec3d>& nb) {
+        cv::Mat m = cv::Mat::zeros(cv::Size((int)nb.size(), 1), CV_64FC3);
+        for (size_t s = 0; s < nb.size(); s++)
+            for (int k = 0; k < 3; k++) reinterpret_cast<double*>(m.data)[3 * s + k] = nb[s][k];
+        return m;
+    }
     fm3d_settings s_;
     fm3d::compat::NeighborhoodsGenerator ng_;
 };

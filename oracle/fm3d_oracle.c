@@ -1339,6 +1339,79 @@ ORC_API int orc_square_neighborhoods(const double *frames, int P, double eps, do
     return size;
 }
 
+/* NeighborhoodsGenerator circular method.  The constructor's lookup table
+   (neighborhoodsgenerator.cpp:50-64): for ray i = 1..rays (outer), angle j = 0..thetas-1 (inner):
+   r = i * (eps/rays), t = j * (2*pi/thetas), st = sin(t), st2 = 2*sin(t/2)*sin(t/2) (libm).
+   computeCircularNeighborhoodsByNormals (:160-224): normals NULL -> n = X * (1/norm(X)) (the
+   empty-normals branch, Vec / double); spanner = (0, 1, -n1/n2) * (1/norm) * eps; W = skew(n)
+   (tools.cpp:122-127); sample = X + r * ((spanner + (W*spanner)*st) + ((st2*W)*W)*spanner), every
+   Matx product summed from 0 in k order (Matx_MatMulOp), norms as normL2Sqr from 0.
+   points / normals: P*3; out: P*thetas*rays*3, sample order ray outer, angle inner. */
+ORC_API int orc_circular_neighborhoods(const double *points, const double *normals, int P, double eps, int thetas,
+                                       int rays, double *out)
+{
+    const int S = thetas * rays;
+    const double rayIncrement = eps / rays, thetaIncrement = 2 * M_PI / thetas;
+    double *lut;
+    int p, i, j;
+    if (thetas <= 0 || rays <= 0) return -1;
+    lut = (double *)malloc(sizeof(double) * 3 * (size_t)S);
+    for (i = 1; i <= rays; i++)
+        for (j = 0; j < thetas; j++) {
+            const double t = j * thetaIncrement;
+            double *e = lut + 3 * ((size_t)(i - 1) * thetas + j);
+            e[0] = (double)i * rayIncrement;
+            e[1] = sin(t);
+            e[2] = 2 * (sin(t / 2)) * (sin(t / 2));
+        }
+    #pragma omp parallel for schedule(static)
+    for (p = 0; p < P; p++) {
+        const double *X = points + 3 * (size_t)p;
+        double n[3], sp[3], W[9], Ws[3], sW[9], M[9], B[3], q, inv;
+        int k, a, b, c;
+        if (normals) {
+            n[0] = normals[3 * (size_t)p]; n[1] = normals[3 * (size_t)p + 1]; n[2] = normals[3 * (size_t)p + 2];
+        } else {
+            q = 0;
+            for (a = 0; a < 3; a++) q += X[a] * X[a];
+            inv = 1. / sqrt(q);
+            for (a = 0; a < 3; a++) n[a] = X[a] * inv;
+        }
+        sp[0] = 0.; sp[1] = 1.; sp[2] = -n[1] / n[2];
+        q = 0;
+        for (a = 0; a < 3; a++) q += sp[a] * sp[a];
+        inv = 1. / sqrt(q);
+        for (a = 0; a < 3; a++) sp[a] = sp[a] * inv * eps;
+        W[0] = 0;     W[1] = -n[2]; W[2] = n[1];
+        W[3] = n[2];  W[4] = 0;     W[5] = -n[0];
+        W[6] = -n[1]; W[7] = n[0];  W[8] = 0;
+        for (a = 0; a < 3; a++) {
+            double s = 0;
+            for (c = 0; c < 3; c++) s += W[3 * a + c] * sp[c];
+            Ws[a] = s;
+        }
+        for (k = 0; k < S; k++) {
+            const double r = lut[3 * k], st = lut[3 * k + 1], st2 = lut[3 * k + 2];
+            double *o = out + ((size_t)p * S + k) * 3;
+            for (a = 0; a < 9; a++) sW[a] = W[a] * st2;
+            for (a = 0; a < 3; a++)
+                for (b = 0; b < 3; b++) {
+                    double s = 0;
+                    for (c = 0; c < 3; c++) s += sW[3 * a + c] * W[3 * c + b];
+                    M[3 * a + b] = s;
+                }
+            for (a = 0; a < 3; a++) {
+                double s = 0;
+                for (c = 0; c < 3; c++) s += M[3 * a + c] * sp[c];
+                B[a] = s;
+            }
+            for (a = 0; a < 3; a++) o[a] = X[a] + ((sp[a] + Ws[a] * st) + B[a]) * r;
+        }
+    }
+    free(lut);
+    return S;
+}
+
 /* cvRodrigues2 round trip of decomposeTransformation + cvProjectPoints2, with libm (mode 0) or
    the deterministic transcendentals (mode ORC_LM_DETMATH; acos(c) = atan2(sqrt((1-c)(1+c)), c)). */
 static void orc_frame_camera(const double F[16], int mode, double R2[9], double t2[3])

@@ -246,6 +246,18 @@ def square_neighborhoods(frames, eps=0.16, cmpp=0.25):
     return out
 
 
+def circular_neighborhoods(points, normals=None, eps=0.16, thetas=15, rays=5):
+    """computeCircularNeighborhoodsByNormals (neighborhoodsgenerator.cpp:160-224): (P, thetas*rays, 3);
+    normals None -> the initial guess X/|X|."""
+    X = _f64(points).reshape(-1, 3)
+    n = X.shape[0]
+    N = _f64(normals).reshape(-1, 3) if normals is not None else None
+    out = np.zeros((n, thetas * rays, 3))
+    lib().orc_circular_neighborhoods(_p(X), _p(N) if N is not None else None, ctypes.c_int(n), ctypes.c_double(eps),
+                                     ctypes.c_int(thetas), ctypes.c_int(rays), _p(out))
+    return out
+
+
 def export_patches(cam, img1, frames, eps=0.16, cmpp=0.25, mode=STRICT, image_points=False):
     img1 = np.ascontiguousarray(img1, dtype=np.uint8)
     h, w = img1.shape

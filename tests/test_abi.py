@@ -64,7 +64,7 @@ def test_library_exports_every_header_symbol(fm3d):
 def test_struct_layouts(fm3d):
     assert fm3d.DMATCH.itemsize == 16          # cv::DMatch
     assert fm3d.RECORD.itemsize == 64
-    assert ctypes.sizeof(fm3d.Settings) == 8 * 9 + 8 * 6 + 8 * 3 + 4 * 2 + 8 + 8 * 12 + 4 * 4 + 8 * 2
+    assert ctypes.sizeof(fm3d.Settings) == (8 * 9 + 8 * 6 + 8 * 3 + 4 * 2 + 8 + 8 * 12 + 4 * 4 + 8 * 2 + 4 * 3 + 7) // 8 * 8
 
 
 def test_settings_default_is_reference_file(fm3d):
@@ -82,8 +82,24 @@ def test_settings_yaml_subset(fm3d, tmp_path):
     assert list(s.pos2) == [4.735536, 7.691893, 1.913166, 0.252828, 0.048977, -2.676886]
     assert list(s.translationIC) == [0.0, 0.015, -0.051]
     assert s.k0 == -0.299957 and s.zThresholdMax == 2.4
+    assert (s.neighMethod, s.neighThetas, s.neighRays) == (0, 15, 5)
     with pytest.raises(fm3d.Fm3dError):
         fm3d.Settings.load(str(tmp_path / "missing.yml"))
+
+
+def test_settings_neighborhood_method(fm3d, tmp_path):
+    """Neighborhoods.method / thetas / rays (neighborhoodsgenerator.cpp:38-73): circular reads its two
+    counts; any other method is the reference's exit(-10), here a ValueError of the generator."""
+    p = tmp_path / "settings.yml"
+    p.write_text(SETTINGS_YML.replace("method: square", "method: circular\n   thetas: 12\n   rays: 4"))
+    s = fm3d.Settings.load(str(p))
+    assert (s.neighMethod, s.neighThetas, s.neighRays) == (1, 12, 4)
+    fm3d.NeighborhoodsGenerator(s)
+    p.write_text(SETTINGS_YML.replace("method: square", "method: hexagonal"))
+    s = fm3d.Settings.load(str(p))
+    assert s.neighMethod == -1
+    with pytest.raises(ValueError):
+        fm3d.NeighborhoodsGenerator(s)
 
 
 def test_g12_host_algebra_bitwise_vs_oracle(fm3d, orc):

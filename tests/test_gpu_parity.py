@@ -446,6 +446,29 @@ def test_square_neighborhoods_bitwise(fm3d, orc, pair):
 
 
 # ---------------------------------------------------------------- BASELINE configs as parity cases
+@pytest.mark.parametrize("given_normals", [True, False])
+def test_circular_neighborhoods_bitwise(fm3d, orc, pair, given_normals):
+    """computeCircularNeighborhoodsByNormals (neighborhoodsgenerator.cpp:160-224) on the GPU against the
+    oracle, bit for bit: triangulated points of the frame pair with their LM-free initial normals
+    perturbed (given) or the empty-normals branch (X/|X|), the reference's 15 x 5 samples."""
+    rng = np.random.default_rng(32)
+    X = np.stack([rng.uniform(-0.6, 0.6, 700), rng.uniform(-0.4, 0.4, 700), rng.uniform(1.6, 2.3, 700)], 1)
+    N = X + rng.normal(0, 0.3, X.shape)
+    N /= np.linalg.norm(N, axis=1, keepdims=True)
+    s = _settings(fm3d, pair.cam, neighMethod=1, neighThetas=15, neighRays=5)
+    ctx = fm3d.Context(s)
+    try:
+        ng = fm3d.NeighborhoodsGenerator(s)
+        got = ng.computeCircularNeighborhoodsByNormals(ctx, X, N if given_normals else None)
+        ref = orc.circular_neighborhoods(X, N if given_normals else None, s.neighEpsilon, 15, 5)
+        assert got.shape == (700, 75, 3) and np.array_equal(got, ref)
+        one = ng.computeCircularNeighborhoodByNormal(ctx, X[3], N[3] if given_normals else (0.0, 0.0, 0.0))
+        assert np.array_equal(one, ref[3])
+        assert ng.computeCircularNeighborhoodsByNormals(ctx, np.zeros((0, 3))).shape == (0, 75, 3)
+    finally:
+        ctx.close()
+
+
 def test_c2_sift10k_match_and_dlt(fm3d, orc, synth):
     """BASELINE configs[1] (C2): 10k SIFT-128 per frame, brute-force L2 match + NNDR + DLT --
     match indices, distances, inlier mask and points bit-exact against the oracle."""

@@ -152,6 +152,59 @@ def test_square_neighborhoods_vs_numpy(orc):
     assert not np.array_equal(out[-1][:, :3], out[-1][:, :3] * 0)  # the w != 1 frame produced points
 
 
+def _circular_numpy(X, N, eps, thetas, rays):
+    """numpy restatement of neighborhoodsgenerator.cpp:50-64 + 160-224 with OpenCV's scalar
+    operation order (Matx products summed from 0 in k order, Vec / double = * (1/d))."""
+    import math
+    lut = []
+    for i in range(1, rays + 1):
+        for j in range(thetas):
+            t = j * (2 * math.pi / thetas)
+            lut.append((i * (eps / rays), math.sin(t), 2 * math.sin(t / 2) * math.sin(t / 2)))
+    out = np.zeros((len(X), len(lut), 3))
+    for p, x in enumerate(X):
+        if N is None:
+            q = ((0.0 + x[0] * x[0]) + x[1] * x[1]) + x[2] * x[2]
+            inv = 1.0 / math.sqrt(q)
+            n = [x[0] * inv, x[1] * inv, x[2] * inv]
+        else:
+            n = list(N[p])
+        sp = [0.0, 1.0, -n[1] / n[2]]
+        q = ((0.0 + sp[0] * sp[0]) + sp[1] * sp[1]) + sp[2] * sp[2]
+        inv = 1.0 / math.sqrt(q)
+        sp = [v * inv * eps for v in sp]
+        W = [[0.0, -n[2], n[1]], [n[2], 0.0, -n[0]], [-n[1], n[0], 0.0]]
+        Ws = [((0.0 + W[a][0] * sp[0]) + W[a][1] * sp[1]) + W[a][2] * sp[2] for a in range(3)]
+        for k, (r, st, st2) in enumerate(lut):
+            sW = [[W[a][b] * st2 for b in range(3)] for a in range(3)]
+            M = [[((0.0 + sW[a][0] * W[0][b]) + sW[a][1] * W[1][b]) + sW[a][2] * W[2][b] for b in range(3)]
+                 for a in range(3)]
+            B = [((0.0 + M[a][0] * sp[0]) + M[a][1] * sp[1]) + M[a][2] * sp[2] for a in range(3)]
+            out[p, k] = [x[a] + ((sp[a] + Ws[a] * st) + B[a]) * r for a in range(3)]
+    return out
+
+
+def test_circular_neighborhoods_vs_numpy(orc):
+    """computeCircularNeighborhoodsByNormals (neighborhoodsgenerator.cpp:160-224): the oracle against
+    the numpy restatement bit for bit, with given normals and with the X/|X| initial guess; the
+    samples lie on circles of radius r*eps in the plane through X orthogonal to n."""
+    rng = np.random.default_rng(31)
+    X = np.stack([rng.uniform(-0.5, 0.5, 12), rng.uniform(-0.4, 0.4, 12), rng.uniform(1.6, 2.3, 12)], 1)
+    Nn = X + rng.normal(0, 0.2, X.shape)
+    Nn /= np.linalg.norm(Nn, axis=1, keepdims=True)
+    for N, thetas, rays, eps in ((Nn, 15, 5, 0.16), (None, 7, 3, 0.05), (Nn, 1, 1, 0.3)):
+        out = orc.circular_neighborhoods(X, N, eps, thetas, rays)
+        assert out.shape == (len(X), thetas * rays, 3)
+        assert np.array_equal(out, _circular_numpy(X, N, eps, thetas, rays))
+        n = N if N is not None else X / np.linalg.norm(X, axis=1, keepdims=True)
+        d = out - X[:, None, :]
+        assert np.abs(np.einsum("pkc,pc->pk", d, n)).max() < 1e-12            # in the tangent plane
+        # on circles of radius r * eps: r = i * eps / rays already carries epsilon and the spanner is
+        # scaled to epsilon as well (the reference's own double scaling)
+        radii = np.repeat(np.arange(1, rays + 1) * (eps / rays), thetas) * eps
+        assert np.abs(np.linalg.norm(d, axis=2) - radii[None, :]).max() < 1e-12
+
+
 def test_reference_patch_size():
     """build/settings.yml (Neighborhoods epsilon 0.16, cmPerPixel 0.25) gives the 128x128 patches
     of the reference's results/*/patch_*.pgm (P5 128 128)."""
