@@ -34,7 +34,7 @@ EXPORTS = (
     "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
-    "fm3d_circular_neighborhoods",
+    "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
 )
 
 
@@ -56,6 +56,9 @@ class Settings(ctypes.Structure):
         ("boundHeight", ctypes.c_int), ("strictNanExit", ctypes.c_int), ("lmWaves", ctypes.c_int),
         ("neighEpsilon", ctypes.c_double), ("cmPerPixel", ctypes.c_double),
         ("neighMethod", ctypes.c_int), ("neighThetas", ctypes.c_int), ("neighRays", ctypes.c_int),
+        ("detectorType", ctypes.c_int), ("extractorType", ctypes.c_int), ("surfHessianThreshold", ctypes.c_double),
+        ("surfOctaves", ctypes.c_int), ("surfOctaveLayers", ctypes.c_int), ("surfExtended", ctypes.c_int),
+        ("surfUpright", ctypes.c_int),
     ]
 
     @staticmethod
@@ -80,6 +83,8 @@ class Settings(ctypes.Structure):
 
 
 DMATCH = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
+KEYPOINT = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                     ("octave", "<i4"), ("class_id", "<i4")])  # cv::KeyPoint (fm3d_keypoint)
 RECORD = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("distance", "<f4"), ("status", "<i4"),
                    ("point", "<f8", (3,)), ("normal", "<f8", (3,))])
 
@@ -208,6 +213,17 @@ class DescriptorsMatcher:
                                        _desc_type(a, self.binary), _vp(out)))
         return out
 
+    def compareWithNNDRImages(self, epsilon: float, image_a: np.ndarray, image_b: np.ndarray,
+                              matches: np.ndarray | None = None):
+        """compareWithNNDR (descriptorsmatcher.cpp:107-131) with the detection it starts with: SURF
+        detect + compute on both images (the settings' detector / extractor, on the GPU), knnMatch,
+        NNDR.  Returns (matches appended as the reference does, kpts_a, kpts_b, desc_a, desc_b)."""
+        surf = SURF(self.ctx)
+        ka, da = surf.detect(image_a, with_descriptors=True)
+        kb, db = surf.detect(image_b, with_descriptors=True)
+        m = self.compareWithNNDR(epsilon, da, db, matches)
+        return m, ka, kb, da, db
+
     def compareWithNNDR(self, epsilon: float, desc_a: np.ndarray, desc_b: np.ndarray,
                         matches: np.ndarray | None = None) -> np.ndarray:
         """compareWithNNDR (descriptorsmatcher.cpp:107-131).  Like the reference, new
@@ -221,6 +237,62 @@ class DescriptorsMatcher:
                                              ctypes.byref(n)))
         new = out[:n.value].copy()
         return new if matches is None else np.concatenate([matches, new])
+
+
+class SURF:
+    """The settings' SURF detector / extractor (DescriptorsMatcher::generateDetector /
+    generateExtractor, descriptorsmatcher.cpp:176-359; OpenCV 2.4 nonfree SURF, upright) on the GPU."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    @property
+    def descriptorSize(self) -> int:
+        return 128 if self.ctx.settings.surfExtended else 64
+
+    def detect(self, image: np.ndarray, with_descriptors: bool = False):
+        """FeatureDetector::detect (descriptorsmatcher.cpp:110-111): KEYPOINT records in
+        KeypointGreater order; with_descriptors: (keypoints, descriptors) of the same call."""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        n = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_surf_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, None, 0,
+                                              ctypes.byref(n), None))
+        k = np.zeros(max(n.value, 1), dtype=KEYPOINT)
+        d = np.zeros((max(n.value, 1), self.descriptorSize), dtype=np.float32) if with_descriptors else None
+        m = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_surf_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(k), n.value,
+                                              ctypes.byref(m), _ptr(d, ctypes.c_float) if d is not None else None))
+        k = k[:m.value]
+        return (k, d[:m.value]) if with_descriptors else k
+
+    def compute(self, image: np.ndarray, keypoints: np.ndarray):
+        """DescriptorExtractor::compute (descriptorsmatcher.cpp:113-114): (kept keypoints, input index
+        of each, descriptors float32 n x 128|64)."""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        kin = np.ascontiguousarray(keypoints, dtype=KEYPOINT)
+        n = len(kin)
+        kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+        kept = np.zeros(max(n, 1), dtype=np.int32)
+        desc = np.zeros((max(n, 1), self.descriptorSize), dtype=np.float32)
+        m = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_surf_compute(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(kin), n,
+                                               _vp(kout), _ptr(kept, ctypes.c_int32), ctypes.byref(m),
+                                               _ptr(desc, ctypes.c_float)))
+        return kout[:m.value], kept[:m.value], desc[:m.value]
+
+    def extractDescriptorsFromPatches(self, patches: np.ndarray) -> np.ndarray:
+        """DescriptorsMatcher::extractDescriptorsFromPatches (descriptorsmatcher.cpp:133-174): one
+        keypoint per square patch at (floor(size/2), floor(size/2)), size = the patch edge, angle -1,
+        then the extractor: (P, 128|64) float32."""
+        P = np.ascontiguousarray(patches, dtype=np.uint8)
+        if P.ndim != 3 or P.shape[1] != P.shape[2]:
+            raise ValueError("patches: (P, size, size) uint8")
+        out = np.zeros((max(P.shape[0], 1), self.descriptorSize), dtype=np.float32)
+        self.ctx.check(lib().fm3d_extract_descriptors_from_patches(self.ctx.handle, _ptr(P, ctypes.c_uint8),
+                                                                   P.shape[0], P.shape[1], _ptr(out, ctypes.c_float)))
+        return out[:P.shape[0]]
 
 
 class SingleCameraTriangulator:

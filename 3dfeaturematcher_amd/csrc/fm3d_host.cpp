@@ -73,6 +73,9 @@ struct fm3d_ctx {
     DevBuf A, B, cqA, ctB, idx, key, fkey, knnOut, cand, flag, matches, count, scanTmp;
     DevBuf partIdx, partKey;  // per-part top-2 lists of the split matchers
     DevBuf A8, B8;            // binary rows unpacked to int8 for the MFMA matcher
+    // SURF detection / description
+    DevBuf sfImg, sfSum, sfDet, sfTr, sfLayers, sfMids, sfCand, sfCount, sfSortTmp, sfFlag, sfPos, sfKp, sfKin, sfSrc,
+        sfDesc, sfDW;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     int nCU = 0;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
@@ -602,6 +605,107 @@ int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int w
     return FM3D_OK;
 }
 
+// ---------------- SURF plan (host side of fm3d_surf.hip; the oracle's orc_surf.c formulas) ----------------
+int cv_round_h(double v) { return (int)std::lrint(v); }
+
+// resizeHaarPattern (surf.cpp) in float, cvRound to nearest even
+void surf_resize_haar(const int src[][5], fm3d::SurfHF* dst, int n, int oldSize, int newSize, int widthStep) {
+    const float ratio = (float)newSize / oldSize;
+    for (int k = 0; k < n; k++) {
+        const int dx1 = cv_round_h(ratio * src[k][0]), dy1 = cv_round_h(ratio * src[k][1]);
+        const int dx2 = cv_round_h(ratio * src[k][2]), dy2 = cv_round_h(ratio * src[k][3]);
+        dst[k].p0 = dy1 * widthStep + dx1;
+        dst[k].p1 = dy2 * widthStep + dx1;
+        dst[k].p2 = dy1 * widthStep + dx2;
+        dst[k].p3 = dy2 * widthStep + dx2;
+        dst[k].w = src[k][4] / ((float)(dx2 - dx1) * (dy2 - dy1));
+    }
+}
+
+struct SurfPlan {
+    std::vector<fm3d::SurfLayer> L;
+    std::vector<fm3d::SurfMid> M;
+    size_t detFloats = 0;
+    long long hTotal = 0, mTotal = 0, candCap = 0;
+};
+
+// fastHessianDetector's layer table: (nOctaveLayers + 2) * nOctaves layers, size (9 + 6*layer) <<
+// octave, sample step 1 << octave; calcLayerDetAndTrace skips layers larger than the image
+SurfPlan surf_plan(int w, int h, int octaves, int layers) {
+    static const int dx_s[3][5] = {{0, 2, 3, 7, 1}, {3, 2, 6, 7, -2}, {6, 2, 9, 7, 1}};
+    static const int dy_s[3][5] = {{2, 0, 7, 3, 1}, {2, 3, 7, 6, -2}, {2, 6, 7, 9, 1}};
+    static const int dxy_s[4][5] = {{1, 1, 4, 4, 1}, {5, 1, 8, 4, -1}, {1, 5, 4, 8, -1}, {5, 5, 8, 8, 1}};
+    SurfPlan P;
+    for (int o = 0; o < octaves; o++)
+        for (int l = 0; l < layers + 2; l++) {
+            fm3d::SurfLayer y{};
+            y.size = (9 + 6 * l) << o;
+            y.step = 1 << o;
+            y.rows = h / y.step;
+            y.cols = w / y.step;
+            y.off = P.detFloats;
+            P.detFloats += (size_t)y.rows * y.cols;
+            y.first = P.hTotal;
+            if (y.size <= h && y.size <= w) {
+                y.si = 1 + (h - y.size) / y.step;
+                y.sj = 1 + (w - y.size) / y.step;
+                y.margin = (y.size / 2) / y.step;
+                surf_resize_haar(dx_s, y.hf, 3, 9, y.size, w + 1);
+                surf_resize_haar(dy_s, y.hf + 3, 3, 9, y.size, w + 1);
+                surf_resize_haar(dxy_s, y.hf + 6, 4, 9, y.size, w + 1);
+            }
+            P.hTotal += (long long)y.si * y.sj;
+            P.L.push_back(y);
+        }
+    for (int o = 0; o < octaves; o++)
+        for (int l = 1; l <= layers; l++) {
+            const int idx = o * (layers + 2) + l;
+            fm3d::SurfMid m{};
+            m.layer = idx;
+            m.octave = o;
+            m.rows = P.L[idx].rows;
+            m.cols = P.L[idx].cols;
+            m.margin = (P.L[idx + 1].size / 2) / P.L[idx].step + 1;
+            m.first = P.mTotal;
+            P.mTotal += (long long)m.rows * m.cols;
+            // strict maxima of a 3x3 neighbourhood: at most one per 2x2 block
+            P.candCap += (long long)((m.rows + 1) / 2) * ((m.cols + 1) / 2);
+            P.M.push_back(m);
+        }
+    P.candCap += 16;
+    return P;
+}
+
+// getGaussianKernel(20, 3.3, CV_32F) outer product: SURFInvoker's descriptor weights DW
+std::vector<float> surf_dw() {
+    float g[20];
+    const double scale2X = -0.5 / (3.3 * 3.3);
+    double sum = 0;
+    for (int i = 0; i < 20; i++) {
+        const double x = i - (20 - 1) * 0.5;
+        g[i] = (float)std::exp(scale2X * x * x);
+        sum += g[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < 20; i++) g[i] = (float)(g[i] * sum);
+    std::vector<float> dw(400);
+    for (int i = 0; i < 20; i++)
+        for (int j = 0; j < 20; j++) dw[i * 20 + j] = g[i] * g[j];
+    return dw;
+}
+
+int surf_upload_image(fm3d_ctx* c, const uint8_t* img, int w, int h) {
+    HIPCHK(c, c->sfImg.ensure((size_t)w * h));
+    HIPCHK(c, hipMemcpyAsync(c->sfImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+    if (c->sfDW.bytes == 0) {
+        const std::vector<float> dw = surf_dw();
+        HIPCHK(c, c->sfDW.ensure(400 * sizeof(float)));
+        HIPCHK(c, hipMemcpyAsync(c->sfDW.p, dw.data(), 400 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // dw leaves scope
+    }
+    return FM3D_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -646,7 +750,9 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
                       &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat,
                       &c->slab, &c->slabI1,
-                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->A8, &c->B8};
+                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->A8, &c->B8,
+                      &c->sfImg, &c->sfSum, &c->sfDet, &c->sfTr, &c->sfLayers, &c->sfMids, &c->sfCand, &c->sfCount,
+                      &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();
@@ -1166,6 +1272,156 @@ int fm3d_circular_neighborhoods(fm3d_ctx* c, const double* points, const double*
                                  c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
+    return FM3D_OK;
+}
+
+int fm3d_surf_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoint* kpts, int cap, int* n,
+                     float* desc) {
+    if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
+    const fm3d_settings& S = c->s;
+    if (S.detectorType != FM3D_FEAT_SURF || (desc && S.extractorType != FM3D_FEAT_SURF))
+        return fail(c, FM3D_ERR_UNSUPPORTED, "only the STATIC SURF detector / extractor runs on the GPU");
+    if (!S.surfUpright) return fail(c, FM3D_ERR_UNSUPPORTED, "SURF Upright 0 (orientation) is not implemented");
+    if (S.surfOctaves < 1 || S.surfOctaveLayers < 1 || S.surfHessianThreshold < 0)
+        return fail(c, FM3D_ERR_INVALID, "SURF NumOctaves / NumOctaveLayers / HessianThreshold out of range");
+    hipSetDevice(c->device);
+    int r;
+    if ((r = surf_upload_image(c, img, w, h))) return r;
+    const SurfPlan P = surf_plan(w, h, S.surfOctaves, S.surfOctaveLayers);
+    HIPCHK(c, c->sfSum.ensure((size_t)(w + 1) * (h + 1) * sizeof(int)));
+    HIPCHK(c, c->sfDet.ensure(P.detFloats * sizeof(float) + 16));
+    HIPCHK(c, c->sfTr.ensure(P.detFloats * sizeof(float) + 16));
+    HIPCHK(c, c->sfLayers.ensure(P.L.size() * sizeof(fm3d::SurfLayer)));
+    HIPCHK(c, c->sfMids.ensure(P.M.size() * sizeof(fm3d::SurfMid)));
+    HIPCHK(c, c->sfCand.ensure((size_t)P.candCap * sizeof(fm3d::SurfCand)));
+    HIPCHK(c, c->sfCount.ensure(64));
+    HIPCHK(c, hipMemcpyAsync(c->sfLayers.p, P.L.data(), P.L.size() * sizeof(fm3d::SurfLayer), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->sfMids.p, P.M.data(), P.M.size() * sizeof(fm3d::SurfMid), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sfDet.p, 0, P.detFloats * sizeof(float), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sfTr.p, 0, P.detFloats * sizeof(float), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sfCount.p, 0, 64, c->stream));
+    fm3d::launch_integral(c->sfImg.as<uint8_t>(), w, h, c->sfSum.as<int>(), c->stream);
+    fm3d::launch_surf_hessian(c->sfSum.as<int>(), w, c->sfLayers.as<fm3d::SurfLayer>(), (int)P.L.size(), P.hTotal,
+                              c->sfDet.as<float>(), c->sfTr.as<float>(), c->stream);
+    fm3d::launch_surf_maxima(c->sfDet.as<float>(), c->sfTr.as<float>(), c->sfLayers.as<fm3d::SurfLayer>(),
+                             c->sfMids.as<fm3d::SurfMid>(), (int)P.M.size(), P.mTotal, (float)S.surfHessianThreshold,
+                             c->sfCand.as<fm3d::SurfCand>(), c->sfCount.as<int>(), (int)P.candCap, c->stream);
+    HIPCHK(c, hipGetLastError());
+    int nc = 0;
+    HIPCHK(c, hipMemcpyAsync(&nc, c->sfCount.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nc > P.candCap) return fail(c, FM3D_ERR_HIP, "SURF candidate buffer overflow");
+    const size_t sortBytes = fm3d::surf_sort_tmp_bytes(nc);
+    HIPCHK(c, c->sfSortTmp.ensure(sortBytes + 16));
+    fm3d::launch_surf_sort(c->sfCand.as<fm3d::SurfCand>(), nc, c->sfSortTmp.p, sortBytes, c->stream);
+    if ((r = ensure_scan_tmp(c, nc))) return r;
+    HIPCHK(c, c->sfFlag.ensure((size_t)(nc + 1) * sizeof(int)));
+    HIPCHK(c, c->sfPos.ensure((size_t)(nc + 1) * sizeof(int)));
+    HIPCHK(c, c->sfKp.ensure((size_t)(nc + 1) * sizeof(fm3d_keypoint)));
+    int nk = 0;
+    if (nc > 0) {
+        fm3d::launch_surf_upright(c->sfCand.as<fm3d::SurfCand>(), c->sfCount.as<int>(), nc, w, h, c->sfFlag.as<int>(),
+                                  c->sfPos.as<int>(), c->count.as<int>(), c->scanTmp.p, c->sfKp.as<fm3d_keypoint>(),
+                                  nullptr, c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    const int nw = std::min(nk, cap);
+    const int dsize = S.surfExtended ? 128 : 64;
+    if (desc && nw > 0) {
+        HIPCHK(c, c->sfDesc.ensure((size_t)nw * dsize * sizeof(float)));
+        fm3d::launch_surf_describe(c->sfImg.as<uint8_t>(), 0, w, h, c->sfKp.as<fm3d_keypoint>(), nw, c->sfDW.as<float>(),
+                                   S.surfExtended, c->sfDesc.as<float>(), c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(desc, c->sfDesc.p, (size_t)nw * dsize * sizeof(float), hipMemcpyDeviceToHost,
+                                 c->stream));
+    }
+    if (nw > 0)
+        HIPCHK(c, hipMemcpyAsync(kpts, c->sfKp.p, (size_t)nw * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *n = nk;
+    return FM3D_OK;
+}
+
+int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,
+                      fm3d_keypoint* kout, int32_t* kept, int* nOut, float* desc) {
+    if (!c || !img || !nOut || w <= 0 || h <= 0 || n < 0 || (n > 0 && (!kpts || !kout || !desc)))
+        return FM3D_ERR_INVALID;
+    const fm3d_settings& S = c->s;
+    if (S.extractorType != FM3D_FEAT_SURF) return fail(c, FM3D_ERR_UNSUPPORTED, "only the SURF extractor runs on the GPU");
+    if (!S.surfUpright) return fail(c, FM3D_ERR_UNSUPPORTED, "SURF Upright 0 (orientation) is not implemented");
+    *nOut = 0;
+    if (n == 0) return FM3D_OK;
+    hipSetDevice(c->device);
+    int r;
+    if ((r = surf_upload_image(c, img, w, h))) return r;
+    if ((r = ensure_scan_tmp(c, n))) return r;
+    HIPCHK(c, c->sfKin.ensure((size_t)n * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->sfKp.ensure((size_t)n * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->sfFlag.ensure((size_t)(n + 1) * sizeof(int)));
+    HIPCHK(c, c->sfPos.ensure((size_t)(n + 1) * sizeof(int)));
+    HIPCHK(c, c->sfSrc.ensure((size_t)(n + 1) * sizeof(int)));
+    HIPCHK(c, hipMemcpyAsync(c->sfKin.p, kpts, (size_t)n * sizeof(fm3d_keypoint), hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_surf_keep(c->sfKin.as<fm3d_keypoint>(), n, w, h, c->sfFlag.as<int>(), c->sfPos.as<int>(),
+                           c->count.as<int>(), c->scanTmp.p, c->sfKp.as<fm3d_keypoint>(), c->sfSrc.as<int>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    int nk = 0;
+    HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int dsize = S.surfExtended ? 128 : 64;
+    if (nk > 0) {
+        HIPCHK(c, c->sfDesc.ensure((size_t)nk * dsize * sizeof(float)));
+        fm3d::launch_surf_describe(c->sfImg.as<uint8_t>(), 0, w, h, c->sfKp.as<fm3d_keypoint>(), nk, c->sfDW.as<float>(),
+                                   S.surfExtended, c->sfDesc.as<float>(), c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(desc, c->sfDesc.p, (size_t)nk * dsize * sizeof(float), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipMemcpyAsync(kout, c->sfKp.p, (size_t)nk * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost, c->stream));
+        if (kept)
+            HIPCHK(c, hipMemcpyAsync(kept, c->sfSrc.p, (size_t)nk * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *nOut = nk;
+    return FM3D_OK;
+}
+
+int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, int P, int size, float* desc) {
+    if (!c || P < 0 || size <= 0 || (P && (!patches || !desc))) return FM3D_ERR_INVALID;
+    const fm3d_settings& S = c->s;
+    if (S.extractorType != FM3D_FEAT_SURF) return fail(c, FM3D_ERR_UNSUPPORTED, "only the SURF extractor runs on the GPU");
+    if (!S.surfUpright) return fail(c, FM3D_ERR_UNSUPPORTED, "SURF Upright 0 (orientation) is not implemented");
+    if (P == 0) return FM3D_OK;
+    // descriptorsmatcher.cpp:146-158: one keypoint per patch at (center, center), center =
+    // (int)floor(size / 2), size = the patch edge, angle -1, response 1, octave 0, class_id 0
+    const float center = (float)(int)std::floor(size / 2);
+    fm3d_keypoint k{center, center, (float)size, -1.f, 1.f, 0, 0};
+    const float s = k.size * 1.2f / 9.0f;
+    const int gws = 2 * cv_round_h(2 * s);
+    if (size + 1 < gws) return fail(c, FM3D_ERR_INVALID, "patch keypoint dropped by SURF (descriptor row missing)");
+    k.angle = 360.f - 90.f;
+    hipSetDevice(c->device);
+    const size_t per = (size_t)size * size;
+    const int dsize = S.surfExtended ? 128 : 64;
+    std::vector<fm3d_keypoint> kp((size_t)P, k);
+    HIPCHK(c, c->sfImg.ensure((size_t)P * per));
+    HIPCHK(c, c->sfKp.ensure((size_t)P * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->sfDesc.ensure((size_t)P * dsize * sizeof(float)));
+    HIPCHK(c, hipMemcpyAsync(c->sfImg.p, patches, (size_t)P * per, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->sfKp.p, kp.data(), kp.size() * sizeof(fm3d_keypoint), hipMemcpyHostToDevice, c->stream));
+    if (c->sfDW.bytes == 0) {
+        const std::vector<float> dw = surf_dw();
+        HIPCHK(c, c->sfDW.ensure(400 * sizeof(float)));
+        HIPCHK(c, hipMemcpyAsync(c->sfDW.p, dw.data(), 400 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    fm3d::launch_surf_describe(c->sfImg.as<uint8_t>(), per, size, size, c->sfKp.as<fm3d_keypoint>(), P,
+                               c->sfDW.as<float>(), S.surfExtended, c->sfDesc.as<float>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(desc, c->sfDesc.p, (size_t)P * dsize * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return FM3D_OK;
 }
 

@@ -99,6 +99,40 @@ void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int di
 void launch_nndr(int type, const int* idx, const int* key, const float* fkey, int nA, int nB, double eps,
                  int queryOffset, fm3d_dmatch* knnOut, fm3d_dmatch* cand, int* flag, hipStream_t s);
 
+// ---------------- SURF (fm3d_surf.hip) ----------------
+struct SurfHF {  // a box of a resized Haar pattern: sum[p0] + sum[p3] - sum[p1] - sum[p2], weight w
+    int p0, p1, p2, p3;
+    float w;
+};
+struct SurfLayer {     // one scale-space layer (calcLayerDetAndTrace)
+    long long first;   // first thread of this layer in the Hessian launch
+    size_t off;        // det / trace offset of the layer (rows x cols floats)
+    int size, step, margin, si, sj, rows, cols;
+    SurfHF hf[10];     // Dx (3), Dy (3), Dxy (4)
+};
+struct SurfMid {  // a middle layer searched for maxima (findMaximaInLayer)
+    long long first;
+    int layer, octave, rows, cols, margin;
+};
+struct SurfCand {
+    float x, y, size, response;
+    int octave, class_id;
+    long long seq;  // discovery order: (layer << 42) | (row << 21) | column
+};
+void launch_integral(const uint8_t* img, int w, int h, int* sum, hipStream_t s);
+void launch_surf_hessian(const int* sum, int w, const SurfLayer* layers, int nL, long long total, float* det,
+                         float* tr, hipStream_t s);
+void launch_surf_maxima(const float* det, const float* tr, const SurfLayer* layers, const SurfMid* mids, int nM,
+                        long long total, float thr, SurfCand* cand, int* count, int cap, hipStream_t s);
+size_t surf_sort_tmp_bytes(int n);
+void launch_surf_sort(SurfCand* cand, int n, void* tmp, size_t tmpBytes, hipStream_t s);
+void launch_surf_upright(const SurfCand* cand, const int* count, int n, int w, int h, int* flag, int* pos, int* total,
+                         void* scanTmp, fm3d_keypoint* out, int* src, hipStream_t s);
+void launch_surf_keep(const fm3d_keypoint* in, int n, int w, int h, int* flag, int* pos, int* total, void* scanTmp,
+                      fm3d_keypoint* out, int* src, hipStream_t s);
+void launch_surf_describe(const uint8_t* img, size_t imgStride, int w, int h, const fm3d_keypoint* kp, int n,
+                          const float* DW, int extended, float* desc, hipStream_t s);
+
 // ---------------- compaction ----------------
 // out[k] = in[i] for flag[i] != 0, stable; *count (device) = number kept.  tmp >= scan_tmp_bytes(n).
 size_t scan_tmp_bytes(int n);

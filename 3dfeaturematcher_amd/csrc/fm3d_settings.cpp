@@ -130,6 +130,13 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->neighMethod = 0;      // method: square
     s->neighThetas = 15;     // the commented-out circular values of build/settings.yml
     s->neighRays = 5;
+    s->detectorType = FM3D_FEAT_SURF;  // FeatureOptions: STATIC SURF detector + extractor
+    s->extractorType = FM3D_FEAT_SURF;
+    s->surfHessianThreshold = 400;
+    s->surfOctaves = 4;
+    s->surfOctaveLayers = 2;
+    s->surfExtended = 1;
+    s->surfUpright = 1;
     return FM3D_OK;
 }
 
@@ -164,6 +171,28 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
             if (m.size() >= 2 && (m[0] == '"' || m[0] == '\'') && m.back() == m[0]) m = m.substr(1, m.size() - 2);
             s->neighMethod = m == "square" ? 0 : (m == "circular" ? 1 : -1);
         }
+    }
+    {
+        auto str = [&](const char* k, std::string& v) {
+            auto it = kv.find(k);
+            if (it == kv.end()) return false;
+            v = it->second;
+            if (v.size() >= 2 && (v[0] == '"' || v[0] == '\'') && v.back() == v[0]) v = v.substr(1, v.size() - 2);
+            return true;
+        };
+        std::string mode = "STATIC", det, ex;
+        str("FeatureOptions.DetectorMode", mode);
+        if (str("FeatureOptions.DetectorType", det))
+            s->detectorType = (mode == "STATIC" && det == "SURF") ? FM3D_FEAT_SURF : FM3D_FEAT_OTHER;
+        if (str("FeatureOptions.ExtractorType", ex)) s->extractorType = ex == "SURF" ? FM3D_FEAT_SURF : FM3D_FEAT_OTHER;
+        get_d(kv, "FeatureOptions.SurfDetector.HessianThreshold", &s->surfHessianThreshold);
+        get_i(kv, "FeatureOptions.SurfDetector.NumOctaves", &s->surfOctaves);
+        get_i(kv, "FeatureOptions.SurfDetector.NumOctaveLayers", &s->surfOctaveLayers);
+        int e = s->surfExtended, u = s->surfUpright;
+        get_i(kv, "FeatureOptions.SurfDetector.Extended", &e);
+        get_i(kv, "FeatureOptions.SurfDetector.Upright", &u);
+        s->surfExtended = e > 0;  // (int)fs[...] > 0
+        s->surfUpright = u > 0;
     }
     get_i(kv, "Neighborhoods.thetas", &s->neighThetas);
     get_i(kv, "Neighborhoods.rays", &s->neighRays);

@@ -71,7 +71,16 @@ typedef struct fm3d_settings {
     /* Neighborhoods.method (neighborhoodsgenerator.cpp:38-73): 0 square, 1 circular, -1 anything
        else (the reference's exit(-10)); thetas / rays of the circular method (:47-48) */
     int neighMethod, neighThetas, neighRays;
+    /* FeatureOptions (descriptorsmatcher.cpp:176-359): DetectorMode STATIC + DetectorType /
+       ExtractorType SURF are FM3D_FEAT_SURF; anything else FM3D_FEAT_OTHER (no GPU implementation).
+       SurfDetector.HessianThreshold / NumOctaves / NumOctaveLayers / Extended / Upright */
+    int detectorType, extractorType;
+    double surfHessianThreshold;
+    int surfOctaves, surfOctaveLayers, surfExtended, surfUpright;
 } fm3d_settings;
+
+#define FM3D_FEAT_SURF 0
+#define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
 typedef struct fm3d_dmatch {
@@ -83,6 +92,12 @@ typedef struct fm3d_dmatch {
 typedef struct fm3d_point2f {
     float x, y;
 } fm3d_point2f;
+
+/* cv::KeyPoint (28 bytes) */
+typedef struct fm3d_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} fm3d_keypoint;
 
 typedef enum fm3d_desc_type {
     FM3D_DESC_F32 = 0,  /* float rows (SURF/SIFT): FLANN L2 order, distance = sqrt */
@@ -218,6 +233,28 @@ int fm3d_square_neighborhoods(fm3d_ctx *ctx, const double *frames, int P, double
    doubles, sample order (ray outer, angle inner).  FM3D_ERR_INVALID unless neighMethod is circular
    (the reference constructor reads thetas / rays only then). */
 int fm3d_circular_neighborhoods(fm3d_ctx *ctx, const double *points, const double *normals, int P, double *out);
+
+/* ---------------- feature detection + description (SURF, OpenCV 2.4 nonfree) ---------------- */
+/* FeatureDetector::detect of the settings' SURF detector (descriptorsmatcher.cpp:110-111 via
+   generateDetector :176-293): fastHessianDetector + the upright SURFInvoker pass, keypoints in
+   KeypointGreater order (response, size, octave, y, x descending).  *n = all keypoints found; the
+   first min(*n, cap) are written to kpts.  desc (may be NULL): their descriptors too (the extractor's
+   compute on the same image, :113-114), min(*n, cap) x (surfExtended ? 128 : 64) floats.
+   FM3D_ERR_UNSUPPORTED unless detector (and, with desc, extractor) is SURF with Upright 1. */
+int fm3d_surf_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, fm3d_keypoint *kpts, int cap, int *n,
+                     float *desc);
+/* DescriptorExtractor::compute of the settings' SURF extractor for given keypoints (:113-114,
+   extractDescriptorsFromPatches :133-174): keypoints whose 2*round(2s) wavelet does not fit the
+   image are removed, the others get angle 270 (upright).  kout / kept (input index of each kept
+   keypoint, may be NULL): capacity n; desc: n x (128 | 64) floats; *nOut = kept count. */
+int fm3d_surf_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const fm3d_keypoint *kpts, int n,
+                      fm3d_keypoint *kout, int32_t *kept, int *nOut, float *desc);
+
+/* DescriptorsMatcher::extractDescriptorsFromPatches (descriptorsmatcher.cpp:133-174): per square
+   patch (P x size x size bytes, e.g. the fm3d_export_patches output) one keypoint at
+   (floor(size/2), floor(size/2)) of size `size`, described by the settings' SURF extractor; the
+   reference's descriptors Mat, one row per patch: P x (128 | 64) floats. */
+int fm3d_extract_descriptors_from_patches(fm3d_ctx *ctx, const uint8_t *patches, int P, int size, float *desc);
 
 /* ---------------- the whole hot path, device resident ---------------- */
 /* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */

@@ -271,3 +271,60 @@ def export_patches(cam, img1, frames, eps=0.16, cmpp=0.25, mode=STRICT, image_po
                              ctypes.c_int(n), ctypes.c_double(eps), ctypes.c_double(cmpp), ctypes.c_int(mode),
                              _p(patches, ctypes.c_uint8), _p(pts) if pts is not None else None)
     return (patches, pts) if image_points else patches
+
+
+# ---------------------------------------------------------------- SURF (orc_surf.c)
+KEYPOINT = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                     ("octave", "<i4"), ("class_id", "<i4")])  # cv::KeyPoint
+
+
+def integral(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.zeros((h + 1, w + 1), dtype=np.int32)
+    lib().orc_integral(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _p(out, ctypes.c_int))
+    return out
+
+
+def surf_detect(img, thr=400.0, octaves=4, layers=2):
+    """SURF detect (fastHessianDetector + the upright detect pass): cv::KeyPoint records, sorted."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    f = lib().orc_surf_detect
+    f.restype = ctypes.c_int
+    args = (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_float(thr), ctypes.c_int(octaves),
+            ctypes.c_int(layers))
+    n = f(*args, None, ctypes.c_int(0))
+    out = np.zeros(max(n, 1), dtype=KEYPOINT)
+    f(*args, out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(n))
+    return out[:n]
+
+
+def surf_describe(img, kpts, extended=True):
+    """SURF compute (upright): (kept keypoints, input index of each, descriptors n x 128|64 float32)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    kin = np.ascontiguousarray(kpts, dtype=KEYPOINT)
+    n = len(kin)
+    kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+    kept = np.zeros(max(n, 1), dtype=np.int32)
+    desc = np.zeros((max(n, 1), 128 if extended else 64), dtype=np.float32)
+    f = lib().orc_surf_describe
+    f.restype = ctypes.c_int
+    m = f(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), kin.ctypes.data_as(ctypes.c_void_p),
+          ctypes.c_int(n), ctypes.c_int(1 if extended else 0), kout.ctypes.data_as(ctypes.c_void_p),
+          _p(kept, ctypes.c_int), _p(desc, ctypes.c_float))
+    return kout[:m], kept[:m], desc[:m]
+
+
+def surf_dw():
+    dw = np.zeros(400, dtype=np.float32)
+    lib().orc_surf_dw(_p(dw, ctypes.c_float))
+    return dw.reshape(20, 20)
+
+
+def resize_area21(win):
+    win = np.ascontiguousarray(win, dtype=np.uint8)
+    out = np.zeros((21, 21), dtype=np.uint8)
+    lib().orc_resize_area21(_p(win, ctypes.c_uint8), ctypes.c_int(win.shape[0]), _p(out, ctypes.c_uint8))
+    return out

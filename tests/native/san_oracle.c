@@ -5,6 +5,7 @@
  * tests/test_sanitizers.py (tests/native/Makefile); any report aborts with a nonzero status. */
 #include <stdio.h>
 #include "../../oracle/fm3d_oracle.c"
+#include "../../oracle/orc_surf.c"
 
 static unsigned long long rs = 0x9E3779B97F4A7C15ULL;
 static unsigned rnd(void) { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return (unsigned)(rs >> 32); }
@@ -87,6 +88,42 @@ int main(void)
             orc_square_neighborhoods(fr, 2, 0.02, 0.25, sq);
             orc_export_patches(&cam, im1, W, H, fr, P, 0.02, 0.25, ORC_LM_STRICT, patch, NULL);
             orc_export_patches(&cam, im1, W, H, fr, P, 0.02, 0.25, ORC_LM_DETMATH, patch, NULL);
+        }
+    }
+    /* circular neighbourhoods (given normals and the X/|X| branch) */
+    {
+        static double X[6] = {0.1, -0.2, 1.9, 0.3, 0.1, 2.1}, N[6] = {0, 0.1, -0.99, 0.2, 0.2, -0.95}, o[2 * 15 * 5 * 3];
+        orc_circular_neighborhoods(X, N, 2, 0.16, 15, 5, o);
+        orc_circular_neighborhoods(X, NULL, 2, 0.16, 15, 5, o);
+    }
+    /* SURF detect + describe on textured images of odd / tiny / wide sizes, patches at the border */
+    {
+        static const int sizes[][2] = {{96, 80}, {33, 29}, {8, 8}, {200, 24}};
+        for (i = 0; i < 4; i++) {
+            const int w = sizes[i][0], h = sizes[i][1];
+            static uint8_t im[200 * 96];
+            static orc_kpt k[4096], k2[4096];
+            static int kept[4096];
+            static float desc[4096 * 128];
+            int x, y, nk, m;
+            for (y = 0; y < h; y++)
+                for (x = 0; x < w; x++) im[y * w + x] = (uint8_t)(128 + 100 * sin(x * 0.37 + y * 0.21) * cos(y * 0.3) + (rnd() & 15));
+            nk = orc_surf_detect(im, w, h, 40.f, 4, 2, k, 4096);
+            if (nk > 4096) nk = 4096;
+            m = orc_surf_describe(im, w, h, k, nk, 1, k2, kept, desc);
+            m = orc_surf_describe(im, w, h, k, nk, 0, k2, kept, desc);
+            (void)m;
+        }
+        {
+            static uint8_t patch[128 * 128], tiny[25 * 25];
+            static orc_kpt kp = {64, 64, 128, -1, 1, 0, 0}, ko;
+            static float d[128];
+            for (i = 0; i < 128 * 128; i++) patch[i] = (uint8_t)rnd();
+            orc_surf_describe(patch, 128, 128, &kp, 1, 1, &ko, NULL, d);
+            for (i = 21; i <= 25 * 25 && i <= 600; i += 21) {
+                const int W = 21 + (i % 5);
+                orc_resize_area21(patch, W, tiny);
+            }
         }
     }
     puts("san_oracle: ok");

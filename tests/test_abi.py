@@ -64,7 +64,19 @@ def test_library_exports_every_header_symbol(fm3d):
 def test_struct_layouts(fm3d):
     assert fm3d.DMATCH.itemsize == 16          # cv::DMatch
     assert fm3d.RECORD.itemsize == 64
-    assert ctypes.sizeof(fm3d.Settings) == (8 * 9 + 8 * 6 + 8 * 3 + 4 * 2 + 8 + 8 * 12 + 4 * 4 + 8 * 2 + 4 * 3 + 7) // 8 * 8
+    # every fm3d_settings / fm3d_keypoint field at the C compiler's offset (the Python mirror and the header agree)
+    import subprocess
+    import tempfile
+    fields = [f for f, _ in fm3d.Settings._fields_]
+    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"fm3d.h\"\nint main(void){printf(\"%zu %zu\\n\", sizeof(fm3d_settings), sizeof(fm3d_keypoint));"
+    src += "".join(f'printf("%zu\\n", offsetof(fm3d_settings, {f}));' for f in fields) + "return 0;}"
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "s.c"), os.path.join(d, "s")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    assert int(out[0]) == ctypes.sizeof(fm3d.Settings) and int(out[1]) == fm3d.KEYPOINT.itemsize == 28
+    assert [int(v) for v in out[2:]] == [getattr(fm3d.Settings, f).offset for f in fields]
 
 
 def test_settings_default_is_reference_file(fm3d):

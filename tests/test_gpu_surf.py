@@ -1,0 +1,127 @@
+"""GPU SURF (csrc/fm3d_surf.hip) against the SURF oracle (oracle/orc_surf.c), bit for bit:
+keypoints (position, size, angle, response, octave, Laplacian sign) in KeypointGreater order and
+their descriptors; compute on given keypoints; extractDescriptorsFromPatches; compareWithNNDR
+starting from the images (descriptorsmatcher.cpp:107-174)."""
+import numpy as np
+import pytest
+
+from conftest import oracle_threads
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(fm3d, **kw):
+    s = fm3d.Settings.default()
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return fm3d.Context(s), s
+
+
+def _same_kpts(a, b):
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
+        assert np.array_equal(a[f], b[f]), f
+
+
+@pytest.mark.parametrize("which", ["img1", "img2"])
+def test_surf_detect_describe_vga_bitwise(fm3d, orc, synth, which):
+    """The reference's settings (threshold 400, 4 octaves, 2 layers, extended, upright) on the
+    synthetic VGA frames."""
+    pair = synth.make_frame_pair(2000, seed=3)
+    img = getattr(pair, which)
+    ctx, s = _ctx(fm3d)
+    try:
+        k, d = fm3d.SURF(ctx).detect(img, with_descriptors=True)
+    finally:
+        ctx.close()
+    ko = orc.surf_detect(img, s.surfHessianThreshold, s.surfOctaves, s.surfOctaveLayers)
+    kd, kept, do = orc.surf_describe(img, ko, extended=True)
+    assert len(ko) > 500
+    _same_kpts(k, ko)
+    assert np.array_equal(kept, np.arange(len(ko)))
+    assert np.array_equal(d, do)
+
+
+@pytest.mark.parametrize("shape,thr,octaves,layers,extended", [
+    ((77, 100), 100.0, 4, 2, 1), ((29, 33), 10.0, 2, 3, 0), ((480, 64), 200.0, 5, 1, 1), ((8, 8), 1.0, 1, 1, 1)])
+def test_surf_shapes_and_settings(fm3d, orc, shape, thr, octaves, layers, extended):
+    """Odd and tiny images, layers that do not fit (skipped), other octave / layer counts, the 64-D
+    descriptor."""
+    rng = np.random.default_rng(sum(shape))
+    h, w = shape
+    yy, xx = np.mgrid[0:h, 0:w]
+    img = np.clip(128 + 90 * np.sin(xx * 0.31 + yy * 0.17) * np.cos(yy * 0.23) + rng.normal(0, 8, shape), 0,
+                  255).astype(np.uint8)
+    ctx, s = _ctx(fm3d, surfHessianThreshold=thr, surfOctaves=octaves, surfOctaveLayers=layers,
+                  surfExtended=extended)
+    try:
+        k, d = fm3d.SURF(ctx).detect(img, with_descriptors=True)
+    finally:
+        ctx.close()
+    ko = orc.surf_detect(img, thr, octaves, layers)
+    _, _, do = orc.surf_describe(img, ko, extended=bool(extended))
+    _same_kpts(k, ko)
+    assert d.shape == (len(ko), 128 if extended else 64) and np.array_equal(d, do)
+
+
+def test_surf_compute_given_keypoints(fm3d, orc, synth):
+    """compute on caller keypoints: a keypoint whose wavelet exceeds the image is removed (the
+    others keep their order, angle 270), windows cut by every border."""
+    img = synth.make_frame_pair(300, seed=8).img1
+    kin = np.zeros(7, dtype=fm3d.KEYPOINT)
+    kin["x"] = [0.0, 639.4, 320.5, 5.0, 100.0, 600.0, 2.5]
+    kin["y"] = [0.0, 479.9, 240.2, 470.0, 3.0, 10.0, 2.5]
+    kin["size"] = [9, 20, 4000, 31, 77, 150, 15]
+    kin["angle"] = -1
+    ctx, _ = _ctx(fm3d)
+    try:
+        k, kept, d = fm3d.SURF(ctx).compute(img, kin)
+    finally:
+        ctx.close()
+    ko, kepto, do = orc.surf_describe(img, kin, extended=True)
+    assert list(kept) == [0, 1, 3, 4, 5, 6] and np.array_equal(kept, kepto)
+    _same_kpts(k, ko)
+    assert np.array_equal(d, do)
+
+
+def test_extract_descriptors_from_patches(fm3d, orc, synth):
+    """extractDescriptorsFromPatches (descriptorsmatcher.cpp:133-174) on the exported 128x128
+    normal-rectified patches: one keypoint at (64, 64) of size 128 per patch."""
+    rng = np.random.default_rng(9)
+    patches = rng.integers(0, 256, (40, 128, 128), dtype=np.uint8)
+    patches[:, 32:96, 32:96] //= 3
+    ctx, _ = _ctx(fm3d)
+    try:
+        d = fm3d.SURF(ctx).extractDescriptorsFromPatches(patches)
+    finally:
+        ctx.close()
+    kp = np.zeros(1, dtype=fm3d.KEYPOINT)
+    kp["x"] = kp["y"] = 64
+    kp["size"] = 128
+    kp["angle"] = -1
+    kp["response"] = 1
+    ref = np.stack([orc.surf_describe(p, kp, extended=True)[2][0] for p in patches])
+    assert d.shape == (40, 128) and np.array_equal(d, ref)
+
+
+def test_compare_with_nndr_from_images(fm3d, orc, synth):
+    """compareWithNNDR from the images: SURF on both frames, FLANN-order L2 knnMatch, NNDR -- the
+    same matches, keypoints and descriptors as the oracle chain."""
+    pair = synth.make_frame_pair(2000, seed=4)
+    ctx, s = _ctx(fm3d)
+    try:
+        dm = fm3d.DescriptorsMatcher(ctx)
+        m, ka, kb, da, db = dm.compareWithNNDRImages(0.55, pair.img1, pair.img2)
+    finally:
+        ctx.close()
+    koa = orc.surf_detect(pair.img1)
+    kob = orc.surf_detect(pair.img2)
+    _, _, doa = orc.surf_describe(pair.img1, koa)
+    _, _, dob = orc.surf_describe(pair.img2, kob)
+    _same_kpts(ka, koa)
+    _same_kpts(kb, kob)
+    assert np.array_equal(da, doa) and np.array_equal(db, dob)
+    idx, dist = orc.knn2(doa, dob, orc.F32, oracle_threads())
+    q, t, dd = orc.nndr(idx, dist, 0.55)
+    assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t) and np.array_equal(m["distance"], dd)
+    assert len(m) > 50
