@@ -528,3 +528,52 @@ def camera2_from_g12(g12):
     t2 = np.zeros(3)
     _check(lib().fm3d_camera2_from_g12(_ptr(np.ascontiguousarray(g12, dtype=np.float64).ravel()), _ptr(R2), _ptr(t2)))
     return R2.reshape(3, 3), t2
+
+
+class MOSAIC:
+    """MOSAIC (mosaic.h:47-70, mosaic.cpp:32-73): the reference's descriptor extractor built on the
+    whole pipeline.  The constructor runs the reference's seven steps on the GPU -- SURF
+    compareWithNNDR on the two images, setg12, setKeypoints + triangulate, setImages +
+    computeOptimizedNormals + computeFeaturesFrames, the reference square neighbourhood, and the
+    normal-rectified patches of image A (projectReferencePointsToImageWithFrames).  The reference's
+    computeImpl is empty (mosaic.cpp:75-79); compute() finishes it the way the reference's main()
+    does (main.cpp:182-183): extractDescriptorsFromPatches of the patches, one SURF row per kept
+    feature (descriptorType CV_32F, descriptorSize 128)."""
+
+    descriptorSize = 128
+
+    def __init__(self, ctx: Context, imgA: np.ndarray, imgB: np.ndarray, tA, tB, rA, rB):
+        self.ctx = ctx
+        s = ctx.settings
+        self.imgA = np.ascontiguousarray(imgA, dtype=np.uint8)
+        self.imgB = np.ascontiguousarray(imgB, dtype=np.uint8)
+        # 2 - matches (descriptorsmatcher.cpp:107-131 from the images)
+        self.dm = DescriptorsMatcher(ctx)
+        self.matches, self.kptsA, self.kptsB, _, _ = self.dm.compareWithNNDRImages(s.nndrEpsilon, self.imgA, self.imgB)
+        # 3 - g12 (singlecameratriangulator.cpp:123-143)
+        self.sct = SingleCameraTriangulator(ctx)
+        self.gAB = self.sct.setg12(tA, tB, rA, rB)
+        # 4 - triangulation of the matches (:145-230)
+        xy = lambda k: np.stack([k["x"], k["y"]], axis=1).astype(np.float32)
+        self.sct.setKeypoints(xy(self.kptsA), xy(self.kptsB), self.matches)
+        pts, self.outliersMask = self.sct.triangulate()
+        # 5 - normals and feature frames (normaloptimizer.cpp:191-504)
+        self.no = NormalOptimizer(ctx, self.sct)
+        self.no.setImages(self.imgA, self.imgB)
+        self.triangulated_points, self.normals = self.no.computeOptimizedNormals(pts)
+        self.features_frames = self.no.computeFeaturesFrames(self.triangulated_points, self.normals)
+        # 6 - the reference neighbourhood (neighborhoodsgenerator.cpp:134-158)
+        self.ng = NeighborhoodsGenerator(s)
+        self.reference_neighborhood = self.ng.getReferenceSquaredNeighborhood()
+        # 7 - patches of image A (singlecameratriangulator.cpp:769-849)
+        self.patches, self.image_points = self.sct.projectReferencePointsToImageWithFrames(
+            self.reference_neighborhood, self.features_frames, image_points=True)
+
+    def descriptorType(self):
+        return np.float32
+
+    def compute(self) -> np.ndarray:
+        """The patch descriptors: (kept features, 128) float32."""
+        if len(self.patches) == 0:
+            return np.zeros((0, SURF(self.ctx).descriptorSize), dtype=np.float32)
+        return SURF(self.ctx).extractDescriptorsFromPatches(self.patches)

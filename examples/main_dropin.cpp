@@ -6,10 +6,10 @@
 //
 // Everything below the includes uses the reference's own types and calls (cv::FileStorage,
 // cv::imread, DescriptorsMatcher(fs, img1, img2).compareWithNNDR(...), SingleCameraTriangulator(fs),
-// NormalOptimizer(fs, &sct), NeighborhoodsGenerator(fs), drawMatches, ...).  Two steps of the
-// reference are left out: extractDescriptorsFromPatches (SURF on the patches, upstream feature
-// extraction, not built) and the PCL viewers (visual only).  Feature detection is upstream too:
-// the keypoints/descriptors come from the images' side files <image>.kpts.f32 / <image>.desc.u8.
+// NormalOptimizer(fs, &sct), NeighborhoodsGenerator(fs), drawMatches, ...).  The PCL viewers are
+// left out (visual only).  With the reference's SURF detector / extractor the features are detected
+// and described on the GPU; with another detector type (no GPU implementation) the keypoints /
+// descriptors come from the images' side files <image>.kpts.f32 / <image>.desc.u8.
 //
 // Usage: main_dropin -s settings.yml    (the reference's command line)
 // Writes matches.pgm, patch_<i>.pgm (via the patch export), projectedPatches.pgm like the
@@ -95,6 +95,16 @@ int main(int argc, char** argv) {
                                                     imagePointsVector);
         for (size_t i = 0; i < patchesVector.size(); i++)  // singlecameratriangulator.cpp:843-846
             cv::imwrite("patch_" + std::to_string(i) + ".pgm", patchesVector[i]);
+        // main.cpp:182-183 (the settings' SURF extractor on the GPU; other extractors are not built)
+        cv::Mat descriptors;
+        if (!patchesVector.empty()) {
+            try {
+                dm.extractDescriptorsFromPatches(patchesVector, descriptors);
+            } catch (const fm3d::compat::Error& e) {
+                if (e.code != FM3D_ERR_UNSUPPORTED) throw;
+                std::cout << "extractDescriptorsFromPatches: " << e.what() << std::endl;
+            }
+        }
         ng.computeSquareNeighborhoodsByNormals(featuresFrames, neighborhoodsVector);
         cv::Mat img1_points;
         drawBackProjectedPoints(img1, img1_points, imagePointsVector, colors);
@@ -105,6 +115,7 @@ int main(int argc, char** argv) {
         dump("out_matches.bin", matches.data(), matches.size() * sizeof(cv::DMatch));
         dump("out_points.f64", triagulated.data(), triagulated.size() * sizeof(cv::Vec3d));
         dump("out_normals.f64", normalsVector.data(), normalsVector.size() * sizeof(cv::Vec3d));
+        dump("out_patch_desc.f32", descriptors.data, descriptors.empty() ? 0 : (size_t)descriptors.rows * descriptors.cols * 4);
         dump("out_neighborhoods.f64", neighborhoodsVector.empty() ? nullptr : neighborhoodsVector[0].data(),
              neighborhoodsVector.empty() ? 0 : neighborhoodsVector[0].size() * sizeof(cv::Vec3d));
         std::cout << matches.size() << " matches, " << triagulated.size() << " points with normals, gravity "

@@ -20,6 +20,7 @@
  *   SingleCameraTriangulator  singlecameratriangulator.h:52-93
  *   NormalOptimizer           normaloptimizer.h:43-59
  *   NeighborhoodsGenerator    neighborhoodsgenerator.h:78-97 (square and circular methods)
+ *   MOSAIC                    mosaic.h:47-70 (the pipeline as a descriptor extractor)
  *
  * What differs, and why:
  *   - feature detection/description (descriptorsmatcher.cpp:110-115) is upstream of the GPU path
@@ -455,16 +456,43 @@ public:
         fm3d::compat::check(c, fm3d_match_nndr(c, A.data, A.rows, B.data, B.rows, A.cols, A.type, epsilon, tmp.data(), &n));
         for (int i = 0; i < n; i++) matches.push_back(reinterpret_cast<const cv::DMatch&>(tmp[i]));
     }
-    // descriptorsmatcher.cpp:133-174: SURF descriptors of the patches' centres -- needs the
-    // upstream extractor, which is not built
-    void extractDescriptorsFromPatches(const std::vector<cv::Mat>& /*patchesVector*/, cv::Mat& /*descriptors*/) {
-        throw fm3d::compat::Error(FM3D_ERR_UNSUPPORTED,
-                                  "extractDescriptorsFromPatches needs the SURF extractor (upstream of the GPU path)");
+    // descriptorsmatcher.cpp:133-174: per patch one keypoint at its centre, size = the patch edge,
+    // described by the settings' SURF extractor on the GPU; one descriptor row per patch
+    void extractDescriptorsFromPatches(const std::vector<cv::Mat>& patchesVector, cv::Mat& descriptors) {
+        if (patchesVector.empty()) throw fm3d::compat::Error(FM3D_ERR_INVALID, "no patches");  // descriptorsVector[0]
+        const int size = patchesVector[0].rows;
+        std::vector<uint8_t> all((size_t)patchesVector.size() * size * size);
+        for (size_t i = 0; i < patchesVector.size(); i++) {
+            const cv::Mat& m = patchesVector[i];
+            if (m.rows != size || m.cols != size || m.type() != CV_8UC1)
+                throw fm3d::compat::Error(FM3D_ERR_INVALID, "patches must be equal-size square 8-bit images");
+            std::memcpy(&all[i * (size_t)size * size], m.data, (size_t)size * size);
+        }
+        const int dsize = s_.surfExtended ? 128 : 64;
+        descriptors.create((int)patchesVector.size(), dsize, CV_32FC1);
+        fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
+        fm3d::compat::check(c, fm3d_extract_descriptors_from_patches(c, all.data(), (int)patchesVector.size(), size,
+                                                                     reinterpret_cast<float*>(descriptors.data)));
     }
 
 private:
-    // the detector/extractor output: the caller's keypoints + descriptors, or the side files
+    // the detector + extractor (:110-115): the settings' SURF on the GPU; another detector type has
+    // no GPU implementation, so its output comes from the images' side files (<image>.kpts.f32 and
+    // <image>.desc.u8 / .desc.f32), or from the caller's keypoints + descriptors
     void features(const cv::Mat& img, std::vector<cv::KeyPoint>& kpts, cv::Mat& d) {
+        if (s_.detectorType == FM3D_FEAT_SURF && s_.extractorType == FM3D_FEAT_SURF) {
+            static_assert(sizeof(cv::KeyPoint) == sizeof(fm3d_keypoint), "cv::KeyPoint layout");
+            fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
+            int n = 0, m = 0;
+            fm3d::compat::check(c, fm3d_surf_detect(c, img.data, img.cols, img.rows, nullptr, 0, &n, nullptr));
+            kpts.assign(n, cv::KeyPoint());
+            const int dsize = s_.surfExtended ? 128 : 64;
+            d.create(n, dsize, CV_32FC1);
+            fm3d::compat::check(c, fm3d_surf_detect(c, img.data, img.cols, img.rows,
+                                                    reinterpret_cast<fm3d_keypoint*>(kpts.data()), n, &m,
+                                                    reinterpret_cast<float*>(d.data)));
+            return;
+        }
         if (!kpts.empty() && !d.empty()) return;
         const std::string base = img.source();
         if (base.empty())
@@ -704,6 +732,60 @@ private:
     }
     fm3d_settings s_;
     fm3d::compat::NeighborhoodsGenerator ng_;
+};
+
+// ---------------------------------------------------------------- MOSAIC (mosaic.h:47-70)
+// The constructor runs mosaic.cpp:32-73's seven steps (on the GPU); the reference's computeImpl is
+// empty, compute() describes the patches as main.cpp:182-183 does (extractDescriptorsFromPatches).
+class MOSAIC {
+public:
+    MOSAIC(cv::FileStorage fs, cv::Mat& imgA, cv::Mat& imgB, const cv::Vec3d tA, const cv::Vec3d tB,
+           const cv::Vec3d rA, const cv::Vec3d rB)
+        : imgA_(imgA), imgB_(imgB), dm_(fs, imgA, imgB), sct_(fs), no_(fs, &sct_), ng_(fs) {
+        cv::Mat desc1, desc2;
+        dm_.compareWithNNDR(fs["NNDR"]["epsilon"], matches_, kptsA_, kptsB_, desc1, desc2);
+        sct_.setg12(tA, tB, rA, rB, gAB_);
+        std::vector<bool> outliersMask;
+        sct_.setKeypoints(kptsA_, kptsB_, matches_);
+        sct_.triangulate(triangulated_points_, outliersMask);
+        no_.setImages(imgA_, imgB_);
+        no_.computeOptimizedNormals(triangulated_points_, normals_vector_, colors_);
+        no_.computeFeaturesFrames(triangulated_points_, normals_vector_, features_frames_);
+        ng_.getReferenceSquaredNeighborhood(reference_neighborhood_);
+        sct_.setImages(imgA_, imgB_);
+        sct_.projectReferencePointsToImageWithFrames(reference_neighborhood_, features_frames_, patches_vector_,
+                                                     image_points_vector_);
+    }
+    int descriptorType() { return CV_32F; }
+    int descriptorSize() { return 128; }
+    // one descriptor row per kept feature (the patches' SURF descriptors)
+    void compute(cv::Mat& descriptors) {
+        if (patches_vector_.empty()) {
+            descriptors = cv::Mat();
+            return;
+        }
+        dm_.extractDescriptorsFromPatches(patches_vector_, descriptors);
+    }
+    const std::vector<cv::DMatch>& matches() const { return matches_; }
+    const std::vector<cv::Vec3d>& points() const { return triangulated_points_; }
+    const std::vector<cv::Vec3d>& normals() const { return normals_vector_; }
+    const std::vector<cv::Mat>& patches() const { return patches_vector_; }
+
+private:
+    cv::Mat imgA_, imgB_;
+    DescriptorsMatcher dm_;
+    std::vector<cv::KeyPoint> kptsA_, kptsB_;
+    std::vector<cv::DMatch> matches_;
+    std::vector<cv::Vec3d> triangulated_points_;
+    SingleCameraTriangulator sct_;
+    cv::Matx44d gAB_;
+    std::vector<cv::Mat> patches_vector_, image_points_vector_;
+    NormalOptimizer no_;
+    std::vector<cv::Vec3d> normals_vector_;
+    std::vector<cv::Matx44d> features_frames_;
+    NeighborhoodsGenerator ng_;
+    std::vector<cv::Vec3d> reference_neighborhood_;
+    std::vector<cv::Scalar> colors_;
 };
 
 // ---------------------------------------------------------------- tools.cpp drawing (visual only)

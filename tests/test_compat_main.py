@@ -204,3 +204,100 @@ def test_dropin_main_matches_python_api(fm3d, synth, orc, tmp_path):
     assert np.array_equal(nb0, orc.square_neighborhoods(frames[:1])[0])
     for f in ("matches.pgm", "projectedPatches.pgm"):
         assert (d / f).read_bytes().startswith(b"P6\n")
+
+
+SURF_OPTIONS = """FeatureOptions:
+   DetectorType: SURF
+   DetectorMode: STATIC
+   SurfDetector:
+      HessianThreshold: 400
+      NumOctaves: 4
+      NumOctaveLayers: 2
+      Extended: 1
+      Upright: 1
+   ExtractorType: SURF
+"""
+
+
+def _python_chain(fm3d, s, img1, img2):
+    """main.cpp:91-183 through the Python mirror: SURF compareWithNNDR from the images, triangulation,
+    normals, frames, patches, patch descriptors."""
+    ctx = fm3d.Context(s)
+    try:
+        m, ka, kb, _, _ = fm3d.DescriptorsMatcher(ctx).compareWithNNDRImages(s.nndrEpsilon, img1, img2)
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.setg12(s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+        xy = lambda k: np.stack([k["x"], k["y"]], axis=1).astype(np.float32)
+        sct.setKeypoints(xy(ka), xy(kb), m)
+        P, _ = sct.triangulate()
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(img1, img2)
+        kept, normals = no.computeOptimizedNormals(P)
+        frames = no.computeFeaturesFrames(kept, normals)
+        patches = sct.projectReferencePointsToImageWithFrames(None, frames)
+        desc = fm3d.SURF(ctx).extractDescriptorsFromPatches(patches) if len(patches) else np.zeros((0, 128), np.float32)
+    finally:
+        ctx.close()
+    return m, kept, normals, patches, desc
+
+
+@pytest.mark.gpu
+def test_dropin_main_surf_detection(fm3d, synth, orc, tmp_path):
+    """main_dropin -s settings.yml with the reference's FeatureOptions (STATIC SURF, upright,
+    extended): features detected and described on the GPU from the images alone, and the patch
+    descriptors of main.cpp:182-183 -- all equal to the Python mirror; the patch descriptors equal
+    the SURF oracle's."""
+    pair = synth.make_frame_pair(1500, seed=24)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.6)
+    yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
+    (d / "settings.yml").write_text(yml + SURF_OPTIONS)
+    r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
+    assert r.returncode == 0, r.stderr + r.stdout
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    assert s.detectorType == 0 and s.extractorType == 0 and s.surfExtended == 1 and s.surfUpright == 1
+    m, kept, normals, patches, desc = _python_chain(fm3d, s, pair.img1, pair.img2)
+    assert np.fromfile(d / "out_matches.bin", dtype=fm3d.DMATCH).tobytes() == m.tobytes()
+    assert np.array_equal(np.fromfile(d / "out_points.f64").reshape(-1, 3), kept)
+    assert np.array_equal(np.fromfile(d / "out_normals.f64").reshape(-1, 3), normals)
+    assert len(m) > 50 and len(kept) > 5
+    pd = np.fromfile(d / "out_patch_desc.f32", dtype=np.float32).reshape(-1, 128)
+    assert np.array_equal(pd, desc)
+    kp = np.zeros(1, dtype=fm3d.KEYPOINT)
+    kp["x"] = kp["y"] = 64
+    kp["size"] = 128
+    kp["angle"] = -1
+    ref = np.stack([orc.surf_describe(p, kp)[2][0] for p in patches[:8]])
+    assert np.array_equal(pd[:8], ref)
+
+
+@pytest.mark.gpu
+def test_mosaic_python_and_cpp(fm3d, synth, tmp_path):
+    """MOSAIC (mosaic.h:47-70, mosaic.cpp:32-73): the Python class and the C++ one (mosaic_demo,
+    include/fm3d_cv.hpp) run the same pipeline; their patch descriptors and points equal the
+    step-by-step chain."""
+    pair = synth.make_frame_pair(1500, seed=25)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.6)
+    yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
+    (d / "settings.yml").write_text(yml + SURF_OPTIONS)
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    m, kept, normals, patches, desc = _python_chain(fm3d, s, pair.img1, pair.img2)
+    ctx = fm3d.Context(s)
+    try:
+        mo = fm3d.MOSAIC(ctx, pair.img1, pair.img2, s.pos1[:3], s.pos2[:3], s.pos1[3:], s.pos2[3:])
+        md = mo.compute()
+    finally:
+        ctx.close()
+    assert mo.matches.tobytes() == m.tobytes()
+    assert np.array_equal(mo.triangulated_points, kept) and np.array_equal(mo.normals, normals)
+    assert np.array_equal(mo.patches, patches) and np.array_equal(md, desc) and md.shape[1] == 128
+    exe = os.path.join(ROOT, "examples", "mosaic_demo")
+    r = subprocess.run([exe, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert np.array_equal(np.fromfile(d / "mosaic_desc.f32", dtype=np.float32).reshape(-1, 128), desc)
+    assert np.array_equal(np.fromfile(d / "mosaic_points.f64").reshape(-1, 3), kept)
