@@ -35,6 +35,7 @@ EXPORTS = (
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
     "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
+    "fm3d_ncc_hypotheses",
 )
 
 
@@ -437,6 +438,20 @@ class NormalOptimizer:
         g = np.zeros(3)
         _check(lib().fm3d_gravity(ctypes.byref(self.ctx.settings), _ptr(g)))
         return g
+
+    def nccHypotheses(self, points3D: np.ndarray, hphi: int = 4, htheta: int = 4, span: float = 0.4):
+        """NCC scoring of hphi x htheta candidate normals per point (fm3d_ncc_hypotheses; BASELINE's
+        "patch NCC over 16 / 32 normal hypotheses" -- an extension, the reference has no NCC search):
+        (scores (P, H) float64, -2 = invalid; best normals (P, 3); best index (P,), -1 = none).
+        Needs setImages and the camera-2 pose of the triangulator."""
+        X = np.ascontiguousarray(points3D, dtype=np.float64).reshape(-1, 3)
+        n, H = X.shape[0], hphi * htheta
+        scores = np.zeros((max(n, 1), H))
+        normals = np.zeros((max(n, 1), 3))
+        best = np.zeros(max(n, 1), dtype=np.int32)
+        self.ctx.check(lib().fm3d_ncc_hypotheses(self.ctx.handle, _ptr(X), n, hphi, htheta, ctypes.c_double(span),
+                                                 _ptr(scores), _ptr(normals), _ptr(best, ctypes.c_int32)))
+        return scores[:n], normals[:n], best[:n]
 
     def computeFeaturesFrames(self, points3D: np.ndarray, normals: np.ndarray) -> np.ndarray:
         """computeFeaturesFrames (normaloptimizer.cpp:454-504): (P, 4, 4) frames, on the GPU."""

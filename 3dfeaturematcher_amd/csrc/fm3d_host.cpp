@@ -1425,6 +1425,54 @@ int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, i
     return FM3D_OK;
 }
 
+int fm3d_ncc_hypotheses(fm3d_ctx* c, const double* points, int P, int Hphi, int Htheta, double span, double* scores,
+                        double* normals, int32_t* best) {
+    if (!c || P < 0 || Hphi <= 0 || Htheta <= 0 || Hphi * Htheta > 32 || (P && (!points || !scores || !normals || !best)))
+        return FM3D_ERR_INVALID;
+    if (c->pyr1.empty()) return fail(c, FM3D_ERR_INVALID, "fm3d_set_images (NormalOptimizer::setImages) not called");
+    if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "fm3d_set_g12 / fm3d_setg12 not called");
+    if (P == 0) return FM3D_OK;
+    hipSetDevice(c->device);
+    int r;
+    if ((r = ensure_offsets(c))) return r;
+    const int H = Hphi * Htheta;
+    DevBuf X, S, N, B;
+    HIPCHK(c, X.ensure((size_t)P * 3 * sizeof(double)));
+    HIPCHK(c, S.ensure((size_t)P * H * sizeof(double)));
+    HIPCHK(c, N.ensure((size_t)P * 3 * sizeof(double)));
+    HIPCHK(c, B.ensure((size_t)P * sizeof(int)));
+    HIPCHK(c, hipMemcpyAsync(X.p, points, (size_t)P * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    fm3d::NccParams p{};
+    p.points = X.as<double>();
+    p.P = P;
+    p.cam = c->cam;
+    std::memcpy(p.R2, c->R2, sizeof(p.R2));
+    std::memcpy(p.t2, c->t2, sizeof(p.t2));
+    p.img1 = c->pyr1[0].as<uint8_t>();
+    p.img2 = c->pyr2[0].as<uint8_t>();
+    p.w = c->lw[0];
+    p.h = c->lh[0];
+    p.offsets = c->offsets.as<int2>();
+    p.nOff = c->nOff;
+    p.nOffPad = c->nOffPad;
+    p.boundW = c->s.boundWidth;
+    p.boundH = c->s.boundHeight;
+    p.cmax = (int)(2 * c->s.zThresholdMax);
+    p.Hphi = Hphi;
+    p.Htheta = Htheta;
+    p.span = span;
+    p.scores = S.as<double>();
+    p.normals = N.as<double>();
+    p.best = B.as<int>();
+    fm3d::launch_ncc_hypotheses(p, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(scores, S.p, (size_t)P * H * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(normals, N.p, (size_t)P * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(best, B.p, (size_t)P * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
 int fm3d_pyrdown(fm3d_ctx* c, const uint8_t* src, int width, int height, uint8_t* dst) {
     if (!c || !src || !dst || width <= 0 || height <= 0) return FM3D_ERR_INVALID;
     hipSetDevice(c->device);

@@ -99,6 +99,24 @@ void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int di
 void launch_nndr(int type, const int* idx, const int* key, const float* fkey, int nA, int nB, double eps,
                  int queryOffset, fm3d_dmatch* knnOut, fm3d_dmatch* cand, int* flag, hipStream_t s);
 
+// ---------------- NCC normal hypotheses (fm3d_ncc.hip) ----------------
+struct NccParams {
+    const double* points;  // P x 3
+    int P;
+    Camera cam;
+    double R2[9], t2[3];
+    const uint8_t *img1, *img2;  // pyramid level 0 (+ zero guard)
+    int w, h;
+    const int2* offsets;  // circle offsets in reference order, padded
+    int nOff, nOffPad, boundW, boundH, cmax;
+    int Hphi, Htheta;  // hypotheses: Hphi x Htheta grid (H <= 32)
+    double span;       // grid half width in radians
+    double* scores;    // P x H (-2: a failing pixel or a flat patch)
+    double* normals;   // P x 3 best normal (the initial guess if none scores)
+    int* best;         // P (-1: none)
+};
+void launch_ncc_hypotheses(const NccParams& p, hipStream_t s);
+
 // ---------------- SURF (fm3d_surf.hip) ----------------
 struct SurfHF {  // a box of a resized Haar pattern: sum[p0] + sum[p3] - sum[p1] - sum[p2], weight w
     int p0, p1, p2, p3;

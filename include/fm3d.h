@@ -203,6 +203,18 @@ int fm3d_get_pyramid_level(const fm3d_ctx *ctx, int which, int level, uint8_t *o
 int fm3d_optimize_normals(fm3d_ctx *ctx, double *points, int P, double *normals, int32_t *status,
                           int32_t *info, int32_t *nfev, int *nKept, fm3d_lm_stats *stats);
 
+/* NCC scoring of Hphi x Htheta candidate normals per point (BASELINE.json's "patch NCC over 16 / 32
+   normal hypotheses"; the reference has no such search -- SURVEY.md D2 -- so this is an extension on
+   the reference's evaluateNormal geometry, normaloptimizer.cpp:65-149): normals sph2car(phi0 + dphi,
+   theta0 + dtheta) on a grid of half width span (radians) around car2sph(X/|X|), scored by the NCC of
+   the pyramid-level-0 image-1 samples of the extractPixelsContour neighbourhood and the image-2
+   samples through each normal's plane (-2: a pixel fails the bounding box / isPixelGood, or a flat
+   patch).  Needs fm3d_set_images and the camera-2 pose (fm3d_set_g12).  scores: P x H doubles
+   (hypothesis h = iphi*Htheta + itheta); normals: P x 3, the best scoring normal (lowest h on ties;
+   the initial guess if none scores); best: P (-1 if none).  H <= 32. */
+int fm3d_ncc_hypotheses(fm3d_ctx *ctx, const double *points, int P, int Hphi, int Htheta, double span, double *scores,
+                        double *normals, int32_t *best);
+
 /* ---------------- feature frames + patch export (after the hot path) ---------------- */
 /* gravity_ of the NormalOptimizer ctor (normaloptimizer.cpp:160-178):
    Rodrigues(rodriguesIC).inv() * (0, 0, -1) */

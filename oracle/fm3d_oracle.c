@@ -1179,6 +1179,95 @@ ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], cons
     return kept;
 }
 
+/* NCC scoring of candidate normals (fm3d_ncc_hypotheses; BASELINE.json's "patch NCC over 16 / 32
+   normal hypotheses" -- the reference has none, SURVEY.md D2, so this restates the extension on the
+   reference's own geometry: extractPixelsContour :341-397, evaluateNormal :65-149 with the
+   deterministic transcendentals).  Per point: normals sph2car(phi0 + dphi, theta0 + dtheta) on an
+   Hphi x Htheta grid of half width span around car2sph(X/|X|); per normal the level-0 samples
+   I1 (image 1 at the pixel) and I2 (image 2 through the plane); score = NCC or -2 (a failing
+   pixel, a flat patch).  The five sums are accumulated per lane l = offset index mod 64 in offset
+   order and combined by the xor tree over 64 lanes -- the GPU's order, so the scores are bit-equal.
+   scores: P x H, normals: P x 3 (best, lowest h on ties; X/|X| if none), best: P (-1 if none). */
+ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const double t2[3], const uint8_t *img1,
+                                const uint8_t *img2, int w, int h, const double *points, int P, int ray, int boundW,
+                                int boundH, double zmax, int Hphi, int Htheta, double span, double *scores,
+                                double *normals, int *best)
+{
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    static const double Z[3] = {0, 0, 0};
+    const int H = Hphi * Htheta, cmax = (int)(2 * zmax);
+    const double cm = (double)cmax;
+    int p;
+    #pragma omp parallel for schedule(dynamic, 1)
+    for (p = 0; p < P; p++) {
+        const double *X = points + 3 * (size_t)p;
+        double ccx, ccy, g[3], phi0, theta0, inv;
+        int hh, e, l, bestH = -1, i, j;
+        double bs = -2.;
+        orc_project1(cam, I, Z, X[0], X[1], X[2], &ccx, &ccy);
+        inv = 1. / sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+        g[0] = X[0] * inv; g[1] = X[1] * inv; g[2] = X[2] * inv;
+        orc_car2sph(ORC_LM_DETMATH, g, &phi0, &theta0);
+        for (hh = 0; hh < H; hh++) {
+            const int ip = hh / Htheta, it = hh - ip * Htheta;
+            const double dphi = span * (double)(2 * ip + 1 - Hphi) / Hphi;
+            const double dtheta = span * (double)(2 * it + 1 - Htheta) / Htheta;
+            double n[3], mm, S[5][64], T[5], sc = -2.;
+            int m = 0, fail = 0, o;
+            orc_sph2car(ORC_LM_DETMATH, phi0 + dphi, theta0 + dtheta, n);
+            mm = n[0] * X[0] + n[1] * X[1] + n[2] * X[2];
+            memset(S, 0, sizeof(S));
+            e = 0;
+            for (i = -ray; i <= ray; i++)
+                for (j = -ray; j <= ray; j++) {
+                    double px, py, ux, uy, nn, k, P0, P1, P2, u, v, a, b;
+                    if (i * i + j * j > ray * ray) continue;
+                    l = e++ & 63;  /* the offset index's lane */
+                    px = ccx + i;
+                    py = ccy + j;
+                    if (px < 0 || py < 0 || px >= boundW || py >= boundH) continue;
+                    m++;
+                    if (fail) continue;
+                    if (!orc_pixel_good(px, py, 1.0, w, h)) { fail = 1; continue; }
+                    a = (double)orc_bilinear(img1, w, h, (float)px, (float)py);
+                    orc_undistort1(cam, px, py, &ux, &uy);
+                    nn = n[0] * ux + n[1] * uy + n[2] * 1.;
+                    k = mm / nn;
+                    P0 = k * ux; P1 = k * uy; P2 = k * 1.;
+                    if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm))) { fail = 1; continue; }
+                    orc_project1(cam, R2, t2, P0, P1, P2, &u, &v);
+                    if (!orc_pixel_good(u, v, 1.0, w, h)) { fail = 1; continue; }
+                    b = (double)orc_bilinear(img2, w, h, (float)u, (float)v);
+                    S[0][l] += a; S[1][l] += b; S[2][l] += a * a; S[3][l] += b * b; S[4][l] += a * b;
+                }
+            for (o = 0; o < 5; o++) {
+                double v[64], t[64];
+                int s2;
+                memcpy(v, S[o], sizeof(v));
+                for (s2 = 32; s2 > 0; s2 >>= 1) {
+                    for (l = 0; l < 64; l++) t[l] = v[l] + v[l ^ s2];
+                    memcpy(v, t, sizeof(v));
+                }
+                T[o] = v[0];
+            }
+            if (!fail && m > 0) {
+                const double cov = T[4] - T[0] * T[1] / m, va = T[2] - T[0] * T[0] / m, vb = T[3] - T[1] * T[1] / m;
+                if (va > 0 && vb > 0) sc = cov / sqrt(va * vb);
+            }
+            scores[(size_t)p * H + hh] = sc;
+            if (sc > bs) { bs = sc; bestH = hh; }
+        }
+        best[p] = bestH;
+        if (bestH >= 0) {
+            const int ip = bestH / Htheta, it = bestH - ip * Htheta;
+            orc_sph2car(ORC_LM_DETMATH, phi0 + span * (double)(2 * ip + 1 - Hphi) / Hphi,
+                        theta0 + span * (double)(2 * it + 1 - Htheta) / Htheta, normals + 3 * (size_t)p);
+        } else {
+            normals[3 * p] = g[0]; normals[3 * p + 1] = g[1]; normals[3 * p + 2] = g[2];
+        }
+    }
+}
+
 /* Single-level LM on one point from a given starting (phi, theta): used by the
    tests that pin lmdif against scipy.optimize.leastsq on the same residual. */
 ORC_API int orc_lm_single_level(const orc_camera *cam, const double R2[9], const double t2[3],

@@ -258,6 +258,27 @@ def circular_neighborhoods(points, normals=None, eps=0.16, thetas=15, rays=5):
     return out
 
 
+def ncc_hypotheses(cam, R2, t2, img1, img2, points, ray, hphi=4, htheta=4, span=0.4, bound=(1024, 768), zmax=2.4):
+    """NCC scoring of hphi x htheta candidate normals per point (the GPU's fm3d_ncc_hypotheses):
+    (scores (P, H), best normals (P, 3), best index (P,))."""
+    X = _f64(points).reshape(-1, 3)
+    n = X.shape[0]
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    h, w = img1.shape
+    H = hphi * htheta
+    scores = np.zeros((max(n, 1), H))
+    normals = np.zeros((max(n, 1), 3))
+    best = np.zeros(max(n, 1), dtype=np.int32)
+    c = OrcCamera.from_cam(cam)
+    lib().orc_ncc_hypotheses(ctypes.byref(c), _p(_f64(R2)), _p(_f64(t2)), _p(img1, ctypes.c_uint8),
+                             _p(img2, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _p(X), ctypes.c_int(n),
+                             ctypes.c_int(ray), ctypes.c_int(bound[0]), ctypes.c_int(bound[1]), ctypes.c_double(zmax),
+                             ctypes.c_int(hphi), ctypes.c_int(htheta), ctypes.c_double(span), _p(scores), _p(normals),
+                             _p(best, ctypes.c_int))
+    return scores[:n], normals[:n], best[:n]
+
+
 def export_patches(cam, img1, frames, eps=0.16, cmpp=0.25, mode=STRICT, image_points=False):
     img1 = np.ascontiguousarray(img1, dtype=np.uint8)
     h, w = img1.shape

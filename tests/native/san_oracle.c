@@ -90,6 +90,17 @@ int main(void)
             orc_export_patches(&cam, im1, W, H, fr, P, 0.02, 0.25, ORC_LM_DETMATH, patch, NULL);
         }
     }
+    /* NCC hypotheses: points inside, behind and far outside the images */
+    {
+        static double nx[9] = {0.05, -0.02, 1.9, 0.0, 0.0, 0.0, 4.0, 4.0, 2.0}, sc[3 * 32], nn[9];
+        static int bb[3];
+        static uint8_t i1[64 * 48], i2[64 * 48];
+        static const double R2i[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t2i[3] = {0.01, 0, 0};
+        orc_camera c0 = {60, 60, 32, 24, {-0.2, 0.05, 0.001, 0.001, 0.0}};
+        for (i = 0; i < 64 * 48; i++) { i1[i] = (uint8_t)rnd(); i2[i] = (uint8_t)rnd(); }
+        orc_ncc_hypotheses(&c0, R2i, t2i, i1, i2, 64, 48, nx, 3, 5, 64, 48, 2.4, 8, 4, 0.4, sc, nn, bb);
+        orc_ncc_hypotheses(&c0, R2i, t2i, i1, i2, 64, 48, nx, 3, 3, 64, 48, 2.4, 1, 1, 0.4, sc, nn, bb);
+    }
     /* circular neighbourhoods (given normals and the X/|X| branch) */
     {
         static double X[6] = {0.1, -0.2, 1.9, 0.3, 0.1, 2.1}, N[6] = {0, 0.1, -0.99, 0.2, 0.2, -0.95}, o[2 * 15 * 5 * 3];

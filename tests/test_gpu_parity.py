@@ -469,6 +469,28 @@ def test_circular_neighborhoods_bitwise(fm3d, orc, pair, given_normals):
         ctx.close()
 
 
+@pytest.mark.parametrize("ray,hphi,htheta", [(16, 4, 4), (32, 8, 4), (8, 1, 3)])
+def test_ncc_hypotheses_bitwise(fm3d, orc, pair, ray, hphi, htheta):
+    """NCC scoring of candidate normals (fm3d_ncc_hypotheses) on the GPU against the oracle, bit for
+    bit: scores of every hypothesis, the best normal and its index (16 and 32 hypotheses, VGA bounds
+    so that border points fail, a degenerate 1 x 3 grid)."""
+    s = _settings(fm3d, pair.cam, pixelsRay=ray, boundWidth=640, boundHeight=480)
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(pair.g12)
+        R2, t2 = sct.camera2()
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(pair.img1, pair.img2)
+        X = np.concatenate([pair.points[:300], [[0.0, 0.0, 0.0], [5.0, 5.0, 2.0]]])
+        sc, nb, b = no.nccHypotheses(X, hphi, htheta, 0.4)
+    finally:
+        ctx.close()
+    rs, rn, rb = orc.ncc_hypotheses(pair.cam, R2, t2, pair.img1, pair.img2, X, ray, hphi, htheta, 0.4, bound=(640, 480))
+    assert np.array_equal(b, rb) and np.array_equal(sc, rs) and np.array_equal(nb, rn)
+    assert (b >= 0).mean() > 0.5
+
+
 def test_c2_sift10k_match_and_dlt(fm3d, orc, synth):
     """BASELINE configs[1] (C2): 10k SIFT-128 per frame, brute-force L2 match + NNDR + DLT --
     match indices, distances, inlier mask and points bit-exact against the oracle."""

@@ -210,3 +210,32 @@ def test_reference_patch_size():
     of the reference's results/*/patch_*.pgm (P5 128 128)."""
     import oracle
     assert oracle.patch_size(0.16, 0.25) == 128
+
+
+def test_ncc_hypotheses_oracle(orc, synth):
+    """NCC scoring of candidate normals (the BASELINE's hypothesis mode; no reference counterpart):
+    (1) with image 2 = image 1 seen from the same pose every plane maps every pixel back onto itself,
+    so every hypothesis scores NCC ~ 1; (2) on the ray-cast scene the best of 4 x 4 hypotheses is
+    closer to the true plane normal than the X/|X| initial guess for most points."""
+    import dataclasses
+    pair = synth.make_frame_pair(400, seed=5)
+    X = pair.points[:120]
+    I3, z3 = np.eye(3), np.zeros(3)
+    # the identity pose: every plane maps a pixel back onto itself (up to the 5-iteration
+    # undistortion's residual), so the scores of a point do not depend on the hypothesis ...
+    sc, _, b = orc.ncc_hypotheses(pair.cam, I3, z3, pair.img1, pair.img1, X, 8, 4, 4, 0.4, bound=(640, 480))
+    ok = (sc > -2).all(axis=1)
+    assert ok.mean() > 0.8 and np.abs(sc[ok] - sc[ok][:, :1]).max() < 1e-9
+    # ... and without lens distortion the round trip is exact: NCC 1 for every hypothesis
+    cam0 = dataclasses.replace(pair.cam, k=(0.0, 0.0, 0.0, 0.0, 0.0))
+    sc, _, b = orc.ncc_hypotheses(cam0, I3, z3, pair.img1, pair.img1, X, 8, 4, 4, 0.4, bound=(640, 480))
+    ok = (sc > -2).all(axis=1)
+    assert ok.mean() > 0.8 and sc[ok].min() > 1 - 1e-9 and (b[ok] == np.argmax(sc[ok], axis=1)).all()
+    R2, t2 = orc.camera2_from_g12(pair.g12)
+    sc, nb, b = orc.ncc_hypotheses(pair.cam, R2, t2, pair.img1, pair.img2, X, 16, 4, 4, 0.4, bound=(640, 480))
+    assert sc.shape == (120, 16) and ((sc >= -1 - 1e-12) | (sc == -2)).all() and (sc <= 1 + 1e-12).all()
+    v = b >= 0
+    g = X / np.linalg.norm(X, axis=1, keepdims=True)
+    ang = lambda a, n: np.degrees(np.arccos(np.clip(np.abs((a * n).sum(1)), 0, 1)))
+    assert v.mean() > 0.6
+    assert (ang(nb, pair.normals[:120]) < ang(g, pair.normals[:120]))[v].mean() > 0.65
