@@ -487,7 +487,8 @@ def test_ncc_hypotheses_bitwise(fm3d, orc, pair, ray, hphi, htheta):
     finally:
         ctx.close()
     rs, rn, rb = orc.ncc_hypotheses(pair.cam, R2, t2, pair.img1, pair.img2, X, ray, hphi, htheta, 0.4, bound=(640, 480))
-    assert np.array_equal(b, rb) and np.array_equal(sc, rs) and np.array_equal(nb, rn)
+    assert np.array_equal(b, rb) and np.array_equal(sc, rs) and np.array_equal(nb, rn, equal_nan=True)
+    assert np.isnan(nb[-2]).all() and b[-2] == -1  # X = 0: no pixel, the initial guess 0/0
     assert (b >= 0).mean() > 0.5
 
 
