@@ -99,7 +99,8 @@ class LMStats(ctypes.Structure):
                 ("wall_clock_khz", ctypes.c_int64), ("class_passes", ctypes.c_int64 * 4),
                 ("class_cycles", ctypes.c_int64 * 4), ("last_group_start_ticks", ctypes.c_int64),
                 ("last_group_end_ticks", ctypes.c_int64), ("cycles_wait", ctypes.c_int64),
-                ("chain_rounds", ctypes.c_int64), ("chain_chunks", ctypes.c_int64)]
+                ("chain_rounds", ctypes.c_int64), ("chain_chunks", ctypes.c_int64),
+                ("queue_empty_ticks", ctypes.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}

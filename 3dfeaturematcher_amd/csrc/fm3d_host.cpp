@@ -438,6 +438,7 @@ void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_st
     st->cycles_wait = (int64_t)cnt[24];
     st->chain_rounds = (int64_t)cnt[21];
     st->chain_chunks = (int64_t)cnt[22];
+    st->queue_empty_ticks = cnt[25] ? (int64_t)(cnt[25] - cnt[20]) : 0;
 }
 
 // LM normals over nPts device points (c->pts), outputs in c->lm*
@@ -929,7 +930,7 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
     if ((r = run_lm(c, P, stats, c->ev[0], c->ev[1]))) return r;
     std::vector<double> nrm((size_t)P * 3);
     std::vector<int> st(P), inf((size_t)P * 8), nf((size_t)P * 8);
-    unsigned long long cnt[25] = {};
+    unsigned long long cnt[26] = {};
     if (P) {
         HIPCHK(c, hipMemcpyAsync(nrm.data(), c->lmNormals.p, nrm.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(st.data(), c->lmStatus.p, st.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1066,7 +1067,7 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
                                  c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
     int kept = 0;
-    unsigned long long cnt[25] = {};
+    unsigned long long cnt[26] = {};
     HIPCHK(c, hipMemcpyAsync(&kept, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));

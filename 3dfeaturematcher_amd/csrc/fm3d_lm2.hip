@@ -141,6 +141,7 @@ struct Ctl2 {
             return;
         }
         S.pidx = q;
+        atomicMax(p->statPass + 22, wall_clock64());  // the last point handed out: the queue runs dry
         S.X0 = p->points[3 * q + 0];
         S.X1 = p->points[3 * q + 1];
         S.X2 = p->points[3 * q + 2];

@@ -342,6 +342,7 @@ def lm_profile(lm):
                                       zip(("jac", "eval", "qr", "once"), lm["class_passes"], lm["class_cycles"])},
         "passes_by_class": dict(zip(("jac", "eval", "qr", "once"), lm["class_passes"])),
         "last_group_end_ms": lm["last_group_end_ticks"] / max(lm["wall_clock_khz"], 1),
+        "queue_empty_ms": lm.get("queue_empty_ticks", 0) / max(lm["wall_clock_khz"], 1),
         # chain wave: cycles per busy round (up to two chunks of 64 dependent adds per lane) and
         # chunks added per round over the group's lanes
         "chain_cycles_per_round": lm["cycles_chain"] / max(lm.get("chain_rounds", 0), 1),

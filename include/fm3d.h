@@ -139,6 +139,9 @@ typedef struct fm3d_lm_stats {
     /* chain wave: busy rounds (each adds up to two chunks per lane) and chunks added, summed
        over workgroups and lanes */
     int64_t chain_rounds, chain_chunks;
+    /* wall-clock ticks from the first workgroup start to the last point handed out (the queue
+       runs dry there: the rest of the launch is the tail) */
+    int64_t queue_empty_ticks;
 } fm3d_lm_stats;
 
 typedef struct fm3d_pipeline_stats {
