@@ -257,16 +257,19 @@ class SURF:
         KeypointGreater order; with_descriptors: (keypoints, descriptors) of the same call."""
         img = np.ascontiguousarray(image, dtype=np.uint8)
         h, w = img.shape
-        n = ctypes.c_int(0)
-        self.ctx.check(lib().fm3d_surf_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, None, 0,
-                                              ctypes.byref(n), None))
-        k = np.zeros(max(n.value, 1), dtype=KEYPOINT)
-        d = np.zeros((max(n.value, 1), self.descriptorSize), dtype=np.float32) if with_descriptors else None
-        m = ctypes.c_int(0)
-        self.ctx.check(lib().fm3d_surf_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(k), n.value,
-                                              ctypes.byref(m), _ptr(d, ctypes.c_float) if d is not None else None))
-        k = k[:m.value]
-        return (k, d[:m.value]) if with_descriptors else k
+        # one detection with room for one keypoint per 64 pixels; again only if more were found
+        cap = max(4096, w * h // 64)
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            d = np.zeros((cap, self.descriptorSize), dtype=np.float32) if with_descriptors else None
+            n = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_surf_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(k), cap,
+                                                  ctypes.byref(n), _ptr(d, ctypes.c_float) if d is not None else None))
+            if n.value <= cap:
+                break
+            cap = n.value
+        k = k[:n.value]
+        return (k, d[:n.value]) if with_descriptors else k
 
     def compute(self, image: np.ndarray, keypoints: np.ndarray):
         """DescriptorExtractor::compute (descriptorsmatcher.cpp:113-114): (kept keypoints, input index

@@ -6,7 +6,7 @@
 // (:133-174).  The algorithm is OpenCV 2.4's nonfree SURF (restated operation for operation in
 // oracle/orc_surf.c; the GPU equals that oracle bit for bit):
 //   integral_rows_kernel / integral_cols_kernel  integral(img, sum, CV_32S): exact int32 prefix sums
-//                        (a wave per row with shuffle scans, then a thread per column);
+//                        (a wave per row with shuffle scans, then banded column scans);
 //   hessian_kernel       calcLayerDetAndTrace for every layer at once: one thread per layer sample,
 //                        10 box sums of the resized Haar patterns (40 integral reads, L2-resident),
 //                        float det / trace;
@@ -14,12 +14,12 @@
 //                        non-maximum suppression, interpolateKeypoint (Cramer's rule in float),
 //                        appended through an atomic counter; then a device merge sort by
 //                        KeypointGreater (discovery order breaks ties) and the upright pass;
-//   describe_kernel      SURFInvoker (upright): one wave per keypoint.  The 21x21 INTER_AREA patch
-//                        is computed per output pixel straight from the image (the rotated,
-//                        border-replicated window is never materialised; each lane generates its
-//                        own computeResizeAreaTab entries and sums them in OpenCV's order), then the
-//                        2x2 Haar gradients with the Gaussian weights, the 4x4 subregion sums (one lane
-//                        each, OpenCV's sample order) and the unit-length scale.
+//   describe_kernel      SURFInvoker (upright): one workgroup per keypoint.  The 21x21 INTER_AREA
+//                        patch comes straight from the image (the rotated, border-replicated window
+//                        is never materialised): OpenCV's row buffers, one per window row, in LDS,
+//                        then the beta-weighted rows per destination row, both in OpenCV's order;
+//                        then the 2x2 Haar gradients with the Gaussian weights, the 4x4 subregion
+//                        sums (one lane each, OpenCV's sample order) and the unit-length scale.
 // Everything is integer or float/double work without reductions across lanes except the
 // descriptor's squared magnitude, summed by lane 0 in the reference's order.
 #include <hip/hip_runtime.h>
@@ -57,16 +57,37 @@ __global__ __launch_bounds__(64) void integral_rows_kernel(const uint8_t* __rest
         carry += __shfl(v, 63);
     }
 }
-// pass 2: column sums down the rows (a thread per column, coalesced across the row)
-__global__ void integral_cols_kernel(int w, int h, int* __restrict__ sum) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x > w) return;
-    sum[x] = 0;
-    int acc = 0;
-    for (int y = 1; y <= h; y++) {
-        int* p = sum + (size_t)y * (w + 1) + x;
-        acc += *p;
-        *p = acc;
+// pass 2: column sums down the rows.  A workgroup takes 64 columns and its 16 waves 16 bands of
+// rows: each band's column sums first (independent loads), then each band's running sums from the
+// bands above it.  Exact: 32-bit wrap-around adds in any order.
+constexpr int kIntBands = 16;
+__global__ __launch_bounds__(64 * kIntBands) void integral_cols_kernel(int w, int h, int* __restrict__ sum) {
+    __shared__ unsigned bandSum[kIntBands][64];
+    const int lane = threadIdx.x & 63, band = threadIdx.x >> 6;
+    const int x = blockIdx.x * 64 + lane;
+    const int rows = (h + kIntBands - 1) / kIntBands;
+    const int y0 = 1 + band * rows, y1 = min(h + 1, y0 + rows);
+    const bool ok = x <= w;
+    const size_t ld = (size_t)w + 1;
+    unsigned t = 0;
+    if (ok)
+        for (int y = y0; y < y1; y++) t += (unsigned)sum[(size_t)y * ld + x];
+    bandSum[band][lane] = t;
+    __syncthreads();
+    if (!ok) return;
+    unsigned acc = 0;
+    for (int b = 0; b < band; b++) acc += bandSum[b][lane];
+    if (band == 0) sum[x] = 0;
+    constexpr int kU = 8;  // loads of a batch issued before its dependent adds
+    for (int y = y0; y < y1; y += kU) {
+        unsigned v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) v[u] = y + u < y1 ? (unsigned)sum[(size_t)(y + u) * ld + x] : 0u;
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            acc += v[u];
+            if (y + u < y1) sum[(size_t)(y + u) * ld + x] = (int)acc;
+        }
     }
 }
 
@@ -235,23 +256,78 @@ __device__ __forceinline__ uint8_t sat_u8(float v) {
     return (uint8_t)(iv < 0 ? 0 : (iv > 255 ? 255 : iv));
 }
 
-// keypoint q's descriptor (the list is compacted: every wavelet fits); one wave per keypoint
+// computeResizeAreaTab (OpenCV 2.4 imgproc/resize.cpp) of destination index d: the partial first
+// cell, the whole cells, the partial last cell, in that order
+struct AreaTab {
+    int s1, cnt, pre, full;  // first whole cell, entries, partial first cell (0/1), whole cells
+    float apre, afull, apost;
+};
+__device__ inline AreaTab area_tab(int d, double scale, int W) {
+    AreaTab t;
+    const double fs1 = d * scale;
+    const double fs2 = fs1 + scale;
+    const double cw = scale < W - fs1 ? scale : W - fs1;
+    int s1 = (int)ceil(fs1);
+    int s2 = (int)floor(fs2);
+    s2 = s2 < W - 1 ? s2 : W - 1;
+    s1 = s1 < s2 ? s1 : s2;
+    t.s1 = s1;
+    t.pre = (s1 - fs1 > 1e-3) ? 1 : 0;
+    const int post = (fs2 - s2 > 1e-3) ? 1 : 0;
+    t.full = s2 - s1;
+    t.cnt = t.pre + t.full + post;
+    t.apre = (float)((s1 - fs1) / cw);
+    t.afull = (float)(1.0 / cw);
+    double a = fs2 - s2;
+    a = a < 1. ? a : 1.;
+    a = a < cw ? a : cw;
+    t.apost = (float)(a / cw);
+    return t;
+}
+// the m-th entry of a tab: source index and weight
+__device__ __forceinline__ int area_entry(const AreaTab& t, int m, float& alpha) {
+    if (t.pre && m == 0) {
+        alpha = t.apre;
+        return t.s1 - 1;
+    }
+    const int r = m - t.pre;
+    if (r < t.full) {
+        alpha = t.afull;
+        return t.s1 + r;
+    }
+    alpha = t.apost;
+    return t.s1 + t.full;
+}
+
+constexpr int kDescThreads = 256;
+constexpr int kDescMaxW = 640;  // window edge whose row buffers fit the LDS of one workgroup
+
+// keypoint q's descriptor (the list is compacted: every wavelet fits); one workgroup per keypoint.
 // imgStride: keypoint q reads image img + q * imgStride (0: one shared image; the patch batch of
-// extractDescriptorsFromPatches: one patch per keypoint)
-__global__ __launch_bounds__(64) void describe_kernel(const uint8_t* __restrict__ img, size_t imgStride, int w, int h,
-                                                      const fm3d_keypoint* __restrict__ kp, int n,
-                                                      const float* __restrict__ DW, int extended,
-                                                      float* __restrict__ desc) {
-    const int q = blockIdx.x, lane = threadIdx.x;
+// extractDescriptorsFromPatches: one patch per keypoint).
+//
+// The W x W window is resized to 21 x 21 with INTER_AREA in OpenCV's two steps: a row buffer per
+// source row (the horizontal weighted sum of that row, in the x-tab's order), then per destination
+// row the beta-weighted rows in the y-tab's order.  A source row's buffer does not depend on the
+// destination row, so each is computed once (all W of them, by the whole workgroup, lanes on
+// consecutive window rows = consecutive image columns, so the byte loads coalesce) and kept in LDS.
+// Windows wider than kDescMaxW take the per-output-pixel path (the same sums, recomputed).
+__global__ __launch_bounds__(kDescThreads) void describe_kernel(const uint8_t* __restrict__ img, size_t imgStride,
+                                                                int w, int h, const fm3d_keypoint* __restrict__ kp,
+                                                                int n, const float* __restrict__ DW, int extended,
+                                                                float* __restrict__ desc) {
+    const int q = blockIdx.x, tid = threadIdx.x;
     if (q >= n) return;
     img += (size_t)q * imgStride;
+    __shared__ float H[kDescMaxW * 21];  // row buffers [window row][destination column]
+    __shared__ AreaTab T[21];
     __shared__ uint8_t P[21 * 21];
     __shared__ float DX[400], DY[400], V[128];
     __shared__ float sc;
     const fm3d_keypoint k = kp[q];
     const float s = k.size * 1.2f / 9.0f;
     const int gws = 2 * cv_roundf(2 * s);
-    if (h + 1 < gws || w + 1 < gws) return;
+    if (h + 1 < gws || w + 1 < gws) return;  // uniform over the workgroup
     const int W = (int)((20 + 1) * s);
     const float win_offset = -(float)(W - 1) / 2;
     const int start_x = cv_roundf(k.x + win_offset), start_y = cv_roundf(k.y - win_offset);
@@ -267,77 +343,97 @@ __global__ __launch_bounds__(64) void describe_kernel(const uint8_t* __restrict_
     const double scale = 1. / (21.0 / W);
     const int iscale = cv_round(scale);
     const bool fast = fabs(scale - iscale) < DBL_EPSILON;
-    for (int pix = lane; pix < 441; pix += 64) {
-        const int dy = pix / 21, dx = pix - dy * 21;
-        if (fast) {
+    if (fast) {
+        // integer scale: exact integer block sums (any order), then OpenCV's rounding:
+        // (sum + 2) >> 2 on the SIMD columns of the 2x2 case, cvRound(sum / iscale^2) elsewhere
+        int* HI = reinterpret_cast<int*>(H);
+        const bool rows = W <= kDescMaxW;
+        if (rows) {
+            for (int e = tid; e < W * 21; e += kDescThreads) {
+                const int dx = e / W, a = e - dx * W;
+                int sm = 0;
+#pragma unroll 8
+                for (int b = 0; b < iscale; b++) sm += WIN(a, dx * iscale + b);
+                HI[a * 21 + dx] = sm;
+            }
+            __syncthreads();
+        }
+        for (int pix = tid; pix < 441; pix += kDescThreads) {
+            const int dy = pix / 21, dx = pix - dy * 21;
             int sm = 0;
-            if (iscale == 2 && dx < 16) {
-                sm = WIN(2 * dy, 2 * dx) + WIN(2 * dy, 2 * dx + 1) + WIN(2 * dy + 1, 2 * dx) + WIN(2 * dy + 1, 2 * dx + 1);
-                P[pix] = (uint8_t)((sm + 2) >> 2);
-            } else {
-                for (int a = 0; a < iscale; a++)
+            for (int a = 0; a < iscale; a++) {
+                if (rows) {
+                    sm += HI[(dy * iscale + a) * 21 + dx];
+                } else {
                     for (int b = 0; b < iscale; b++) sm += WIN(dy * iscale + a, dx * iscale + b);
-                P[pix] = sat_u8(sm * (1.f / (iscale * iscale)));
+                }
             }
-            continue;
+            P[pix] = (iscale == 2 && dx < 16) ? (uint8_t)((sm + 2) >> 2) : sat_u8(sm * (1.f / (iscale * iscale)));
         }
-        // computeResizeAreaTab entries of destination row dy / column dx, generated one by one
-        // (OpenCV's order: the partial first cell, the whole cells, the partial last cell)
-        struct Tab {
-            double fs1, cw;
-            int s1, s2, pre, cnt;
-            float apre, afull, apost;
-        };
-        auto tab = [&](int d) {
-            Tab t;
-            t.fs1 = d * scale;
-            const double fs2 = t.fs1 + scale;
-            t.cw = scale < W - t.fs1 ? scale : W - t.fs1;
-            t.s1 = (int)ceil(t.fs1);
-            t.s2 = (int)floor(fs2);
-            t.s2 = t.s2 < W - 1 ? t.s2 : W - 1;
-            t.s1 = t.s1 < t.s2 ? t.s1 : t.s2;
-            t.pre = (t.s1 - t.fs1 > 1e-3) ? 1 : 0;
-            const int post = (fs2 - t.s2 > 1e-3) ? 1 : 0;
-            t.cnt = t.pre + (t.s2 - t.s1) + post;
-            t.apre = (float)((t.s1 - t.fs1) / t.cw);
-            t.afull = (float)(1.0 / t.cw);
-            double a = fs2 - t.s2;
-            a = a < 1. ? a : 1.;
-            a = a < t.cw ? a : t.cw;
-            t.apost = (float)(a / t.cw);
-            return t;
-        };
-        auto entry = [](const Tab& t, int m, float& alpha) {
-            if (t.pre && m == 0) {
-                alpha = t.apre;
-                return t.s1 - 1;
+    } else {
+        if (tid < 21) T[tid] = area_tab(tid, scale, W);
+        __syncthreads();
+        if (W <= kDescMaxW) {
+            // row buffers: H[a][dx] = sum over the x-tab entries of dx of WIN(a, sx) * alpha
+            for (int e = tid; e < W * 21; e += kDescThreads) {
+                const int dx = e / W, a = e - dx * W;
+                const AreaTab tx = T[dx];
+                float buf = 0.f;
+                // batches of kB gathers in flight before their (ordered) accumulation
+                constexpr int kB = 8;
+                for (int b0 = 0; b0 < tx.cnt; b0 += kB) {
+                    int px[kB];
+#pragma unroll
+                    for (int u = 0; u < kB; u++) {
+                        float alpha;
+                        px[u] = b0 + u < tx.cnt ? WIN(a, area_entry(tx, b0 + u, alpha)) : 0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; u++) {
+                        if (b0 + u < tx.cnt) {
+                            float alpha;
+                            area_entry(tx, b0 + u, alpha);
+                            buf += px[u] * alpha;
+                        }
+                    }
+                }
+                H[a * 21 + dx] = buf;
             }
-            const int r = m - t.pre;
-            if (r < t.s2 - t.s1) {
-                alpha = t.afull;
-                return t.s1 + r;
+            __syncthreads();
+            for (int pix = tid; pix < 441; pix += kDescThreads) {
+                const int dy = pix / 21, dx = pix - dy * 21;
+                const AreaTab ty = T[dy];
+                float acc = 0.f;
+                for (int a = 0; a < ty.cnt; a++) {
+                    float beta;
+                    const int sy = area_entry(ty, a, beta);
+                    const float buf = H[sy * 21 + dx];
+                    acc = a == 0 ? beta * buf : acc + beta * buf;
+                }
+                P[pix] = sat_u8(acc);
             }
-            alpha = t.apost;
-            return t.s2;
-        };
-        const Tab ty = tab(dy), tx = tab(dx);
-        float acc = 0.f;
-        for (int a = 0; a < ty.cnt; a++) {
-            float beta;
-            const int sy = entry(ty, a, beta);
-            float buf = 0.f;
-            for (int b = 0; b < tx.cnt; b++) {
-                float alpha;
-                const int sx = entry(tx, b, alpha);
-                buf += WIN(sy, sx) * alpha;
+        } else {
+            for (int pix = tid; pix < 441; pix += kDescThreads) {
+                const int dy = pix / 21, dx = pix - dy * 21;
+                const AreaTab ty = T[dy], tx = T[dx];
+                float acc = 0.f;
+                for (int a = 0; a < ty.cnt; a++) {
+                    float beta;
+                    const int sy = area_entry(ty, a, beta);
+                    float buf = 0.f;
+                    for (int b = 0; b < tx.cnt; b++) {
+                        float alpha;
+                        const int sx = area_entry(tx, b, alpha);
+                        buf += WIN(sy, sx) * alpha;
+                    }
+                    acc = a == 0 ? beta * buf : acc + beta * buf;
+                }
+                P[pix] = sat_u8(acc);
             }
-            acc = a == 0 ? beta * buf : acc + beta * buf;
         }
-        P[pix] = sat_u8(acc);
     }
     __syncthreads();
-    for (int e = lane; e < 400; e += 64) {
+    for (int e = tid; e < 400; e += kDescThreads) {
         const int i = e / 20, j = e - i * 20;
         const float dw = DW[e];
         DX[e] = (P[i * 21 + j + 1] - P[i * 21 + j] + P[(i + 1) * 21 + j + 1] - P[(i + 1) * 21 + j]) * dw;
@@ -345,8 +441,8 @@ __global__ __launch_bounds__(64) void describe_kernel(const uint8_t* __restrict_
     }
     __syncthreads();
     const int per = extended ? 8 : 4, dsize = extended ? 128 : 64;
-    if (lane < 16) {
-        const int i = lane >> 2, j = lane & 3;
+    if (tid < 16) {
+        const int i = tid >> 2, j = tid & 3;
         float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int y = i * 5; y < i * 5 + 5; y++)
             for (int x = j * 5; x < j * 5 + 5; x++) {
@@ -373,17 +469,17 @@ __global__ __launch_bounds__(64) void describe_kernel(const uint8_t* __restrict_
                     v[3] += fabsf(ty);
                 }
             }
-        for (int kk = 0; kk < per; kk++) V[lane * per + kk] = v[kk];
+        for (int kk = 0; kk < per; kk++) V[tid * per + kk] = v[kk];
     }
     __syncthreads();
-    if (lane == 0) {
+    if (tid == 0) {
         double sq = 0;
         for (int kk = 0; kk < dsize; kk++) sq += V[kk] * V[kk];
         sc = (float)(1. / (sqrt(sq) + DBL_EPSILON));
     }
     __syncthreads();
     float* o = desc + (size_t)q * dsize;
-    for (int kk = lane; kk < dsize; kk += 64) o[kk] = V[kk] * sc;
+    for (int kk = tid; kk < dsize; kk += kDescThreads) o[kk] = V[kk] * sc;
 }
 
 }  // namespace
@@ -391,7 +487,7 @@ __global__ __launch_bounds__(64) void describe_kernel(const uint8_t* __restrict_
 void launch_integral(const uint8_t* img, int w, int h, int* sum, hipStream_t s) {
     if (w <= 0 || h <= 0) return;
     integral_rows_kernel<<<h, 64, 0, s>>>(img, w, h, sum);
-    integral_cols_kernel<<<(w + 1 + 255) / 256, 256, 0, s>>>(w, h, sum);
+    integral_cols_kernel<<<(w + 1 + 63) / 64, 64 * kIntBands, 0, s>>>(w, h, sum);
 }
 
 void launch_surf_hessian(const int* sum, int w, const SurfLayer* layers, int nL, long long total, float* det,
@@ -436,7 +532,7 @@ void launch_surf_keep(const fm3d_keypoint* in, int n, int w, int h, int* flag, i
 void launch_surf_describe(const uint8_t* img, size_t imgStride, int w, int h, const fm3d_keypoint* kp, int n,
                           const float* DW, int extended, float* desc, hipStream_t s) {
     if (n <= 0) return;
-    describe_kernel<<<n, 64, 0, s>>>(img, imgStride, w, h, kp, n, DW, extended, desc);
+    describe_kernel<<<n, kDescThreads, 0, s>>>(img, imgStride, w, h, kp, n, DW, extended, desc);
 }
 
 }  // namespace fm3d

@@ -483,14 +483,22 @@ private:
         if (s_.detectorType == FM3D_FEAT_SURF && s_.extractorType == FM3D_FEAT_SURF) {
             static_assert(sizeof(cv::KeyPoint) == sizeof(fm3d_keypoint), "cv::KeyPoint layout");
             fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
-            int n = 0, m = 0;
-            fm3d::compat::check(c, fm3d_surf_detect(c, img.data, img.cols, img.rows, nullptr, 0, &n, nullptr));
-            kpts.assign(n, cv::KeyPoint());
             const int dsize = s_.surfExtended ? 128 : 64;
+            // one detection with room for one keypoint per 64 pixels; again only if more were found
+            int cap = std::max(4096, img.cols * img.rows / 64), n = 0;
+            std::vector<fm3d_keypoint> k;
+            std::vector<float> f;
+            for (;;) {
+                k.resize(cap);
+                f.resize((size_t)cap * dsize);
+                fm3d::compat::check(c, fm3d_surf_detect(c, img.data, img.cols, img.rows, k.data(), cap, &n, f.data()));
+                if (n <= cap) break;
+                cap = n;
+            }
+            kpts.assign(n, cv::KeyPoint());
+            if (n > 0) std::memcpy(static_cast<void*>(kpts.data()), k.data(), (size_t)n * sizeof(fm3d_keypoint));
             d.create(n, dsize, CV_32FC1);
-            fm3d::compat::check(c, fm3d_surf_detect(c, img.data, img.cols, img.rows,
-                                                    reinterpret_cast<fm3d_keypoint*>(kpts.data()), n, &m,
-                                                    reinterpret_cast<float*>(d.data)));
+            if (n > 0) std::memcpy(d.data, f.data(), (size_t)n * dsize * sizeof(float));
             return;
         }
         if (!kpts.empty() && !d.empty()) return;
