@@ -352,7 +352,6 @@ __global__ __launch_bounds__(kDescThreads) void describe_kernel(const uint8_t* _
             for (int e = tid; e < W * 21; e += kDescThreads) {
                 const int dx = e / W, a = e - dx * W;
                 int sm = 0;
-#pragma unroll 8
                 for (int b = 0; b < iscale; b++) sm += WIN(a, dx * iscale + b);
                 HI[a * 21 + dx] = sm;
             }
@@ -379,23 +378,10 @@ __global__ __launch_bounds__(kDescThreads) void describe_kernel(const uint8_t* _
                 const int dx = e / W, a = e - dx * W;
                 const AreaTab tx = T[dx];
                 float buf = 0.f;
-                // batches of kB gathers in flight before their (ordered) accumulation
-                constexpr int kB = 8;
-                for (int b0 = 0; b0 < tx.cnt; b0 += kB) {
-                    int px[kB];
-#pragma unroll
-                    for (int u = 0; u < kB; u++) {
-                        float alpha;
-                        px[u] = b0 + u < tx.cnt ? WIN(a, area_entry(tx, b0 + u, alpha)) : 0;
-                    }
-#pragma unroll
-                    for (int u = 0; u < kB; u++) {
-                        if (b0 + u < tx.cnt) {
-                            float alpha;
-                            area_entry(tx, b0 + u, alpha);
-                            buf += px[u] * alpha;
-                        }
-                    }
+                for (int b = 0; b < tx.cnt; b++) {
+                    float alpha;
+                    const int sx = area_entry(tx, b, alpha);
+                    buf += WIN(a, sx) * alpha;
                 }
                 H[a * 21 + dx] = buf;
             }

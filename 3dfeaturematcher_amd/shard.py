@@ -2,20 +2,26 @@
 
 Every stage of the path is independent per query keypoint once frame B's
 descriptors and both image pyramids are present on a device, so one frame pair
-splits into contiguous query blocks, one per rank:
+splits into query blocks, one set per rank, each rank running the whole path on
+its device against ALL of frame B:
 
-  rank r takes queries [lo_r, hi_r) of frame A against ALL of frame B, runs the
-  whole path on its device (fm3d_pipeline_upload with queryOffset = lo_r, so
-  queryIdx stays global), and the per-rank survivor records are all-gathered
-  (count first, then fixed-capacity 64-byte records, all_gather_device) and
-  concatenated in rank order (merge_gathered).  bench.py --gpus N runs exactly
-  this on one 1M-keypoint frame pair (C5) with the record buffers on the GPUs.
+  * block-cyclic (query_blocks, what bench.py --gpus N runs on C5's 1M-keypoint
+    frame pair): blocks of BLOCK queries dealt round-robin, so every rank sees
+    the same mix of queries.  The rank uploads its queries gathered into one
+    array (queryIdx local), and the merge maps them back to global indices and
+    orders the records by query.  Contiguous blocks left C5's last rank a fifth
+    of the work of the others: the synthetic frame's last tenth are distractor
+    descriptors without a match (profiles/r02_c5_balance_contiguous.json);
+  * contiguous (partition): queries [lo_r, hi_r) with queryOffset = lo_r, so
+    queryIdx stays global and the rank-order concatenation is already in query
+    order.
 
-Rank order x query order inside a shard == query order, so the merged list is
-byte-identical to the single-GPU run.  The collective is torch.distributed's
-all_gather (RCCL over xGMI with backend "nccl", or gloo on CPU for tests); no
-other exchange is needed.  The reference has no distributed component to
-mirror: main.cpp:91-155 runs the three stages in one process.
+The per-rank survivor records are all-gathered (count first, then fixed-capacity
+64-byte records, all_gather_device) and merged (merge_gathered): either way the
+merged list is byte-identical to the single-GPU run.  The collective is
+torch.distributed's all_gather (RCCL over xGMI with backend "nccl", or gloo on
+CPU for tests); no other exchange is needed.  The reference has no distributed
+component to mirror: main.cpp:91-155 runs the three stages in one process.
 """
 from __future__ import annotations
 
@@ -25,6 +31,7 @@ from typing import Callable
 import numpy as np
 
 RECORD_BYTES = 64
+BLOCK = 4096  # queries per block of the block-cyclic partition
 
 
 def partition(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -39,6 +46,23 @@ def partition(n: int, world: int, rank: int) -> tuple[int, int]:
 def shard_capacity(n: int, world: int) -> int:
     """Records per rank buffer: the largest block's query count (>= 1)."""
     return max(1, max(hi - lo for lo, hi in (partition(n, world, r) for r in range(world))))
+
+
+def query_blocks(n: int, world: int, rank: int, block: int = BLOCK) -> np.ndarray:
+    """Global indices of `rank`'s queries under the block-cyclic partition: blocks
+    rank, rank + world, ... of `block` queries each, in increasing order."""
+    if world <= 0 or not 0 <= rank < world or block <= 0:
+        raise ValueError(f"bad rank {rank} of {world} (block {block})")
+    starts = np.arange(rank * block, n, world * block, dtype=np.int64)
+    if len(starts) == 0:
+        return np.zeros(0, dtype=np.int64)
+    idx = (starts[:, None] + np.arange(block, dtype=np.int64)[None, :]).reshape(-1)
+    return idx[idx < n]
+
+
+def blocks_capacity(n: int, world: int, block: int = BLOCK) -> int:
+    """Records per rank buffer under the block-cyclic partition (>= 1)."""
+    return max(1, max(len(query_blocks(n, world, r, block)) for r in range(world)))
 
 
 def all_gather_device(rec_buf, n_kept: int, group=None):
@@ -58,22 +82,39 @@ def all_gather_device(rec_buf, n_kept: int, group=None):
     return gathered, counts
 
 
-def merge_gathered(gathered, counts) -> np.ndarray:
-    """Rank-order concatenation of the valid records of every rank's buffer: the single-
-    device record list (rank order x query order inside a shard == query order)."""
+def merge_gathered(gathered, counts, index_maps=None, by_query: bool = False) -> np.ndarray:
+    """The valid records of every rank's buffer as the single-device record list.
+    index_maps None: queryIdx is already global and the rank-order concatenation is in
+    query order (contiguous blocks) -- unless by_query, which orders by queryIdx.
+    index_maps[r]: rank r's records carry local query indices into index_maps[r] (the
+    block-cyclic partition); they are mapped to global ones and ordered by query."""
     rec_dtype = importlib.import_module("3dfeaturematcher_amd").RECORD
     g = np.ascontiguousarray(gathered.cpu().numpy() if hasattr(gathered, "cpu") else gathered, dtype=np.uint8)
     c = np.asarray(counts.cpu().numpy() if hasattr(counts, "cpu") else counts).astype(np.int64)
     cap = g.shape[1]
     if g.ndim != 3 or g.shape[2] != RECORD_BYTES or (c < 0).any() or (c > cap).any():
         raise ValueError("gathered record buffers of an unexpected shape or count")
-    parts = [g[r, : c[r]].reshape(-1).view(rec_dtype) for r in range(g.shape[0])]
-    return np.concatenate(parts) if parts else np.zeros(0, dtype=rec_dtype)
+    if index_maps is not None and len(index_maps) != g.shape[0]:
+        raise ValueError("one index map per rank")
+    parts = []
+    for r in range(g.shape[0]):
+        rec = g[r, : c[r]].reshape(-1).view(rec_dtype).copy()
+        if index_maps is not None:
+            m = np.asarray(index_maps[r])
+            if len(rec) and (rec["queryIdx"].min() < 0 or rec["queryIdx"].max() >= len(m)):
+                raise ValueError("a local query index outside the rank's index map")
+            rec["queryIdx"] = m[rec["queryIdx"]]
+        parts.append(rec)
+    out = np.concatenate(parts) if parts else np.zeros(0, dtype=rec_dtype)
+    if index_maps is not None or by_query:
+        out = out[np.argsort(out["queryIdx"], kind="stable")]
+    return out
 
 
 def gather_records(records: np.ndarray, capacity: int, group=None, device=None) -> np.ndarray:
-    """All-gather every rank's survivor records (fm3d RECORD dtype) and merge them in
-    rank order.  `capacity` = the largest shard's query count (fixed-size buffers)."""
+    """All-gather every rank's survivor records (fm3d RECORD dtype, global queryIdx) and
+    merge them in query order.  `capacity` = the largest shard's query count (fixed-size
+    buffers)."""
     import torch
     import torch.distributed as dist
 
@@ -88,7 +129,7 @@ def gather_records(records: np.ndarray, capacity: int, group=None, device=None) 
     if device is not None:
         mine = mine.to(device)
     gathered, counts = all_gather_device(mine, n, group=group)
-    return merge_gathered(gathered, counts)
+    return merge_gathered(gathered, counts, by_query=True)
 
 
 def run_shard(pair, settings, lo: int, hi: int, device: int = 0) -> np.ndarray:
@@ -107,16 +148,36 @@ def run_shard(pair, settings, lo: int, hi: int, device: int = 0) -> np.ndarray:
         ctx.close()
 
 
+def run_shard_queries(pair, settings, idx: np.ndarray, device: int = 0) -> np.ndarray:
+    """The queries idx (global indices, increasing) through the whole path on this rank's
+    GPU, uploaded as one gathered array: records with global queryIdx."""
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    idx = np.asarray(idx, dtype=np.int64)
+    ctx = fm3d.Context(settings, device=device)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(pair.g12)
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(pair.desc1[idx], pair.desc2, pair.kp1[idx], pair.kp2, pair.img1, pair.img2, query_offset=0)
+        n, _ = pipe.run()
+        rec = pipe.records(n)
+        rec["queryIdx"] = idx[rec["queryIdx"]]
+        return rec
+    finally:
+        ctx.close()
+
+
 def run_sharded(pair, settings, group=None, device=None,
-                shard_fn: Callable[..., np.ndarray] | None = None) -> np.ndarray:
-    """One frame pair split over the ranks of `group`; every rank returns the merged
-    records (identical to a single-device run).  `shard_fn(pair, settings, lo, hi)`
-    computes one block; by default the GPU path (run_shard)."""
+                shard_fn: Callable[..., np.ndarray] | None = None, block: int = BLOCK) -> np.ndarray:
+    """One frame pair split block-cyclically over the ranks of `group`; every rank returns
+    the merged records (identical to a single-device run).  `shard_fn(pair, settings, idx)`
+    computes the queries idx with global queryIdx; by default the GPU path
+    (run_shard_queries)."""
     import torch.distributed as dist
 
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     n = len(pair.desc1)
-    lo, hi = partition(n, world, rank)
-    fn = shard_fn or (lambda p, s, a, b: run_shard(p, s, a, b, device=device.index if device is not None else 0))
-    rec = fn(pair, settings, lo, hi)
-    return gather_records(rec, shard_capacity(n, world), group=group, device=device)
+    idx = query_blocks(n, world, rank, block)
+    fn = shard_fn or (lambda p, s, q: run_shard_queries(p, s, q, device=device.index if device is not None else 0))
+    rec = fn(pair, settings, idx)
+    return gather_records(rec, blocks_capacity(n, world, block), group=group, device=device)

@@ -8,13 +8,15 @@ Workloads (BASELINE.json configs):
     refinement with pixelsRay 64 over 3+1 pyramid levels).
   * C5 (configs[4], the default at N > 1 GPUs): ONE 1M-keypoint frame pair (the C4 scene and
     settings, 1M sub-pixel keypoints per 640x480 frame), sharded over the N
-    ranks: rank r takes the contiguous query block shard.partition(1M, N, r)
-    against all of frame B (replicated), runs the whole path on its GPU, and the per-rank
-    survivor records (queryIdx, trainIdx, distance, 3D point, normal) are all-gathered over
-    RCCL (counts, then fixed-capacity record buffers) every step.  value = kept keypoints of
-    the frame pair / max-over-ranks time (strong scaling).  After the timed steps rank 0 runs
-    the same frame pair unsharded on its GPU and checks that the rank-order merge of the
-    gathered records is byte-identical to it.
+    ranks: rank r takes the query blocks shard.query_blocks(1M, N, r) (4,096
+    queries each, dealt round-robin so every rank gets the same mix: contiguous blocks left the
+    last rank the synthetic frame's distractor tail, a fifth of the others' work) against all
+    of frame B (replicated), runs the whole path on its GPU, and the per-rank survivor records
+    (queryIdx, trainIdx, distance, 3D point, normal) are all-gathered over RCCL (counts, then
+    fixed-capacity record buffers) every step.  value = kept keypoints of the frame pair /
+    max-over-ranks time (strong scaling).  After the timed steps rank 0 runs the same frame
+    pair unsharded on its GPU and checks that the merge of the gathered records (local query
+    indices mapped back, in query order) is byte-identical to it.
   * --weak: the round-1 mode, every rank its own C4 frame pair (weak scaling), labelled weak.
 
 One step = one frame pair (or one shard of it) through the path with its inputs already
@@ -115,18 +117,20 @@ def main():
     s.pyramids = args.levels
     s.lmWaves = args.lm_waves
     n = len(pair.desc1)
-    lo, hi = shard.partition(n, world, rank) if sharded else (0, n)
+    # this rank's queries (block-cyclic over the ranks), gathered into one array: local queryIdx
+    qidx = shard.query_blocks(n, world, rank) if sharded else None
     ctx = fm3d.Context(s, device=local if world > 1 else 0)
     sct = fm3d.SingleCameraTriangulator(ctx)
     sct.set_g12(pair.g12)
     pipe = fm3d.Pipeline(ctx)
+    d1, k1 = (pair.desc1, pair.kp1) if qidx is None else (pair.desc1[qidx], pair.kp1[qidx])
     t_up = time.perf_counter()
-    pipe.upload(pair.desc1[lo:hi], pair.desc2, pair.kp1[lo:hi], pair.kp2, pair.img1, pair.img2, query_offset=lo)
+    pipe.upload(d1, pair.desc2, k1, pair.kp2, pair.img1, pair.img2, query_offset=0)
     upload_ms = (time.perf_counter() - t_up) * 1e3
 
     rec_buf = None
     if dist is not None:
-        cap = shard.shard_capacity(n, world) if sharded else n
+        cap = shard.blocks_capacity(n, world) if sharded else n
         rec_buf = torch.empty((cap, shard.RECORD_BYTES), dtype=torch.uint8, device=f"cuda:{local}")
     last = {}
 
@@ -170,7 +174,8 @@ def main():
     if dist is None:
         mine = pipe.records(stats[-1]["kept"])
     else:
-        merged = shard.merge_gathered(last["gathered"], last["counts"])
+        maps = [shard.query_blocks(n, world, r) for r in range(world)] if sharded else None
+        merged = shard.merge_gathered(last["gathered"], last["counts"], index_maps=maps)
     download_ms = (time.perf_counter() - t_dl) * 1e3
 
     check = None
@@ -212,7 +217,7 @@ def main():
                 "workload": desc,
                 "keypoints_per_frame": wl["keypoints"], "width": wl["width"], "height": wl["height"],
                 "pixelsRay": args.ray, "pyramids": args.levels,
-                "parallelism": (f"dp{world}: contiguous query blocks of one frame pair, frame B replicated, "
+                "parallelism": (f"dp{world}: 4,096-query blocks of one frame pair dealt round-robin, frame B replicated, "
                                 f"RCCL all-gather of counts + 64-B survivor records each step") if sharded else
                                (f"dp{world}: one frame pair per rank (weak)" if world > 1 else "1 GPU"),
                 "timed": ("match -> NNDR -> DLT -> LM -> survivor records on HBM-resident inputs (descriptors, "
@@ -244,7 +249,7 @@ def main():
 
 def check_against_one_gpu(args, fm3d, pair, s, merged, local, rank, dist, torch):
     """Rank 0: the unsharded frame pair on its own GPU (one run, untimed by the metric), byte
-    for byte against the rank-order merge of the last step's gathered records."""
+    for byte against the merge of the last step's gathered records (query order)."""
     res = None
     if rank == 0 and not args.no_check:
         ctx = fm3d.Context(s, device=local)

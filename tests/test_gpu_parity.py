@@ -378,16 +378,21 @@ def test_pipeline_end_to_end(fm3d, orc, pair):
 
 
 def test_sharded_blocks_equal_single_run(fm3d, pair):
-    """Contiguous query blocks with queryOffset (multi-GPU partition, run here one block
-    after the other on one GPU) concatenate to the single-run records byte for byte."""
+    """Both multi-GPU partitions, run here one share after the other on one GPU: contiguous
+    query blocks with queryOffset concatenate to the single-run records byte for byte, and
+    the block-cyclic shares (gathered queries, local indices mapped back) merge to them."""
     import importlib
     shard = importlib.import_module("3dfeaturematcher_amd.shard")
     s = _settings(fm3d, pair.cam, pixelsRay=10, pyramids=2)
-    full = shard.run_shard(pair, s, 0, len(pair.desc1))
-    parts = [shard.run_shard(pair, s, *shard.partition(len(pair.desc1), 3, r)) for r in range(3)]
+    n = len(pair.desc1)
+    full = shard.run_shard(pair, s, 0, n)
+    parts = [shard.run_shard(pair, s, *shard.partition(n, 3, r)) for r in range(3)]
     merged = np.concatenate(parts)
     assert len(full) > 100
     assert merged.tobytes() == full.tobytes()
+    cyc = np.concatenate([shard.run_shard_queries(pair, s, shard.query_blocks(n, 3, r, 64)) for r in range(3)])
+    cyc = cyc[np.argsort(cyc["queryIdx"], kind="stable")]
+    assert cyc.tobytes() == full.tobytes()
 
 
 # ---------------------------------------------------------------- patch export (§8(f))
@@ -719,17 +724,18 @@ def test_c4_sift100k_full_pipeline(fm3d, orc, synth):
 @pytest.mark.timeout(900)
 def test_c5_1m_keypoints_query_blocks(fm3d, orc, synth):
     """BASELINE configs[4] (C5) on one GPU: one 1M-keypoint frame pair (640x480, sub-pixel
-    keypoints; pixelsRay 64, pyramids 3) run whole and as the 4 contiguous query
-    blocks of a 4-GPU shard (queryOffset): the merged block records are byte-identical to the
-    whole run.  A seeded 2,000-query sample goes through the oracle (match, NNDR, DLT, LM in
+    keypoints; pixelsRay 64, pyramids 3) run whole and as the 4 block-cyclic
+    shares of a 4-GPU run (bench.py --gpus 4): the merged share records are byte-identical to
+    the whole run.  A seeded 2,000-query sample goes through the oracle (match, NNDR, DLT, LM in
     DETMATH mode): the whole run's records of those queries are exactly the oracle's survivors."""
     shard = importlib.import_module("3dfeaturematcher_amd.shard")
     fp = synth.make_frame_pair(1_000_000, 640, 480, seed=7)
     s = _settings(fm3d, fp.cam, pixelsRay=64, pyramids=3)
     n = len(fp.desc1)
     full = shard.run_shard(fp, s, 0, n)
-    parts = [shard.run_shard(fp, s, *shard.partition(n, 4, r)) for r in range(4)]
+    parts = [shard.run_shard_queries(fp, s, shard.query_blocks(n, 4, r)) for r in range(4)]
     merged = np.concatenate(parts)
+    merged = merged[np.argsort(merged["queryIdx"], kind="stable")]
     assert len(full) > 200_000
     assert merged.tobytes() == full.tobytes()
     rng = np.random.default_rng(55)

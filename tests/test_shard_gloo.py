@@ -1,8 +1,8 @@
 """Multi-rank sharding of one frame pair on CPU: world size 2 with
-the gloo backend.  Each rank computes its contiguous query block with the CPU oracle
-standing in for the device (tests may call the oracle; the product's shard_fn is the
-GPU path), the records are all-gathered and merged in rank order, and the merge must
-equal the single-process result byte for byte."""
+the gloo backend.  Each rank computes its block-cyclic share of the queries with the CPU
+oracle standing in for the device (tests may call the oracle; the product's shard_fn is
+the GPU path), the records are all-gathered and merged in query order, and the merge
+must equal the single-process result byte for byte."""
 import importlib
 import os
 import socket
@@ -22,19 +22,21 @@ def _free_port():
     return port
 
 
-def oracle_records(pair, s, lo, hi):
-    """The whole path for queries [lo, hi) on the CPU oracle, as fm3d records."""
+def oracle_records(pair, s, idx):
+    """The whole path for the queries idx (global indices, increasing) on the CPU oracle,
+    as fm3d records with global queryIdx."""
     import oracle as orc
     fm3d = importlib.import_module("3dfeaturematcher_amd")
-    q, t, d = orc.match_nndr(pair.desc1[lo:hi], pair.desc2, orc.U8, s.nndrEpsilon, 2)
-    pts, mask = orc.triangulate(pair.cam, pair.g12, s.zThresholdMin, s.zThresholdMax, pair.kp1[lo:hi], pair.kp2,
+    idx = np.asarray(idx, dtype=np.int64)
+    q, t, d = orc.match_nndr(pair.desc1[idx], pair.desc2, orc.U8, s.nndrEpsilon, 2)
+    pts, mask = orc.triangulate(pair.cam, pair.g12, s.zThresholdMin, s.zThresholdMax, pair.kp1[idx], pair.kp2,
                                 q, t)
     R2, t2 = fm3d.camera2_from_g12(pair.g12)
     r = orc.optimize_normals(pair.cam, R2, t2, pair.img1, pair.img2, s.pyramids, pts, s.pixelsRay,
                              mode=orc.DETMATH, nthreads=2)
     ok = r["status"] == 0
     rec = np.zeros(int(ok.sum()), dtype=fm3d.RECORD)
-    rec["queryIdx"] = q[mask][ok] + lo
+    rec["queryIdx"] = idx[q[mask][ok]]
     rec["trainIdx"] = t[mask][ok]
     rec["distance"] = d[mask][ok]
     rec["point"] = pts[ok]
@@ -63,7 +65,8 @@ def _worker(rank, world, port, q):
         synth = importlib.import_module("3dfeaturematcher_amd.synth")
         shard = importlib.import_module("3dfeaturematcher_amd.shard")
         pair = synth.make_frame_pair(301, 160, 120, seed=4)
-        merged = shard.run_sharded(pair, _settings(pair), shard_fn=oracle_records)
+        # 32-query blocks: each rank's share interleaves with the other's
+        merged = shard.run_sharded(pair, _settings(pair), shard_fn=oracle_records, block=32)
         q.put((rank, merged.tobytes()))
     finally:
         dist.destroy_process_group()
@@ -82,9 +85,53 @@ def test_partition_covers_in_order():
         shard.partition(10, 2, 2)
 
 
+def test_query_blocks_cover_round_robin():
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    for n in (0, 1, 7, 100, 1001, 10_000):
+        for w in (1, 2, 3, 8):
+            for block in (1, 16, 4096):
+                parts = [shard.query_blocks(n, w, r, block) for r in range(w)]
+                allq = np.concatenate(parts) if parts else np.zeros(0)
+                assert np.array_equal(np.sort(allq), np.arange(n))
+                assert all((np.diff(p) > 0).all() for p in parts)
+                sizes = [len(p) for p in parts]
+                assert max(sizes) - min(sizes) <= block
+                assert shard.blocks_capacity(n, w, block) == max(1, max(sizes))
+                # block b of the frame goes to rank b mod w
+                for r, p in enumerate(parts):
+                    assert ((p // block) % w == r).all()
+    with pytest.raises(ValueError):
+        shard.query_blocks(10, 2, 2)
+
+
+def test_merge_gathered_index_maps(fm3d):
+    """Block-cyclic merge: every rank's records carry local query indices into its share;
+    the merge maps them to global ones and orders by query (what the single run lists)."""
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    rng = np.random.default_rng(1)
+    n, w, block = 50, 3, 4
+    maps = [shard.query_blocks(n, w, r, block) for r in range(w)]
+    cap = shard.blocks_capacity(n, w, block)
+    full = np.zeros(20, dtype=fm3d.RECORD)
+    full["queryIdx"] = np.sort(rng.choice(n, 20, replace=False))
+    full["point"] = rng.normal(size=(20, 3))
+    g = rng.integers(0, 256, (w, cap, shard.RECORD_BYTES), dtype=np.uint8)  # stale bytes past the counts
+    counts = []
+    for r in range(w):
+        mine = full[np.isin(full["queryIdx"], maps[r])].copy()
+        mine["queryIdx"] = np.searchsorted(maps[r], mine["queryIdx"])  # local indices
+        g[r, :len(mine)] = mine.view(np.uint8).reshape(len(mine), shard.RECORD_BYTES)
+        counts.append(len(mine))
+    merged = shard.merge_gathered(g, np.array(counts, dtype=np.int32), index_maps=maps)
+    assert merged.tobytes() == full.tobytes()
+    bad = [m[:1] for m in maps]
+    with pytest.raises(ValueError):
+        shard.merge_gathered(g, np.array(counts, dtype=np.int32), index_maps=bad)
+
+
 def test_sharded_merge_equals_single_run_gloo(synth, fm3d):
     pair = synth.make_frame_pair(301, 160, 120, seed=4)
-    full = oracle_records(pair, _settings(pair), 0, len(pair.desc1))
+    full = oracle_records(pair, _settings(pair), np.arange(len(pair.desc1)))
     assert len(full) > 10
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

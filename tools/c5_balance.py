@@ -1,9 +1,10 @@
-"""Load balance of C5's contiguous query blocks (bench.py --gpus N): the 1M-keypoint frame pair on
-ONE GPU, block by block as rank r of N would run it (fm3d_pipeline_upload with queryOffset), with
-each block's step time, LM time and survivors.  The max over blocks is what bench.py's
-max-over-ranks clock sees at N GPUs.
+"""Load balance of C5's query shares (bench.py --gpus N): the 1M-keypoint frame pair on ONE GPU,
+share by share as rank r of N would run it, with each share's step time, LM time and survivors.
+The max over shares is what bench.py's max-over-ranks clock sees at N GPUs.  --contiguous: the
+contiguous blocks of shard.partition (queryOffset); default: the block-cyclic shares of
+shard.query_blocks that bench.py runs.
 
-    python tools/c5_balance.py [--ranks 2 4 8] [--out gpurun_out/c5_balance.json]
+    python tools/c5_balance.py [--ranks 2 4 8] [--contiguous] [--out gpurun_out/c5_balance.json]
 """
 import argparse
 import importlib
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--keypoints", type=int, default=1_000_000)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--contiguous", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     fm3d = importlib.import_module("3dfeaturematcher_amd")
@@ -37,15 +39,23 @@ def main():
     sct = fm3d.SingleCameraTriangulator(ctx)
     sct.set_g12(pair.g12)
     pipe = fm3d.Pipeline(ctx)
-    out = {"keypoints": a.keypoints, "blocks": {}}
+    out = {"keypoints": a.keypoints, "partition": "contiguous" if a.contiguous else f"block-cyclic ({shard.BLOCK})",
+           "blocks": {}}
     n = len(pair.desc1)
     for N in a.ranks:
         rows = []
         for r in range(N):
-            lo, hi = shard.partition(n, N, r)
-            pipe.upload(pair.desc1[lo:hi], pair.desc2, pair.kp1[lo:hi], pair.kp2, pair.img1, pair.img2, query_offset=lo)
+            if a.contiguous:
+                lo, hi = shard.partition(n, N, r)
+                pipe.upload(pair.desc1[lo:hi], pair.desc2, pair.kp1[lo:hi], pair.kp2, pair.img1, pair.img2,
+                            query_offset=lo)
+                nq = hi - lo
+            else:
+                q = shard.query_blocks(n, N, r)
+                pipe.upload(pair.desc1[q], pair.desc2, pair.kp1[q], pair.kp2, pair.img1, pair.img2, query_offset=0)
+                nq = len(q)
             k, st = pipe.run()
-            rows.append({"rank": r, "queries": hi - lo, "inliers": st["inliers"], "kept": k,
+            rows.append({"rank": r, "queries": nq, "inliers": st["inliers"], "kept": k,
                          "total_ms": st["total_ms"], "lm_ms": st["lm_ms"], "match_ms": st["match_ms"]})
             print(json.dumps({"N": N, **rows[-1]}), flush=True)
         tmax = max(x["total_ms"] for x in rows)
