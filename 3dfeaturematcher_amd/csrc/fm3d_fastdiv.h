@@ -30,6 +30,13 @@ __device__ __forceinline__ double mdiv(double a, double d, double y, bool mok) {
     }
     return q;
 }
+// the same sequence without the guard: for callers that have bounded |a| < 1e100 and checked
+// mdiv_ok(d) for the whole pass
+__device__ __forceinline__ double mdiv_fast(double a, double d, double y) {
+    const double q0 = a * y;
+    const double r = __builtin_fma(-d, q0, a);
+    return __builtin_fma(r, y, q0);
+}
 __device__ __forceinline__ bool mdiv_ok(double d) { return fabs(d) > 1e-200 && fabs(d) < 1e200; }
 
 // z ? 1/z : 1 (cvProjectPoints2).  For 2^-700 <= |z| <= 2^700 the hardware sequence

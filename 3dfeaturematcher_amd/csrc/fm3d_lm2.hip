@@ -430,7 +430,7 @@ struct Shared {
     // chunk terms [slot][ring position][sum][entry]; entry kE holds the chunk's slow flag for
     // that sum (nonzero: raw values for MINPACK's full enorm instead of squares)
     double ring[kW][kR][2][kRow];
-    int rowTag[kW][kR];            // chunk index whose terms a ring position holds (published last)
+    int rowTag[kW][kR];            // (chunk index << 2) | slow flags of the terms a ring position holds (published last)
     int consumed[kW][2];           // chunks consumed, per chain lane (monotonic)
     int resultId[kW][2];           // id of the last pass whose result is published
     double result[kW][2];
@@ -444,6 +444,11 @@ struct Shared {
     int helpDone[kW];              // id of the last announced pass whose helper share is complete
     int hfail[kW][2], hph3[kW][2]; // the helper share's failures (as fail0/fail1, ph30/ph31 != 0)
     int hAtt[kW], hSeen[kW], hAnn[kW];  // per wave (lane 0): attached slot, passes taken, passes announced
+    // per-wave statistics, kept in LDS (lane 0) so that they hold no scalar registers across
+    // the pass loops: class passes / cycles, terms / control cycles, producer waits, passes
+    struct WaveStat {
+        unsigned long long cnt[4], cyc[4], terms, ctl, wait, nPass, iter, t0;
+    } ws[kW];
     PassDesc pd[kW];
     SlotP2 sp[kW];
     SlotS2 ss[kW];
@@ -465,12 +470,10 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
 
 // sum += row[0..64) in index order: 64 dependent adds, fed by ds_read_b128 into four
 // register sets of 8 values in rotation, so three sets (24 values) are in flight while one is
-// added.  Compiler barriers keep the reads in that order.  slow: the row's slow flag (entry
-// kE), read with the data and tested by the caller after the sum.
-__device__ __forceinline__ double chain_sum64(double sum, const double* row, double& slow) {
+// added.  Compiler barriers keep the reads in that order.
+__device__ __forceinline__ double chain_sum64(double sum, const double* row) {
 #if FM3D_ABL_CHAIN
     // ablation (timing experiments only, wrong sums): one add per chunk
-    slow = 0.;
     return sum + row[0];
 #endif
     const double2* R = reinterpret_cast<const double2*>(row);
@@ -493,7 +496,6 @@ __device__ __forceinline__ double chain_sum64(double sum, const double* row, dou
     ld(v0, 0);
     ld(v1, 1);
     ld(v2, 2);
-    slow = row[kE];
     ld(v3, 3);
     add(v0);
     ld(v0, 4);
@@ -511,6 +513,9 @@ __device__ __forceinline__ double chain_sum64(double sum, const double* row, dou
 }
 
 __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned long long rfl_u64(unsigned long long v) {
+    return ((unsigned long long)(unsigned)rfl((int)(v >> 32)) << 32) | (unsigned)rfl((int)v);
+}
 __device__ __forceinline__ const uint8_t* rfl_ptr(const uint8_t* q) {
     const unsigned long long v = (unsigned long long)q;
     return (const uint8_t*)(((unsigned long long)(unsigned)rfl((int)(v >> 32)) << 32) | (unsigned)rfl((int)v));
@@ -521,16 +526,16 @@ __device__ __forceinline__ const uint8_t* rfl_ptr(const uint8_t* q) {
 // space, writes the two term rows and their slow flags, then releases the position's tag.
 struct Producer {
     Shared* sh;
-    int w, lane;
+    int w, lane, me;  // me: the producing wave (w: the slot it publishes for)
     int cmin;  // chunks both chain lanes had consumed at the last read of their counters
-    long long waitCycles;
     unsigned long long deadline;  // wall clock: the watchdog ends a wait that a broken chain never releases
 
-    __device__ __forceinline__ void put(int c, double t0, double t1, int slowBits) {
-        // c and cmin are wave-uniform: kept in SGPRs (readfirstlane on every LDS read)
+    // Waits for ring space for chunk c (both chain lanes have consumed chunk c - kR).  Called
+    // before the chunk's terms are computed, so that the term code is one basic block.  The
+    // counters are read only when the space seen last time is used up, the clock only when
+    // still full.  c and cmin are wave-uniform (SGPRs; readfirstlane on every LDS read).
+    __device__ __forceinline__ void reserve(int c) {
         if (c >= cmin + kR) {
-            // ring space: both chain lanes have consumed chunk c - kR.  The counters are read
-            // only when the space seen last time is used up, the clock only when still full.
             cmin = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])));
             if (c >= cmin + kR) {
                 const long long c0 = clock64();
@@ -538,20 +543,30 @@ struct Producer {
                     __builtin_amdgcn_s_sleep(1);
                     cmin = rfl(min(lds_load_acq(&sh->consumed[w][0]), lds_load_acq(&sh->consumed[w][1])));
                 } while (c >= cmin + kR && wall_clock64() < deadline);
-                waitCycles += clock64() - c0;
+                const unsigned long long dt = clock64() - c0;
+                if (lane == 0) sh->ws[me].wait += dt;
             }
         }
+    }
+    // Publishes chunk c (reserved) into ring position c % kR: the term rows, then the tag.
+    // TWO: the pass has a second sum (otherwise the second row is not written: its chain lane
+    // sums whatever the row holds and publishes nothing).
+    template <bool TWO = true>
+    __device__ __forceinline__ void write(int c, double t0, double t1, int slowBits) {
         const int pos = c & (kR - 1);
         double* row0 = &sh->ring[w][pos][0][0];
         row0[lane] = t0;
-        row0[kRow + lane] = t1;
-        // the flags and the tag are written by every lane (same address, same value): no
-        // lane-0 branch, so c stays a scalar
-        row0[kE] = (slowBits & 1) ? 1. : 0.;
-        row0[kRow + kE] = (slowBits & 2) ? 1. : 0.;
-        // every lane's ring stores are done before the tag is published (lgkmcnt is per wave)
+        if (TWO) row0[kRow + lane] = t1;
+        // every lane's ring stores are done before the tag is published (lgkmcnt is per wave).
+        // The tag carries the chunk index and the two sums' slow flags (bit k: sum k holds raw
+        // values); it is written by every lane (same address, same value): no lane-0 branch
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        lds_store_rel(&sh->rowTag[w][pos], c);
+        lds_store_rel(&sh->rowTag[w][pos], (c << 2) | slowBits);
+    }
+    template <bool TWO = true>
+    __device__ __forceinline__ void put(int c, double t0, double t1, int slowBits) {
+        reserve(c);
+        write<TWO>(c, t0, t1, slowBits);
     }
 };
 
@@ -577,40 +592,72 @@ __device__ __forceinline__ const cProjConst* proj_consts(const ProjConst* p) {
 //    used when good, so the r6 NaN propagation of project1 is not needed: an infinite or
 //    NaN r6 makes u or v infinite or NaN either way;
 //  * off: byte offset of the bilinear window in image 2 (0 when not good).
+// Lane masks: every test below is the ballot of one compare (the compare's own SGPR result; the
+// term code runs with all 64 lanes active), combined with scalar ANDs.  A ballot of a combined
+// bool would cost two extra VALU instructions (v_cndmask + v_cmp) per ballot.
+typedef unsigned long long LaneMask;
+// v where the lane's bit of m is set, else +0 (v_cndmask with the mask as its selector)
+__device__ __forceinline__ double sel_mask(double v, LaneMask m) {
+    unsigned lo = __double2loint(v), hi = __double2hiint(v);
+    asm("v_cndmask_b32_e64 %0, 0, %0, %1" : "+v"(lo) : "s"(m));
+    asm("v_cndmask_b32_e64 %0, 0, %0, %1" : "+v"(hi) : "s"(m));
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ unsigned sel_mask_u32(unsigned v, LaneMask m) {
+    asm("v_cndmask_b32_e64 %0, 0, %0, %1" : "+v"(v) : "s"(m));
+    return v;
+}
+// lanes whose entry k*64 + lane lies below len (scalar arithmetic only)
+__device__ __forceinline__ LaneMask in_mask(int k, int len) {
+    const int rem = len - k * kE;
+    return rem >= kE ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1));
+}
+
 struct Geo2 {
     float fx, fy;
     unsigned off;
-    bool inbox, good;
+    LaneMask inbox, good;  // lane masks
 };
+// MMOK: div_nn_ok(mm) holds (pass-uniform), so the ray-plane quotient takes the fast sequence.
+// xmaxb / ymaxb: the bit patterns of the level bounds xmax, ymax (> 0).  u >= 0 && u <= xmax is
+// bits(u) <= bits(xmax) as unsigned integers, because u is never -0 (u = xd*fx + cx with cx > 0,
+// host-checked): negative values and NaNs have the sign or exponent bits that put them above.
+// a2 = r2 + 2*x*x and a3 = r2 + 2*y*y are single FMAs: 2*RN(x*x) == RN(2x*x) (a power-of-two
+// scaling) wherever x*x is normal, so fma(xx, 2, r2) rounds the same exact sum; where x*x is
+// subnormal, |x|, |y| < 1e-150 and u, v round to cx, cy either way.
+template <bool MMOK>
 __device__ __forceinline__ Geo2 geometry2(const LMParams& p, double ux, double uy, double n0, double n1, double n2,
-                                          double mm, bool mmok, double scale, double xmax, double ymax, int lw,
-                                          double cm) {
+                                          double mm, double scale, unsigned long long xmaxb,
+                                          unsigned long long ymaxb, int lw, double cm) {
     const cProjConst* pc = proj_consts(p.proj);
     Geo2 r;
     const double nn = n0 * ux + n1 * uy + n2 * 1.;
-    const double kk = div_nn(mm, nn, mmok);
+    const double kk = MMOK ? div_nn(mm, nn, true) : mm / nn;
     const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-    r.inbox = fabs(P0) < cm && fabs(P1) < cm && P2 > 0. && P2 < cm;
+    r.inbox = __ballot(fabs(P0) < cm) & __ballot(fabs(P1) < cm) & __ballot(P2 > 0.) & __ballot(P2 < cm);
     double x = pc->R[0] * P0 + pc->R[1] * P1 + pc->R[2] * P2 + pc->t[0];
     double y = pc->R[3] * P0 + pc->R[4] * P1 + pc->R[5] * P2 + pc->t[1];
     const double z = recip_z_lo(pc->R[6] * P0 + pc->R[7] * P1 + pc->R[8] * P2 + pc->t[2]);
     x *= z;
     y *= z;
-    const double r2 = x * x + y * y;
+    const double xx = x * x, yy = y * y;
+    const double r2 = xx + yy;
     const double r4 = r2 * r2;
     const double r6 = r4 * r2;
-    const double a1 = 2 * x * y;
-    const double a2 = r2 + 2 * x * x;
-    const double a3 = r2 + 2 * y * y;
+    const double a1 = (x + x) * y;
+    const double a2 = __builtin_fma(xx, 2., r2);
+    const double a3 = __builtin_fma(yy, 2., r2);
     const double cdist = 1 + pc->cam.k[0] * r2 + pc->cam.k[1] * r4 + pc->cam.k[4] * r6;
     const double xd = x * cdist + pc->cam.k[2] * a1 + pc->cam.k[3] * a2;
     const double yd = y * cdist + pc->cam.k[2] * a3 + pc->cam.k[3] * a1;
     const double u = xd * pc->cam.fx + pc->cam.cx;
     const double v = yd * pc->cam.fy + pc->cam.cy;
-    r.good = r.inbox && u >= 0 && u <= xmax && v >= 0 && v <= ymax;
+    r.good = r.inbox & __ballot((unsigned long long)__double_as_longlong(u) <= xmaxb) &
+             __ballot((unsigned long long)__double_as_longlong(v) <= ymaxb);
     r.fx = (float)(scale * u);
     r.fy = (float)(scale * v);
-    r.off = r.good ? (unsigned)((int)floorf(r.fy) * lw + (int)floorf(r.fx)) : 0u;
+    const unsigned o = __umul24((unsigned)(int)floorf(r.fy), (unsigned)lw) + (unsigned)(int)floorf(r.fx);
+    r.off = sel_mask_u32(o, r.good);
     return r;
 }
 
@@ -639,7 +686,7 @@ __device__ __forceinline__ float bilinear_w(unsigned lo, unsigned hi, float x, f
 // any lane of the wave does (a wave-uniform ballot of the lane tests).
 __device__ __forceinline__ double enorm_term2(double x, double agiant, bool& slow) {
     const double xa = fabs(x);
-    slow = __ballot(!(xa < agiant) || (xa <= 3.834e-20 && xa != 0.)) != 0;
+    slow = (__ballot(!(xa < agiant)) | (__ballot(xa <= 3.834e-20) & __ballot(xa != 0.))) != 0;
     return x * x;
 }
 
@@ -679,7 +726,8 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
     for (;;) {
         if ((long long)(wall_clock64() - tStart) > maxTicks) break;
         if (!__any(alive)) break;
-        const bool have = alive && lds_load_acq(&g_sh.rowTag[ss_][cur & (kR - 1)]) == cur;
+        const int tag0 = alive ? lds_load_acq(&g_sh.rowTag[ss_][cur & (kR - 1)]) : -1;
+        const bool have = (tag0 >> 2) == cur;
         if (have && !inPass) {
             const PassDesc& d = g_sh.pd[ss_];
             rem = d.nChunks;
@@ -698,19 +746,19 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
             wasBusy = true;
             // up to two chunks per lane per round, never past the pass's last chunk; every
             // lane runs the same add chain (S_NONE lanes sum zeros they never publish)
-            const int nb =
-                have ? ((rem >= 2 && lds_load_acq(&g_sh.rowTag[ss_][(cur + 1) & (kR - 1)]) == cur + 1) ? 2 : 1) : 0;
+            const int tag1 = (have && rem >= 2) ? lds_load_acq(&g_sh.rowTag[ss_][(cur + 1) & (kR - 1)]) : -1;
+            const int nb = have ? (((tag1 >> 2) == cur + 1) ? 2 : 1) : 0;
             rounds++;
             chunks += nb;
 #pragma nounroll
             for (int b = 0; b < 2; b++) {
                 if (b < nb) {
                     const double* row = &g_sh.ring[ss_][cur & (kR - 1)][which][0];
-                    double slow;
+                    const bool slow = (((b ? tag1 : tag0) >> which) & 1) != 0;
                     const double acc0 = acc;
-                    acc = chain_sum64(acc, row, slow);
+                    acc = chain_sum64(acc, row);
                     // a chunk of raw values (rare): again, with MINPACK's full enorm
-                    if (kind == S_ENORM && slow != 0.) acc = chain_slow(lane, acc0, row);
+                    if (kind == S_ENORM && slow) acc = chain_slow(lane, acc0, row);
                     cur++;
                     rem--;
                 }
@@ -763,29 +811,33 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
         const int w = rfl(wave);
         const long gslot = (long)blockIdx.x * kW + w;
         Ctl2& ctl = sh.ctl[w];
-        const Slab sl = slab_of(p, gslot);
+
         // the summed passes address the slabs as grid-uniform array bases (ProjConst, scalar
         // loads) + one 32-bit byte offset per entry (global_load ... vOffset, sBase)
         if (lane == 0) {
             ctl.p = &sh.P;
-            ctl.sl = sl;
+            ctl.sl = slab_of(p, gslot);
             ctl.eps = sqrt(p.epsfcn > DBL_EPSILON ? p.epsfcn : DBL_EPSILON);
             ctl.cnt_eval = 0;
             ctl.cnt_pix = 0;
         }
         PassOut2& OUT = sh.out[w];
-        Producer prod{&sh, w, lane, 0, 0, tStart + (unsigned long long)p.maxTicks};  // publishes into slot prod.w's ring
+        Producer prod{&sh, w, lane, w, 0, tStart + (unsigned long long)p.maxTicks};  // publishes into slot prod.w's ring
         int chunkSeq = 0;  // chunks of this slot published so far (all passes)
         // sh.hAtt[w] != -2: no points left for slot w; the wave helps slot prod.w
         const double cm = (double)p.cmax;
         const gi64* __restrict__ offsets = (const gi64*)p.offsets;
         const unsigned long long ltMask = (1ull << lane) - 1;
         int passId = 0;
-        long long nPass = 0, iterations = 0;
-        unsigned long long cyCtl = 0, cyTerms = 0, clsCnt[4] = {0, 0, 0, 0}, clsCyc[4] = {0, 0, 0, 0};
-        if (lane == 0) ctl.fetch(sh.ss[w], sh.sp[w]);
+        Shared::WaveStat& WS = sh.ws[w];
+        if (lane == 0) {
+            for (int k = 0; k < 4; k++) WS.cnt[k] = WS.cyc[k] = 0;
+            WS.terms = WS.ctl = WS.wait = WS.nPass = WS.iter = 0;
+            ctl.fetch(sh.ss[w], sh.sp[w]);
+        }
         for (;;) {
-            if (++iterations > p.maxIter || (long long)(wall_clock64() - tStart) > p.maxTicks) {
+            if ((long long)rfl_u64(lane == 0 ? ++WS.iter : 0) > p.maxIter ||
+                (long long)(wall_clock64() - tStart) > p.maxTicks) {
                 if (lane == 0) atomicExch(p.overflow, 1);  // cannot happen for a correct state machine
                 break;
             }
@@ -848,13 +900,16 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 }
                 continue;
             }
-            const unsigned long long tp0 = clock64();
+            if (lane == 0) WS.t0 = clock64();
             const int len = rfl(SP.len);
             const int nCh = (len + kE - 1) / kE;
             int cls = 3;
             if (pass == Q_INIT) {
                 // ---- extractPixelsContour(Vec2d) (:341-374): keep 0 <= p < (boundW, boundH) in
                 // offset order -> compact entries; undistorted rays (get3dPointsFromImage1Pixels :542)
+                // (the slab views are re-read from LDS here: held across the loop they would take
+                // 14 scalar registers)
+                const Slab sl2 = ctl.sl;
                 const double ccx = SP.ccx, ccy = SP.ccy;
                 int base = 0;
                 for (int k = 0; k < nCh; k++) {
@@ -867,15 +922,16 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         const int pos = base + __popcll(bm & ltMask);
                         double ux, uy;
                         undistort1(p.cam, px, py, ux, uy);
-                        sl.RX[pos] = ux;
-                        sl.RY[pos] = uy;
-                        sl.KI[pos] = e;
+                        sl2.RX[pos] = ux;
+                        sl2.RY[pos] = uy;
+                        sl2.KI[pos] = e;
                     }
                     base += __popcll(bm);
                 }
                 if (lane == 0) OUT.cnt = base;
             } else if (pass == Q_LEVEL) {
                 // ---- updateImage1PixelsIntensity (:576-589)
+                const Slab sl2 = ctl.sl;
                 const double ccx = SP.ccx, ccy = SP.ccy, scale = SP.scale, xmax = SP.xmax, ymax = SP.ymax;
                 const gu8* img1 = (const gu8*)SP.img1;
                 const int lw = rfl(SP.lw);
@@ -883,14 +939,14 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 for (int k = 0; k < nCh; k++) {
                     const int e = k * kE + lane;
                     if (e < len) {
-                        const long long o2 = offsets[sl.KI[e]];
+                        const long long o2 = offsets[sl2.KI[e]];
                         const double px = ccx + (double)(int)o2, py = ccy + (double)(int)(o2 >> 32);
                         if (!pixel_good_b(px, py, xmax, ymax)) {
                             bad = true;
                         } else {
                             const float fx = (float)(scale * px), fy = (float)(scale * py);
                             const gu8* g = img1 + (long)(int)floorf(fy) * lw + (int)floorf(fx);
-                            sl.I1[e] = bilinear4(g[0], g[1], g[lw], g[lw + 1], fx, fy);
+                            sl2.I1[e] = bilinear4(g[0], g[1], g[lw], g[lw + 1], fx, fy);
                         }
                     }
                 }
@@ -903,12 +959,15 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 int cbase = hBase, k0 = 1, kS = 2;
                 if (own) {
                     passId++;
-                    nPass++;
+                    if (lane == 0) WS.nPass++;
                     cbase = chunkSeq;
                     chunkSeq = cbase + nCh;
                     k0 = 0;
                     kS = (p.coop && rfl(lds_load_acq(&sh.helper[w])) != 0) ? 2 : 1;  // 2: split
                 }
+                cbase = rfl(cbase);
+                k0 = rfl(k0);
+                kS = rfl(kS);
                 const unsigned s8 = (unsigned)(((size_t)blockIdx.x * kW + tw) * p.nOffPad * 8);  // slot tw's, < 2^32 (host-checked)
                 const int ekind = rfl(SP.ekind);
                 const int nev = rfl(SP.nev);
@@ -929,7 +988,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     }
                 }
                 int fail0 = 0x7fffffff, fail1 = 0x7fffffff;
-                unsigned long long ph30 = 0, ph31 = 0;  // image-2 failures seen (lane masks)
+                int ph30 = 0, ph31 = 0;  // image-2 failures seen (wave-uniform flags)
                 double aqs1 = 0.;
                 if (pass == Q_EVAL) {
                     const double n00 = SP.n0[0], n10 = SP.n1[0], n20 = SP.n2[0], mm0 = SP.mm[0], w0 = SP.w[0];
@@ -937,21 +996,37 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     const double h0 = SP.hj[0], h1 = SP.hj[1], wF = SP.wF;
                     const double y0 = 1. / h0, y1 = 1. / h1;
                     const bool mok0 = mdiv_ok(h0), mok1 = mdiv_ok(h1);
-                    const double scale = SP.scale, xmax = SP.xmax, ymax = SP.ymax;
+                    const double scale = SP.scale;
+                    const unsigned long long xmaxb = (unsigned long long)__double_as_longlong(SP.xmax);
+                    const unsigned long long ymaxb = (unsigned long long)__double_as_longlong(SP.ymax);
                     const uint8_t* img2 = SP.img2;
                     const int lw = rfl(SP.lw);
                     const bool i1ok = rfl(SS.i1ok) != 0;
+                    const gu8* img2b = (const gu8*)rfl_ptr(img2);
+                    // The fast form (FAST): the ray-plane quotients take div_nn's fast sequence
+                    // (div_nn_ok of the pass's numerators) and the JAC divisions by h_j have no
+                    // per-lane guard.  The latter holds because the divided numerators of good
+                    // pixels, w_j*dI_j - wF*dI_F, combine samples in [0, 255] (|dI| < 256) with the
+                    // pass-uniform weights; other lanes are zeroed after the division.
+                    const bool fast = div_nn_ok(mm0) && (nev < 2 || div_nn_ok(mm1)) &&
+                                      (!jac || (mok0 && 256. * 1.01 * (w0 + wF) < 1e99 &&
+                                                (nev < 2 || (mok1 && 256. * 1.01 * (w1 + wF) < 1e99))));
                     // NEV evaluations per entry (2: both forward-difference columns); JAC: the
                     // values are Jacobian columns (r - fvec)/h_j, else the residual fvec itself
-                    const bool mmok0 = div_nn_ok(mm0);
-                    const bool mmok1 = div_nn_ok(mm1);
-                    const gu8* img2b = (const gu8*)rfl_ptr(img2);
-                    auto run = [&](auto nevc, auto jacc) {
+                    auto run = [&](auto nevc, auto jacc, auto fastc) {
                         constexpr int NEV = decltype(nevc)::value;
                         constexpr bool JAC = decltype(jacc)::value;
+                        constexpr bool FAST = decltype(fastc)::value;
                         struct Ld {
                             double ux, uy, dF;
                             float i1;
+                        };
+                        auto geo = [&](double ux, double uy, double n0, double n1, double n2, double mm) {
+                            return FAST ? geometry2<true>(p, ux, uy, n0, n1, n2, mm, scale, xmaxb, ymaxb, lw, cm)
+                                        : geometry2<false>(p, ux, uy, n0, n1, n2, mm, scale, xmaxb, ymaxb, lw, cm);
+                        };
+                        auto jdiv = [&](double a, double h, double y, bool mok) {
+                            return FAST ? mdiv_fast(a, h, y) : mdiv(a, h, y, mok);
                         };
                         // o8 / o4: byte offsets of the chunk's entries in the 8- / 4-byte slab arrays.
                         // Entries past len (up to three chunks past the pass) read slab padding.  The
@@ -970,39 +1045,39 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             return make_uint2(*(const gu16u*)(img2b + off), *(const gu16u*)(img2b + (off + lw)));
                         };
                         auto chunk = [&](const Ld& L, int k, unsigned o4) {
-                            const bool in = k * kE + lane < len;
-                            const Geo2 g0 = geometry2(p, L.ux, L.uy, n00, n10, n20, mm0, mmok0, scale, xmax, ymax, lw, cm);
+                            prod.reserve(cbase + k);
+                            const LaneMask in = in_mask(k, len), ok = i1ok ? in : 0ull;
+                            const Geo2 g0 = geo(L.ux, L.uy, n00, n10, n20, mm0);
                             Geo2 g1;
-                            if (NEV == 2)
-                                g1 = geometry2(p, L.ux, L.uy, n01, n11, n21, mm1, mmok1, scale, xmax, ymax, lw, cm);
+                            if (NEV == 2) g1 = geo(L.ux, L.uy, n01, n11, n21, mm1);
                             // gathers for every lane: a failed entry reads the image's first bytes
                             const uint2 a = gather(g0.off);
                             uint2 c;
                             if (NEV == 2) c = gather(g1.off);
                             // failures: first NaN-plane / bounding-box pixel in index order; image-2 flags
                             {
-                                const unsigned long long b0 = __ballot(in && !g0.inbox);
+                                const LaneMask b0 = in & ~g0.inbox;
                                 if (b0 && fail0 == 0x7fffffff) {
                                     const int l = __ffsll((long long)b0) - 1;
                                     const int cd = plane_code(L.ux, L.uy, n00, n10, n20, mm0);
                                     fail0 = (k * kE + l) * 4 + __shfl(cd, l);
                                 }
-                                ph30 |= __ballot(in && g0.inbox && !g0.good);
+                                ph30 |= (in & g0.inbox & ~g0.good) != 0;
                                 if (NEV == 2) {
-                                    const unsigned long long b1 = __ballot(in && !g1.inbox);
+                                    const LaneMask b1 = in & ~g1.inbox;
                                     if (b1 && fail1 == 0x7fffffff) {
                                         const int l = __ffsll((long long)b1) - 1;
                                         const int cd = plane_code(L.ux, L.uy, n01, n11, n21, mm1);
                                         fail1 = (k * kE + l) * 4 + __shfl(cd, l);
                                     }
-                                    ph31 |= __ballot(in && g1.inbox && !g1.good);
+                                    ph31 |= (in & g1.inbox & ~g1.good) != 0;
                                 }
                             }
                             // evaluateNormal :145-148 (fvec), fdjac2 forward differences (JAC)
                             const float dI0 = L.i1 - bilinear_w(a.x, a.y, g0.fx, g0.fy);
                             const double r0 = w0 * (double)dI0;
-                            double v0 = JAC ? mdiv(r0 - wF * L.dF, h0, y0, mok0) : r0;
-                            v0 = (in && i1ok && g0.good) ? v0 : 0.;
+                            double v0 = JAC ? jdiv(r0 - wF * L.dF, h0, y0, mok0) : r0;
+                            v0 = sel_mask(v0, ok & g0.good);
                             {
                                 const cProjConst* pc = proj_consts(p.proj);
                                 *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + o4) = dI0;
@@ -1013,12 +1088,12 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             if (NEV == 2) {
                                 const float dI1 = L.i1 - bilinear_w(c.x, c.y, g1.fx, g1.fy);
                                 const double r1 = w1 * (double)dI1;
-                                v1 = mdiv(r1 - wF * L.dF, h1, y1, mok1);
-                                v1 = (in && i1ok && g1.good) ? v1 : 0.;
+                                v1 = jdiv(r1 - wF * L.dF, h1, y1, mok1);
+                                v1 = sel_mask(v1, ok & g1.good);
                                 *(gfloat*)(proj_consts(p.proj)->slabDJ1 + o4) = dI1;
                                 t1 = enorm_term2(v1, agiant, slow1);
                             }
-                            prod.put(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
+                            prod.write<NEV == 2>(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
                         };
                         // this wave's chunks: k0, k0 + kS, ...; st8 / st4: the offset step between them
                         unsigned o8 = s8 + lane * 8u + (unsigned)k0 * 512u, o4 = o8 >> 1;
@@ -1047,17 +1122,18 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             for (int k = k0; k < nCh; k += 2 * kS) {
                                 const int kB = k + kS;
                                 const bool two = kB < nCh;  // wave-uniform
-                                const bool inA = k * kE + lane < len, inB = kB * kE + lane < len;
-                                const Geo2 gA = geometry2(p, A.ux, A.uy, n00, n10, n20, mm0, mmok0, scale, xmax, ymax, lw, cm);
+                                prod.reserve(cbase + (two ? kB : k));  // space for both chunks
+                                const LaneMask inA = in_mask(k, len), inB = in_mask(kB, len);
+                                const Geo2 gA = geo(A.ux, A.uy, n00, n10, n20, mm0);
                                 // past the last chunk B holds slab padding: its entries are not
                                 // `in`, its gathers read the image's first bytes, nothing is stored
-                                const Geo2 gB = geometry2(p, B.ux, B.uy, n00, n10, n20, mm0, mmok0, scale, xmax, ymax, lw, cm);
+                                const Geo2 gB = geo(B.ux, B.uy, n00, n10, n20, mm0);
                                 const uint2 a = gather(gA.off), b = gather(gB.off);
                                 const float i1A = A.i1, i1B = B.i1;
                                 const double dFA = A.dF, dFB = B.dF;
                                 // failures in entry order: chunk k before chunk k + 1
-                                const unsigned long long bA = __ballot(inA && !gA.inbox);
-                                const unsigned long long bB = __ballot(inB && !gB.inbox);
+                                const LaneMask bA = inA & ~gA.inbox;
+                                const LaneMask bB = inB & ~gB.inbox;
                                 if ((bA | bB) && fail0 == 0x7fffffff) {
                                     const bool first = bA != 0;
                                     const int l = __ffsll((long long)(first ? bA : bB)) - 1;
@@ -1065,21 +1141,21 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                                          : plane_code(B.ux, B.uy, n00, n10, n20, mm0);
                                     fail0 = ((first ? k : kB) * kE + l) * 4 + __shfl(cd, l);
                                 }
-                                ph30 |= __ballot(inA && gA.inbox && !gA.good) | __ballot(inB && gB.inbox && !gB.good);
+                                ph30 |= ((inA & gA.inbox & ~gA.good) | (inB & gB.inbox & ~gB.good)) != 0;
                                 A = load(o8 + 2 * st8, o4 + 2 * st4);
                                 B = load(o8 + 3 * st8, o4 + 3 * st4);
-                                auto back1 = [&](const Geo2& g, uint2 w, float i1, double dF, bool in, unsigned oo, int kk) {
+                                auto back1 = [&](const Geo2& g, uint2 w, float i1, double dF, LaneMask in, unsigned oo, int kk) {
                                     const float dI = i1 - bilinear_w(w.x, w.y, g.fx, g.fy);
                                     const double r = w0 * (double)dI;
-                                    double v = JAC ? mdiv(r - wF * dF, h0, y0, mok0) : r;
-                                    v = (in && i1ok && g.good) ? v : 0.;
+                                    double v = JAC ? jdiv(r - wF * dF, h0, y0, mok0) : r;
+                                    v = sel_mask(v, (i1ok ? in : 0ull) & g.good);
                                     {
                                         const cProjConst* pc = proj_consts(p.proj);
                                         *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + oo) = dI;
                                     }
                                     bool slow;
                                     const double t = enorm_term2(v, agiant, slow);
-                                    prod.put(cbase + kk, slow ? v : t, 0., slow ? 1 : 0);
+                                    prod.write<false>(cbase + kk, slow ? v : t, 0., slow ? 1 : 0);
                                 };
                                 back1(gA, a, i1A, dFA, inA, o4, k);
                                 if (two) back1(gB, b, i1B, dFB, inB, o4 + st4, kB);
@@ -1088,12 +1164,25 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             }
                         }
                     };
-                    if (nev == 2)
-                        run(std::integral_constant<int, 2>(), std::true_type());
-                    else if (jac)
-                        run(std::integral_constant<int, 1>(), std::true_type());
-                    else
-                        run(std::integral_constant<int, 1>(), std::false_type());
+                    using I1 = std::integral_constant<int, 1>;
+                    using I2 = std::integral_constant<int, 2>;
+                    using T = std::true_type;
+                    using F = std::false_type;
+                    if (fast) {
+                        if (nev == 2)
+                            run(I2(), T(), T());
+                        else if (jac)
+                            run(I1(), T(), T());
+                        else
+                            run(I1(), F(), T());
+                    } else {
+                        if (nev == 2)
+                            run(I2(), T(), F());
+                        else if (jac)
+                            run(I1(), T(), F());
+                        else
+                            run(I1(), F(), F());
+                    }
                 } else {
                     // ---- Householder passes (qrfac / lmdif qtf for n = 2) on the stored columns
                     const int pc = rfl(SP.pivot), t0f = rfl(SP.t0), t1f = rfl(SP.t1), q0f = rfl(SP.q0);
@@ -1104,8 +1193,20 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     const bool moka0 = mdiv_ok(ajn0s);
                     const double ajn1s = SP.ajn1s, ya1 = 1. / ajn1s, tq0 = SP.tq0;
                     const bool moka1 = mdiv_ok(ajn1s);
-                    auto run = [&](auto kindc) {
+                    // The fast form: no per-lane guard in mdiv and no flag selects.  A pass runs only
+                    // after evaluations whose every kept pixel was good, so each stored dI (in-range
+                    // entries) is a difference of two samples in [0, 255]: |dI| < 256.  The numerators
+                    // are then bounded by the pass-uniform weights, and within these bounds every
+                    // quotient the pass forms stays below mdiv's 1e100 (the 1.01 covers the roundings).
+                    // Entries past len compute garbage the edge chunks zero.
+                    const double bnum = 256. * 1.01 * (wp + wq + 2. * wF);
+                    const double bap = bnum / fabs(hp), baq = bnum / fabs(hq);
+                    const bool fast = t0f && q0f && mokp && mokq && moka0 && bnum < 1e99 && bap < 1e99 &&
+                                      baq < 1e99 && (pass != Q_QR3 || (t1f && moka1 &&
+                                      baq + fabs(tq) * (bap / fabs(ajn0s) + 1.) < 1e99));
+                    auto run = [&](auto kindc, auto fastc) {
                         constexpr int KIND = decltype(kindc)::value;
+                        constexpr bool FAST = decltype(fastc)::value;
                         struct Ld {
                             float p, q, f;
                         };
@@ -1120,48 +1221,57 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             L.f = __builtin_nontemporal_load((const gfloat*)(pcs->slabDF + o4));  // J = (w_j dI_j - F) / h_j needs F
                             return L;
                         };
-                        // edge: the first or the last chunk (the diagonal entries 0 and 1, entries
+                        auto dv = [&](double a, double d, double y, bool mok) {
+                            return FAST ? mdiv_fast(a, d, y) : mdiv(a, d, y, mok);
+                        };
+                        // EDGE: the first or the last chunk (the diagonal entries 0 and 1, entries
                         // past len); every other chunk skips those tests
-                        auto chunk = [&](const Ld& L, int k, bool edge) {
+                        struct Terms {
+                            double t0, t1;
+                            int slow;
+                        };
+                        auto chunk = [&](const Ld& L, int k, auto edgec) {
+                            constexpr bool EDGE = decltype(edgec)::value;
                             const int e = k * kE + lane;
                             const bool in = e < len;
                             // the stored columns: F = wF*dI_F, J_j = (w_j*dI_j - F)/h_j (as the JAC pass)
                             const double F = wF * (double)L.f;
-                            const double ap = mdiv(wp * (double)L.p - F, hp, yp, mokp);
-                            const double aq = mdiv(wq * (double)L.q - F, hq, yq, mokq);
+                            const double ap = dv(wp * (double)L.p - F, hp, yp, mokp);
+                            const double aq = dv(wq * (double)L.q - F, hq, yq, mokq);
                             double t0 = 0., t1 = 0., a = 0.;
                             bool slow = false;
                             if (KIND == Q_QR1) {
                                 // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); v*a_q, v*f
-                                double v = mdiv(ap, ajn0s, ya0, moka0);
-                                if (edge && e == 0) v = v + 1.;
+                                double v = dv(ap, ajn0s, ya0, moka0);
+                                if (EDGE && e == 0) v = v + 1.;
                                 t0 = v * aq;
                                 t1 = v * F;
-                                if (edge && !in) t0 = t1 = 0.;
+                                if (EDGE && !in) t0 = t1 = 0.;
                             } else if (KIND == Q_QR2) {
                                 // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
                                 a = aq;
-                                if (t0f) a = a - tq * mdiv(ap, ajn0s, ya0, moka0);
-                                if (edge) {
+                                if (FAST || t0f) a = a - tq * dv(ap, ajn0s, ya0, moka0);
+                                if (EDGE) {
                                     a = (in && e > 0) ? a : 0.;
                                     if (e == 1) aqs1 = a;
                                 }
                                 t0 = enorm_term2(a, agiant, slow);
                             } else {
                                 // lmdif qtf, j = 1: u_i * wa4_i
-                                const double v = t0f ? mdiv(ap, ajn0s, ya0, moka0) : 0.;
+                                const double v = (FAST || t0f) ? dv(ap, ajn0s, ya0, moka0) : 0.;
                                 double b = aq;
-                                if (t0f) b = b - tq * v;
-                                double u = t1f ? mdiv(b, ajn1s, ya1, moka1) : b;
-                                if (edge && t1f && e == 1) u = u + 1.;
+                                if (FAST || t0f) b = b - tq * v;
+                                double u = (FAST || t1f) ? dv(b, ajn1s, ya1, moka1) : b;
+                                if (EDGE && (FAST || t1f) && e == 1) u = u + 1.;
                                 double wa = F;
-                                if (q0f) wa = wa + v * tq0;
+                                if (FAST || q0f) wa = wa + v * tq0;
                                 t0 = u * wa;
-                                if (edge && !(in && e > 0)) t0 = 0.;
+                                if (EDGE && !(in && e > 0)) t0 = 0.;
                             }
-                            prod.put(cbase + k, slow ? a : t0, t1, slow ? 1 : 0);
+                            return Terms{slow ? a : t0, t1, slow ? 1 : 0};
                         };
-                        // kQD chunks of loads in flight: this pass computes little per entry
+                        // kQD chunks of loads in flight: this pass computes little per entry.  A
+                        // buffer is refilled after its chunk is consumed (no register copies)
                         constexpr int kQD = 8;
                         unsigned o4 = (s8 >> 1) + lane * 4u + (unsigned)k0 * 256u;
                         const unsigned st4 = (unsigned)kS * 256u;
@@ -1178,20 +1288,30 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             for (int j = 0; j < kQD; j++) {
                                 const int kc = k + j * kS;
                                 if (kc < nCh) {
-                                    const Ld nx = load(o4);
-                                    chunk(buf[j], kc, kc == 0 || kc == nCh - 1);
-                                    buf[j] = nx;
+                                    const Terms T = (kc == 0 || kc == nCh - 1) ? chunk(buf[j], kc, std::true_type())
+                                                                               : chunk(buf[j], kc, std::false_type());
+                                    prod.put<KIND == Q_QR1>(cbase + kc, T.t0, T.t1, T.slow);
+                                    buf[j] = load(o4);
                                 }
                                 o4 += st4;
                             }
                         }
                     };
-                    if (pass == Q_QR1)
-                        run(std::integral_constant<int, Q_QR1>());
-                    else if (pass == Q_QR2)
-                        run(std::integral_constant<int, Q_QR2>());
-                    else
-                        run(std::integral_constant<int, Q_QR3>());
+                    if (fast) {
+                        if (pass == Q_QR1)
+                            run(std::integral_constant<int, Q_QR1>(), std::true_type());
+                        else if (pass == Q_QR2)
+                            run(std::integral_constant<int, Q_QR2>(), std::true_type());
+                        else
+                            run(std::integral_constant<int, Q_QR3>(), std::true_type());
+                    } else {
+                        if (pass == Q_QR1)
+                            run(std::integral_constant<int, Q_QR1>(), std::false_type());
+                        else if (pass == Q_QR2)
+                            run(std::integral_constant<int, Q_QR2>(), std::false_type());
+                        else
+                            run(std::integral_constant<int, Q_QR3>(), std::false_type());
+                    }
                     aqs1 = __shfl(aqs1, 1);  // QR2: entry 1 lives in lane 1 of chunk 0
                 }
                 if (!own) {
@@ -1219,8 +1339,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         hp0 = sh.hph3[w][0] != 0;
                         hp1 = sh.hph3[w][1] != 0;
                     }
-                    prod.waitCycles += clock64() - c0;
                     if (lane == 0) {
+                        WS.wait += clock64() - c0;
                         OUT.nrm[0] = OUT.sum[0] = sh.result[w][0];
                         OUT.nrm[1] = OUT.sum[1] = sh.result[w][1];
                         OUT.fail[0] = fail0;
@@ -1234,27 +1354,29 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
             // every lane's slab and LDS stores are done before the bookkeeping reads them
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            const unsigned long long tp1 = clock64();
-            if (own && lane == 0) ctl.after_pass(SS, SP, OUT);
+            if (lane == 0) {
+                const unsigned long long tp1 = clock64();
+                if (own) ctl.after_pass(SS, SP, OUT);
+                const unsigned long long tp2 = clock64();
+                WS.terms += tp1 - WS.t0;
+                WS.ctl += tp2 - tp1;
+                WS.cnt[cls]++;
+                WS.cyc[cls] += tp2 - WS.t0;
+            }
             __builtin_amdgcn_s_waitcnt(0);
-            const unsigned long long tp2 = clock64();
-            cyTerms += tp1 - tp0;
-            cyCtl += tp2 - tp1;
-            clsCnt[cls]++;
-            clsCyc[cls] += tp2 - tp0;
         }
         if (lane == 0) {
             lds_store_rel(&sh.done[w], 1);
             atomicAdd(p.statEval, (unsigned long long)ctl.cnt_eval);
             atomicAdd(p.statPix, (unsigned long long)ctl.cnt_pix);
-            atomicAdd(p.statPass + 0, (unsigned long long)nPass);
-            atomicAdd(p.statPass + 1, cyTerms);
-            atomicAdd(p.statPass + 3, cyCtl);
+            atomicAdd(p.statPass + 0, WS.nPass);
+            atomicAdd(p.statPass + 1, WS.terms);
+            atomicAdd(p.statPass + 3, WS.ctl);
             for (int k = 0; k < 4; k++) {
-                atomicAdd(p.statPass + 7 + k, clsCnt[k]);
-                atomicAdd(p.statPass + 11 + k, clsCyc[k]);
+                atomicAdd(p.statPass + 7 + k, WS.cnt[k]);
+                atomicAdd(p.statPass + 11 + k, WS.cyc[k]);
             }
-            atomicAdd(p.statPass + 21, (unsigned long long)prod.waitCycles);
+            atomicAdd(p.statPass + 21, WS.wait);
         }
     } else {
         chain_wave(lane, tStart, p.maxTicks, p.statPass + 2, p.statPass + 18);

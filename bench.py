@@ -236,6 +236,8 @@ def main():
         }
         if check is not None:
             out["sharding_check"] = check
+        if dist is None:  # bit-identity across builds / boxes (A/B runs compare it)
+            out["records_sha256"] = records_digest(mine.tobytes())
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:
