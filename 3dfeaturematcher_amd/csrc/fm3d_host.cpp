@@ -447,6 +447,11 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     if ((r = ensure_offsets(c))) return r;
     if (c->pyr1.empty()) return fail(c, FM3D_ERR_INVALID, "fm3d_set_images (NormalOptimizer::setImages) not called");
     if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "g12 not set (SingleCameraTriangulator::setg12)");
+    // the kernel's isPixelGood compares bit patterns (u = xd*fx + cx is never -0) and its
+    // distortion terms round like the reference's only where u, v are dominated by cx, cy near the
+    // optical axis (fm3d_lm2.hip, geometry2): a principal point inside the image
+    if (!(c->cam.cx >= 1e-3 && c->cam.cy >= 1e-3))
+        return fail(c, FM3D_ERR_UNSUPPORTED, "computeOptimizedNormals needs a principal point with cx, cy > 0");
     const int levels = c->s.pyramids;
     HIPCHK(c, c->lmNormals.ensure((size_t)(P + 1) * 3 * sizeof(double)));
     HIPCHK(c, c->lmStatus.ensure((size_t)(P + 1) * sizeof(int)));
@@ -542,6 +547,8 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         c->wallKhz = khz;
         const char* co = getenv("FM3D_LM_COOP");  // A/B switch for the tail help
         p.coop = co ? atoi(co) : 1;
+        const char* sf = getenv("FM3D_LM_SAFE");  // test switch: the guarded pass forms only
+        p.safe = sf ? atoi(sf) : 0;
     }
     // the counters (incl. the overflow word) are reset for every call, also for P == 0
     HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 256, c->stream));

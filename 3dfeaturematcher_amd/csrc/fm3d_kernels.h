@@ -53,6 +53,7 @@ struct LMParams {
     long long maxTicks;      // safety bound on wall-clock ticks per workgroup
     int* overflow;           // set to 1 if a workgroup hit a guard
     int coop;                // 1: waves without points help busy slots (tail of the launch)
+    int safe;                // 1: every pass takes the guarded (per-lane) form (tests of that form)
     // [passes, cycles terms, cycles chain, cycles control, cycles total, wall ticks sum, wall ticks
     //  max, class passes x4, class cycles x4, max start, max end, min start, ..., producer waits]
     unsigned long long* statPass;

@@ -56,6 +56,11 @@ constexpr int kE = 64;         // entries per chunk: one per lane
 constexpr int kR = kLM2Ring;   // chunks in flight per slot (LDS ring depth)
 static_assert((kR & (kR - 1)) == 0, "ring depth: a power of two");
 constexpr int kRow = kE + 2;   // padded ring row: consecutive rows start 4 banks apart
+// doubles per ring position: 2 rows per slot, padded to a multiple of 256 B (64 banks x 4 B)
+constexpr int kRS = (2 * kLM2Slots * kRow * 8 + 255) / 256 * 256 / 8;
+#ifndef FM3D_EVAL_PIPE
+#define FM3D_EVAL_PIPE 1
+#endif
 
 enum PassKind2 { Q_IDLE = 0, Q_INIT, Q_LEVEL, Q_EVAL, Q_QR1, Q_QR2, Q_QR3, Q_DONE };
 enum SumKind { S_NONE = 0, S_ENORM, S_DOT };
@@ -427,9 +432,12 @@ struct Ctl2 {
 };
 
 struct Shared {
-    // chunk terms [slot][ring position][sum][entry]; entry kE holds the chunk's slow flag for
-    // that sum (nonzero: raw values for MINPACK's full enorm instead of squares)
-    double ring[kW][kR][2][kRow];
+    // chunk terms (rows padded to kRow; the slow flags travel in the tags):
+    // ring[pos][(2s + k) * kRow + e]: ring position pos holds, for every slot s and sum k, one
+    // row, the chain lane's (2s + k).  Rows of one position lie 528 B apart (16 B mod 256) and a
+    // position spans a multiple of 256 B, so in the chain's ds_read_b128 every lane of a 16-lane
+    // group reads its own four banks whatever ring positions the slots are at (conflict-free).
+    alignas(256) double ring[kR][kRS];
     int rowTag[kW][kR];            // (chunk index << 2) | slow flags of the terms a ring position holds (published last)
     int consumed[kW][2];           // chunks consumed, per chain lane (monotonic)
     int resultId[kW][2];           // id of the last pass whose result is published
@@ -470,7 +478,8 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
 
 // sum += row[0..64) in index order: 64 dependent adds, fed by ds_read_b128 into four
 // register sets of 8 values in rotation, so three sets (24 values) are in flight while one is
-// added.  Compiler barriers keep the reads in that order.
+// added.  Compiler barriers keep the reads in that order.  (A generic form indexing the sets
+// modulo their count compiled to indexed register moves: 4-5x slower rounds.)
 __device__ __forceinline__ double chain_sum64(double sum, const double* row) {
 #if FM3D_ABL_CHAIN
     // ablation (timing experiments only, wrong sums): one add per chunk
@@ -554,14 +563,18 @@ struct Producer {
     template <bool TWO = true>
     __device__ __forceinline__ void write(int c, double t0, double t1, int slowBits) {
         const int pos = c & (kR - 1);
-        double* row0 = &sh->ring[w][pos][0][0];
+        double* row0 = &sh->ring[pos][2 * w * kRow];
         row0[lane] = t0;
         if (TWO) row0[kRow + lane] = t1;
         // every lane's ring stores are done before the tag is published (lgkmcnt is per wave).
         // The tag carries the chunk index and the two sums' slow flags (bit k: sum k holds raw
         // values); it is written by every lane (same address, same value): no lane-0 branch
+#if FM3D_TAG_NOWAIT
+        __hip_atomic_store(&sh->rowTag[w][pos], (c << 2) | slowBits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         lds_store_rel(&sh->rowTag[w][pos], (c << 2) | slowBits);
+#endif
     }
     template <bool TWO = true>
     __device__ __forceinline__ void put(int c, double t0, double t1, int slowBits) {
@@ -681,6 +694,15 @@ __device__ __forceinline__ float bilinear_w(unsigned lo, unsigned hi, float x, f
     return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
 }
 
+// the same with the fractions x - floor(x), y - floor(y) given
+__device__ __forceinline__ float bilinear_f(unsigned lo, unsigned hi, float xf, float yf) {
+    const float b00 = (float)(lo & 0xff), b01 = (float)((lo >> 8) & 0xff);
+    const float b10 = (float)(hi & 0xff), b11 = (float)((hi >> 8) & 0xff);
+    const float xm0 = 1.0f - xf, xm1 = xf;
+    const float ym0 = 1.0f - yf, ym1 = yf;
+    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
+}
+
 // enorm term with the slow-path flag: x^2 is the term whenever no lane of the chunk needs
 // MINPACK's small/large component handling (x = 0 adds +0, as enorm does).  slow: whether
 // any lane of the wave does (a wave-uniform ballot of the lane tests).
@@ -753,7 +775,7 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
 #pragma nounroll
             for (int b = 0; b < 2; b++) {
                 if (b < nb) {
-                    const double* row = &g_sh.ring[ss_][cur & (kR - 1)][which][0];
+                    const double* row = &g_sh.ring[cur & (kR - 1)][lane * kRow];
                     const bool slow = (((b ? tag1 : tag0) >> which) & 1) != 0;
                     const double acc0 = acc;
                     acc = chain_sum64(acc, row);
@@ -1008,7 +1030,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     // per-lane guard.  The latter holds because the divided numerators of good
                     // pixels, w_j*dI_j - wF*dI_F, combine samples in [0, 255] (|dI| < 256) with the
                     // pass-uniform weights; other lanes are zeroed after the division.
-                    const bool fast = div_nn_ok(mm0) && (nev < 2 || div_nn_ok(mm1)) &&
+                    const bool fast = !p.safe && div_nn_ok(mm0) && (nev < 2 || div_nn_ok(mm1)) &&
                                       (!jac || (mok0 && 256. * 1.01 * (w0 + wF) < 1e99 &&
                                                 (nev < 2 || (mok1 && 256. * 1.01 * (w1 + wF) < 1e99))));
                     // NEV evaluations per entry (2: both forward-difference columns); JAC: the
@@ -1098,7 +1120,86 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         // this wave's chunks: k0, k0 + kS, ...; st8 / st4: the offset step between them
                         unsigned o8 = s8 + lane * 8u + (unsigned)k0 * 512u, o4 = o8 >> 1;
                         const unsigned st8 = (unsigned)kS * 512u, st4 = st8 >> 1;
-                        if (NEV == 2) {
+                        if (NEV == 2 && FM3D_EVAL_PIPE) {
+                            // both forward-difference columns of a chunk side by side (their
+                            // geometries interleave), software-pipelined: chunk k + 1's geometries and
+                            // gathers are computed while chunk k's gathers are in flight, then chunk
+                            // k's samples and terms; unrolled by two chunks so that the stages
+                            // alternate without copies.  Failures are taken in entry order.
+                            struct St2 {
+                                float xf0, yf0, xf1, yf1, i1, dF;
+                                uint2 a, c;
+                                LaneMask ok0, ok1;  // in & i1ok & good, per column
+                            };
+                            auto front2 = [&](const Ld& L, int k) {
+                                const LaneMask in = in_mask(k, len), ok = i1ok ? in : 0ull;
+                                const Geo2 g0 = geo(L.ux, L.uy, n00, n10, n20, mm0);
+                                const Geo2 g1 = geo(L.ux, L.uy, n01, n11, n21, mm1);
+                                St2 S;
+                                S.a = gather(g0.off);  // every lane: a failed entry reads the image's first bytes
+                                S.c = gather(g1.off);
+                                const LaneMask b0 = in & ~g0.inbox;
+                                if (b0 && fail0 == 0x7fffffff) {
+                                    const int l = __ffsll((long long)b0) - 1;
+                                    const int cd = plane_code(L.ux, L.uy, n00, n10, n20, mm0);
+                                    fail0 = (k * kE + l) * 4 + __shfl(cd, l);
+                                }
+                                ph30 |= (in & g0.inbox & ~g0.good) != 0;
+                                const LaneMask b1 = in & ~g1.inbox;
+                                if (b1 && fail1 == 0x7fffffff) {
+                                    const int l = __ffsll((long long)b1) - 1;
+                                    const int cd = plane_code(L.ux, L.uy, n01, n11, n21, mm1);
+                                    fail1 = (k * kE + l) * 4 + __shfl(cd, l);
+                                }
+                                ph31 |= (in & g1.inbox & ~g1.good) != 0;
+                                S.xf0 = g0.fx - floorf(g0.fx);  // the bilinear fractions
+                                S.yf0 = g0.fy - floorf(g0.fy);
+                                S.xf1 = g1.fx - floorf(g1.fx);
+                                S.yf1 = g1.fy - floorf(g1.fy);
+                                S.i1 = L.i1;
+                                S.dF = (float)L.dF;  // a float value: exact
+                                S.ok0 = ok & g0.good;
+                                S.ok1 = ok & g1.good;
+                                return S;
+                            };
+                            auto back2 = [&](const St2& S, int k, unsigned oo) {
+                                // evaluateNormal :145-148, fdjac2 forward differences
+                                const float dI0 = S.i1 - bilinear_f(S.a.x, S.a.y, S.xf0, S.yf0);
+                                const float dI1 = S.i1 - bilinear_f(S.c.x, S.c.y, S.xf1, S.yf1);
+                                const double F = wF * (double)S.dF;
+                                double v0 = jdiv(w0 * (double)dI0 - F, h0, y0, mok0);
+                                double v1 = jdiv(w1 * (double)dI1 - F, h1, y1, mok1);
+                                v0 = sel_mask(v0, S.ok0);
+                                v1 = sel_mask(v1, S.ok1);
+                                bool slow0, slow1;
+                                const double t0 = enorm_term2(v0, agiant, slow0);
+                                const double t1 = enorm_term2(v1, agiant, slow1);
+                                prod.reserve(cbase + k);
+                                {
+                                    const cProjConst* pc = proj_consts(p.proj);
+                                    *(gfloat*)(pc->slabDJ0 + oo) = dI0;
+                                    *(gfloat*)(pc->slabDJ1 + oo) = dI1;
+                                }
+                                prod.write<true>(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
+                            };
+                            // A stage past the last chunk computes garbage from slab padding (its
+                            // entries are not `in`: no failures); no branch between gathers and use
+                            Ld A = load(o8, o4), B = load(o8 + st8, o4 + st4);
+                            St2 S = front2(A, k0), N;
+                            A = load(o8 + 2 * st8, o4 + 2 * st4);
+                            for (int k = k0; k < nCh; k += 2 * kS) {
+                                N = front2(B, k + kS);
+                                B = load(o8 + 3 * st8, o4 + 3 * st4);
+                                back2(S, k, o4);
+                                if (k + kS >= nCh) break;  // wave-uniform
+                                S = front2(A, k + 2 * kS);
+                                A = load(o8 + 4 * st8, o4 + 4 * st4);
+                                back2(N, k + kS, o4 + st4);
+                                o8 += 2 * st8;
+                                o4 += 2 * st4;
+                            }
+                        } else if (NEV == 2) {
+                            // (the unpipelined form, FM3D_EVAL_PIPE=0)
                             // two chunks of slab loads in flight ahead of the one being computed
                             Ld A = load(o8, o4), B = load(o8 + st8, o4 + st4);
                             for (int k = k0; k < nCh; k += 2 * kS) {
@@ -1113,7 +1214,101 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 o8 += 2 * st8;
                                 o4 += 2 * st4;
                             }
+                        } else if (FM3D_EVAL_PIPE) {
+                            // one evaluation per entry: two chunks side by side (their geometries
+                            // interleave), software-pipelined: the geometry and the image-2 gathers
+                            // of pair p + 1 are computed while pair p's gathers are in flight, then
+                            // pair p's samples, residuals and terms.  Failures are still taken in
+                            // entry order (pair p's in the previous iteration).
+                            struct St {
+                                float fxA, fyA, fxB, fyB, i1A, i1B, dFA, dFB;
+                                uint2 a, b;
+                                LaneMask okA, okB;  // in & i1ok & good
+                            };
+                            auto front = [&](const Ld& A, const Ld& B, int k) {
+                                const int kB = k + kS;
+                                const LaneMask inA = in_mask(k, len), inB = in_mask(kB, len);
+                                const Geo2 gA = geo(A.ux, A.uy, n00, n10, n20, mm0);
+                                // past the last chunk B holds slab padding: its entries are not
+                                // `in`, its gathers read the image's first bytes, nothing is stored
+                                const Geo2 gB = geo(B.ux, B.uy, n00, n10, n20, mm0);
+                                St S;
+                                S.a = gather(gA.off);
+                                S.b = gather(gB.off);
+                                const LaneMask bA = inA & ~gA.inbox;
+                                const LaneMask bB = inB & ~gB.inbox;
+                                if ((bA | bB) && fail0 == 0x7fffffff) {
+                                    const bool first = bA != 0;
+                                    const int l = __ffsll((long long)(first ? bA : bB)) - 1;
+                                    const int cd = first ? plane_code(A.ux, A.uy, n00, n10, n20, mm0)
+                                                         : plane_code(B.ux, B.uy, n00, n10, n20, mm0);
+                                    fail0 = ((first ? k : kB) * kE + l) * 4 + __shfl(cd, l);
+                                }
+                                ph30 |= ((inA & gA.inbox & ~gA.good) | (inB & gB.inbox & ~gB.good)) != 0;
+                                S.fxA = gA.fx - floorf(gA.fx);  // the bilinear fractions (the floors are the geometry's)
+                                S.fyA = gA.fy - floorf(gA.fy);
+                                S.fxB = gB.fx - floorf(gB.fx);
+                                S.fyB = gB.fy - floorf(gB.fy);
+                                S.i1A = A.i1;
+                                S.i1B = B.i1;
+                                S.dFA = (float)A.dF;  // a float value: exact
+                                S.dFB = (float)B.dF;
+                                S.okA = (i1ok ? inA : 0ull) & gA.good;
+                                S.okB = (i1ok ? inB : 0ull) & gB.good;
+                                return S;
+                            };
+                            // the residual / Jacobian value of one chunk of the stage (the samples wait
+                            // for the stage's gathers)
+                            auto value = [&](float xf, float yf, uint2 w, float i1, float dF, LaneMask ok, float& dI) {
+                                dI = i1 - bilinear_f(w.x, w.y, xf, yf);
+                                const double r = w0 * (double)dI;
+                                const double v = JAC ? jdiv(r - wF * (double)dF, h0, y0, mok0) : r;
+                                return sel_mask(v, ok);
+                            };
+                            auto publish = [&](double v, float dI, unsigned oo, int kk) {
+                                {
+                                    const cProjConst* pc = proj_consts(p.proj);
+                                    *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + oo) = dI;
+                                }
+                                bool slow;
+                                const double t = enorm_term2(v, agiant, slow);
+                                prod.write<false>(cbase + kk, slow ? v : t, 0., slow ? 1 : 0);
+                            };
+                            // both chunks' values first (no branch between the gathers and their
+                            // use), then the ring space, then the stores of the chunks that exist
+                            auto back = [&](const St& S, int k, unsigned oo) {
+                                const int kB = k + kS;
+                                const bool two = kB < nCh;  // wave-uniform
+                                float dIA, dIB;
+                                const double vA = value(S.fxA, S.fyA, S.a, S.i1A, S.dFA, S.okA, dIA);
+                                const double vB = value(S.fxB, S.fyB, S.b, S.i1B, S.dFB, S.okB, dIB);
+                                prod.reserve(cbase + (two ? kB : k));  // space for both chunks
+                                publish(vA, dIA, oo, k);
+                                if (two) publish(vB, dIB, oo + st4, kB);
+                            };
+                            // unrolled by two pairs, so that the stages alternate without copies.
+                            // A stage past the last chunk computes garbage from slab padding and
+                            // the image's first bytes (its entries are not `in`: no failures, no
+                            // stores); it keeps the loop free of branches between gathers and use.
+                            Ld A = load(o8, o4), B = load(o8 + st8, o4 + st4);
+                            St S = front(A, B, k0), N;
+                            A = load(o8 + 2 * st8, o4 + 2 * st4);
+                            B = load(o8 + 3 * st8, o4 + 3 * st4);
+                            for (int k = k0; k < nCh; k += 4 * kS) {
+                                N = front(A, B, k + 2 * kS);
+                                A = load(o8 + 4 * st8, o4 + 4 * st4);
+                                B = load(o8 + 5 * st8, o4 + 5 * st4);
+                                back(S, k, o4);
+                                if (k + 2 * kS >= nCh) break;  // wave-uniform
+                                S = front(A, B, k + 4 * kS);
+                                A = load(o8 + 6 * st8, o4 + 6 * st4);
+                                B = load(o8 + 7 * st8, o4 + 7 * st4);
+                                back(N, k + 2 * kS, o4 + 2 * st4);
+                                o8 += 4 * st8;
+                                o4 += 4 * st4;
+                            }
                         } else {
+                            // (the unpipelined form, FM3D_EVAL_PIPE=0)
                             // one evaluation per entry: two chunks side by side, so the two
                             // independent geometries interleave (as the two columns of a Jacobian
                             // pass do); the slab loads of the next pair are issued once the pair's
@@ -1201,7 +1396,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     // Entries past len compute garbage the edge chunks zero.
                     const double bnum = 256. * 1.01 * (wp + wq + 2. * wF);
                     const double bap = bnum / fabs(hp), baq = bnum / fabs(hq);
-                    const bool fast = t0f && q0f && mokp && mokq && moka0 && bnum < 1e99 && bap < 1e99 &&
+                    const bool fast = !p.safe && t0f && q0f && mokp && mokq && moka0 && bnum < 1e99 && bap < 1e99 &&
                                       baq < 1e99 && (pass != Q_QR3 || (t1f && moka1 &&
                                       baq + fabs(tq) * (bap / fabs(ajn0s) + 1.) < 1e99));
                     auto run = [&](auto kindc, auto fastc) {
@@ -1272,7 +1467,10 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry.  A
                         // buffer is refilled after its chunk is consumed (no register copies)
-                        constexpr int kQD = 8;
+#ifndef FM3D_QR_DEPTH
+#define FM3D_QR_DEPTH 8
+#endif
+                        constexpr int kQD = FM3D_QR_DEPTH;
                         unsigned o4 = (s8 >> 1) + lane * 4u + (unsigned)k0 * 256u;
                         const unsigned st4 = (unsigned)kS * 256u;
                         Ld buf[kQD];

@@ -250,8 +250,11 @@ def _normals_case(fm3d, orc, pair, points, ray, bound=(1024, 768), levels=3):
     return kept, normals, st, info, nfev, ref, (R2, t2)
 
 
-@pytest.mark.parametrize("ray", [8, 16])
-def test_normals_bitwise_vs_oracle(fm3d, orc, pair, ray):
+@pytest.mark.parametrize("ray,safe", [(8, 0), (16, 0), (16, 1)])
+def test_normals_bitwise_vs_oracle(fm3d, orc, pair, ray, safe, monkeypatch):
+    # safe = 1: every pass takes the guarded form (per-lane division guards, general flags) that
+    # the kernel otherwise keeps for out-of-range weights and numerators
+    monkeypatch.setenv("FM3D_LM_SAFE", str(safe))
     # triangulated points of the pair (oracle chain), plus border / degenerate cases
     q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
     pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)

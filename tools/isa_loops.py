@@ -47,7 +47,8 @@ def main():
               f"f64 {sum(n for k, n in c.items() if k.startswith('v_') and 'f64' in k):4d} "
               f"ds {sum(n for k, n in c.items() if k.startswith('ds_')):3d} "
               f"glob {sum(n for k, n in c.items() if k.startswith('global_')):3d} "
-              f"SALU {sum(n for k, n in c.items() if k.startswith('s_')):4d}")
+              f"SALU {sum(n for k, n in c.items() if k.startswith('s_')):4d} "
+              f"scratch {sum(n for k, n in c.items() if k.startswith('scratch_')):3d}")
 
 
 if __name__ == "__main__":
