@@ -695,12 +695,17 @@ __device__ __forceinline__ float bilinear_w(unsigned lo, unsigned hi, float x, f
 }
 
 // the same with the fractions x - floor(x), y - floor(y) given
+// (as two-lane float vectors: v_pk_mul_f32 / v_pk_add_f32 do the two columns' independent
+// products and sums, each rounded as the scalar operation; 11 instructions instead of 17)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bilinear_f(unsigned lo, unsigned hi, float xf, float yf) {
-    const float b00 = (float)(lo & 0xff), b01 = (float)((lo >> 8) & 0xff);
-    const float b10 = (float)(hi & 0xff), b11 = (float)((hi >> 8) & 0xff);
-    const float xm0 = 1.0f - xf, xm1 = xf;
+    const f32x2 b0 = {(float)(lo & 0xff), (float)((lo >> 8) & 0xff)};  // b00, b01
+    const f32x2 b1 = {(float)(hi & 0xff), (float)((hi >> 8) & 0xff)};  // b10, b11
     const float ym0 = 1.0f - yf, ym1 = yf;
-    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
+    const f32x2 sc = b0 * ym0 + b1 * ym1;  // (b00 ym0 + b10 ym1, b01 ym0 + b11 ym1)
+    const f32x2 xm = {1.0f - xf, xf};
+    const f32x2 q = xm * sc;
+    return q.x + q.y;  // xm0 * (...) + xm1 * (...)
 }
 
 // enorm term with the slow-path flag: x^2 is the term whenever no lane of the chunk needs
@@ -1033,12 +1038,32 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     const bool fast = !p.safe && div_nn_ok(mm0) && (nev < 2 || div_nn_ok(mm1)) &&
                                       (!jac || (mok0 && 256. * 1.01 * (w0 + wF) < 1e99 &&
                                                 (nev < 2 || (mok1 && 256. * 1.01 * (w1 + wF) < 1e99))));
+                    // the slab bases, once per pass (scalar registers; used where FM3D_EVAL_HOIST)
+#ifndef FM3D_EVAL_HOIST
+#define FM3D_EVAL_HOIST 0
+#endif
+                    struct SlabB {
+                        const char *slabRX, *slabRY, *slabI1;
+                        char *slabDF, *slabDJ0, *slabDJ1;
+                    };
+                    const SlabB sbh = [&] {
+                        const cProjConst* q = proj_consts(p.proj);
+                        return SlabB{q->slabRX, q->slabRY, q->slabI1, q->slabDF, q->slabDJ0, q->slabDJ1};
+                    }();
                     // NEV evaluations per entry (2: both forward-difference columns); JAC: the
                     // values are Jacobian columns (r - fvec)/h_j, else the residual fvec itself
                     auto run = [&](auto nevc, auto jacc, auto fastc) {
                         constexpr int NEV = decltype(nevc)::value;
                         constexpr bool JAC = decltype(jacc)::value;
                         constexpr bool FAST = decltype(fastc)::value;
+                        // hoisted bases in the single-evaluation passes; the Jacobian passes,
+                        // short of scalar registers, re-read them (hoisted there, they spill)
+                        auto sb = [&]() {
+                            if constexpr (FM3D_EVAL_HOIST && !JAC)
+                                return &sbh;
+                            else
+                                return proj_consts(p.proj);
+                        };
                         struct Ld {
                             double ux, uy, dF;
                             float i1;
@@ -1055,7 +1080,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         // slab streams are read once per pass (nontemporal: they leave L2 to the
                         // image gathers).
                         auto load = [&](unsigned o8, unsigned o4) {
-                            const cProjConst* pc = proj_consts(p.proj);
+                            const auto* pc = sb();
                             Ld L;
                             L.ux = __builtin_nontemporal_load((const gdouble*)(pc->slabRX + o8));
                             L.uy = __builtin_nontemporal_load((const gdouble*)(pc->slabRY + o8));
@@ -1101,7 +1126,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             double v0 = JAC ? jdiv(r0 - wF * L.dF, h0, y0, mok0) : r0;
                             v0 = sel_mask(v0, ok & g0.good);
                             {
-                                const cProjConst* pc = proj_consts(p.proj);
+                                const auto* pc = sb();
                                 *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + o4) = dI0;
                             }
                             bool slow0 = false, slow1 = false;
@@ -1112,7 +1137,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 const double r1 = w1 * (double)dI1;
                                 v1 = jdiv(r1 - wF * L.dF, h1, y1, mok1);
                                 v1 = sel_mask(v1, ok & g1.good);
-                                *(gfloat*)(proj_consts(p.proj)->slabDJ1 + o4) = dI1;
+                                *(gfloat*)(sb()->slabDJ1 + o4) = dI1;
                                 t1 = enorm_term2(v1, agiant, slow1);
                             }
                             prod.write<NEV == 2>(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
@@ -1176,7 +1201,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 const double t1 = enorm_term2(v1, agiant, slow1);
                                 prod.reserve(cbase + k);
                                 {
-                                    const cProjConst* pc = proj_consts(p.proj);
+                                    const auto* pc = sb();
                                     *(gfloat*)(pc->slabDJ0 + oo) = dI0;
                                     *(gfloat*)(pc->slabDJ1 + oo) = dI1;
                                 }
@@ -1267,7 +1292,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             };
                             auto publish = [&](double v, float dI, unsigned oo, int kk) {
                                 {
-                                    const cProjConst* pc = proj_consts(p.proj);
+                                    const auto* pc = sb();
                                     *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + oo) = dI;
                                 }
                                 bool slow;
@@ -1345,7 +1370,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                     double v = JAC ? jdiv(r - wF * dF, h0, y0, mok0) : r;
                                     v = sel_mask(v, (i1ok ? in : 0ull) & g.good);
                                     {
-                                        const cProjConst* pc = proj_consts(p.proj);
+                                        const auto* pc = sb();
                                         *(gfloat*)((JAC ? pc->slabDJ0 : pc->slabDF) + oo) = dI;
                                     }
                                     bool slow;
@@ -1406,10 +1431,29 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             float p, q, f;
                         };
                         // o4: byte offset of the chunk's entries in the 4-byte slab arrays
+#ifndef FM3D_QR_HOIST
+#define FM3D_QR_HOIST 1
+#endif
+#if FM3D_QR_HOIST
+                        // the three slab bases once per pass (scalar registers; the per-chunk
+                        // re-read cost a dozen scalar instructions per chunk)
+                        const cProjConst* pcs0 = proj_consts(p.proj);
+                        const char* const Dp0 = pc ? pcs0->slabDJ1 : pcs0->slabDJ0;
+                        const char* const Dq0 = pc ? pcs0->slabDJ0 : pcs0->slabDJ1;
+                        const char* const Df0 = pcs0->slabDF;
+#endif
                         auto load = [&](unsigned o4) {
+#if FM3D_QR_HOIST
+                            const char* Dp = Dp0;
+                            const char* Dq = Dq0;
+                            struct {
+                                const char* slabDF;
+                            } s0{Df0}, *pcs = &s0;
+#else
                             const cProjConst* pcs = proj_consts(p.proj);
                             const char* Dp = pc ? pcs->slabDJ1 : pcs->slabDJ0;
                             const char* Dq = pc ? pcs->slabDJ0 : pcs->slabDJ1;
+#endif
                             Ld L;
                             L.p = __builtin_nontemporal_load((const gfloat*)(Dp + o4));
                             L.q = __builtin_nontemporal_load((const gfloat*)(Dq + o4));
