@@ -227,6 +227,8 @@ def main():
             "upload_ms": upload_ms,
             "download_ms": download_ms,
             "pcie_inclusive_value": all_kept / args.steps / (frame_s + (upload_ms + download_ms) * 1e-3),
+            # the input rate beside the kept rate (queries of the frame pair per second)
+            "input_keypoints_per_s": wl["keypoints"] * (world if args.weak else 1) / frame_s,
             "roofline": roofline(stats, lm_ms, pix, evals, args, pair, s),
             "cpu_baseline": cpu,
             "stages_ms": {k: last_st[k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "lm_ms", "total_ms")},

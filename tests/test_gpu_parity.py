@@ -520,12 +520,15 @@ def test_c2_sift10k_match_and_dlt(fm3d, orc, synth):
     assert len(q) > 8000 and np.mean(fp.true_train[q] == t) > 0.99
 
 
-def test_c3_orb10k_pipeline_ray32(fm3d, orc, synth):
-    """BASELINE configs[2] (C3): 10k ORB-256 (Hamming) + normals on 64x64-pixel neighbourhoods
-    (pixelsRay 32), through the device-resident pipeline.  Matching and DLT are checked in full;
-    the LM on the records of the first 150 triangulated points (the oracle's CPU time bound)."""
+@pytest.mark.parametrize("ray,k", [(32, 150), (64, 96)])
+def test_c3_orb10k_pipeline(fm3d, orc, synth, ray, k):
+    """BASELINE configs[2] (C3): 10k ORB-256 (Hamming) + normals, through the device-resident
+    pipeline, in SURVEY.md §8(d)'s two variants: 64x64-pixel neighbourhoods (pixelsRay 32) and
+    pixelsRay 64.  Matching and DLT are checked in full; the LM on a seeded random sample of k
+    inliers (the oracle's CPU time bound) bit-exact against the oracle's DETMATH mode: which
+    points survive, and their normals."""
     fp = synth.make_frame_pair(10_000, seed=102, desc="orb")
-    s = _settings(fm3d, fp.cam, pixelsRay=32, nndrEpsilon=0.8)
+    s = _settings(fm3d, fp.cam, pixelsRay=ray, nndrEpsilon=0.8)
     ctx = fm3d.Context(s)
     try:
         sct = fm3d.SingleCameraTriangulator(ctx)
@@ -537,20 +540,22 @@ def test_c3_orb10k_pipeline_ray32(fm3d, orc, synth):
         rec = pipe.records(n)
     finally:
         ctx.close()
-    q, t, _ = orc.match_nndr(fp.desc1, fp.desc2, orc.BITS, 0.8, oracle_threads())
+    q, t, d = orc.match_nndr(fp.desc1, fp.desc2, orc.BITS, 0.8, oracle_threads())
     assert stats["matches"] == len(q)
     pts, mask = orc.triangulate(fp.cam, fp.g12, 1.5, 2.4, fp.kp1, fp.kp2, q, t)
     assert stats["inliers"] == len(pts)
-    k = 150
-    ref = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, 3, pts[:k], 32, mode=orc.DETMATH,
+    # survivors: in match order, each carrying its match and its triangulated point
+    pos = np.searchsorted(q[mask], rec["queryIdx"])
+    assert (np.diff(rec["queryIdx"]) > 0).all() and np.array_equal(q[mask][pos], rec["queryIdx"])
+    assert np.array_equal(rec["trainIdx"], t[mask][pos]) and np.array_equal(rec["distance"], d[mask][pos])
+    assert np.array_equal(rec["point"], pts[pos])
+    sel = np.sort(np.random.default_rng(1000 + ray).choice(len(pts), k, replace=False))
+    ref = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, 3, pts[sel], ray, mode=orc.DETMATH,
                                nthreads=oracle_threads())
     ok = ref["status"] == 0
-    qi = q[mask][:k]
-    sub = rec[np.isin(rec["queryIdx"], qi)]
-    assert np.array_equal(sub["queryIdx"], qi[ok])
-    assert np.array_equal(sub["point"], pts[:k][ok])
-    assert np.array_equal(sub["normal"], ref["normals"][ok])
-    assert n > 0.3 * len(pts)
+    assert np.array_equal(np.isin(sel, pos), ok)
+    assert np.array_equal(rec[np.isin(pos, sel)]["normal"], ref["normals"][ok])
+    assert ok.sum() > k // 4 and n > 0.3 * len(pts)
 
 
 # ---------------------------------------------------------------- error paths and part boundaries
