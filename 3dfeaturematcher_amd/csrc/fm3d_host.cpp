@@ -483,7 +483,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     if (cap < 1) cap = 1;
     if (groups > cap) groups = cap;
     // the summed passes address a slab array with a 32-bit byte offset
-    const long cap32 = (long)((((size_t)1 << 32) - ((size_t)1 << 20)) / (ents * sizeof(double)));
+    const long cap32 = (long)((((size_t)1 << 32) - ((size_t)1 << 20)) / (ents * sizeof(double) * (FM3D_RAY_AOS ? 2 : 1)));
     if (groups > cap32) groups = cap32;
     if (groups < 1) groups = 1;
     // +8 KiB: the passes prefetch up to eight 64-entry chunks past a slot's last entry
@@ -502,7 +502,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         pc.cam = c->cam;
         const size_t Gn = (size_t)groups * slots * c->nOffPad;  // entries per slab array
         pc.slabRX = (const char*)c->slab.p;
-        pc.slabRY = pc.slabRX + Gn * sizeof(double);
+        pc.slabRY = FM3D_RAY_AOS ? pc.slabRX + sizeof(double) : pc.slabRX + Gn * sizeof(double);
         pc.slabI1 = (const char*)c->slabI1.p;
         pc.slabDF = (char*)c->slabI1.p + Gn * 4;
         pc.slabDJ0 = pc.slabDF + Gn * 4;

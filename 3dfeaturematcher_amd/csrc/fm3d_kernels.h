@@ -7,6 +7,15 @@
 #include "fm3d.h"
 #include "fm3d_device.h"
 
+// LM ray slab layout: 1 = one (ux, uy) record of 16 bytes per entry (one 16-byte load per
+// entry), 0 = separate ux and uy arrays (two 8-byte loads; round 2's first layout).  Same-box
+// A/B at C4 (profiles/r02_lm_ray_aos_ab.json): with the single-evaluation passes' slab bases
+// in scalar registers (FM3D_EVAL_HOIST), 3.6 % fewer cycles per single-evaluation pass (launch
+// within box noise, 0.5-1.2 % fewer cycles), bit-identical records.
+#ifndef FM3D_RAY_AOS
+#define FM3D_RAY_AOS 1
+#endif
+
 namespace fm3d {
 
 struct LevelDesc {

@@ -67,6 +67,8 @@ enum SumKind { S_NONE = 0, S_ENORM, S_DOT };
 
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) float gfloat;
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) d2v gd2v;
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) const long long gi64;  // an int2 offset (x low, y high)
 typedef __attribute__((address_space(1))) const uint8_t gu8;
@@ -120,8 +122,13 @@ struct Slab {
 __device__ inline Slab slab_of(const LMParams& p, long gslot) {
     const size_t n = (size_t)p.nOffPad, G = (size_t)p.nWaves * kW;
     Slab s;
+#if FM3D_RAY_AOS
+    s.RX = (gdouble*)p.slab + gslot * n * 2;  // (ux, uy) pairs: one 16-byte record per entry
+    s.RY = s.RX + 1;
+#else
     s.RX = (gdouble*)p.slab + gslot * n;
     s.RY = s.RX + G * n;
+#endif
     s.I1 = (gfloat*)p.slabI1 + gslot * n;
     s.DF = s.I1 + G * n;
     s.DJ0 = s.DF + G * n;
@@ -949,8 +956,12 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         const int pos = base + __popcll(bm & ltMask);
                         double ux, uy;
                         undistort1(p.cam, px, py, ux, uy);
+#if FM3D_RAY_AOS
+                        *(gd2v*)(sl2.RX + 2 * pos) = d2v{ux, uy};
+#else
                         sl2.RX[pos] = ux;
                         sl2.RY[pos] = uy;
+#endif
                         sl2.KI[pos] = e;
                     }
                     base += __popcll(bm);
@@ -1040,7 +1051,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                                 (nev < 2 || (mok1 && 256. * 1.01 * (w1 + wF) < 1e99))));
                     // the slab bases, once per pass (scalar registers; used where FM3D_EVAL_HOIST)
 #ifndef FM3D_EVAL_HOIST
-#define FM3D_EVAL_HOIST 0
+#define FM3D_EVAL_HOIST 1
 #endif
                     struct SlabB {
                         const char *slabRX, *slabRY, *slabI1;
@@ -1082,8 +1093,15 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         auto load = [&](unsigned o8, unsigned o4) {
                             const auto* pc = sb();
                             Ld L;
+#if FM3D_RAY_AOS
+                            // the entry's (ux, uy) record: one 16-byte load (byte offset 2 * o8)
+                            const d2v r = __builtin_nontemporal_load((const gd2v*)(pc->slabRX + 2 * o8));
+                            L.ux = r.x;
+                            L.uy = r.y;
+#else
                             L.ux = __builtin_nontemporal_load((const gdouble*)(pc->slabRX + o8));
                             L.uy = __builtin_nontemporal_load((const gdouble*)(pc->slabRY + o8));
+#endif
                             L.i1 = __builtin_nontemporal_load((const gfloat*)(pc->slabI1 + o4));
                             L.dF = JAC ? (double)__builtin_nontemporal_load((const gfloat*)(pc->slabDF + o4)) : 0.;
                             return L;
