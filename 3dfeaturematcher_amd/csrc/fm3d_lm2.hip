@@ -588,6 +588,35 @@ struct Producer {
         reserve(c);
         write<TWO>(c, t0, t1, slowBits);
     }
+#ifndef FM3D_SLOW_BRANCH
+#define FM3D_SLOW_BRANCH 1
+#endif
+    // The same with the enorm terms t_k = x_k^2 and the raw values v_k: sum k carries v_k where
+    // slow_k (wave-uniform; rare).  FM3D_SLOW_BRANCH: the rows are written with the terms and, in a
+    // branch only a slow chunk takes, overwritten with the raw values, so the common chunk spends
+    // no VALU selects on the rows or the tag (the asm keeps the compiler from turning the branch
+    // back into selects)
+    template <bool TWO = true>
+    __device__ __forceinline__ void write_terms(int c, double t0, double v0, bool slow0, double t1, double v1,
+                                                bool slow1) {
+#if FM3D_SLOW_BRANCH
+        const int pos = c & (kR - 1);
+        double* row0 = &sh->ring[pos][2 * w * kRow];
+        row0[lane] = t0;
+        if (TWO) row0[kRow + lane] = t1;
+        int slowBits = 0;
+        if (slow0 || (TWO && slow1)) {
+            asm volatile("" ::: "memory");
+            if (slow0) row0[lane] = v0;
+            if (TWO && slow1) row0[kRow + lane] = v1;
+            slowBits = (slow0 ? 1 : 0) | ((TWO && slow1) ? 2 : 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the rows before the tag (as write)
+        lds_store_rel(&sh->rowTag[w][pos], (c << 2) | slowBits);
+#else
+        write<TWO>(c, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
+#endif
+    }
 };
 
 typedef __attribute__((address_space(4))) const ProjConst cProjConst;
@@ -1158,7 +1187,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 *(gfloat*)(sb()->slabDJ1 + o4) = dI1;
                                 t1 = enorm_term2(v1, agiant, slow1);
                             }
-                            prod.write<NEV == 2>(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
+                            prod.write_terms<NEV == 2>(cbase + k, t0, v0, slow0, t1, v1, slow1);
                         };
                         // this wave's chunks: k0, k0 + kS, ...; st8 / st4: the offset step between them
                         unsigned o8 = s8 + lane * 8u + (unsigned)k0 * 512u, o4 = o8 >> 1;
@@ -1223,7 +1252,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                     *(gfloat*)(pc->slabDJ0 + oo) = dI0;
                                     *(gfloat*)(pc->slabDJ1 + oo) = dI1;
                                 }
-                                prod.write<true>(cbase + k, slow0 ? v0 : t0, slow1 ? v1 : t1, (slow0 ? 1 : 0) | (slow1 ? 2 : 0));
+                                prod.write_terms<true>(cbase + k, t0, v0, slow0, t1, v1, slow1);
                             };
                             // A stage past the last chunk computes garbage from slab padding (its
                             // entries are not `in`: no failures); no branch between gathers and use
@@ -1315,7 +1344,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 }
                                 bool slow;
                                 const double t = enorm_term2(v, agiant, slow);
-                                prod.write<false>(cbase + kk, slow ? v : t, 0., slow ? 1 : 0);
+                                prod.write_terms<false>(cbase + kk, t, v, slow, 0., 0., false);
                             };
                             // both chunks' values first (no branch between the gathers and their
                             // use), then the ring space, then the stores of the chunks that exist
@@ -1393,7 +1422,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                     }
                                     bool slow;
                                     const double t = enorm_term2(v, agiant, slow);
-                                    prod.write<false>(cbase + kk, slow ? v : t, 0., slow ? 1 : 0);
+                                    prod.write_terms<false>(cbase + kk, t, v, slow, 0., 0., false);
                                 };
                                 back1(gA, a, i1A, dFA, inA, o4, k);
                                 if (two) back1(gB, b, i1B, dFB, inB, o4 + st4, kB);
@@ -1484,8 +1513,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         // EDGE: the first or the last chunk (the diagonal entries 0 and 1, entries
                         // past len); every other chunk skips those tests
                         struct Terms {
-                            double t0, t1;
-                            int slow;
+                            double t0, t1, a;  // a: QR2's raw value, published instead of t0 if slow
+                            bool slow;
                         };
                         auto chunk = [&](const Ld& L, int k, auto edgec) {
                             constexpr bool EDGE = decltype(edgec)::value;
@@ -1525,7 +1554,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 t0 = u * wa;
                                 if (EDGE && !(in && e > 0)) t0 = 0.;
                             }
-                            return Terms{slow ? a : t0, t1, slow ? 1 : 0};
+                            return Terms{t0, t1, a, slow};
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry.  A
                         // buffer is refilled after its chunk is consumed (no register copies)
@@ -1550,7 +1579,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 if (kc < nCh) {
                                     const Terms T = (kc == 0 || kc == nCh - 1) ? chunk(buf[j], kc, std::true_type())
                                                                                : chunk(buf[j], kc, std::false_type());
-                                    prod.put<KIND == Q_QR1>(cbase + kc, T.t0, T.t1, T.slow);
+                                    prod.reserve(cbase + kc);
+                                    prod.write_terms<KIND == Q_QR1>(cbase + kc, T.t0, T.a, T.slow, T.t1, 0., false);
                                     buf[j] = load(o4);
                                 }
                                 o4 += st4;
