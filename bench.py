@@ -193,9 +193,10 @@ def main():
     if rank == 0:
         kp_k = wl["keypoints"] // 1000
         if workload == "c5":
-            desc = (f"C5: one {kp_k}k-keypoint SIFT-128 (u8) 640x480-class frame pair ({wl['width']}x{wl['height']}), "
-                    f"full pipeline, pixelsRay {args.ray}, pyramids {args.levels}, query blocks sharded over "
-                    f"{world} GPU(s), RCCL all-gather of survivor records")
+            desc = (f"C5: one {kp_k}k-keypoint SIFT-128 (u8) frame pair ({wl['width']}x{wl['height']}, sub-pixel "
+                    f"keypoints), full pipeline, pixelsRay {args.ray}, pyramids {args.levels}, " +
+                    (f"query blocks sharded over {world} GPUs, RCCL all-gather of survivor records" if sharded else
+                     "whole on one GPU (the reference point of the N-GPU strong-scaling runs)"))
         else:
             desc = (f"C4: {kp_k}k SIFT-128 (u8) keypoints per {wl['width']}x{wl['height']} frame pair, full "
                     f"pipeline, pixelsRay {args.ray}, pyramids {args.levels}")
