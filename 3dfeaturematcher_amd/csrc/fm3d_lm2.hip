@@ -809,15 +809,36 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
             wasBusy = true;
             // up to two chunks per lane per round, never past the pass's last chunk; every
             // lane runs the same add chain (S_NONE lanes sum zeros they never publish)
+#ifndef FM3D_CHAIN_NB
+#define FM3D_CHAIN_NB 4
+#endif
+#if FM3D_CHAIN_NB == 4
+            // up to four chunks per lane and round: the three further tags read together (relaxed),
+            // then one acquire fence before the rows are read
+            const int tag1 = (have && rem >= 2) ? __hip_atomic_load(&g_sh.rowTag[ss_][(cur + 1) & (kR - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : -1;
+            const int tag2 = (have && rem >= 3) ? __hip_atomic_load(&g_sh.rowTag[ss_][(cur + 2) & (kR - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : -1;
+            const int tag3 = (have && rem >= 4) ? __hip_atomic_load(&g_sh.rowTag[ss_][(cur + 3) & (kR - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : -1;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            int nb = have ? 1 : 0;
+            if (nb == 1 && (tag1 >> 2) == cur + 1) nb = 2;
+            if (nb == 2 && (tag2 >> 2) == cur + 2) nb = 3;
+            if (nb == 3 && (tag3 >> 2) == cur + 3) nb = 4;
+            const int slowm = (tag0 & 3) | ((tag1 & 3) << 2) | ((tag2 & 3) << 4) | ((tag3 & 3) << 6);
+#else
             const int tag1 = (have && rem >= 2) ? lds_load_acq(&g_sh.rowTag[ss_][(cur + 1) & (kR - 1)]) : -1;
             const int nb = have ? (((tag1 >> 2) == cur + 1) ? 2 : 1) : 0;
+#endif
             rounds++;
             chunks += nb;
 #pragma nounroll
-            for (int b = 0; b < 2; b++) {
+            for (int b = 0; b < FM3D_CHAIN_NB; b++) {
                 if (b < nb) {
                     const double* row = &g_sh.ring[cur & (kR - 1)][lane * kRow];
+#if FM3D_CHAIN_NB == 4
+                    const bool slow = ((slowm >> (2 * b + which)) & 1) != 0;
+#else
                     const bool slow = (((b ? tag1 : tag0) >> which) & 1) != 0;
+#endif
                     const double acc0 = acc;
                     acc = chain_sum64(acc, row);
                     // a chunk of raw values (rare): again, with MINPACK's full enorm
