@@ -789,7 +789,20 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
     for (;;) {
         if ((long long)(wall_clock64() - tStart) > maxTicks) break;
         if (!__any(alive)) break;
+#ifndef FM3D_CHAIN_ONETRIP
+#define FM3D_CHAIN_ONETRIP 1
+#endif
+#if FM3D_CHAIN_ONETRIP
+        // the four ring tags of a round in one LDS round trip: relaxed loads, one acquire fence
+        // (the pass descriptor and the rows are read after it); chunks past the pass are cut by rem
+        auto tagRel = [&](int b) {
+            return alive ? __hip_atomic_load(&g_sh.rowTag[ss_][(cur + b) & (kR - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : -1;
+        };
+        const int tag0 = tagRel(0), tg1 = tagRel(1), tg2 = tagRel(2), tg3 = tagRel(3);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
         const int tag0 = alive ? lds_load_acq(&g_sh.rowTag[ss_][cur & (kR - 1)]) : -1;
+#endif
         const bool have = (tag0 >> 2) == cur;
         if (have && !inPass) {
             const PassDesc& d = g_sh.pd[ss_];
@@ -815,10 +828,15 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
 #if FM3D_CHAIN_NB == 4
             // up to four chunks per lane and round: the three further tags read together (relaxed),
             // then one acquire fence before the rows are read
+#if FM3D_CHAIN_ONETRIP
+            const int tag1 = (have && rem >= 2) ? tg1 : -1, tag2 = (have && rem >= 3) ? tg2 : -1;
+            const int tag3 = (have && rem >= 4) ? tg3 : -1;
+#else
             const int tag1 = (have && rem >= 2) ? __hip_atomic_load(&g_sh.rowTag[ss_][(cur + 1) & (kR - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : -1;
             const int tag2 = (have && rem >= 3) ? __hip_atomic_load(&g_sh.rowTag[ss_][(cur + 2) & (kR - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : -1;
             const int tag3 = (have && rem >= 4) ? __hip_atomic_load(&g_sh.rowTag[ss_][(cur + 3) & (kR - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : -1;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
             int nb = have ? 1 : 0;
             if (nb == 1 && (tag1 >> 2) == cur + 1) nb = 2;
             if (nb == 2 && (tag2 >> 2) == cur + 2) nb = 3;
