@@ -8,11 +8,15 @@
  *   #include "Triangulator/singlecameratriangulator.h"  -> class SingleCameraTriangulator
  *   #include "Triangulator/normaloptimizer.h"           -> class NormalOptimizer
  *   #include "Triangulator/neighborhoodsgenerator.h"    -> class NeighborhoodsGenerator
- *   #include "pclvisualizerthread.h" / "tools.h"        -> drawMatches, drawBackProjectedPoints
+ *   #include "pclvisualizerthread.h" / "tools.h"        -> drawMatches, drawBackProjectedPoints,
+ *                                                          pcl::PointCloud / pcl::Normal and the
+ *                                                          view* functions (no-op viewers)
  *
- * Replacing those lines by `#include "fm3d_cv.hpp"` lets main.cpp's call sequence compile unchanged
- * (tests/test_compat_main.py compiles examples/main_dropin.cpp, the same sequence written for this
- * repository, and checks its outputs against the Python mirror of the classes).  The classes keep
+ * Replacing those lines by `#include "fm3d_cv.hpp"` lets the reference main.cpp compile unchanged:
+ * tests/test_compat_main.py::test_reference_main_compiles_with_includes_swapped does exactly that
+ * to /root/reference/main.cpp when it is readable, and compiles examples/main_dropin.cpp (the same
+ * call sequence written for this repository), whose outputs it checks against the Python mirror of
+ * the classes.  The classes keep
  * the reference's names, constructors, method signatures and out-parameter semantics and run the
  * hot path through the C ABI (fm3d.h) on GPU 0:
  *   DescriptorsMatcher        descriptorsmatcher.h:39-111   (ctor :47, compare / crosscompare /
@@ -23,17 +27,18 @@
  *   MOSAIC                    mosaic.h:47-70 (the pipeline as a descriptor extractor)
  *
  * What differs, and why:
- *   - feature detection/description (descriptorsmatcher.cpp:110-115) is upstream of the GPU path
- *     and not built: compareWithNNDR / compare / crosscompare use the keypoints and descriptors the
- *     caller passes in; when they are empty (main.cpp:94 passes empty vectors for the detector to
- *     fill) they are read from the image's feature side files, written by whatever detector the
- *     user runs: <image>.kpts.f32 (N x 2 float32 positions) and <image>.desc.u8 (N x 128 uint8) or
- *     <image>.desc.f32 (N x 128 float32; SURF) -- FeatureOptions.ExtractorType ORB / BRISK / FREAK
+ *   - feature detection/description (descriptorsmatcher.cpp:110-115): when main.cpp:94 passes
+ *     empty vectors, the settings' detector / extractor runs on the GPU (SURF of
+ *     build/settings.yml, fm3d_surf_detect; see fm3d.h for the detector types built); a detector
+ *     without a GPU implementation falls back to the image's feature side files:
+ *     <image>.kpts.f32 (N x 2 float32 positions) and <image>.desc.u8 (N x 128 uint8) or
+ *     <image>.desc.f32 (N x 128 float32) -- FeatureOptions.ExtractorType ORB / BRISK / FREAK
  *     selects Hamming matching on <image>.desc.u8 rows of 32 / 64 bytes (descriptorsmatcher.cpp:64-71);
  *   - the matcher is exact brute force, ties to the lowest train index;
- *   - extractDescriptorsFromPatches needs the SURF extractor and throws fm3d::compat::Error;
- *   - the PCL viewer is visual only: start/stopVisualizerThread are no-ops; drawMatches /
- *     drawBackProjectedPoints draw with plain loops (colors from one seeded generator);
+ *   - extractDescriptorsFromPatches runs the settings' SURF extractor on the GPU;
+ *   - the PCL viewer is visual only: start/stopVisualizerThread and the view* functions are
+ *     no-ops; drawMatches / drawBackProjectedPoints draw with plain loops, in the reference's
+ *     colours (cv::RNG(0xFFF0FF0F), random_color);
  *   - errors throw fm3d::compat::Error where the reference exit()s.
  */
 #ifndef FM3D_CV_HPP
@@ -147,6 +152,26 @@ struct Size {
     Size() {}
     Size(int w, int h) : width(w), height(h) {}
 };
+
+// cv::RNG (OpenCV 2.4 core): multiply-with-carry, next() = the low 32 bits of the new state
+class RNG {
+public:
+    explicit RNG(uint64_t state = 0xffffffffULL) : state_(state ? state : 0xffffffffULL) {}
+    unsigned next() {
+        state_ = (uint64_t)(unsigned)state_ * 4164903690U + (unsigned)(state_ >> 32);
+        return (unsigned)state_;
+    }
+    operator unsigned() { return next(); }
+
+private:
+    uint64_t state_;
+};
+
+// CV_RGB(r, g, b) is Scalar(b, g, r, 0); random_color (tools.cpp:116-120)
+inline Scalar random_color(RNG& rng) {
+    const int color = (int)rng.next();
+    return Scalar((color >> 16) & 255, (color >> 8) & 255, color & 255, 0);
+}
 
 // cv::Mat: 2-D, continuous, reference-counted storage (the element types main.cpp's path uses)
 class Mat {
@@ -820,14 +845,12 @@ inline void drawMatches(const cv::Mat& img1, const cv::Mat& img2, cv::Mat& windo
     auto circle = [&](double x, double y, const cv::Scalar& col) {
         for (int a = 0; a < 64; a++) put((int)std::lround(x + 4 * std::cos(a * M_PI / 32)), (int)std::lround(y + 4 * std::sin(a * M_PI / 32)), col);
     };
-    unsigned long long st = 0xFFF0FF0FULL;  // the reference seeds cv::RNG with this constant
+    // cv::RNG rng(0xFFF0FF0F) and random_color (tools.cpp:116-120, 159-167): the same colour sequence
+    // as the reference, so results/*/image{1,2}pixels.pgm and projectedPatches.pgm colours line up
+    cv::RNG rng(0xFFF0FF0FULL);
     for (size_t i = 0; i < matches.size() && i < outliersMask.size(); i++) {
         if (!outliersMask[i]) continue;
-        cv::Scalar col;
-        for (int k = 0; k < 3; k++) {
-            st = st * 6364136223846793005ULL + 1442695040888963407ULL;
-            col[k] = (double)(st >> 56);
-        }
+        const cv::Scalar col = cv::random_color(rng);
         colors.push_back(col);
         const cv::Point2f p1 = kpts1.at(matches[i].queryIdx).pt, p2 = kpts2.at(matches[i].trainIdx).pt;
         circle(p1.x, p1.y, col);
@@ -851,5 +874,49 @@ inline void drawBackProjectedPoints(const cv::Mat& input, cv::Mat& output, const
             for (int ch = 0; ch < 3; ch++) output.at<cv::uchar>(y, 3 * x + ch) = (cv::uchar)colors[i][ch];
         }
 }
+
+// ---------------------------------------------------------------- PCL stand-ins (visual only)
+// main.cpp:199-217 collects the normals into a pcl::PointCloud<pcl::Normal> and opens a PCL viewer
+// (tools.h:79-91).  The viewer is out of scope: the cloud types hold the data, the
+// view* functions return at once.
+namespace pcl {
+struct Normal {  // pcl::Normal's fields (PCL 1.x point_types.h)
+    float normal_x = 0, normal_y = 0, normal_z = 0, curvature = 0;
+    Normal() {}
+    Normal(float nx, float ny, float nz, float c = 0) : normal_x(nx), normal_y(ny), normal_z(nz), curvature(c) {}
+};
+template <class PointT>
+class PointCloud {
+public:
+    typedef std::shared_ptr<PointCloud<PointT> > Ptr;
+    typedef std::shared_ptr<const PointCloud<PointT> > ConstPtr;
+    std::vector<PointT> points;
+    uint32_t width = 0, height = 1;
+    bool is_dense = true;
+    size_t size() const { return points.size(); }
+    bool empty() const { return points.empty(); }
+    void push_back(const PointT& p) {
+        points.push_back(p);
+        width = (uint32_t)points.size();
+        height = 1;
+    }
+};
+}  // namespace pcl
+
+// tools.h:79-91: the PCL viewers (blocking windows in the reference), no-ops here
+inline void viewPointCloud(const cv::Mat&, const std::vector<cv::Scalar>&) {}
+inline void viewPointCloud(const std::vector<cv::Vec3d>&) {}
+inline void viewPointCloud(const std::vector<cv::Vec3d>&, const cv::Vec3d&) {}
+inline void viewPointCloudAndNormals(const std::vector<cv::Vec3d>&, pcl::PointCloud<pcl::Normal>::ConstPtr,
+                                     const std::vector<cv::Scalar>&) {}
+inline void viewPointCloudNormalsAndFrames(const std::vector<cv::Vec3d>&, pcl::PointCloud<pcl::Normal>::ConstPtr,
+                                           const std::vector<cv::Scalar>&, std::vector<cv::Matx44d>&) {}
+inline void viewPointCloudNeighborhood(const cv::Mat&, std::vector<cv::Mat>&, const std::vector<cv::Scalar>&) {}
+inline void viewPointCloudNormalsFramesAndNeighborhood(const std::vector<std::vector<cv::Vec3d> >&,
+                                                       std::vector<cv::Vec3d>&, const std::vector<cv::Scalar>&,
+                                                       std::vector<cv::Matx44d>&) {}
+inline void viewPointCloudNormalsFramesNeighborhoodAndGravity(const std::vector<std::vector<cv::Vec3d> >&,
+                                                              std::vector<cv::Vec3d>&, const std::vector<cv::Scalar>&,
+                                                              std::vector<cv::Matx44d>&, cv::Vec3d&) {}
 
 #endif  // FM3D_CV_HPP

@@ -128,6 +128,52 @@ def test_dropin_main_compiles_against_cv_standins():
     assert r.returncode != 0 and "Usage" in r.stdout
 
 
+REF_MAIN = "/root/reference/main.cpp"
+
+
+@pytest.mark.skipif(not os.access(REF_MAIN, os.R_OK), reason="the reference tree is not on this machine")
+def test_reference_main_compiles_with_includes_swapped(tmp_path):
+    """north_star's "main.cpp drops in unchanged": the reference's own main.cpp, copied at test time
+    (no reference text is stored in this repository) with only its include block (main.cpp:8-20:
+    lmmin.h, the OpenCV headers, the four class headers, pclvisualizerthread.h, tools.h) replaced by
+    include/fm3d_cv.hpp, compiles with -Wall and links against libfm3d.so; run without arguments it
+    prints the reference's usage line and exits -1 (main.cpp:45-49)."""
+    lines = open(REF_MAIN).read().split("\n")
+    assert lines[7].startswith("#include <lmmin.h>") and lines[19].startswith('#include "tools.h"')
+    src = tmp_path / "main.cpp"
+    src.write_text("\n".join(lines[:7] + ['#include "fm3d_cv.hpp"'] + lines[20:]))
+    exe = tmp_path / "main_ref"
+    libdir = os.path.join(ROOT, "3dfeaturematcher_amd")
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                        "-L" + libdir, "-lfm3d", "-Wl,-rpath," + libdir, "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "warning" not in r.stderr, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 255 and "Usage: 3dfeaturematcher -s <settings.yml>" in r.stdout
+
+
+def test_reference_rng_colours():
+    """drawMatches' colours (tools.cpp:116-120, 159-167): cv::RNG(0xFFF0FF0F) + CV_RGB.  The first
+    15 are the colours of the 15 frames painted in the reference's build/projectedPatches.pgm (RGB
+    order in the file); tests/golden/ref_pins.npz holds them as read from that file."""
+    src = r'''
+#include "fm3d_cv.hpp"
+#include <cstdio>
+int main() { cv::RNG rng(0xFFF0FF0F); for (int i = 0; i < 23; i++) { cv::Scalar c = cv::random_color(rng);
+  std::printf("%d %d %d\n", (int)c[2], (int)c[1], (int)c[0]); } return 0; }
+'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "c.cpp"), "w").write(src)
+        r = subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), os.path.join(d, "c.cpp"), "-o",
+                            os.path.join(d, "c")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        out = subprocess.run([os.path.join(d, "c")], capture_output=True, text=True).stdout.split("\n")
+    rgb = [tuple(int(v) for v in line.split()) for line in out if line]
+    assert rgb[0] == (150, 195, 189) and rgb[14] == (62, 232, 43) and rgb[22] == (172, 160, 148)
+
+
 def test_settings_lookup_filestorage_nodes(fm3d, tmp_path):
     """fm3d_settings_lookup (cv::FileNode of the stand-ins) on the reference's settings layout."""
     import ctypes
