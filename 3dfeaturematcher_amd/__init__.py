@@ -35,7 +35,9 @@ EXPORTS = (
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
     "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
-    "fm3d_ncc_hypotheses",
+    "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
+    "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
+    "fm3d_plane_to_image2",
 )
 
 
@@ -133,6 +135,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         L.fm3d_last_error.restype = ctypes.c_char_p
         L.fm3d_version.restype = ctypes.c_char_p
+        L.fm3d_mgpu_last_error.restype = ctypes.c_char_p
         _LIB = L
     return _LIB
 
@@ -322,6 +325,23 @@ class SingleCameraTriangulator:
         t2 = np.zeros(3)
         self.ctx.check(lib().fm3d_get_camera2(self.ctx.handle, _ptr(R2), _ptr(t2)))
         return R2.reshape(3, 3), t2
+
+    def plane_to_image2(self, X, n):
+        """fm3d_plane_to_image2 (device kernel): extractPixelsContour(X) and the level-0 projection of
+        those pixels through the plane (X, n) into image 2 -- (image-1 pixels (m, 2), image-2 uv
+        (m, 2), status (m,))."""
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        n = np.ascontiguousarray(n, dtype=np.float64)
+        R = self.ctx.settings.pixelsRay
+        cap = (2 * R + 1) ** 2
+        xy = np.zeros((cap, 2))
+        uv = np.zeros((cap, 2))
+        st = np.zeros(cap, dtype=np.int32)
+        m = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_plane_to_image2(self.ctx.handle, _ptr(X), _ptr(n), _ptr(xy), _ptr(uv),
+                                                  _ptr(st, ctypes.c_int32), cap, ctypes.byref(m)))
+        k = m.value
+        return xy[:k], uv[:k], st[:k]
 
     def setKeypoints(self, kpts1: np.ndarray, kpts2: np.ndarray, matches: np.ndarray) -> None:
         """setKeypoints (:145-171): keypoint positions (N, 2) float32 + DMATCH array."""
@@ -531,6 +551,88 @@ class Pipeline:
         self.ctx.check(lib().fm3d_records_download(self.ctx.handle, ctypes.c_void_p(records_dev_ptr or 0), n,
                                                    _vp(out)))
         return out[:n]
+
+
+SHARE_BLOCK = 4096  # queries per block of the block-cyclic partition (fm3d_mgpu, shard.py)
+
+
+def share_queries(n: int, shares: int, s: int, block: int = SHARE_BLOCK) -> np.ndarray:
+    """fm3d_share_queries: global query indices of share s (blocks dealt round-robin)."""
+    cnt = ctypes.c_int(0)
+    _check(lib().fm3d_share_queries(n, shares, s, block, None, 0, ctypes.byref(cnt)))
+    idx = np.zeros(max(cnt.value, 1), dtype=np.int32)
+    _check(lib().fm3d_share_queries(n, shares, s, block, _ptr(idx, ctypes.c_int32), len(idx), ctypes.byref(cnt)))
+    return idx[:cnt.value].astype(np.int64)
+
+
+def merge_shares(parts, n: int, block: int = SHARE_BLOCK) -> np.ndarray:
+    """fm3d_merge_shares (the C++ merge of fm3d_mgpu_pipeline_run, host only): parts[s] = share s's
+    survivor records with local query indices -> all records with global indices, query order."""
+    parts = [np.ascontiguousarray(p, dtype=RECORD) for p in parts]
+    shares = len(parts)
+    ptrs = (ctypes.c_void_p * max(shares, 1))(*[p.ctypes.data for p in parts])
+    counts = np.array([len(p) for p in parts], dtype=np.int32)
+    out = np.zeros(max(int(counts.sum()), 1), dtype=RECORD)
+    k = ctypes.c_int(0)
+    _check(lib().fm3d_merge_shares(n, shares, block, ptrs, _ptr(counts, ctypes.c_int32), _vp(out), ctypes.byref(k)))
+    return out[:k.value]
+
+
+class MultiGPU:
+    """fm3d_mgpu: the whole path over several GPUs in one process -- query
+    blocks dealt round-robin over `shares` logical shares (share s on devices[s % ndev]), frame B
+    and the images replicated, RCCL all-gather of the survivor records, merged in query order."""
+
+    def __init__(self, settings: Settings, devices=(0,), shares: int | None = None, block: int = SHARE_BLOCK):
+        self.settings = settings
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        self.ndev = len(devs)
+        self.shares = shares or self.ndev
+        self._h = ctypes.c_void_p()
+        rc = lib().fm3d_mgpu_create(ctypes.byref(settings), self.ndev, _ptr(devs, ctypes.c_int32), self.shares, block,
+                                    ctypes.byref(self._h))
+        if rc != FM3D_OK:
+            raise Fm3dError(rc, "fm3d_mgpu_create failed (no HIP devices / RCCL?)")
+        self.n_queries = 0
+
+    def check(self, rc):
+        if rc != FM3D_OK:
+            raise Fm3dError(rc, lib().fm3d_mgpu_last_error(self._h).decode(errors="replace"))
+
+    def set_g12(self, g12):
+        self.check(lib().fm3d_mgpu_set_g12(self._h, _ptr(np.ascontiguousarray(g12, dtype=np.float64).ravel())))
+
+    def upload(self, desc_a, desc_b, kp1, kp2, img1, img2, binary=False):
+        a = np.ascontiguousarray(desc_a)
+        b = np.ascontiguousarray(desc_b)
+        k1 = np.ascontiguousarray(kp1, dtype=np.float32)
+        k2 = np.ascontiguousarray(kp2, dtype=np.float32)
+        i1 = np.ascontiguousarray(img1, dtype=np.uint8)
+        i2 = np.ascontiguousarray(img2, dtype=np.uint8)
+        h, w = i1.shape
+        self.n_queries = a.shape[0]
+        self.check(lib().fm3d_mgpu_pipeline_upload(self._h, _vp(a), a.shape[0], _vp(b), b.shape[0], a.shape[1],
+                                                   _desc_type(a, binary), _vp(k1), _vp(k2), _ptr(i1, ctypes.c_uint8),
+                                                   _ptr(i2, ctypes.c_uint8), w, h))
+
+    def run(self):
+        """One pass over all devices: (records in query order, stats dict)."""
+        out = np.zeros(max(self.n_queries, 1), dtype=RECORD)
+        n = ctypes.c_int(0)
+        st = PipelineStats()
+        self.check(lib().fm3d_mgpu_pipeline_run(self._h, _vp(out), ctypes.byref(n), ctypes.byref(st)))
+        return out[:n.value], st.as_dict()
+
+    def close(self):
+        if self._h:
+            lib().fm3d_mgpu_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def g12_from_poses(settings: Settings, T1, T2, r1, r2) -> np.ndarray:

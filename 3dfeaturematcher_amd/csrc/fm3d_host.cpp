@@ -1363,6 +1363,15 @@ int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_
     if (!S.surfUpright) return fail(c, FM3D_ERR_UNSUPPORTED, "SURF Upright 0 (orientation) is not implemented");
     *nOut = 0;
     if (n == 0) return FM3D_OK;
+    // a kept keypoint of size < 7.5 has a window narrower than the 21 x 21 patch: OpenCV resizes it
+    // UP, with INTER_AREA's bilinear emulation, a branch neither the kernel nor the oracle restates
+    for (int q = 0; q < n; q++) {
+        const float sz = kpts[q].size, s = sz * 1.2f / 9.0f;
+        const int gws = 2 * (int)std::lrint(2 * s);
+        if (!(sz >= FLT_EPSILON) || h + 1 < gws || w + 1 < gws) continue;  // dropped anyway
+        if ((int)((20 + 1) * s) < 21)
+            return fail(c, FM3D_ERR_UNSUPPORTED, "SURF compute: keypoint size < 7.5 (OpenCV upscales the window)");
+    }
     hipSetDevice(c->device);
     int r;
     if ((r = surf_upload_image(c, img, w, h))) return r;
@@ -1518,6 +1527,65 @@ int fm3d_neighborhood(fm3d_ctx* c, const double X[3], double* xy, int cap, int* 
                 n++;
             }
     *m = n;
+    return FM3D_OK;
+}
+
+int fm3d_plane_to_image2(fm3d_ctx* c, const double X[3], const double n[3], double* xy, double* uv, int32_t* status,
+                         int cap, int* m) {
+    if (!c || !X || !n || !m || cap < 0) return FM3D_ERR_INVALID;
+    if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "no camera-2 pose: call fm3d_setg12 / fm3d_set_g12 first");
+    hipSetDevice(c->device);
+    int r;
+    if ((r = ensure_offsets(c))) return r;
+    const int N = c->nOff;
+    DevBuf bxy, buv, bkeep, bst;
+    HIPCHK(c, bxy.ensure((size_t)N * 16));
+    HIPCHK(c, buv.ensure((size_t)N * 16));
+    HIPCHK(c, bkeep.ensure((size_t)N * 4));
+    HIPCHK(c, bst.ensure((size_t)N * 4));
+    fm3d::PlaneProjParams p{};
+    p.cam = c->cam;
+    std::memcpy(p.R2, c->R2, sizeof(p.R2));
+    std::memcpy(p.t2, c->t2, sizeof(p.t2));
+    for (int k = 0; k < 3; k++) {
+        p.X[k] = X[k];
+        p.n[k] = n[k];
+    }
+    p.cmax = (double)(int)(2 * c->s.zThresholdMax);
+    p.offsets = c->offsets.as<int2>();
+    p.nOff = N;
+    p.boundW = c->s.boundWidth;
+    p.boundH = c->s.boundHeight;
+    p.w = c->w;  // isPixelGood bounds of the images set with fm3d_set_images (0: none)
+    p.h = c->h;
+    p.xy = bxy.as<double>();
+    p.uv = buv.as<double>();
+    p.keep = bkeep.as<int>();
+    p.status = bst.as<int>();
+    fm3d::launch_plane_project(p, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<double> hxy((size_t)2 * N), huv((size_t)2 * N);
+    std::vector<int> hk(N), hs(N);
+    HIPCHK(c, hipMemcpy(hxy.data(), bxy.p, (size_t)N * 16, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(huv.data(), buv.p, (size_t)N * 16, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(hk.data(), bkeep.p, (size_t)N * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(hs.data(), bst.p, (size_t)N * 4, hipMemcpyDeviceToHost));
+    int k = 0;
+    for (int t = 0; t < N; t++) {
+        if (!hk[t]) continue;
+        if (k < cap) {
+            if (xy) { xy[2 * k] = hxy[2 * t]; xy[2 * k + 1] = hxy[2 * t + 1]; }
+            if (uv) { uv[2 * k] = huv[2 * t]; uv[2 * k + 1] = huv[2 * t + 1]; }
+            if (status) status[k] = hs[t];
+        }
+        k++;
+    }
+    *m = k;
+    bxy.release();
+    buv.release();
+    bkeep.release();
+    bst.release();
     return FM3D_OK;
 }
 

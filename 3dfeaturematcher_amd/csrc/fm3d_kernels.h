@@ -190,6 +190,18 @@ void launch_triangulate(const TriParams& p, hipStream_t s);
 void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s);
 void launch_undistort(const Camera& cam, const double* xy, int n, double* out, hipStream_t s);
 
+// extractPixelsContour + the level-0 geometry of evaluateNormal through a given plane (fm3d_misc.hip)
+struct PlaneProjParams {
+    Camera cam;
+    double R2[9], t2[3], X[3], n[3];
+    double cmax;  // int(2 * zThresholdMax), isInBoundingBox :648
+    const int2* offsets;
+    int nOff, boundW, boundH, w, h;
+    double *xy, *uv;
+    int *keep, *status;
+};
+void launch_plane_project(const PlaneProjParams& p, hipStream_t s);
+
 // ---------------- feature frames + patch export (fm3d_patch.hip) ----------------
 void launch_features_frames(const double* pts, const double* nrm, int P, const double g[3], double* frames,
                             hipStream_t s);

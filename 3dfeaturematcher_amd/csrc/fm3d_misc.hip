@@ -120,6 +120,43 @@ __global__ void undistort_kernel(Camera cam, const double* __restrict__ xy, int 
     undistort1(cam, xy[2 * i], xy[2 * i + 1], out[2 * i], out[2 * i + 1]);
 }
 
+// extractPixelsContour(X) (singlecameratriangulator.cpp:341-397) and, for every kept pixel,
+// get3dPointsFromImage1Pixels (:530-574: undistortPoints, projectPointToPlane :421-470,
+// isInBoundingBox :646-655) + projectPointsToImage2 (:591-626) at scale 1 through the plane (X, n):
+// one thread per circle offset (reference order).  keep[t] = 1 for pixels inside the bound
+// (compacted on the host in offset order), status[t] 0 / 5 NaN plane / 2 bounding box / 4 image-2
+// pixel outside isPixelGood(.., 1.0) of a w x h image (w = 0: not tested).
+__global__ void plane_project_kernel(PlaneProjParams p) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p.nOff) return;
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Z[3] = {0, 0, 0};
+    double cx, cy;
+    project1(p.cam, I, Z, p.X[0], p.X[1], p.X[2], cx, cy);
+    const int2 o = p.offsets[t];
+    const double px = cx + o.x, py = cy + o.y;
+    const int keep = !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+    p.keep[t] = keep;
+    p.xy[2 * t] = px;
+    p.xy[2 * t + 1] = py;
+    if (!keep) return;
+    double ux, uy;
+    undistort1(p.cam, px, py, ux, uy);
+    const double mm = p.n[0] * p.X[0] + p.n[1] * p.X[1] + p.n[2] * p.X[2];
+    const double nn = p.n[0] * ux + p.n[1] * uy + p.n[2] * 1.;
+    const double k = mm / nn;
+    const double P0 = k * ux, P1 = k * uy, P2 = k * 1.;
+    const double cm = p.cmax;
+    int st = 0;
+    if (P0 != P0 || P1 != P1 || P2 != P2) st = 5;
+    else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm))) st = 2;
+    double u, v;
+    project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
+    if (!st && p.w > 0 && !pixel_good(u, v, 1.0, p.w, p.h)) st = 4;
+    p.uv[2 * t] = u;
+    p.uv[2 * t + 1] = v;
+    p.status[t] = st;
+}
+
 // ---------------- stable compaction (three-phase scan) ----------------
 constexpr int kScanBlock = 1024;  // items per block (256 threads x 4)
 
@@ -263,6 +300,10 @@ void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t 
     const int dw = (w + 1) / 2, dh = (h + 1) / 2;
     dim3 blk(32, 8), grd((dw + 31) / 32, (dh + 7) / 8);
     pyrdown_kernel<<<grd, blk, 0, s>>>(src, w, h, dst);
+}
+
+void launch_plane_project(const PlaneProjParams& p, hipStream_t s) {
+    if (p.nOff > 0) plane_project_kernel<<<(p.nOff + 255) / 256, 256, 0, s>>>(p);
 }
 
 void launch_undistort(const Camera& cam, const double* xy, int n, double* out, hipStream_t s) {

@@ -235,9 +235,11 @@ __global__ void keypoint_scatter_kernel(const SurfCand* __restrict__ c, const in
 __global__ void keep_flag_kernel(const fm3d_keypoint* __restrict__ k, int n, int w, int h, int* __restrict__ flag) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
+    // DescriptorExtractor::compute runs KeyPointsFilter::runByKeypointSize(FLT_EPSILON) first
+    // (runByImageBorder(0) removes nothing); then SURFInvoker's drop of wavelets larger than the image
     const float s = k[q].size * 1.2f / 9.0f;
     const int gws = 2 * cv_roundf(2 * s);
-    flag[q] = (h + 1 < gws || w + 1 < gws) ? 0 : 1;
+    flag[q] = (!(k[q].size >= 1.19209290e-07f) || h + 1 < gws || w + 1 < gws) ? 0 : 1;
 }
 __global__ void keep_scatter_kernel(const fm3d_keypoint* __restrict__ k, const int* __restrict__ flag,
                                     const int* __restrict__ pos, int n, fm3d_keypoint* __restrict__ out,

@@ -89,11 +89,7 @@ def merge_gathered(gathered, counts, index_maps=None, by_query: bool = False) ->
     index_maps[r]: rank r's records carry local query indices into index_maps[r] (the
     block-cyclic partition); they are mapped to global ones and ordered by query."""
     rec_dtype = importlib.import_module("3dfeaturematcher_amd").RECORD
-    g = np.ascontiguousarray(gathered.cpu().numpy() if hasattr(gathered, "cpu") else gathered, dtype=np.uint8)
-    c = np.asarray(counts.cpu().numpy() if hasattr(counts, "cpu") else counts).astype(np.int64)
-    cap = g.shape[1]
-    if g.ndim != 3 or g.shape[2] != RECORD_BYTES or (c < 0).any() or (c > cap).any():
-        raise ValueError("gathered record buffers of an unexpected shape or count")
+    g, c = _host_gathered(gathered, counts)
     if index_maps is not None and len(index_maps) != g.shape[0]:
         raise ValueError("one index map per rank")
     parts = []
@@ -109,6 +105,24 @@ def merge_gathered(gathered, counts, index_maps=None, by_query: bool = False) ->
     if index_maps is not None or by_query:
         out = out[np.argsort(out["queryIdx"], kind="stable")]
     return out
+
+
+def _host_gathered(gathered, counts):
+    g = np.ascontiguousarray(gathered.cpu().numpy() if hasattr(gathered, "cpu") else gathered, dtype=np.uint8)
+    c = np.asarray(counts.cpu().numpy() if hasattr(counts, "cpu") else counts).astype(np.int64).reshape(-1)
+    if g.ndim != 3 or g.shape[2] != RECORD_BYTES or len(c) != g.shape[0] or (c < 0).any() or (c > g.shape[1]).any():
+        raise ValueError("gathered record buffers of an unexpected shape or count")
+    return g, c
+
+
+def merge_gathered_shares(gathered, counts, n: int, block: int = BLOCK) -> np.ndarray:
+    """The block-cyclic merge through the C++ merge of the C ABI (fm3d_merge_shares, the code
+    fm3d_mgpu_pipeline_run runs after its RCCL all-gather): rank r's buffer holds its survivor
+    records with local query indices of query_blocks(n, world, r, block)."""
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    g, c = _host_gathered(gathered, counts)
+    parts = [g[r, : c[r]].reshape(-1).view(fm3d.RECORD) for r in range(g.shape[0])]
+    return fm3d.merge_shares(parts, n, block)
 
 
 def gather_records(records: np.ndarray, capacity: int, group=None, device=None) -> np.ndarray:
@@ -179,5 +193,15 @@ def run_sharded(pair, settings, group=None, device=None,
     n = len(pair.desc1)
     idx = query_blocks(n, world, rank, block)
     fn = shard_fn or (lambda p, s, q: run_shard_queries(p, s, q, device=device.index if device is not None else 0))
-    rec = fn(pair, settings, idx)
-    return gather_records(rec, blocks_capacity(n, world, block), group=group, device=device)
+    rec = np.ascontiguousarray(fn(pair, settings, idx))
+    # local query indices on the wire (as fm3d_mgpu exchanges them); the C++ merge maps them back
+    rec["queryIdx"] = np.searchsorted(idx, rec["queryIdx"])
+    cap = blocks_capacity(n, world, block)
+    buf = np.zeros((cap, RECORD_BYTES), dtype=np.uint8)
+    buf[:len(rec)] = rec.view(np.uint8).reshape(len(rec), RECORD_BYTES)
+    import torch
+    mine = torch.from_numpy(buf)
+    if device is not None:
+        mine = mine.to(device)
+    gathered, counts = all_gather_device(mine, len(rec), group=group)
+    return merge_gathered_shares(gathered, counts, n, block)

@@ -174,8 +174,9 @@ def main():
     if dist is None:
         mine = pipe.records(stats[-1]["kept"])
     else:
-        maps = [shard.query_blocks(n, world, r) for r in range(world)] if sharded else None
-        merged = shard.merge_gathered(last["gathered"], last["counts"], index_maps=maps)
+        # the C++ merge of the C ABI (fm3d_merge_shares, as fm3d_mgpu_pipeline_run merges)
+        merged = (shard.merge_gathered_shares(last["gathered"], last["counts"], n) if sharded else
+                  shard.merge_gathered(last["gathered"], last["counts"]))
     download_ms = (time.perf_counter() - t_dl) * 1e3
 
     check = None
@@ -241,6 +242,7 @@ def main():
             out["sharding_check"] = check
         if dist is None:  # bit-identity across builds / boxes (A/B runs compare it)
             out["records_sha256"] = records_digest(mine.tobytes())
+            out.update(verify_against_fixture(args, wl, workload, pair, mine))
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:
@@ -250,6 +252,30 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def verify_against_fixture(args, wl, workload, pair, rec):
+    """The headline run's own correctness proof: for the default C4 workload, the generated inputs'
+    digests and ALL survivor records against the committed oracle run of the same frame pair
+    (tests/golden/full_c4.npz: the CPU oracle in DETMATH mode over every inlier, made in the
+    container by tests/golden/make_full_fixtures.py).  Other workloads: "verified": null."""
+    default = (workload == "c4" and wl == WORKLOADS["c4"] and args.seed == 7 and args.ray == 64 and args.levels == 3)
+    if not default:
+        return {"verified": None, "verified_note": "no committed oracle fixture for this workload"}
+    import importlib.util
+    path = os.path.join(ROOT, "tests", "golden", "make_full_fixtures.py")
+    spec = importlib.util.spec_from_file_location("make_full_fixtures", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    fx = mod.load_fixture("c4")
+    got = mod.input_digests(pair)
+    inputs_ok = all(got[k] == v for k, v in fx["digests"].items())
+    records_ok = rec.tobytes() == fx["records"].tobytes()
+    return {"verified": bool(inputs_ok and records_ok),
+            "verification": {"fixture": "tests/golden/full_c4.npz", "inputs_digest_equal": bool(inputs_ok),
+                             "records_equal": bool(records_ok), "records": int(len(rec)),
+                             "fixture_records": int(len(fx["records"])),
+                             "fixture_records_sha256": str(fx["records_sha256"])}}
 
 
 def check_against_one_gpu(args, fm3d, pair, s, merged, local, rank, dist, torch):

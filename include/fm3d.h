@@ -283,11 +283,50 @@ int fm3d_pipeline_run(fm3d_ctx *ctx, fm3d_record *recordsDev, int *nKept, fm3d_p
 /* copy n records from a device record buffer (NULL = internal) to host */
 int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, fm3d_record *out);
 
+/* ---------------- several GPUs of one node, one process ---------------- */
+/* The reference runs main.cpp:91-155 in one process on one device; these calls are the same
+   pipeline over ndev devices.  The queries split into `shares` logical shares (blocks of `block`
+   queries, 0 = 4096, dealt round-robin; share s runs on devices[s % ndev], shares >= ndev); frame B,
+   its keypoints and both images are replicated to every device; every device runs the whole path
+   on its shares; the survivor counts and 64-byte records are all-gathered with RCCL over xGMI
+   (ncclCommInitAll, ncclAllGather); the host merge (fm3d_merge_shares) returns the records in query
+   order, byte-identical to fm3d_pipeline_run of the whole frame pair.  devices may be NULL (0..ndev-1).
+   FM3D_ERR_UNSUPPORTED when RCCL (librccl.so.1) cannot be loaded. */
+typedef struct fm3d_mgpu fm3d_mgpu;
+int fm3d_mgpu_create(const fm3d_settings *s, int ndev, const int *devices, int shares, int block, fm3d_mgpu **out);
+void fm3d_mgpu_destroy(fm3d_mgpu *m);
+const char *fm3d_mgpu_last_error(const fm3d_mgpu *m);
+/* setg12 result for every device (else each device uses the settings' pos1 / pos2) */
+int fm3d_mgpu_set_g12(fm3d_mgpu *m, const double g12[16]);
+int fm3d_mgpu_pipeline_upload(fm3d_mgpu *m, const void *descA, int nA, const void *descB, int nB, int dim, int type,
+                              const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1,
+                              const uint8_t *img2, int width, int height);
+/* out: host buffer, capacity nA records; stats: counts summed over the shares, total_ms = the
+   slowest device's pipeline time */
+int fm3d_mgpu_pipeline_run(fm3d_mgpu *m, fm3d_record *out, int *nKept, fm3d_pipeline_stats *stats);
+/* the block-cyclic partition: global query indices of share s (increasing); idx NULL asks for *n */
+int fm3d_share_queries(int nA, int shares, int s, int block, int32_t *idx, int cap, int *n);
+/* the merge (host only, no GPU): recs[s] holds counts[s] records of share s with LOCAL query
+   indices (positions in share s's query list, increasing); out (capacity nA) receives them with
+   global indices in query order.  FM3D_ERR_INVALID on a local index outside the share or out of
+   order. */
+int fm3d_merge_shares(int nA, int shares, int block, const fm3d_record *const *recs, const int *counts,
+                      fm3d_record *out, int *nOut);
+
 /* ---------------- building blocks exposed for tests ---------------- */
 /* cv::pyrDown of one 8-bit image (normaloptimizer.cpp:216-217) */
 int fm3d_pyrdown(fm3d_ctx *ctx, const uint8_t *src, int width, int height, uint8_t *dst);
 /* extractPixelsContour(Vec3d) (:376-397): kept pixel coordinates (2*cap doubles), returns m via *m */
 int fm3d_neighborhood(fm3d_ctx *ctx, const double X[3], double *xy, int cap, int *m);
+/* extractPixelsContour(X) (singlecameratriangulator.cpp:341-397) and the level-0 geometry of one
+   evaluateNormal call through the plane (X, n) -- get3dPointsFromImage1Pixels (:530-574) +
+   projectPointsToImage2 (:591-626) at scale 1 -- on the device: what the reference's image2pixels
+   drawing code paints (normaloptimizer.cpp:421-445).  Uses the context's camera, pixelsRay,
+   bounds, zThresholdMax and camera-2 pose.  xy / uv: 2*cap doubles (image-1 pixel, image-2
+   projection), status: cap codes (0, FM3D_ST_NAN_PLANE, FM3D_ST_ABORT_BBOX, FM3D_ST_ABORT_PIX2
+   against the fm3d_set_images size); any may be NULL.  *m = kept pixels (m_dat). */
+int fm3d_plane_to_image2(fm3d_ctx *ctx, const double X[3], const double n[3], double *xy, double *uv, int32_t *status,
+                         int cap, int *m);
 /* cv::undistortPoints of n pixel coordinates (device kernel) */
 int fm3d_undistort(fm3d_ctx *ctx, const double *xy, int n, double *out);
 

@@ -602,6 +602,21 @@ enum {
 };
 /* LM modes (mode bit 2: fm3d_detmath transcendentals instead of libm) */
 enum { ORC_LM_STRICT = 0, ORC_LM_DETMATH = 2 };
+/* lmfit variants (parity-risk study only, tools/parity_risk.py).  The reference calls
+   lmfit's lmmin with the printout callback + lm_princon_struct signature and reads status.info
+   (normaloptimizer.cpp:269-287): the lmfit 3.x API.  The restatement is MINPACK lmdif; where lmfit
+   3.x's published lmmin.c is recalled to differ (not verifiable here: lmfit is not in the image),
+   one mode bit switches to the lmfit form:
+     ORC_LMV_FDFLOOR   forward-difference step MAX(eps*eps, eps*|x|)  (MINPACK: eps*|x|, eps if 0)
+     ORC_LMV_ENORM     lm_enorm thresholds sqrt(DBL_MIN) / sqrt(DBL_MAX) (MINPACK: 3.834e-20 / 1.304e19)
+     ORC_LMV_DWARFEXIT return at once with info 0 when the starting fnorm <= DBL_MIN (lmfit's
+                       "sum of squares below underflow limit"; MINPACK goes on to a Jacobian)
+     ORC_LMV_TOL1E14   ftol = xtol = gtol = 1e-14 (the LM_USERTOL of lmfit builds that use the
+                       hard-coded "x86" constants instead of float.h's 30*DBL_EPSILON)
+   The user-break mapping (evaluate sets *info < 0 -> lmdif returns -> status.info = 11) is the
+   same in both. */
+enum { ORC_LMV_FDFLOOR = 4, ORC_LMV_ENORM = 8, ORC_LMV_DWARFEXIT = 16, ORC_LMV_TOL1E14 = 32 };
+static int orc_lmv_enorm = 0; /* set from the mode before the (parallel) point loop; read-only after */
 
 typedef struct {
     const uint8_t *img[2][8]; /* pyramid levels of image 1 and 2 */
@@ -720,6 +735,51 @@ static int orc_eval(orc_lmdata *D, const double *par, double *fvec)
     return 0;
 }
 
+/* The geometry of one evaluateNormal call without the intensities: image-1 pixels -> undistorted
+   rays -> plane (X, n) -> camera-2 projection at pyramid level 0, i.e. get3dPointsFromImage1Pixels
+   (singlecameratriangulator.cpp:530-574, projectPointToPlane :421-470, isInBoundingBox :646-655)
+   followed by projectPointsToImage2 (:591-626) with scale 1.  This is what the reference's
+   image2pixels drawing code paints (normaloptimizer.cpp:421-445: get3dPointsFromImage1Pixels +
+   projectPointsToImage2(pointGroup, 1.0, ...) at the final normal).  uv: m x 2; status per pixel
+   (0, ORC_ST_NAN_PLANE, ORC_ST_ABORT_BBOX, or ORC_ST_ABORT_PIX2 when w > 0 and the projection
+   fails isPixelGood for a w x h image).  Returns the first non-zero status (the reference stops
+   there), 0 if none. */
+ORC_API int orc_plane_to_image2(const orc_camera *cam, const double R2[9], const double t2[3], const double X[3],
+                                const double n[3], const double *pix, int m, double zmax, int w, int h, double *uv,
+                                int *status)
+{
+    const double cm = (double)(int)(2 * zmax);
+    double mm = n[0] * X[0] + n[1] * X[1] + n[2] * X[2];
+    int i, first = 0;
+    for (i = 0; i < m; i++) {
+        double ux, uy, nn, k, P0, P1, P2;
+        int st = 0;
+        orc_undistort1(cam, pix[2 * i], pix[2 * i + 1], &ux, &uy);
+        nn = n[0] * ux + n[1] * uy + n[2] * 1.;
+        k = mm / nn;
+        P0 = k * ux; P1 = k * uy; P2 = k * 1.;
+        if (P0 != P0 || P1 != P1 || P2 != P2) st = ORC_ST_NAN_PLANE;
+        else if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm))) st = ORC_ST_ABORT_BBOX;
+        orc_project1(cam, R2, t2, P0, P1, P2, &uv[2 * i], &uv[2 * i + 1]);
+        if (!st && w > 0 && !orc_pixel_good(uv[2 * i], uv[2 * i + 1], 1.0, w, h)) st = ORC_ST_ABORT_PIX2;
+        status[i] = st;
+        if (st && !first) first = st;
+    }
+    return first;
+}
+
+/* The patch sample of projectPointsToImage / projectReferencePointsToImageWithFrame
+   (singlecameratriangulator.cpp:737-766, :819-848): 0 where isPixelGood(p, 1.0) fails for a
+   w x h image, else static_cast<uchar>(getBilinearInterpPix32f(img, x, y)) (truncation). */
+ORC_API void orc_sample_points(const uint8_t *img, int w, int h, const double *uv, int n, uint8_t *out)
+{
+    int i;
+    for (i = 0; i < n; i++) {
+        double x = uv[2 * i], y = uv[2 * i + 1];
+        out[i] = orc_pixel_good(x, y, 1.0, w, h) ? (uint8_t)orc_bilinear(img, w, h, (float)x, (float)y) : 0;
+    }
+}
+
 /* ---- MINPACK building blocks (lmfit's lm_enorm/lm_qrfac/lm_lmpar/lm_qrsolv) ---- */
 #define LM_EPSMCH DBL_EPSILON
 #define LM_DWARF DBL_MIN
@@ -727,7 +787,7 @@ static int orc_eval(orc_lmdata *D, const double *par, double *fvec)
 /* enorm: scaled Euclidean norm (MINPACK) */
 static double orc_enorm(int n, const double *x)
 {
-    const double rdwarf = 3.834e-20, rgiant = 1.304e19;
+    const double rdwarf = orc_lmv_enorm ? sqrt(DBL_MIN) : 3.834e-20, rgiant = orc_lmv_enorm ? sqrt(DBL_MAX) : 1.304e19;
     double s1 = 0, s2 = 0, s3 = 0, x1max = 0, x3max = 0, agiant = rgiant / (double)n, xabs, temp;
     int i;
     for (i = 0; i < n; i++) {
@@ -897,7 +957,9 @@ static int orc_jac_qr(orc_lmdata *D, double *x, const double *fvec, double eps,
     for (j = 0; j < 2; j++) {
         double temp = x[j];
         h[j] = eps * fabs(temp);
-        if (h[j] == 0.) h[j] = eps;
+        if (D->mode & ORC_LMV_FDFLOOR) {
+            if (h[j] < eps * eps) h[j] = eps * eps;  /* lmfit: step = MAX(eps*eps, eps*fabs(x)) */
+        } else if (h[j] == 0.) h[j] = eps;
         x[j] = temp + h[j];
         st = orc_eval(D, x, wa4);
         x[j] = temp;
@@ -973,7 +1035,8 @@ static int orc_lmdif(orc_lmdata *D, double *x, double epsfcn, double *fvec, doub
                      double *tmp, int *nfev_out)
 {
     const int n = 2, maxfev = 100 * (2 + 1);
-    const double ftol = 30 * LM_EPSMCH, xtol = 30 * LM_EPSMCH, gtol = 30 * LM_EPSMCH, factor = 100.;
+    const double tol = (D->mode & ORC_LMV_TOL1E14) ? 1e-14 : 30 * LM_EPSMCH;
+    const double ftol = tol, xtol = tol, gtol = tol, factor = 100.;
     const double p1 = 0.1, p5 = 0.5, p25 = 0.25, p75 = 0.75, p0001 = 1.0e-4;
     double eps = sqrt(epsfcn > LM_EPSMCH ? epsfcn : LM_EPSMCH);
     double diag[2], r[4], qtf[2], acnorm[2], wa1[2], wa2[2], wa3[2], sdiag[2], lw[2];
@@ -985,6 +1048,7 @@ static int orc_lmdif(orc_lmdata *D, double *x, double epsfcn, double *fvec, doub
     st = orc_eval(D, x, fvec);
     if (st) { *nfev_out = (int)D->nfev; return -st; }
     fnorm = orc_enorm(D->m, fvec);
+    if ((D->mode & ORC_LMV_DWARFEXIT) && fnorm <= LM_DWARF) { *nfev_out = (int)D->nfev; return 0; }
     for (;;) {
         st = orc_jac_qr(D, x, fvec, eps, fjac, wa4, tmp, r, qtf, acnorm, ipvt);
         if (st) { *nfev_out = (int)D->nfev; return -st; }
@@ -1165,6 +1229,7 @@ ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], cons
     uint8_t *bufs[16] = {0};
     int i, kept = 0, cmax = (int)(2 * zmax);
     if (levels > 7) return -1;
+    orc_lmv_enorm = (mode & ORC_LMV_ENORM) != 0;
     orc_build_pyramid(img1, img2, w, h, levels, &pyr, bufs);
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);

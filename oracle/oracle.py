@@ -165,6 +165,32 @@ def neighborhood(cam, X, ray, bound_w=1024, bound_h=768):
     return out[:n].copy()
 
 
+def plane_to_image2(cam, R2, t2, X, n, pix, zmax=2.4, size=None):
+    """orc_plane_to_image2: image-1 pixels through the plane (X, n) into image 2 at level 0
+    (get3dPointsFromImage1Pixels + projectPointsToImage2): (uv (m, 2), status (m,))."""
+    pix = _f64(pix).reshape(-1, 2)
+    m = pix.shape[0]
+    uv = np.zeros((max(m, 1), 2))
+    st = np.zeros(max(m, 1), dtype=np.int32)
+    w, h = size if size is not None else (0, 0)
+    c = OrcCamera.from_cam(cam)
+    lib().orc_plane_to_image2(ctypes.byref(c), _p(_f64(np.asarray(R2).ravel())), _p(_f64(t2)), _p(_f64(X)), _p(_f64(n)),
+                              _p(pix), ctypes.c_int(m), ctypes.c_double(zmax), ctypes.c_int(w), ctypes.c_int(h), _p(uv),
+                              _p(st, ctypes.c_int))
+    return uv[:m], st[:m]
+
+
+def sample_points(img, uv):
+    """orc_sample_points: the (uchar) bilinear patch sample at each uv (0 where isPixelGood fails)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    uv = _f64(uv).reshape(-1, 2)
+    out = np.zeros(max(len(uv), 1), dtype=np.uint8)
+    lib().orc_sample_points(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _p(uv), ctypes.c_int(len(uv)),
+                            _p(out, ctypes.c_uint8))
+    return out[:len(uv)]
+
+
 def optimize_normals(cam, R2, t2, img1, img2, levels, points, ray, bound_w=1024, bound_h=768,
                      epsfcn=1e-10, zmax=2.4, mode=STRICT, nthreads=0):
     img1 = np.ascontiguousarray(img1, dtype=np.uint8)
@@ -335,6 +361,8 @@ def surf_describe(img, kpts, extended=True):
     m = f(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), kin.ctypes.data_as(ctypes.c_void_p),
           ctypes.c_int(n), ctypes.c_int(1 if extended else 0), kout.ctypes.data_as(ctypes.c_void_p),
           _p(kept, ctypes.c_int), _p(desc, ctypes.c_float))
+    if m < 0:
+        raise ValueError("SURF describe: a keypoint of size < 7.5 (OpenCV upscales its window; not restated)")
     return kout[:m], kept[:m], desc[:m]
 
 

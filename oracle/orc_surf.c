@@ -421,9 +421,13 @@ ORC_API int orc_surf_describe(const uint8_t *img, int w, int h, const orc_kpt *k
         float DXa[400], DYa[400];
         double square_mag = 0;
         float scale;
+        /* DescriptorExtractor::compute: KeyPointsFilter::runByKeypointSize(FLT_EPSILON) first
+           (runByImageBorder with border 0 removes nothing), then the SURFInvoker wavelet drop */
+        if (!(k.size >= FLT_EPSILON)) continue;
         if (h + 1 < gws || w + 1 < gws) continue;
         k.angle = 360.f - 90.f;
         win_size = (int)((20 + 1) * s);
+        if (win_size < 21) return -1; /* OpenCV's INTER_AREA upscale branch: not restated */
         win_offset = -(float)(win_size - 1) / 2;
         start_x = cv_round(k.x + win_offset);
         start_y = cv_round(k.y - win_offset);

@@ -11,7 +11,7 @@ import importlib
 import numpy as np
 import pytest
 
-from conftest import oracle_threads
+from conftest import assert_inputs, full_fixture, oracle_threads
 
 pytestmark = pytest.mark.gpu
 
@@ -525,9 +525,12 @@ def test_c3_orb10k_pipeline(fm3d, orc, synth, ray, k):
     """BASELINE configs[2] (C3): 10k ORB-256 (Hamming) + normals, through the device-resident
     pipeline, in SURVEY.md §8(d)'s two variants: 64x64-pixel neighbourhoods (pixelsRay 32) and
     pixelsRay 64.  Matching and DLT are checked in full; the LM on a seeded random sample of k
-    inliers (the oracle's CPU time bound) bit-exact against the oracle's DETMATH mode: which
-    points survive, and their normals."""
+    inliers bit-exact against the oracle's DETMATH mode run here (which points survive, and their
+    normals), and every survivor record byte for byte against the committed oracle run over ALL
+    inliers (tests/golden/full_c3r<ray>.npz; the generated inputs' digests are checked first)."""
+    mod, fx = full_fixture(f"c3r{ray}")
     fp = synth.make_frame_pair(10_000, seed=102, desc="orb")
+    assert_inputs(mod, fx, fp)
     s = _settings(fm3d, fp.cam, pixelsRay=ray, nndrEpsilon=0.8)
     ctx = fm3d.Context(s)
     try:
@@ -549,6 +552,8 @@ def test_c3_orb10k_pipeline(fm3d, orc, synth, ray, k):
     assert (np.diff(rec["queryIdx"]) > 0).all() and np.array_equal(q[mask][pos], rec["queryIdx"])
     assert np.array_equal(rec["trainIdx"], t[mask][pos]) and np.array_equal(rec["distance"], d[mask][pos])
     assert np.array_equal(rec["point"], pts[pos])
+    # every survivor record against the oracle's DETMATH run over all inliers (full_c3r<ray>.npz)
+    assert rec.tobytes() == fx["records"].tobytes()
     sel = np.sort(np.random.default_rng(1000 + ray).choice(len(pts), k, replace=False))
     ref = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, 3, pts[sel], ray, mode=orc.DETMATH,
                                nthreads=oracle_threads())
@@ -673,11 +678,15 @@ def test_c4_sift100k_full_pipeline(fm3d, orc, synth):
       * NNDR: every one of the 100k queries (the oracle's NNDR on the GPU's knn lists);
       * DLT: all matches, inlier mask and points bit-exact;
       * records: every survivor's (queryIdx, trainIdx, distance, point) equal to its match / point;
-      * LM: a seeded random 128-point sample of the inliers bit-exact against the oracle's
-        DETMATH mode (statuses and normals), and against libm (STRICT): same statuses, normals
+      * the whole result: the generated inputs' digests equal the fixture's, then ALL 36,151
+        survivor records byte for byte against the oracle's DETMATH run over all 71,223 inliers
+        (tests/golden/full_c4.npz, made by tests/golden/make_full_fixtures.py in the container);
+      * LM vs libm (STRICT) on a seeded random 128-point sample: same statuses, normals
         within 1e-4 for >= 99 % of the kept points (tools/parity_risk.py measures 0.2 % beyond
         1e-4 at these settings: 1-ulp transcendental differences amplified by the LM)."""
+    mod, fx = full_fixture("c4")
     fp = synth.make_frame_pair(100_000, 640, 480, seed=7)
+    assert_inputs(mod, fx, fp)
     s = _settings(fm3d, fp.cam, pixelsRay=64, pyramids=3)
     ctx = fm3d.Context(s)
     try:
@@ -710,18 +719,19 @@ def test_c4_sift100k_full_pipeline(fm3d, orc, synth):
     assert (np.diff(rec["queryIdx"]) > 0).all() and np.array_equal(q[mask][pos], rec["queryIdx"])
     assert np.array_equal(rec["trainIdx"], t[mask][pos]) and np.array_equal(rec["distance"], d[mask][pos])
     assert np.array_equal(rec["point"], pts[pos])
-    # LM on a seeded random sample of the inliers
+    # EVERY survivor record (all 71,223 inliers through the LM) byte for byte against the oracle's
+    # DETMATH run of the whole frame pair (tests/golden/full_c4.npz)
+    assert n == len(fx["records"]) and tuple(fx["counts"]) == (100_000, stats["matches"], stats["inliers"], n)
+    assert rec.tobytes() == fx["records"].tobytes()
+    assert mod.records_digest(rec) == str(fx["records_sha256"])
+    # libm (STRICT) on a seeded random sample of the inliers
     sel = np.sort(rng.choice(len(pts), 128, replace=False))
-    ref = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, 3, pts[sel], 64, mode=orc.DETMATH,
-                               nthreads=oracle_threads())
-    ok = ref["status"] == 0
     kept_sel = np.isin(sel, pos)
-    assert np.array_equal(kept_sel, ok)
+    ok = kept_sel
     got = rec[np.isin(pos, sel)]
-    assert np.array_equal(got["normal"], ref["normals"][ok])
     strict = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, 3, pts[sel], 64, mode=orc.STRICT,
                                   nthreads=oracle_threads())
-    assert np.array_equal(strict["status"], ref["status"])
+    assert np.array_equal(strict["status"] == 0, kept_sel)
     dev = np.abs(got["normal"] - strict["normals"][ok]).max(axis=1)
     print(f"C4 LM sample: {ok.sum()} of 128 kept; max |n - n_libm| {dev.max():.3g}, "
           f"{int((dev > 1e-4).sum())} beyond 1e-4")
@@ -760,3 +770,36 @@ def test_c5_1m_keypoints_query_blocks(fm3d, orc, synth):
     assert np.array_equal(sub["point"], pts[ok])
     assert np.array_equal(sub["normal"], ref["normals"][ok])
     assert ok.sum() > 500
+
+
+# ---------------------------------------------------------------- multi-GPU behind the C ABI (fm3d_mgpu)
+@pytest.mark.parametrize("n,block,shares", [(3000, 256, 4), (20_000, 4096, 4), (5, 4096, 4)])
+def test_mgpu_one_device_shares_equal_pipeline_run(fm3d, synth, n, block, shares):
+    """fm3d_mgpu with an ndev = 1 RCCL communicator and `shares` logical shares
+    (block-cyclic query blocks, run one after the other on the device, records written into the
+    all-gather send buffer, ncclAllGather, C++ merge): byte-identical to fm3d_pipeline_run of the
+    whole frame pair.  (5 queries: three of the four shares are empty.)"""
+    pair = synth.make_frame_pair(n, seed=31)
+    s = _settings(fm3d, pair.cam, pixelsRay=12, pyramids=1)
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(pair.g12)
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+        k, st = pipe.run()
+        full = pipe.records(k)
+    finally:
+        ctx.close()
+    mg = fm3d.MultiGPU(s, devices=[0], shares=shares, block=block)
+    try:
+        mg.set_g12(pair.g12)
+        mg.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+        rec, mst = mg.run()
+        rec2, _ = mg.run()  # re-run on the staged inputs
+    finally:
+        mg.close()
+    assert rec.tobytes() == full.tobytes() and rec2.tobytes() == full.tobytes()
+    assert mst["kept"] == k and mst["matches"] == st["matches"] and mst["inliers"] == st["inliers"]
+    if n >= 3000:
+        assert k > 50

@@ -84,6 +84,36 @@ def test_surf_compute_given_keypoints(fm3d, orc, synth):
     assert np.array_equal(d, do)
 
 
+def test_surf_compute_size_filter_and_outside_centres(fm3d, orc, synth):
+    """ADVICE r02: DescriptorExtractor::compute first drops keypoints of size < FLT_EPSILON
+    (KeyPointsFilter::runByKeypointSize; runByImageBorder with border 0 removes nothing), so size 0
+    and negative sizes disappear; centres outside the image keep their border-replicated window;
+    a kept keypoint of size < 7.5 (window narrower than 21 pixels, which OpenCV resizes UP) is
+    FM3D_ERR_UNSUPPORTED on the GPU and an error in the oracle, not a silent wrong descriptor."""
+    img = synth.make_frame_pair(300, seed=8).img1
+    kin = np.zeros(6, dtype=fm3d.KEYPOINT)
+    kin["x"] = [100.0, -20.0, 700.0, 320.0, 50.0, 320.0]
+    kin["y"] = [100.0, 240.0, 500.0, -5.5, 60.0, 240.0]
+    kin["size"] = [0.0, 24.0, 31.0, 18.0, -3.0, 1e-9]
+    kin["angle"] = -1
+    ctx, _ = _ctx(fm3d)
+    try:
+        k, kept, d = fm3d.SURF(ctx).compute(img, kin)
+        small = kin[[1]].copy()
+        small["size"] = 4.0
+        with pytest.raises(fm3d.Fm3dError) as e:
+            fm3d.SURF(ctx).compute(img, small)
+        assert e.value.code == fm3d.ERR_UNSUPPORTED
+    finally:
+        ctx.close()
+    ko, kepto, do = orc.surf_describe(img, kin, extended=True)
+    assert list(kept) == [1, 2, 3] and np.array_equal(kept, kepto)
+    _same_kpts(k, ko)
+    assert np.array_equal(d, do)
+    with pytest.raises(ValueError):
+        orc.surf_describe(img, small, extended=True)
+
+
 def test_extract_descriptors_from_patches(fm3d, orc, synth):
     """extractDescriptorsFromPatches (descriptorsmatcher.cpp:133-174) on the exported 128x128
     normal-rectified patches: one keypoint at (64, 64) of size 128 per patch."""

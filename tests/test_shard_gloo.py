@@ -168,3 +168,51 @@ def test_merge_gathered_ragged_counts(fm3d):
     with pytest.raises(ValueError):
         shard.merge_gathered(g, np.array([7, 0, 0, 0]))
     assert shard.shard_capacity(10, 4) == 3 and shard.shard_capacity(0, 2) == 1
+
+
+def test_share_queries_cpp_equals_query_blocks(fm3d):
+    """fm3d_share_queries (the C ABI's block-cyclic partition) == shard.query_blocks."""
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    for n in (0, 1, 4095, 4097, 100_000):
+        for w in (1, 2, 3, 8):
+            for block in (1, 32, 4096):
+                for r in range(w):
+                    assert np.array_equal(fm3d.share_queries(n, w, r, block), shard.query_blocks(n, w, r, block))
+
+
+def test_merge_shares_cpp_on_fabricated_buffers(fm3d):
+    """fm3d_merge_shares (the C++ merge behind fm3d_mgpu_pipeline_run and bench.py's C5 step) on
+    fabricated per-share record buffers with local query indices: equal to the single-run list
+    (global indices, query order), whatever the shares' ragged counts; bad local indices raise."""
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    rng = np.random.default_rng(7)
+    for n, w, block in ((50, 3, 4), (10_000, 8, 64), (9_000, 4, 4096), (5, 4, 4096)):
+        full = np.zeros(min(n, 37 + n // 5), dtype=fm3d.RECORD)
+        full["queryIdx"] = np.sort(rng.choice(n, len(full), replace=False))
+        full["trainIdx"] = rng.integers(0, 1 << 20, len(full))
+        full["distance"] = rng.random(len(full)).astype(np.float32)
+        full["point"] = rng.normal(size=(len(full), 3))
+        full["normal"] = rng.normal(size=(len(full), 3))
+        cap = shard.blocks_capacity(n, w, block)
+        g = rng.integers(0, 256, (w, cap, shard.RECORD_BYTES), dtype=np.uint8)  # stale bytes past the counts
+        counts = []
+        for r in range(w):
+            m = shard.query_blocks(n, w, r, block)
+            mine = full[np.isin(full["queryIdx"], m)].copy()
+            mine["queryIdx"] = np.searchsorted(m, mine["queryIdx"])
+            g[r, :len(mine)] = mine.view(np.uint8).reshape(len(mine), shard.RECORD_BYTES)
+            counts.append(len(mine))
+        merged = shard.merge_gathered_shares(g, np.array(counts, dtype=np.int32), n, block)
+        assert merged.tobytes() == full.tobytes()
+        maps = [shard.query_blocks(n, w, r, block) for r in range(w)]
+        assert shard.merge_gathered(g, np.array(counts, dtype=np.int32), index_maps=maps).tobytes() == full.tobytes()
+    # a local index past the share's query count, or out of order, is an error of the C ABI
+    bad = np.zeros(2, dtype=fm3d.RECORD)
+    bad["queryIdx"] = [0, 10_000]
+    with pytest.raises(fm3d.Fm3dError):
+        fm3d.merge_shares([bad, bad[:0]], 100, 32)
+    bad["queryIdx"] = [3, 1]
+    with pytest.raises(fm3d.Fm3dError):
+        fm3d.merge_shares([bad, bad[:0]], 100, 32)
+    with pytest.raises(ValueError):
+        shard.merge_gathered_shares(np.zeros((2, 3), dtype=np.uint8), np.zeros(2), 10)

@@ -10,7 +10,12 @@ plausibly introduce, and compared with the unperturbed run:
   * t2 moved by one ulp (each component up; each component down);
   * fx moved by one ulp (undistortion of the neighbourhood pixels and the camera-2
     projection: the inputs of every bilinear sample coordinate);
-  * the deterministic transcendentals of the GPU (DETMATH) instead of libm.
+  * the deterministic transcendentals of the GPU (DETMATH) instead of libm;
+  * lmfit 3.x's lmmin where it is recalled to differ from the MINPACK lmdif the oracle restates
+    (oracle/fm3d_oracle.c ORC_LMV_*): the forward-difference step floor
+    MAX(eps^2, eps|x|), lm_enorm's sqrt(DBL_MIN) / sqrt(DBL_MAX) thresholds, the early return on a
+    starting fnorm <= DBL_MIN, all three together (the lmfit 3.x set), and the 1e-14 tolerances of
+    lmfit builds with the hard-coded "x86" constants.
 
 For each variant: the fraction of points whose keep/drop status changes, and among the points
 kept by both, the fraction whose normal moves by more than 1e-4 (and 1e-6), plus the largest
@@ -69,7 +74,7 @@ def main():
     ap.add_argument("--points", type=int, default=1000)
     ap.add_argument("--threads", type=int, default=len(os.sched_getaffinity(0)))
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02_parity_risk.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03_parity_risk.json"))
     args = ap.parse_args()
     synth = importlib.import_module("3dfeaturematcher_amd.synth")
     pair = synth.make_frame_pair(100_000, 640, 480, seed=args.seed)  # the C4 bench frame pair
@@ -86,6 +91,8 @@ def main():
     U, _, Vt = np.linalg.svd(R)
     R2svd = orc.rodrigues_v2m(m2v_no_polar(U @ Vt))
 
+    LMV_FDFLOOR, LMV_ENORM, LMV_DWARFEXIT, LMV_TOL1E14 = 4, 8, 16, 32  # fm3d_oracle.c ORC_LMV_*
+
     def run(cam=pair.cam, R2_=R2, t2_=t2, mode=orc.STRICT):
         return orc.optimize_normals(cam, R2_, t2_, pair.img1, pair.img2, 3, P, 64, mode=mode,
                                     nthreads=args.threads)
@@ -99,6 +106,11 @@ def main():
         "t2_minus_1ulp": run(t2_=np.nextafter(t2, -np.inf)),
         "fx_plus_1ulp": run(cam=cam_fx),
         "detmath_vs_libm": run(mode=orc.DETMATH),
+        "lmfit_fd_step_floor": run(mode=orc.STRICT | LMV_FDFLOOR),
+        "lmfit_enorm_thresholds": run(mode=orc.STRICT | LMV_ENORM),
+        "lmfit_dwarf_exit": run(mode=orc.STRICT | LMV_DWARFEXIT),
+        "lmfit3_all_three": run(mode=orc.STRICT | LMV_FDFLOOR | LMV_ENORM | LMV_DWARFEXIT),
+        "lmfit_tol_1e-14": run(mode=orc.STRICT | LMV_TOL1E14),
     }
     out = {
         "workload": "C4 frame pair (100k SIFT, 640x480, seed %d), pixelsRay 64, pyramids 3, oracle STRICT" % args.seed,
