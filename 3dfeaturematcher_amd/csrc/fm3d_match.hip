@@ -610,15 +610,15 @@ int knn2_u8_parts(int nA, int nB, int nCU) {
     // the extra staging of more, shorter blocks costs more than the balance gains).  Then aim at
     // four blocks per CU, each part keeping >= 4 tiles: at 10k x 10k (79 query blocks) 16 parts
     // take the u8 kernel 63 -> 29 us and the bits kernel 56 -> 43 us (rocprofv3, MI355X).
-    // FM3D_I8_PARTS overrides (tuning).
-    static const int forced = [] {
-        const char* e = getenv("FM3D_I8_PARTS");
-        return e ? atoi(e) : 0;
-    }();
+    // FM3D_I8_PARTS overrides the part count (a tuning-only knob, read on every call so A/B runs in
+    // one process see changes); it is clamped to [1, tiles] and ignored when the query blocks
+    // already fill the CUs.
+    const char* e = getenv("FM3D_I8_PARTS");
+    const int forced = e ? atoi(e) : 0;
     const int nBlk = (nA + kQ - 1) / kQ;
     const int nTiles = (nB + kT - 1) / kT;
-    if (forced > 0) return forced;
     if (nBlk <= 0 || nCU <= 0 || nBlk >= nCU) return 1;
+    if (forced > 0) return forced < (nTiles > 1 ? nTiles : 1) ? forced : (nTiles > 1 ? nTiles : 1);
     int p = (4 * nCU + nBlk - 1) / nBlk;
     if (p > 16) p = 16;
     while (p > 1 && nTiles / p < 4) p--;

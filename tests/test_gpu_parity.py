@@ -803,3 +803,22 @@ def test_mgpu_one_device_shares_equal_pipeline_run(fm3d, synth, n, block, shares
     assert mst["kept"] == k and mst["matches"] == st["matches"] and mst["inliers"] == st["inliers"]
     if n >= 3000:
         assert k > 50
+
+
+def test_principal_point_limit(fm3d, pair):
+    """a principal point on or outside the image's top/left edge (cx or cy < 1e-3) is
+    an explicit FM3D_ERR_UNSUPPORTED of computeOptimizedNormals, not a wrong
+    result."""
+    s = _settings(fm3d, pair.cam, pixelsRay=8)
+    s.Cx = 0.0
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(pair.g12)
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(pair.img1, pair.img2)
+        with pytest.raises(fm3d.Fm3dError) as e:
+            no.computeOptimizedNormals(np.array([[0.1, 0.1, 2.0]]))
+        assert e.value.code == fm3d.ERR_UNSUPPORTED
+    finally:
+        ctx.close()

@@ -26,6 +26,7 @@ from conftest import ROOT
 
 PINS = os.path.join(ROOT, "tests", "golden", "ref_pins.npz")
 W, H, RAY = 1024, 768, 64
+pytestmark = pytest.mark.skipif(not os.path.exists(PINS), reason="tests/golden/ref_pins.npz not generated yet")
 
 
 class Cam:
