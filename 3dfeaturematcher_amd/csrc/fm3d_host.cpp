@@ -75,7 +75,7 @@ struct fm3d_ctx {
     DevBuf A8, B8;            // binary rows unpacked to int8 for the MFMA matcher
     // SURF detection / description
     DevBuf sfImg, sfSum, sfDet, sfTr, sfLayers, sfMids, sfCand, sfCount, sfSortTmp, sfFlag, sfPos, sfKp, sfKin, sfSrc,
-        sfDesc, sfDW;
+        sfDesc, sfDW, sfAng;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     int nCU = 0;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
@@ -702,6 +702,33 @@ std::vector<float> surf_dw() {
     return dw;
 }
 
+// SURFInvoker's orientation samples (the constructor's apt / aptw): the disc of radius 6, i (x)
+// outer, j (y) inner, weights G(i) * G(j), G = getGaussianKernel(13, 2.5, CV_32F)
+const fm3d::SurfOri& surf_ori() {
+    static const fm3d::SurfOri ori = [] {
+        fm3d::SurfOri o{};
+        float g[13];
+        const double scale2X = -0.5 / (2.5 * 2.5);
+        double sum = 0;
+        for (int i = 0; i < 13; i++) {
+            const double x = i - (13 - 1) * 0.5;
+            g[i] = (float)std::exp(scale2X * x * x);
+            sum += g[i];
+        }
+        sum = 1. / sum;
+        for (int i = 0; i < 13; i++) g[i] = (float)(g[i] * sum);
+        for (int i = -6; i <= 6; i++)
+            for (int j = -6; j <= 6; j++)
+                if (i * i + j * j <= 36) {
+                    o.ax[o.n] = i;
+                    o.ay[o.n] = j;
+                    o.w[o.n++] = g[i + 6] * g[j + 6];
+                }
+        return o;
+    }();
+    return ori;
+}
+
 int surf_upload_image(fm3d_ctx* c, const uint8_t* img, int w, int h) {
     HIPCHK(c, c->sfImg.ensure((size_t)w * h));
     HIPCHK(c, hipMemcpyAsync(c->sfImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
@@ -760,7 +787,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->slab, &c->slabI1,
                       &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->A8, &c->B8,
                       &c->sfImg, &c->sfSum, &c->sfDet, &c->sfTr, &c->sfLayers, &c->sfMids, &c->sfCand, &c->sfCount,
-                      &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW};
+                      &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW, &c->sfAng};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();
@@ -1289,7 +1316,6 @@ int fm3d_surf_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoin
     const fm3d_settings& S = c->s;
     if (S.detectorType != FM3D_FEAT_SURF || (desc && S.extractorType != FM3D_FEAT_SURF))
         return fail(c, FM3D_ERR_UNSUPPORTED, "only the STATIC SURF detector / extractor runs on the GPU");
-    if (!S.surfUpright) return fail(c, FM3D_ERR_UNSUPPORTED, "SURF Upright 0 (orientation) is not implemented");
     if (S.surfOctaves < 1 || S.surfOctaveLayers < 1 || S.surfHessianThreshold < 0)
         return fail(c, FM3D_ERR_INVALID, "SURF NumOctaves / NumOctaveLayers / HessianThreshold out of range");
     hipSetDevice(c->device);
@@ -1330,9 +1356,16 @@ int fm3d_surf_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoin
     HIPCHK(c, c->sfKp.ensure((size_t)(nc + 1) * sizeof(fm3d_keypoint)));
     int nk = 0;
     if (nc > 0) {
+        const float* ang = nullptr;
+        if (!S.surfUpright) {  // SURFInvoker's orientation; keypoints without a sample are removed
+            HIPCHK(c, c->sfAng.ensure((size_t)(nc + 1) * sizeof(float)));
+            fm3d::launch_surf_orient(c->sfCand.p, sizeof(fm3d::SurfCand), nc, c->sfSum.as<int>(), 0, w, h, surf_ori(),
+                                     c->sfFlag.as<int>(), c->sfAng.as<float>(), c->stream);
+            ang = c->sfAng.as<float>();
+        }
         fm3d::launch_surf_upright(c->sfCand.as<fm3d::SurfCand>(), c->sfCount.as<int>(), nc, w, h, c->sfFlag.as<int>(),
                                   c->sfPos.as<int>(), c->count.as<int>(), c->scanTmp.p, c->sfKp.as<fm3d_keypoint>(),
-                                  nullptr, c->stream);
+                                  nullptr, ang, c->stream);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1342,7 +1375,7 @@ int fm3d_surf_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoin
     if (desc && nw > 0) {
         HIPCHK(c, c->sfDesc.ensure((size_t)nw * dsize * sizeof(float)));
         fm3d::launch_surf_describe(c->sfImg.as<uint8_t>(), 0, w, h, c->sfKp.as<fm3d_keypoint>(), nw, c->sfDW.as<float>(),
-                                   S.surfExtended, c->sfDesc.as<float>(), c->stream);
+                                   S.surfExtended, S.surfUpright, c->sfDesc.as<float>(), c->stream);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(desc, c->sfDesc.p, (size_t)nw * dsize * sizeof(float), hipMemcpyDeviceToHost,
                                  c->stream));
@@ -1360,7 +1393,6 @@ int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_
         return FM3D_ERR_INVALID;
     const fm3d_settings& S = c->s;
     if (S.extractorType != FM3D_FEAT_SURF) return fail(c, FM3D_ERR_UNSUPPORTED, "only the SURF extractor runs on the GPU");
-    if (!S.surfUpright) return fail(c, FM3D_ERR_UNSUPPORTED, "SURF Upright 0 (orientation) is not implemented");
     *nOut = 0;
     if (n == 0) return FM3D_OK;
     // a kept keypoint of size < 7.5 has a window narrower than the 21 x 21 patch: OpenCV resizes it
@@ -1382,8 +1414,18 @@ int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_
     HIPCHK(c, c->sfPos.ensure((size_t)(n + 1) * sizeof(int)));
     HIPCHK(c, c->sfSrc.ensure((size_t)(n + 1) * sizeof(int)));
     HIPCHK(c, hipMemcpyAsync(c->sfKin.p, kpts, (size_t)n * sizeof(fm3d_keypoint), hipMemcpyHostToDevice, c->stream));
+    const float* ang = nullptr;
+    if (!S.surfUpright) {  // the orientation needs the integral image (SURF::operator() computes it)
+        HIPCHK(c, c->sfSum.ensure((size_t)(w + 1) * (h + 1) * sizeof(int)));
+        HIPCHK(c, c->sfAng.ensure((size_t)(n + 1) * sizeof(float)));
+        fm3d::launch_integral(c->sfImg.as<uint8_t>(), w, h, c->sfSum.as<int>(), c->stream);
+        fm3d::launch_surf_orient(c->sfKin.p, sizeof(fm3d_keypoint), n, c->sfSum.as<int>(), 0, w, h, surf_ori(),
+                                 c->sfFlag.as<int>(), c->sfAng.as<float>(), c->stream);
+        ang = c->sfAng.as<float>();
+    }
     fm3d::launch_surf_keep(c->sfKin.as<fm3d_keypoint>(), n, w, h, c->sfFlag.as<int>(), c->sfPos.as<int>(),
-                           c->count.as<int>(), c->scanTmp.p, c->sfKp.as<fm3d_keypoint>(), c->sfSrc.as<int>(), c->stream);
+                           c->count.as<int>(), c->scanTmp.p, c->sfKp.as<fm3d_keypoint>(), c->sfSrc.as<int>(), ang,
+                           c->stream);
     HIPCHK(c, hipGetLastError());
     int nk = 0;
     HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1392,7 +1434,7 @@ int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_
     if (nk > 0) {
         HIPCHK(c, c->sfDesc.ensure((size_t)nk * dsize * sizeof(float)));
         fm3d::launch_surf_describe(c->sfImg.as<uint8_t>(), 0, w, h, c->sfKp.as<fm3d_keypoint>(), nk, c->sfDW.as<float>(),
-                                   S.surfExtended, c->sfDesc.as<float>(), c->stream);
+                                   S.surfExtended, S.surfUpright, c->sfDesc.as<float>(), c->stream);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(desc, c->sfDesc.p, (size_t)nk * dsize * sizeof(float), hipMemcpyDeviceToHost,
                                  c->stream));
@@ -1409,7 +1451,6 @@ int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, i
     if (!c || P < 0 || size <= 0 || (P && (!patches || !desc))) return FM3D_ERR_INVALID;
     const fm3d_settings& S = c->s;
     if (S.extractorType != FM3D_FEAT_SURF) return fail(c, FM3D_ERR_UNSUPPORTED, "only the SURF extractor runs on the GPU");
-    if (!S.surfUpright) return fail(c, FM3D_ERR_UNSUPPORTED, "SURF Upright 0 (orientation) is not implemented");
     if (P == 0) return FM3D_OK;
     // descriptorsmatcher.cpp:146-158: one keypoint per patch at (center, center), center =
     // (int)floor(size / 2), size = the patch edge, angle -1, response 1, octave 0, class_id 0
@@ -1418,7 +1459,7 @@ int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, i
     const float s = k.size * 1.2f / 9.0f;
     const int gws = 2 * cv_round_h(2 * s);
     if (size + 1 < gws) return fail(c, FM3D_ERR_INVALID, "patch keypoint dropped by SURF (descriptor row missing)");
-    k.angle = 360.f - 90.f;
+    if (S.surfUpright) k.angle = 360.f - 90.f;
     hipSetDevice(c->device);
     const size_t per = (size_t)size * size;
     const int dsize = S.surfExtended ? 128 : 64;
@@ -1428,6 +1469,32 @@ int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, i
     HIPCHK(c, c->sfDesc.ensure((size_t)P * dsize * sizeof(float)));
     HIPCHK(c, hipMemcpyAsync(c->sfImg.p, patches, (size_t)P * per, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->sfKp.p, kp.data(), kp.size() * sizeof(fm3d_keypoint), hipMemcpyHostToDevice, c->stream));
+    if (!S.surfUpright) {
+        // every patch keypoint's orientation on that patch's integral image; a patch whose keypoint
+        // has no orientation sample would lose its descriptor row (never for the centred keypoint
+        // of a patch this size, but checked)
+        const int r = ensure_scan_tmp(c, P);
+        if (r) return r;
+        const size_t sumPer = (size_t)(size + 1) * (size + 1);
+        HIPCHK(c, c->sfSum.ensure((size_t)P * sumPer * sizeof(int)));
+        HIPCHK(c, c->sfAng.ensure((size_t)(P + 1) * sizeof(float)));
+        HIPCHK(c, c->sfFlag.ensure((size_t)(P + 1) * sizeof(int)));
+        HIPCHK(c, c->sfPos.ensure((size_t)(P + 1) * sizeof(int)));
+        HIPCHK(c, c->sfKin.ensure((size_t)P * sizeof(fm3d_keypoint)));
+        HIPCHK(c, hipMemcpyAsync(c->sfKin.p, kp.data(), kp.size() * sizeof(fm3d_keypoint), hipMemcpyHostToDevice,
+                                 c->stream));
+        fm3d::launch_integral_batch(c->sfImg.as<uint8_t>(), size, size, P, c->sfSum.as<int>(), c->stream);
+        fm3d::launch_surf_orient(c->sfKin.p, sizeof(fm3d_keypoint), P, c->sfSum.as<int>(), sumPer, size, size,
+                                 surf_ori(), c->sfFlag.as<int>(), c->sfAng.as<float>(), c->stream);
+        fm3d::launch_surf_keep(c->sfKin.as<fm3d_keypoint>(), P, size, size, c->sfFlag.as<int>(), c->sfPos.as<int>(),
+                               c->count.as<int>(), c->scanTmp.p, c->sfKp.as<fm3d_keypoint>(), nullptr,
+                               c->sfAng.as<float>(), c->stream);
+        HIPCHK(c, hipGetLastError());
+        int nk = 0;
+        HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (nk != P) return fail(c, FM3D_ERR_INVALID, "patch keypoint dropped by SURF (no orientation sample)");
+    }
     if (c->sfDW.bytes == 0) {
         const std::vector<float> dw = surf_dw();
         HIPCHK(c, c->sfDW.ensure(400 * sizeof(float)));
@@ -1435,7 +1502,7 @@ int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, i
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     fm3d::launch_surf_describe(c->sfImg.as<uint8_t>(), per, size, size, c->sfKp.as<fm3d_keypoint>(), P,
-                               c->sfDW.as<float>(), S.surfExtended, c->sfDesc.as<float>(), c->stream);
+                               c->sfDW.as<float>(), S.surfExtended, S.surfUpright, c->sfDesc.as<float>(), c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(desc, c->sfDesc.p, (size_t)P * dsize * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -147,19 +147,34 @@ struct SurfCand {
     int octave, class_id;
     long long seq;  // discovery order: (layer << 42) | (row << 21) | column
 };
+// SURFInvoker's orientation samples: the disc of radius 6 (x outer, y inner), Gaussian weights
+constexpr int kOriMax = 128;
+struct SurfOri {
+    int n;
+    int ax[kOriMax], ay[kOriMax];
+    float w[kOriMax];
+};
 void launch_integral(const uint8_t* img, int w, int h, int* sum, hipStream_t s);
+// nb images of w x h back to back, their (w+1) x (h+1) sums back to back
+void launch_integral_batch(const uint8_t* img, int w, int h, int nb, int* sum, hipStream_t s);
+// Upright 0: flag[q] / angle[q] of keypoint q = (x, y, size) at kp + q*kstride, on the integral
+// image sum + q*sumStride
+void launch_surf_orient(const void* kp, size_t kstride, int n, const int* sum, size_t sumStride, int w, int h,
+                        const SurfOri& ori, int* flag, float* angle, hipStream_t s);
 void launch_surf_hessian(const int* sum, int w, const SurfLayer* layers, int nL, long long total, float* det,
                          float* tr, hipStream_t s);
 void launch_surf_maxima(const float* det, const float* tr, const SurfLayer* layers, const SurfMid* mids, int nM,
                         long long total, float thr, SurfCand* cand, int* count, int cap, hipStream_t s);
 size_t surf_sort_tmp_bytes(int n);
 void launch_surf_sort(SurfCand* cand, int n, void* tmp, size_t tmpBytes, hipStream_t s);
+// angle == nullptr: the upright pass (flags computed here, angle 270); else flag / angle from
+// launch_surf_orient
 void launch_surf_upright(const SurfCand* cand, const int* count, int n, int w, int h, int* flag, int* pos, int* total,
-                         void* scanTmp, fm3d_keypoint* out, int* src, hipStream_t s);
+                         void* scanTmp, fm3d_keypoint* out, int* src, const float* angle, hipStream_t s);
 void launch_surf_keep(const fm3d_keypoint* in, int n, int w, int h, int* flag, int* pos, int* total, void* scanTmp,
-                      fm3d_keypoint* out, int* src, hipStream_t s);
+                      fm3d_keypoint* out, int* src, const float* angle, hipStream_t s);
 void launch_surf_describe(const uint8_t* img, size_t imgStride, int w, int h, const fm3d_keypoint* kp, int n,
-                          const float* DW, int extended, float* desc, hipStream_t s);
+                          const float* DW, int extended, int upright, float* desc, hipStream_t s);
 
 // ---------------- compaction ----------------
 // out[k] = in[i] for flag[i] != 0, stable; *count (device) = number kept.  tmp >= scan_tmp_bytes(n).

@@ -14,9 +14,14 @@
 //                        non-maximum suppression, interpolateKeypoint (Cramer's rule in float),
 //                        appended through an atomic counter; then a device merge sort by
 //                        KeypointGreater (discovery order breaks ties) and the upright pass;
-//   describe_kernel      SURFInvoker (upright): one workgroup per keypoint.  The 21x21 INTER_AREA
-//                        patch comes straight from the image (the rotated, border-replicated window
-//                        is never materialised): OpenCV's row buffers, one per window row, in LDS,
+//   orient_kernel        SURFInvoker's dominant orientation (Upright 0): a wave per keypoint, the
+//                        113 disc samples' Haar responses compacted in sample order by ballot, the
+//                        72 sliding 60-degree windows one lane each (each lane sums its window in
+//                        the reference's sample order), the first largest window by a wave argmax;
+//   describe_kernel      SURFInvoker: one workgroup per keypoint.  The 21x21 INTER_AREA patch comes
+//                        straight from the image (the border-replicated upright window or the
+//                        bilinear rotated one is never materialised): OpenCV's row buffers, one per
+//                        window row, in LDS,
 //                        then the beta-weighted rows per destination row, both in OpenCV's order;
 //                        then the 2x2 Haar gradients with the Gaussian weights, the 4x4 subregion
 //                        sums (one lane each, OpenCV's sample order) and the unit-length scale.
@@ -29,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "fm3d_kernels.h"
+#include "fm3d_detmath.h"
 
 namespace fm3d {
 
@@ -40,9 +46,12 @@ __device__ __forceinline__ int cv_round(double v) { return (int)rint(v); }
 
 // ---------------------------------------------------------------- integral image
 // sum: (h+1) x (w+1) int32, row 0 and column 0 zero.  Pass 1: row prefix sums (a wave per row).
+// blockIdx.y: image of a batch (image b at img + b*w*h, its sum at sum + b*(w+1)*(h+1))
 __global__ __launch_bounds__(64) void integral_rows_kernel(const uint8_t* __restrict__ img, int w, int h,
                                                             int* __restrict__ sum) {
     const int y = blockIdx.x, lane = threadIdx.x;
+    img += (size_t)blockIdx.y * w * h;
+    sum += (size_t)blockIdx.y * (w + 1) * (h + 1);
     int* row = sum + (size_t)(y + 1) * (w + 1);
     if (lane == 0) row[0] = 0;
     int carry = 0;
@@ -64,6 +73,7 @@ constexpr int kIntBands = 16;
 __global__ __launch_bounds__(64 * kIntBands) void integral_cols_kernel(int w, int h, int* __restrict__ sum) {
     __shared__ unsigned bandSum[kIntBands][64];
     const int lane = threadIdx.x & 63, band = threadIdx.x >> 6;
+    sum += (size_t)blockIdx.y * (w + 1) * (h + 1);
     const int x = blockIdx.x * 64 + lane;
     const int rows = (h + kIntBands - 1) / kIntBands;
     const int y0 = 1 + band * rows, y1 = min(h + 1, y0 + rows);
@@ -214,15 +224,15 @@ __global__ void upright_flag_kernel(const SurfCand* __restrict__ c, const int* _
     flag[q] = (h + 1 < gws || w + 1 < gws) ? 0 : 1;
 }
 __global__ void keypoint_scatter_kernel(const SurfCand* __restrict__ c, const int* __restrict__ flag,
-                                        const int* __restrict__ pos, int cap, fm3d_keypoint* __restrict__ out,
-                                        int* __restrict__ src) {
+                                        const int* __restrict__ pos, const float* __restrict__ angle, int cap,
+                                        fm3d_keypoint* __restrict__ out, int* __restrict__ src) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= cap || !flag[q]) return;
     fm3d_keypoint k;
     k.x = c[q].x;
     k.y = c[q].y;
     k.size = c[q].size;
-    k.angle = 360.f - 90.f;
+    k.angle = angle ? angle[q] : 360.f - 90.f;
     k.response = c[q].response;
     k.octave = c[q].octave;
     k.class_id = c[q].class_id;
@@ -242,14 +252,163 @@ __global__ void keep_flag_kernel(const fm3d_keypoint* __restrict__ k, int n, int
     flag[q] = (!(k[q].size >= 1.19209290e-07f) || h + 1 < gws || w + 1 < gws) ? 0 : 1;
 }
 __global__ void keep_scatter_kernel(const fm3d_keypoint* __restrict__ k, const int* __restrict__ flag,
-                                    const int* __restrict__ pos, int n, fm3d_keypoint* __restrict__ out,
-                                    int* __restrict__ src) {
+                                    const int* __restrict__ pos, const float* __restrict__ angle, int n,
+                                    fm3d_keypoint* __restrict__ out, int* __restrict__ src) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n || !flag[q]) return;
     fm3d_keypoint o = k[q];
-    o.angle = 360.f - 90.f;
+    o.angle = angle ? angle[q] : 360.f - 90.f;
     out[pos[q]] = o;
     if (src) src[pos[q]] = q;
+}
+
+
+// ---------------------------------------------------------------- orientation (Upright 0)
+// cv::fastAtan2 / phase(..., true) of OpenCV 2.4.9+ (the polynomial; degrees in [0, 360))
+__device__ __forceinline__ float fast_atan2f(float y, float x) {
+    constexpr float P1 = 0.9997878412794807f * (float)(180 / M_PI);
+    constexpr float P3 = -0.3258083974640975f * (float)(180 / M_PI);
+    constexpr float P5 = 0.1555786518463281f * (float)(180 / M_PI);
+    constexpr float P7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a;
+    if (ax >= ay) {
+        const float c = ay / (ax + (float)DBL_EPSILON), c2 = c * c;
+        a = (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    } else {
+        const float c = ax / (ay + (float)DBL_EPSILON), c2 = c * c;
+        a = 90.f - (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// resizeHaarPattern of SURFInvoker's 4x4 orientation wavelets (dx_s / dy_s) to size gws
+__device__ inline void ori_haar(int gws, int W1, SurfHF* dx, SurfHF* dy) {
+    const int DXO[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};
+    const int DYO[2][5] = {{0, 0, 4, 2, 1}, {0, 2, 4, 4, -1}};
+    const float ratio = (float)gws / 4;
+    for (int t = 0; t < 2; t++)
+        for (int k = 0; k < 2; k++) {
+            const int(*src)[5] = t ? DYO : DXO;
+            SurfHF& d = t ? dy[k] : dx[k];
+            const int dx1 = cv_roundf(ratio * src[k][0]), dy1 = cv_roundf(ratio * src[k][1]);
+            const int dx2 = cv_roundf(ratio * src[k][2]), dy2 = cv_roundf(ratio * src[k][3]);
+            d.p0 = dy1 * W1 + dx1;
+            d.p1 = dy2 * W1 + dx1;
+            d.p2 = dy1 * W1 + dx2;
+            d.p3 = dy2 * W1 + dx2;
+            d.w = src[k][4] / ((float)(dx2 - dx1) * (dy2 - dy1));
+        }
+}
+
+constexpr int kOriWaves = 4;
+// keypoint q = (x, y, size) at kp + q * kstride (SurfCand and fm3d_keypoint both start with them);
+// its integral image at sum + q * sumStride (0: one image).  flag[q] = the keypoint survives
+// SURFInvoker (size >= FLT_EPSILON -- DescriptorExtractor::compute's runByKeypointSize --, the
+// wavelet fits, at least one orientation sample inside); angle[q] = its dominant orientation.
+__global__ __launch_bounds__(64 * kOriWaves) void orient_kernel(const char* __restrict__ kp, size_t kstride, int n,
+                                                              const int* __restrict__ sum, size_t sumStride, int w,
+                                                              int h, SurfOri ori, int* __restrict__ flag,
+                                                              float* __restrict__ angle) {
+    __shared__ float SXs[kOriWaves][kOriMax], SYs[kOriWaves][kOriMax];
+    __shared__ int SAs[kOriWaves][kOriMax];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x * kOriWaves + wv;
+    if (q >= n) return;  // a whole wave; the waves share no barrier
+    float* SX = SXs[wv];
+    float* SY = SYs[wv];
+    int* SA = SAs[wv];
+    const float* k = reinterpret_cast<const float*>(kp + (size_t)q * kstride);
+    const float kx = k[0], ky = k[1], ksize = k[2];
+    const int W1 = w + 1, H1 = h + 1;
+    const float s = ksize * 1.2f / 9.0f;
+    const int gws = 2 * cv_roundf(2 * s);
+    if (!(ksize >= FLT_EPSILON) || H1 < gws || W1 < gws) {
+        if (lane == 0) flag[q] = 0;
+        return;
+    }
+    sum += (size_t)q * sumStride;
+    SurfHF dxt[2], dyt[2];
+    ori_haar(gws, W1, dxt, dyt);
+    // the disc samples inside the integral image, compacted in sample order
+    int nangle = 0;
+    for (int base = 0; base < ori.n; base += 64) {
+        const int kk = base + lane;
+        bool in = false;
+        float X = 0, Y = 0;
+        if (kk < ori.n) {
+            const int x = cv_roundf(kx + ori.ax[kk] * s - (float)(gws - 1) / 2);
+            const int y = cv_roundf(ky + ori.ay[kk] * s - (float)(gws - 1) / 2);
+            in = !(y < 0 || y >= H1 - gws || x < 0 || x >= W1 - gws);
+            if (in) {
+                const int* o = sum + (size_t)y * W1 + x;
+                X = haar_sum(o, dxt, 2) * ori.w[kk];
+                Y = haar_sum(o, dyt, 2) * ori.w[kk];
+            }
+        }
+        const unsigned long long m = __ballot(in);
+        if (in) {
+            const int at = nangle + __popcll(m & ((1ull << lane) - 1));
+            SX[at] = X;
+            SY[at] = Y;
+            SA[at] = cv_roundf(fast_atan2f(Y, X));
+        }
+        nangle += __popcll(m);
+    }
+    if (nangle == 0) {  // kp.size = -1: removed
+        if (lane == 0) flag[q] = 0;
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // windows i = 0, 5, ..., 355: lane l takes 5l and (l < 8) 5(l + 64); sequential sums as the source
+    const int i0 = 5 * lane, i1 = 5 * (lane + 64);
+    const bool two = lane < 72 - 64;
+    float sx0 = 0, sy0 = 0, sx1 = 0, sy1 = 0;
+    for (int j = 0; j < nangle; j++) {
+        const float X = SX[j], Y = SY[j];
+        const int a = SA[j];
+        const int d0 = abs(a - i0);
+        if (d0 < 30 || d0 > 360 - 30) {
+            sx0 += X;
+            sy0 += Y;
+        }
+        const int d1 = abs(a - i1);
+        if (two && (d1 < 30 || d1 > 360 - 30)) {
+            sx1 += X;
+            sy1 += Y;
+        }
+    }
+    // descriptor_mod: the first window of the largest sumx^2 + sumy^2 (strictly above 0)
+    float bm = sx0 * sx0 + sy0 * sy0, bx = sx0, by = sy0;
+    int bi = i0;
+    if (two) {
+        const float m1 = sx1 * sx1 + sy1 * sy1;
+        if (m1 > bm) {
+            bm = m1;
+            bx = sx1;
+            by = sy1;
+            bi = i1;
+        }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float om = __shfl_xor(bm, off), ox = __shfl_xor(bx, off), oy = __shfl_xor(by, off);
+        const int oi = __shfl_xor(bi, off);
+        if (om > bm || (om == bm && oi < bi)) {
+            bm = om;
+            bx = ox;
+            by = oy;
+            bi = oi;
+        }
+    }
+    if (!(bm > 0)) bx = by = 0;
+    if (lane == 0) {
+        flag[q] = 1;
+        angle[q] = fast_atan2f(-by, bx);
+    }
 }
 
 // ---------------------------------------------------------------- descriptors
@@ -301,6 +460,18 @@ __device__ __forceinline__ int area_entry(const AreaTab& t, int m, float& alpha)
     return t.s1 + t.full;
 }
 
+// start + j * step (j < W) of a float start and a float step, summed into a double one step at a
+// time, equals the closed form when every partial sum is a double exactly: all are multiples of
+// g = 2^(min exponent - 23) (the coarser of the two float ulps, conservatively) and below
+// |start| + W |step| in magnitude, so exact when that bound is under 2^53 g
+__device__ inline bool seq_exact(float start, float step, int W) {
+    if (step == 0.f) return true;
+    int e = ilogbf(step);
+    if (start != 0.f) e = min(e, ilogbf(start));
+    const double M = fabs((double)start) + (double)W * fabs((double)step);
+    return M * (1 + 1e-12) < ldexp(1.0, 53 + e - 23);
+}
+
 constexpr int kDescThreads = 256;
 constexpr int kDescMaxW = 640;  // window edge whose row buffers fit the LDS of one workgroup
 
@@ -317,7 +488,7 @@ constexpr int kDescMaxW = 640;  // window edge whose row buffers fit the LDS of 
 __global__ __launch_bounds__(kDescThreads) void describe_kernel(const uint8_t* __restrict__ img, size_t imgStride,
                                                                 int w, int h, const fm3d_keypoint* __restrict__ kp,
                                                                 int n, const float* __restrict__ DW, int extended,
-                                                                float* __restrict__ desc) {
+                                                                int upright, float* __restrict__ desc) {
     const int q = blockIdx.x, tid = threadIdx.x;
     if (q >= n) return;
     img += (size_t)q * imgStride;
@@ -326,6 +497,8 @@ __global__ __launch_bounds__(kDescThreads) void describe_kernel(const uint8_t* _
     __shared__ uint8_t P[21 * 21];
     __shared__ float DX[400], DY[400], V[128];
     __shared__ float sc;
+    __shared__ float RSX[kDescMaxW], RSY[kDescMaxW];
+    __shared__ bool RX[kDescMaxW];
     const fm3d_keypoint k = kp[q];
     const float s = k.size * 1.2f / 9.0f;
     const int gws = 2 * cv_roundf(2 * s);
@@ -333,9 +506,76 @@ __global__ __launch_bounds__(kDescThreads) void describe_kernel(const uint8_t* _
     const int W = (int)((20 + 1) * s);
     const float win_offset = -(float)(W - 1) / 2;
     const int start_x = cv_roundf(k.x + win_offset), start_y = cv_roundf(k.y - win_offset);
-    // window pixel (row r, column c) = img(clamp(start_y - c), clamp(start_x + r))
+    // rotated window (Upright 0): row r starts at (RSX[r], RSY[r]), accumulated in float row after
+    // row as the source does; along a row the source steps a double by cos_dir / -sin_dir.  RX[r]:
+    // every such partial sum of row r is a double exactly (seq_exact), so start + c * step is the
+    // same number; else the row is stepped sequentially
+    float sin_dir = 0.f, cos_dir = 0.f, rsx0 = 0.f, rsy0 = 0.f;
+    const bool rot = !upright;
+    if (rot) {
+        const float dir = k.angle * (float)(M_PI / 180);
+        sin_dir = -(float)fm3d_sin((double)dir);
+        cos_dir = (float)fm3d_cos((double)dir);
+        rsx0 = k.x + win_offset * cos_dir + win_offset * sin_dir;
+        rsy0 = k.y - win_offset * sin_dir + win_offset * cos_dir;
+        if (W <= kDescMaxW) {
+            if (tid < 2) {  // lane 0 the x starts, lane 1 the y starts
+                float v = tid ? rsy0 : rsx0;
+                const float st = tid ? cos_dir : sin_dir;
+                float* R = tid ? RSY : RSX;
+                for (int r = 0; r < W; r++, v += st) R[r] = v;
+            }
+            __syncthreads();
+            for (int r = tid; r < W; r += kDescThreads)
+                RX[r] = seq_exact(RSX[r], cos_dir, W) && seq_exact(RSY[r], -sin_dir, W);
+            __syncthreads();
+        }
+    }
+    // window pixel (row r, column c): upright = img(clamp(start_y - c), clamp(start_x + r))
     auto WIN = [&](int r, int c) -> int {
-        int x = start_x + r, y = start_y - c;
+        if (!rot) {
+            int x = start_x + r, y = start_y - c;
+            x = x > 0 ? x : 0;
+            y = y > 0 ? y : 0;
+            x = x < w - 1 ? x : w - 1;
+            y = y < h - 1 ? y : h - 1;
+            return img[(size_t)y * w + x];
+        }
+        float sx, sy;
+        bool exact;
+        if (W <= kDescMaxW) {
+            sx = RSX[r];
+            sy = RSY[r];
+            exact = RX[r];
+        } else {
+            sx = rsx0;
+            sy = rsy0;
+            for (int i = 0; i < r; i++) {
+                sx += sin_dir;
+                sy += cos_dir;
+            }
+            exact = seq_exact(sx, cos_dir, W) && seq_exact(sy, -sin_dir, W);
+        }
+        double px, py;
+        if (exact) {
+            px = (double)sx + (double)c * (double)cos_dir;
+            py = (double)sy - (double)c * (double)sin_dir;
+        } else {
+            px = sx;
+            py = sy;
+            for (int j = 0; j < c; j++) {
+                px += cos_dir;
+                py -= sin_dir;
+            }
+        }
+        const int ix = (int)floor(px), iy = (int)floor(py);
+        if ((unsigned)ix < (unsigned)(w - 1) && (unsigned)iy < (unsigned)(h - 1)) {
+            const float a = (float)(px - ix), b = (float)(py - iy);
+            const uint8_t* p = img + (size_t)iy * w + ix;
+            return (uint8_t)cv_roundf(p[0] * (1.f - a) * (1.f - b) + p[1] * a * (1.f - b) + p[w] * (1.f - a) * b +
+                                      p[w + 1] * a * b);
+        }
+        int x = cv_round(px), y = cv_round(py);
         x = x > 0 ? x : 0;
         y = y > 0 ? y : 0;
         x = x < w - 1 ? x : w - 1;
@@ -501,26 +741,39 @@ void launch_surf_sort(SurfCand* cand, int n, void* tmp, size_t tmpBytes, hipStre
     hipcub::DeviceMergeSort::SortKeys(tmp, tmpBytes, cand, n, KpGreater(), s);
 }
 
-void launch_surf_upright(const SurfCand* cand, const int* count, int n, int w, int h, int* flag, int* pos, int* total,
-                         void* scanTmp, fm3d_keypoint* out, int* src, hipStream_t s) {
+void launch_integral_batch(const uint8_t* img, int w, int h, int nb, int* sum, hipStream_t s) {
+    if (w <= 0 || h <= 0 || nb <= 0) return;
+    integral_rows_kernel<<<dim3(h, nb), 64, 0, s>>>(img, w, h, sum);
+    integral_cols_kernel<<<dim3((w + 1 + 63) / 64, nb), 64 * kIntBands, 0, s>>>(w, h, sum);
+}
+
+void launch_surf_orient(const void* kp, size_t kstride, int n, const int* sum, size_t sumStride, int w, int h,
+                        const SurfOri& ori, int* flag, float* angle, hipStream_t s) {
     if (n <= 0) return;
-    upright_flag_kernel<<<(n + 255) / 256, 256, 0, s>>>(cand, count, n, w, h, flag);
+    orient_kernel<<<(n + kOriWaves - 1) / kOriWaves, 64 * kOriWaves, 0, s>>>(
+        static_cast<const char*>(kp), kstride, n, sum, sumStride, w, h, ori, flag, angle);
+}
+
+void launch_surf_upright(const SurfCand* cand, const int* count, int n, int w, int h, int* flag, int* pos, int* total,
+                         void* scanTmp, fm3d_keypoint* out, int* src, const float* angle, hipStream_t s) {
+    if (n <= 0) return;
+    if (!angle) upright_flag_kernel<<<(n + 255) / 256, 256, 0, s>>>(cand, count, n, w, h, flag);
     launch_exclusive_scan(flag, n, pos, total, scanTmp, s);
-    keypoint_scatter_kernel<<<(n + 255) / 256, 256, 0, s>>>(cand, flag, pos, n, out, src);
+    keypoint_scatter_kernel<<<(n + 255) / 256, 256, 0, s>>>(cand, flag, pos, angle, n, out, src);
 }
 
 void launch_surf_keep(const fm3d_keypoint* in, int n, int w, int h, int* flag, int* pos, int* total, void* scanTmp,
-                      fm3d_keypoint* out, int* src, hipStream_t s) {
+                      fm3d_keypoint* out, int* src, const float* angle, hipStream_t s) {
     if (n <= 0) return;
-    keep_flag_kernel<<<(n + 255) / 256, 256, 0, s>>>(in, n, w, h, flag);
+    if (!angle) keep_flag_kernel<<<(n + 255) / 256, 256, 0, s>>>(in, n, w, h, flag);
     launch_exclusive_scan(flag, n, pos, total, scanTmp, s);
-    keep_scatter_kernel<<<(n + 255) / 256, 256, 0, s>>>(in, flag, pos, n, out, src);
+    keep_scatter_kernel<<<(n + 255) / 256, 256, 0, s>>>(in, flag, pos, angle, n, out, src);
 }
 
 void launch_surf_describe(const uint8_t* img, size_t imgStride, int w, int h, const fm3d_keypoint* kp, int n,
-                          const float* DW, int extended, float* desc, hipStream_t s) {
+                          const float* DW, int extended, int upright, float* desc, hipStream_t s) {
     if (n <= 0) return;
-    describe_kernel<<<n, kDescThreads, 0, s>>>(img, imgStride, w, h, kp, n, DW, extended, desc);
+    describe_kernel<<<n, kDescThreads, 0, s>>>(img, imgStride, w, h, kp, n, DW, extended, upright, desc);
 }
 
 }  // namespace fm3d

@@ -333,22 +333,24 @@ def integral(img):
     return out
 
 
-def surf_detect(img, thr=400.0, octaves=4, layers=2):
-    """SURF detect (fastHessianDetector + the upright detect pass): cv::KeyPoint records, sorted."""
+def surf_detect(img, thr=400.0, octaves=4, layers=2, upright=True):
+    """SURF detect (fastHessianDetector + the detect pass of SURFInvoker: upright angle, or the
+    dominant orientation with upright False): cv::KeyPoint records, sorted."""
     img = np.ascontiguousarray(img, dtype=np.uint8)
     h, w = img.shape
-    f = lib().orc_surf_detect
+    f = lib().orc_surf_detect2
     f.restype = ctypes.c_int
     args = (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_float(thr), ctypes.c_int(octaves),
-            ctypes.c_int(layers))
+            ctypes.c_int(layers), ctypes.c_int(1 if upright else 0))
     n = f(*args, None, ctypes.c_int(0))
     out = np.zeros(max(n, 1), dtype=KEYPOINT)
     f(*args, out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(n))
     return out[:n]
 
 
-def surf_describe(img, kpts, extended=True):
-    """SURF compute (upright): (kept keypoints, input index of each, descriptors n x 128|64 float32)."""
+def surf_describe(img, kpts, extended=True, upright=True):
+    """SURF compute (upright, or oriented with upright False): (kept keypoints, input index of each,
+    descriptors n x 128|64 float32)."""
     img = np.ascontiguousarray(img, dtype=np.uint8)
     h, w = img.shape
     kin = np.ascontiguousarray(kpts, dtype=KEYPOINT)
@@ -356,14 +358,29 @@ def surf_describe(img, kpts, extended=True):
     kout = np.zeros(max(n, 1), dtype=KEYPOINT)
     kept = np.zeros(max(n, 1), dtype=np.int32)
     desc = np.zeros((max(n, 1), 128 if extended else 64), dtype=np.float32)
-    f = lib().orc_surf_describe
+    f = lib().orc_surf_describe2
     f.restype = ctypes.c_int
     m = f(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), kin.ctypes.data_as(ctypes.c_void_p),
-          ctypes.c_int(n), ctypes.c_int(1 if extended else 0), kout.ctypes.data_as(ctypes.c_void_p),
+          ctypes.c_int(n), ctypes.c_int(1 if extended else 0), ctypes.c_int(1 if upright else 0),
+          kout.ctypes.data_as(ctypes.c_void_p),
           _p(kept, ctypes.c_int), _p(desc, ctypes.c_float))
     if m < 0:
         raise ValueError("SURF describe: a keypoint of size < 7.5 (OpenCV upscales its window; not restated)")
     return kout[:m], kept[:m], desc[:m]
+
+
+def fast_atan2(y, x):
+    f = lib().orc_fast_atan2
+    f.restype = ctypes.c_float
+    return f(ctypes.c_float(y), ctypes.c_float(x))
+
+
+def surf_ori_samples():
+    """SURFInvoker's orientation disc: (apt (n, 2) int, aptw (n,) float32)"""
+    apt = np.zeros((169, 2), dtype=np.int32)
+    aptw = np.zeros(169, dtype=np.float32)
+    n = lib().orc_surf_ori_samples(_p(apt, ctypes.c_int), _p(aptw, ctypes.c_float))
+    return apt[:n], aptw[:n]
 
 
 def surf_dw():

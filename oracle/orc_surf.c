@@ -27,6 +27,7 @@
  */
 #include <float.h>
 #include <math.h>
+#include "fm3d_detmath.h"
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -74,6 +75,9 @@ static float haar(const int *origin, const orc_hf *f, int n)
 static const int DX_S[3][5] = {{0, 2, 3, 7, 1}, {3, 2, 6, 7, -2}, {6, 2, 9, 7, 1}};
 static const int DY_S[3][5] = {{2, 0, 7, 3, 1}, {2, 3, 7, 6, -2}, {2, 6, 7, 9, 1}};
 static const int DXY_S[4][5] = {{1, 1, 4, 4, 1}, {5, 1, 8, 4, -1}, {1, 5, 4, 8, -1}, {5, 5, 8, 8, 1}};
+/* SURFInvoker's orientation wavelets (dx_s / dy_s, 4x4 base size) */
+static const int DXO_S[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};
+static const int DYO_S[2][5] = {{0, 0, 4, 2, 1}, {0, 2, 4, 4, -1}};
 
 ORC_API void orc_integral(const uint8_t *img, int w, int h, int *sum)
 {
@@ -160,8 +164,9 @@ static int kcmp(const void *pa, const void *pb)
 
 /* fastHessianDetector + the detect-time SURFInvoker pass (upright: angle 270, oversized wavelets
    dropped).  Returns the number of keypoints (<= cap written). */
-ORC_API int orc_surf_detect(const uint8_t *img, int w, int h, float thr, int nOctaves, int nOctaveLayers,
-                            orc_kpt *out, int cap)
+static int surf_orientation(const int *sum, int w, int h, orc_kpt *k);
+ORC_API int orc_surf_detect2(const uint8_t *img, int w, int h, float thr, int nOctaves, int nOctaveLayers,
+                             int upright, orc_kpt *out, int cap)
 {
     const int W1 = w + 1, nTotal = (nOctaveLayers + 2) * nOctaves;
     int *sum = (int *)malloc(sizeof(int) * (size_t)W1 * (h + 1));
@@ -247,13 +252,15 @@ ORC_API int orc_surf_detect(const uint8_t *img, int w, int h, float thr, int nOc
                 }
         }
     if (nk > 1) qsort(ks, nk, sizeof(kseq), kcmp);
-    /* SURFInvoker (detect): upright angle; the gradient wavelet must fit the integral image */
+    /* SURFInvoker (detect): the gradient wavelet must fit the integral image; upright angle 270,
+       else the dominant orientation (no orientation sample inside the image: dropped) */
     for (q = 0; q < nk; q++) {
         orc_kpt k = ks[q].k;
         const float s = k.size * 1.2f / 9.0f;
         const int gws = 2 * cv_round(2 * s);
         if (h + 1 < gws || w + 1 < gws) continue;
-        k.angle = 360.f - 90.f;
+        if (upright) k.angle = 360.f - 90.f;
+        else if (!surf_orientation(sum, w, h, &k)) continue;
         if (n < cap) out[n] = k;
         n++;
     }
@@ -269,6 +276,11 @@ ORC_API int orc_surf_detect(const uint8_t *img, int w, int h, float thr, int nOc
     free(ks);
     return n;
 }
+ORC_API int orc_surf_detect(const uint8_t *img, int w, int h, float thr, int nOctaves, int nOctaveLayers,
+                            orc_kpt *out, int cap)
+{
+    return orc_surf_detect2(img, w, h, thr, nOctaves, nOctaveLayers, 1, out, cap);
+}
 
 /* getGaussianKernel(n, sigma, CV_32F) */
 static void gaussian_kernel(int n, double sigma, float *cf)
@@ -283,6 +295,102 @@ static void gaussian_kernel(int n, double sigma, float *cf)
     }
     sum = 1. / sum;
     for (i = 0; i < n; i++) cf[i] = (float)(cf[i] * sum);
+}
+
+/* cv::fastAtan2 (OpenCV 2.4.9+ core/mathfuncs.cpp; FastAtan2_32f's SSE2 and scalar paths compute the
+   same float operations): degrees in [0, 360) */
+#define ORC_ATAN2_P1 (0.9997878412794807f * (float)(180 / M_PI))
+#define ORC_ATAN2_P3 (-0.3258083974640975f * (float)(180 / M_PI))
+#define ORC_ATAN2_P5 (0.1555786518463281f * (float)(180 / M_PI))
+#define ORC_ATAN2_P7 (-0.04432655554792128f * (float)(180 / M_PI))
+static float fast_atan2f(float y, float x)
+{
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((ORC_ATAN2_P7 * c2 + ORC_ATAN2_P5) * c2 + ORC_ATAN2_P3) * c2 + ORC_ATAN2_P1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((ORC_ATAN2_P7 * c2 + ORC_ATAN2_P5) * c2 + ORC_ATAN2_P3) * c2 + ORC_ATAN2_P1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+ORC_API float orc_fast_atan2(float y, float x) { return fast_atan2f(y, x); }
+
+/* the orientation samples of the SURFInvoker constructor: the disc of radius ORI_RADIUS = 6
+   (i outer = x, j inner = y), weights G(i) * G(j) with G = getGaussianKernel(13, 2.5, CV_32F) */
+enum { ORI_RADIUS = 6, ORI_SAMPLES_MAX = (2 * 6 + 1) * (2 * 6 + 1), ORI_SEARCH_INC = 5, ORI_WIN = 60 };
+static void gaussian_kernel(int n, double sigma, float *cf);
+static int ori_samples(int apt[][2], float *aptw)
+{
+    float g[2 * ORI_RADIUS + 1];
+    int i, j, n = 0;
+    gaussian_kernel(2 * ORI_RADIUS + 1, 2.5, g);
+    for (i = -ORI_RADIUS; i <= ORI_RADIUS; i++)
+        for (j = -ORI_RADIUS; j <= ORI_RADIUS; j++)
+            if (i * i + j * j <= ORI_RADIUS * ORI_RADIUS) {
+                apt[n][0] = i;
+                apt[n][1] = j;
+                aptw[n++] = g[i + ORI_RADIUS] * g[j + ORI_RADIUS];
+            }
+    return n;
+}
+ORC_API int orc_surf_ori_samples(int *apt, float *aptw) { return ori_samples((int(*)[2])apt, aptw); }
+
+/* SURFInvoker's dominant orientation (upright == 0): Haar responses of size 2*cvRound(2s) at the
+   disc samples scaled by s, Gaussian weighted, their angles (cvCartToPolar in degrees = the
+   fastAtan2 polynomial), the 60-degree window of largest |sum| over 72 steps of 5 degrees, angle
+   fastAtan2(-besty, bestx).  Returns 0 when no sample fits the integral image (the keypoint is
+   dropped: kp.size = -1). */
+static int surf_orientation(const int *sum, int w, int h, orc_kpt *k)
+{
+    int apt[ORI_SAMPLES_MAX][2], nOri;
+    float aptw[ORI_SAMPLES_MAX];
+    const int W1 = w + 1, H1 = h + 1;
+    const float s = k->size * 1.2f / 9.0f;
+    const int gws = 2 * cv_round(2 * s);
+    float X[ORI_SAMPLES_MAX], Y[ORI_SAMPLES_MAX], ang[ORI_SAMPLES_MAX];
+    float bestx = 0, besty = 0, descriptor_mod = 0;
+    orc_hf dxt[2], dyt[2];
+    int kk, nangle = 0, i, j;
+    nOri = ori_samples(apt, aptw);
+    resize_haar(DXO_S, dxt, 2, 4, gws, W1);
+    resize_haar(DYO_S, dyt, 2, 4, gws, W1);
+    for (kk = 0; kk < nOri; kk++) {
+        const int x = cv_round(k->x + apt[kk][0] * s - (float)(gws - 1) / 2);
+        const int y = cv_round(k->y + apt[kk][1] * s - (float)(gws - 1) / 2);
+        const int *ptr;
+        if (y < 0 || y >= H1 - gws || x < 0 || x >= W1 - gws) continue;
+        ptr = sum + (size_t)y * W1 + x;
+        X[nangle] = haar(ptr, dxt, 2) * aptw[kk];
+        Y[nangle] = haar(ptr, dyt, 2) * aptw[kk];
+        nangle++;
+    }
+    if (nangle == 0) return 0;
+    for (j = 0; j < nangle; j++) ang[j] = fast_atan2f(Y[j], X[j]);
+    for (i = 0; i < 360; i += ORI_SEARCH_INC) {
+        float sumx = 0, sumy = 0, temp_mod;
+        for (j = 0; j < nangle; j++) {
+            const int d = abs(cv_round(ang[j]) - i);
+            if (d < ORI_WIN / 2 || d > 360 - ORI_WIN / 2) {
+                sumx += X[j];
+                sumy += Y[j];
+            }
+        }
+        temp_mod = sumx * sumx + sumy * sumy;
+        if (temp_mod > descriptor_mod) {
+            descriptor_mod = temp_mod;
+            bestx = sumx;
+            besty = sumy;
+        }
+    }
+    k->angle = fast_atan2f(-besty, bestx);
+    return 1;
 }
 
 /* the 20x20 descriptor weights DW (SURFInvoker constructor) */
@@ -401,22 +509,82 @@ void resize_area(const uint8_t *src, int W, uint8_t *dst)
     }
 }
 
-/* SURFInvoker descriptors of the upright extractor for given keypoints (SURF::operator() with
-   useProvidedKeypoints): keypoints whose wavelet exceeds the integral image are dropped (compacted
-   with their descriptors, kept[] gets the input index of each survivor).  desc: n x (128 | 64). */
-ORC_API int orc_surf_describe(const uint8_t *img, int w, int h, const orc_kpt *kin, int n, int extended,
-                              orc_kpt *kout, int *kept, float *desc)
+/* the W x W window of SURFInvoker around keypoint k: upright (angle 270: border-replicated pixels,
+   rows = x) or rotated by k.angle (degrees): the subpixel version, bilinear inside the image and
+   nearest (clamped) outside, start positions accumulated in float and the positions along a row in
+   double, as the source does.  sin / cos of the float angle in radians: correctly rounded float
+   values (fm3d_detmath in double, rounded; glibc's sinf / cosf give the same floats in practice). */
+static void surf_window(const uint8_t *img, int w, int h, const orc_kpt *k, int upright, int W, uint8_t *win)
+{
+    const float win_offset = -(float)(W - 1) / 2;
+    int i, j;
+    if (upright) {
+        int start_x = cv_round(k->x + win_offset), start_y = cv_round(k->y - win_offset);
+        for (i = 0; i < W; i++, start_x++) {
+            int pixel_x = start_x, pixel_y = start_y;
+            for (j = 0; j < W; j++, pixel_y--) {
+                int x = pixel_x > 0 ? pixel_x : 0, y = pixel_y > 0 ? pixel_y : 0;
+                x = x < w - 1 ? x : w - 1;
+                y = y < h - 1 ? y : h - 1;
+                win[(size_t)i * W + j] = img[(size_t)y * w + x];
+            }
+        }
+        return;
+    }
+    {
+        const float dir = k->angle * (float)(M_PI / 180);
+        const float sin_dir = -(float)fm3d_sin((double)dir), cos_dir = (float)fm3d_cos((double)dir);
+        float start_x = k->x + win_offset * cos_dir + win_offset * sin_dir;
+        float start_y = k->y - win_offset * sin_dir + win_offset * cos_dir;
+        const int ncols1 = w - 1, nrows1 = h - 1;
+        for (i = 0; i < W; i++, start_x += sin_dir, start_y += cos_dir) {
+            double pixel_x = start_x, pixel_y = start_y;
+            for (j = 0; j < W; j++, pixel_x += cos_dir, pixel_y -= sin_dir) {
+                const int ix = (int)floor(pixel_x), iy = (int)floor(pixel_y);
+                uint8_t v;
+                if ((unsigned)ix < (unsigned)ncols1 && (unsigned)iy < (unsigned)nrows1) {
+                    const float a = (float)(pixel_x - ix), b = (float)(pixel_y - iy);
+                    const uint8_t *p = img + (size_t)iy * w + ix;
+                    v = (uint8_t)cv_round(p[0] * (1.f - a) * (1.f - b) + p[1] * a * (1.f - b) + p[w] * (1.f - a) * b +
+                                          p[w + 1] * a * b);
+                } else {
+                    int x = cv_round(pixel_x), y = cv_round(pixel_y);
+                    x = x > 0 ? x : 0;
+                    y = y > 0 ? y : 0;
+                    x = x < ncols1 ? x : ncols1;
+                    y = y < nrows1 ? y : nrows1;
+                    v = img[(size_t)y * w + x];
+                }
+                win[(size_t)i * W + j] = v;
+            }
+        }
+    }
+}
+
+/* SURFInvoker descriptors for given keypoints (SURF::operator() with useProvidedKeypoints, via
+   DescriptorExtractor::compute): size < FLT_EPSILON dropped first, then keypoints whose wavelet
+   exceeds the integral image, and (upright == 0) those without an orientation sample; the others get
+   angle 270 (upright) or their dominant orientation.  Compacted with their descriptors, kept[] gets
+   the input index of each survivor.  desc: n x (128 | 64).  Returns -1 for a kept keypoint of size
+   < 7.5 (OpenCV's upscaling INTER_AREA branch, not restated). */
+ORC_API int orc_surf_describe2(const uint8_t *img, int w, int h, const orc_kpt *kin, int n, int extended, int upright,
+                               orc_kpt *kout, int *kept, float *desc)
 {
     const int dsize = extended ? 128 : 64;
     float DW[400];
     int q, m = 0;
+    int *sum = NULL;
     orc_surf_dw(DW);
+    if (!upright) {
+        sum = (int *)malloc(sizeof(int) * (size_t)(w + 1) * (h + 1));
+        orc_integral(img, w, h, sum);
+    }
     for (q = 0; q < n; q++) {
         orc_kpt k = kin[q];
         const float s = k.size * 1.2f / 9.0f;
         const int gws = 2 * cv_round(2 * s);
-        int win_size, start_x, start_y, i, j, kk;
-        float win_offset, *vec;
+        int win_size, i, j, kk;
+        float *vec;
         uint8_t *win, patch[21 * 21];
         float DXa[400], DYa[400];
         double square_mag = 0;
@@ -425,22 +593,12 @@ ORC_API int orc_surf_describe(const uint8_t *img, int w, int h, const orc_kpt *k
            (runByImageBorder with border 0 removes nothing), then the SURFInvoker wavelet drop */
         if (!(k.size >= FLT_EPSILON)) continue;
         if (h + 1 < gws || w + 1 < gws) continue;
-        k.angle = 360.f - 90.f;
+        if (upright) k.angle = 360.f - 90.f;
+        else if (!surf_orientation(sum, w, h, &k)) continue;
         win_size = (int)((20 + 1) * s);
-        if (win_size < 21) return -1; /* OpenCV's INTER_AREA upscale branch: not restated */
-        win_offset = -(float)(win_size - 1) / 2;
-        start_x = cv_round(k.x + win_offset);
-        start_y = cv_round(k.y - win_offset);
+        if (win_size < 21) { free(sum); return -1; } /* OpenCV's INTER_AREA upscale branch: not restated */
         win = (uint8_t *)malloc((size_t)win_size * win_size);
-        for (i = 0; i < win_size; i++, start_x++) {
-            int pixel_x = start_x, pixel_y = start_y;
-            for (j = 0; j < win_size; j++, pixel_y--) {
-                int x = pixel_x > 0 ? pixel_x : 0, y = pixel_y > 0 ? pixel_y : 0;
-                x = x < w - 1 ? x : w - 1;
-                y = y < h - 1 ? y : h - 1;
-                win[(size_t)i * win_size + j] = img[(size_t)y * w + x];
-            }
-        }
+        surf_window(img, w, h, &k, upright, win_size, win);
         resize_area(win, win_size, patch);
         free(win);
         for (i = 0; i < 20; i++)
@@ -491,5 +649,11 @@ ORC_API int orc_surf_describe(const uint8_t *img, int w, int h, const orc_kpt *k
         if (kept) kept[m] = q;
         m++;
     }
+    free(sum);
     return m;
+}
+ORC_API int orc_surf_describe(const uint8_t *img, int w, int h, const orc_kpt *kin, int n, int extended,
+                              orc_kpt *kout, int *kept, float *desc)
+{
+    return orc_surf_describe2(img, w, h, kin, n, extended, 1, kout, kept, desc);
 }

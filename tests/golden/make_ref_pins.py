@@ -335,6 +335,55 @@ def fit(geo, M, later, ab, entries=None, log=print, extra_starts=()):
     return par, f
 
 
+FIT_RUN = "64px4l.5c.32e"
+
+
+def patch_l1(geo, X, n, rk, lab1, lab2, bg1, bg2, patches, g, run):
+    """sum over both images of |oracle sample - reference patch| on the eligible pixels (four
+    bilinear taps unpainted) of run `run`'s patch_<rk>.pgm"""
+    orc = geo.orc
+    F = orc.features_frames(X[None], n[None], g)
+    eps, cmpp = PATCH_PARAMS[run]
+    pts = orc.square_neighborhoods(F, eps, cmpp)[0]
+    tot = 0
+    for image, R, t, lab, bg in ((1, np.eye(3), np.zeros(3), lab1, bg1), (2, geo.R2, geo.t2, lab2, bg2)):
+        uv = orc.project(Cam, R, t, pts)
+        x0 = np.floor(uv[:, 0].astype(np.float32)).astype(np.int64)
+        y0 = np.floor(uv[:, 1].astype(np.float32)).astype(np.int64)
+        ok = (x0 >= 0) & (y0 >= 0) & (x0 + 1 < W) & (y0 + 1 < H)
+        e = np.zeros(len(uv), bool)
+        i = np.nonzero(ok)[0]
+        e[i] = (lab[y0[i], x0[i]] == 0) & (lab[y0[i] + 1, x0[i]] == 0) & (lab[y0[i], x0[i] + 1] == 0) & (
+            lab[y0[i] + 1, x0[i] + 1] == 0)
+        want = patches[f"{run}_img{image}"][rk].T.reshape(-1)
+        tot += int(np.abs(orc.sample_points(bg, uv)[e].astype(np.int64) - want[e]).sum())
+    return tot
+
+
+def refine_on_patches(geo, p0, sg, rk, lab1, lab2, bg1, bg2, patches, ab, g):
+    """Nelder-Mead on the FIT_RUN patch L1 from the label fit, three simplex scales"""
+    from scipy.optimize import minimize
+    Mk, later = lab2 == rk + 1, lab2 > rk + 1
+    m0, _ = mismatch(geo, p0, Mk, later, ab)
+
+    def f(p):
+        m, _ = mismatch(geo, p, Mk, later, ab)
+        if m > m0:
+            return 1e12 + m
+        return patch_l1(geo, geo.point(*p[:3]), sg * geo.normal(p[3], p[4]), rk, lab1, lab2, bg1, bg2, patches, g,
+                        FIT_RUN)
+
+    best, fb = p0.copy(), f(p0)
+    step = np.array([1.0, 1.0, 0.05, 1.0, 1.0])
+    for sc in (1e-2, 3e-3, 1e-3):
+        simplex = np.vstack([best] + [best + sc * step[i] * np.eye(5)[i] for i in range(5)])
+        r = minimize(f, best, method="Nelder-Mead",
+                     options=dict(initial_simplex=simplex, maxfev=600, xatol=1e-7, fatol=0.5))
+        if r.fun < fb:
+            best, fb = r.x, r.fun
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=1)
@@ -412,9 +461,26 @@ def main():
         sign[rk] = 1.0 if score[0] >= score[1] else -1.0
         print(f"  survivor {rk}: normal sign {sign[rk]:+.0f} (patch pixels equal {score})", flush=True)
     n = n * sign[:, None]
+    # sub-pixel refinement: the label images pin the 5 numbers to integer rounding only; the
+    # patches are bilinear samples at sub-pixel positions.  Fit on the FIT_RUN patches (both
+    # images), the label mismatch never above the label fit's; the other runs are held out.
+    refined = np.zeros((S, 5))
+    for rk in range(S):
+        t0 = time.time()
+        if f"ref{rk}" in cache:
+            refined[rk] = cache[f"ref{rk}"]
+        else:
+            refined[rk] = refine_on_patches(geo, params[rk], sign[rk], rk, lab1, lab2, bg1, bg2, patches,
+                                            centres[rk], g)
+            cache[f"ref{rk}"] = refined[rk]
+            np.savez(cache_path, **cache)
+        print(f"  survivor {rk}: refined {(refined[rk] - params[rk]).tolist()} ({time.time() - t0:.0f} s)", flush=True)
+    X = np.stack([geo.point(*p[:3]) for p in refined])
+    n = np.stack([geo.normal(p[3], p[4]) for p in refined]) * sign[:, None]
+    fit_mis = np.array([mismatch(geo, refined[rk], lab2 == rk + 1, lab2 > rk + 1, centres[rk])[0] for rk in range(S)])
     np.savez_compressed(
         OUT, lab1=lab1, lab2=lab2, bg1=bg1, bg2=bg2, survivors=np.array(surv), colours=np.array(cols[:max(surv) + 1]),
-        centres=np.array(centres), params=params, X=X, n=n, fit_mismatch=fit_mis, heldout=held,
+        centres=np.array(centres), params=refined, label_params=params, fit_run=FIT_RUN, X=X, n=n, fit_mismatch=fit_mis, heldout=held,
         camera=np.array([Cam.fx, Cam.fy, Cam.cx, Cam.cy, *Cam.k]), rIC=RIC, tIC=TIC, pos1=POS1, pos2=POS2,
         g12=geo.g12, **{"patch_" + d.replace(".", "_"): patches[d] for d in PATCH_DIRS})
     print("wrote", OUT, flush=True)

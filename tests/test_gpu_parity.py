@@ -563,6 +563,31 @@ def test_c3_orb10k_pipeline(fm3d, orc, synth, ray, k):
     assert ok.sum() > k // 4 and n > 0.3 * len(pts)
 
 
+def test_c3_ncc_leg_16_hypotheses_r32(fm3d, orc, synth):
+    """the C3 NCC leg -- 16 normal hypotheses (4 x 4 over a 0.4 rad span) scored by NCC
+    over pixelsRay-32 neighbourhoods for EVERY DLT inlier of the 10k-ORB pair (configs[2]); a seeded
+    1,000-point sample bit-exact against the oracle (scores, best normal, best index)."""
+    fp = synth.make_frame_pair(10_000, seed=102, desc="orb")
+    q, t, _ = orc.match_nndr(fp.desc1, fp.desc2, orc.BITS, 0.8, oracle_threads())
+    pts, _ = orc.triangulate(fp.cam, fp.g12, 1.5, 2.4, fp.kp1, fp.kp2, q, t)
+    s = _settings(fm3d, fp.cam, pixelsRay=32, nndrEpsilon=0.8, boundWidth=640, boundHeight=480)
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(fp.g12)
+        R2, t2 = sct.camera2()
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(fp.img1, fp.img2)
+        sc, nb, b = no.nccHypotheses(pts, 4, 4, 0.4)
+    finally:
+        ctx.close()
+    assert sc.shape == (len(pts), 16) and len(pts) > 5000
+    sel = np.sort(np.random.default_rng(33).choice(len(pts), 1000, replace=False))
+    rs, rn, rb = orc.ncc_hypotheses(fp.cam, R2, t2, fp.img1, fp.img2, pts[sel], 32, 4, 4, 0.4, bound=(640, 480))
+    assert np.array_equal(b[sel], rb) and np.array_equal(sc[sel], rs) and np.array_equal(nb[sel], rn, equal_nan=True)
+    assert (b >= 0).mean() > 0.5
+
+
 # ---------------------------------------------------------------- ADVICE r01: error paths and part boundaries
 def test_knn2_u8_train_parts_ties(fm3d, orc, ctx):
     """A small query set against >= 4096 train rows: the u8 kernel splits the train tiles into

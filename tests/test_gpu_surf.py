@@ -1,7 +1,8 @@
 """GPU SURF (csrc/fm3d_surf.hip) against the SURF oracle (oracle/orc_surf.c), bit for bit:
 keypoints (position, size, angle, response, octave, Laplacian sign) in KeypointGreater order and
 their descriptors; compute on given keypoints; extractDescriptorsFromPatches; compareWithNNDR
-starting from the images (descriptorsmatcher.cpp:107-174)."""
+starting from the images (descriptorsmatcher.cpp:107-174); the same with Upright 0 (the settings'
+SURF Upright key, descriptorsmatcher.cpp:176-359: dominant orientation + rotated window)."""
 import numpy as np
 import pytest
 
@@ -155,3 +156,74 @@ def test_compare_with_nndr_from_images(fm3d, orc, synth):
     q, t, dd = orc.nndr(idx, dist, 0.55)
     assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t) and np.array_equal(m["distance"], dd)
     assert len(m) > 50
+
+
+# ---------------------------------------------------------------- Upright 0 (SURFInvoker orientation)
+@pytest.mark.parametrize("extended", [1, 0])
+def test_surf_oriented_detect_describe_bitwise(fm3d, orc, synth, extended):
+    """Upright 0: every keypoint's dominant orientation (orient_kernel) and its descriptor of the
+    rotated, bilinear window (describe_kernel) equal the oracle's, keypoints without an orientation
+    sample removed in both"""
+    img = synth.make_frame_pair(2000, seed=3).img1
+    ctx, s = _ctx(fm3d, surfUpright=0, surfExtended=extended)
+    try:
+        k, d = fm3d.SURF(ctx).detect(img, with_descriptors=True)
+    finally:
+        ctx.close()
+    ko = orc.surf_detect(img, s.surfHessianThreshold, s.surfOctaves, s.surfOctaveLayers, upright=False)
+    _, kept, do = orc.surf_describe(img, ko, extended=bool(extended), upright=False)
+    assert len(ko) > 500 and len(np.unique(ko["angle"])) > 100
+    _same_kpts(k, ko)
+    assert np.array_equal(kept, np.arange(len(ko))) and np.array_equal(d, do)
+
+
+def test_surf_oriented_compute_borders_and_axis_angles(fm3d, orc, synth):
+    """Upright 0 on caller keypoints: windows cut by every border (the nearest-pixel branch), a
+    keypoint whose orientation disc misses the integral image (removed), and images whose gradients
+    are exactly horizontal / vertical, so angles 0 / 90 / 180 / 270 whose cos or sin is ~1e-8 --
+    row positions that are not closed-form exact, the kernel's sequential fallback"""
+    img = synth.make_frame_pair(300, seed=8).img1
+    kin = np.zeros(9, dtype=fm3d.KEYPOINT)
+    kin["x"] = [0.0, 639.4, 320.5, 5.0, 100.0, 600.0, 2.5, -300.0, 320.0]
+    kin["y"] = [0.0, 479.9, 240.2, 470.0, 3.0, 10.0, 2.5, -300.0, 240.0]
+    kin["size"] = [9, 20, 4000, 31, 77, 150, 15, 12, 0.0]
+    kin["angle"] = -1
+    xx = np.arange(640)
+    stripes_x = np.tile((128 + 100 * np.sin(xx * 0.05)).astype(np.uint8), (480, 1))
+    ramp_y = np.tile(np.clip(np.arange(480) // 2, 0, 255).astype(np.uint8)[:, None], (1, 640))
+    ctx, _ = _ctx(fm3d, surfUpright=0)
+    try:
+        for im in (img, stripes_x, ramp_y, np.ascontiguousarray(255 - ramp_y)):
+            k, kept, d = fm3d.SURF(ctx).compute(im, kin)
+            ko, kepto, do = orc.surf_describe(im, kin, extended=True, upright=False)
+            assert np.array_equal(kept, kepto) and 7 not in list(kept) and 8 not in list(kept)
+            _same_kpts(k, ko)
+            assert np.array_equal(d, do)
+        angles = set(np.round(orc.surf_describe(stripes_x, kin, upright=False)[0]["angle"], 3)) | set(
+            np.round(orc.surf_describe(ramp_y, kin, upright=False)[0]["angle"], 3))
+        assert angles & {0.0, 90.0, 180.0, 270.0}, angles
+    finally:
+        ctx.close()
+
+
+def test_surf_oriented_patches(fm3d, orc):
+    """extractDescriptorsFromPatches with Upright 0: each patch's keypoint oriented on that patch's
+    own integral image (launch_integral_batch), then its rotated window"""
+    rng = np.random.default_rng(19)
+    patches = rng.integers(0, 256, (24, 128, 128), dtype=np.uint8)
+    yy, xx = np.mgrid[0:128, 0:128]
+    for i in range(24):
+        a = i * 15 * np.pi / 180
+        patches[i] = np.clip(patches[i] // 4 + 96 + 0.6 * ((xx - 64) * np.cos(a) + (yy - 64) * np.sin(a)), 0, 255)
+    ctx, _ = _ctx(fm3d, surfUpright=0)
+    try:
+        d = fm3d.SURF(ctx).extractDescriptorsFromPatches(patches)
+    finally:
+        ctx.close()
+    kp = np.zeros(1, dtype=fm3d.KEYPOINT)
+    kp["x"] = kp["y"] = 64
+    kp["size"] = 128
+    kp["angle"] = -1
+    kp["response"] = 1
+    ref = np.stack([orc.surf_describe(p, kp, extended=True, upright=False)[2][0] for p in patches])
+    assert d.shape == (24, 128) and np.array_equal(d, ref)

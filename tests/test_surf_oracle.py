@@ -151,3 +151,101 @@ def test_descriptors_unit_and_short(orc, synth):
     sx = big[:, :, 0] + big[:, :, 2]
     cos = (sx * short[:, :, 0]).sum(1) / (np.linalg.norm(sx, axis=1) * np.linalg.norm(short[:, :, 0], axis=1))
     assert (cos > 0.999).all()
+
+
+# ---------------------------------------------------------------- Upright 0 (orientation)
+def _fast_atan2_numpy(y, x):
+    """cv::fastAtan2 of OpenCV 2.4.9+ in float32 operations (core/mathfuncs.cpp)"""
+    f = np.float32
+    k = f(180 / math.pi)
+    p1, p3, p5, p7 = f(0.9997878412794807) * k, f(-0.3258083974640975) * k, f(0.1555786518463281) * k, \
+        f(-0.04432655554792128) * k
+    y, x = f(y), f(x)
+    ax, ay = abs(x), abs(y)
+    eps = f(np.finfo(np.float64).eps)
+    if ax >= ay:
+        c = ay / (ax + eps)
+        c2 = c * c
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c
+    else:
+        c = ax / (ay + eps)
+        c2 = c * c
+        a = f(90) - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c
+    if x < 0:
+        a = f(180) - a
+    if y < 0:
+        a = f(360) - a
+    return a
+
+
+def test_fast_atan2_vs_numpy(orc):
+    """the polynomial fastAtan2 (phase(..., true) and fastAtan2 of SURFInvoker): equal to a float32
+    numpy restatement, within 0.01 degree of atan2, in [0, 360)"""
+    rng = np.random.default_rng(11)
+    vals = list(rng.normal(0, 100, (400, 2))) + [(0, 0), (0, 1), (1, 0), (-1, 0), (0, -1), (-0.0, 5), (3, 3), (-3, 3)]
+    for y, x in vals:
+        got = orc.fast_atan2(float(np.float32(y)), float(np.float32(x)))
+        want = float(_fast_atan2_numpy(y, x))
+        assert got == want, (y, x, got, want)
+        assert 0 <= got < 360
+        if (x, y) != (0, 0):
+            exact = math.degrees(math.atan2(float(np.float32(y)), float(np.float32(x)))) % 360
+            assert min(abs(got - exact), 360 - abs(got - exact)) < 0.01
+
+
+def test_orientation_samples_vs_numpy(orc):
+    """SURFInvoker's orientation disc: 113 samples of radius 6, x outer / y inner, Gaussian weights
+    getGaussianKernel(13, 2.5, CV_32F) outer product"""
+    apt, aptw = orc.surf_ori_samples()
+    want = [(i, j) for i in range(-6, 7) for j in range(-6, 7) if i * i + j * j <= 36]
+    assert len(apt) == 113 and [tuple(a) for a in apt] == want
+    x = np.arange(13) - 6.0
+    g = np.exp(-0.5 / (2.5 * 2.5) * x * x).astype(np.float32)
+    g = (g.astype(np.float64) * (1.0 / g.astype(np.float64).sum())).astype(np.float32)
+    assert np.array_equal(aptw, np.array([g[i + 6] * g[j + 6] for i, j in want], dtype=np.float32))
+
+
+@pytest.mark.parametrize("deg", [0, 30, 100, 200, 315])
+def test_orientation_of_a_ramp(orc, deg):
+    """an intensity ramp rising along direction a (image axes, y down): the dx wavelet is +1 on the
+    right, the dy wavelet +1 on the TOP half, so every sample is (X, Y) ~ (cos a, -sin a) and the
+    dominant orientation fastAtan2(-sumY, sumX) is a; the descriptor is unit length"""
+    h = w = 200
+    a = math.radians(deg)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.clip(np.rint(128 + 0.5 * ((xx - 100) * math.cos(a) + (yy - 100) * math.sin(a))), 0, 255).astype(np.uint8)
+    kin = np.zeros(3, dtype=orc.KEYPOINT)
+    kin["x"], kin["y"], kin["size"], kin["angle"] = [100, 90.5, 110.2], [100, 105, 95.7], [20, 15, 31], -1
+    k, kept, d = orc.surf_describe(img, kin, upright=False)
+    assert list(kept) == [0, 1, 2]
+    for ang in k["angle"]:
+        diff = abs(float(ang) - deg)
+        assert min(diff, 360 - diff) < 2.0, (deg, float(ang))
+    assert np.abs(np.linalg.norm(d.astype(np.float64), axis=1) - 1).max() < 1e-5
+
+
+def test_orientation_rotation_covariance(orc, synth):
+    """rotating the image by 90 degrees (np.rot90: exact) moves keypoint (x, y) to (y, W-1-x) and a
+    direction (c, s) to (s, -c): the orientation loses 90 degrees, up to the sampling grid's
+    rounding; the rotation-invariant descriptors stay close"""
+    img = synth.make_frame_pair(300, seed=5).img1[100:356, 100:356]
+    k0 = orc.surf_detect(img, upright=False)
+    r = np.ascontiguousarray(np.rot90(img))  # r[y, x] = img[x, W-1-y]
+    k1 = orc.surf_detect(r, upright=False)
+    _, _, d0 = orc.surf_describe(img, k0, upright=False)
+    _, _, d1 = orc.surf_describe(r, k1, upright=False)
+    W = img.shape[1]
+    # keypoint (x, y) of img -> (y, W-1-x) in r
+    pos1 = {(round(float(x), 2), round(float(y), 2), float(s)): i for i, (x, y, s) in
+            enumerate(zip(k1["x"], k1["y"], k1["size"]))}
+    hits, close, good = 0, 0, 0
+    for i in range(len(k0)):
+        key = (round(float(k0["y"][i]), 2), round(float(W - 1 - k0["x"][i]), 2), float(k0["size"][i]))
+        j = pos1.get(key)
+        if j is None:
+            continue
+        hits += 1
+        diff = abs((float(k0["angle"][i]) - 90) % 360 - float(k1["angle"][j]))
+        close += min(diff, 360 - diff) < 5.0
+        good += float(np.dot(d0[i].astype(np.float64), d1[j].astype(np.float64))) > 0.9
+    assert hits > 20 and close >= 0.9 * hits and good >= 0.8 * hits, (hits, close, good, len(k0))
