@@ -394,3 +394,155 @@ def resize_area21(win):
     out = np.zeros((21, 21), dtype=np.uint8)
     lib().orc_resize_area21(_p(win, ctypes.c_uint8), ctypes.c_int(win.shape[0]), _p(out, ctypes.c_uint8))
     return out
+
+
+# ---------------------------------------------------------------- ORB (orc_orb.c)
+ORB_DEFAULTS = dict(nfeatures=500, scaleFactor=1.2, nlevels=8, edgeThreshold=31, patchSize=31, fastThreshold=20)
+
+
+def _kp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def orb_scale(scaleFactor, level):
+    f = lib().orc_orb_scale
+    f.restype = ctypes.c_float
+    return f(ctypes.c_double(scaleFactor), ctypes.c_int(level))
+
+
+def orb_level_size(w, h, scaleFactor, level):
+    lw, lh = ctypes.c_int(0), ctypes.c_int(0)
+    lib().orc_orb_level_size(ctypes.c_int(w), ctypes.c_int(h), ctypes.c_double(scaleFactor), ctypes.c_int(level),
+                             ctypes.byref(lw), ctypes.byref(lh))
+    return lw.value, lh.value
+
+
+def orb_resize(src, dw, dh):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    out = np.zeros((dh, dw), dtype=np.uint8)
+    lib().orc_orb_resize(_p(src, ctypes.c_uint8), ctypes.c_int(src.shape[1]), ctypes.c_int(src.shape[0]),
+                         _p(out, ctypes.c_uint8), ctypes.c_int(dw), ctypes.c_int(dh))
+    return out
+
+
+def vresize_sse_end(width):
+    return lib().orc_vresize_sse_end(ctypes.c_int(width))
+
+
+def fast9(img, thr=20):
+    """FAST(img, kpts, thr, true): KEYPOINT records in raster order"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    n = lib().orc_fast9(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(thr), None, 0)
+    out = np.zeros(max(n, 1), dtype=KEYPOINT)
+    lib().orc_fast9(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(thr), _kp(out),
+                    ctypes.c_int(n))
+    return out[:n]
+
+
+def nth_element(kpts, nth):
+    """std::nth_element(k, k + nth, k + n, KeypointResponseGreater()) on a copy"""
+    k = np.ascontiguousarray(kpts, dtype=KEYPOINT).copy()
+    lib().orc_nth_element(_kp(k), ctypes.c_long(nth), ctypes.c_long(len(k)))
+    return k
+
+
+def partition_ge(kpts, lo, hi, thr):
+    """std::partition(k + lo, k + hi, response >= thr) on a copy: (array, split index)"""
+    k = np.ascontiguousarray(kpts, dtype=KEYPOINT).copy()
+    f = lib().orc_partition_ge
+    f.restype = ctypes.c_long
+    m = f(_kp(k), ctypes.c_long(lo), ctypes.c_long(hi), ctypes.c_float(thr))
+    return k, int(m)
+
+
+def retain_best(kpts, npts):
+    k = np.ascontiguousarray(kpts, dtype=KEYPOINT).copy()
+    m = lib().orc_retain_best(_kp(k), ctypes.c_int(len(k)), ctypes.c_int(npts))
+    return k[:m]
+
+
+def harris(img, kpts, block=7, k=0.04):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    kk = np.ascontiguousarray(kpts, dtype=KEYPOINT).copy()
+    lib().orc_harris(_p(img, ctypes.c_uint8), ctypes.c_int(img.shape[1]), _kp(kk), ctypes.c_int(len(kk)),
+                     ctypes.c_int(block), ctypes.c_float(k))
+    return kk["response"]
+
+
+def orb_umax(half):
+    u = np.zeros(half + 2, dtype=np.int32)
+    lib().orc_orb_umax(ctypes.c_int(half), _p(u, ctypes.c_int))
+    return u
+
+
+def ic_angle(img, half, x, y):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    u = orb_umax(half)
+    f = lib().orc_ic_angle
+    f.restype = ctypes.c_float
+    return f(_p(img, ctypes.c_uint8), ctypes.c_int(img.shape[1]), ctypes.c_int(half), ctypes.c_float(x),
+             ctypes.c_float(y), _p(u, ctypes.c_int))
+
+
+def orb_blur_kernel():
+    k = np.zeros(7, dtype=np.int32)
+    lib().orc_orb_blur_kernel(_p(k, ctypes.c_int))
+    return k
+
+
+def orb_blur(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.zeros_like(img)
+    lib().orc_orb_blur(_p(img, ctypes.c_uint8), ctypes.c_int(img.shape[1]), ctypes.c_int(img.shape[0]),
+                       _p(out, ctypes.c_uint8))
+    return out
+
+
+def orb_random_pattern(patchSize=31, npoints=512):
+    xy = np.zeros((npoints, 2), dtype=np.int32)
+    lib().orc_orb_random_pattern(ctypes.c_int(patchSize), _p(xy, ctypes.c_int), ctypes.c_int(npoints))
+    return xy
+
+
+def _pattern(pattern, patchSize):
+    if pattern is None:
+        return orb_random_pattern(patchSize)
+    p = np.ascontiguousarray(pattern, dtype=np.int32).reshape(512, 2)
+    return p
+
+
+def orb_detect(img, nfeatures=500, scaleFactor=1.2, nlevels=8, edgeThreshold=31, patchSize=31, fastThreshold=20,
+               pattern=None, descriptors=True):
+    """ORB::operator()(img, noArray(), kpts, desc): (KEYPOINT records level-major, (n, 32) uint8
+    descriptors or None)"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    pat = _pattern(pattern, patchSize)
+    args = (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(nfeatures),
+            ctypes.c_double(scaleFactor), ctypes.c_int(nlevels), ctypes.c_int(edgeThreshold), ctypes.c_int(patchSize),
+            ctypes.c_int(fastThreshold), _p(pat, ctypes.c_int))
+    n = lib().orc_orb_detect(*args, None, None, ctypes.c_int(0))
+    out = np.zeros(max(n, 1), dtype=KEYPOINT)
+    d = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    lib().orc_orb_detect(*args, _kp(out), _p(d, ctypes.c_uint8) if descriptors else None, ctypes.c_int(n))
+    return out[:n], (d[:n] if descriptors else None)
+
+
+def orb_compute(img, kpts, scaleFactor=1.2, edgeThreshold=31, patchSize=31, pattern=None):
+    """ORB::compute on given keypoints: (kept keypoints level-major, input index of each, (m, 32)
+    uint8 descriptors)"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    kin = np.ascontiguousarray(kpts, dtype=KEYPOINT)
+    n = len(kin)
+    kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+    kept = np.zeros(max(n, 1), dtype=np.int32)
+    d = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    pat = _pattern(pattern, patchSize)
+    m = lib().orc_orb_compute(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _kp(kin), ctypes.c_int(n),
+                              ctypes.c_double(scaleFactor), ctypes.c_int(edgeThreshold), ctypes.c_int(patchSize),
+                              _p(pat, ctypes.c_int), _kp(kout), _p(kept, ctypes.c_int), _p(d, ctypes.c_uint8))
+    if m < 0:
+        raise ValueError("ORB compute: a keypoint with a negative octave (OpenCV indexes allKeypoints[-1])")
+    return kout[:m], kept[:m], d[:m]
