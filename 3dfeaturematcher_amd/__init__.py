@@ -23,6 +23,7 @@ LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
+FEAT_SURF, FEAT_ORB, FEAT_OTHER = 0, 1, -1  # fm3d_settings.detectorType / extractorType
 DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
@@ -35,6 +36,7 @@ EXPORTS = (
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
     "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
+    "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2",
@@ -62,6 +64,8 @@ class Settings(ctypes.Structure):
         ("detectorType", ctypes.c_int), ("extractorType", ctypes.c_int), ("surfHessianThreshold", ctypes.c_double),
         ("surfOctaves", ctypes.c_int), ("surfOctaveLayers", ctypes.c_int), ("surfExtended", ctypes.c_int),
         ("surfUpright", ctypes.c_int),
+        ("orbNumFeatures", ctypes.c_int), ("orbScaleFactor", ctypes.c_double), ("orbNumLevels", ctypes.c_int),
+        ("orbEdgeThreshold", ctypes.c_int), ("orbPatchSize", ctypes.c_int), ("orbFastThreshold", ctypes.c_int),
     ]
 
     @staticmethod
@@ -220,9 +224,18 @@ class DescriptorsMatcher:
 
     def compareWithNNDRImages(self, epsilon: float, image_a: np.ndarray, image_b: np.ndarray,
                               matches: np.ndarray | None = None):
-        """compareWithNNDR (descriptorsmatcher.cpp:107-131) with the detection it starts with: SURF
-        detect + compute on both images (the settings' detector / extractor, on the GPU), knnMatch,
-        NNDR.  Returns (matches appended as the reference does, kpts_a, kpts_b, desc_a, desc_b)."""
+        """compareWithNNDR (descriptorsmatcher.cpp:107-131) with the detection it starts with: the
+        settings' detector + extractor on both images on the GPU (SURF; or ORB: detect, then compute
+        on the detected keypoints as the reference's two calls, Hamming matching as its binary
+        extractor types select, :64), knnMatch, NNDR.  Returns (matches appended as the reference
+        does, kpts_a, kpts_b, desc_a, desc_b)."""
+        S = self.ctx.settings
+        if S.detectorType == FEAT_ORB and S.extractorType == FEAT_ORB:
+            orb = ORB(self.ctx)
+            ka, _, da = orb.compute(image_a, orb.detect(image_a))
+            kb, _, db = orb.compute(image_b, orb.detect(image_b))
+            m = DescriptorsMatcher(self.ctx, binary=True).compareWithNNDR(epsilon, da, db, matches)
+            return m, ka, kb, da, db
         surf = SURF(self.ctx)
         ka, da = surf.detect(image_a, with_descriptors=True)
         kb, db = surf.detect(image_b, with_descriptors=True)
@@ -301,6 +314,61 @@ class SURF:
         self.ctx.check(lib().fm3d_extract_descriptors_from_patches(self.ctx.handle, _ptr(P, ctypes.c_uint8),
                                                                    P.shape[0], P.shape[1], _ptr(out, ctypes.c_float)))
         return out[:P.shape[0]]
+
+
+class ORB:
+    """The settings' ORB detector / extractor (FeatureOptions DetectorType / ExtractorType ORB,
+    descriptorsmatcher.cpp:273-279, 336-341: cv::ORB(NumFeatures, ScaleFactor, NumLevels) of OpenCV
+    2.4) on the GPU.  Descriptors are 32 bytes (Hamming)."""
+
+    descriptorSize = 32
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def set_pattern(self, xy) -> None:
+        """the 512 rBRIEF test points (OpenCV's bit_pattern_31_ for patchSize 31); None: the default
+        makeRandomPattern(orbPatchSize)"""
+        if xy is None:
+            self.ctx.check(lib().fm3d_orb_set_pattern(self.ctx.handle, None, 0))
+            return
+        p = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1)
+        if p.size != 1024:
+            raise ValueError("pattern: 512 (x, y) points")
+        self.ctx.check(lib().fm3d_orb_set_pattern(self.ctx.handle, _ptr(p, ctypes.c_int32), 512))
+
+    def detect(self, image: np.ndarray, with_descriptors: bool = False):
+        """FeatureDetector::detect (descriptorsmatcher.cpp:110-111): KEYPOINT records, level-major;
+        with_descriptors: (keypoints, (n, 32) uint8) of ORB::operator()'s one call"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap = max(1024, self.ctx.settings.orbNumFeatures * 2)
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            d = np.zeros((cap, 32), dtype=np.uint8) if with_descriptors else None
+            n = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_orb_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(k), cap,
+                                                 ctypes.byref(n), _ptr(d, ctypes.c_uint8) if d is not None else None))
+            if n.value <= cap:
+                break
+            cap = n.value
+        k = k[:n.value]
+        return (k, d[:n.value]) if with_descriptors else k
+
+    def compute(self, image: np.ndarray, keypoints: np.ndarray):
+        """DescriptorExtractor::compute (descriptorsmatcher.cpp:113-114): (kept keypoints level-major,
+        input index of each, (m, 32) uint8)"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        kin = np.ascontiguousarray(keypoints, dtype=KEYPOINT)
+        n = len(kin)
+        kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+        kept = np.zeros(max(n, 1), dtype=np.int32)
+        desc = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        m = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_orb_compute(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(kin), n, _vp(kout),
+                                              _ptr(kept, ctypes.c_int32), ctypes.byref(m), _ptr(desc, ctypes.c_uint8)))
+        return kout[:m.value], kept[:m.value], desc[:m.value]
 
 
 class SingleCameraTriangulator:

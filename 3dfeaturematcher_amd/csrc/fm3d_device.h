@@ -6,6 +6,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <float.h>
 #include <stdint.h>
 
 #include "fm3d_detmath.h"
@@ -141,6 +142,28 @@ __host__ __device__ inline double enorm2(const double* x) {
     e.add(x[0]);
     e.add(x[1]);
     return e.finish();
+}
+
+// cv::fastAtan2 / phase(..., true) of OpenCV 2.4.9+ (core/mathfuncs.cpp, the polynomial; degrees in
+// [0, 360)); SURF's orientation and ORB's IC_Angle.  Needs the correctly rounded float division
+// (-fhip-fp32-correctly-rounded-divide-sqrt)
+__device__ __forceinline__ float fast_atan2f(float y, float x) {
+    constexpr float P1 = 0.9997878412794807f * (float)(180 / M_PI);
+    constexpr float P3 = -0.3258083974640975f * (float)(180 / M_PI);
+    constexpr float P5 = 0.1555786518463281f * (float)(180 / M_PI);
+    constexpr float P7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a;
+    if (ax >= ay) {
+        const float c = ay / (ax + (float)DBL_EPSILON), c2 = c * c;
+        a = (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    } else {
+        const float c = ax / (ay + (float)DBL_EPSILON), c2 = c * c;
+        a = 90.f - (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
 }
 
 }  // namespace fm3d

@@ -76,6 +76,9 @@ struct fm3d_ctx {
     // SURF detection / description
     DevBuf sfImg, sfSum, sfDet, sfTr, sfLayers, sfMids, sfCand, sfCount, sfSortTmp, sfFlag, sfPos, sfKp, sfKin, sfSrc,
         sfDesc, sfDW, sfAng;
+    // ORB detection / description
+    DevBuf orbPyr, orbTab, orbLev, orbMap, orbFlag, orbPos, orbKp, orbR, orbBlur, orbDesc, orbPat;
+    std::vector<int> orbUserPattern;  // fm3d_orb_set_pattern (empty: makeRandomPattern(orbPatchSize))
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     int nCU = 0;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
@@ -729,6 +732,193 @@ const fm3d::SurfOri& surf_ori() {
     return ori;
 }
 
+// ---------------- ORB (host side of fm3d_orb.hip; the oracle's orc_orb.c formulas) ----------------
+// getScale (orb.cpp): (float)pow(scaleFactor, level)
+float orb_scale(double scaleFactor, int level) { return (float)std::pow(scaleFactor, (double)level); }
+
+struct OrbPlan {
+    std::vector<fm3d::OrbLevel> L;
+    long long total = 0;
+};
+
+// the pyramid levels: size cvRound(cols * (1 / getScale)), concatenated pixel after pixel
+OrbPlan orb_plan(int w, int h, double scaleFactor, int nl) {
+    OrbPlan P;
+    for (int l = 0; l < nl; l++) {
+        const float scale = 1 / orb_scale(scaleFactor, l);
+        fm3d::OrbLevel v;
+        v.w = (int)std::lrint((float)(w * scale));
+        v.h = (int)std::lrint((float)(h * scale));
+        v.first = P.total;
+        P.total += (long long)std::max(v.w, 0) * std::max(v.h, 0);
+        P.L.push_back(v);
+    }
+    return P;
+}
+
+short sat_short(float v) {
+    const long i = std::lrint(v);
+    return (short)(i < -32768 ? -32768 : (i > 32767 ? 32767 : i));
+}
+
+// resize(INTER_LINEAR)'s fixed-point tables for src (sw x sh) -> dst (dw x dh), packed as
+// [xofs dw][yofs dh] ints then [alpha 2dw][beta 2dh] shorts; returns xmax
+int orb_resize_tabs(int sw, int sh, int dw, int dh, std::vector<int>& ofs, std::vector<short>& ab) {
+    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) {
+            fx = 0;
+            sx = 0;
+        }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) {
+                fx = 0;
+                sx = sw - 1;
+            }
+        }
+        ofs.push_back(sx);
+        ab.push_back(sat_short((1.f - fx) * 2048));
+        ab.push_back(sat_short(fx * 2048));
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        const int sy = (int)std::floor(fy);
+        fy -= sy;
+        ofs.push_back(sy);
+        ab.push_back(sat_short((1.f - fy) * 2048));
+        ab.push_back(sat_short(fy * 2048));
+    }
+    return xmax;
+}
+
+// VResizeLinearVec_32s8u's columns: the 16-wide loop, then the 4-wide one while x < width - 4
+int orb_vresize_sse_end(int width) {
+    int x = 0;
+    for (; x <= width - 16; x += 16) {}
+    for (; x < width - 4; x += 4) {}
+    return x;
+}
+
+// image -> level 0, then every level from the previous one (orb.cpp's pyramid loop)
+int orb_build_pyramid(fm3d_ctx* c, const uint8_t* img, int w, int h, const OrbPlan& P) {
+    const int nl = (int)P.L.size();
+    HIPCHK(c, c->orbPyr.ensure((size_t)P.total + 64));
+    HIPCHK(c, c->orbLev.ensure(P.L.size() * sizeof(fm3d::OrbLevel)));
+    HIPCHK(c, hipMemcpyAsync(c->orbPyr.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->orbLev.p, P.L.data(), P.L.size() * sizeof(fm3d::OrbLevel), hipMemcpyHostToDevice,
+                             c->stream));
+    std::vector<int> ofs;
+    std::vector<short> ab;
+    std::vector<int> xmax(nl, 0);
+    std::vector<size_t> oOfs(nl, 0), oAb(nl, 0);
+    for (int l = 1; l < nl; l++) {
+        oOfs[l] = ofs.size();
+        oAb[l] = ab.size();
+        xmax[l] = orb_resize_tabs(P.L[l - 1].w, P.L[l - 1].h, P.L[l].w, P.L[l].h, ofs, ab);
+    }
+    const size_t ofsBytes = ofs.size() * sizeof(int);
+    HIPCHK(c, c->orbTab.ensure(ofsBytes + ab.size() * sizeof(short) + 64));
+    if (!ofs.empty()) {
+        HIPCHK(c, hipMemcpyAsync(c->orbTab.p, ofs.data(), ofsBytes, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(static_cast<char*>(c->orbTab.p) + ofsBytes, ab.data(), ab.size() * sizeof(short),
+                                 hipMemcpyHostToDevice, c->stream));
+    }
+    const int* T = c->orbTab.as<int>();
+    const short* A = reinterpret_cast<const short*>(static_cast<const char*>(c->orbTab.p) + ofsBytes);
+    uint8_t* pyr = c->orbPyr.as<uint8_t>();
+    for (int l = 1; l < nl; l++) {
+        const fm3d::OrbLevel &s0 = P.L[l - 1], &d0 = P.L[l];
+        if (d0.w <= 0 || d0.h <= 0 || s0.w <= 0 || s0.h <= 0) continue;
+        fm3d::launch_orb_resize(pyr + s0.first, s0.w, s0.h, pyr + d0.first, d0.w, d0.h, T + oOfs[l], A + oAb[l],
+                                T + oOfs[l] + d0.w, A + oAb[l] + 2 * d0.w, xmax[l], orb_vresize_sse_end(d0.w),
+                                c->stream);
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // ofs / ab leave scope
+    return FM3D_OK;
+}
+
+// KeyPointsFilter::retainBest with libstdc++'s own nth_element / partition (the order they leave
+// decides which tied keypoints survive and the output order)
+int orb_retain_best(fm3d_keypoint* k, int n, int npts) {
+    if (npts >= 0 && n > npts) {
+        if (npts == 0) return 0;
+        auto greater = [](const fm3d_keypoint& a, const fm3d_keypoint& b) { return a.response > b.response; };
+        std::nth_element(k, k + npts, k + n, greater);
+        const float amb = k[npts - 1].response;
+        return (int)(std::partition(k + npts, k + n, [amb](const fm3d_keypoint& p) { return p.response >= amb; }) - k);
+    }
+    return n;
+}
+
+// the 512-point pattern: the caller's, else makeRandomPattern(patchSize) (cv::RNG(0x34985739))
+int orb_upload_pattern(fm3d_ctx* c, int patchSize) {
+    std::vector<int> xy = c->orbUserPattern;
+    if (xy.empty()) {
+        uint64_t state = 0x34985739;
+        const int a = -patchSize / 2, b = patchSize / 2 + 1;
+        for (int i = 0; i < 1024; i++) {
+            state = (uint64_t)(unsigned)state * 4164903690U + (unsigned)(state >> 32);
+            xy.push_back((int)((unsigned)state % (unsigned)(b - a) + (unsigned)a));
+        }
+    }
+    HIPCHK(c, c->orbPat.ensure(1024 * sizeof(int)));
+    HIPCHK(c, hipMemcpyAsync(c->orbPat.p, xy.data(), 1024 * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+fm3d::OrbBlurK orb_blur_kernel() {
+    fm3d::OrbBlurK k;
+    float g[7];
+    const double scale2X = -0.5 / (2.0 * 2.0);
+    double sum = 0;
+    for (int i = 0; i < 7; i++) {
+        const double x = i - 3.0;
+        g[i] = (float)std::exp(scale2X * x * x);
+        sum += g[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < 7; i++) g[i] = (float)(g[i] * sum);
+    for (int i = 0; i < 7; i++) k.ik[i] = (int)std::lrint(g[i] * 256.f);
+    for (int i = 0; i < 4; i++) k.fk[i] = (float)(k.ik[3 + i] * (1. / 65536));
+    return k;
+}
+
+// blurred levels + descriptors of the (device) keypoints kp[0..n) in level coordinates
+int orb_describe(fm3d_ctx* c, const OrbPlan& P, int n, uint8_t* desc) {
+    if (n <= 0) return FM3D_OK;
+    int r;
+    if ((r = orb_upload_pattern(c, c->s.orbPatchSize))) return r;
+    HIPCHK(c, c->orbR.ensure((size_t)P.total * sizeof(int) + 64));
+    HIPCHK(c, c->orbBlur.ensure((size_t)P.total + 64));
+    HIPCHK(c, c->orbDesc.ensure((size_t)n * 32));
+    fm3d::launch_orb_blur(c->orbPyr.as<uint8_t>(), c->orbLev.as<fm3d::OrbLevel>(), (int)P.L.size(), P.total,
+                          orb_blur_kernel(), c->orbR.as<int>(), c->orbBlur.as<uint8_t>(), c->stream);
+    fm3d::launch_orb_desc(c->orbBlur.as<uint8_t>(), c->orbLev.as<fm3d::OrbLevel>(), c->orbKp.as<fm3d_keypoint>(), n,
+                          c->orbPat.as<int>(), c->orbDesc.as<uint8_t>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(desc, c->orbDesc.p, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
+    return FM3D_OK;
+}
+
+int orb_check_settings(fm3d_ctx* c) {
+    const fm3d_settings& S = c->s;
+    if (S.orbNumLevels < 1 || S.orbNumLevels > 64 || !(S.orbScaleFactor > 1.0) || S.orbNumFeatures < 0 ||
+        S.orbEdgeThreshold < 0 || S.orbPatchSize < 2 || S.orbPatchSize > 124 || S.orbFastThreshold < 0)
+        return fail(c, FM3D_ERR_INVALID, "ORB NumLevels / ScaleFactor / NumFeatures / edgeThreshold / patchSize out of range");
+    // the descriptor reads pattern points up to patchSize/2 * sqrt(2) + 1 from the centre and the
+    // blur 3 more: inside the edge border, as OpenCV's defaults guarantee
+    if (S.orbEdgeThreshold < (int)std::ceil(S.orbPatchSize / 2 * 1.4143) + 4)
+        return fail(c, FM3D_ERR_INVALID, "ORB edgeThreshold too small for patchSize (reads past the level border)");
+    return FM3D_OK;
+}
+
 int surf_upload_image(fm3d_ctx* c, const uint8_t* img, int w, int h) {
     HIPCHK(c, c->sfImg.ensure((size_t)w * h));
     HIPCHK(c, hipMemcpyAsync(c->sfImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
@@ -787,7 +977,9 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->slab, &c->slabI1,
                       &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->A8, &c->B8,
                       &c->sfImg, &c->sfSum, &c->sfDet, &c->sfTr, &c->sfLayers, &c->sfMids, &c->sfCand, &c->sfCount,
-                      &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW, &c->sfAng};
+                      &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW, &c->sfAng,
+                      &c->orbPyr, &c->orbTab, &c->orbLev, &c->orbMap, &c->orbFlag, &c->orbPos, &c->orbKp, &c->orbR,
+                      &c->orbBlur, &c->orbDesc, &c->orbPat};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();
@@ -1506,6 +1698,203 @@ int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, i
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(desc, c->sfDesc.p, (size_t)P * dsize * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+int fm3d_orb_set_pattern(fm3d_ctx* c, const int32_t* xy, int npoints) {
+    if (!c || (xy && npoints != 512)) return FM3D_ERR_INVALID;
+    c->orbUserPattern.clear();
+    if (xy) c->orbUserPattern.assign(xy, xy + 1024);
+    return FM3D_OK;
+}
+
+int fm3d_orb_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoint* kpts, int cap, int* n,
+                    uint8_t* desc) {
+    if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
+    const fm3d_settings& S = c->s;
+    if (S.detectorType != FM3D_FEAT_ORB || (desc && S.extractorType != FM3D_FEAT_ORB))
+        return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' detector (extractor) is not ORB");
+    int r;
+    if ((r = orb_check_settings(c))) return r;
+    hipSetDevice(c->device);
+    const int nl = S.orbNumLevels, half = S.orbPatchSize / 2;
+    // computeKeyPoints: features per level
+    std::vector<int> nper(nl);
+    {
+        const float factor = (float)(1.0 / S.orbScaleFactor);
+        float nd = S.orbNumFeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+        int sum = 0;
+        for (int l = 0; l < nl - 1; l++) {
+            nper[l] = (int)std::lrint(nd);
+            sum += nper[l];
+            nd *= factor;
+        }
+        nper[nl - 1] = std::max(S.orbNumFeatures - sum, 0);
+    }
+    const OrbPlan P = orb_plan(w, h, S.orbScaleFactor, nl);
+    if ((r = orb_build_pyramid(c, img, w, h, P))) return r;
+    // FAST + non-max + border over all levels, compacted in level-major raster order
+    if (P.total > INT32_MAX / 2) return fail(c, FM3D_ERR_INVALID, "image too large for the ORB pyramid");
+    const int tot = (int)P.total;
+    if ((r = ensure_scan_tmp(c, tot))) return r;
+    HIPCHK(c, c->orbMap.ensure((size_t)tot * sizeof(uint16_t) + 64));
+    HIPCHK(c, c->orbFlag.ensure((size_t)(tot + 1) * sizeof(int)));
+    HIPCHK(c, c->orbPos.ensure((size_t)(tot + 1) * sizeof(int)));
+    fm3d::launch_orb_fast(c->orbPyr.as<uint8_t>(), c->orbLev.as<fm3d::OrbLevel>(), nl, P.total, S.orbFastThreshold,
+                          S.orbEdgeThreshold, c->orbMap.as<uint16_t>(), c->orbFlag.as<int>(), c->stream);
+    fm3d::launch_exclusive_scan(c->orbFlag.as<int>(), tot, c->orbPos.as<int>(), c->count.as<int>(), c->scanTmp.p,
+                                c->stream);
+    HIPCHK(c, hipGetLastError());
+    int nc = 0;
+    HIPCHK(c, hipMemcpyAsync(&nc, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, c->orbKp.ensure((size_t)(nc + 1) * sizeof(fm3d_keypoint)));
+    fm3d::launch_orb_fast_scatter(c->orbMap.as<uint16_t>(), c->orbLev.as<fm3d::OrbLevel>(), nl, P.total,
+                                  c->orbFlag.as<int>(), c->orbPos.as<int>(), c->orbKp.as<fm3d_keypoint>(), c->stream);
+    std::vector<fm3d_keypoint> k((size_t)nc + 1);
+    if (nc > 0)
+        HIPCHK(c, hipMemcpyAsync(k.data(), c->orbKp.p, (size_t)nc * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // per level: retainBest(2 * n), Harris, retainBest(n)
+    std::vector<int> start(nl + 1, 0);
+    for (int i = 0; i < nc; i++) start[k[i].octave + 1]++;
+    for (int l = 0; l < nl; l++) start[l + 1] += start[l];
+    std::vector<fm3d_keypoint> kb;
+    std::vector<int> bstart(nl + 1, 0);
+    for (int l = 0; l < nl; l++) {
+        const int m = orb_retain_best(k.data() + start[l], start[l + 1] - start[l], 2 * nper[l]);
+        kb.insert(kb.end(), k.begin() + start[l], k.begin() + start[l] + m);
+        bstart[l + 1] = (int)kb.size();
+    }
+    const int nb = (int)kb.size();
+    if (nb > 0) {
+        HIPCHK(c, hipMemcpyAsync(c->orbKp.p, kb.data(), (size_t)nb * sizeof(fm3d_keypoint), hipMemcpyHostToDevice,
+                                 c->stream));
+        fm3d::launch_orb_harris(c->orbPyr.as<uint8_t>(), c->orbLev.as<fm3d::OrbLevel>(), c->orbKp.as<fm3d_keypoint>(),
+                                nb, c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(kb.data(), c->orbKp.p, (size_t)nb * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    std::vector<fm3d_keypoint> kf;
+    for (int l = 0; l < nl; l++) {
+        const int m = orb_retain_best(kb.data() + bstart[l], bstart[l + 1] - bstart[l], nper[l]);
+        const float sf = orb_scale(S.orbScaleFactor, l);
+        for (int i = 0; i < m; i++) {
+            fm3d_keypoint q = kb[bstart[l] + i];
+            q.octave = l;
+            q.size = S.orbPatchSize * sf;
+            kf.push_back(q);
+        }
+    }
+    const int nf = (int)kf.size(), nw = std::min(nf, cap);
+    if (nf > 0) {
+        fm3d::OrbUmax um{};
+        {  // computeKeyPoints' umax
+            const int vmax = (int)std::floor(half * std::sqrt(2.f) / 2 + 1);
+            const int vmin = (int)std::ceil(half * std::sqrt(2.f) / 2);
+            for (int v = 0; v <= vmax; ++v) um.u[v] = (int)std::lrint(std::sqrt((double)half * half - v * v));
+            for (int v = half, v0 = 0; v >= vmin; --v) {
+                while (um.u[v0] == um.u[v0 + 1]) ++v0;
+                um.u[v] = v0;
+                ++v0;
+            }
+        }
+        HIPCHK(c, hipMemcpyAsync(c->orbKp.p, kf.data(), (size_t)nf * sizeof(fm3d_keypoint), hipMemcpyHostToDevice,
+                                 c->stream));
+        fm3d::launch_orb_angle(c->orbPyr.as<uint8_t>(), c->orbLev.as<fm3d::OrbLevel>(), c->orbKp.as<fm3d_keypoint>(), nf,
+                               half, um, c->stream);
+        HIPCHK(c, hipGetLastError());
+        if (desc && nw > 0 && (r = orb_describe(c, P, nw, desc))) return r;
+        HIPCHK(c, hipMemcpyAsync(kf.data(), c->orbKp.p, (size_t)nf * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    for (int i = 0; i < nw; i++) {
+        fm3d_keypoint q = kf[i];
+        if (q.octave != 0) {
+            const float sf = orb_scale(S.orbScaleFactor, q.octave);
+            q.x *= sf;
+            q.y *= sf;
+        }
+        kpts[i] = q;
+    }
+    *n = nf;
+    return FM3D_OK;
+}
+
+int fm3d_orb_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,
+                     fm3d_keypoint* kout, int32_t* kept, int* nOut, uint8_t* desc) {
+    if (!c || !img || !nOut || w <= 0 || h <= 0 || n < 0 || (n > 0 && (!kpts || !kout || !desc)))
+        return FM3D_ERR_INVALID;
+    const fm3d_settings& S = c->s;
+    if (S.extractorType != FM3D_FEAT_ORB) return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' extractor is not ORB");
+    int r;
+    if ((r = orb_check_settings(c))) return r;
+    *nOut = 0;
+    if (n == 0) return FM3D_OK;
+    const int b = S.orbEdgeThreshold;
+    // runByKeypointSize(FLT_EPSILON) (NaN kept), runByImageBorder(edgeThreshold) on rounded positions
+    std::vector<int> src;
+    int L = 0;
+    for (int i = 0; i < n; i++) {
+        const float sz = kpts[i].size;
+        if (sz < FLT_EPSILON || sz > FLT_MAX) continue;
+        if (b > 0) {
+            if (h <= 2 * b || w <= 2 * b) continue;
+            const long ix = std::lrint(kpts[i].x), iy = std::lrint(kpts[i].y);
+            if (!(ix >= b && ix < b + (w - 2 * b) && iy >= b && iy < b + (h - 2 * b))) continue;
+        }
+        if (kpts[i].octave < 0) return fail(c, FM3D_ERR_INVALID, "ORB compute: keypoint with a negative octave");
+        if (kpts[i].octave >= 64) return fail(c, FM3D_ERR_INVALID, "ORB compute: keypoint octave >= 64");
+        L = std::max(L, kpts[i].octave + 1);
+        src.push_back(i);
+    }
+    if (src.empty()) return FM3D_OK;
+    // grouped by octave (input order within a level), positions in level coordinates
+    std::vector<fm3d_keypoint> k;
+    std::vector<int> order;
+    for (int l = 0; l < L; l++) {
+        const float inv = 1 / orb_scale(S.orbScaleFactor, l);
+        for (int i : src) {
+            if (kpts[i].octave != l) continue;
+            fm3d_keypoint q = kpts[i];
+            if (l != 0) {
+                q.x *= inv;
+                q.y *= inv;
+            }
+            k.push_back(q);
+            order.push_back(i);
+        }
+    }
+    hipSetDevice(c->device);
+    const OrbPlan P = orb_plan(w, h, S.orbScaleFactor, L);
+    for (const fm3d_keypoint& q : k) {  // the descriptor's reads stay inside the level
+        const fm3d::OrbLevel& lv = P.L[q.octave];
+        const long ix = std::lrint(q.x), iy = std::lrint(q.y);
+        const int reach = (int)std::ceil(S.orbPatchSize / 2 * 1.4143) + 4;
+        if (ix < reach || iy < reach || ix >= lv.w - reach || iy >= lv.h - reach)
+            return fail(c, FM3D_ERR_INVALID, "ORB compute: keypoint octave inconsistent with its position");
+    }
+    if ((r = orb_build_pyramid(c, img, w, h, P))) return r;
+    const int m = (int)k.size();
+    HIPCHK(c, c->orbKp.ensure((size_t)m * sizeof(fm3d_keypoint)));
+    HIPCHK(c, hipMemcpyAsync(c->orbKp.p, k.data(), (size_t)m * sizeof(fm3d_keypoint), hipMemcpyHostToDevice, c->stream));
+    if ((r = orb_describe(c, P, m, desc))) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < m; i++) {
+        fm3d_keypoint q = k[i];
+        if (q.octave != 0) {
+            const float sf = orb_scale(S.orbScaleFactor, q.octave);
+            q.x *= sf;
+            q.y *= sf;
+        }
+        kout[i] = q;
+        if (kept) kept[i] = order[i];
+    }
+    *nOut = m;
     return FM3D_OK;
 }
 

@@ -176,6 +176,33 @@ void launch_surf_keep(const fm3d_keypoint* in, int n, int w, int h, int* flag, i
 void launch_surf_describe(const uint8_t* img, size_t imgStride, int w, int h, const fm3d_keypoint* kp, int n,
                           const float* DW, int extended, int upright, float* desc, hipStream_t s);
 
+// ---------------- ORB (fm3d_orb.hip) ----------------
+struct OrbLevel {     // one pyramid level, levels concatenated pixel after pixel
+    int w, h;
+    long long first;  // first pixel of the level in the concatenation (== its byte offset)
+};
+struct OrbUmax {  // computeKeyPoints' umax (halfPatchSize <= 62)
+    int u[64];
+};
+struct OrbBlurK {  // GaussianBlur(7x7, 2): the x256 fixed-point kernel; the SSE2 column weights
+    int ik[7];
+    float fk[4];
+};
+void launch_orb_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh, const int* xofs,
+                       const short* alpha, const int* yofs, const short* beta, int xmax, int xs, hipStream_t s);
+// map: corner | score per pixel; flag: the keypoints FAST + non-max + the edge border keep
+void launch_orb_fast(const uint8_t* pyr, const OrbLevel* L, int nL, long long total, int thr, int border,
+                     uint16_t* map, int* flag, hipStream_t s);
+void launch_orb_fast_scatter(const uint16_t* map, const OrbLevel* L, int nL, long long total, const int* flag,
+                             const int* pos, fm3d_keypoint* out, hipStream_t s);
+void launch_orb_harris(const uint8_t* pyr, const OrbLevel* L, fm3d_keypoint* kp, int n, hipStream_t s);
+void launch_orb_angle(const uint8_t* pyr, const OrbLevel* L, fm3d_keypoint* kp, int n, int half, const OrbUmax& um,
+                      hipStream_t s);
+void launch_orb_blur(const uint8_t* pyr, const OrbLevel* L, int nL, long long total, const OrbBlurK& bk, int* R,
+                     uint8_t* out, hipStream_t s);
+void launch_orb_desc(const uint8_t* blur, const OrbLevel* L, const fm3d_keypoint* kp, int n, const int* pattern,
+                     uint8_t* desc, hipStream_t s);
+
 // ---------------- compaction ----------------
 // out[k] = in[i] for flag[i] != 0, stable; *count (device) = number kept.  tmp >= scan_tmp_bytes(n).
 size_t scan_tmp_bytes(int n);

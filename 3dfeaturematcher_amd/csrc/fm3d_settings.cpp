@@ -137,6 +137,12 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->surfOctaveLayers = 2;
     s->surfExtended = 1;
     s->surfUpright = 1;
+    s->orbNumFeatures = 500;  // cv::ORB's defaults (FeatureOptions.OrbDetector, absent from settings.yml)
+    s->orbScaleFactor = 1.2;
+    s->orbNumLevels = 8;
+    s->orbEdgeThreshold = 31;
+    s->orbPatchSize = 31;
+    s->orbFastThreshold = 20;
     return FM3D_OK;
 }
 
@@ -183,8 +189,15 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
         std::string mode = "STATIC", det, ex;
         str("FeatureOptions.DetectorMode", mode);
         if (str("FeatureOptions.DetectorType", det))
-            s->detectorType = (mode == "STATIC" && det == "SURF") ? FM3D_FEAT_SURF : FM3D_FEAT_OTHER;
-        if (str("FeatureOptions.ExtractorType", ex)) s->extractorType = ex == "SURF" ? FM3D_FEAT_SURF : FM3D_FEAT_OTHER;
+            s->detectorType = mode != "STATIC" ? FM3D_FEAT_OTHER
+                              : det == "SURF"  ? FM3D_FEAT_SURF
+                              : det == "ORB"   ? FM3D_FEAT_ORB
+                                               : FM3D_FEAT_OTHER;
+        if (str("FeatureOptions.ExtractorType", ex))
+            s->extractorType = ex == "SURF" ? FM3D_FEAT_SURF : ex == "ORB" ? FM3D_FEAT_ORB : FM3D_FEAT_OTHER;
+        get_i(kv, "FeatureOptions.OrbDetector.NumFeatures", &s->orbNumFeatures);
+        get_d(kv, "FeatureOptions.OrbDetector.ScaleFactor", &s->orbScaleFactor);
+        get_i(kv, "FeatureOptions.OrbDetector.NumLevels", &s->orbNumLevels);
         get_d(kv, "FeatureOptions.SurfDetector.HessianThreshold", &s->surfHessianThreshold);
         get_i(kv, "FeatureOptions.SurfDetector.NumOctaves", &s->surfOctaves);
         get_i(kv, "FeatureOptions.SurfDetector.NumOctaveLayers", &s->surfOctaveLayers);

@@ -34,7 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "fm3d_kernels.h"
-#include "fm3d_detmath.h"
+#include "fm3d_device.h"
 
 namespace fm3d {
 
@@ -264,26 +264,6 @@ __global__ void keep_scatter_kernel(const fm3d_keypoint* __restrict__ k, const i
 
 
 // ---------------------------------------------------------------- orientation (Upright 0)
-// cv::fastAtan2 / phase(..., true) of OpenCV 2.4.9+ (the polynomial; degrees in [0, 360))
-__device__ __forceinline__ float fast_atan2f(float y, float x) {
-    constexpr float P1 = 0.9997878412794807f * (float)(180 / M_PI);
-    constexpr float P3 = -0.3258083974640975f * (float)(180 / M_PI);
-    constexpr float P5 = 0.1555786518463281f * (float)(180 / M_PI);
-    constexpr float P7 = -0.04432655554792128f * (float)(180 / M_PI);
-    const float ax = fabsf(x), ay = fabsf(y);
-    float a;
-    if (ax >= ay) {
-        const float c = ay / (ax + (float)DBL_EPSILON), c2 = c * c;
-        a = (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
-    } else {
-        const float c = ax / (ay + (float)DBL_EPSILON), c2 = c * c;
-        a = 90.f - (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
-    }
-    if (x < 0) a = 180.f - a;
-    if (y < 0) a = 360.f - a;
-    return a;
-}
-
 // resizeHaarPattern of SURFInvoker's 4x4 orientation wavelets (dx_s / dy_s) to size gws
 __device__ inline void ori_haar(int gws, int W1, SurfHF* dx, SurfHF* dy) {
     const int DXO[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};

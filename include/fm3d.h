@@ -72,14 +72,23 @@ typedef struct fm3d_settings {
        else (the reference's exit(-10)); thetas / rays of the circular method (:47-48) */
     int neighMethod, neighThetas, neighRays;
     /* FeatureOptions (descriptorsmatcher.cpp:176-359): DetectorMode STATIC + DetectorType /
-       ExtractorType SURF are FM3D_FEAT_SURF; anything else FM3D_FEAT_OTHER (no GPU implementation).
+       ExtractorType SURF are FM3D_FEAT_SURF, ORB FM3D_FEAT_ORB; anything else FM3D_FEAT_OTHER (no GPU
+       implementation).
        SurfDetector.HessianThreshold / NumOctaves / NumOctaveLayers / Extended / Upright */
     int detectorType, extractorType;
     double surfHessianThreshold;
     int surfOctaves, surfOctaveLayers, surfExtended, surfUpright;
+    /* FeatureOptions.OrbDetector.NumFeatures / ScaleFactor / NumLevels (cv::ORB's first three
+       arguments, descriptorsmatcher.cpp:276-279, 338-341); defaults OpenCV's 500 / 1.2 / 8.  The
+       extensions after them are cv::ORB's defaulted arguments: edgeThreshold 31, patchSize 31, and
+       computeKeyPoints' hard-coded FAST threshold 20 */
+    int orbNumFeatures;
+    double orbScaleFactor;
+    int orbNumLevels, orbEdgeThreshold, orbPatchSize, orbFastThreshold;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
+#define FM3D_FEAT_ORB 1
 #define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
@@ -251,11 +260,12 @@ int fm3d_circular_neighborhoods(fm3d_ctx *ctx, const double *points, const doubl
 
 /* ---------------- feature detection + description (SURF, OpenCV 2.4 nonfree) ---------------- */
 /* FeatureDetector::detect of the settings' SURF detector (descriptorsmatcher.cpp:110-111 via
-   generateDetector :176-293): fastHessianDetector + the upright SURFInvoker pass, keypoints in
-   KeypointGreater order (response, size, octave, y, x descending).  *n = all keypoints found; the
-   first min(*n, cap) are written to kpts.  desc (may be NULL): their descriptors too (the extractor's
-   compute on the same image, :113-114), min(*n, cap) x (surfExtended ? 128 : 64) floats.
-   FM3D_ERR_UNSUPPORTED unless detector (and, with desc, extractor) is SURF with Upright 1. */
+   generateDetector :176-293): fastHessianDetector + the SURFInvoker pass (Upright 1: angle 270;
+   Upright 0: the dominant orientation, keypoints without one removed), keypoints in KeypointGreater
+   order (response, size, octave, y, x descending).  *n = all keypoints found; the first min(*n, cap)
+   are written to kpts.  desc (may be NULL): their descriptors too (the extractor's compute on the
+   same image, :113-114), min(*n, cap) x (surfExtended ? 128 : 64) floats.
+   FM3D_ERR_UNSUPPORTED unless detector (and, with desc, extractor) is SURF. */
 int fm3d_surf_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, fm3d_keypoint *kpts, int cap, int *n,
                      float *desc);
 /* DescriptorExtractor::compute of the settings' SURF extractor for given keypoints (:113-114,
@@ -270,6 +280,28 @@ int fm3d_surf_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, 
    (floor(size/2), floor(size/2)) of size `size`, described by the settings' SURF extractor; the
    reference's descriptors Mat, one row per patch: P x (128 | 64) floats. */
 int fm3d_extract_descriptors_from_patches(fm3d_ctx *ctx, const uint8_t *patches, int P, int size, float *desc);
+
+/* ---------------- feature detection + description (ORB, OpenCV 2.4) ---------------- */
+/* FeatureDetector::detect of the settings' ORB detector (descriptorsmatcher.cpp:273-279:
+   cv::ORB(orbNumFeatures, orbScaleFactor, orbNumLevels), edgeThreshold / patchSize orbEdgeThreshold /
+   orbPatchSize, FAST threshold orbFastThreshold): level-major keypoints (FAST + Harris retainBest
+   per level, IC_Angle orientation), positions scaled to the image.  *n = all; min(*n, cap) written.
+   desc (may be NULL): ORB::operator()'s descriptors of the same call, min(*n, cap) x 32 bytes (the
+   reference computes them with a separate compute, fm3d_orb_compute, whose float round trip of the
+   positions can move them by an ulp).  FM3D_ERR_UNSUPPORTED unless the detector is ORB. */
+int fm3d_orb_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, fm3d_keypoint *kpts, int cap, int *n,
+                    uint8_t *desc);
+/* DescriptorExtractor::compute of the settings' ORB extractor (descriptorsmatcher.cpp:113-114,
+   336-341): size < FLT_EPSILON and the orbEdgeThreshold border (rounded positions) removed, the rest
+   grouped by octave (level-major, input order within a level) and described on the blurred level
+   of their octave.  kout / kept (input index, may be NULL): capacity n; desc: n x 32 bytes; *nOut =
+   kept count.  FM3D_ERR_INVALID for a kept keypoint with a negative octave. */
+int fm3d_orb_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const fm3d_keypoint *kpts, int n,
+                     fm3d_keypoint *kout, int32_t *kept, int *nOut, uint8_t *desc);
+/* the 512 rBRIEF test points (x, y interleaved): OpenCV's bit_pattern_31_ for patchSize 31 is not
+   part of this library -- pass it here for descriptor parity with OpenCV; NULL restores the default,
+   makeRandomPattern(orbPatchSize) (cv::RNG(0x34985739), OpenCV's pattern for every other patchSize). */
+int fm3d_orb_set_pattern(fm3d_ctx *ctx, const int32_t *xy, int npoints);
 
 /* ---------------- the whole hot path, device resident ---------------- */
 /* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */
