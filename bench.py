@@ -243,6 +243,8 @@ def main():
         if dist is None:  # bit-identity across builds / boxes (A/B runs compare it)
             out["records_sha256"] = records_digest(mine.tobytes())
             out.update(verify_against_fixture(args, wl, workload, pair, mine))
+        elif sharded:  # the merged records of the N-GPU run against the committed oracle run
+            out.update(verify_against_fixture(args, wl, workload, pair, merged))
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:
@@ -255,11 +257,14 @@ def main():
 
 
 def verify_against_fixture(args, wl, workload, pair, rec):
-    """The headline run's own correctness proof: for the default C4 workload, the generated inputs'
-    digests and ALL survivor records against the committed oracle run of the same frame pair
-    (tests/golden/full_c4.npz: the CPU oracle in DETMATH mode over every inlier, made in the
-    container by tests/golden/make_full_fixtures.py).  Other workloads: "verified": null."""
-    default = (workload == "c4" and wl == WORKLOADS["c4"] and args.seed == 7 and args.ray == 64 and args.levels == 3)
+    """The headline run's own correctness proof: the generated inputs' digests and the survivor
+    records against the committed oracle run of the same frame pair (the CPU oracle in DETMATH mode,
+    made in the container by tests/golden/make_full_fixtures.py): for the default C4 workload ALL
+    records (tests/golden/full_c4.npz); for the default C5 workload -- whole on one GPU or merged
+    from N -- the records of every 10th 4,096-query block (tests/golden/full_c5sub.npz, 102,400
+    queries against all 1M train rows).  Other workloads: "verified": null."""
+    default = (workload in WORKLOADS and wl == WORKLOADS[workload] and args.seed == 7 and args.ray == 64 and
+               args.levels == 3)
     if not default:
         return {"verified": None, "verified_note": "no committed oracle fixture for this workload"}
     import importlib.util
@@ -267,14 +272,19 @@ def verify_against_fixture(args, wl, workload, pair, rec):
     spec = importlib.util.spec_from_file_location("make_full_fixtures", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    fx = mod.load_fixture("c4")
+    name = "c4" if workload == "c4" else "c5sub"
+    fx = mod.load_fixture(name)
     got = mod.input_digests(pair)
     inputs_ok = all(got[k] == v for k, v in fx["digests"].items())
-    records_ok = rec.tobytes() == fx["records"].tobytes()
+    checked = rec
+    if name == "c5sub":
+        qsel = mod.subset_queries(mod.WORKLOADS["c5sub"], len(pair.desc1))
+        checked = rec[np.isin(rec["queryIdx"], qsel)]
+    records_ok = checked.tobytes() == fx["records"].tobytes()
     return {"verified": bool(inputs_ok and records_ok),
-            "verification": {"fixture": "tests/golden/full_c4.npz", "inputs_digest_equal": bool(inputs_ok),
-                             "records_equal": bool(records_ok), "records": int(len(rec)),
-                             "fixture_records": int(len(fx["records"])),
+            "verification": {"fixture": f"tests/golden/full_{name}.npz", "inputs_digest_equal": bool(inputs_ok),
+                             "records_equal": bool(records_ok), "records_checked": int(len(checked)),
+                             "records": int(len(rec)), "fixture_records": int(len(fx["records"])),
                              "fixture_records_sha256": str(fx["records_sha256"])}}
 
 

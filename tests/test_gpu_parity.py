@@ -769,13 +769,20 @@ def test_c5_1m_keypoints_query_blocks(fm3d, orc, synth):
     """BASELINE configs[4] (C5) on one GPU: one 1M-keypoint frame pair (640x480, sub-pixel
     keypoints; pixelsRay 64, pyramids 3) run whole and as the 4 block-cyclic
     shares of a 4-GPU run (bench.py --gpus 4): the merged share records are byte-identical to
-    the whole run.  A seeded 2,000-query sample goes through the oracle (match, NNDR, DLT, LM in
-    DETMATH mode): the whole run's records of those queries are exactly the oracle's survivors."""
+    the whole run.  Every 10th 4,096-query block (102,400 queries, 36,448 survivors) against the
+    committed oracle run over all 1M train rows (tests/golden/full_c5sub.npz),
+    record for record; and a seeded 2,000-query sample through the oracle here (match, NNDR, DLT, LM
+    in DETMATH mode): the whole run's records of those queries are exactly the oracle's survivors."""
     shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    mod, fx = full_fixture("c5sub")
     fp = synth.make_frame_pair(1_000_000, 640, 480, seed=7)
+    assert_inputs(mod, fx, fp)
     s = _settings(fm3d, fp.cam, pixelsRay=64, pyramids=3)
     n = len(fp.desc1)
     full = shard.run_shard(fp, s, 0, n)
+    qsel = mod.subset_queries(mod.WORKLOADS["c5sub"], n)
+    sub10 = full[np.isin(full["queryIdx"], qsel)]
+    assert len(sub10) == len(fx["records"]) == 36_448 and sub10.tobytes() == fx["records"].tobytes()
     parts = [shard.run_shard_queries(fp, s, shard.query_blocks(n, 4, r)) for r in range(4)]
     merged = np.concatenate(parts)
     merged = merged[np.argsort(merged["queryIdx"], kind="stable")]
