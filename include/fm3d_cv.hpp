@@ -501,9 +501,9 @@ public:
     }
 
 private:
-    // the detector + extractor (:110-115): the settings' SURF on the GPU; another detector type has
-    // no GPU implementation, so its output comes from the images' side files (<image>.kpts.f32 and
-    // <image>.desc.u8 / .desc.f32), or from the caller's keypoints + descriptors
+    // the detector + extractor (:110-115): the settings' SURF or ORB on the GPU; another detector
+    // type has no GPU implementation, so its output comes from the images' side files
+    // (<image>.kpts.f32 and <image>.desc.u8 / .desc.f32), or from the caller's keypoints + descriptors
     void features(const cv::Mat& img, std::vector<cv::KeyPoint>& kpts, cv::Mat& d) {
         if (s_.detectorType == FM3D_FEAT_SURF && s_.extractorType == FM3D_FEAT_SURF) {
             static_assert(sizeof(cv::KeyPoint) == sizeof(fm3d_keypoint), "cv::KeyPoint layout");
@@ -524,6 +524,29 @@ private:
             if (n > 0) std::memcpy(static_cast<void*>(kpts.data()), k.data(), (size_t)n * sizeof(fm3d_keypoint));
             d.create(n, dsize, CV_32FC1);
             if (n > 0) std::memcpy(d.data, f.data(), (size_t)n * dsize * sizeof(float));
+            return;
+        }
+        if (s_.detectorType == FM3D_FEAT_ORB && s_.extractorType == FM3D_FEAT_ORB) {
+            // the reference's two calls (:110-115): detect, then compute on the detected keypoints
+            fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
+            int cap = std::max(1024, 2 * s_.orbNumFeatures), n = 0;
+            std::vector<fm3d_keypoint> k;
+            for (;;) {
+                k.resize(cap);
+                fm3d::compat::check(c, fm3d_orb_detect(c, img.data, img.cols, img.rows, k.data(), cap, &n, nullptr));
+                if (n <= cap) break;
+                cap = n;
+            }
+            std::vector<fm3d_keypoint> ko(n > 0 ? n : 1);
+            std::vector<uint8_t> desc((size_t)(n > 0 ? n : 1) * 32);
+            int m = 0;
+            if (n > 0)
+                fm3d::compat::check(c, fm3d_orb_compute(c, img.data, img.cols, img.rows, k.data(), n, ko.data(), nullptr,
+                                                        &m, desc.data()));
+            kpts.assign(m, cv::KeyPoint());
+            if (m > 0) std::memcpy(static_cast<void*>(kpts.data()), ko.data(), (size_t)m * sizeof(fm3d_keypoint));
+            d.create(m, 32, CV_8UC1);
+            if (m > 0) std::memcpy(d.data, desc.data(), (size_t)m * 32);
             return;
         }
         if (!kpts.empty() && !d.empty()) return;
