@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--ray", type=int, default=64)
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--desc", choices=("sift", "orb"), default="sift",
+                    help="descriptor kind of the synthetic pair (orb: 256-bit, Hamming; BASELINE C3 with "
+                         "--keypoints 10000 --seed 102 --nndr 0.8 --ray 32|64)")
+    ap.add_argument("--nndr", type=float, default=0.55)
     ap.add_argument("--lm-waves", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -109,10 +113,11 @@ def main():
 
     t_gen = time.time()
     seed = args.seed + (1000 * rank if args.weak else 0)
-    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=seed)
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=seed, desc=args.desc)
     t_gen = time.time() - t_gen
     s = fm3d.Settings.default()
     s.set_camera(pair.cam)
+    s.nndrEpsilon = args.nndr
     s.pixelsRay = args.ray
     s.pyramids = args.levels
     s.lmWaves = args.lm_waves
@@ -125,7 +130,7 @@ def main():
     pipe = fm3d.Pipeline(ctx)
     d1, k1 = (pair.desc1, pair.kp1) if qidx is None else (pair.desc1[qidx], pair.kp1[qidx])
     t_up = time.perf_counter()
-    pipe.upload(d1, pair.desc2, k1, pair.kp2, pair.img1, pair.img2, query_offset=0)
+    pipe.upload(d1, pair.desc2, k1, pair.kp2, pair.img1, pair.img2, query_offset=0, binary=args.desc == "orb")
     upload_ms = (time.perf_counter() - t_up) * 1e3
 
     rec_buf = None
@@ -188,7 +193,7 @@ def main():
     evals = float(np.mean([st["lm"]["evaluations"] for st in stats]))
     last_st = stats[-1]
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.desc == "sift":
         cpu = cpu_baseline(pair, s, last_st, args)
 
     if rank == 0:
@@ -198,6 +203,9 @@ def main():
                     f"keypoints), full pipeline, pixelsRay {args.ray}, pyramids {args.levels}, " +
                     (f"query blocks sharded over {world} GPUs, RCCL all-gather of survivor records" if sharded else
                      "whole on one GPU (the reference point of the N-GPU strong-scaling runs)"))
+        elif args.desc == "orb":
+            desc = (f"C3-like: {kp_k}k ORB-256 (Hamming) keypoints per {wl['width']}x{wl['height']} frame pair, "
+                    f"NNDR {args.nndr}, full pipeline, pixelsRay {args.ray}, pyramids {args.levels}")
         else:
             desc = (f"C4: {kp_k}k SIFT-128 (u8) keypoints per {wl['width']}x{wl['height']} frame pair, full "
                     f"pipeline, pixelsRay {args.ray}, pyramids {args.levels}")
@@ -259,26 +267,27 @@ def main():
 def verify_against_fixture(args, wl, workload, pair, rec):
     """The headline run's own correctness proof: the generated inputs' digests and the survivor
     records against the committed oracle run of the same frame pair (the CPU oracle in DETMATH mode,
-    made in the container by tests/golden/make_full_fixtures.py): for the default C4 workload ALL
-    records (tests/golden/full_c4.npz); for the default C5 workload -- whole on one GPU or merged
-    from N -- the records of every 10th 4,096-query block (tests/golden/full_c5sub.npz, 102,400
-    queries against all 1M train rows).  Other workloads: "verified": null."""
-    default = (workload in WORKLOADS and wl == WORKLOADS[workload] and args.seed == 7 and args.ray == 64 and
-               args.levels == 3)
-    if not default:
-        return {"verified": None, "verified_note": "no committed oracle fixture for this workload"}
+    made in the container by tests/golden/make_full_fixtures.py): for the default C4 workload and the
+    C3 lines (10k ORB, --seed 102 --nndr 0.8, pixelsRay 32 or 64) ALL records (full_c4.npz,
+    full_c3r32.npz, full_c3r64.npz); for the default C5 workload -- whole on one GPU or merged from
+    N -- the records of every 10th 4,096-query block (full_c5sub.npz, 102,400 queries against all 1M
+    train rows).  Other workloads: "verified": null."""
     import importlib.util
     path = os.path.join(ROOT, "tests", "golden", "make_full_fixtures.py")
     spec = importlib.util.spec_from_file_location("make_full_fixtures", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    name = "c4" if workload == "c4" else "c5sub"
+    mine = dict(n=wl["keypoints"], w=wl["width"], h=wl["height"], seed=args.seed, desc=args.desc, ray=args.ray,
+                levels=args.levels, eps=args.nndr)
+    name = next((k for k, v in mod.WORKLOADS.items() if {x: v[x] for x in mine} == mine), None)
+    if name is None:
+        return {"verified": None, "verified_note": "no committed oracle fixture for this workload"}
     fx = mod.load_fixture(name)
     got = mod.input_digests(pair)
     inputs_ok = all(got[k] == v for k, v in fx["digests"].items())
     checked = rec
-    if name == "c5sub":
-        qsel = mod.subset_queries(mod.WORKLOADS["c5sub"], len(pair.desc1))
+    qsel = mod.subset_queries(mod.WORKLOADS[name], len(pair.desc1))
+    if qsel is not None:
         checked = rec[np.isin(rec["queryIdx"], qsel)]
     records_ok = checked.tobytes() == fx["records"].tobytes()
     return {"verified": bool(inputs_ok and records_ok),

@@ -1,6 +1,6 @@
 """Drive the kernels outside the C4 bench for rocprofv3 --kernel-trace --stats:
 SURF detect + describe on the VGA frames (Upright 1 = the reference's settings, and Upright 0),
-extractDescriptorsFromPatches, the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
+extractDescriptorsFromPatches, ORB detect + describe and compute (2,000 / 10,000 features), the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
 of the 10k-ORB pair) and the circular neighbourhoods of the C4 inliers.  Product path only (no
 oracle); each leg timed with host wall clock after a warm-up call, printed as one JSON line.
 
@@ -41,6 +41,20 @@ def main():
             patches = np.random.default_rng(9).integers(0, 256, (1000, 128, 128), dtype=np.uint8)
             _, ms = timed(lambda: fm3d.SURF(ctx).extractDescriptorsFromPatches(patches), 3)
             res[f"surf_patches_1000x128_upright{upright}"] = {"ms": round(ms, 3)}
+        finally:
+            ctx.close()
+    # ORB (DetectorType / ExtractorType ORB) on the VGA frame: 2,000 and 10,000 features
+    for nf in (2000, 10_000):
+        s = fm3d.Settings.default()
+        s.detectorType = s.extractorType = fm3d.FEAT_ORB
+        s.orbNumFeatures = nf
+        ctx = fm3d.Context(s)
+        try:
+            orb = fm3d.ORB(ctx)
+            (k, d), ms = timed(lambda: orb.detect(pair.img1, with_descriptors=True), 5)
+            res[f"orb_detect_describe_vga_{nf}"] = {"keypoints": int(len(k)), "ms": round(ms, 3)}
+            (kc, _, _), ms = timed(lambda: orb.compute(pair.img1, k), 5)
+            res[f"orb_compute_vga_{nf}"] = {"keypoints": int(len(kc)), "ms": round(ms, 3)}
         finally:
             ctx.close()
     # C3 NCC leg: the 10k-ORB pair's DLT inliers, 16 hypotheses, pixelsRay 32
