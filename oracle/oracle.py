@@ -546,3 +546,166 @@ def orb_compute(img, kpts, scaleFactor=1.2, edgeThreshold=31, patchSize=31, patt
     if m < 0:
         raise ValueError("ORB compute: a keypoint with a negative octave (OpenCV indexes allKeypoints[-1])")
     return kout[:m], kept[:m], d[:m]
+
+
+# ---------------------------------------------------------------- SIFT (orc_sift.c)
+SIFT_DEFAULTS = dict(nfeatures=0, nOctaveLayers=3, contrastThreshold=0.04, edgeThreshold=10.0, sigma=1.6)
+
+
+def _fn(name, restype):
+    f = getattr(lib(), name)
+    f.restype = restype
+    return f
+
+
+def cv_exp_at(x, k, n):
+    """element k of cv::exp over an array of n floats (SSE2 loop or scalar loop by position)"""
+    return _fn("orc_cv_exp_at", ctypes.c_float)(ctypes.c_float(x), ctypes.c_int(k), ctypes.c_int(n))
+
+
+def cv_exp2f(y):
+    return _fn("orc_cv_exp2f", ctypes.c_float)(ctypes.c_float(y))
+
+
+def cv_cosf(x):
+    return _fn("orc_cv_cosf", ctypes.c_float)(ctypes.c_float(x))
+
+
+def cv_sinf(x):
+    return _fn("orc_cv_sinf", ctypes.c_float)(ctypes.c_float(x))
+
+
+def cv_atan2_deg(y, x):
+    return _fn("orc_cv_atan2_deg", ctypes.c_float)(ctypes.c_float(y), ctypes.c_float(x))
+
+
+def sift_gauss_kernel(sigma):
+    n = lib().orc_sift_gauss_ksize(ctypes.c_double(sigma))
+    k = np.zeros(n, dtype=np.float32)
+    lib().orc_sift_gauss_kernel(ctypes.c_double(sigma), _p(k, ctypes.c_float))
+    return k
+
+
+def sift_blur(img, sigma):
+    """GaussianBlur(img, Size(), sigma) of a float32 image"""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros_like(img)
+    lib().orc_sift_blur(_p(img, ctypes.c_float), _p(out, ctypes.c_float), ctypes.c_int(img.shape[1]),
+                        ctypes.c_int(img.shape[0]), ctypes.c_double(sigma))
+    return out
+
+
+def sift_resize_linear(img, dw, dh):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros((dh, dw), dtype=np.float32)
+    lib().orc_sift_resize_linear(_p(img, ctypes.c_float), ctypes.c_int(img.shape[1]), ctypes.c_int(img.shape[0]),
+                                 _p(out, ctypes.c_float), ctypes.c_int(dw), ctypes.c_int(dh))
+    return out
+
+
+def sift_resize_nn(img, dw, dh):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros((dh, dw), dtype=np.float32)
+    lib().orc_sift_resize_nn(_p(img, ctypes.c_float), ctypes.c_int(img.shape[1]), ctypes.c_int(img.shape[0]),
+                             _p(out, ctypes.c_float), ctypes.c_int(dw), ctypes.c_int(dh))
+    return out
+
+
+def sift_num_octaves(w, h, first_octave=-1):
+    return lib().orc_sift_num_octaves(ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(first_octave))
+
+
+def sift_sigmas(layers=3, sigma=1.6):
+    s = np.zeros(layers + 3)
+    lib().orc_sift_sigmas(ctypes.c_int(layers), ctypes.c_double(sigma), _p(s))
+    return s
+
+
+def sift_pyramid(img, first_octave=-1, octaves=None, layers=3, sigma=1.6, dog=False):
+    """the Gaussian (or DoG) pyramid levels, octave-major: a list of float32 images"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    if octaves is None:
+        octaves = sift_num_octaves(w, h, first_octave)
+    f = _fn("orc_sift_pyramid", ctypes.c_long)
+    args = (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(first_octave),
+            ctypes.c_int(octaves), ctypes.c_int(layers), ctypes.c_double(sigma), ctypes.c_int(1 if dog else 0))
+    tot = f(*args, None, None)
+    if tot < 0:
+        raise ValueError("SIFT pyramid: an octave would be empty")
+    nl = octaves * (layers + 2 if dog else layers + 3)
+    out = np.zeros(max(tot, 1), dtype=np.float32)
+    sizes = np.zeros(2 * nl, dtype=np.int32)
+    f(*args, _p(out, ctypes.c_float), _p(sizes, ctypes.c_int))
+    levels, o = [], 0
+    for i in range(nl):
+        lw, lh = int(sizes[2 * i]), int(sizes[2 * i + 1])
+        levels.append(out[o:o + lw * lh].reshape(lh, lw))
+        o += lw * lh
+    return levels
+
+
+def sift_solve3(H, b):
+    H = np.ascontiguousarray(H, dtype=np.float32).ravel()
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    x = np.zeros(3, dtype=np.float32)
+    lib().orc_sift_solve3(_p(H, ctypes.c_float), _p(b, ctypes.c_float), _p(x, ctypes.c_float))
+    return x
+
+
+def sift_ori_hist(level, x, y, radius, sigma, n=36):
+    level = np.ascontiguousarray(level, dtype=np.float32)
+    hist = np.zeros(n, dtype=np.float32)
+    f = _fn("orc_sift_ori_hist", ctypes.c_float)
+    m = f(_p(level, ctypes.c_float), ctypes.c_int(level.shape[1]), ctypes.c_int(level.shape[0]), ctypes.c_int(x),
+          ctypes.c_int(y), ctypes.c_int(radius), ctypes.c_float(sigma), _p(hist, ctypes.c_float), ctypes.c_int(n))
+    return m, hist
+
+
+def sift_descriptor(level, x, y, ori, scl):
+    level = np.ascontiguousarray(level, dtype=np.float32)
+    d = np.zeros(128, dtype=np.float32)
+    lib().orc_sift_descriptor(_p(level, ctypes.c_float), ctypes.c_int(level.shape[1]), ctypes.c_int(level.shape[0]),
+                              ctypes.c_float(x), ctypes.c_float(y), ctypes.c_float(ori), ctypes.c_float(scl),
+                              _p(d, ctypes.c_float))
+    return d
+
+
+def remove_duplicated(kpts):
+    k = np.ascontiguousarray(kpts, dtype=KEYPOINT).copy()
+    m = lib().orc_remove_duplicated(_kp(k), ctypes.c_int(len(k)))
+    return k[:m]
+
+
+def sift_detect(img, nfeatures=0, nOctaveLayers=3, contrastThreshold=0.04, edgeThreshold=10.0, sigma=1.6, raw=False):
+    """FeatureDetector::detect with cv::SIFT: KEYPOINT records (raw: the findScaleSpaceExtrema list in
+    doubled-image coordinates, before removeDuplicated / retainBest)"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    args = (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(nfeatures),
+            ctypes.c_int(nOctaveLayers), ctypes.c_double(contrastThreshold), ctypes.c_double(edgeThreshold),
+            ctypes.c_double(sigma), ctypes.c_int(1 if raw else 0))
+    n = lib().orc_sift_detect(*args, None, ctypes.c_int(0))
+    if n < 0:
+        raise ValueError("SIFT detect: an octave would be empty")
+    out = np.zeros(max(n, 1), dtype=KEYPOINT)
+    lib().orc_sift_detect(*args, _kp(out), ctypes.c_int(n))
+    return out[:n]
+
+
+def sift_compute(img, kpts, nOctaveLayers=3, sigma=1.6):
+    """DescriptorExtractor::compute with cv::SIFT: (kept keypoints, input index of each, (m, 128)
+    float32 descriptors holding integers 0..255)"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    kin = np.ascontiguousarray(kpts, dtype=KEYPOINT)
+    n = len(kin)
+    kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+    kept = np.zeros(max(n, 1), dtype=np.int32)
+    d = np.zeros((max(n, 1), 128), dtype=np.float32)
+    m = lib().orc_sift_compute(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(nOctaveLayers),
+                               ctypes.c_double(sigma), _kp(kin), ctypes.c_int(n), _kp(kout), _p(kept, ctypes.c_int),
+                               _p(d, ctypes.c_float))
+    if m < 0:
+        raise ValueError("SIFT compute: OpenCV asserts (octave < -1, layer > nOctaveLayers + 2, or an empty octave)")
+    return kout[:m], kept[:m], d[:m]
