@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
-FEAT_SURF, FEAT_ORB, FEAT_OTHER = 0, 1, -1  # fm3d_settings.detectorType / extractorType
+FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_OTHER = 0, 1, 2, -1  # fm3d_settings.detectorType / extractorType
 DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
@@ -36,7 +36,8 @@ EXPORTS = (
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
     "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
-    "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern",
+    "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern", "fm3d_sift_detect", "fm3d_sift_compute",
+    "fm3d_sift_pyramid",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2",
@@ -66,6 +67,9 @@ class Settings(ctypes.Structure):
         ("surfUpright", ctypes.c_int),
         ("orbNumFeatures", ctypes.c_int), ("orbScaleFactor", ctypes.c_double), ("orbNumLevels", ctypes.c_int),
         ("orbEdgeThreshold", ctypes.c_int), ("orbPatchSize", ctypes.c_int), ("orbFastThreshold", ctypes.c_int),
+        ("siftNumFeatures", ctypes.c_int), ("siftOctaveLayers", ctypes.c_int),
+        ("siftContrastThreshold", ctypes.c_double), ("siftEdgeThreshold", ctypes.c_double),
+        ("siftSigma", ctypes.c_double),
     ]
 
     @staticmethod
@@ -225,11 +229,17 @@ class DescriptorsMatcher:
     def compareWithNNDRImages(self, epsilon: float, image_a: np.ndarray, image_b: np.ndarray,
                               matches: np.ndarray | None = None):
         """compareWithNNDR (descriptorsmatcher.cpp:107-131) with the detection it starts with: the
-        settings' detector + extractor on both images on the GPU (SURF; or ORB: detect, then compute
-        on the detected keypoints as the reference's two calls, Hamming matching as its binary
+        settings' detector + extractor on both images on the GPU (SURF; SIFT; or ORB: detect, then
+        compute on the detected keypoints as the reference's two calls, Hamming matching as its binary
         extractor types select, :64), knnMatch, NNDR.  Returns (matches appended as the reference
         does, kpts_a, kpts_b, desc_a, desc_b)."""
         S = self.ctx.settings
+        if S.detectorType == FEAT_SIFT and S.extractorType == FEAT_SIFT:
+            sift = SIFT(self.ctx)
+            ka, _, da = sift.compute(image_a, sift.detect(image_a))
+            kb, _, db = sift.compute(image_b, sift.detect(image_b))
+            m = self.compareWithNNDR(epsilon, da, db, matches)
+            return m, ka, kb, da, db
         if S.detectorType == FEAT_ORB and S.extractorType == FEAT_ORB:
             orb = ORB(self.ctx)
             ka, _, da = orb.compute(image_a, orb.detect(image_a))
@@ -368,6 +378,74 @@ class ORB:
         m = ctypes.c_int(0)
         self.ctx.check(lib().fm3d_orb_compute(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(kin), n, _vp(kout),
                                               _ptr(kept, ctypes.c_int32), ctypes.byref(m), _ptr(desc, ctypes.c_uint8)))
+        return kout[:m.value], kept[:m.value], desc[:m.value]
+
+
+class SIFT:
+    """The settings' SIFT detector / extractor (FeatureOptions DetectorType / ExtractorType SIFT,
+    descriptorsmatcher.cpp:243-257, 302-315: cv::SIFT(NumFeatures, NumOctaveLayers, ContrastThreshold,
+    EdgeThreshold, Sigma) of OpenCV 2.4 nonfree) on the GPU.  Descriptors are 128 floats holding the
+    integers 0..255 (the matcher takes them on its exact integer path)."""
+
+    descriptorSize = 128
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def detect(self, image: np.ndarray, with_descriptors: bool = False):
+        """FeatureDetector::detect (descriptorsmatcher.cpp:110-111): KEYPOINT records in the
+        reference's order; with_descriptors: (keypoints, (n, 128) float32) -- the extractor's compute
+        on the same image"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap = max(4096, self.ctx.settings.siftNumFeatures * 2)
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            d = np.zeros((cap, 128), dtype=np.float32) if with_descriptors else None
+            n = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_sift_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(k), cap,
+                                                  ctypes.byref(n), _ptr(d, ctypes.c_float) if d is not None else None))
+            if n.value <= cap:
+                break
+            cap = n.value
+        k = k[:n.value]
+        return (k, d[:n.value]) if with_descriptors else k
+
+    def pyramid(self, image: np.ndarray, first_octave: int = -1, octaves: int | None = None, dog: bool = False):
+        """buildGaussianPyramid (dog False) / buildDoGPyramid levels, octave-major: float32 images"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        if octaves is None:
+            bw, bh = (2 * w, 2 * h) if first_octave < 0 else (w, h)
+            octaves = int(np.rint(np.log(min(bw, bh)) / np.log(2.0) - 2)) - first_octave
+        nl = octaves * (self.ctx.settings.siftOctaveLayers + (2 if dog else 3))
+        sizes = np.zeros(2 * nl, dtype=np.int32)
+        tot = ctypes.c_int64(0)
+        args = (self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, first_octave, octaves, 1 if dog else 0)
+        self.ctx.check(lib().fm3d_sift_pyramid(*args, None, _ptr(sizes, ctypes.c_int32), ctypes.byref(tot)))
+        out = np.zeros(max(tot.value, 1), dtype=np.float32)
+        self.ctx.check(lib().fm3d_sift_pyramid(*args, _ptr(out, ctypes.c_float), None, ctypes.byref(tot)))
+        levels, o = [], 0
+        for i in range(nl):
+            lw, lh = int(sizes[2 * i]), int(sizes[2 * i + 1])
+            levels.append(out[o:o + lw * lh].reshape(lh, lw))
+            o += lw * lh
+        return levels
+
+    def compute(self, image: np.ndarray, keypoints: np.ndarray):
+        """DescriptorExtractor::compute (descriptorsmatcher.cpp:113-114): (kept keypoints, input index
+        of each, (m, 128) float32)"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        kin = np.ascontiguousarray(keypoints, dtype=KEYPOINT)
+        n = len(kin)
+        kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+        kept = np.zeros(max(n, 1), dtype=np.int32)
+        desc = np.zeros((max(n, 1), 128), dtype=np.float32)
+        m = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_sift_compute(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(kin), n,
+                                               _vp(kout), _ptr(kept, ctypes.c_int32), ctypes.byref(m),
+                                               _ptr(desc, ctypes.c_float)))
         return kout[:m.value], kept[:m.value], desc[:m.value]
 
 

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -79,6 +80,9 @@ struct fm3d_ctx {
     // ORB detection / description
     DevBuf orbPyr, orbTab, orbLev, orbMap, orbFlag, orbPos, orbKp, orbR, orbBlur, orbDesc, orbPat;
     std::vector<int> orbUserPattern;  // fm3d_orb_set_pattern (empty: makeRandomPattern(orbPatchSize))
+    // SIFT detection / description
+    DevBuf siftImg, siftBase, siftG, siftD, siftGL, siftDL, siftTaps, siftScan, siftFlag, siftPos, siftCand, siftAng,
+        siftNpk, siftKp, siftDesc;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     int nCU = 0;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
@@ -919,6 +923,232 @@ int orb_check_settings(fm3d_ctx* c) {
     return FM3D_OK;
 }
 
+// ---------------- SIFT (host side of fm3d_sift.hip; the oracle's orc_sift.c formulas) ----------------
+// the pyramid plan: level sizes and offsets, Gaussian levels nOct * (L + 3), DoG levels nOct * (L + 2)
+struct SiftPlan {
+    int firstOctave = 0, nOct = 0, L = 0;
+    std::vector<fm3d::SiftLevel> G, D;
+    long long gTotal = 0, dTotal = 0;
+};
+
+// false when an octave would be empty (OpenCV's resize asserts there)
+bool sift_plan(int w, int h, int firstOctave, int nOct, int L, SiftPlan& P) {
+    P = SiftPlan{};
+    P.firstOctave = firstOctave;
+    P.nOct = nOct;
+    P.L = L;
+    int ow = firstOctave < 0 ? 2 * w : w, oh = firstOctave < 0 ? 2 * h : h;
+    for (int o = 0; o < nOct; o++) {
+        if (o > 0) {
+            ow /= 2;
+            oh /= 2;
+        }
+        if (ow < 1 || oh < 1) return false;
+        for (int i = 0; i < L + 3; i++) {
+            P.G.push_back({ow, oh, P.gTotal});
+            P.gTotal += (long long)ow * oh;
+        }
+        for (int i = 0; i < L + 2; i++) {
+            P.D.push_back({ow, oh, P.dTotal});
+            P.dTotal += (long long)ow * oh;
+        }
+    }
+    return true;
+}
+
+int sift_num_octaves(int w, int h, int firstOctave) {
+    const int bw = firstOctave < 0 ? 2 * w : w, bh = firstOctave < 0 ? 2 * h : h;
+    return (int)std::lrint(std::log((double)std::min(bw, bh)) / std::log(2.) - 2) - firstOctave;
+}
+
+// getGaussianKernel(cvRound(sigma*8+1)|1, sigma, CV_32F)
+std::vector<float> sift_gauss_kernel(double sigma) {
+    const int n = (int)std::lrint(sigma * 4 * 2 + 1) | 1;
+    std::vector<float> cf(n);
+    const double scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < n; i++) {
+        const double x = i - (n - 1) * 0.5;
+        cf[i] = (float)std::exp(scale2X * x * x);
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; i++) cf[i] = (float)(cf[i] * sum);
+    return cf;
+}
+
+constexpr int kSiftMaxTaps = 65;  // the blur tile's LDS (r <= 32: sigma up to ~8)
+
+// createInitialImage + buildGaussianPyramid (+ buildDoGPyramid) into siftG / siftD
+int sift_build(fm3d_ctx* c, const uint8_t* img, int w, int h, const SiftPlan& P, bool dog) {
+    const fm3d_settings& S = c->s;
+    const int L = P.L, nl = L + 3;
+    // the blur kernels: [0] sig_diff of the initial image, [i] sig[i] of the octave levels
+    std::vector<std::vector<float>> taps(nl);
+    {
+        const float sigma = (float)S.siftSigma;
+        const float sd = P.firstOctave < 0 ? std::sqrt(std::max(sigma * sigma - 0.5f * 0.5f * 4, 0.01f))
+                                           : std::sqrt(std::max(sigma * sigma - 0.5f * 0.5f, 0.01f));
+        taps[0] = sift_gauss_kernel(sd);
+        const double k = std::pow(2., 1. / L);
+        for (int i = 1; i < nl; i++) {
+            const double sig_prev = std::pow(k, (double)(i - 1)) * S.siftSigma;
+            const double sig_total = sig_prev * k;
+            taps[i] = sift_gauss_kernel(std::sqrt(sig_total * sig_total - sig_prev * sig_prev));
+        }
+    }
+    for (auto& t : taps)
+        if ((int)t.size() > kSiftMaxTaps)
+            return fail(c, FM3D_ERR_UNSUPPORTED, "SIFT sigma too large for the GPU blur tile (kernel > 65 taps)");
+    std::vector<float> tapBuf((size_t)nl * 128, 0.f);
+    for (int i = 0; i < nl; i++) std::copy(taps[i].begin(), taps[i].end(), tapBuf.begin() + (size_t)i * 128);
+    HIPCHK(c, c->siftTaps.ensure(tapBuf.size() * sizeof(float)));
+    HIPCHK(c, hipMemcpyAsync(c->siftTaps.p, tapBuf.data(), tapBuf.size() * sizeof(float), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, c->siftImg.ensure((size_t)w * h));
+    HIPCHK(c, hipMemcpyAsync(c->siftImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->siftG.ensure((size_t)P.gTotal * sizeof(float) + 64));
+    if (dog) HIPCHK(c, c->siftD.ensure((size_t)P.dTotal * sizeof(float) + 64));
+    const int bw = P.G[0].w, bh = P.G[0].h;
+    HIPCHK(c, c->siftBase.ensure((size_t)bw * bh * sizeof(float)));
+    float* G = c->siftG.as<float>();
+    float* D = dog ? c->siftD.as<float>() : nullptr;
+    const float* T = c->siftTaps.as<float>();
+    {
+        fm3d::SiftResize rp{};
+        rp.sw = w;
+        rp.sh = h;
+        rp.dw = bw;
+        rp.dh = bh;
+        rp.doubled = P.firstOctave < 0;
+        rp.scx = 1. / ((double)bw / w);
+        rp.scy = 1. / ((double)bh / h);
+        rp.xmax = bw;
+        for (int dx = 0; dx < bw; dx++) {  // resize's xmax: the first column whose right tap leaves the row
+            const float fx = (float)((dx + 0.5) * rp.scx - 0.5);
+            if ((int)std::floor(fx) + 1 >= w) {
+                rp.xmax = dx;
+                break;
+            }
+        }
+        fm3d::launch_sift_init(c->siftImg.as<uint8_t>(), c->siftBase.as<float>(), rp, c->stream);
+        fm3d::launch_sift_blur(c->siftBase.as<float>(), G, nullptr, bw, bh, T, (int)taps[0].size(), c->stream);
+    }
+    for (int o = 0; o < P.nOct; o++)
+        for (int i = 0; i < nl; i++) {
+            const fm3d::SiftLevel& d = P.G[o * nl + i];
+            if (o == 0 && i == 0) continue;
+            if (i == 0) {
+                const fm3d::SiftLevel& s = P.G[(o - 1) * nl + L];
+                fm3d::launch_sift_down(G + s.first, s.w, s.h, G + d.first, d.w, d.h, 1. / ((double)d.w / s.w),
+                                       1. / ((double)d.h / s.h), c->stream);
+            } else {
+                const fm3d::SiftLevel& s = P.G[o * nl + i - 1];
+                fm3d::launch_sift_blur(G + s.first, G + d.first, D ? D + P.D[o * (L + 2) + i - 1].first : nullptr, d.w,
+                                       d.h, T + (size_t)i * 128, (int)taps[i].size(), c->stream);
+            }
+        }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, c->siftGL.ensure(P.G.size() * sizeof(fm3d::SiftLevel)));
+    HIPCHK(c, hipMemcpyAsync(c->siftGL.p, P.G.data(), P.G.size() * sizeof(fm3d::SiftLevel), hipMemcpyHostToDevice,
+                             c->stream));
+    if (dog) {
+        HIPCHK(c, c->siftDL.ensure(P.D.size() * sizeof(fm3d::SiftLevel)));
+        HIPCHK(c, hipMemcpyAsync(c->siftDL.p, P.D.data(), P.D.size() * sizeof(fm3d::SiftLevel), hipMemcpyHostToDevice,
+                                 c->stream));
+    }
+    // the host vectors leave scope: finish the copies
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+int sift_check_settings(fm3d_ctx* c) {
+    const fm3d_settings& S = c->s;
+    if (S.siftOctaveLayers < 1 || S.siftOctaveLayers > 16 || S.siftNumFeatures < 0 || !(S.siftSigma > 0) ||
+        !(S.siftContrastThreshold >= 0) || !(S.siftEdgeThreshold >= 0))
+        return fail(c, FM3D_ERR_INVALID, "SIFT NumOctaveLayers / NumFeatures / Sigma / thresholds out of range");
+    return FM3D_OK;
+}
+
+// KeyPointsFilter::removeDuplicated: KeyPoint_LessThan order with the index as the last key, the
+// first of each group of equal (pt, size, angle) kept, input order preserved
+int sift_remove_duplicated(std::vector<fm3d_keypoint>& k) {
+    const int n = (int)k.size();
+    if (n < 2) return n;
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](int i, int j) {
+        const fm3d_keypoint &a = k[i], &b = k[j];
+        if (a.x != b.x) return a.x < b.x;
+        if (a.y != b.y) return a.y < b.y;
+        if (a.size != b.size) return a.size > b.size;
+        if (a.angle != b.angle) return a.angle < b.angle;
+        if (a.response != b.response) return a.response > b.response;
+        if (a.octave != b.octave) return a.octave > b.octave;
+        if (a.class_id != b.class_id) return a.class_id > b.class_id;
+        return i < j;
+    });
+    std::vector<uint8_t> mask(n, 1);
+    for (int i = 1, j = 0; i < n; i++) {
+        const fm3d_keypoint &a = k[idx[i]], &b = k[idx[j]];
+        if (a.x != b.x || a.y != b.y || a.size != b.size || a.angle != b.angle)
+            j = i;
+        else
+            mask[idx[i]] = 0;
+    }
+    int j = 0;
+    for (int i = 0; i < n; i++)
+        if (mask[i]) k[j++] = k[i];
+    k.resize(j);
+    return j;
+}
+
+void sift_unpack_octave(const fm3d_keypoint& k, int& octave, int& layer) {
+    octave = k.octave & 255;
+    layer = (k.octave >> 8) & 255;
+    octave = octave < 128 ? octave : (-128 | octave);
+}
+
+// SIFT::operator()(img, Mat(), kpts, desc, true) on keypoints that passed runByKeypointSize:
+// the pyramid from firstOctave = min(0, octaves), nOctaves = max - first + 1 (reused when the detect
+// call just built the same levels), calcDescriptors.  desc: m x 128 floats (host)
+int sift_describe(fm3d_ctx* c, const uint8_t* img, int w, int h, const std::vector<fm3d_keypoint>& k, float* desc,
+                  const SiftPlan* built) {
+    const int m = (int)k.size(), L = c->s.siftOctaveLayers;
+    if (m == 0) return FM3D_OK;
+    int firstOctave = 0, maxOctave = INT_MIN, actualNLayers = 0;
+    for (const auto& q : k) {
+        int o, l;
+        sift_unpack_octave(q, o, l);
+        firstOctave = std::min(firstOctave, o);
+        maxOctave = std::max(maxOctave, o);
+        actualNLayers = std::max(actualNLayers, l - 2);
+    }
+    firstOctave = std::min(firstOctave, 0);
+    if (firstOctave < -1 || actualNLayers > L)
+        return fail(c, FM3D_ERR_INVALID, "SIFT compute: a keypoint octave < -1 or layer > nOctaveLayers + 2");
+    const int nOct = maxOctave - firstOctave + 1;
+    int r;
+    SiftPlan P;
+    if (built && built->firstOctave == firstOctave && built->nOct >= nOct) {
+        P = *built;
+    } else {
+        if (!sift_plan(w, h, firstOctave, nOct, L, P))
+            return fail(c, FM3D_ERR_INVALID, "SIFT compute: a keypoint octave the image cannot hold");
+        if ((r = sift_build(c, img, w, h, P, false))) return r;
+    }
+    HIPCHK(c, c->siftKp.ensure((size_t)m * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->siftDesc.ensure((size_t)m * 128 * sizeof(float)));
+    HIPCHK(c, hipMemcpyAsync(c->siftKp.p, k.data(), (size_t)m * sizeof(fm3d_keypoint), hipMemcpyHostToDevice,
+                             c->stream));
+    fm3d::launch_sift_desc(c->siftG.as<float>(), c->siftGL.as<fm3d::SiftLevel>(), L, firstOctave,
+                           c->siftKp.as<fm3d_keypoint>(), m, c->siftDesc.as<float>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(desc, c->siftDesc.p, (size_t)m * 128 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
 int surf_upload_image(fm3d_ctx* c, const uint8_t* img, int w, int h) {
     HIPCHK(c, c->sfImg.ensure((size_t)w * h));
     HIPCHK(c, hipMemcpyAsync(c->sfImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
@@ -979,7 +1209,9 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->sfImg, &c->sfSum, &c->sfDet, &c->sfTr, &c->sfLayers, &c->sfMids, &c->sfCand, &c->sfCount,
                       &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW, &c->sfAng,
                       &c->orbPyr, &c->orbTab, &c->orbLev, &c->orbMap, &c->orbFlag, &c->orbPos, &c->orbKp, &c->orbR,
-                      &c->orbBlur, &c->orbDesc, &c->orbPat};
+                      &c->orbBlur, &c->orbDesc, &c->orbPat, &c->siftImg, &c->siftBase, &c->siftG, &c->siftD,
+                      &c->siftGL, &c->siftDL, &c->siftTaps, &c->siftScan, &c->siftFlag, &c->siftPos, &c->siftCand,
+                      &c->siftAng, &c->siftNpk, &c->siftKp, &c->siftDesc};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();
@@ -1822,6 +2054,150 @@ int fm3d_orb_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoint
         kpts[i] = q;
     }
     *n = nf;
+    return FM3D_OK;
+}
+
+int fm3d_sift_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoint* kpts, int cap, int* n,
+                     float* desc) {
+    if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
+    const fm3d_settings& S = c->s;
+    if (S.detectorType != FM3D_FEAT_SIFT || (desc && S.extractorType != FM3D_FEAT_SIFT))
+        return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' detector (extractor) is not SIFT");
+    int r;
+    if ((r = sift_check_settings(c))) return r;
+    hipSetDevice(c->device);
+    const int L = S.siftOctaveLayers, firstOctave = -1;
+    const int nOct = sift_num_octaves(w, h, firstOctave);
+    std::vector<fm3d_keypoint> k;
+    SiftPlan P;
+    if (nOct >= 1) {
+        if (!sift_plan(w, h, firstOctave, nOct, L, P))
+            return fail(c, FM3D_ERR_INVALID, "SIFT: an octave of the image would be empty");
+        if ((r = sift_build(c, img, w, h, P, true))) return r;
+        // findScaleSpaceExtrema: flags over every (octave, layer 1..L, row, column), compacted in that order
+        std::vector<fm3d::SiftScan> scan;
+        long long total = 0;
+        for (int o = 0; o < nOct; o++)
+            for (int i = 1; i <= L; i++) {
+                const fm3d::SiftLevel& d = P.D[o * (L + 2) + i];
+                scan.push_back({total, o * (L + 2) + i, o, i, 0});
+                total += (long long)d.w * d.h;
+            }
+        if (total > INT32_MAX / 2) return fail(c, FM3D_ERR_INVALID, "image too large for the SIFT scan");
+        const int tot = (int)total;
+        const int threshold = (int)std::floor(0.5 * S.siftContrastThreshold / L * 255 * 1);
+        HIPCHK(c, c->siftScan.ensure(scan.size() * sizeof(fm3d::SiftScan)));
+        HIPCHK(c, hipMemcpyAsync(c->siftScan.p, scan.data(), scan.size() * sizeof(fm3d::SiftScan), hipMemcpyHostToDevice,
+                                 c->stream));
+        if ((r = ensure_scan_tmp(c, tot))) return r;
+        HIPCHK(c, c->siftFlag.ensure((size_t)(tot + 1) * sizeof(int)));
+        HIPCHK(c, c->siftPos.ensure((size_t)(tot + 1) * sizeof(int)));
+        fm3d::launch_sift_extrema(c->siftD.as<float>(), c->siftDL.as<fm3d::SiftLevel>(), c->siftScan.as<fm3d::SiftScan>(),
+                                  (int)scan.size(), total, threshold, c->siftFlag.as<int>(), c->stream);
+        fm3d::launch_exclusive_scan(c->siftFlag.as<int>(), tot, c->siftPos.as<int>(), c->count.as<int>(), c->scanTmp.p,
+                                    c->stream);
+        HIPCHK(c, hipGetLastError());
+        int nc = 0;
+        HIPCHK(c, hipMemcpyAsync(&nc, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (nc > 0) {
+            HIPCHK(c, c->siftCand.ensure((size_t)nc * sizeof(fm3d::SiftCand)));
+            HIPCHK(c, c->siftAng.ensure((size_t)nc * 36 * sizeof(float)));
+            HIPCHK(c, c->siftNpk.ensure((size_t)nc * sizeof(int)));
+            fm3d::launch_sift_cand_scatter(c->siftDL.as<fm3d::SiftLevel>(), c->siftScan.as<fm3d::SiftScan>(),
+                                           (int)scan.size(), total, c->siftFlag.as<int>(), c->siftPos.as<int>(),
+                                           c->siftCand.as<fm3d::SiftCand>(), c->stream);
+            fm3d::launch_sift_adjust(c->siftD.as<float>(), c->siftDL.as<fm3d::SiftLevel>(), L,
+                                     (float)S.siftContrastThreshold, (float)S.siftEdgeThreshold, (float)S.siftSigma,
+                                     c->siftCand.as<fm3d::SiftCand>(), nc, c->stream);
+            fm3d::launch_sift_orient(c->siftG.as<float>(), c->siftGL.as<fm3d::SiftLevel>(), L,
+                                     c->siftCand.as<fm3d::SiftCand>(), nc, c->siftAng.as<float>(),
+                                     c->siftNpk.as<int>(), c->stream);
+            HIPCHK(c, hipGetLastError());
+            std::vector<fm3d::SiftCand> cand(nc);
+            std::vector<int> npk(nc);
+            std::vector<float> ang((size_t)nc * 36);
+            HIPCHK(c, hipMemcpyAsync(cand.data(), c->siftCand.p, (size_t)nc * sizeof(fm3d::SiftCand),
+                                     hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(npk.data(), c->siftNpk.p, (size_t)nc * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(ang.data(), c->siftAng.p, ang.size() * sizeof(float), hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            for (int q = 0; q < nc; q++) {
+                const fm3d::SiftCand& C = cand[q];
+                if (!C.ok) continue;
+                for (int p = 0; p < npk[q]; p++)
+                    k.push_back({C.x, C.y, C.size, ang[(size_t)q * 36 + p], C.response, C.koct, -1});
+            }
+        }
+        sift_remove_duplicated(k);
+        if (S.siftNumFeatures > 0) k.resize(orb_retain_best(k.data(), (int)k.size(), S.siftNumFeatures));
+        for (auto& q : k) {  // firstOctave -1: back to the image's coordinates
+            const float scale = 1.f / (float)(1 << -firstOctave);
+            q.octave = (q.octave & ~255) | ((q.octave + firstOctave) & 255);
+            q.x *= scale;
+            q.y *= scale;
+            q.size *= scale;
+        }
+    }
+    const int nf = (int)k.size(), nw = std::min(nf, cap);
+    for (int i = 0; i < nw; i++) kpts[i] = k[i];
+    *n = nf;
+    if (desc && nw > 0) {
+        // the reference's separate compute (runByKeypointSize keeps all: detected sizes are > 0)
+        std::vector<fm3d_keypoint> kd(k.begin(), k.begin() + nw);
+        if ((r = sift_describe(c, img, w, h, kd, desc, nOct >= 1 ? &P : nullptr))) return r;
+    }
+    return FM3D_OK;
+}
+
+int fm3d_sift_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,
+                      fm3d_keypoint* kout, int32_t* kept, int* nOut, float* desc) {
+    if (!c || !img || !nOut || w <= 0 || h <= 0 || n < 0 || (n > 0 && (!kpts || !kout || !desc)))
+        return FM3D_ERR_INVALID;
+    if (c->s.extractorType != FM3D_FEAT_SIFT) return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' extractor is not SIFT");
+    int r;
+    if ((r = sift_check_settings(c))) return r;
+    hipSetDevice(c->device);
+    // DescriptorExtractor::compute: runByKeypointSize(FLT_EPSILON) (runByImageBorder(0) keeps all)
+    std::vector<fm3d_keypoint> k;
+    std::vector<int> src;
+    for (int i = 0; i < n; i++)
+        if (!(kpts[i].size < FLT_EPSILON || kpts[i].size > FLT_MAX)) {
+            k.push_back(kpts[i]);
+            src.push_back(i);
+        }
+    if ((r = sift_describe(c, img, w, h, k, desc, nullptr))) return r;
+    for (size_t i = 0; i < k.size(); i++) {
+        kout[i] = k[i];
+        if (kept) kept[i] = src[i];
+    }
+    *nOut = (int)k.size();
+    return FM3D_OK;
+}
+
+int fm3d_sift_pyramid(fm3d_ctx* c, const uint8_t* img, int w, int h, int firstOctave, int nOctaves, int dog,
+                      float* out, int32_t* sizes, int64_t* total) {
+    if (!c || !img || !total || w <= 0 || h <= 0 || firstOctave < -1 || firstOctave > 0 || nOctaves < 1)
+        return FM3D_ERR_INVALID;
+    int r;
+    if ((r = sift_check_settings(c))) return r;
+    hipSetDevice(c->device);
+    SiftPlan P;
+    if (!sift_plan(w, h, firstOctave, nOctaves, c->s.siftOctaveLayers, P))
+        return fail(c, FM3D_ERR_INVALID, "SIFT: an octave of the image would be empty");
+    const std::vector<fm3d::SiftLevel>& Lv = dog ? P.D : P.G;
+    *total = dog ? P.dTotal : P.gTotal;
+    if (sizes)
+        for (size_t i = 0; i < Lv.size(); i++) {
+            sizes[2 * i] = Lv[i].w;
+            sizes[2 * i + 1] = Lv[i].h;
+        }
+    if (!out) return FM3D_OK;
+    if ((r = sift_build(c, img, w, h, P, dog != 0))) return r;
+    HIPCHK(c, hipMemcpyAsync(out, dog ? c->siftD.p : c->siftG.p, (size_t)*total * sizeof(float), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return FM3D_OK;
 }
 

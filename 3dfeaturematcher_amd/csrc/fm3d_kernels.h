@@ -203,6 +203,43 @@ void launch_orb_blur(const uint8_t* pyr, const OrbLevel* L, int nL, long long to
 void launch_orb_desc(const uint8_t* blur, const OrbLevel* L, const fm3d_keypoint* kp, int n, const int* pattern,
                      uint8_t* desc, hipStream_t s);
 
+// ---------------- SIFT (fm3d_sift.hip) ----------------
+struct SiftLevel {    // one pyramid level, levels concatenated float after float
+    int w, h;
+    long long first;  // first float of the level
+};
+struct SiftResize {   // createInitialImage: gray (sw x sh) -> float (dw x dh), doubled with INTER_LINEAR
+    int sw, sh, dw, dh, xmax, doubled;
+    double scx, scy;  // 1 / inv_scale
+};
+struct SiftScan {     // one DoG layer scanned by findScaleSpaceExtrema, flags concatenated
+    long long first;  // first flag of the layer
+    int dog, octave, layer, pad;
+};
+struct SiftCand {     // a scale-space extremum, then adjustLocalExtrema's keypoint
+    float x, y, size, response;
+    int koct;              // KeyPoint::octave: octv + (layer << 8) + (round((xi + 0.5) * 255) << 16)
+    int octave, layer, r, c, ok;
+};
+void launch_sift_init(const uint8_t* img, float* dst, const SiftResize& p, hipStream_t s);
+size_t sift_blur_lds(int n);
+// dst = GaussianBlur(src, taps[0..n)), dog = dst - src (dog may be null)
+void launch_sift_blur(const float* src, float* dst, float* dog, int w, int h, const float* taps, int n,
+                      hipStream_t s);
+void launch_sift_down(const float* src, int sw, int sh, float* dst, int dw, int dh, double ifx, double ify,
+                      hipStream_t s);
+void launch_sift_extrema(const float* dog, const SiftLevel* DL, const SiftScan* S, int nS, long long total,
+                         int threshold, int* flag, hipStream_t s);
+void launch_sift_cand_scatter(const SiftLevel* DL, const SiftScan* S, int nS, long long total, const int* flag,
+                              const int* pos, SiftCand* cand, hipStream_t s);
+void launch_sift_adjust(const float* dog, const SiftLevel* DL, int L, float contrastThreshold, float edgeThreshold,
+                        float sigma, SiftCand* cand, int n, hipStream_t s);
+// angles: 36 per candidate (the first npk[q] are its peaks, in bin order)
+void launch_sift_orient(const float* gp, const SiftLevel* GL, int L, const SiftCand* cand, int n, float* angles,
+                        int* npk, hipStream_t s);
+void launch_sift_desc(const float* gp, const SiftLevel* GL, int L, int firstOctave, const fm3d_keypoint* kp, int n,
+                      float* desc, hipStream_t s);
+
 // ---------------- compaction ----------------
 // out[k] = in[i] for flag[i] != 0, stable; *count (device) = number kept.  tmp >= scan_tmp_bytes(n).
 size_t scan_tmp_bytes(int n);

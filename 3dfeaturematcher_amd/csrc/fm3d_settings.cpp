@@ -143,6 +143,11 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->orbEdgeThreshold = 31;
     s->orbPatchSize = 31;
     s->orbFastThreshold = 20;
+    s->siftNumFeatures = 0;  // cv::SIFT's defaults (FeatureOptions.SiftDetector, absent from settings.yml)
+    s->siftOctaveLayers = 3;
+    s->siftContrastThreshold = 0.04;
+    s->siftEdgeThreshold = 10;
+    s->siftSigma = 1.6;
     return FM3D_OK;
 }
 
@@ -192,9 +197,18 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
             s->detectorType = mode != "STATIC" ? FM3D_FEAT_OTHER
                               : det == "SURF"  ? FM3D_FEAT_SURF
                               : det == "ORB"   ? FM3D_FEAT_ORB
+                              : det == "SIFT"  ? FM3D_FEAT_SIFT
                                                : FM3D_FEAT_OTHER;
         if (str("FeatureOptions.ExtractorType", ex))
-            s->extractorType = ex == "SURF" ? FM3D_FEAT_SURF : ex == "ORB" ? FM3D_FEAT_ORB : FM3D_FEAT_OTHER;
+            s->extractorType = ex == "SURF"   ? FM3D_FEAT_SURF
+                               : ex == "ORB"  ? FM3D_FEAT_ORB
+                               : ex == "SIFT" ? FM3D_FEAT_SIFT
+                                              : FM3D_FEAT_OTHER;
+        get_i(kv, "FeatureOptions.SiftDetector.NumFeatures", &s->siftNumFeatures);
+        get_i(kv, "FeatureOptions.SiftDetector.NumOctaveLayers", &s->siftOctaveLayers);
+        get_d(kv, "FeatureOptions.SiftDetector.ContrastThreshold", &s->siftContrastThreshold);
+        get_d(kv, "FeatureOptions.SiftDetector.EdgeThreshold", &s->siftEdgeThreshold);
+        get_d(kv, "FeatureOptions.SiftDetector.Sigma", &s->siftSigma);
         get_i(kv, "FeatureOptions.OrbDetector.NumFeatures", &s->orbNumFeatures);
         get_d(kv, "FeatureOptions.OrbDetector.ScaleFactor", &s->orbScaleFactor);
         get_i(kv, "FeatureOptions.OrbDetector.NumLevels", &s->orbNumLevels);

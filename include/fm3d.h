@@ -85,10 +85,17 @@ typedef struct fm3d_settings {
     int orbNumFeatures;
     double orbScaleFactor;
     int orbNumLevels, orbEdgeThreshold, orbPatchSize, orbFastThreshold;
+    /* FeatureOptions.SiftDetector.NumFeatures / NumOctaveLayers / ContrastThreshold / EdgeThreshold /
+       Sigma (cv::SIFT's five arguments, descriptorsmatcher.cpp:246-251, 305-310); OpenCV's defaults
+       0 / 3 / 0.04 / 10 / 1.6 when the file names none (the reference would read 0 from a missing
+       node) */
+    int siftNumFeatures, siftOctaveLayers;
+    double siftContrastThreshold, siftEdgeThreshold, siftSigma;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
 #define FM3D_FEAT_ORB 1
+#define FM3D_FEAT_SIFT 2
 #define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
@@ -302,6 +309,31 @@ int fm3d_orb_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, c
    part of this library -- pass it here for descriptor parity with OpenCV; NULL restores the default,
    makeRandomPattern(orbPatchSize) (cv::RNG(0x34985739), OpenCV's pattern for every other patchSize). */
 int fm3d_orb_set_pattern(fm3d_ctx *ctx, const int32_t *xy, int npoints);
+
+/* ---------------- feature detection + description (SIFT, OpenCV 2.4 nonfree) ---------------- */
+/* FeatureDetector::detect of the settings' SIFT detector (descriptorsmatcher.cpp:243-251:
+   cv::SIFT(siftNumFeatures, siftOctaveLayers, siftContrastThreshold, siftEdgeThreshold, siftSigma)):
+   the doubled-image scale space, DoG extrema in scan order (octave, layer, row, column), one keypoint
+   per orientation peak, removeDuplicated, retainBest(NumFeatures) when > 0; octave codes and
+   positions as OpenCV returns them (octave -1 = the doubled image).  *n = all; min(*n, cap) written.
+   desc (may be NULL): the extractor's compute on the same image (:113-114, 302-310), min(*n, cap) x
+   128 floats holding integers 0..255.  FM3D_ERR_UNSUPPORTED unless the detector (and, with desc, the
+   extractor) is SIFT, or when a blur needs more than 65 taps (sigma above ~8). */
+int fm3d_sift_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, fm3d_keypoint *kpts, int cap, int *n,
+                     float *desc);
+/* DescriptorExtractor::compute of the settings' SIFT extractor (:113-114, 302-310): keypoints with
+   size < FLT_EPSILON removed (input order kept), the rest described on the pyramid of firstOctave =
+   min(0, their octaves).  kout / kept (input index, may be NULL): capacity n; desc: n x 128 floats;
+   *nOut = kept count.  FM3D_ERR_INVALID for an octave below -1, a layer above NumOctaveLayers + 2 or an
+   octave the image cannot hold (OpenCV asserts there). */
+int fm3d_sift_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const fm3d_keypoint *kpts, int n,
+                      fm3d_keypoint *kout, int32_t *kept, int *nOut, float *desc);
+/* the scale space SIFT builds (cv::SIFT::buildGaussianPyramid / buildDoGPyramid, public in OpenCV 2.4):
+   firstOctave -1 (doubled) or 0, nOctaves octaves of NumOctaveLayers + 3 Gaussian levels (dog 0) or
+   NumOctaveLayers + 2 DoG levels (dog 1), concatenated octave-major.  *total = floats; sizes (may be
+   NULL): (w, h) per level; out (may be NULL to ask for the sizes): *total floats. */
+int fm3d_sift_pyramid(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int firstOctave, int nOctaves, int dog,
+                      float *out, int32_t *sizes, int64_t *total);
 
 /* ---------------- the whole hot path, device resident ---------------- */
 /* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */
