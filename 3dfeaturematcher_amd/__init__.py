@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
-FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_OTHER = 0, 1, 2, -1  # fm3d_settings.detectorType / extractorType
+FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_OTHER = 0, 1, 2, 3, -1  # fm3d_settings.detectorType / extractorType
 DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
@@ -37,7 +37,7 @@ EXPORTS = (
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
     "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
     "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern", "fm3d_sift_detect", "fm3d_sift_compute",
-    "fm3d_sift_pyramid",
+    "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2",
@@ -70,6 +70,8 @@ class Settings(ctypes.Structure):
         ("siftNumFeatures", ctypes.c_int), ("siftOctaveLayers", ctypes.c_int),
         ("siftContrastThreshold", ctypes.c_double), ("siftEdgeThreshold", ctypes.c_double),
         ("siftSigma", ctypes.c_double),
+        ("detectorMode", ctypes.c_int), ("fastThreshold", ctypes.c_int), ("fastNonmax", ctypes.c_int),
+        ("adaptiveMinFeatures", ctypes.c_int), ("adaptiveMaxFeatures", ctypes.c_int), ("adaptiveMaxIters", ctypes.c_int),
     ]
 
     @staticmethod
@@ -234,11 +236,14 @@ class DescriptorsMatcher:
         extractor types select, :64), knnMatch, NNDR.  Returns (matches appended as the reference
         does, kpts_a, kpts_b, desc_a, desc_b)."""
         S = self.ctx.settings
-        if S.detectorType == FEAT_SIFT and S.extractorType == FEAT_SIFT:
-            sift = SIFT(self.ctx)
-            ka, _, da = sift.compute(image_a, sift.detect(image_a))
-            kb, _, db = sift.compute(image_b, sift.detect(image_b))
-            m = self.compareWithNNDR(epsilon, da, db, matches)
+        if S.detectorMode == 1 or S.detectorType in (FEAT_SIFT, FEAT_FAST) or S.extractorType != S.detectorType:
+            # the reference's two calls with any detector / extractor pair built here (fm3d_detect,
+            # fm3d_compute): detect, then compute on the detected keypoints
+            feats = Features(self.ctx)
+            ka, _, da = feats.compute(image_a, feats.detect(image_a))
+            kb, _, db = feats.compute(image_b, feats.detect(image_b))
+            binary = S.extractorType == FEAT_ORB
+            m = DescriptorsMatcher(self.ctx, binary=binary).compareWithNNDR(epsilon, da, db, matches)
             return m, ka, kb, da, db
         if S.detectorType == FEAT_ORB and S.extractorType == FEAT_ORB:
             orb = ORB(self.ctx)
@@ -447,6 +452,67 @@ class SIFT:
                                                _vp(kout), _ptr(kept, ctypes.c_int32), ctypes.byref(m),
                                                _ptr(desc, ctypes.c_float)))
         return kout[:m.value], kept[:m.value], desc[:m.value]
+
+    extractDescriptorsFromPatches = SURF.extractDescriptorsFromPatches  # the C ABI picks the settings' extractor
+
+
+class Features:
+    """The settings' detector and extractor, whatever their types (descriptorsmatcher.cpp:176-359):
+    STATIC SURF / ORB / SIFT / FAST or ADAPTIVE FAST / SURF detection (fm3d_detect), SURF / SIFT / ORB
+    description (fm3d_compute) on any keypoints."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def descriptor_info(self):
+        """(columns, numpy dtype) of the extractor's rows"""
+        cols, typ = ctypes.c_int(0), ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_descriptor_info(self.ctx.handle, ctypes.byref(cols), ctypes.byref(typ)))
+        return cols.value, (np.uint8 if typ.value == DESC_BITS else np.float32)
+
+    def detect(self, image: np.ndarray) -> np.ndarray:
+        """feature_detector_->detect (descriptorsmatcher.cpp:110-111): KEYPOINT records"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap = 4096
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            n = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(k), cap,
+                                             ctypes.byref(n)))
+            if n.value <= cap:
+                return k[:n.value]
+            cap = n.value
+
+    def compute(self, image: np.ndarray, keypoints: np.ndarray):
+        """descriptor_extractor_->compute (descriptorsmatcher.cpp:113-114): (kept keypoints, input index
+        of each, descriptor rows)"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cols, dt = self.descriptor_info()
+        kin = np.ascontiguousarray(keypoints, dtype=KEYPOINT)
+        n = len(kin)
+        kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+        kept = np.zeros(max(n, 1), dtype=np.int32)
+        desc = np.zeros((max(n, 1), cols), dtype=dt)
+        m = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_compute(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(kin), n, _vp(kout),
+                                          _ptr(kept, ctypes.c_int32), ctypes.byref(m), _vp(desc)))
+        return kout[:m.value], kept[:m.value], desc[:m.value]
+
+    def fast(self, image: np.ndarray, threshold: int = 10, nonmax: bool = True) -> np.ndarray:
+        """cv::FastFeatureDetector(threshold, nonmax).detect: KEYPOINT records in raster order"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap = 4096
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            n = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_fast_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, threshold,
+                                                  1 if nonmax else 0, _vp(k), cap, ctypes.byref(n)))
+            if n.value <= cap:
+                return k[:n.value]
+            cap = n.value
 
 
 class SingleCameraTriangulator:
@@ -841,6 +907,7 @@ class MOSAIC:
 
     def compute(self) -> np.ndarray:
         """The patch descriptors: (kept features, 128) float32."""
+        ex = SIFT(self.ctx) if self.ctx.settings.extractorType == FEAT_SIFT else SURF(self.ctx)
         if len(self.patches) == 0:
-            return np.zeros((0, SURF(self.ctx).descriptorSize), dtype=np.float32)
-        return SURF(self.ctx).extractDescriptorsFromPatches(self.patches)
+            return np.zeros((0, ex.descriptorSize), dtype=np.float32)
+        return ex.extractDescriptorsFromPatches(self.patches)

@@ -1031,8 +1031,8 @@ int sift_build(fm3d_ctx* c, const uint8_t* img, int w, int h, const SiftPlan& P,
                 break;
             }
         }
-        fm3d::launch_sift_init(c->siftImg.as<uint8_t>(), c->siftBase.as<float>(), rp, c->stream);
-        fm3d::launch_sift_blur(c->siftBase.as<float>(), G, nullptr, bw, bh, T, (int)taps[0].size(), c->stream);
+        fm3d::launch_sift_init(c->siftImg.as<uint8_t>(), c->siftBase.as<float>(), rp, 1, c->stream);
+        fm3d::launch_sift_blur(c->siftBase.as<float>(), G, nullptr, bw, bh, T, (int)taps[0].size(), 1, c->stream);
     }
     for (int o = 0; o < P.nOct; o++)
         for (int i = 0; i < nl; i++) {
@@ -1045,7 +1045,7 @@ int sift_build(fm3d_ctx* c, const uint8_t* img, int w, int h, const SiftPlan& P,
             } else {
                 const fm3d::SiftLevel& s = P.G[o * nl + i - 1];
                 fm3d::launch_sift_blur(G + s.first, G + d.first, D ? D + P.D[o * (L + 2) + i - 1].first : nullptr, d.w,
-                                       d.h, T + (size_t)i * 128, (int)taps[i].size(), c->stream);
+                                       d.h, T + (size_t)i * 128, (int)taps[i].size(), 1, c->stream);
             }
         }
     HIPCHK(c, hipGetLastError());
@@ -1142,10 +1142,102 @@ int sift_describe(fm3d_ctx* c, const uint8_t* img, int w, int h, const std::vect
     HIPCHK(c, hipMemcpyAsync(c->siftKp.p, k.data(), (size_t)m * sizeof(fm3d_keypoint), hipMemcpyHostToDevice,
                              c->stream));
     fm3d::launch_sift_desc(c->siftG.as<float>(), c->siftGL.as<fm3d::SiftLevel>(), L, firstOctave,
-                           c->siftKp.as<fm3d_keypoint>(), m, c->siftDesc.as<float>(), c->stream);
+                           c->siftKp.as<fm3d_keypoint>(), nullptr, m, c->siftDesc.as<float>(), c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(desc, c->siftDesc.p, (size_t)m * 128 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+// extractDescriptorsFromPatches with the SIFT extractor (descriptorsmatcher.cpp:133-174, 302-310): per
+// patch SIFT::operator()(patch, Mat(), {kp}, desc, true) with kp = (center, size, angle -1, octave 0):
+// firstOctave 0, one octave, and the descriptor reads level 0 of it, blur(patch, sig_diff) -- so every
+// patch needs only that level (batched: one init and one blur launch for all patches)
+int sift_patches(fm3d_ctx* c, const uint8_t* patches, int P, int size, float* desc) {
+    int r;
+    if ((r = sift_check_settings(c))) return r;
+    if (P == 0) return FM3D_OK;
+    hipSetDevice(c->device);
+    const fm3d_settings& S = c->s;
+    const float center = (float)(int)std::floor(size / 2);
+    const fm3d_keypoint k{center, center, (float)size, -1.f, 1.f, 0, 0};
+    const float sigma = (float)S.siftSigma;
+    const std::vector<float> taps = sift_gauss_kernel(std::sqrt(std::max(sigma * sigma - 0.5f * 0.5f, 0.01f)));
+    if ((int)taps.size() > kSiftMaxTaps)
+        return fail(c, FM3D_ERR_UNSUPPORTED, "SIFT sigma too large for the GPU blur tile (kernel > 65 taps)");
+    const size_t per = (size_t)size * size;
+    std::vector<fm3d::SiftLevel> GL((size_t)P);
+    std::vector<int> lvl((size_t)P);
+    for (int p = 0; p < P; p++) {
+        GL[p] = {size, size, (long long)(p * per)};
+        lvl[p] = p;
+    }
+    std::vector<fm3d_keypoint> kp((size_t)P, k);
+    HIPCHK(c, c->siftTaps.ensure(128 * sizeof(float)));
+    HIPCHK(c, c->siftImg.ensure((size_t)P * per));
+    HIPCHK(c, c->siftBase.ensure((size_t)P * per * sizeof(float)));
+    HIPCHK(c, c->siftG.ensure((size_t)P * per * sizeof(float)));
+    HIPCHK(c, c->siftGL.ensure((size_t)P * sizeof(fm3d::SiftLevel)));
+    HIPCHK(c, c->siftPos.ensure((size_t)P * sizeof(int)));
+    HIPCHK(c, c->siftKp.ensure((size_t)P * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->siftDesc.ensure((size_t)P * 128 * sizeof(float)));
+    HIPCHK(c, hipMemcpyAsync(c->siftTaps.p, taps.data(), taps.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->siftImg.p, patches, (size_t)P * per, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->siftGL.p, GL.data(), GL.size() * sizeof(fm3d::SiftLevel), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->siftPos.p, lvl.data(), lvl.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->siftKp.p, kp.data(), kp.size() * sizeof(fm3d_keypoint), hipMemcpyHostToDevice,
+                             c->stream));
+    fm3d::SiftResize rp{};
+    rp.sw = rp.dw = size;
+    rp.sh = rp.dh = size;
+    rp.doubled = 0;
+    fm3d::launch_sift_init(c->siftImg.as<uint8_t>(), c->siftBase.as<float>(), rp, P, c->stream);
+    fm3d::launch_sift_blur(c->siftBase.as<float>(), c->siftG.as<float>(), nullptr, size, size, c->siftTaps.as<float>(),
+                           (int)taps.size(), P, c->stream);
+    fm3d::launch_sift_desc(c->siftG.as<float>(), c->siftGL.as<fm3d::SiftLevel>(), S.siftOctaveLayers, 0,
+                           c->siftKp.as<fm3d_keypoint>(), c->siftPos.as<int>(), P, c->siftDesc.as<float>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(desc, c->siftDesc.p, (size_t)P * 128 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+// FastFeatureDetector(thr, nonmax).detect (features2d/src/fast.cpp): FAST-9 on the image itself, the
+// ORB level-0 kernels with no edge border; KeyPoint(x, y, 7, -1, score) in raster order, the score 0
+// without non-max suppression (FAST_t computes it only for the suppression)
+int fast_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int thr, bool nonmax, std::vector<fm3d_keypoint>& k) {
+    k.clear();
+    thr = std::min(std::max(thr, 0), 255);
+    const long long total = (long long)w * h;
+    if (total > INT32_MAX / 2) return fail(c, FM3D_ERR_INVALID, "image too large for FAST");
+    const fm3d::OrbLevel lv{w, h, 0};
+    int r;
+    if ((r = ensure_scan_tmp(c, (int)total))) return r;
+    HIPCHK(c, c->orbPyr.ensure((size_t)total + 64));
+    HIPCHK(c, c->orbLev.ensure(sizeof(fm3d::OrbLevel)));
+    HIPCHK(c, c->orbMap.ensure((size_t)total * sizeof(uint16_t) + 64));
+    HIPCHK(c, c->orbFlag.ensure((size_t)(total + 1) * sizeof(int)));
+    HIPCHK(c, c->orbPos.ensure((size_t)(total + 1) * sizeof(int)));
+    HIPCHK(c, hipMemcpyAsync(c->orbPyr.p, img, (size_t)total, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->orbLev.p, &lv, sizeof(lv), hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_orb_fast(c->orbPyr.as<uint8_t>(), c->orbLev.as<fm3d::OrbLevel>(), 1, total, thr, 0, nonmax ? 1 : 0,
+                          c->orbMap.as<uint16_t>(), c->orbFlag.as<int>(), c->stream);
+    fm3d::launch_exclusive_scan(c->orbFlag.as<int>(), (int)total, c->orbPos.as<int>(), c->count.as<int>(), c->scanTmp.p,
+                                c->stream);
+    HIPCHK(c, hipGetLastError());
+    int nc = 0;
+    HIPCHK(c, hipMemcpyAsync(&nc, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nc == 0) return FM3D_OK;
+    HIPCHK(c, c->orbKp.ensure((size_t)(nc + 1) * sizeof(fm3d_keypoint)));
+    fm3d::launch_orb_fast_scatter(c->orbMap.as<uint16_t>(), c->orbLev.as<fm3d::OrbLevel>(), 1, total,
+                                  c->orbFlag.as<int>(), c->orbPos.as<int>(), c->orbKp.as<fm3d_keypoint>(), c->stream);
+    k.resize(nc);
+    HIPCHK(c, hipMemcpyAsync(k.data(), c->orbKp.p, (size_t)nc * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!nonmax)
+        for (auto& q : k) q.response = 0.f;
     return FM3D_OK;
 }
 
@@ -1874,7 +1966,9 @@ int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_
 int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, int P, int size, float* desc) {
     if (!c || P < 0 || size <= 0 || (P && (!patches || !desc))) return FM3D_ERR_INVALID;
     const fm3d_settings& S = c->s;
-    if (S.extractorType != FM3D_FEAT_SURF) return fail(c, FM3D_ERR_UNSUPPORTED, "only the SURF extractor runs on the GPU");
+    if (S.extractorType == FM3D_FEAT_SIFT) return sift_patches(c, patches, P, size, desc);
+    if (S.extractorType != FM3D_FEAT_SURF)
+        return fail(c, FM3D_ERR_UNSUPPORTED, "only the SURF and SIFT extractors describe patches on the GPU");
     if (P == 0) return FM3D_OK;
     // descriptorsmatcher.cpp:146-158: one keypoint per patch at (center, center), center =
     // (int)floor(size / 2), size = the patch edge, angle -1, response 1, octave 0, class_id 0
@@ -1973,7 +2067,7 @@ int fm3d_orb_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoint
     HIPCHK(c, c->orbFlag.ensure((size_t)(tot + 1) * sizeof(int)));
     HIPCHK(c, c->orbPos.ensure((size_t)(tot + 1) * sizeof(int)));
     fm3d::launch_orb_fast(c->orbPyr.as<uint8_t>(), c->orbLev.as<fm3d::OrbLevel>(), nl, P.total, S.orbFastThreshold,
-                          S.orbEdgeThreshold, c->orbMap.as<uint16_t>(), c->orbFlag.as<int>(), c->stream);
+                          S.orbEdgeThreshold, 1, c->orbMap.as<uint16_t>(), c->orbFlag.as<int>(), c->stream);
     fm3d::launch_exclusive_scan(c->orbFlag.as<int>(), tot, c->orbPos.as<int>(), c->count.as<int>(), c->scanTmp.p,
                                 c->stream);
     HIPCHK(c, hipGetLastError());
@@ -2199,6 +2293,153 @@ int fm3d_sift_pyramid(fm3d_ctx* c, const uint8_t* img, int w, int h, int firstOc
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return FM3D_OK;
+}
+
+int fm3d_fast_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int threshold, int nonmax, fm3d_keypoint* kpts,
+                     int cap, int* n) {
+    if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    std::vector<fm3d_keypoint> k;
+    int r;
+    if ((r = fast_detect(c, img, w, h, threshold, nonmax != 0, k))) return r;
+    for (int i = 0; i < (int)k.size() && i < cap; i++) kpts[i] = k[i];
+    *n = (int)k.size();
+    return FM3D_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// one detector call into a host vector (the entries' cap / count protocol)
+template <class F>
+int detect_into(F&& f, std::vector<fm3d_keypoint>& k) {
+    int cap = 4096, n = 0, r;
+    for (;;) {
+        k.resize(cap);
+        if ((r = f(k.data(), cap, &n))) return r;
+        if (n <= cap) break;
+        cap = n;
+    }
+    k.resize(n);
+    return FM3D_OK;
+}
+
+// the settings' detector as it stands (STATIC, or one ADAPTIVE detector call with threshold thr)
+int detect_static(fm3d_ctx* c, const uint8_t* img, int w, int h, std::vector<fm3d_keypoint>& k) {
+    const fm3d_settings& S = c->s;
+    switch (S.detectorType) {
+    case FM3D_FEAT_SURF:
+        return detect_into([&](fm3d_keypoint* p, int cap, int* n) { return fm3d_surf_detect(c, img, w, h, p, cap, n, nullptr); }, k);
+    case FM3D_FEAT_ORB:
+        return detect_into([&](fm3d_keypoint* p, int cap, int* n) { return fm3d_orb_detect(c, img, w, h, p, cap, n, nullptr); }, k);
+    case FM3D_FEAT_SIFT:
+        return detect_into([&](fm3d_keypoint* p, int cap, int* n) { return fm3d_sift_detect(c, img, w, h, p, cap, n, nullptr); }, k);
+    case FM3D_FEAT_FAST:
+        return fast_detect(c, img, w, h, S.fastThreshold, S.fastNonmax != 0, k);
+    default:
+        return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' detector type has no GPU implementation");
+    }
+}
+
+// DynamicAdaptedFeatureDetector(AdjusterAdapter::create(type), min, max, iters)::detect
+// (features2d/src/dynamic.cpp): detect, then raise / lower the adjuster's threshold until the count
+// is in [min, max], the threshold leaves the adjuster's range, the iterations run out or it
+// oscillates.  FastAdjuster(20, true, 1, 200): FastFeatureDetector(thresh, true), -- / ++ by one;
+// SurfAdjuster(400, 2, 1000): the default SURF (4 octaves, 2 layers, not upright) at hessianThreshold
+// thresh, * 0.9 (floored at 1.1) / * 1.1.  The keypoints are the last call's.
+int detect_adaptive(fm3d_ctx* c, const uint8_t* img, int w, int h, std::vector<fm3d_keypoint>& k) {
+    const fm3d_settings S = c->s;
+    const bool fast = S.detectorType == FM3D_FEAT_FAST;
+    if (!fast && S.detectorType != FM3D_FEAT_SURF)
+        return fail(c, FM3D_ERR_UNSUPPORTED, "ADAPTIVE runs the FAST and SURF adjusters on the GPU");
+    double thresh = fast ? 20 : 400;
+    const double minT = fast ? 1 : 2, maxT = fast ? 200 : 1000;
+    bool down = false, up = false, good = false;
+    int iters = S.adaptiveMaxIters, r = FM3D_OK;
+    k.clear();
+    while (iters > 0 && !(down && up) && !good && thresh > minT && thresh < maxT) {
+        if (fast) {
+            r = fast_detect(c, img, w, h, (int)thresh, true, k);
+        } else {
+            fm3d_settings t = S;  // FeatureDetector::create("SURF") + set("hessianThreshold", thresh)
+            t.detectorMode = 0;
+            t.surfHessianThreshold = thresh;
+            t.surfOctaves = 4;
+            t.surfOctaveLayers = 2;
+            t.surfExtended = 0;
+            t.surfUpright = 0;
+            c->s = t;
+            r = detect_static(c, img, w, h, k);
+            c->s = S;
+        }
+        if (r) return r;
+        if ((int)k.size() < S.adaptiveMinFeatures) {
+            down = true;
+            if (fast)
+                thresh -= 1;
+            else if ((thresh *= 0.9) < 1.1)
+                thresh = 1.1;
+        } else if ((int)k.size() > S.adaptiveMaxFeatures) {
+            up = true;
+            if (fast)
+                thresh += 1;
+            else
+                thresh *= 1.1;
+        } else {
+            good = true;
+        }
+        iters--;
+    }
+    return FM3D_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int fm3d_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, fm3d_keypoint* kpts, int cap, int* n) {
+    if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    std::vector<fm3d_keypoint> k;
+    int r = c->s.detectorMode == 1 ? detect_adaptive(c, img, w, h, k) : detect_static(c, img, w, h, k);
+    if (r) return r;
+    for (int i = 0; i < (int)k.size() && i < cap; i++) kpts[i] = k[i];
+    *n = (int)k.size();
+    return FM3D_OK;
+}
+
+int fm3d_descriptor_info(const fm3d_ctx* c, int* cols, int* type) {
+    if (!c || !cols || !type) return FM3D_ERR_INVALID;
+    switch (c->s.extractorType) {
+    case FM3D_FEAT_SURF:
+        *cols = c->s.surfExtended ? 128 : 64;
+        *type = FM3D_DESC_F32;
+        return FM3D_OK;
+    case FM3D_FEAT_SIFT:
+        *cols = 128;
+        *type = FM3D_DESC_F32;
+        return FM3D_OK;
+    case FM3D_FEAT_ORB:
+        *cols = 32;
+        *type = FM3D_DESC_BITS;
+        return FM3D_OK;
+    default:
+        return FM3D_ERR_UNSUPPORTED;
+    }
+}
+
+int fm3d_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n, fm3d_keypoint* kout,
+                 int32_t* kept, int* nOut, void* desc) {
+    switch (c ? c->s.extractorType : FM3D_FEAT_OTHER) {
+    case FM3D_FEAT_SURF:
+        return fm3d_surf_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<float*>(desc));
+    case FM3D_FEAT_SIFT:
+        return fm3d_sift_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<float*>(desc));
+    case FM3D_FEAT_ORB:
+        return fm3d_orb_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<uint8_t*>(desc));
+    default:
+        return c ? fail(c, FM3D_ERR_UNSUPPORTED, "the settings' extractor type has no GPU implementation")
+                 : FM3D_ERR_INVALID;
+    }
 }
 
 int fm3d_orb_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,

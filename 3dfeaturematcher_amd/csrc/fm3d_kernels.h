@@ -190,8 +190,8 @@ struct OrbBlurK {  // GaussianBlur(7x7, 2): the x256 fixed-point kernel; the SSE
 };
 void launch_orb_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh, const int* xofs,
                        const short* alpha, const int* yofs, const short* beta, int xmax, int xs, hipStream_t s);
-// map: corner | score per pixel; flag: the keypoints FAST + non-max + the edge border keep
-void launch_orb_fast(const uint8_t* pyr, const OrbLevel* L, int nL, long long total, int thr, int border,
+// map: corner | score per pixel; flag: the keypoints FAST (+ non-max when nonmax) + the edge border keep
+void launch_orb_fast(const uint8_t* pyr, const OrbLevel* L, int nL, long long total, int thr, int border, int nonmax,
                      uint16_t* map, int* flag, hipStream_t s);
 void launch_orb_fast_scatter(const uint16_t* map, const OrbLevel* L, int nL, long long total, const int* flag,
                              const int* pos, fm3d_keypoint* out, hipStream_t s);
@@ -221,10 +221,11 @@ struct SiftCand {     // a scale-space extremum, then adjustLocalExtrema's keypo
     int koct;              // KeyPoint::octave: octv + (layer << 8) + (round((xi + 0.5) * 255) << 16)
     int octave, layer, r, c, ok;
 };
-void launch_sift_init(const uint8_t* img, float* dst, const SiftResize& p, hipStream_t s);
+// batch: that many equal-size images back to back (patches)
+void launch_sift_init(const uint8_t* img, float* dst, const SiftResize& p, int batch, hipStream_t s);
 size_t sift_blur_lds(int n);
-// dst = GaussianBlur(src, taps[0..n)), dog = dst - src (dog may be null)
-void launch_sift_blur(const float* src, float* dst, float* dog, int w, int h, const float* taps, int n,
+// dst = GaussianBlur(src, taps[0..n)), dog = dst - src (dog may be null); batch images back to back
+void launch_sift_blur(const float* src, float* dst, float* dog, int w, int h, const float* taps, int n, int batch,
                       hipStream_t s);
 void launch_sift_down(const float* src, int sw, int sh, float* dst, int dw, int dh, double ifx, double ify,
                       hipStream_t s);
@@ -237,8 +238,9 @@ void launch_sift_adjust(const float* dog, const SiftLevel* DL, int L, float cont
 // angles: 36 per candidate (the first npk[q] are its peaks, in bin order)
 void launch_sift_orient(const float* gp, const SiftLevel* GL, int L, const SiftCand* cand, int n, float* angles,
                         int* npk, hipStream_t s);
-void launch_sift_desc(const float* gp, const SiftLevel* GL, int L, int firstOctave, const fm3d_keypoint* kp, int n,
-                      float* desc, hipStream_t s);
+// lvl (may be null): the level of keypoint q, else its octave code's (octave - firstOctave) * (L + 3) + layer
+void launch_sift_desc(const float* gp, const SiftLevel* GL, int L, int firstOctave, const fm3d_keypoint* kp,
+                      const int* lvl, int n, float* desc, hipStream_t s);
 
 // ---------------- compaction ----------------
 // out[k] = in[i] for flag[i] != 0, stable; *count (device) = number kept.  tmp >= scan_tmp_bytes(n).

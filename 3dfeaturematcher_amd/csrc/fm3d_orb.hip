@@ -129,7 +129,8 @@ __global__ __launch_bounds__(256) void orb_fast_kernel(const uint8_t* __restrict
 // flag = a corner whose score beats its 8 neighbours' (0 for non-corners), inside the edge border
 // (runByImageBorder on the level: Rect(b, b, w - 2b, h - 2b))
 __global__ __launch_bounds__(256) void orb_nms_kernel(const uint16_t* __restrict__ map, const OrbLevel* __restrict__ L,
-                                                      int nL, long long total, int border, int* __restrict__ flag) {
+                                                      int nL, long long total, int border, int nonmax,
+                                                      int* __restrict__ flag) {
     const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
     if (t >= total) return;
     const int l = level_of(L, nL, t);
@@ -141,8 +142,8 @@ __global__ __launch_bounds__(256) void orb_nms_kernel(const uint16_t* __restrict
         y < lv.h - border) {
         const int s = m & 0xff, w = lv.w;
         const uint16_t* c = map + t;
-        f = s > (c[-1] & 0xff) && s > (c[1] & 0xff) && s > (c[-w - 1] & 0xff) && s > (c[-w] & 0xff) &&
-            s > (c[-w + 1] & 0xff) && s > (c[w - 1] & 0xff) && s > (c[w] & 0xff) && s > (c[w + 1] & 0xff);
+        f = !nonmax || (s > (c[-1] & 0xff) && s > (c[1] & 0xff) && s > (c[-w - 1] & 0xff) && s > (c[-w] & 0xff) &&
+            s > (c[-w + 1] & 0xff) && s > (c[w - 1] & 0xff) && s > (c[w] & 0xff) && s > (c[w + 1] & 0xff));
     }
     flag[t] = f;
 }
@@ -309,11 +310,11 @@ void launch_orb_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw,
                                                                   xmax, xs);
 }
 
-void launch_orb_fast(const uint8_t* pyr, const OrbLevel* L, int nL, long long total, int thr, int border,
+void launch_orb_fast(const uint8_t* pyr, const OrbLevel* L, int nL, long long total, int thr, int border, int nonmax,
                      uint16_t* map, int* flag, hipStream_t s) {
     if (total <= 0) return;
     orb_fast_kernel<<<blocks(total), 256, 0, s>>>(pyr, L, nL, total, thr, map);
-    orb_nms_kernel<<<blocks(total), 256, 0, s>>>(map, L, nL, total, border, flag);
+    orb_nms_kernel<<<blocks(total), 256, 0, s>>>(map, L, nL, total, border, nonmax, flag);
 }
 
 void launch_orb_fast_scatter(const uint16_t* map, const OrbLevel* L, int nL, long long total, const int* flag,

@@ -148,6 +148,12 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->siftContrastThreshold = 0.04;
     s->siftEdgeThreshold = 10;
     s->siftSigma = 1.6;
+    s->detectorMode = 0;
+    s->fastThreshold = 10;  // cv::FastFeatureDetector's defaults
+    s->fastNonmax = 1;
+    s->adaptiveMinFeatures = 400;  // cv::DynamicAdaptedFeatureDetector's defaults
+    s->adaptiveMaxFeatures = 500;
+    s->adaptiveMaxIters = 5;
     return FM3D_OK;
 }
 
@@ -193,12 +199,29 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
         };
         std::string mode = "STATIC", det, ex;
         str("FeatureOptions.DetectorMode", mode);
-        if (str("FeatureOptions.DetectorType", det))
-            s->detectorType = mode != "STATIC" ? FM3D_FEAT_OTHER
-                              : det == "SURF"  ? FM3D_FEAT_SURF
-                              : det == "ORB"   ? FM3D_FEAT_ORB
-                              : det == "SIFT"  ? FM3D_FEAT_SIFT
-                                               : FM3D_FEAT_OTHER;
+        s->detectorMode = mode == "ADAPTIVE" ? 1 : 0;
+        if (str("FeatureOptions.DetectorType", det)) {
+            if (mode == "STATIC")
+                s->detectorType = det == "SURF"   ? FM3D_FEAT_SURF
+                                  : det == "ORB"  ? FM3D_FEAT_ORB
+                                  : det == "SIFT" ? FM3D_FEAT_SIFT
+                                  : det == "FAST" ? FM3D_FEAT_FAST
+                                                  : FM3D_FEAT_OTHER;
+            else  // ADAPTIVE: the FAST / SURF adjusters (STAR's has no GPU implementation)
+                s->detectorType = mode != "ADAPTIVE" ? FM3D_FEAT_OTHER
+                                  : det == "SURF"    ? FM3D_FEAT_SURF
+                                  : det == "FAST"    ? FM3D_FEAT_FAST
+                                                     : FM3D_FEAT_OTHER;
+        }
+        {
+            int nm = s->fastNonmax;
+            get_i(kv, "FeatureOptions.FastDetector.Threshold", &s->fastThreshold);
+            get_i(kv, "FeatureOptions.FastDetector.NonMaxSuppression", &nm);
+            s->fastNonmax = nm > 0;  // (int)fs[...] > 0
+        }
+        get_i(kv, "FeatureOptions.Adaptive.MinFeatures", &s->adaptiveMinFeatures);
+        get_i(kv, "FeatureOptions.Adaptive.MaxFeatures", &s->adaptiveMaxFeatures);
+        get_i(kv, "FeatureOptions.Adaptive.MaxIters", &s->adaptiveMaxIters);
         if (str("FeatureOptions.ExtractorType", ex))
             s->extractorType = ex == "SURF"   ? FM3D_FEAT_SURF
                                : ex == "ORB"  ? FM3D_FEAT_ORB

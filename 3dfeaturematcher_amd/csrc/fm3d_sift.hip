@@ -56,6 +56,8 @@ __global__ __launch_bounds__(256) void sift_init_kernel(const uint8_t* __restric
                                                         SiftResize p) {
     const int dx = blockIdx.x * 256 + threadIdx.x, dy = blockIdx.y;
     if (dx >= p.dw) return;
+    img += (size_t)blockIdx.z * p.sw * p.sh;  // a batch of equal-size images (patches)
+    dst += (size_t)blockIdx.z * p.dw * p.dh;
     if (!p.doubled) {
         dst[(size_t)dy * p.dw + dx] = (float)img[(size_t)dy * p.sw + dx];
         return;
@@ -101,6 +103,12 @@ __global__ __launch_bounds__(256) void sift_blur_kernel(const float* __restrict_
     float* T = lds;            // TH x TW source tile (reflected halo)
     float* R = lds + TH * TW;  // TH x kBX row-filtered
     const int x0 = blockIdx.x * kBX, y0 = blockIdx.y * kBY, tid = threadIdx.x;
+    {  // a batch of equal-size images (patches): image blockIdx.z
+        const size_t b = (size_t)blockIdx.z * w * h;
+        src += b;
+        dst += b;
+        if (dog) dog += b;
+    }
     for (int i = tid; i < TH * TW; i += 256) {
         const int ty = i / TW, tx = i - ty * TW;
         const int sy = fm3d_cv_reflect101(y0 - r + ty, h), sx = fm3d_cv_reflect101(x0 - r + tx, w);
@@ -380,7 +388,7 @@ __global__ __launch_bounds__(256) void sift_orient_kernel(const float* __restric
 // calcSIFTDescriptor (d 4, n 8) for keypoint q of kp (octave = the SIFT octave code)
 __global__ __launch_bounds__(256) void sift_desc_kernel(const float* __restrict__ gp, const SiftLevel* __restrict__ GL,
                                                         int L, int firstOctave, const fm3d_keypoint* __restrict__ kp,
-                                                        int n, float* __restrict__ desc) {
+                                                        const int* __restrict__ lvl, int n, float* __restrict__ desc) {
     __shared__ float hs[4][360 + 128];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, q = blockIdx.x * 4 + wv;
     if (q >= n) return;
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(256) void sift_desc_kernel(const float* __restrict_
     const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
     const float size = K.size * scale;
     const float ptx = K.x * scale, pty = K.y * scale;
-    const SiftLevel G = GL[(octave - firstOctave) * (L + 3) + layer];
+    const SiftLevel G = GL[lvl ? lvl[q] : (octave - firstOctave) * (L + 3) + layer];
     const float* g = gp + G.first;
     float ori = 360.f - K.angle;
     if (fabsf(ori - 360.f) < FLT_EPSILON) ori = 0.f;
@@ -537,8 +545,8 @@ __global__ __launch_bounds__(256) void sift_desc_kernel(const float* __restrict_
 
 }  // namespace
 
-void launch_sift_init(const uint8_t* img, float* dst, const SiftResize& p, hipStream_t s) {
-    hipLaunchKernelGGL(sift_init_kernel, dim3((p.dw + 255) / 256, p.dh), dim3(256), 0, s, img, dst, p);
+void launch_sift_init(const uint8_t* img, float* dst, const SiftResize& p, int batch, hipStream_t s) {
+    hipLaunchKernelGGL(sift_init_kernel, dim3((p.dw + 255) / 256, p.dh, batch), dim3(256), 0, s, img, dst, p);
 }
 
 size_t sift_blur_lds(int n) {
@@ -546,10 +554,10 @@ size_t sift_blur_lds(int n) {
     return sizeof(float) * ((size_t)(kBY + 2 * r) * (kBX + 2 * r) + (size_t)(kBY + 2 * r) * kBX);
 }
 
-void launch_sift_blur(const float* src, float* dst, float* dog, int w, int h, const float* taps, int n,
+void launch_sift_blur(const float* src, float* dst, float* dog, int w, int h, const float* taps, int n, int batch,
                       hipStream_t s) {
-    hipLaunchKernelGGL(sift_blur_kernel, dim3((w + kBX - 1) / kBX, (h + kBY - 1) / kBY), dim3(256), sift_blur_lds(n), s,
-                       src, dst, dog, w, h, taps, n);
+    hipLaunchKernelGGL(sift_blur_kernel, dim3((w + kBX - 1) / kBX, (h + kBY - 1) / kBY, batch), dim3(256),
+                       sift_blur_lds(n), s, src, dst, dog, w, h, taps, n);
 }
 
 void launch_sift_down(const float* src, int sw, int sh, float* dst, int dw, int dh, double ifx, double ify,
@@ -582,10 +590,10 @@ void launch_sift_orient(const float* gp, const SiftLevel* GL, int L, const SiftC
     hipLaunchKernelGGL(sift_orient_kernel, dim3((n + 3) / 4), dim3(256), 0, s, gp, GL, L, cand, n, angles, npk);
 }
 
-void launch_sift_desc(const float* gp, const SiftLevel* GL, int L, int firstOctave, const fm3d_keypoint* kp, int n,
-                      float* desc, hipStream_t s) {
+void launch_sift_desc(const float* gp, const SiftLevel* GL, int L, int firstOctave, const fm3d_keypoint* kp,
+                      const int* lvl, int n, float* desc, hipStream_t s) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(sift_desc_kernel, dim3((n + 3) / 4), dim3(256), 0, s, gp, GL, L, firstOctave, kp, n, desc);
+    hipLaunchKernelGGL(sift_desc_kernel, dim3((n + 3) / 4), dim3(256), 0, s, gp, GL, L, firstOctave, kp, lvl, n, desc);
 }
 
 }  // namespace fm3d

@@ -91,11 +91,20 @@ typedef struct fm3d_settings {
        node) */
     int siftNumFeatures, siftOctaveLayers;
     double siftContrastThreshold, siftEdgeThreshold, siftSigma;
+    /* FeatureOptions.DetectorMode: 0 STATIC, 1 ADAPTIVE (DynamicAdaptedFeatureDetector over
+       AdjusterAdapter::create(DetectorType), :185-201; FAST and SURF run on the GPU);
+       FeatureOptions.FastDetector.Threshold / NonMaxSuppression (:215-222, cv::FastFeatureDetector's
+       defaults 10 / 1); FeatureOptions.Adaptive.MinFeatures / MaxFeatures / MaxIters (the
+       DynamicAdaptedFeatureDetector defaults 400 / 500 / 5) */
+    int detectorMode;
+    int fastThreshold, fastNonmax;
+    int adaptiveMinFeatures, adaptiveMaxFeatures, adaptiveMaxIters;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
 #define FM3D_FEAT_ORB 1
 #define FM3D_FEAT_SIFT 2
+#define FM3D_FEAT_FAST 3
 #define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
@@ -284,8 +293,10 @@ int fm3d_surf_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, 
 
 /* DescriptorsMatcher::extractDescriptorsFromPatches (descriptorsmatcher.cpp:133-174): per square
    patch (P x size x size bytes, e.g. the fm3d_export_patches output) one keypoint at
-   (floor(size/2), floor(size/2)) of size `size`, described by the settings' SURF extractor; the
-   reference's descriptors Mat, one row per patch: P x (128 | 64) floats. */
+   (floor(size/2), floor(size/2)) of size `size`, angle -1, octave 0, described by the settings' SURF
+   extractor (P x (128 | 64) floats) or SIFT extractor (P x 128 floats: the patch's own firstOctave-0
+   level 0, as SIFT::operator() with that keypoint builds it); the reference's descriptors Mat, one
+   row per patch. */
 int fm3d_extract_descriptors_from_patches(fm3d_ctx *ctx, const uint8_t *patches, int P, int size, float *desc);
 
 /* ---------------- feature detection + description (ORB, OpenCV 2.4) ---------------- */
@@ -334,6 +345,25 @@ int fm3d_sift_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, 
    NULL): (w, h) per level; out (may be NULL to ask for the sizes): *total floats. */
 int fm3d_sift_pyramid(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int firstOctave, int nOctaves, int dog,
                       float *out, int32_t *sizes, int64_t *total);
+
+/* ---------------- any detector / extractor of the settings ---------------- */
+/* cv::FastFeatureDetector(threshold, nonmax).detect (descriptorsmatcher.cpp:215-222): FAST-9 on the
+   image, KeyPoint(x, y, 7, -1, score) in raster order (score 0 without non-max suppression). */
+int fm3d_fast_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int threshold, int nonmax,
+                     fm3d_keypoint *kpts, int cap, int *n);
+/* feature_detector_->detect(img, kpts) of generateDetector (descriptorsmatcher.cpp:110-111, 176-293):
+   STATIC SURF / ORB / SIFT / FAST, or ADAPTIVE with the FAST or SURF adjuster (the threshold walk of
+   DynamicAdaptedFeatureDetector).  *n = all; min(*n, cap) written.  FM3D_ERR_UNSUPPORTED for the
+   detector types without a GPU implementation (STAR, MSER, the STAR adjuster). */
+int fm3d_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, fm3d_keypoint *kpts, int cap, int *n);
+/* the row layout of the settings' extractor: SURF 64 | 128 and SIFT 128 (FM3D_DESC_F32), ORB 32 bytes
+   (FM3D_DESC_BITS); FM3D_ERR_UNSUPPORTED for BRISK / FREAK. */
+int fm3d_descriptor_info(const fm3d_ctx *ctx, int *cols, int *type);
+/* descriptor_extractor_->compute(img, kpts, desc) of generateExtractor (:113-114, 295-359): the
+   settings' SURF / SIFT / ORB extractor on any keypoints (fm3d_surf_compute / fm3d_sift_compute /
+   fm3d_orb_compute); desc: n rows of fm3d_descriptor_info's layout. */
+int fm3d_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const fm3d_keypoint *kpts, int n,
+                 fm3d_keypoint *kout, int32_t *kept, int *nOut, void *desc);
 
 /* ---------------- the whole hot path, device resident ---------------- */
 /* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */

@@ -29,13 +29,13 @@
  * What differs, and why:
  *   - feature detection/description (descriptorsmatcher.cpp:110-115): when main.cpp:94 passes
  *     empty vectors, the settings' detector / extractor runs on the GPU (SURF of
- *     build/settings.yml, fm3d_surf_detect; see fm3d.h for the detector types built); a detector
+ *     build/settings.yml, fm3d_surf_detect; ORB and SIFT too, see fm3d.h); a detector
  *     without a GPU implementation falls back to the image's feature side files:
  *     <image>.kpts.f32 (N x 2 float32 positions) and <image>.desc.u8 (N x 128 uint8) or
  *     <image>.desc.f32 (N x 128 float32) -- FeatureOptions.ExtractorType ORB / BRISK / FREAK
  *     selects Hamming matching on <image>.desc.u8 rows of 32 / 64 bytes (descriptorsmatcher.cpp:64-71);
  *   - the matcher is exact brute force, ties to the lowest train index;
- *   - extractDescriptorsFromPatches runs the settings' SURF extractor on the GPU;
+ *   - extractDescriptorsFromPatches runs the settings' SURF or SIFT extractor on the GPU;
  *   - the PCL viewer is visual only: start/stopVisualizerThread and the view* functions are
  *     no-ops; drawMatches / drawBackProjectedPoints draw with plain loops, in the reference's
  *     colours (cv::RNG(0xFFF0FF0F), random_color);
@@ -482,7 +482,7 @@ public:
         for (int i = 0; i < n; i++) matches.push_back(reinterpret_cast<const cv::DMatch&>(tmp[i]));
     }
     // descriptorsmatcher.cpp:133-174: per patch one keypoint at its centre, size = the patch edge,
-    // described by the settings' SURF extractor on the GPU; one descriptor row per patch
+    // described by the settings' SURF or SIFT extractor on the GPU; one descriptor row per patch
     void extractDescriptorsFromPatches(const std::vector<cv::Mat>& patchesVector, cv::Mat& descriptors) {
         if (patchesVector.empty()) throw fm3d::compat::Error(FM3D_ERR_INVALID, "no patches");  // descriptorsVector[0]
         const int size = patchesVector[0].rows;
@@ -493,7 +493,7 @@ public:
                 throw fm3d::compat::Error(FM3D_ERR_INVALID, "patches must be equal-size square 8-bit images");
             std::memcpy(&all[i * (size_t)size * size], m.data, (size_t)size * size);
         }
-        const int dsize = s_.surfExtended ? 128 : 64;
+        const int dsize = s_.extractorType == FM3D_FEAT_SIFT ? 128 : (s_.surfExtended ? 128 : 64);
         descriptors.create((int)patchesVector.size(), dsize, CV_32FC1);
         fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
         fm3d::compat::check(c, fm3d_extract_descriptors_from_patches(c, all.data(), (int)patchesVector.size(), size,
@@ -501,7 +501,7 @@ public:
     }
 
 private:
-    // the detector + extractor (:110-115): the settings' SURF or ORB on the GPU; another detector
+    // the detector + extractor (:110-115): the settings' SURF, ORB or SIFT on the GPU; another detector
     // type has no GPU implementation, so its output comes from the images' side files
     // (<image>.kpts.f32 and <image>.desc.u8 / .desc.f32), or from the caller's keypoints + descriptors
     void features(const cv::Mat& img, std::vector<cv::KeyPoint>& kpts, cv::Mat& d) {
@@ -547,6 +547,30 @@ private:
             if (m > 0) std::memcpy(static_cast<void*>(kpts.data()), ko.data(), (size_t)m * sizeof(fm3d_keypoint));
             d.create(m, 32, CV_8UC1);
             if (m > 0) std::memcpy(d.data, desc.data(), (size_t)m * 32);
+            return;
+        }
+        if (s_.detectorType == FM3D_FEAT_SIFT && s_.extractorType == FM3D_FEAT_SIFT) {
+            // the reference's two calls (:110-115): detect, then compute on the detected keypoints;
+            // SIFT's descriptors are CV_32F rows holding integers 0..255
+            fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
+            int cap = std::max(4096, 2 * s_.siftNumFeatures), n = 0;
+            std::vector<fm3d_keypoint> k;
+            for (;;) {
+                k.resize(cap);
+                fm3d::compat::check(c, fm3d_sift_detect(c, img.data, img.cols, img.rows, k.data(), cap, &n, nullptr));
+                if (n <= cap) break;
+                cap = n;
+            }
+            std::vector<fm3d_keypoint> ko(n > 0 ? n : 1);
+            std::vector<float> desc((size_t)(n > 0 ? n : 1) * 128);
+            int m = 0;
+            if (n > 0)
+                fm3d::compat::check(c, fm3d_sift_compute(c, img.data, img.cols, img.rows, k.data(), n, ko.data(), nullptr,
+                                                         &m, desc.data()));
+            kpts.assign(m, cv::KeyPoint());
+            if (m > 0) std::memcpy(static_cast<void*>(kpts.data()), ko.data(), (size_t)m * sizeof(fm3d_keypoint));
+            d.create(m, 128, CV_32FC1);
+            if (m > 0) std::memcpy(d.data, desc.data(), (size_t)m * 128 * sizeof(float));
             return;
         }
         if (!kpts.empty() && !d.empty()) return;

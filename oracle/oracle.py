@@ -440,6 +440,17 @@ def fast9(img, thr=20):
     return out[:n]
 
 
+def fast_detect(img, thr=10, nonmax=True):
+    """FastFeatureDetector(thr, nonmax).detect(img): KEYPOINT records in raster order"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    args = (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(thr), ctypes.c_int(1 if nonmax else 0))
+    n = lib().orc_fast_detect(*args, None, 0)
+    out = np.zeros(max(n, 1), dtype=KEYPOINT)
+    lib().orc_fast_detect(*args, _kp(out), ctypes.c_int(n))
+    return out[:n]
+
+
 def nth_element(kpts, nth):
     """std::nth_element(k, k + nth, k + n, KeypointResponseGreater()) on a copy"""
     k = np.ascontiguousarray(kpts, dtype=KEYPOINT).copy()
@@ -709,3 +720,36 @@ def sift_compute(img, kpts, nOctaveLayers=3, sigma=1.6):
     if m < 0:
         raise ValueError("SIFT compute: OpenCV asserts (octave < -1, layer > nOctaveLayers + 2, or an empty octave)")
     return kout[:m], kept[:m], d[:m]
+
+
+# ---------------------------------------------------------------- DynamicAdaptedFeatureDetector
+def adaptive_detect(img, kind, min_features=400, max_features=500, max_iters=5):
+    """DynamicAdaptedFeatureDetector(AdjusterAdapter::create(kind), min, max, iters)::detect
+    (OpenCV 2.4 features2d/src/dynamic.cpp): FastAdjuster(20, true, 1, 200) steps the FAST threshold by
+    one; SurfAdjuster(400, 2, 1000) runs the default SURF (4 octaves, 2 layers, not upright) and scales
+    its Hessian threshold by 0.9 (floored at 1.1) / 1.1.  Returns the last call's keypoints."""
+    fast = kind == "FAST"
+    thresh, lo, hi = (20, 1, 200) if fast else (400.0, 2, 1000)
+    down = up = good = False
+    it = max_iters
+    k = np.zeros(0, dtype=KEYPOINT)
+    while it > 0 and not (down and up) and not good and lo < thresh < hi:
+        k = fast_detect(img, int(thresh), True) if fast else surf_detect(img, float(thresh), 4, 2, upright=False)
+        if len(k) < min_features:
+            down = True
+            if fast:
+                thresh -= 1
+            else:
+                thresh *= 0.9
+                if thresh < 1.1:
+                    thresh = 1.1
+        elif len(k) > max_features:
+            up = True
+            if fast:
+                thresh += 1
+            else:
+                thresh *= 1.1
+        else:
+            good = True
+        it -= 1
+    return k

@@ -201,9 +201,11 @@ static int fast_corner(const uint8_t *img, int w, int x, int y, int thr, int *sc
     return 1;
 }
 
-/* FAST(img, keypoints, thr, nonmaxSuppression = true): KeyPoint(x, y, 7, -1, score) in raster
-   order; returns the count (out may be NULL to count) */
-ORC_API int orc_fast9(const uint8_t *img, int w, int h, int thr, orc_kpt *out, int cap)
+/* FAST(img, keypoints, thr, nonmaxSuppression): KeyPoint(x, y, 7, -1, score) in raster order, the
+   score 0 without non-max suppression (FAST_t computes it only for the suppression); returns the
+   count (out may be NULL to count).  FastFeatureDetector(thr, nonmax) (features2d/src/fast.cpp,
+   descriptorsmatcher.cpp:215-222) is this on the image itself. */
+ORC_API int orc_fast_detect(const uint8_t *img, int w, int h, int thr, int nonmax, orc_kpt *out, int cap)
 {
     /* S: the (uchar) score of every corner, 0 elsewhere (FAST_t's row buffers); C: corner flags */
     uint8_t *S = (uint8_t *)calloc((size_t)w * h, 1), *C = (uint8_t *)calloc((size_t)w * h, 1);
@@ -222,11 +224,11 @@ ORC_API int orc_fast9(const uint8_t *img, int w, int h, int thr, orc_kpt *out, i
             const uint8_t *c = S + (size_t)y * w + x;
             const int s = c[0];
             if (!C[(size_t)y * w + x]) continue;
-            if (!(s > c[-1] && s > c[1] && s > c[-w - 1] && s > c[-w] && s > c[-w + 1] && s > c[w - 1] && s > c[w] &&
-                  s > c[w + 1]))
+            if (nonmax && !(s > c[-1] && s > c[1] && s > c[-w - 1] && s > c[-w] && s > c[-w + 1] && s > c[w - 1] &&
+                            s > c[w] && s > c[w + 1]))
                 continue;
             if (out && n < cap) {
-                orc_kpt k = {(float)x, (float)y, 7.f, -1.f, (float)s, 0, -1};
+                orc_kpt k = {(float)x, (float)y, 7.f, -1.f, nonmax ? (float)s : 0.f, 0, -1};
                 out[n] = k;
             }
             n++;
@@ -234,6 +236,12 @@ ORC_API int orc_fast9(const uint8_t *img, int w, int h, int thr, orc_kpt *out, i
     free(S);
     free(C);
     return n;
+}
+
+/* FAST(img, keypoints, thr, true) */
+ORC_API int orc_fast9(const uint8_t *img, int w, int h, int thr, orc_kpt *out, int cap)
+{
+    return orc_fast_detect(img, w, h, thr, 1, out, cap);
 }
 
 /* KeyPointsFilter::runByImageBorder: stable, Rect(b, b, w - 2b, h - 2b).contains(pt), where pt

@@ -145,3 +145,37 @@ def test_gravity_and_patch_size_host(fm3d, orc):
     assert np.array_equal(g, orc.gravity(list(s.rodriguesIC)))  # same operations, bit for bit
     assert fm3d.lib().fm3d_patch_size(ctypes.byref(s)) == 128
     assert fm3d.NeighborhoodsGenerator(s).getReferenceSquaredNeighborhood().shape == (128 * 128, 3)
+
+
+def test_settings_feature_options(fm3d, tmp_path):
+    """FeatureOptions (descriptorsmatcher.cpp:176-359): SIFT's five constructor values, FAST's
+    threshold / suppression, the ADAPTIVE mode and its bounds; OpenCV's defaults where the file names
+    none; detector types with no GPU implementation map to FEAT_OTHER."""
+    def load(text):
+        p = tmp_path / "s.yml"
+        p.write_text("%YAML:1.0\n" + text)
+        return fm3d.Settings.load(str(p))
+
+    s = load("FeatureOptions:\n   DetectorMode: STATIC\n   DetectorType: SIFT\n   ExtractorType: SIFT\n"
+             "   SiftDetector:\n      NumFeatures: 300\n      NumOctaveLayers: 4\n      ContrastThreshold: 0.03\n"
+             "      EdgeThreshold: 12\n      Sigma: 1.5\n")
+    assert (s.detectorType, s.extractorType, s.detectorMode) == (fm3d.FEAT_SIFT, fm3d.FEAT_SIFT, 0)
+    assert (s.siftNumFeatures, s.siftOctaveLayers) == (300, 4)
+    assert (s.siftContrastThreshold, s.siftEdgeThreshold, s.siftSigma) == (0.03, 12.0, 1.5)
+    s = load("FeatureOptions:\n   DetectorType: SIFT\n   ExtractorType: ORB\n")
+    assert (s.siftNumFeatures, s.siftOctaveLayers, s.siftContrastThreshold, s.siftEdgeThreshold, s.siftSigma) == \
+        (0, 3, 0.04, 10.0, 1.6)
+    assert s.extractorType == fm3d.FEAT_ORB
+    s = load("FeatureOptions:\n   DetectorMode: STATIC\n   DetectorType: FAST\n   ExtractorType: SIFT\n"
+             "   FastDetector:\n      Threshold: 33\n      NonMaxSuppression: 0\n")
+    assert (s.detectorType, s.fastThreshold, s.fastNonmax) == (fm3d.FEAT_FAST, 33, 0)
+    s = load("FeatureOptions:\n   DetectorMode: ADAPTIVE\n   DetectorType: SURF\n   ExtractorType: SURF\n"
+             "   Adaptive:\n      MinFeatures: 100\n      MaxFeatures: 200\n      MaxIters: 7\n")
+    assert (s.detectorType, s.detectorMode) == (fm3d.FEAT_SURF, 1)
+    assert (s.adaptiveMinFeatures, s.adaptiveMaxFeatures, s.adaptiveMaxIters) == (100, 200, 7)
+    for mode, det in (("ADAPTIVE", "STAR"), ("ADAPTIVE", "ORB"), ("STATIC", "MSER"), ("STATIC", "STAR"), ("OTHER", "SURF")):
+        s = load(f"FeatureOptions:\n   DetectorMode: {mode}\n   DetectorType: {det}\n")
+        assert s.detectorType == fm3d.FEAT_OTHER, (mode, det)
+    d = fm3d.Settings.default()
+    assert (d.fastThreshold, d.fastNonmax, d.adaptiveMinFeatures, d.adaptiveMaxFeatures, d.adaptiveMaxIters) == \
+        (10, 1, 400, 500, 5)

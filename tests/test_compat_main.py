@@ -216,7 +216,8 @@ def test_dropin_main_matches_python_api(fm3d, synth, orc, tmp_path):
     pair.desc2.tofile(d / "img2.pgm.desc.u8")
     yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.55)
     yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
-    yml += "FeatureOptions:\n   DetectorType: SIFT\n   ExtractorType: SIFT\n"
+    # a detector type with no GPU implementation (FAST): the side files are read
+    yml += "FeatureOptions:\n   DetectorType: FAST\n   ExtractorType: SIFT\n"
     (d / "settings.yml").write_text(yml)
     r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
     assert r.returncode == 0, r.stderr + r.stdout
@@ -281,7 +282,8 @@ def _python_chain(fm3d, s, img1, img2):
         kept, normals = no.computeOptimizedNormals(P)
         frames = no.computeFeaturesFrames(kept, normals)
         patches = sct.projectReferencePointsToImageWithFrames(None, frames)
-        desc = fm3d.SURF(ctx).extractDescriptorsFromPatches(patches) if len(patches) else np.zeros((0, 128), np.float32)
+        ex = fm3d.SIFT(ctx) if s.extractorType == fm3d.FEAT_SIFT else fm3d.SURF(ctx)
+        desc = ex.extractDescriptorsFromPatches(patches) if len(patches) else np.zeros((0, 128), np.float32)
     finally:
         ctx.close()
     return m, kept, normals, patches, desc
@@ -316,6 +318,52 @@ def test_dropin_main_surf_detection(fm3d, synth, orc, tmp_path):
     kp["size"] = 128
     kp["angle"] = -1
     ref = np.stack([orc.surf_describe(p, kp)[2][0] for p in patches[:8]])
+    assert np.array_equal(pd[:8], ref)
+
+
+SIFT_OPTIONS = """FeatureOptions:
+   DetectorType: SIFT
+   DetectorMode: STATIC
+   SiftDetector:
+      NumFeatures: 0
+      NumOctaveLayers: 3
+      ContrastThreshold: 0.04
+      EdgeThreshold: 10
+      Sigma: 1.6
+   ExtractorType: SIFT
+"""
+
+
+@pytest.mark.gpu
+def test_dropin_main_sift_detection(fm3d, synth, orc, tmp_path):
+    """main_dropin -s settings.yml with FeatureOptions SIFT: SIFT detection + description of both
+    images on the GPU (the reference's detect, then compute), and the patch descriptors of
+    main.cpp:182-183 by the SIFT extractor -- equal to the Python mirror; the patch descriptors equal
+    the SIFT oracle's (SIFT::operator() on each patch with its centred keypoint)."""
+    pair = synth.make_frame_pair(1500, seed=26)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.6)
+    yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
+    (d / "settings.yml").write_text(yml + SIFT_OPTIONS)
+    r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
+    assert r.returncode == 0, r.stderr + r.stdout
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    assert s.detectorType == fm3d.FEAT_SIFT and s.extractorType == fm3d.FEAT_SIFT and s.siftOctaveLayers == 3
+    m, kept, normals, patches, desc = _python_chain(fm3d, s, pair.img1, pair.img2)
+    assert np.fromfile(d / "out_matches.bin", dtype=fm3d.DMATCH).tobytes() == m.tobytes()
+    assert np.array_equal(np.fromfile(d / "out_points.f64").reshape(-1, 3), kept)
+    assert np.array_equal(np.fromfile(d / "out_normals.f64").reshape(-1, 3), normals)
+    assert len(m) > 50 and len(kept) > 5
+    pd = np.fromfile(d / "out_patch_desc.f32", dtype=np.float32).reshape(-1, 128)
+    assert np.array_equal(pd, desc)
+    kp = np.zeros(1, dtype=fm3d.KEYPOINT)
+    kp["x"] = kp["y"] = 64
+    kp["size"] = 128
+    kp["angle"] = -1
+    kp["response"] = 1
+    ref = np.stack([orc.sift_compute(p, kp)[2][0] for p in patches[:8]])
     assert np.array_equal(pd[:8], ref)
 
 

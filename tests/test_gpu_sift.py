@@ -154,3 +154,26 @@ def test_sift_compare_with_nndr_images(fm3d, orc, synth):
     assert len(m) == len(qi) > 100
     assert np.array_equal(m["queryIdx"], qi) and np.array_equal(m["trainIdx"], ti)
     assert np.array_equal(m["distance"], dist)
+
+
+def test_sift_patches_bitwise(fm3d, orc):
+    """extractDescriptorsFromPatches with the SIFT extractor (descriptorsmatcher.cpp:133-174): per patch
+    SIFT::operator() with the centred keypoint (size = the edge, angle -1, octave 0), equal to the
+    oracle's compute on each patch; odd patch sizes too"""
+    rng = np.random.default_rng(13)
+    ctx, s = _ctx(fm3d)
+    try:
+        for size, P in ((128, 40), (65, 12)):
+            yy, xx = np.mgrid[0:size, 0:size]
+            patches = np.stack([np.clip(128 + 60 * np.sin(xx * rng.uniform(0.05, 0.3) + yy * rng.uniform(0.05, 0.3))
+                                        + rng.normal(0, 20, (size, size)), 0, 255).astype(np.uint8) for _ in range(P)])
+            d = fm3d.SIFT(ctx).extractDescriptorsFromPatches(patches)
+            kp = np.zeros(1, dtype=fm3d.KEYPOINT)
+            kp["x"] = kp["y"] = size // 2
+            kp["size"] = size
+            kp["angle"] = -1
+            kp["response"] = 1
+            ref = np.stack([orc.sift_compute(p, kp)[2][0] for p in patches])
+            assert d.shape == (P, 128) and np.array_equal(d, ref), size
+    finally:
+        ctx.close()

@@ -1,6 +1,6 @@
 """Drive the kernels outside the C4 bench for rocprofv3 --kernel-trace --stats:
 SURF detect + describe on the VGA frames (Upright 1 = the reference's settings, and Upright 0),
-extractDescriptorsFromPatches, ORB detect + describe and compute (2,000 / 10,000 features), the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
+extractDescriptorsFromPatches, ORB detect + describe and compute (2,000 / 10,000 features), SIFT detect + describe and compute, the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
 of the 10k-ORB pair) and the circular neighbourhoods of the C4 inliers.  Product path only (no
 oracle); each leg timed with host wall clock after a warm-up call, printed as one JSON line.
 
@@ -57,6 +57,21 @@ def main():
             res[f"orb_compute_vga_{nf}"] = {"keypoints": int(len(kc)), "ms": round(ms, 3)}
         finally:
             ctx.close()
+    # SIFT (DetectorType / ExtractorType SIFT, OpenCV's defaults) on the VGA frame: detect + describe,
+    # and compute on the detected keypoints (the reference's second call)
+    s = fm3d.Settings.default()
+    s.detectorType = s.extractorType = fm3d.FEAT_SIFT
+    ctx = fm3d.Context(s)
+    try:
+        sift = fm3d.SIFT(ctx)
+        (k, d), ms = timed(lambda: sift.detect(pair.img1, with_descriptors=True), 5)
+        res["sift_detect_describe_vga"] = {"keypoints": int(len(k)), "ms": round(ms, 3)}
+        _, ms = timed(lambda: sift.detect(pair.img1), 5)
+        res["sift_detect_vga"] = {"keypoints": int(len(k)), "ms": round(ms, 3)}
+        (kc, _, _), ms = timed(lambda: sift.compute(pair.img1, k), 5)
+        res["sift_compute_vga"] = {"keypoints": int(len(kc)), "ms": round(ms, 3)}
+    finally:
+        ctx.close()
     # C3 NCC leg: the 10k-ORB pair's DLT inliers, 16 hypotheses, pixelsRay 32
     fp = synth.make_frame_pair(10_000, seed=102, desc="orb")
     s = fm3d.Settings.default()
