@@ -84,6 +84,7 @@ struct fm3d_ctx {
     DevBuf siftImg, siftBase, siftG, siftD, siftGL, siftDL, siftTaps, siftScan, siftFlag, siftPos, siftCand, siftAng,
         siftNpk, siftKp, siftDesc;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
+    DevBuf f32Work;           // the bf16 MFMA prefilter's scratch (rows, norms, bounds, candidates)
     int nCU = 0;
     DevBuf kp1, kp2, triPts, triMask, triMask8, pts, srcIdx;
     long lmGroups = 0;
@@ -350,6 +351,12 @@ bool bits_mfma() {
     return !(e && e[0] == '0');
 }
 
+// FM3D_F32_MFMA=0 keeps float rows on the exact VALU scan (A/B comparisons)
+bool f32_mfma() {
+    const char* e = getenv("FM3D_F32_MFMA");
+    return !(e && e[0] == '0');
+}
+
 // knn2 + NNDR flags on staged descriptors (device), results in c->idx/key/fkey/cand/flag
 int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int queryOffset, bool wantKnn) {
     HIPCHK(c, c->idx.ensure((size_t)nA * 2 * sizeof(int) + 16));
@@ -377,6 +384,35 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         fm3d::launch_knn2_i8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, 0, c->cqA.as<int>(),
                              c->ctB.as<int>(), parts, c->partIdx.as<int>(), c->partKey.as<int>(), c->idx.as<int>(),
                              c->key.as<int>(), c->stream);
+    } else if (type == FM3D_DESC_F32 && (dimPad == 64 || dimPad == 128) && nB >= 64 &&
+               (long long)nA * nB >= (1LL << 22) && f32_mfma()) {
+        // float rows (SURF): the bf16 MFMA prefilter lists each query's possible top-2 rows, whose exact
+        // FLANN-order distances decide (fm3d_match.hip); the same result as the full exact scan
+        const int parts = fm3d::knn2_f32_mfma_parts(nA, nB, c->nCU);
+        HIPCHK(c, c->f32Work.ensure(fm3d::knn2_f32_mfma_bytes(nA, nB, dimPad, parts)));
+        fm3d::launch_knn2_f32_mfma(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, parts, c->f32Work.p,
+                                   c->idx.as<int>(), c->fkey.as<float>(), c->stream);
+        int nResc = 0;
+        HIPCHK(c, hipMemcpyAsync(&nResc, fm3d::knn2_f32_mfma_rescan_count(c->f32Work.p, nA, nB, dimPad, parts),
+                                 sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (nResc > 0 && nResc <= nA / 8) {
+            // the queries whose bound held more rows than the candidate list: an exact wave-per-query scan
+            fm3d::launch_knn2_f32_mfma_rescan(c->A.as<float>(), c->B.as<float>(), nB, dimPad, c->f32Work.p, nA, parts,
+                                              nResc, c->idx.as<int>(), c->fkey.as<float>(), c->stream);
+        } else if (nResc > 0) {
+            // descriptors with no margin between neighbours (e.g. uniform noise in high dimension):
+            // the full exact scan for every query
+            const int p2 = fm3d::knn2_parts(nA, nB, dimPad, c->nCU);
+            if (p2 > 1) {
+                HIPCHK(c, c->partIdx.ensure((size_t)p2 * nA * 2 * sizeof(int) + 16));
+                HIPCHK(c, c->partKey.ensure((size_t)p2 * nA * 2 * sizeof(float) + 16));
+            }
+            HIPCHK(c, c->bPairs.ensure(fm3d::knn2_f32_pairs_bytes(nB, dimPad) + 16));
+            fm3d::launch_knn2_f32(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, p2, c->partIdx.as<int>(),
+                                  c->partKey.as<float>(), c->bPairs.as<float>(), c->idx.as<int>(), c->fkey.as<float>(),
+                                  c->stream);
+        }
     } else if (type == FM3D_DESC_F32) {
         const int parts = (dimPad == 64 || dimPad == 128) ? fm3d::knn2_parts(nA, nB, dimPad, c->nCU) : 1;
         if (parts > 1) {
@@ -1297,7 +1333,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
                       &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat,
                       &c->slab, &c->slabI1,
-                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->A8, &c->B8,
+                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->f32Work, &c->A8, &c->B8,
                       &c->sfImg, &c->sfSum, &c->sfDet, &c->sfTr, &c->sfLayers, &c->sfMids, &c->sfCand, &c->sfCount,
                       &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW, &c->sfAng,
                       &c->orbPyr, &c->orbTab, &c->orbLev, &c->orbMap, &c->orbFlag, &c->orbPos, &c->orbKp, &c->orbR,

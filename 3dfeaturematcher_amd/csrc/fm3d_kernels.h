@@ -102,6 +102,16 @@ int knn2_parts(int nA, int nB, int dim, int nCU);
 size_t knn2_f32_pairs_bytes(int nB, int dim);  // the row-pair copy of B (dim 64 / 128)
 void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, int parts, int* partIdx,
                      float* partKey, float* pairs, int* idx, float* key, hipStream_t s);
+// f32 rows (dim 64 / 128) through the bf16 MFMA prefilter (fm3d_match.hip): the same top-2 and keys
+// as launch_knn2_f32; work: knn2_f32_mfma_bytes(nA, nB, dim, parts) bytes of device scratch
+size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts);
+int knn2_f32_mfma_parts(int nA, int nB, int nCU);
+void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, void* work, int* idx,
+                          float* key, hipStream_t s);
+// the number of queries the prefilter could not settle (device int in work), and their exact rescan
+int* knn2_f32_mfma_rescan_count(void* work, int nA, int nB, int dim, int parts);
+void launch_knn2_f32_mfma_rescan(const float* A, const float* B, int nB, int dim, void* work, int nA, int parts,
+                                 int nResc, int* idx, float* key, hipStream_t s);
 // binary rows: `parts` train ranges (knn2_parts), merged through partIdx/partKey
 void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimBytes, int parts, int* partIdx,
                       int* partKey, int* idx, int* key, hipStream_t s);

@@ -564,6 +564,303 @@ __global__ void nndr_kernel(int type, const int* __restrict__ idx, const int* __
     cand[q] = fm3d_dmatch{q + queryOffset, i1, 0, d1};
 }
 
+// ---------------- float rows: a bf16 MFMA prefilter, then the exact FLANN-order distances ----------------
+// s'_j = |b_j|^2 - 2 a_hi . b_hi,j (a_hi, b_hi = the rows rounded to bf16; the dot products on
+// v_mfma_f32_32x32x16_bf16, |b_j|^2 in fp32) ranks train row j for query a up to
+//   |s'_j - s_j| <= eps_q = 0.0079 |a| Bmax + 1e-5 Bmax^2        (s_j = |a - b_j|^2 - |a|^2)
+// (bf16 rounding 2^-9 per element, an exact bf16 product and <= 127 fp32 roundings per dot, the
+// fp32 norm), and FLANN's float L2 is within phi_q = 2e-5 (|a| + Bmax)^2 of the true distance
+// (dim <= 128).  So every member of the exact top-2 has s'_j <= s'_(2) + 2 eps_q + 2 phi_q: pass 1
+// finds s'_(2), pass 2 lists the rows under that bound, pass 3 computes their exact FLANN-order
+// distances and keeps the (distance, index) top-2 -- the same two rows and keys the full exact scan
+// returns.  A query with more than kCandMax such rows, or a non-finite norm, is rescanned exactly.
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+constexpr int kCandMax = 32;
+
+__device__ inline uint32_t bf16_rne(float x) {
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// rows (dim 64 / 128) -> bf16 rows, 8 elements (16 bytes) per thread; |row|^2 in fp32; the largest
+// train |b|^2 into *bmax (as ordered bits: non-negative floats compare as ints)
+__global__ void f32_bf16_rows_kernel(const float* __restrict__ A, int nA, const float* __restrict__ B, int nB, int dim,
+                                     uint16_t* __restrict__ outA, uint16_t* __restrict__ outB, float* __restrict__ nA2,
+                                     float* __restrict__ nB2, unsigned* __restrict__ bmax) {
+    const int cpr = dim / 8;  // 8 or 16 lanes per row
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long r = t / cpr;
+    const int k = (int)(t - r * cpr);
+    const bool isA = r < nA;
+    const long long rr = isA ? r : r - nA;
+    float s = 0.f;
+    if (r < (long long)nA + nB) {
+        const float4* x = (const float4*)((isA ? A : B) + rr * dim + 8 * k);
+        const float4 u = x[0], v = x[1];
+        const float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        v4i o;
+#pragma unroll
+        for (int w = 0; w < 4; w++) o[w] = (int)(bf16_rne(e[2 * w]) | (bf16_rne(e[2 * w + 1]) << 16));
+        *(v4i*)((isA ? outA : outB) + rr * dim + 8 * k) = o;
+#pragma unroll
+        for (int w = 0; w < 8; w++) s += e[w] * e[w];
+    }
+    for (int o = 1; o < cpr; o <<= 1) s += __shfl_xor(s, o);
+    if (k == 0 && r < (long long)nA + nB) {
+        if (isA) {
+            nA2[rr] = s;
+        } else {
+            nB2[rr] = s;
+            atomicMax(bmax, (s == s && s <= 3.4e38f) ? __float_as_uint(s) : 0x7f800000u);  // non-finite: +inf
+        }
+    }
+}
+
+// MODE 0: per (part, query) the two smallest s'; MODE 1: the rows with s' <= thr[q] appended to the
+// query's candidate list.  The tiling is knn2_i8_kernel's (128 queries x 128-row LDS tiles, the
+// query row as the MFMA's B operand; a bf16 k-step is the same 32 bytes as an int8 one).
+template <int KS, int MODE>
+__global__ __launch_bounds__(kThreads) void knn2_bf16_kernel(const uint16_t* __restrict__ A, int nA,
+                                                             const uint16_t* __restrict__ B, int nB,
+                                                             const float* __restrict__ nb2, int tilesPerPart,
+                                                             const float* __restrict__ thr, float* __restrict__ keyOut,
+                                                             int* __restrict__ cnt, int* __restrict__ cand) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int rowBytes = 32 * KS, tileBytes = kT * rowBytes, chunksPerRow = rowBytes / 16;
+    unsigned char* tiles = smem;                           // 2 x tileBytes
+    float* ctl = (float*)(smem + 2 * (size_t)tileBytes);    // 2 x kT |b|^2
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qrow = blockIdx.x * kQ + wave * 32 + (lane & 31);
+    const int half = lane >> 5;
+    v4i bq[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; kk++) {
+        v4i v = {0, 0, 0, 0};
+        if (qrow < nA) v = *(const v4i*)((const unsigned char*)A + (size_t)qrow * rowBytes + 32 * kk + 16 * half);
+        bq[kk] = v;
+    }
+    const float inf = __builtin_inff();
+    const float tq = (MODE == 1 && qrow < nA) ? thr[qrow] : -inf;
+    float p1 = inf, p2 = inf;
+    const int tBeg = blockIdx.y * tilesPerPart;
+    const int tEnd = min((nB + kT - 1) / kT, tBeg + tilesPerPart);
+    constexpr int kPre = (kT * chunksPerRow + kThreads - 1) / kThreads;
+    constexpr int total = kT * chunksPerRow;
+    v4i pre[kPre];
+    float preCt = inf;
+    auto load_tile = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < kPre; i++) {
+            const int c = tid + i * kThreads;
+            v4i v = {0, 0, 0, 0};
+            if (c < total) {
+                const int row = c / chunksPerRow, ch = c - row * chunksPerRow;
+                const int j = t * kT + row;
+                if (j < nB) v = *(const v4i*)((const unsigned char*)B + (size_t)j * rowBytes + 16 * ch);
+            }
+            pre[i] = v;
+        }
+        if (tid < kT) {
+            const int j = t * kT + tid;
+            preCt = (j < nB) ? nb2[j] : inf;  // rows past nB: +inf never ranks
+        }
+    };
+    auto store_tile = [&](int buf) {
+        unsigned char* dst = tiles + (size_t)buf * tileBytes;
+#pragma unroll
+        for (int i = 0; i < kPre; i++) {
+            const int c = tid + i * kThreads;
+            if (c < total) {
+                const int row = c / chunksPerRow, ch = c - row * chunksPerRow;
+                *(v4i*)(dst + (size_t)row * rowBytes + 16 * swz_chunk(row, ch)) = pre[i];
+            }
+        }
+        if (tid < kT) ctl[buf * kT + tid] = preCt;
+    };
+    if (tBeg < tEnd) {
+        load_tile(tBeg);
+        store_tile(0);
+    }
+    __syncthreads();
+    for (int t = tBeg; t < tEnd; t++) {
+        const int buf = (t - tBeg) & 1;
+        if (t + 1 < tEnd) load_tile(t + 1);
+        const unsigned char* tl = tiles + (size_t)buf * tileBytes;
+        const float* ct = ctl + buf * kT;
+        auto mma = [&](int rb) {
+            v16f acc = {0};
+            const int arow = rb * 32 + (lane & 31);
+#pragma unroll
+            for (int kk = 0; kk < KS; kk++) {
+                const v4i a = *(const v4i*)(tl + (size_t)arow * rowBytes + 16 * swz_chunk(arow, 2 * kk + half));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, a), __builtin_bit_cast(v8bf, bq[kk]),
+                                                              acc, 0, 0, 0);
+            }
+            return acc;
+        };
+        v16f accCur = mma(0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int rb = 0; rb < kT / 32; rb++) {
+            v16f accNext;
+            if (rb + 1 < kT / 32) accNext = mma(rb + 1);
+            unsigned hits = 0;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const float v = fmaf(-2.f, accCur[r], ct[row]);
+                if (MODE == 0) {
+                    p2 = __builtin_amdgcn_fmed3f(p1, p2, v);
+                    p1 = fminf(p1, v);
+                } else {
+                    hits |= (v <= tq ? 1u : 0u) << r;
+                }
+            }
+            if (MODE == 1 && hits) {
+                do {
+                    const int r = __builtin_ctz(hits);
+                    hits &= hits - 1;
+                    const int j = t * kT + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    const int slot = atomicAdd(&cnt[qrow], 1);
+                    if (slot < kCandMax) cand[(size_t)qrow * kCandMax + slot] = j;
+                } while (hits);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (rb + 1 < kT / 32) accCur = accNext;
+        }
+        if (t + 1 < tEnd) store_tile(buf ^ 1);
+        __syncthreads();
+    }
+    if (MODE == 0) {
+        // lanes l and l + 32 hold the same query (the other 16 rows of every block)
+        const float q1 = __shfl_xor(p1, 32), q2 = __shfl_xor(p2, 32);
+        const float n1 = fminf(p1, q1), n2 = fminf(fmaxf(p1, q1), fminf(p2, q2));
+        if (half == 0 && qrow < nA) {
+            const size_t o = ((size_t)blockIdx.y * nA + qrow) * 2;
+            keyOut[o] = n1;
+            keyOut[o + 1] = n2;
+        }
+    }
+}
+
+// the bound thr[q] = s'_(2) over all parts + 2 eps_q + 2 phi_q (+ slack), rounded up; cnt[q] = 0.
+// A non-finite norm or bound sends the query to the exact rescan (thr = -inf, cnt = kCandMax + 1).
+__global__ void knn2_bf16_bound_kernel(const float* __restrict__ partKey, int nA, int parts,
+                                       const float* __restrict__ nA2, const unsigned* __restrict__ bmax,
+                                       float* __restrict__ thr, int* __restrict__ cnt) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    float p1 = __builtin_inff(), p2 = __builtin_inff();
+    for (int s = 0; s < parts; s++) {
+        const size_t o = ((size_t)s * nA + q) * 2;
+        const float c1 = partKey[o], c2 = partKey[o + 1];
+        p2 = fminf(fmaxf(p1, c1), fminf(p2, c2));
+        p1 = fminf(p1, c1);
+    }
+    const double a = sqrt((double)nA2[q]), bm = sqrt((double)__uint_as_float(*bmax));
+    const double eps = 0.0079 * a * bm + 1e-5 * bm * bm, phi = 2e-5 * (a + bm) * (a + bm);
+    const double t = (double)p2 + 2 * eps + 2 * phi + 1e-6 * (a + bm) * (a + bm);
+    const bool ok = t == t && t < 1e37 && a < 1e18;
+    float t32 = (float)t;
+    if ((double)t32 < t) t32 = nextafterf(t32, __builtin_inff());  // rounded up
+    thr[q] = ok ? t32 : -__builtin_inff();
+    cnt[q] = ok ? 0 : kCandMax + 1;
+}
+
+// FLANN L2<float> (flann/dist.h): groups of four, result += d0^2 + d1^2 + d2^2 + d3^2, then the tail
+__device__ inline float flann_l2(const float* __restrict__ a, const float* __restrict__ b, int dim) {
+    float result = 0.f;
+    int i = 0;
+    for (; i + 3 < dim; i += 4) {
+        const float d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1], d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+        result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    for (; i < dim; i++) {
+        const float d0 = a[i] - b[i];
+        result += d0 * d0;
+    }
+    return result;
+}
+
+__device__ inline bool lex_lt_f(float a, int ia, float b, int ib) { return a < b || (a == b && ia < ib); }
+
+// the candidates' exact distances, (distance, index) top-2; overflowing queries into the rescan list
+__global__ void knn2_f32_recheck_kernel(const float* __restrict__ A, int nA, const float* __restrict__ B, int dim,
+                                        const int* __restrict__ cnt, const int* __restrict__ cand,
+                                        int* __restrict__ idxOut, float* __restrict__ keyOut,
+                                        int* __restrict__ resc, int* __restrict__ nResc) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    const int n = cnt[q];
+    if (n > kCandMax) {
+        resc[atomicAdd(nResc, 1)] = q;
+        return;
+    }
+    const float* a = A + (size_t)q * dim;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = -1, i2 = -1;
+    for (int c = 0; c < n; c++) {
+        const int j = cand[(size_t)q * kCandMax + c];
+        const float d = flann_l2(a, B + (size_t)j * dim, dim);
+        if (!(d < __builtin_inff())) continue;  // NaN / +inf never enter (the scan's rule)
+        if (lex_lt_f(d, j, b1, i1 < 0 ? INT_MAX : i1)) {
+            b2 = b1;
+            i2 = i1;
+            b1 = d;
+            i1 = j;
+        } else if (lex_lt_f(d, j, b2, i2 < 0 ? INT_MAX : i2)) {
+            b2 = d;
+            i2 = j;
+        }
+    }
+    idxOut[2 * q] = i1;
+    idxOut[2 * q + 1] = i2;
+    keyOut[2 * q] = b1;
+    keyOut[2 * q + 1] = b2;
+}
+
+// the exact scan for the listed queries: a wave per query, lane l takes rows l, l + 64, ... (in
+// increasing order, the scan's rule per lane), then the lanes' lists merge lexicographically
+__global__ __launch_bounds__(256) void knn2_f32_rescan_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                              int nB, int dim, const int* __restrict__ resc,
+                                                              const int* __restrict__ nResc, int* __restrict__ idxOut,
+                                                              float* __restrict__ keyOut) {
+    const int lane = threadIdx.x & 63;
+    const int n = *nResc;
+    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < n; w += gridDim.x * 4) {
+        const int q = resc[w];
+        const float* a = A + (size_t)q * dim;
+        float b1 = __builtin_inff(), b2 = __builtin_inff();
+        int i1 = -1, i2 = -1;
+        for (int j = lane; j < nB; j += 64) top2_insert_f(flann_l2(a, B + (size_t)j * dim, dim), j, b1, i1, b2, i2);
+        for (int o = 1; o < 64; o <<= 1) {
+            const float c1 = __shfl_xor(b1, o), c2 = __shfl_xor(b2, o);
+            const int j1 = __shfl_xor(i1, o), j2 = __shfl_xor(i2, o);
+            // merge (b1, i1, b2, i2) with (c1, j1, c2, j2) lexicographically (-1 = none, sorts last)
+            const int k1 = i1 < 0 ? INT_MAX : i1, k2 = i2 < 0 ? INT_MAX : i2;
+            const int l1 = j1 < 0 ? INT_MAX : j1, l2 = j2 < 0 ? INT_MAX : j2;
+            float r1, r2;
+            int s1, s2;
+            if (lex_lt_f(b1, k1, c1, l1)) {
+                r1 = b1, s1 = k1;
+                if (lex_lt_f(b2, k2, c1, l1)) r2 = b2, s2 = k2; else r2 = c1, s2 = l1;
+            } else {
+                r1 = c1, s1 = l1;
+                if (lex_lt_f(b1, k1, c2, l2)) r2 = b1, s2 = k1; else r2 = c2, s2 = l2;
+            }
+            b1 = r1, i1 = s1 == INT_MAX ? -1 : s1;
+            b2 = r2, i2 = s2 == INT_MAX ? -1 : s2;
+        }
+        if (lane == 0) {
+            idxOut[2 * q] = i1;
+            idxOut[2 * q + 1] = i2;
+            keyOut[2 * q] = b1;
+            keyOut[2 * q + 1] = b2;
+        }
+    }
+}
+
 }  // namespace
 
 void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int* cq, int* ctp,
@@ -603,6 +900,85 @@ void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
     else
         go(knn2_i8_kernel<0, false>);
     if (parts > 1) knn2_int_merge<<<(nA + 255) / 256, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
+}
+
+size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts) {
+    // bf16 rows, norms, bound, candidate lists, part keys, rescan list (+ alignment slack)
+    return (size_t)(nA + nB) * dim * 2 + (size_t)(nA + nB) * 4 + 64 + (size_t)nA * 4 * 3 + (size_t)nA * kCandMax * 4 +
+           (size_t)parts * nA * 2 * 4 + (size_t)nA * 4 + 16 * 256;
+}
+
+int knn2_f32_mfma_parts(int nA, int nB, int nCU) { return knn2_u8_parts(nA, nB, nCU); }
+
+void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, void* work, int* idx,
+                          float* key, hipStream_t s) {
+    if (nA <= 0) return;
+    char* w = (char*)work;
+    auto take = [&](size_t bytes) {
+        char* p = w;
+        w += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    uint16_t* a16 = (uint16_t*)take((size_t)nA * dim * 2);
+    uint16_t* b16 = (uint16_t*)take((size_t)nB * dim * 2);
+    float* nA2 = (float*)take((size_t)nA * 4);
+    float* nB2 = (float*)take((size_t)nB * 4);
+    unsigned* bmax = (unsigned*)take(64);
+    float* thr = (float*)take((size_t)nA * 4);
+    int* cnt = (int*)take((size_t)nA * 4);
+    int* cand = (int*)take((size_t)nA * kCandMax * 4);
+    float* partKey = (float*)take((size_t)parts * nA * 2 * 4);
+    int* resc = (int*)take((size_t)nA * 4);
+    int* nResc = (int*)take(64);
+    (void)hipMemsetAsync(bmax, 0, 4, s);
+    (void)hipMemsetAsync(nResc, 0, 4, s);
+    const long long thr8 = (long long)(nA + nB) * (dim / 8);
+    f32_bf16_rows_kernel<<<(unsigned)((thr8 + 255) / 256), 256, 0, s>>>(A, nA, B, nB, dim, a16, b16, nA2, nB2, bmax);
+    const int KS = dim / 16;
+    const size_t lds = 2 * (size_t)kT * 32 * KS + 2 * kT * sizeof(float);
+    const int nTiles = (nB + kT - 1) / kT;
+    const int tilesPerPart = parts > 1 ? (nTiles + parts - 1) / parts : (nTiles > 0 ? nTiles : 1);
+    const dim3 g((nA + kQ - 1) / kQ, parts);
+    auto go = [&](auto k0, auto k1) {
+        if (lds > 65536) {
+            (void)hipFuncSetAttribute((const void*)k0, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            (void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        }
+        k0<<<g, kThreads, lds, s>>>(a16, nA, b16, nB, nB2, tilesPerPart, nullptr, partKey, nullptr, nullptr);
+        knn2_bf16_bound_kernel<<<(nA + 255) / 256, 256, 0, s>>>(partKey, nA, parts, nA2, bmax, thr, cnt);
+        k1<<<g, kThreads, lds, s>>>(a16, nA, b16, nB, nB2, tilesPerPart, thr, nullptr, cnt, cand);
+    };
+    if (KS == 8)
+        go(knn2_bf16_kernel<8, 0>, knn2_bf16_kernel<8, 1>);
+    else
+        go(knn2_bf16_kernel<4, 0>, knn2_bf16_kernel<4, 1>);
+    knn2_f32_recheck_kernel<<<(nA + 255) / 256, 256, 0, s>>>(A, nA, B, dim, cnt, cand, idx, key, resc, nResc);
+}
+
+int* knn2_f32_mfma_rescan_count(void* work, int nA, int nB, int dim, int parts) {
+    // the last slot of launch_knn2_f32_mfma's layout
+    size_t o = 0;
+    auto take = [&](size_t bytes) { o += (bytes + 255) & ~(size_t)255; };
+    take((size_t)nA * dim * 2);
+    take((size_t)nB * dim * 2);
+    take((size_t)nA * 4);
+    take((size_t)nB * 4);
+    take(64);
+    take((size_t)nA * 4);
+    take((size_t)nA * 4);
+    take((size_t)nA * kCandMax * 4);
+    take((size_t)parts * nA * 2 * 4);
+    take((size_t)nA * 4);
+    return (int*)((char*)work + o);
+}
+
+void launch_knn2_f32_mfma_rescan(const float* A, const float* B, int nB, int dim, void* work, int nA, int parts,
+                                 int nResc, int* idx, float* key, hipStream_t s) {
+    if (nResc <= 0) return;
+    int* nR = knn2_f32_mfma_rescan_count(work, nA, nB, dim, parts);
+    const int* resc = nR - ((((size_t)nA * 4) + 255) & ~(size_t)255) / sizeof(int);
+    const int grid = (nResc + 3) / 4 < 1024 ? (nResc + 3) / 4 : 1024;
+    knn2_f32_rescan_kernel<<<grid, 256, 0, s>>>(A, B, nB, dim, resc, nR, idx, key);
 }
 
 int knn2_u8_parts(int nA, int nB, int nCU) {
