@@ -761,7 +761,8 @@ __global__ void knn2_bf16_bound_kernel(const float* __restrict__ partKey, int nA
     const double a = sqrt((double)nA2[q]), bm = sqrt((double)__uint_as_float(*bmax));
     const double eps = 0.0079 * a * bm + 1e-5 * bm * bm, phi = 2e-5 * (a + bm) * (a + bm);
     const double t = (double)p2 + 2 * eps + 2 * phi + 1e-6 * (a + bm) * (a + bm);
-    const bool ok = t == t && t < 1e37 && a < 1e18;
+    // (rows of norm below 1e-10 are rescanned: the bound does not cover the MFMA's denormal handling)
+    const bool ok = t == t && t < 1e37 && a < 1e18 && a + bm > 1e-10;
     float t32 = (float)t;
     if ((double)t32 < t) t32 = nextafterf(t32, __builtin_inff());  // rounded up
     thr[q] = ok ? t32 : -__builtin_inff();
