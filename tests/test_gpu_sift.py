@@ -7,6 +7,8 @@ descriptorsmatcher.cpp:243-257, 302-315)."""
 import numpy as np
 import pytest
 
+from conftest import oracle_threads
+
 pytestmark = pytest.mark.gpu
 
 
@@ -177,3 +179,55 @@ def test_sift_patches_bitwise(fm3d, orc):
             assert d.shape == (P, 128) and np.array_equal(d, ref), size
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("nfeat", [3_500])
+def test_c2_sift_from_images_full_pipeline(fm3d, orc, synth, nfeat):
+    """BASELINE configs[1] (C2: SIFT-128 per 640x480 frame, match + DLT) starting from the images, as
+    the reference does with DetectorType / ExtractorType SIFT: SIFT detection and description on the
+    GPU (ContrastThreshold 0.02; the synthetic frame pair holds 7.8k / 3.9k such keypoints, so
+    retainBest(NumFeatures 3,500) trims both -- C2's 10k rows per frame are matched from the
+    generated descriptors in test_c2_sift10k_match_and_dlt), then the
+    device-resident pipeline (match + NNDR on the integer-valued float rows, DLT, LM).  Keypoints,
+    descriptors, matches, inliers and points are checked in full against the oracle chain; the LM on
+    a seeded 96-point sample bit-exact against the oracle's DETMATH mode."""
+    fp = synth.make_frame_pair(10_000, seed=101)
+    s = fm3d.Settings.default()
+    s.set_camera(fp.cam)
+    s.detectorType = s.extractorType = fm3d.FEAT_SIFT
+    s.siftNumFeatures, s.siftContrastThreshold = nfeat, 0.02
+    ctx = fm3d.Context(s)
+    try:
+        sift = fm3d.SIFT(ctx)
+        ka, _, da = sift.compute(fp.img1, sift.detect(fp.img1))
+        kb, _, db = sift.compute(fp.img2, sift.detect(fp.img2))
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(fp.g12)
+        R2, t2 = sct.camera2()
+        xy = lambda k: np.stack([k["x"], k["y"]], axis=1).astype(np.float32)
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(da, db, xy(ka), xy(kb), fp.img1, fp.img2)
+        n, stats = pipe.run()
+        rec = pipe.records(n)
+    finally:
+        ctx.close()
+    kw = dict(nfeatures=nfeat, contrastThreshold=0.02)
+    oa, ob = orc.sift_detect(fp.img1, **kw), orc.sift_detect(fp.img2, **kw)
+    _same_kpts(ka, oa)
+    _same_kpts(kb, ob)
+    assert nfeat <= len(oa) < nfeat * 1.01 and nfeat <= len(ob) < nfeat * 1.01
+    oda, odb = orc.sift_compute(fp.img1, oa)[2], orc.sift_compute(fp.img2, ob)[2]
+    assert np.array_equal(da, oda) and np.array_equal(db, odb)
+    q, t, d = orc.match_nndr(oda.astype(np.uint8), odb.astype(np.uint8), orc.U8, s.nndrEpsilon)
+    assert stats["matches"] == len(q) > 500
+    pts, mask = orc.triangulate(fp.cam, fp.g12, 1.5, 2.4, xy(oa), xy(ob), q, t)
+    assert stats["inliers"] == len(pts)
+    pos = np.searchsorted(q[mask], rec["queryIdx"])
+    assert np.array_equal(q[mask][pos], rec["queryIdx"]) and np.array_equal(rec["trainIdx"], t[mask][pos])
+    assert np.array_equal(rec["distance"], d[mask][pos]) and np.array_equal(rec["point"], pts[pos])
+    sel = np.sort(np.random.default_rng(1101).choice(len(pts), min(96, len(pts)), replace=False))
+    ref = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, s.pyramids, pts[sel], s.pixelsRay, mode=orc.DETMATH,
+                               nthreads=oracle_threads())
+    ok = ref["status"] == 0
+    assert np.array_equal(np.isin(sel, pos), ok)
+    assert np.array_equal(rec[np.isin(pos, sel)]["normal"], ref["normals"][ok])
