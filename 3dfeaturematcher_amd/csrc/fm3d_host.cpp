@@ -390,12 +390,20 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         // FLANN-order distances decide (fm3d_match.hip); the same result as the full exact scan
         const int parts = fm3d::knn2_f32_mfma_parts(nA, nB, c->nCU);
         HIPCHK(c, c->f32Work.ensure(fm3d::knn2_f32_mfma_bytes(nA, nB, dimPad, parts)));
-        fm3d::launch_knn2_f32_mfma(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, parts, c->f32Work.p,
-                                   c->idx.as<int>(), c->fkey.as<float>(), c->stream);
+        // one fused pass; when more than 1/8 of the queries overflow its lists, the two-pass form (whose
+        // lists hold only the rows under the final bound); FM3D_F32_FUSED=0 starts with the two-pass form
+        const char* fe = getenv("FM3D_F32_FUSED");
+        bool fused = !(fe && fe[0] == '0');
         int nResc = 0;
-        HIPCHK(c, hipMemcpyAsync(&nResc, fm3d::knn2_f32_mfma_rescan_count(c->f32Work.p, nA, nB, dimPad, parts),
-                                 sizeof(int), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (;;) {
+            fm3d::launch_knn2_f32_mfma(c->A.as<float>(), nA, c->B.as<float>(), nB, dimPad, parts, fused, c->f32Work.p,
+                                       c->idx.as<int>(), c->fkey.as<float>(), c->stream);
+            HIPCHK(c, hipMemcpyAsync(&nResc, fm3d::knn2_f32_mfma_rescan_count(c->f32Work.p, nA, nB, dimPad, parts),
+                                     sizeof(int), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (!fused || nResc <= nA / 8) break;
+            fused = false;
+        }
         if (nResc > 0 && nResc <= nA / 8) {
             // the queries whose bound held more rows than the candidate list: an exact wave-per-query scan
             fm3d::launch_knn2_f32_mfma_rescan(c->A.as<float>(), c->B.as<float>(), nB, dimPad, c->f32Work.p, nA, parts,

@@ -106,8 +106,10 @@ void launch_knn2_f32(const float* A, int nA, const float* B, int nB, int dim, in
 // as launch_knn2_f32; work: knn2_f32_mfma_bytes(nA, nB, dim, parts) bytes of device scratch
 size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts);
 int knn2_f32_mfma_parts(int nA, int nB, int nCU);
-void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, void* work, int* idx,
-                          float* key, hipStream_t s);
+// fused: one MFMA pass listing the rows under each lane's running bound (default); else two passes
+// (the bound first, then the lists: fewer candidates per query)
+void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, bool fused, void* work,
+                          int* idx, float* key, hipStream_t s);
 // the number of queries the prefilter could not settle (device int in work), and their exact rescan
 int* knn2_f32_mfma_rescan_count(void* work, int nA, int nB, int dim, int parts);
 void launch_knn2_f32_mfma_rescan(const float* A, const float* B, int nB, int dim, void* work, int nA, int parts,

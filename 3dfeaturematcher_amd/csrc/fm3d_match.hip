@@ -577,6 +577,7 @@ __global__ void nndr_kernel(int type, const int* __restrict__ idx, const int* __
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int kCandMax = 32;
+constexpr int kCandMax2 = 128;  // the fused pass: a lane's running records (~2 ln N) come on top
 
 __device__ inline uint32_t bf16_rne(float x) {
     const uint32_t u = __float_as_uint(x);
@@ -625,7 +626,8 @@ __global__ __launch_bounds__(kThreads) void knn2_bf16_kernel(const uint16_t* __r
                                                              const uint16_t* __restrict__ B, int nB,
                                                              const float* __restrict__ nb2, int tilesPerPart,
                                                              const float* __restrict__ thr, float* __restrict__ keyOut,
-                                                             int* __restrict__ cnt, int* __restrict__ cand) {
+                                                             int* __restrict__ cnt, int* __restrict__ cand,
+                                                             float* __restrict__ candKey) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int rowBytes = 32 * KS, tileBytes = kT * rowBytes, chunksPerRow = rowBytes / 16;
     unsigned char* tiles = smem;                           // 2 x tileBytes
@@ -641,7 +643,8 @@ __global__ __launch_bounds__(kThreads) void knn2_bf16_kernel(const uint16_t* __r
         bq[kk] = v;
     }
     const float inf = __builtin_inff();
-    const float tq = (MODE == 1 && qrow < nA) ? thr[qrow] : -inf;
+    // MODE 1: the bound; MODE 2: the margin added to the running second-best
+    const float tq = (MODE != 0 && qrow < nA) ? thr[qrow] : -inf;
     float p1 = inf, p2 = inf;
     const int tBeg = blockIdx.y * tilesPerPart;
     const int tEnd = min((nB + kT - 1) / kT, tBeg + tilesPerPart);
@@ -710,20 +713,25 @@ __global__ __launch_bounds__(kThreads) void knn2_bf16_kernel(const uint16_t* __r
             for (int r = 0; r < 16; r++) {
                 const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
                 const float v = fmaf(-2.f, accCur[r], ct[row]);
-                if (MODE == 0) {
+                if (MODE != 1) {
                     p2 = __builtin_amdgcn_fmed3f(p1, p2, v);
                     p1 = fminf(p1, v);
-                } else {
-                    hits |= (v <= tq ? 1u : 0u) << r;
                 }
+                if (MODE == 1) hits |= (v <= tq ? 1u : 0u) << r;
+                // MODE 2: under this lane's running second-best + the margin (>= the final bound)
+                if (MODE == 2) hits |= (v <= p2 + tq ? 1u : 0u) << r;
             }
-            if (MODE == 1 && hits) {
+            if (MODE != 0 && hits) {
                 do {
                     const int r = __builtin_ctz(hits);
                     hits &= hits - 1;
                     const int j = t * kT + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
                     const int slot = atomicAdd(&cnt[qrow], 1);
-                    if (slot < kCandMax) cand[(size_t)qrow * kCandMax + slot] = j;
+                    if (MODE == 1 && slot < kCandMax) cand[(size_t)qrow * kCandMax + slot] = j;
+                    if (MODE == 2 && slot < kCandMax2) {
+                        cand[(size_t)qrow * kCandMax2 + slot] = j;
+                        candKey[(size_t)qrow * kCandMax2 + slot] = fmaf(-2.f, accCur[r], ct[rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half]);
+                    }
                 } while (hits);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -732,7 +740,7 @@ __global__ __launch_bounds__(kThreads) void knn2_bf16_kernel(const uint16_t* __r
         if (t + 1 < tEnd) store_tile(buf ^ 1);
         __syncthreads();
     }
-    if (MODE == 0) {
+    if (MODE != 1) {
         // lanes l and l + 32 hold the same query (the other 16 rows of every block)
         const float q1 = __shfl_xor(p1, 32), q2 = __shfl_xor(p2, 32);
         const float n1 = fminf(p1, q1), n2 = fminf(fmaxf(p1, q1), fminf(p2, q2));
@@ -805,6 +813,67 @@ __global__ void knn2_f32_recheck_kernel(const float* __restrict__ A, int nA, con
         const int j = cand[(size_t)q * kCandMax + c];
         const float d = flann_l2(a, B + (size_t)j * dim, dim);
         if (!(d < __builtin_inff())) continue;  // NaN / +inf never enter (the scan's rule)
+        if (lex_lt_f(d, j, b1, i1 < 0 ? INT_MAX : i1)) {
+            b2 = b1;
+            i2 = i1;
+            b1 = d;
+            i1 = j;
+        } else if (lex_lt_f(d, j, b2, i2 < 0 ? INT_MAX : i2)) {
+            b2 = d;
+            i2 = j;
+        }
+    }
+    idxOut[2 * q] = i1;
+    idxOut[2 * q + 1] = i2;
+    keyOut[2 * q] = b1;
+    keyOut[2 * q + 1] = b2;
+}
+
+// the fused pass's per-query margin 2 eps_q + 2 phi_q + slack (rounded up); cnt[q] = 0, or the
+// rescan mark (margin -inf) for a non-finite norm
+__global__ void knn2_bf16_margin_kernel(const float* __restrict__ nA2, int nA, const unsigned* __restrict__ bmax,
+                                        float* __restrict__ margin, int* __restrict__ cnt) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    const double a = sqrt((double)nA2[q]), bm = sqrt((double)__uint_as_float(*bmax));
+    const double m = 2 * (0.0079 * a * bm + 1e-5 * bm * bm) + 2 * 2e-5 * (a + bm) * (a + bm) + 1e-6 * (a + bm) * (a + bm);
+    const bool ok = m == m && m < 1e37 && a < 1e18 && a + bm > 1e-10;
+    float m32 = (float)m;
+    if ((double)m32 < m) m32 = nextafterf(m32, __builtin_inff());
+    margin[q] = ok ? m32 : -__builtin_inff();
+    cnt[q] = ok ? 0 : kCandMax2 + 1;
+}
+
+// the fused pass's candidates: those under the final bound s'_(2) + margin get their exact
+// FLANN-order distances; (distance, index) top-2; overflowing queries into the rescan list
+__global__ void knn2_f32_recheck2_kernel(const float* __restrict__ A, int nA, const float* __restrict__ B, int dim,
+                                         const float* __restrict__ partKey, int parts, const float* __restrict__ margin,
+                                         const int* __restrict__ cnt, const int* __restrict__ cand,
+                                         const float* __restrict__ candKey, int* __restrict__ idxOut,
+                                         float* __restrict__ keyOut, int* __restrict__ resc, int* __restrict__ nResc) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nA) return;
+    const int n = cnt[q];
+    if (n > kCandMax2) {
+        resc[atomicAdd(nResc, 1)] = q;
+        return;
+    }
+    float p1 = __builtin_inff(), p2 = __builtin_inff();
+    for (int s = 0; s < parts; s++) {
+        const size_t o = ((size_t)s * nA + q) * 2;
+        const float c1 = partKey[o], c2 = partKey[o + 1];
+        p2 = fminf(fmaxf(p1, c1), fminf(p2, c2));
+        p1 = fminf(p1, c1);
+    }
+    const float T = p2 + margin[q];  // the fp32 add rounds: the candidates were emitted under larger bounds
+    const float* a = A + (size_t)q * dim;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = -1, i2 = -1;
+    for (int c = 0; c < n; c++) {
+        if (!(candKey[(size_t)q * kCandMax2 + c] <= nextafterf(T, __builtin_inff()))) continue;
+        const int j = cand[(size_t)q * kCandMax2 + c];
+        const float d = flann_l2(a, B + (size_t)j * dim, dim);
+        if (!(d < __builtin_inff())) continue;
         if (lex_lt_f(d, j, b1, i1 < 0 ? INT_MAX : i1)) {
             b2 = b1;
             i2 = i1;
@@ -904,15 +973,17 @@ void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
 }
 
 size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts) {
-    // bf16 rows, norms, bound, candidate lists, part keys, rescan list (+ alignment slack)
-    return (size_t)(nA + nB) * dim * 2 + (size_t)(nA + nB) * 4 + 64 + (size_t)nA * 4 * 3 + (size_t)nA * kCandMax * 4 +
+    // bf16 rows, norms, bound, candidate lists (+ keys), part keys, rescan list (+ alignment slack)
+    return (size_t)(nA + nB) * dim * 2 + (size_t)(nA + nB) * 4 + 64 + (size_t)nA * 4 * 3 + (size_t)nA * kCandMax2 * 8 +
            (size_t)parts * nA * 2 * 4 + (size_t)nA * 4 + 16 * 256;
 }
 
+
+
 int knn2_f32_mfma_parts(int nA, int nB, int nCU) { return knn2_u8_parts(nA, nB, nCU); }
 
-void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, void* work, int* idx,
-                          float* key, hipStream_t s) {
+void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, bool fused, void* work,
+                          int* idx, float* key, hipStream_t s) {
     if (nA <= 0) return;
     char* w = (char*)work;
     auto take = [&](size_t bytes) {
@@ -927,7 +998,8 @@ void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int di
     unsigned* bmax = (unsigned*)take(64);
     float* thr = (float*)take((size_t)nA * 4);
     int* cnt = (int*)take((size_t)nA * 4);
-    int* cand = (int*)take((size_t)nA * kCandMax * 4);
+    int* cand = (int*)take((size_t)nA * kCandMax2 * 4);
+    float* candKey = (float*)take((size_t)nA * kCandMax2 * 4);
     float* partKey = (float*)take((size_t)parts * nA * 2 * 4);
     int* resc = (int*)take((size_t)nA * 4);
     int* nResc = (int*)take(64);
@@ -940,20 +1012,29 @@ void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int di
     const int nTiles = (nB + kT - 1) / kT;
     const int tilesPerPart = parts > 1 ? (nTiles + parts - 1) / parts : (nTiles > 0 ? nTiles : 1);
     const dim3 g((nA + kQ - 1) / kQ, parts);
-    auto go = [&](auto k0, auto k1) {
+    auto go = [&](auto k0, auto k1, auto k2) {
         if (lds > 65536) {
             (void)hipFuncSetAttribute((const void*)k0, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             (void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            (void)hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         }
-        k0<<<g, kThreads, lds, s>>>(a16, nA, b16, nB, nB2, tilesPerPart, nullptr, partKey, nullptr, nullptr);
-        knn2_bf16_bound_kernel<<<(nA + 255) / 256, 256, 0, s>>>(partKey, nA, parts, nA2, bmax, thr, cnt);
-        k1<<<g, kThreads, lds, s>>>(a16, nA, b16, nB, nB2, tilesPerPart, thr, nullptr, cnt, cand);
+        if (fused) {
+            knn2_bf16_margin_kernel<<<(nA + 255) / 256, 256, 0, s>>>(nA2, nA, bmax, thr, cnt);
+            k2<<<g, kThreads, lds, s>>>(a16, nA, b16, nB, nB2, tilesPerPart, thr, partKey, cnt, cand, candKey);
+            knn2_f32_recheck2_kernel<<<(nA + 255) / 256, 256, 0, s>>>(A, nA, B, dim, partKey, parts, thr, cnt, cand,
+                                                                      candKey, idx, key, resc, nResc);
+        } else {
+            k0<<<g, kThreads, lds, s>>>(a16, nA, b16, nB, nB2, tilesPerPart, nullptr, partKey, nullptr, nullptr,
+                                        nullptr);
+            knn2_bf16_bound_kernel<<<(nA + 255) / 256, 256, 0, s>>>(partKey, nA, parts, nA2, bmax, thr, cnt);
+            k1<<<g, kThreads, lds, s>>>(a16, nA, b16, nB, nB2, tilesPerPart, thr, nullptr, cnt, cand, nullptr);
+            knn2_f32_recheck_kernel<<<(nA + 255) / 256, 256, 0, s>>>(A, nA, B, dim, cnt, cand, idx, key, resc, nResc);
+        }
     };
     if (KS == 8)
-        go(knn2_bf16_kernel<8, 0>, knn2_bf16_kernel<8, 1>);
+        go(knn2_bf16_kernel<8, 0>, knn2_bf16_kernel<8, 1>, knn2_bf16_kernel<8, 2>);
     else
-        go(knn2_bf16_kernel<4, 0>, knn2_bf16_kernel<4, 1>);
-    knn2_f32_recheck_kernel<<<(nA + 255) / 256, 256, 0, s>>>(A, nA, B, dim, cnt, cand, idx, key, resc, nResc);
+        go(knn2_bf16_kernel<4, 0>, knn2_bf16_kernel<4, 1>, knn2_bf16_kernel<4, 2>);
 }
 
 int* knn2_f32_mfma_rescan_count(void* work, int nA, int nB, int dim, int parts) {
@@ -967,7 +1048,8 @@ int* knn2_f32_mfma_rescan_count(void* work, int nA, int nB, int dim, int parts) 
     take(64);
     take((size_t)nA * 4);
     take((size_t)nA * 4);
-    take((size_t)nA * kCandMax * 4);
+    take((size_t)nA * kCandMax2 * 4);
+    take((size_t)nA * kCandMax2 * 4);
     take((size_t)parts * nA * 2 * 4);
     take((size_t)nA * 4);
     return (int*)((char*)work + o);

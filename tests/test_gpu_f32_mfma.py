@@ -20,14 +20,23 @@ def ctx(fm3d):
     c.close()
 
 
+def _knn(dm, A, B, **env):
+    for k, v in env.items():
+        os.environ[k] = v
+    try:
+        return dm.knn_match(A, B)
+    finally:
+        for k in env:
+            del os.environ[k]
+
+
 def _check(fm3d, orc, ctx, A, B, eps=0.7):
+    """the fused prefilter (default), the two-pass prefilter (FM3D_F32_FUSED=0) and the VALU scan
+    (FM3D_F32_MFMA=0) byte-identical, and equal to the oracle"""
     dm = fm3d.DescriptorsMatcher(ctx)
     got = dm.knn_match(A, B)
-    os.environ["FM3D_F32_MFMA"] = "0"
-    try:
-        ref = dm.knn_match(A, B)
-    finally:
-        del os.environ["FM3D_F32_MFMA"]
+    assert got.tobytes() == _knn(dm, A, B, FM3D_F32_FUSED="0").tobytes()
+    ref = _knn(dm, A, B, FM3D_F32_MFMA="0")
     assert got.tobytes() == ref.tobytes()
     idx, dist = orc.knn2(A, B, orc.F32, oracle_threads())
     assert np.array_equal(got["trainIdx"], idx)
@@ -66,13 +75,13 @@ def test_f32_mfma_random_rows(fm3d, orc, ctx, dim, nA, nB):
 
 def test_f32_mfma_ties_and_duplicates(fm3d, orc, ctx):
     """exact duplicates among the train rows (equal distances: the lowest index first), queries equal
-    to train rows (distance 0), many rows inside the prefilter's bound (more than its candidate list
-    holds: those queries are rescanned)"""
+    to train rows (distance 0), many rows inside the prefilter's bound (more than either candidate
+    list holds: those queries are rescanned)"""
     rng = np.random.default_rng(7)
     B = rng.normal(0, 0.1, (4096, 128)).astype(np.float32)
     B[2000] = B[17]
     B[3000] = B[17]
-    B[100:140] = B[99]  # 41 identical rows: one query's bound holds them all
+    B[100:300] = B[99]  # 201 identical rows: one query's bound holds them all
     A = np.concatenate([B[17:18], B[99:100], B[:1500], rng.normal(0, 0.1, (1000, 128))]).astype(np.float32)
     _check(fm3d, orc, ctx, A, B)
     got = fm3d.DescriptorsMatcher(ctx).knn_match(A, B)
@@ -87,9 +96,5 @@ def test_f32_mfma_nonfinite_rows_rescanned(fm3d, orc, ctx):
     B[5, 3] = np.inf
     dm = fm3d.DescriptorsMatcher(ctx)
     got = dm.knn_match(A, B)
-    os.environ["FM3D_F32_MFMA"] = "0"
-    try:
-        ref = dm.knn_match(A, B)
-    finally:
-        del os.environ["FM3D_F32_MFMA"]
-    assert got.tobytes() == ref.tobytes()
+    assert got.tobytes() == _knn(dm, A, B, FM3D_F32_FUSED="0").tobytes()
+    assert got.tobytes() == _knn(dm, A, B, FM3D_F32_MFMA="0").tobytes()

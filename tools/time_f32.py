@@ -59,13 +59,19 @@ def main():
         m = fm3d.DescriptorsMatcher(ctx)
         for name, (a, b) in cases.items():
             got, t_mfma = timed(lambda: m.knn_match(a, b), args.reps)
+            os.environ["FM3D_F32_FUSED"] = "0"
+            try:
+                two, t_two = timed(lambda: m.knn_match(a, b), args.reps)
+            finally:
+                del os.environ["FM3D_F32_FUSED"]
             os.environ["FM3D_F32_MFMA"] = "0"
             try:
                 ref, t_valu = timed(lambda: m.knn_match(a, b), args.reps)
             finally:
                 del os.environ["FM3D_F32_MFMA"]
-            res[name] = {"nA": len(a), "nB": len(b), "mfma_ms": round(t_mfma, 2), "valu_ms": round(t_valu, 2),
-                         "identical": bool(got.tobytes() == ref.tobytes())}
+            res[name] = {"nA": len(a), "nB": len(b), "mfma_fused_ms": round(t_mfma, 2),
+                         "mfma_two_pass_ms": round(t_two, 2), "valu_ms": round(t_valu, 2),
+                         "identical": bool(got.tobytes() == ref.tobytes() == two.tobytes())}
             print(name, res[name], flush=True)
     finally:
         ctx.close()
