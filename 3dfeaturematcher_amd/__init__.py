@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
-FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_OTHER = 0, 1, 2, 3, -1  # fm3d_settings.detectorType / extractorType
+FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_STAR, FEAT_OTHER = 0, 1, 2, 3, 4, -1  # fm3d_settings.detectorType / extractorType
 DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
@@ -37,7 +37,7 @@ EXPORTS = (
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
     "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
     "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern", "fm3d_sift_detect", "fm3d_sift_compute",
-    "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
+    "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_star_detect", "fm3d_star_responses", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2",
@@ -72,6 +72,8 @@ class Settings(ctypes.Structure):
         ("siftSigma", ctypes.c_double),
         ("detectorMode", ctypes.c_int), ("fastThreshold", ctypes.c_int), ("fastNonmax", ctypes.c_int),
         ("adaptiveMinFeatures", ctypes.c_int), ("adaptiveMaxFeatures", ctypes.c_int), ("adaptiveMaxIters", ctypes.c_int),
+        ("starMaxSize", ctypes.c_int), ("starResponse", ctypes.c_int), ("starLineThreshold", ctypes.c_int),
+        ("starLineBinarized", ctypes.c_int), ("starSuppression", ctypes.c_int),
     ]
 
     @staticmethod
@@ -236,7 +238,7 @@ class DescriptorsMatcher:
         extractor types select, :64), knnMatch, NNDR.  Returns (matches appended as the reference
         does, kpts_a, kpts_b, desc_a, desc_b)."""
         S = self.ctx.settings
-        if S.detectorMode == 1 or S.detectorType in (FEAT_SIFT, FEAT_FAST) or S.extractorType != S.detectorType:
+        if S.detectorMode == 1 or S.detectorType in (FEAT_SIFT, FEAT_FAST, FEAT_STAR) or S.extractorType != S.detectorType:
             # the reference's two calls with any detector / extractor pair built here (fm3d_detect,
             # fm3d_compute): detect, then compute on the detected keypoints
             feats = Features(self.ctx)
@@ -458,7 +460,7 @@ class SIFT:
 
 class Features:
     """The settings' detector and extractor, whatever their types (descriptorsmatcher.cpp:176-359):
-    STATIC SURF / ORB / SIFT / FAST or ADAPTIVE FAST / SURF detection (fm3d_detect), SURF / SIFT / ORB
+    STATIC SURF / ORB / SIFT / FAST / STAR or ADAPTIVE FAST / SURF / STAR detection (fm3d_detect), SURF / SIFT / ORB
     description (fm3d_compute) on any keypoints."""
 
     def __init__(self, ctx: Context):
@@ -513,6 +515,36 @@ class Features:
             if n.value <= cap:
                 return k[:n.value]
             cap = n.value
+
+
+    def star(self, image: np.ndarray, max_size: int = 45, response: int = 30, line_threshold: int = 10,
+             line_binarized: int = 8, suppression: int = 5) -> np.ndarray:
+        """cv::StarFeatureDetector(maxSize, response, lineThreshold, lineBinarized, suppression).detect:
+        KEYPOINT records in tile order"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap = 4096
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            n = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_star_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, max_size, response,
+                                                  line_threshold, line_binarized, suppression, _vp(k), cap,
+                                                  ctypes.byref(n)))
+            if n.value <= cap:
+                return k[:n.value]
+            cap = n.value
+
+
+    def star_responses(self, image: np.ndarray, max_size: int = 45):
+        """StarDetectorComputeResponses: (border, float32 responses, int16 signed sizes)"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        R = np.zeros((h, w), np.float32)
+        Z = np.zeros((h, w), np.int16)
+        b = ctypes.c_int(0)
+        self.ctx.check(lib().fm3d_star_responses(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, max_size,
+                                                 _ptr(R, ctypes.c_float), _ptr(Z, ctypes.c_int16), ctypes.byref(b)))
+        return b.value, R, Z
 
 
 class SingleCameraTriangulator:

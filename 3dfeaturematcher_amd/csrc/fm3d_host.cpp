@@ -83,6 +83,8 @@ struct fm3d_ctx {
     // SIFT detection / description
     DevBuf siftImg, siftBase, siftG, siftD, siftGL, siftDL, siftTaps, siftScan, siftFlag, siftPos, siftCand, siftAng,
         siftNpk, siftKp, siftDesc;
+    // STAR detection
+    DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     DevBuf f32Work;           // the bf16 MFMA prefilter's scratch (rows, norms, bounds, candidates)
     int nCU = 0;
@@ -1285,6 +1287,120 @@ int fast_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int thr, bool non
     return FM3D_OK;
 }
 
+// StarDetector(maxSize, response, lineProj, lineBin, supp)(img) (features2d/src/stardetector.cpp):
+// the pattern set on the host (StarDetectorComputeResponses' loop), the integrals, responses and tile
+// suppression on the GPU (fm3d_star.hip), keypoints in tile order.  Undefined in OpenCV (and
+// FM3D_ERR_INVALID here): min(w, h) <= 6, maxSize > 128; a suppression window wider than the border
+// (the reference reads outside the image) too.
+int star_patterns(int w, int h, int maxSize, fm3d::StarPat& P) {
+    static const int sizes0[17] = {1, 2, 3, 4, 6, 8, 11, 12, 16, 22, 23, 32, 45, 46, 64, 90, 128};
+    static const int pairs[12][2] = {{1, 0}, {3, 1}, {4, 2}, {5, 3}, {7, 4}, {8, 5},
+                                     {9, 6}, {11, 8}, {13, 10}, {14, 11}, {15, 12}, {16, 14}};
+    const int st = w + 1, mn = std::min(w, h);
+    if (maxSize > 128 || mn <= 6) return 0;
+    int np = 0;
+    while (np < 12 && !(sizes0[pairs[np][0]] >= maxSize ||
+                        sizes0[pairs[np + 1][0]] + sizes0[pairs[np + 1][0]] / 2 >= mn))
+        np++;
+    if (np == 0) return 0;
+    np = std::min(np + 1, 12);  // the first pattern past the range stays, for the size rejection
+    memset(&P, 0, sizeof(P));
+    P.np = np;
+    P.maxIdx = pairs[np - 1][0];
+    int area[17];
+    for (int i = 0; i <= P.maxIdx; i++) {
+        const int u = sizes0[i], t = u + u / 2;
+        int* o = P.ofs + 8 * i;
+        o[0] = (u + 1) * st + u + 1;
+        o[1] = -u * st + u + 1;
+        o[2] = (u + 1) * st - u;
+        o[3] = -u * st - u;
+        o[4] = (t + 1) * st + 1;
+        o[5] = -t;
+        o[6] = t + 1;
+        o[7] = -t * st + 1;
+        area[i] = (2 * u + 1) * (2 * u + 1) + t * t + (t + 1) * (t + 1);
+        P.sizes1[i] = u;
+    }
+    P.sizes1[0] = -P.sizes1[0];
+    P.sizes1[1] = -P.sizes1[1];
+    P.sizes1[P.maxIdx] = -P.sizes1[P.maxIdx];
+    P.border = sizes0[P.maxIdx] + sizes0[P.maxIdx] / 2;
+    P.nsimd = w - 2 * P.border >= 0 ? 4 * ((w - 2 * P.border) / 4) : 0;
+    for (int i = 0; i < np; i++) {
+        const int inner = area[pairs[i][1]], outer = area[pairs[i][0]] - inner;
+        P.inv[2 * i] = 1.f / (float)outer;
+        P.inv[2 * i + 1] = 1.f / (float)inner;
+    }
+    return np;
+}
+
+// the image, its integrals and StarDetectorComputeResponses' maps on the device (starR, starZ)
+int star_responses(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, fm3d::StarPat& P) {
+    if (!star_patterns(w, h, maxSize, P))
+        return fail(c, FM3D_ERR_INVALID, "STAR: undefined for min(w, h) <= 6 or MaxSize > 128");
+    if (w > fm3d::star_tilted_max_width() || fm3d::star_tilted_lds_bytes(w) > 160 * 1024)
+        return fail(c, FM3D_ERR_INVALID, "STAR: image wider than 4,607 pixels");
+    const long long W1H1 = (long long)(w + 1) * (h + 1), WH = (long long)w * h;
+    if (W1H1 > INT32_MAX / 4) return fail(c, FM3D_ERR_INVALID, "image too large for STAR");
+    HIPCHK(c, c->starImg.ensure((size_t)WH));
+    HIPCHK(c, c->starS.ensure((size_t)W1H1 * sizeof(int)));
+    HIPCHK(c, c->starT.ensure((size_t)W1H1 * sizeof(int)));
+    HIPCHK(c, c->starF.ensure((size_t)W1H1 * sizeof(int)));
+    HIPCHK(c, c->starR.ensure((size_t)WH * sizeof(float)));
+    HIPCHK(c, c->starZ.ensure((size_t)WH * sizeof(short)));
+    HIPCHK(c, hipMemcpyAsync(c->starImg.p, img, (size_t)WH, hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_integral(c->starImg.as<uint8_t>(), w, h, c->starS.as<int>(), c->stream);
+    fm3d::launch_star_tilted(c->starImg.as<uint8_t>(), w, h, c->starT.as<int>(), c->starF.as<int>(), c->stream);
+    fm3d::launch_star_resp(c->starS.as<int>(), c->starT.as<int>(), c->starF.as<int>(), w, h, P, c->starR.as<float>(),
+                           c->starZ.as<short>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    return FM3D_OK;
+}
+
+int star_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, int respThr, int lineProj, int lineBin,
+                int supp, std::vector<fm3d_keypoint>& k) {
+    k.clear();
+    fm3d::StarPat P;
+    if (!star_patterns(w, h, maxSize, P))
+        return fail(c, FM3D_ERR_INVALID, "STAR: undefined for min(w, h) <= 6 or MaxSize > 128");
+    const int delta = supp / 2;
+    if (delta < 0 || delta > P.border) return fail(c, FM3D_ERR_INVALID, "STAR: Suppression wider than the border");
+    fm3d::StarNms N{P.border, delta, 0, 0, respThr, lineProj, lineBin};
+    if (h - 2 * P.border > 0 && w - 2 * P.border > 0) {
+        N.ny = (h - 2 * P.border + delta) / (delta + 1);
+        N.nx = (w - 2 * P.border + delta) / (delta + 1);
+    }
+    const int nslot = 2 * N.nx * N.ny;
+    int r;
+    if ((r = ensure_scan_tmp(c, std::max(nslot, 1)))) return r;
+    HIPCHK(c, c->starKp.ensure((size_t)(nslot + 1) * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->starFlag.ensure((size_t)(nslot + 1) * sizeof(int)));
+    HIPCHK(c, c->starPos.ensure((size_t)(nslot + 1) * sizeof(int)));
+    if ((r = star_responses(c, img, w, h, maxSize, P))) return r;
+    if (nslot == 0) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return FM3D_OK;
+    }
+    fm3d::launch_star_nms(c->starR.as<float>(), c->starZ.as<short>(), w, h, N, c->starKp.as<fm3d_keypoint>(),
+                          c->starFlag.as<int>(), c->stream);
+    fm3d::launch_exclusive_scan(c->starFlag.as<int>(), nslot, c->starPos.as<int>(), c->count.as<int>(), c->scanTmp.p,
+                                c->stream);
+    HIPCHK(c, hipGetLastError());
+    int nk = 0;
+    HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nk == 0) return FM3D_OK;
+    HIPCHK(c, c->starOut.ensure((size_t)nk * sizeof(fm3d_keypoint)));
+    fm3d::launch_star_scatter(c->starKp.as<fm3d_keypoint>(), c->starFlag.as<int>(), c->starPos.as<int>(), nslot,
+                              c->starOut.as<fm3d_keypoint>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    k.resize(nk);
+    HIPCHK(c, hipMemcpyAsync(k.data(), c->starOut.p, (size_t)nk * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
 int surf_upload_image(fm3d_ctx* c, const uint8_t* img, int w, int h) {
     HIPCHK(c, c->sfImg.ensure((size_t)w * h));
     HIPCHK(c, hipMemcpyAsync(c->sfImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
@@ -1955,14 +2071,14 @@ int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_
     if (S.extractorType != FM3D_FEAT_SURF) return fail(c, FM3D_ERR_UNSUPPORTED, "only the SURF extractor runs on the GPU");
     *nOut = 0;
     if (n == 0) return FM3D_OK;
-    // a kept keypoint of size < 7.5 has a window narrower than the 21 x 21 patch: OpenCV resizes it
-    // UP, with INTER_AREA's bilinear emulation, a branch neither the kernel nor the oracle restates
+    // a kept keypoint of size < 0.36 has an empty window: OpenCV's resize asserts (a window narrower
+    // than the 21 x 21 patch, size < 7.5, is enlarged by the kernel as OpenCV's INTER_AREA does)
     for (int q = 0; q < n; q++) {
         const float sz = kpts[q].size, s = sz * 1.2f / 9.0f;
         const int gws = 2 * (int)std::lrint(2 * s);
         if (!(sz >= FLT_EPSILON) || h + 1 < gws || w + 1 < gws) continue;  // dropped anyway
-        if ((int)((20 + 1) * s) < 21)
-            return fail(c, FM3D_ERR_UNSUPPORTED, "SURF compute: keypoint size < 7.5 (OpenCV upscales the window)");
+        if ((int)((20 + 1) * s) < 1)
+            return fail(c, FM3D_ERR_INVALID, "SURF compute: keypoint size < 0.36 (an empty window; OpenCV asserts)");
     }
     hipSetDevice(c->device);
     int r;
@@ -2351,6 +2467,32 @@ int fm3d_fast_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int threshol
     return FM3D_OK;
 }
 
+int fm3d_star_responses(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, float* resp, int16_t* sizes,
+                        int* border) {
+    if (!c || !img || !resp || !sizes || !border || w <= 0 || h <= 0) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    fm3d::StarPat P;
+    int r;
+    if ((r = star_responses(c, img, w, h, maxSize, P))) return r;
+    HIPCHK(c, hipMemcpyAsync(resp, c->starR.p, (size_t)w * h * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(sizes, c->starZ.p, (size_t)w * h * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *border = P.border;
+    return FM3D_OK;
+}
+
+int fm3d_star_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, int response, int lineThreshold,
+                     int lineBinarized, int suppression, fm3d_keypoint* kpts, int cap, int* n) {
+    if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    std::vector<fm3d_keypoint> k;
+    int r;
+    if ((r = star_detect(c, img, w, h, maxSize, response, lineThreshold, lineBinarized, suppression, k))) return r;
+    for (int i = 0; i < (int)k.size() && i < cap; i++) kpts[i] = k[i];
+    *n = (int)k.size();
+    return FM3D_OK;
+}
+
 }  // extern "C"
 
 namespace {
@@ -2380,6 +2522,9 @@ int detect_static(fm3d_ctx* c, const uint8_t* img, int w, int h, std::vector<fm3
         return detect_into([&](fm3d_keypoint* p, int cap, int* n) { return fm3d_sift_detect(c, img, w, h, p, cap, n, nullptr); }, k);
     case FM3D_FEAT_FAST:
         return fast_detect(c, img, w, h, S.fastThreshold, S.fastNonmax != 0, k);
+    case FM3D_FEAT_STAR:
+        return star_detect(c, img, w, h, S.starMaxSize, S.starResponse, S.starLineThreshold, S.starLineBinarized,
+                           S.starSuppression, k);
     default:
         return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' detector type has no GPU implementation");
     }
@@ -2390,20 +2535,23 @@ int detect_static(fm3d_ctx* c, const uint8_t* img, int w, int h, std::vector<fm3
 // is in [min, max], the threshold leaves the adjuster's range, the iterations run out or it
 // oscillates.  FastAdjuster(20, true, 1, 200): FastFeatureDetector(thresh, true), -- / ++ by one;
 // SurfAdjuster(400, 2, 1000): the default SURF (4 octaves, 2 layers, not upright) at hessianThreshold
-// thresh, * 0.9 (floored at 1.1) / * 1.1.  The keypoints are the last call's.
+// thresh, * 0.9 (floored at 1.1) / * 1.1; StarAdjuster(30, 2, 200): StarFeatureDetector(16,
+// cvRound(thresh), 10, 8, 3), the same scaling.  The keypoints are the last call's.
 int detect_adaptive(fm3d_ctx* c, const uint8_t* img, int w, int h, std::vector<fm3d_keypoint>& k) {
     const fm3d_settings S = c->s;
-    const bool fast = S.detectorType == FM3D_FEAT_FAST;
-    if (!fast && S.detectorType != FM3D_FEAT_SURF)
-        return fail(c, FM3D_ERR_UNSUPPORTED, "ADAPTIVE runs the FAST and SURF adjusters on the GPU");
-    double thresh = fast ? 20 : 400;
-    const double minT = fast ? 1 : 2, maxT = fast ? 200 : 1000;
+    const bool fast = S.detectorType == FM3D_FEAT_FAST, star = S.detectorType == FM3D_FEAT_STAR;
+    if (!fast && !star && S.detectorType != FM3D_FEAT_SURF)
+        return fail(c, FM3D_ERR_UNSUPPORTED, "ADAPTIVE runs the FAST, SURF and STAR adjusters");
+    double thresh = fast ? 20 : star ? 30 : 400;
+    const double minT = fast ? 1 : 2, maxT = fast ? 200 : star ? 200 : 1000;
     bool down = false, up = false, good = false;
     int iters = S.adaptiveMaxIters, r = FM3D_OK;
     k.clear();
     while (iters > 0 && !(down && up) && !good && thresh > minT && thresh < maxT) {
         if (fast) {
             r = fast_detect(c, img, w, h, (int)thresh, true, k);
+        } else if (star) {
+            r = star_detect(c, img, w, h, 16, (int)std::nearbyint(thresh), 10, 8, 3, k);
         } else {
             fm3d_settings t = S;  // FeatureDetector::create("SURF") + set("hessianThreshold", thresh)
             t.detectorMode = 0;

@@ -316,4 +316,24 @@ void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int n
 void launch_compact_records(const fm3d_record* in, const int* flag, int n, fm3d_record* out, int* count, void* tmp,
                             hipStream_t s);
 
+// ---------------------------------------------------------------- STAR (fm3d_star.hip)
+struct StarPat {   // StarDetectorComputeResponses' pattern set (oracle/orc_star.c orc_star_patterns)
+    int np, maxIdx, border, nsimd;  // pairs, largest pattern, border, columns of the SSE2 block
+    int sizes1[17];                 // pattern sizes, the range's ends negated
+    int ofs[17 * 8];                // integral offsets per pattern: 0-3 into S, 4 and 7 into T, 5 and 6 into F
+    float inv[24];                  // per pair 1/outerArea, 1/innerArea
+};
+struct StarNms {   // StarDetectorSuppressNonmax's tiling and thresholds
+    int border, delta, nx, ny, respThr, lineProj, lineBin;
+};
+size_t star_tilted_lds_bytes(int w);
+int star_tilted_max_width();
+void launch_star_tilted(const uint8_t* img, int w, int h, int* T, int* F, hipStream_t s);
+void launch_star_resp(const int* S, const int* T, const int* F, int w, int h, const StarPat& P, float* resp,
+                      short* sizes, hipStream_t s);
+void launch_star_nms(const float* resp, const short* sizes, int w, int h, const StarNms& N, fm3d_keypoint* kp, int* flag,
+                     hipStream_t s);
+void launch_star_scatter(const fm3d_keypoint* kp, const int* flag, const int* pos, int n, fm3d_keypoint* out,
+                         hipStream_t s);
+
 }  // namespace fm3d

@@ -154,6 +154,11 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->adaptiveMinFeatures = 400;  // cv::DynamicAdaptedFeatureDetector's defaults
     s->adaptiveMaxFeatures = 500;
     s->adaptiveMaxIters = 5;
+    s->starMaxSize = 45;  // cv::StarDetector's defaults
+    s->starResponse = 30;
+    s->starLineThreshold = 10;
+    s->starLineBinarized = 8;
+    s->starSuppression = 5;
     return FM3D_OK;
 }
 
@@ -206,11 +211,13 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
                                   : det == "ORB"  ? FM3D_FEAT_ORB
                                   : det == "SIFT" ? FM3D_FEAT_SIFT
                                   : det == "FAST" ? FM3D_FEAT_FAST
+                                  : det == "STAR" ? FM3D_FEAT_STAR
                                                   : FM3D_FEAT_OTHER;
-            else  // ADAPTIVE: the FAST / SURF adjusters (STAR's has no GPU implementation)
+            else  // ADAPTIVE: the FAST / SURF / STAR adjusters
                 s->detectorType = mode != "ADAPTIVE" ? FM3D_FEAT_OTHER
                                   : det == "SURF"    ? FM3D_FEAT_SURF
                                   : det == "FAST"    ? FM3D_FEAT_FAST
+                                  : det == "STAR"    ? FM3D_FEAT_STAR
                                                      : FM3D_FEAT_OTHER;
         }
         {
@@ -219,6 +226,11 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
             get_i(kv, "FeatureOptions.FastDetector.NonMaxSuppression", &nm);
             s->fastNonmax = nm > 0;  // (int)fs[...] > 0
         }
+        get_i(kv, "FeatureOptions.StarDetector.MaxSize", &s->starMaxSize);
+        get_i(kv, "FeatureOptions.StarDetector.Response", &s->starResponse);
+        get_i(kv, "FeatureOptions.StarDetector.LineThreshold", &s->starLineThreshold);
+        get_i(kv, "FeatureOptions.StarDetector.LineBinarized", &s->starLineBinarized);
+        get_i(kv, "FeatureOptions.StarDetector.Suppression", &s->starSuppression);
         get_i(kv, "FeatureOptions.Adaptive.MinFeatures", &s->adaptiveMinFeatures);
         get_i(kv, "FeatureOptions.Adaptive.MaxFeatures", &s->adaptiveMaxFeatures);
         get_i(kv, "FeatureOptions.Adaptive.MaxIters", &s->adaptiveMaxIters);

@@ -565,7 +565,42 @@ __global__ __launch_bounds__(kDescThreads) void describe_kernel(const uint8_t* _
     const double scale = 1. / (21.0 / W);
     const int iscale = cv_round(scale);
     const bool fast = fabs(scale - iscale) < DBL_EPSILON;
-    if (fast) {
+    if (W < 21) {
+        // a window narrower than the patch (size < 7.5): INTER_AREA enlarges by OpenCV's linear
+        // emulation (oracle orc_resize_area_up): area-mode coefficients in 11-bit fixed point, the
+        // horizontal pass in int (nearest from xmax on), the vertical one as VResizeLinearVec_32s8u on
+        // columns 0..19 and FixedPtCast on column 20.  The window first goes to LDS.
+        __shared__ uint8_t Wn[20 * 20];
+        for (int e = tid; e < W * W; e += kDescThreads) Wn[e] = (uint8_t)WIN(e / W, e - (e / W) * W);
+        __syncthreads();
+        const double inv = 21.0 / W;
+        auto tab = [&](int d, bool col, int& sx, int& a0, int& a1, bool& lin) {
+            sx = (int)floor(d * scale);
+            float f = (float)((d + 1) - (sx + 1) * inv);
+            f = f <= 0 ? 0.f : f - floorf(f);
+            lin = sx + 1 < W;  // columns: d < xmax
+            if (col && sx >= W - 1) {
+                f = 0.f;
+                sx = W - 1;
+            }
+            a0 = (int)rintf(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
+            a1 = (int)rintf(__fmul_rn(f, 2048.f));
+        };
+        for (int pix = tid; pix < 441; pix += kDescThreads) {
+            const int dy = pix / 21, dx = pix - dy * 21;
+            int sx, a0, a1, sy, b0, b1;
+            bool lin, lin_y;
+            tab(dx, true, sx, a0, a1, lin);
+            tab(dy, false, sy, b0, b1, lin_y);
+            const int r0 = min(max(sy, 0), W - 1), r1 = min(max(sy + 1, 0), W - 1);
+            const uint8_t *S0 = Wn + r0 * W, *S1 = Wn + r1 * W;
+            const int h0 = lin ? S0[sx] * a0 + S0[sx + 1] * a1 : S0[sx] * 2048;
+            const int h1 = lin ? S1[sx] * a0 + S1[sx + 1] * a1 : S1[sx] * 2048;
+            int v = dx < 20 ? ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2
+                            : (b0 * h0 + b1 * h1 + (1 << 21)) >> 22;
+            P[pix] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+        }
+    } else if (fast) {
         // integer scale: exact integer block sums (any order), then OpenCV's rounding:
         // (sum + 2) >> 2 on the SIMD columns of the 2x2 case, cvRound(sum / iscale^2) elsewhere
         int* HI = reinterpret_cast<int*>(H);

@@ -92,19 +92,23 @@ typedef struct fm3d_settings {
     int siftNumFeatures, siftOctaveLayers;
     double siftContrastThreshold, siftEdgeThreshold, siftSigma;
     /* FeatureOptions.DetectorMode: 0 STATIC, 1 ADAPTIVE (DynamicAdaptedFeatureDetector over
-       AdjusterAdapter::create(DetectorType), :185-201; FAST and SURF run on the GPU);
+       AdjusterAdapter::create(DetectorType), :185-201; FAST, SURF and STAR run on the GPU);
        FeatureOptions.FastDetector.Threshold / NonMaxSuppression (:215-222, cv::FastFeatureDetector's
        defaults 10 / 1); FeatureOptions.Adaptive.MinFeatures / MaxFeatures / MaxIters (the
        DynamicAdaptedFeatureDetector defaults 400 / 500 / 5) */
     int detectorMode;
     int fastThreshold, fastNonmax;
     int adaptiveMinFeatures, adaptiveMaxFeatures, adaptiveMaxIters;
+    /* FeatureOptions.StarDetector.MaxSize / Response / LineThreshold / LineBinarized / Suppression
+       (:207-212, cv::StarDetector's defaults 45 / 30 / 10 / 8 / 5) */
+    int starMaxSize, starResponse, starLineThreshold, starLineBinarized, starSuppression;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
 #define FM3D_FEAT_ORB 1
 #define FM3D_FEAT_SIFT 2
 #define FM3D_FEAT_FAST 3
+#define FM3D_FEAT_STAR 4
 #define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
@@ -351,6 +355,16 @@ int fm3d_sift_pyramid(fm3d_ctx *ctx, const uint8_t *img, int width, int height, 
    image, KeyPoint(x, y, 7, -1, score) in raster order (score 0 without non-max suppression). */
 int fm3d_fast_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int threshold, int nonmax,
                      fm3d_keypoint *kpts, int cap, int *n);
+/* cv::StarFeatureDetector(maxSize, response, lineThreshold, lineBinarized, suppression).detect
+   (descriptorsmatcher.cpp:204-213; OpenCV 2.4.9 StarDetector, CenSurE): KeyPoint(x, y, size, -1,
+   response) in tile order.  FM3D_ERR_INVALID where OpenCV's result is undefined (min(w, h) <= 6,
+   maxSize > 128, suppression / 2 beyond the pattern border). */
+int fm3d_star_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int maxSize, int response,
+                     int lineThreshold, int lineBinarized, int suppression, fm3d_keypoint *kpts, int cap, int *n);
+/* StarDetectorComputeResponses (the step fm3d_star_detect starts with): per pixel the float response and
+   the signed pattern size (0 in the border), w*h each; *border the pattern border. */
+int fm3d_star_responses(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int maxSize, float *resp,
+                        int16_t *sizes, int *border);
 /* feature_detector_->detect(img, kpts) of generateDetector (descriptorsmatcher.cpp:110-111, 176-293):
    STATIC SURF / ORB / SIFT / FAST, or ADAPTIVE with the FAST or SURF adjuster (the threshold walk of
    DynamicAdaptedFeatureDetector).  *n = all; min(*n, cap) written.  FM3D_ERR_UNSUPPORTED for the

@@ -501,8 +501,9 @@ public:
     }
 
 private:
-    // the detector + extractor (:110-115): the settings' SURF, ORB or SIFT on the GPU; another detector
-    // type has no GPU implementation, so its output comes from the images' side files
+    // the detector + extractor (:110-115): the settings' pair on the GPU (SURF, ORB, SIFT, FAST, STAR,
+    // ADAPTIVE, mixed pairs); a type with no GPU implementation (MSER; BRISK / FREAK) takes its output
+    // from the images' side files
     // (<image>.kpts.f32 and <image>.desc.u8 / .desc.f32), or from the caller's keypoints + descriptors
     void features(const cv::Mat& img, std::vector<cv::KeyPoint>& kpts, cv::Mat& d) {
         if (s_.detectorType == FM3D_FEAT_SURF && s_.extractorType == FM3D_FEAT_SURF) {
@@ -571,6 +572,33 @@ private:
             if (m > 0) std::memcpy(static_cast<void*>(kpts.data()), ko.data(), (size_t)m * sizeof(fm3d_keypoint));
             d.create(m, 128, CV_32FC1);
             if (m > 0) std::memcpy(d.data, desc.data(), (size_t)m * 128 * sizeof(float));
+            return;
+        }
+        if (s_.detectorType != FM3D_FEAT_OTHER && s_.extractorType != FM3D_FEAT_OTHER) {
+            // any other pair built here (FAST, STAR, the ADAPTIVE mode, a detector of one type with an
+            // extractor of another): the reference's two calls through fm3d_detect / fm3d_compute
+            fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
+            int cap = std::max(4096, img.cols * img.rows / 64), n = 0;
+            std::vector<fm3d_keypoint> k;
+            for (;;) {
+                k.resize(cap);
+                fm3d::compat::check(c, fm3d_detect(c, img.data, img.cols, img.rows, k.data(), cap, &n));
+                if (n <= cap) break;
+                cap = n;
+            }
+            int cols = 0, type = 0;
+            fm3d::compat::check(c, fm3d_descriptor_info(c, &cols, &type));
+            const size_t esz = type == FM3D_DESC_BITS ? 1 : sizeof(float);
+            std::vector<fm3d_keypoint> ko(n > 0 ? n : 1);
+            std::vector<uint8_t> desc((size_t)(n > 0 ? n : 1) * cols * esz);
+            int m = 0;
+            if (n > 0)
+                fm3d::compat::check(c, fm3d_compute(c, img.data, img.cols, img.rows, k.data(), n, ko.data(), nullptr, &m,
+                                                    desc.data()));
+            kpts.assign(m, cv::KeyPoint());
+            if (m > 0) std::memcpy(static_cast<void*>(kpts.data()), ko.data(), (size_t)m * sizeof(fm3d_keypoint));
+            d.create(m, cols, type == FM3D_DESC_BITS ? CV_8UC1 : CV_32FC1);
+            if (m > 0) std::memcpy(d.data, desc.data(), (size_t)m * cols * esz);
             return;
         }
         if (!kpts.empty() && !d.empty()) return;

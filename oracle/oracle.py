@@ -365,8 +365,17 @@ def surf_describe(img, kpts, extended=True, upright=True):
           kout.ctypes.data_as(ctypes.c_void_p),
           _p(kept, ctypes.c_int), _p(desc, ctypes.c_float))
     if m < 0:
-        raise ValueError("SURF describe: a keypoint of size < 7.5 (OpenCV upscales its window; not restated)")
+        raise ValueError("SURF describe: a keypoint of size < 0.36 (an empty window; OpenCV's resize asserts)")
     return kout[:m], kept[:m], desc[:m]
+
+
+def resize_area_up(win, D=21):
+    """resize(win, (D, D), INTER_AREA) of a W x W window with W < D: OpenCV's linear emulation"""
+    win = np.ascontiguousarray(win, dtype=np.uint8)
+    W = win.shape[0]
+    out = np.zeros((D, D), np.uint8)
+    lib().orc_resize_area_up(_p(win, ctypes.c_uint8), ctypes.c_int(W), ctypes.c_int(D), _p(out, ctypes.c_uint8))
+    return out
 
 
 def fast_atan2(y, x):
@@ -727,14 +736,21 @@ def adaptive_detect(img, kind, min_features=400, max_features=500, max_iters=5):
     """DynamicAdaptedFeatureDetector(AdjusterAdapter::create(kind), min, max, iters)::detect
     (OpenCV 2.4 features2d/src/dynamic.cpp): FastAdjuster(20, true, 1, 200) steps the FAST threshold by
     one; SurfAdjuster(400, 2, 1000) runs the default SURF (4 octaves, 2 layers, not upright) and scales
-    its Hessian threshold by 0.9 (floored at 1.1) / 1.1.  Returns the last call's keypoints."""
+    its Hessian threshold by 0.9 (floored at 1.1) / 1.1; StarAdjuster(30, 2, 200) runs
+    StarFeatureDetector(16, cvRound(thresh), 10, 8, 3) with the same scaling.  Returns the last call's
+    keypoints."""
     fast = kind == "FAST"
-    thresh, lo, hi = (20, 1, 200) if fast else (400.0, 2, 1000)
+    thresh, lo, hi = {"FAST": (20, 1, 200), "SURF": (400.0, 2, 1000), "STAR": (30.0, 2, 200)}[kind]
     down = up = good = False
     it = max_iters
     k = np.zeros(0, dtype=KEYPOINT)
     while it > 0 and not (down and up) and not good and lo < thresh < hi:
-        k = fast_detect(img, int(thresh), True) if fast else surf_detect(img, float(thresh), 4, 2, upright=False)
+        if fast:
+            k = fast_detect(img, int(thresh), True)
+        elif kind == "SURF":
+            k = surf_detect(img, float(thresh), 4, 2, upright=False)
+        else:  # StarAdjuster: StarFeatureDetector(16, cvRound(thresh), 10, 8, 3)
+            k = star_detect(img, 16, int(np.rint(thresh)), 10, 8, 3)
         if len(k) < min_features:
             down = True
             if fast:
@@ -753,3 +769,50 @@ def adaptive_detect(img, kind, min_features=400, max_features=500, max_iters=5):
             good = True
         it -= 1
     return k
+
+
+def star_integrals(img):
+    """computeIntegralImages (stardetector.cpp): (S, T, F), (h+1, w+1) int32 each"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    S, T, F = (np.zeros((h + 1, w + 1), np.int32) for _ in range(3))
+    lib().orc_star_integrals(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _p(S, ctypes.c_int),
+                             _p(T, ctypes.c_int), _p(F, ctypes.c_int))
+    return S, T, F
+
+
+def star_patterns(w, h, max_size=45):
+    """(npairs, maxIdx, border, signed sizes, (17, 8) integral offsets, (12, 2) reciprocal areas)"""
+    mi, b = ctypes.c_int(0), ctypes.c_int(0)
+    sz = np.zeros(17, np.int32)
+    ofs = np.zeros((17, 8), np.int32)
+    inv = np.zeros((12, 2), np.float32)
+    n = lib().orc_star_patterns(ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(max_size), ctypes.byref(mi),
+                                ctypes.byref(b), _p(sz, ctypes.c_int), _p(ofs, ctypes.c_int), _p(inv, ctypes.c_float))
+    return n, mi.value, b.value, sz, ofs, inv
+
+
+def star_responses(img, max_size=45):
+    """StarDetectorComputeResponses: (border, float32 responses, int16 sizes); border -1 if undefined"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    R = np.zeros((h, w), np.float32)
+    Z = np.zeros((h, w), np.int16)
+    b = lib().orc_star_responses(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(max_size),
+                                 _p(R, ctypes.c_float), _p(Z, ctypes.c_short))
+    return b, R, Z
+
+
+def star_detect(img, max_size=45, response=30, line_proj=10, line_bin=8, suppression=5):
+    """StarFeatureDetector(maxSize, responseThreshold, lineThresholdProjected, lineThresholdBinarized,
+    suppressNonmaxSize).detect(img): KEYPOINT records in tile order"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    args = (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(max_size), ctypes.c_int(response),
+            ctypes.c_int(line_proj), ctypes.c_int(line_bin), ctypes.c_int(suppression))
+    n = lib().orc_star_detect(*args, None, ctypes.c_int(0))
+    if n < 0:
+        raise ValueError("STAR detect: undefined for this image size / MaxSize / Suppression")
+    out = np.zeros(max(n, 1), dtype=KEYPOINT)
+    lib().orc_star_detect(*args, _kp(out), ctypes.c_int(n))
+    return out[:n]

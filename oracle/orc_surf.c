@@ -561,12 +561,78 @@ static void surf_window(const uint8_t *img, int w, int h, const orc_kpt *k, int 
     }
 }
 
+static short sat_short2048(float v)
+{
+    const int i = (int)lrintf(v * 2048);
+    return (short)(i < -32768 ? -32768 : (i > 32767 ? 32767 : i));
+}
+
+/* resize(src W x W, dst D x D, INTER_AREA) with W < D (OpenCV 2.4.9 imgproc/resize.cpp): INTER_AREA only
+ * averages when shrinking; enlarging runs the generic linear path with area-mode coefficients:
+ * s = floor(d * scale), f = (float)((d + 1) - (s + 1) / scale), f = f <= 0 ? 0 : f - floor(f), the
+ * coefficients (1 - f, f) * 2048 rounded to short.  Columns: s + 1 >= W ends the interpolated range
+ * (xmax) and s >= W - 1 becomes (W - 1, f = 0); rows: s and s + 1 clamped to [0, W - 1].
+ * HResizeLinear in int (S[s] * 2048 from xmax on), VResizeLinear as VResizeLinearVec_32s8u's SSE2
+ * arithmetic ((S >> 4) mulhi b, (+2) >> 2) on its columns and FixedPtCast ((+2^21) >> 22) on the rest. */
+ORC_API void orc_resize_area_up(const uint8_t *src, int W, int D, uint8_t *dst)
+{
+    const double inv = (double)D / W, scale = 1. / inv;
+    int xo[64], yo[64], H0[64], H1[64], xmax = D, xs = 0, d;
+    short xa[128], yb[128];
+    for (; xs <= D - 16; xs += 16) {}
+    for (; xs < D - 4; xs += 4) {}
+    for (d = 0; d < D; d++) {
+        int sx = (int)floor(d * scale);
+        float f = (float)((d + 1) - (sx + 1) * inv);
+        f = f <= 0 ? 0.f : f - floorf(f);
+        yo[d] = sx;
+        yb[2 * d] = sat_short2048(1.f - f);
+        yb[2 * d + 1] = sat_short2048(f);
+        if (sx + 1 >= W) {
+            if (d < xmax) xmax = d;
+            if (sx >= W - 1) {
+                f = 0;
+                sx = W - 1;
+            }
+        }
+        xo[d] = sx;
+        xa[2 * d] = sat_short2048(1.f - f);
+        xa[2 * d + 1] = sat_short2048(f);
+    }
+    for (d = 0; d < D; d++) {
+        const int r0 = yo[d] < 0 ? 0 : (yo[d] > W - 1 ? W - 1 : yo[d]);
+        const int r1 = yo[d] + 1 < 0 ? 0 : (yo[d] + 1 > W - 1 ? W - 1 : yo[d] + 1);
+        const uint8_t *S0 = src + (size_t)r0 * W, *S1 = src + (size_t)r1 * W;
+        const int b0 = yb[2 * d], b1 = yb[2 * d + 1];
+        int dx;
+        for (dx = 0; dx < D; dx++) {
+            const int sx = xo[dx];
+            if (dx < xmax) {
+                H0[dx] = S0[sx] * xa[2 * dx] + S0[sx + 1] * xa[2 * dx + 1];
+                H1[dx] = S1[sx] * xa[2 * dx] + S1[sx + 1] * xa[2 * dx + 1];
+            } else {
+                H0[dx] = S0[sx] * 2048;
+                H1[dx] = S1[sx] * 2048;
+            }
+        }
+        for (dx = 0; dx < D; dx++) {
+            int v;
+            if (dx < xs)
+                v = ((((H0[dx] >> 4) * b0) >> 16) + (((H1[dx] >> 4) * b1) >> 16) + 2) >> 2;
+            else
+                v = (b0 * H0[dx] + b1 * H1[dx] + (1 << 21)) >> 22;
+            dst[(size_t)d * D + dx] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+        }
+    }
+}
+
 /* SURFInvoker descriptors for given keypoints (SURF::operator() with useProvidedKeypoints, via
    DescriptorExtractor::compute): size < FLT_EPSILON dropped first, then keypoints whose wavelet
    exceeds the integral image, and (upright == 0) those without an orientation sample; the others get
    angle 270 (upright) or their dominant orientation.  Compacted with their descriptors, kept[] gets
-   the input index of each survivor.  desc: n x (128 | 64).  Returns -1 for a kept keypoint of size
-   < 7.5 (OpenCV's upscaling INTER_AREA branch, not restated). */
+   the input index of each survivor.  desc: n x (128 | 64).  A window narrower than the 21 x 21 patch
+   (size < 7.5) is enlarged by orc_resize_area_up; returns -1 for an empty window (size < 0.36: OpenCV's
+   resize asserts). */
 ORC_API int orc_surf_describe2(const uint8_t *img, int w, int h, const orc_kpt *kin, int n, int extended, int upright,
                                orc_kpt *kout, int *kept, float *desc)
 {
@@ -596,10 +662,13 @@ ORC_API int orc_surf_describe2(const uint8_t *img, int w, int h, const orc_kpt *
         if (upright) k.angle = 360.f - 90.f;
         else if (!surf_orientation(sum, w, h, &k)) continue;
         win_size = (int)((20 + 1) * s);
-        if (win_size < 21) { free(sum); return -1; } /* OpenCV's INTER_AREA upscale branch: not restated */
+        if (win_size < 1) { free(sum); return -1; } /* resize of an empty Mat: OpenCV asserts */
         win = (uint8_t *)malloc((size_t)win_size * win_size);
         surf_window(img, w, h, &k, upright, win_size, win);
-        resize_area(win, win_size, patch);
+        if (win_size < 21)
+            orc_resize_area_up(win, win_size, 21, patch);
+        else
+            resize_area(win, win_size, patch);
         free(win);
         for (i = 0; i < 20; i++)
             for (j = 0; j < 20; j++) {

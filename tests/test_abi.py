@@ -173,7 +173,16 @@ def test_settings_feature_options(fm3d, tmp_path):
              "   Adaptive:\n      MinFeatures: 100\n      MaxFeatures: 200\n      MaxIters: 7\n")
     assert (s.detectorType, s.detectorMode) == (fm3d.FEAT_SURF, 1)
     assert (s.adaptiveMinFeatures, s.adaptiveMaxFeatures, s.adaptiveMaxIters) == (100, 200, 7)
-    for mode, det in (("ADAPTIVE", "STAR"), ("ADAPTIVE", "ORB"), ("STATIC", "MSER"), ("STATIC", "STAR"), ("OTHER", "SURF")):
+    s = load("FeatureOptions:\n   DetectorMode: STATIC\n   DetectorType: STAR\n   ExtractorType: SIFT\n"
+             "   StarDetector:\n      MaxSize: 32\n      Response: 25\n      LineThreshold: 9\n"
+             "      LineBinarized: 7\n      Suppression: 4\n")
+    assert (s.detectorType, s.starMaxSize, s.starResponse, s.starLineThreshold, s.starLineBinarized,
+            s.starSuppression) == (fm3d.FEAT_STAR, 32, 25, 9, 7, 4)
+    s = load("FeatureOptions:\n   DetectorMode: ADAPTIVE\n   DetectorType: STAR\n")
+    assert (s.detectorType, s.detectorMode) == (fm3d.FEAT_STAR, 1)
+    assert (s.starMaxSize, s.starResponse, s.starLineThreshold, s.starLineBinarized, s.starSuppression) == \
+        (45, 30, 10, 8, 5)
+    for mode, det in (("ADAPTIVE", "ORB"), ("STATIC", "MSER"), ("OTHER", "SURF")):
         s = load(f"FeatureOptions:\n   DetectorMode: {mode}\n   DetectorType: {det}\n")
         assert s.detectorType == fm3d.FEAT_OTHER, (mode, det)
     d = fm3d.Settings.default()

@@ -216,8 +216,8 @@ def test_dropin_main_matches_python_api(fm3d, synth, orc, tmp_path):
     pair.desc2.tofile(d / "img2.pgm.desc.u8")
     yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.55)
     yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
-    # a detector type with no GPU implementation (FAST): the side files are read
-    yml += "FeatureOptions:\n   DetectorType: FAST\n   ExtractorType: SIFT\n"
+    # a detector type with no GPU implementation (MSER): the side files are read
+    yml += "FeatureOptions:\n   DetectorType: MSER\n   ExtractorType: SIFT\n"
     (d / "settings.yml").write_text(yml)
     r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
     assert r.returncode == 0, r.stderr + r.stdout
@@ -365,6 +365,49 @@ def test_dropin_main_sift_detection(fm3d, synth, orc, tmp_path):
     kp["response"] = 1
     ref = np.stack([orc.sift_compute(p, kp)[2][0] for p in patches[:8]])
     assert np.array_equal(pd[:8], ref)
+
+
+STAR_OPTIONS = """FeatureOptions:
+   DetectorType: STAR
+   DetectorMode: STATIC
+   StarDetector:
+      MaxSize: 45
+      Response: 20
+      LineThreshold: 10
+      LineBinarized: 8
+      Suppression: 5
+   ExtractorType: SIFT
+"""
+
+
+@pytest.mark.gpu
+def test_dropin_main_star_detection(fm3d, synth, orc, tmp_path):
+    """main_dropin -s settings.yml with DetectorType STAR and ExtractorType SIFT (a pair the reference
+    builds from two FeatureOptions entries): STAR detection and SIFT description of both images on the
+    GPU through fm3d_detect / fm3d_compute; matches, points and normals equal the Python mirror's, the
+    keypoints of image 1 equal the oracle chain's."""
+    pair = synth.make_frame_pair(1500, seed=27)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.6)
+    yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
+    (d / "settings.yml").write_text(yml + STAR_OPTIONS)
+    r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
+    assert r.returncode == 0, r.stderr + r.stdout
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    assert (s.detectorType, s.extractorType, s.starResponse) == (fm3d.FEAT_STAR, fm3d.FEAT_SIFT, 20)
+    m, kept, normals, patches, desc = _python_chain(fm3d, s, pair.img1, pair.img2)
+    assert np.fromfile(d / "out_matches.bin", dtype=fm3d.DMATCH).tobytes() == m.tobytes()
+    assert np.array_equal(np.fromfile(d / "out_points.f64").reshape(-1, 3), kept)
+    assert np.array_equal(np.fromfile(d / "out_normals.f64").reshape(-1, 3), normals)
+    assert len(m) > 20 and len(kept) > 3
+    pd = np.fromfile(d / "out_patch_desc.f32", dtype=np.float32).reshape(-1, 128)
+    assert np.array_equal(pd, desc)
+    ko, _, dk = orc.sift_compute(pair.img1, orc.star_detect(pair.img1, 45, 20, 10, 8, 5))
+    q, t, _ = orc.match_nndr(dk.astype(np.uint8), orc.sift_compute(
+        pair.img2, orc.star_detect(pair.img2, 45, 20, 10, 8, 5))[2].astype(np.uint8), orc.U8, s.nndrEpsilon)
+    assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t)
 
 
 @pytest.mark.gpu

@@ -53,12 +53,14 @@ def test_adaptive_detector_bitwise(fm3d, orc, synth, kind, lo, hi):
     _same_kpts(k, ko)
 
 
-@pytest.mark.parametrize("det,ex", [("FAST", "SIFT"), ("SURF", "SIFT"), ("ORB", "SIFT"), ("FAST", "ORB")])
+@pytest.mark.parametrize("det,ex", [("FAST", "SIFT"), ("SURF", "SIFT"), ("ORB", "SIFT"), ("FAST", "ORB"),
+                                    ("STAR", "SIFT"), ("STAR", "ORB"), ("FAST", "SURF"), ("STAR", "SURF")])
 def test_mixed_detector_extractor(fm3d, orc, synth, det, ex):
     """feature_detector_ and descriptor_extractor_ of different types (the reference builds them
     independently): detect with one, compute with the other, as compareWithNNDR's two calls"""
     fp = synth.make_frame_pair(3000, seed=33)
-    T = {"FAST": fm3d.FEAT_FAST, "SURF": fm3d.FEAT_SURF, "SIFT": fm3d.FEAT_SIFT, "ORB": fm3d.FEAT_ORB}
+    T = {"FAST": fm3d.FEAT_FAST, "SURF": fm3d.FEAT_SURF, "SIFT": fm3d.FEAT_SIFT, "ORB": fm3d.FEAT_ORB,
+         "STAR": fm3d.FEAT_STAR}
     ctx, s = _ctx(fm3d, detectorType=T[det], extractorType=T[ex])
     try:
         m, ka, kb, da, db = fm3d.DescriptorsMatcher(ctx).compareWithNNDRImages(0.8, fp.img1, fp.img2)
@@ -70,6 +72,9 @@ def test_mixed_detector_extractor(fm3d, orc, synth, det, ex):
             return orc.fast_detect(img, s.fastThreshold, bool(s.fastNonmax))
         if det == "SURF":
             return orc.surf_detect(img, s.surfHessianThreshold, s.surfOctaves, s.surfOctaveLayers, upright=bool(s.surfUpright))
+        if det == "STAR":
+            return orc.star_detect(img, s.starMaxSize, s.starResponse, s.starLineThreshold, s.starLineBinarized,
+                                   s.starSuppression)
         if det == "ORB":
             return orc.orb_detect(img, s.orbNumFeatures, s.orbScaleFactor, s.orbNumLevels, s.orbEdgeThreshold,
                                   s.orbPatchSize, s.orbFastThreshold, descriptors=False)[0]
@@ -78,6 +83,8 @@ def test_mixed_detector_extractor(fm3d, orc, synth, det, ex):
     def compute(img, k):
         if ex == "SIFT":
             return orc.sift_compute(img, k)
+        if ex == "SURF":  # FAST's size 7 and STAR's 4..6 take the enlarged-window path
+            return orc.surf_describe(img, k, extended=bool(s.surfExtended), upright=bool(s.surfUpright))
         return orc.orb_compute(img, k)
 
     oa, ob = compute(fp.img1, detect(fp.img1)), compute(fp.img2, detect(fp.img2))
@@ -86,6 +93,8 @@ def test_mixed_detector_extractor(fm3d, orc, synth, det, ex):
     assert np.array_equal(da, oa[2]) and np.array_equal(db, ob[2])
     if ex == "ORB":
         q, t, dist = orc.match_nndr(oa[2], ob[2], orc.BITS, 0.8)
+    elif ex == "SURF":
+        q, t, dist = orc.match_nndr(oa[2], ob[2], orc.F32, 0.8)
     else:
         q, t, dist = orc.match_nndr(oa[2].astype(np.uint8), ob[2].astype(np.uint8), orc.U8, 0.8)
     assert len(m) == len(q) > 5

@@ -89,8 +89,8 @@ def test_surf_compute_size_filter_and_outside_centres(fm3d, orc, synth):
     """ADVICE r02: DescriptorExtractor::compute first drops keypoints of size < FLT_EPSILON
     (KeyPointsFilter::runByKeypointSize; runByImageBorder with border 0 removes nothing), so size 0
     and negative sizes disappear; centres outside the image keep their border-replicated window;
-    a kept keypoint of size < 7.5 (window narrower than 21 pixels, which OpenCV resizes UP) is
-    FM3D_ERR_UNSUPPORTED on the GPU and an error in the oracle, not a silent wrong descriptor."""
+    a kept keypoint of size < 0.36 (an empty window: OpenCV's resize asserts) is FM3D_ERR_INVALID on
+    the GPU and an error in the oracle, not a silent wrong descriptor."""
     img = synth.make_frame_pair(300, seed=8).img1
     kin = np.zeros(6, dtype=fm3d.KEYPOINT)
     kin["x"] = [100.0, -20.0, 700.0, 320.0, 50.0, 320.0]
@@ -101,10 +101,10 @@ def test_surf_compute_size_filter_and_outside_centres(fm3d, orc, synth):
     try:
         k, kept, d = fm3d.SURF(ctx).compute(img, kin)
         small = kin[[1]].copy()
-        small["size"] = 4.0
+        small["size"] = 0.3
         with pytest.raises(fm3d.Fm3dError) as e:
             fm3d.SURF(ctx).compute(img, small)
-        assert e.value.code == fm3d.ERR_UNSUPPORTED
+        assert e.value.code == fm3d.ERR_INVALID
     finally:
         ctx.close()
     ko, kepto, do = orc.surf_describe(img, kin, extended=True)
@@ -113,6 +113,32 @@ def test_surf_compute_size_filter_and_outside_centres(fm3d, orc, synth):
     assert np.array_equal(d, do)
     with pytest.raises(ValueError):
         orc.surf_describe(img, small, extended=True)
+
+
+@pytest.mark.parametrize("upright", [1, 0])
+def test_surf_compute_small_keypoints_enlarge_the_window(fm3d, orc, synth, upright):
+    """keypoints of size < 7.5 (FAST's 7, STAR's 4..6, ...): the window is narrower than the 21 x 21
+    patch and OpenCV's INTER_AREA enlarges it by its linear emulation (oracle orc_resize_area_up);
+    windows of 1 to 20 pixels, inside the image and cut by its borders, upright and oriented."""
+    img = synth.make_frame_pair(300, seed=18).img1
+    sizes = [0.4, 1.0, 2.2, 3.0, 4.0, 5.0, 6.0, 6.9, 7.0, 7.1, 7.4, 7.5, 8.0, 12.0]
+    rng = np.random.default_rng(4)
+    kin = np.zeros(3 * len(sizes), dtype=fm3d.KEYPOINT)
+    kin["size"] = sizes * 3
+    kin["x"] = np.concatenate([rng.uniform(20, 620, len(sizes)), rng.uniform(-3, 3, len(sizes)),
+                               rng.uniform(636, 642, len(sizes))])
+    kin["y"] = np.concatenate([rng.uniform(20, 460, len(sizes)), rng.uniform(0, 479, len(sizes)),
+                               rng.uniform(-2, 481, len(sizes))])
+    kin["angle"] = -1
+    ctx, _ = _ctx(fm3d, surfUpright=upright)
+    try:
+        k, kept, d = fm3d.SURF(ctx).compute(img, kin)
+    finally:
+        ctx.close()
+    ko, kepto, do = orc.surf_describe(img, kin, extended=True, upright=bool(upright))
+    assert len(ko) > len(kin) // 2 and np.array_equal(kept, kepto)
+    _same_kpts(k, ko)
+    assert np.array_equal(d, do)
 
 
 def test_extract_descriptors_from_patches(fm3d, orc, synth):

@@ -84,6 +84,55 @@ def test_resize_area_vs_numpy(orc, W):
     assert np.array_equal(orc.resize_area21(win), _resize_area21_numpy(win))
 
 
+def _resize_area_up_numpy(win, D=21):
+    """INTER_AREA enlarging as OpenCV 2.4.9 emulates it: bilinear with area-mode coefficients in
+    11-bit fixed point, restated independently (per output pixel, numpy scalars)"""
+    W = win.shape[0]
+    inv = D / W
+    scale = 1.0 / inv
+
+    def coef(d):
+        s = int(np.floor(d * scale))
+        f = np.float32((d + 1) - (s + 1) * inv)
+        f = np.float32(0) if f <= 0 else np.float32(f - np.floor(f))
+        return s, f
+
+    def q(v):  # saturate_cast<short>(float * 2048)
+        return int(np.rint(np.float32(v) * np.float32(2048)))
+
+    out = np.zeros((D, D), np.uint8)
+    for dy in range(D):
+        sy, fy = coef(dy)
+        b0, b1 = q(np.float32(1) - fy), q(fy)
+        rows = [win[min(max(sy, 0), W - 1)], win[min(max(sy + 1, 0), W - 1)]]
+        for dx in range(D):
+            sx, fx = coef(dx)
+            interp = sx + 1 < W
+            if sx >= W - 1:
+                sx, fx = W - 1, np.float32(0)
+            a0, a1 = q(np.float32(1) - fx), q(fx)
+            h = [int(r[sx]) * a0 + int(r[sx + 1]) * a1 if interp else int(r[sx]) * 2048 for r in rows]
+            if dx < 20:  # VResizeLinearVec_32s8u's columns (16 + 4 of 21)
+                v = ((((h[0] >> 4) * b0) >> 16) + (((h[1] >> 4) * b1) >> 16) + 2) >> 2
+            else:
+                v = (b0 * h[0] + b1 * h[1] + (1 << 21)) >> 22
+            out[dy, dx] = min(max(v, 0), 255)
+    return out
+
+
+@pytest.mark.parametrize("W", [1, 2, 3, 7, 10, 11, 14, 19, 20])
+def test_resize_area_up_vs_numpy(orc, W):
+    """windows narrower than the 21 x 21 patch (keypoints of size < 7.5) are enlarged"""
+    rng = np.random.default_rng(100 + W)
+    win = rng.integers(0, 256, (W, W), dtype=np.uint8)
+    out = orc.resize_area_up(win)
+    assert np.array_equal(out, _resize_area_up_numpy(win))
+    flat = np.full((W, W), 173, np.uint8)
+    assert (orc.resize_area_up(flat) == 173).all()
+    # each output pixel lies between its two source rows' and columns' extremes
+    assert out.min() >= win.min() and out.max() <= win.max()
+
+
 def test_descriptor_weights_vs_numpy(orc):
     """getGaussianKernel(20, 3.3, CV_32F) outer product (SURFInvoker ctor)."""
     x = np.arange(20) - 9.5

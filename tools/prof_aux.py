@@ -1,6 +1,6 @@
 """Drive the kernels outside the C4 bench for rocprofv3 --kernel-trace --stats:
 SURF detect + describe on the VGA frames (Upright 1 = the reference's settings, and Upright 0),
-extractDescriptorsFromPatches, ORB detect + describe and compute (2,000 / 10,000 features), SIFT detect + describe and compute, the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
+extractDescriptorsFromPatches, ORB detect + describe and compute (2,000 / 10,000 features), SIFT detect + describe and compute, STAR detection (static and ADAPTIVE), the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
 of the 10k-ORB pair) and the circular neighbourhoods of the C4 inliers.  Product path only (no
 oracle); each leg timed with host wall clock after a warm-up call, printed as one JSON line.
 
@@ -70,6 +70,24 @@ def main():
         res["sift_detect_vga"] = {"keypoints": int(len(k)), "ms": round(ms, 3)}
         (kc, _, _), ms = timed(lambda: sift.compute(pair.img1, k), 5)
         res["sift_compute_vga"] = {"keypoints": int(len(kc)), "ms": round(ms, 3)}
+    finally:
+        ctx.close()
+    # STAR (DetectorType STAR, cv::StarDetector's defaults) on the VGA frame, and the StarAdjuster walk
+    s = fm3d.Settings.default()
+    s.detectorType = fm3d.FEAT_STAR
+    ctx = fm3d.Context(s)
+    try:
+        feats = fm3d.Features(ctx)
+        k, ms = timed(lambda: feats.detect(pair.img1), 5)
+        res["star_detect_vga"] = {"keypoints": int(len(k)), "ms": round(ms, 3)}
+    finally:
+        ctx.close()
+    s.detectorMode, s.adaptiveMinFeatures, s.adaptiveMaxFeatures, s.adaptiveMaxIters = 1, 400, 500, 30
+    ctx = fm3d.Context(s)
+    try:
+        feats = fm3d.Features(ctx)
+        k, ms = timed(lambda: feats.detect(pair.img1), 3)
+        res["star_adaptive_vga_400_500"] = {"keypoints": int(len(k)), "ms": round(ms, 3)}
     finally:
         ctx.close()
     # C3 NCC leg: the 10k-ORB pair's DLT inliers, 16 hypotheses, pixelsRay 32
