@@ -135,6 +135,15 @@ int main(void)
                 const int W = 21 + (i % 5);
                 orc_resize_area21(patch, W, tiny);
             }
+            for (i = 1; i <= 20; i++) orc_resize_area_up(patch, i, 21, tiny); /* windows narrower than the patch */
+            {   /* small keypoints: enlarged windows, upright and oriented, inside and across the borders */
+                static orc_kpt ks[6] = {{64, 64, 4, -1, 1, 0, 0}, {1, 2, 7, -1, 1, 0, 0}, {127, 120, 0.4f, -1, 1, 0, 0},
+                                        {30, 0, 6.9f, -1, 1, 0, 0}, {100, 127, 2.2f, -1, 1, 0, 0}, {64, 64, 0.3f, -1, 1, 0, 0}};
+                static orc_kpt ko6[6];
+                orc_surf_describe2(patch, 128, 128, ks, 5, 1, 1, ko6, NULL, (float[6 * 128]){0});
+                orc_surf_describe2(patch, 128, 128, ks, 5, 1, 0, ko6, NULL, (float[6 * 128]){0});
+                if (orc_surf_describe2(patch, 128, 128, ks, 6, 1, 1, ko6, NULL, (float[6 * 128]){0}) != -1) return 1;
+            }
         }
     }
     puts("san_oracle: ok");

@@ -53,6 +53,23 @@ def test_star_responses_bitwise(fm3d, orc, synth, name, max_size):
     assert np.count_nonzero(R) > 0
 
 
+@pytest.mark.parametrize("h,w", [(1080, 1920), (300, 4100), (61, 6000), (2000, 40)])
+def test_star_responses_image_shapes(fm3d, orc, synth, h, w):
+    """wide images take fewer staged rows per block in the tilted-integral kernel (and more than
+    64 KiB of LDS), tall narrow ones many blocks"""
+    base = _images(synth)["vga"]
+    img = np.ascontiguousarray(np.tile(base, (h // 480 + 1, w // 640 + 1))[:h, :w])
+    ctx, _ = _ctx(fm3d)
+    try:
+        b, R, Z = fm3d.Features(ctx).star_responses(img, 16)
+        k = fm3d.Features(ctx).star(img, 16, 30, 10, 8, 3)
+    finally:
+        ctx.close()
+    bo, Ro, Zo = orc.star_responses(img, 16)
+    assert b == bo and np.array_equal(R.view(np.uint32), Ro.view(np.uint32)) and np.array_equal(Z, Zo)
+    _same_kpts(k, orc.star_detect(img, 16, 30, 10, 8, 3))
+
+
 @pytest.mark.parametrize("name,params", [("vga", (45, 30, 10, 8, 5)), ("vga", (16, 30, 10, 8, 3)),
                                          ("vga2", (45, 10, 10, 8, 5)), ("blobs", (23, 20, 6, 5, 7)),
                                          ("blobs", (64, 15, 10, 8, 1)), ("bright", (128, 0, 100, 100, 3)),
