@@ -1340,7 +1340,7 @@ int star_responses(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, f
     if (!star_patterns(w, h, maxSize, P))
         return fail(c, FM3D_ERR_INVALID, "STAR: undefined for min(w, h) <= 6 or MaxSize > 128");
     if (w > fm3d::star_tilted_max_width() || fm3d::star_tilted_lds_bytes(w) > 160 * 1024)
-        return fail(c, FM3D_ERR_INVALID, "STAR: image wider than 4,607 pixels");
+        return fail(c, FM3D_ERR_INVALID, "STAR: image wider than 6,000 pixels");
     const long long W1H1 = (long long)(w + 1) * (h + 1), WH = (long long)w * h;
     if (W1H1 > INT32_MAX / 4) return fail(c, FM3D_ERR_INVALID, "image too large for STAR");
     HIPCHK(c, c->starImg.ensure((size_t)WH));

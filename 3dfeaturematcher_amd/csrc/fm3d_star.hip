@@ -7,9 +7,9 @@
 //   integral (fm3d_surf.hip)  the upright sum S
 //   star_tilted_kernel        the tilted sum T and the flat-tilted sum F: one workgroup walks the rows
 //                             (each row needs the two above it at x-1, x, x+1), a thread per column,
-//                             the last three rows of each in an LDS ring, separate waves storing the
-//                             finished rows; OpenCV's row recursions with its own formulas at columns
-//                             0, 1 and w.  Integer adds: exact.
+//                             the last three rows of each in an LDS ring and the image rows staged in
+//                             LDS a block of rows at a time; OpenCV's row recursions with its own
+//                             formulas at columns 0, 1 and w.  Integer adds: exact.
 //   star_resp_kernel          a thread per pixel: every pattern's box sum from 8 integral reads (int),
 //                             then the (inner, outer) pairs in OpenCV's order and float arithmetic, the
 //                             SSE2 block's float(vals) - float(inner) on its columns and the scalar
@@ -20,6 +20,8 @@
 // The L2-resident integrals (3 x 4 (w+1)(h+1) bytes) serve the responses' gathers.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "fm3d_kernels.h"
 
@@ -32,13 +34,11 @@ constexpr int kTiltThreads = 1024;
 __device__ constexpr int kStarPairs[12][2] = {{1, 0}, {3, 1}, {4, 2}, {5, 3}, {7, 4}, {8, 5},
                                               {9, 6}, {11, 8}, {13, 10}, {14, 11}, {15, 12}, {16, 14}};
 
-// T and F, (h+1) x (w+1) int32.  LDS: the last three rows of each (row y written, y-1 and y-2 read).
-// Waves 0-11 compute, a thread per column (the image bytes of the next row loaded one row ahead);
-// waves 12-15 copy the finished row y-1 from LDS to global memory while row y is computed, so the
-// computing waves never issue a store and their per-row barrier waits on LDS only (s_waitcnt is per
-// wave: a store would make the next image load's wait cover it).
-constexpr int kTiltCompute = 768, kTiltMaxCols = 6;  // columns per computing thread: w + 1 <= 4608
-
+// T and F, (h+1) x (w+1) int32.  LDS: the last three rows of each (row y written, y-1 and y-2 read)
+// and the image rows of the current block of rows.  Per block of `bk` rows the workgroup first stages
+// the bk + 1 image rows the block reads (one round trip to memory per block instead of one per row);
+// then each row is a thread per column and a barrier that waits on LDS only: the row's global stores
+// stay in flight (no load in the row loop waits behind them).
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -46,84 +46,63 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 __global__ __launch_bounds__(kTiltThreads) void star_tilted_kernel(const uint8_t* __restrict__ I, int w, int h,
-                                                                   int* __restrict__ T, int* __restrict__ F) {
-    extern __shared__ int ring[];  // [3][w+1] of T, then [3][w+1] of F
+                                                                   int bk, int* __restrict__ T, int* __restrict__ F) {
+    extern __shared__ int ring[];  // [3][w+1] of T, [3][w+1] of F, then (bk + 1) x w image bytes
     const int st = w + 1, tid = threadIdx.x;
     int* RT = ring;
     int* RF = ring + 3 * st;
-    const bool compute = tid < kTiltCompute;
-    // image bytes per column slot: I(r, x-1) and I(r, x) of rows y-1 (c), y-2 (p) and y (n, prefetch)
-    int cm1[kTiltMaxCols], c0[kTiltMaxCols], pm1[kTiltMaxCols], p0[kTiltMaxCols];
-    auto ld = [&](int r, int x, int& m1, int& z) {
-        const uint8_t* row = I + (size_t)r * w;
-        m1 = x >= 1 && x <= w ? row[x - 1] : 0;
-        z = x < w ? row[x] : 0;
-    };
-    if (compute) {
-#pragma unroll
-        for (int j = 0; j < kTiltMaxCols; j++) {
-            const int x = tid + j * kTiltCompute;
-            if (x > w) break;
-            ld(0, x, pm1[j], p0[j]);
-            // row 0: zeros; row 1: the top image row alone
-            const int t = x == 0 ? 0 : pm1[j];
-            const int f = x == 0 ? p0[j] : x == w ? pm1[j] : p0[j] + pm1[j];
-            T[x] = F[x] = 0;
-            RT[x] = RF[x] = 0;
-            T[st + x] = t;
-            F[st + x] = f;
-            RT[st + x] = t;
-            RF[st + x] = f;
-            if (h >= 2) ld(1, x, cm1[j], c0[j]);
-        }
+    uint8_t* G = reinterpret_cast<uint8_t*>(ring + 6 * st);
+    // rows 0 and 1: zeros, then the top image row alone
+    for (int x = tid; x <= w; x += kTiltThreads) {
+        const int m1 = x >= 1 ? I[x - 1] : 0, z = x < w ? I[x] : 0;
+        const int t = x == 0 ? 0 : m1;
+        const int f = x == 0 ? z : x == w ? m1 : z + m1;
+        T[x] = F[x] = 0;
+        RT[x] = RF[x] = 0;
+        T[st + x] = t;
+        F[st + x] = f;
+        RT[st + x] = t;
+        RF[st + x] = f;
     }
-    __syncthreads();
-    for (int y = 2; y <= h; y++) {
-        const int cur = y % 3, q1 = (y - 1) % 3, q2 = (y - 2) % 3;
-        if (compute) {
+    int* Trow = T + (size_t)2 * st;
+    int* Frow = F + (size_t)2 * st;
+    int cur = 2, q1 = 1, q2 = 0;  // ring slots of rows y, y-1, y-2
+    for (int yb = 2; yb <= h; yb += bk) {
+        // image rows yb-2 .. min(yb+bk-2, h-1) into G (row r at (r - (yb-2)) * w)
+        const int nrow = min(bk + 1, h - (yb - 2));
+        __syncthreads();  // the previous block's reads of G are done (and rows 0-1 are in the ring)
+        for (int e = tid; e < nrow * w; e += kTiltThreads) G[e] = I[(size_t)(yb - 2) * w + e];
+        __syncthreads();
+        const int ye = min(yb + bk - 1, h);
+        for (int y = yb; y <= ye; y++) {
             const int *t1 = RT + q1 * st, *t2 = RT + q2 * st, *f1 = RF + q1 * st, *f2 = RF + q2 * st;
             int *tc = RT + cur * st, *fc = RF + cur * st;
-#pragma unroll
-            for (int j = 0; j < kTiltMaxCols; j++) {
-                const int x = tid + j * kTiltCompute;
-                if (x > w) break;
-                int nm1 = 0, n0 = 0;
-                if (y < h) ld(y, x, nm1, n0);  // the next row's bytes, in flight over this row
-                // a = image row y-1 (cm1 = a[x-1], c0 = a[x]), b = row y-2 (pm1 = b[x-1], p0 = b[x])
-                int t, f;
-                if (x >= 2 && x < w) {
-                    t = t1[x - 1] + t1[x + 1] - t2[x] + pm1[j] + cm1[j];
-                    f = f1[x - 1] + f1[x + 1] - f2[x] + c0[j] + cm1[j];
-                } else if (x == w) {
-                    t = f = t1[w - 1] + pm1[j] + cm1[j];
-                } else if (x == 1) {
-                    t = t1[2] + pm1[j] + cm1[j];
-                    f = f1[2] + pm1[j] + c0[j] + cm1[j];
-                } else {  // x == 0: T[0] = T(y-1, 1), F[0] = T[1] of this row = T(y-1, 2) + b[0] + a[0]
-                    t = t1[1];
-                    f = t1[2] + p0[j] + c0[j];
-                }
+            const uint8_t *a = G + (y - yb + 1) * w, *b = a - w;  // image rows y-1 and y-2
+            // branch-free (a divergent boundary wave would run every case's loads in turn and hold up
+            // the barrier): OpenCV's column-0, 1 and w formulas as masked terms of the general one.
+            // Column 1's F, f1[2] + b[0] + a[1] + a[0], equals the general form because
+            // F(y-1, 0) - F(y-2, 1) = b[0] (both are sums of the same triangles bar that pixel).
+            const int t1_2 = t1[2], a0 = a[0], b0 = b[0];
+            for (int x = tid; x <= w; x += kTiltThreads) {
+                const int xl = max(x - 1, 0), xr = min(x + 1, w);
+                const int L = (x >= 2 || x == w) ? t1[xl] : 0, Rr = x < w ? t1[xr] : 0;
+                const int M = (x >= 2 && x < w) ? t2[x] : 0;
+                const int am = x >= 1 ? a[xl] : 0, bm = x >= 1 ? b[xl] : 0, az = x < w ? a[min(x, w - 1)] : 0;
+                const int t = L + Rr - M + bm + am;
+                const int fg = f1[xl] + f1[xr] - f2[x] + az + am;
+                const int f = x == w ? t : (x == 0 ? t1_2 + b0 + a0 : fg);
                 tc[x] = t;
                 fc[x] = f;
-                pm1[j] = cm1[j];
-                p0[j] = c0[j];
-                cm1[j] = nm1;
-                c0[j] = n0;
+                Trow[x] = t;
+                Frow[x] = f;
             }
-        } else {  // copy the finished row y-1 (read-only during this row) to global memory
-            const int r = (y - 1) % 3;
-            for (int x = tid - kTiltCompute; x <= w; x += kTiltThreads - kTiltCompute) {
-                T[(size_t)(y - 1) * st + x] = RT[r * st + x];
-                F[(size_t)(y - 1) * st + x] = RF[r * st + x];
-            }
-        }
-        lds_barrier();
-    }
-    if (!compute && h >= 2) {  // the last row
-        const int r = h % 3;
-        for (int x = tid - kTiltCompute; x <= w; x += kTiltThreads - kTiltCompute) {
-            T[(size_t)h * st + x] = RT[r * st + x];
-            F[(size_t)h * st + x] = RF[r * st + x];
+            Trow += st;
+            Frow += st;
+            const int nx = q2;
+            q2 = q1;
+            q1 = cur;
+            cur = nx;
+            lds_barrier();
         }
     }
 }
@@ -252,12 +231,26 @@ __global__ __launch_bounds__(256) void star_scatter_kernel(const fm3d_keypoint* 
 
 }  // namespace
 
-size_t star_tilted_lds_bytes(int w) { return (size_t)6 * (w + 1) * sizeof(int); }
-int star_tilted_max_width() { return kTiltCompute * kTiltMaxCols - 1; }
+// the rows per staged block: as many as fit the LDS beside the two 3-row rings, at most 32
+static int star_tilted_block(int w) {
+    const long ring = 6L * (w + 1) * sizeof(int), room = 160L * 1024 - ring;
+    return (int)std::min<long>(32, room / w - 1);
+}
+
+size_t star_tilted_lds_bytes(int w) {
+    const int bk = star_tilted_block(w);
+    return (size_t)6 * (w + 1) * sizeof(int) + (size_t)(bk + 1) * w;
+}
+int star_tilted_max_width() { return 6000; }  // staged blocks of >= 2 rows
 
 void launch_star_tilted(const uint8_t* img, int w, int h, int* T, int* F, hipStream_t s) {
     if (w <= 0 || h <= 0) return;
-    star_tilted_kernel<<<1, kTiltThreads, star_tilted_lds_bytes(w), s>>>(img, w, h, T, F);
+    const int bk = star_tilted_block(w);
+    const size_t lds = star_tilted_lds_bytes(w);
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&star_tilted_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    star_tilted_kernel<<<1, kTiltThreads, lds, s>>>(img, w, h, bk, T, F);
 }
 
 void launch_star_resp(const int* S, const int* T, const int* F, int w, int h, const StarPat& P, float* resp,
