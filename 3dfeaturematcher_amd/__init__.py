@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
-FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_STAR, FEAT_OTHER = 0, 1, 2, 3, 4, -1  # fm3d_settings.detectorType / extractorType
+FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_STAR, FEAT_BRISK, FEAT_OTHER = 0, 1, 2, 3, 4, 5, -1  # fm3d_settings.detectorType / extractorType
 DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
@@ -37,7 +37,7 @@ EXPORTS = (
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
     "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
     "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern", "fm3d_sift_detect", "fm3d_sift_compute",
-    "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_star_detect", "fm3d_star_responses", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
+    "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_star_detect", "fm3d_brisk_compute", "fm3d_star_responses", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2",
@@ -74,6 +74,7 @@ class Settings(ctypes.Structure):
         ("adaptiveMinFeatures", ctypes.c_int), ("adaptiveMaxFeatures", ctypes.c_int), ("adaptiveMaxIters", ctypes.c_int),
         ("starMaxSize", ctypes.c_int), ("starResponse", ctypes.c_int), ("starLineThreshold", ctypes.c_int),
         ("starLineBinarized", ctypes.c_int), ("starSuppression", ctypes.c_int),
+        ("briskThreshold", ctypes.c_int), ("briskOctaves", ctypes.c_int),
     ]
 
     @staticmethod
@@ -244,7 +245,7 @@ class DescriptorsMatcher:
             feats = Features(self.ctx)
             ka, _, da = feats.compute(image_a, feats.detect(image_a))
             kb, _, db = feats.compute(image_b, feats.detect(image_b))
-            binary = S.extractorType == FEAT_ORB
+            binary = S.extractorType in (FEAT_ORB, FEAT_BRISK)
             m = DescriptorsMatcher(self.ctx, binary=binary).compareWithNNDR(epsilon, da, db, matches)
             return m, ka, kb, da, db
         if S.detectorType == FEAT_ORB and S.extractorType == FEAT_ORB:
@@ -460,7 +461,7 @@ class SIFT:
 
 class Features:
     """The settings' detector and extractor, whatever their types (descriptorsmatcher.cpp:176-359):
-    STATIC SURF / ORB / SIFT / FAST / STAR or ADAPTIVE FAST / SURF / STAR detection (fm3d_detect), SURF / SIFT / ORB
+    STATIC SURF / ORB / SIFT / FAST / STAR or ADAPTIVE FAST / SURF / STAR detection (fm3d_detect), SURF / SIFT / ORB / BRISK
     description (fm3d_compute) on any keypoints."""
 
     def __init__(self, ctx: Context):

@@ -83,6 +83,8 @@ struct fm3d_ctx {
     // SIFT detection / description
     DevBuf siftImg, siftBase, siftG, siftD, siftGL, siftDL, siftTaps, siftScan, siftFlag, siftPos, siftCand, siftAng,
         siftNpk, siftKp, siftDesc;
+    // BRISK description
+    DevBuf brImg, brSum, brKp, brIdx, brPat, brPairs, brDesc;
     // STAR detection
     DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
@@ -2467,6 +2469,163 @@ int fm3d_fast_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int threshol
     return FM3D_OK;
 }
 
+// ---------------------------------------------------------------- BRISK extractor
+// cv::BRISK's descriptor on given keypoints (OpenCV 2.4.9 brisk.cpp; oracle/orc_brisk.c): what OpenCV's
+// constructor precomputes (pattern points per scale and rotation, the short pairs, the size list) and
+// its per-keypoint bookkeeping (scale, rotation bin, border filter) stay on the host, in the same
+// float / double expressions and glibc calls; the intensities and bits run on the GPU.
+}  // extern "C"
+namespace brisk {
+constexpr int kScales = 64, kRot = 1024, kPoints = 60;
+const int kNum[5] = {1, 10, 14, 15, 20};
+void radii(float* r) {
+    const double f = 0.85 * 1.0;
+    r[0] = (float)(f * 0.);
+    r[1] = (float)(f * 2.9);
+    r[2] = (float)(f * 4.9);
+    r[3] = (float)(f * 7.4);
+    r[4] = (float)(f * 10.8);
+}
+float scale_factor(int scale) {
+    const float lb_scale = (float)(std::log(30.0) / std::log(2.0));
+    const float step = lb_scale / kScales;
+    return (float)std::pow(2.0, (double)(scale * step));
+}
+void point(int scale, int rot, int i, float& px, float& py, float& sg, int* ringOut = nullptr) {
+    float r[5];
+    radii(r);
+    const float sc = scale_factor(scale);
+    const double theta = (double)rot * 2 * M_PI / (double)kRot;
+    int ring = 0, num = i;
+    while (num >= kNum[ring]) num -= kNum[ring++];
+    const double alpha = (double)num * 2 * M_PI / (double)kNum[ring];
+    const float rr = sc * r[ring];
+    px = (float)(rr * std::cos(alpha + theta));
+    py = (float)(rr * std::sin(alpha + theta));
+    sg = ring == 0 ? 1.3f * sc * 0.5f : (float)(1.3f * sc * (double)r[ring] * std::sin(M_PI / kNum[ring]));
+    if (ringOut) *ringOut = ring;
+}
+int size_of(int scale) {
+    float r[5];
+    radii(r);
+    const float sc = scale_factor(scale);
+    int best = 0;
+    for (int i = 0; i < kPoints; i++) {
+        float x, y, sg;
+        int ring;
+        point(scale, 0, i, x, y, sg, &ring);
+        best = std::max(best, (int)std::ceil(sc * r[ring] + sg) + 1);
+    }
+    return best;
+}
+int kscale(float size) {
+    const float log2c = 0.693147180559945f;
+    const float lb = (float)(logf(30.f) / log2c);
+    const float b06 = 12.0f * 0.6f;
+    int s = (int)(kScales / lb * (logf(size / b06) / log2c) + 0.5);
+    return std::min(std::max(s, 0), kScales - 1);
+}
+int theta(float angle) {
+    if (angle == -1) return 0;
+    int t = (int)(kRot * (angle / 360.0) + 0.5);
+    if (t < 0) t += kRot;
+    if (t >= kRot) t -= kRot;
+    return t;
+}
+std::vector<int> short_pairs() {  // (i, j) interleaved, in generation order
+    const float dMin = (float)(8.2 * 1.0), dMax = (float)(5.85 * 1.0);
+    const float dMin_sq = dMin * dMin, dMax_sq = dMax * dMax;
+    float X[kPoints], Y[kPoints], sg;
+    for (int i = 0; i < kPoints; i++) point(0, 0, i, X[i], Y[i], sg);
+    std::vector<int> p;
+    for (int i = 1; i < kPoints; i++)
+        for (int j = 0; j < i; j++) {
+            const float dx = X[j] - X[i], dy = Y[j] - Y[i];
+            const float n2 = dx * dx + dy * dy;
+            if (n2 > dMin_sq) continue;
+            if (n2 < dMax_sq) {
+                p.push_back(i);
+                p.push_back(j);
+            }
+        }
+    return p;
+}
+}  // namespace brisk
+
+int brisk_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n, fm3d_keypoint* kout,
+                  int32_t* kept, int* nOut, uint8_t* desc) {
+    static const std::vector<int> pairs = brisk::short_pairs();
+    static const std::vector<int> sizes = [] {
+        std::vector<int> v(brisk::kScales);
+        for (int s = 0; s < brisk::kScales; s++) v[s] = brisk::size_of(s);
+        return v;
+    }();
+    *nOut = 0;
+    // runByKeypointSize(FLT_EPSILON), then the scale-dependent border (RoiPredicate), order kept
+    std::vector<fm3d_keypoint> K;
+    std::vector<int> src, combo;
+    std::vector<long> keys;
+    for (int q = 0; q < n; q++) {
+        const fm3d_keypoint& k = kpts[q];
+        if (!(k.size >= FLT_EPSILON)) continue;
+        const int sc = brisk::kscale(k.size), b = sizes[sc];
+        if (k.x < (float)b || k.x >= (float)(w - b) || k.y < (float)b || k.y >= (float)(h - b)) continue;
+        K.push_back(k);
+        src.push_back(q);
+        keys.push_back((long)sc * brisk::kRot + brisk::theta(k.angle));
+    }
+    const int m = (int)K.size();
+    if (m == 0) return FM3D_OK;
+    // the pattern rows in use
+    std::vector<long> uniq(keys);
+    std::sort(uniq.begin(), uniq.end());
+    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    std::vector<float> pat(uniq.size() * brisk::kPoints * 4, 0.f);
+    for (size_t u = 0; u < uniq.size(); u++)
+        for (int i = 0; i < brisk::kPoints; i++) {
+            float* p = &pat[(u * brisk::kPoints + i) * 4];
+            brisk::point((int)(uniq[u] / brisk::kRot), (int)(uniq[u] % brisk::kRot), i, p[0], p[1], p[2]);
+        }
+    std::vector<int> pidx(m);
+    for (int i = 0; i < m; i++) pidx[i] = (int)(std::lower_bound(uniq.begin(), uniq.end(), keys[i]) - uniq.begin());
+    const long long W1H1 = (long long)(w + 1) * (h + 1);
+    if (W1H1 > INT32_MAX / 4) return fail(c, FM3D_ERR_INVALID, "image too large for BRISK");
+    HIPCHK(c, c->brImg.ensure((size_t)w * h));
+    HIPCHK(c, c->brSum.ensure((size_t)W1H1 * sizeof(int)));
+    HIPCHK(c, c->brKp.ensure((size_t)m * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->brIdx.ensure((size_t)m * sizeof(int)));
+    HIPCHK(c, c->brPat.ensure(pat.size() * sizeof(float)));
+    HIPCHK(c, c->brPairs.ensure(pairs.size() * sizeof(int)));
+    HIPCHK(c, c->brDesc.ensure((size_t)m * 64));
+    HIPCHK(c, hipMemcpyAsync(c->brImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->brKp.p, K.data(), (size_t)m * sizeof(fm3d_keypoint), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->brIdx.p, pidx.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->brPat.p, pat.data(), pat.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->brPairs.p, pairs.data(), pairs.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_integral(c->brImg.as<uint8_t>(), w, h, c->brSum.as<int>(), c->stream);
+    fm3d::launch_brisk_desc(c->brImg.as<uint8_t>(), c->brSum.as<int>(), w, c->brKp.as<fm3d_keypoint>(),
+                            c->brIdx.as<int>(), m, c->brPat.as<float4>(), c->brPairs.as<int2>(), (int)pairs.size() / 2,
+                            c->brDesc.as<uint8_t>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(desc, c->brDesc.p, (size_t)m * 64, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < m; i++) {
+        kout[i] = K[i];
+        if (kept) kept[i] = src[i];
+    }
+    *nOut = m;
+    return FM3D_OK;
+}
+
+extern "C" {
+int fm3d_brisk_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,
+                       fm3d_keypoint* kout, int32_t* kept, int* nOut, uint8_t* desc) {
+    if (!c || !img || !nOut || w <= 0 || h <= 0 || n < 0 || (n > 0 && (!kpts || !kout || !desc)))
+        return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    return brisk_compute(c, img, w, h, kpts, n, kout, kept, nOut, desc);
+}
+
 int fm3d_star_responses(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, float* resp, int16_t* sizes,
                         int* border) {
     if (!c || !img || !resp || !sizes || !border || w <= 0 || h <= 0) return FM3D_ERR_INVALID;
@@ -2614,6 +2773,10 @@ int fm3d_descriptor_info(const fm3d_ctx* c, int* cols, int* type) {
         *cols = 32;
         *type = FM3D_DESC_BITS;
         return FM3D_OK;
+    case FM3D_FEAT_BRISK:
+        *cols = 64;
+        *type = FM3D_DESC_BITS;
+        return FM3D_OK;
     default:
         return FM3D_ERR_UNSUPPORTED;
     }
@@ -2628,6 +2791,8 @@ int fm3d_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypo
         return fm3d_sift_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<float*>(desc));
     case FM3D_FEAT_ORB:
         return fm3d_orb_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<uint8_t*>(desc));
+    case FM3D_FEAT_BRISK:
+        return fm3d_brisk_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<uint8_t*>(desc));
     default:
         return c ? fail(c, FM3D_ERR_UNSUPPORTED, "the settings' extractor type has no GPU implementation")
                  : FM3D_ERR_INVALID;

@@ -336,4 +336,10 @@ void launch_star_nms(const float* resp, const short* sizes, int w, int h, const 
 void launch_star_scatter(const fm3d_keypoint* kp, const int* flag, const int* pos, int n, fm3d_keypoint* out,
                          hipStream_t s);
 
+// ---------------------------------------------------------------- BRISK (fm3d_brisk.hip)
+// pat: 60 (x, y, sigma, 0) pattern points per (scale, rotation) in use; pidx: each keypoint's row of pat;
+// pairs: the short pairs (i, j); desc: n x 64 bytes
+void launch_brisk_desc(const uint8_t* img, const int* II, int w, const fm3d_keypoint* kp, const int* pidx, int n,
+                       const float4* pat, const int2* pairs, int npairs, uint8_t* desc, hipStream_t s);
+
 }  // namespace fm3d

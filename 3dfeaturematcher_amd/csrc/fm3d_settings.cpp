@@ -159,6 +159,8 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->starLineThreshold = 10;
     s->starLineBinarized = 8;
     s->starSuppression = 5;
+    s->briskThreshold = 30;  // cv::BRISK's defaults
+    s->briskOctaves = 3;
     return FM3D_OK;
 }
 
@@ -235,10 +237,13 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
         get_i(kv, "FeatureOptions.Adaptive.MaxFeatures", &s->adaptiveMaxFeatures);
         get_i(kv, "FeatureOptions.Adaptive.MaxIters", &s->adaptiveMaxIters);
         if (str("FeatureOptions.ExtractorType", ex))
-            s->extractorType = ex == "SURF"   ? FM3D_FEAT_SURF
-                               : ex == "ORB"  ? FM3D_FEAT_ORB
-                               : ex == "SIFT" ? FM3D_FEAT_SIFT
-                                              : FM3D_FEAT_OTHER;
+            s->extractorType = ex == "SURF"    ? FM3D_FEAT_SURF
+                               : ex == "ORB"   ? FM3D_FEAT_ORB
+                               : ex == "SIFT"  ? FM3D_FEAT_SIFT
+                               : ex == "BRISK" ? FM3D_FEAT_BRISK
+                                               : FM3D_FEAT_OTHER;
+        get_i(kv, "FeatureOptions.BriskDetector.Threshold", &s->briskThreshold);
+        get_i(kv, "FeatureOptions.BriskDetector.Octaves", &s->briskOctaves);
         get_i(kv, "FeatureOptions.SiftDetector.NumFeatures", &s->siftNumFeatures);
         get_i(kv, "FeatureOptions.SiftDetector.NumOctaveLayers", &s->siftOctaveLayers);
         get_d(kv, "FeatureOptions.SiftDetector.ContrastThreshold", &s->siftContrastThreshold);

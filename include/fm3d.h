@@ -102,6 +102,9 @@ typedef struct fm3d_settings {
     /* FeatureOptions.StarDetector.MaxSize / Response / LineThreshold / LineBinarized / Suppression
        (:207-212, cv::StarDetector's defaults 45 / 30 / 10 / 8 / 5) */
     int starMaxSize, starResponse, starLineThreshold, starLineBinarized, starSuppression;
+    /* FeatureOptions.BriskDetector.Threshold / Octaves (:345-347, build/settings.yml:46-48): cv::BRISK's
+       detection parameters, which its descriptor does not use (OpenCV defaults 30 / 3) */
+    int briskThreshold, briskOctaves;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
@@ -109,6 +112,7 @@ typedef struct fm3d_settings {
 #define FM3D_FEAT_SIFT 2
 #define FM3D_FEAT_FAST 3
 #define FM3D_FEAT_STAR 4
+#define FM3D_FEAT_BRISK 5 /* extractor only: the reference's generateDetector has no BRISK branch */
 #define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
@@ -355,6 +359,13 @@ int fm3d_sift_pyramid(fm3d_ctx *ctx, const uint8_t *img, int width, int height, 
    image, KeyPoint(x, y, 7, -1, score) in raster order (score 0 without non-max suppression). */
 int fm3d_fast_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int threshold, int nonmax,
                      fm3d_keypoint *kpts, int cap, int *n);
+/* descriptor_extractor_->compute(img, kpts, desc) of the settings' BRISK extractor
+   (descriptorsmatcher.cpp:343-348: cv::BRISK(Threshold, Octaves); OpenCV 2.4.9 brisk.cpp, the default
+   pattern, no orientation step for given keypoints): keypoints of size < FLT_EPSILON and those within
+   the pattern's reach of the border dropped (order kept; kept[] = input index, may be NULL), then 64
+   bytes (512 bits) per kept keypoint. */
+int fm3d_brisk_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const fm3d_keypoint *kpts, int n,
+                       fm3d_keypoint *kout, int32_t *kept, int *nOut, uint8_t *desc);
 /* cv::StarFeatureDetector(maxSize, response, lineThreshold, lineBinarized, suppression).detect
    (descriptorsmatcher.cpp:204-213; OpenCV 2.4.9 StarDetector, CenSurE): KeyPoint(x, y, size, -1,
    response) in tile order.  FM3D_ERR_INVALID where OpenCV's result is undefined (min(w, h) <= 6,

@@ -816,3 +816,57 @@ def star_detect(img, max_size=45, response=30, line_proj=10, line_bin=8, suppres
     out = np.zeros(max(n, 1), dtype=KEYPOINT)
     lib().orc_star_detect(*args, _kp(out), ctypes.c_int(n))
     return out[:n]
+
+
+def brisk_point(scale, rot, i):
+    """BRISK generateKernel's point i at (scale, rotation): (x, y, sigma) float32"""
+    x, y, s = ctypes.c_float(0), ctypes.c_float(0), ctypes.c_float(0)
+    lib().orc_brisk_point(ctypes.c_int(scale), ctypes.c_int(rot), ctypes.c_int(i), ctypes.byref(x), ctypes.byref(y),
+                          ctypes.byref(s))
+    return np.float32(x.value), np.float32(y.value), np.float32(s.value)
+
+
+def brisk_scale_factor(scale):
+    return np.float32(_fn("orc_brisk_scale_factor", ctypes.c_float)(ctypes.c_int(scale)))
+
+
+def brisk_size(scale):
+    return int(lib().orc_brisk_size(ctypes.c_int(scale)))
+
+
+def brisk_short_pairs():
+    """(i, j) of the short pairs in generation order"""
+    pi = np.zeros(1770, np.int32)
+    pj = np.zeros(1770, np.int32)
+    n = lib().orc_brisk_short_pairs(_p(pi, ctypes.c_int), _p(pj, ctypes.c_int))
+    return pi[:n], pj[:n]
+
+
+def brisk_kscale(size):
+    return int(lib().orc_brisk_kscale(ctypes.c_float(size)))
+
+
+def brisk_theta(angle):
+    return int(lib().orc_brisk_theta(ctypes.c_float(angle)))
+
+
+def brisk_intensity(img, kx, ky, px, py, sigma):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    return int(lib().orc_brisk_intensity(_p(img, ctypes.c_uint8), None, ctypes.c_int(img.shape[1]), ctypes.c_float(kx),
+                                         ctypes.c_float(ky), ctypes.c_float(px), ctypes.c_float(py),
+                                         ctypes.c_float(sigma)))
+
+
+def brisk_compute(img, kpts):
+    """DescriptorExtractor::compute with cv::BRISK (provided keypoints): (kept keypoints, input index of
+    each, (m, 64) uint8 descriptors)"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    kin = np.ascontiguousarray(kpts, dtype=KEYPOINT)
+    n = len(kin)
+    kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+    kept = np.zeros(max(n, 1), dtype=np.int32)
+    desc = np.zeros((max(n, 1), 64), dtype=np.uint8)
+    m = lib().orc_brisk_compute(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _kp(kin), ctypes.c_int(n),
+                                _kp(kout), _p(kept, ctypes.c_int), _p(desc, ctypes.c_uint8))
+    return kout[:m], kept[:m], desc[:m]

@@ -182,6 +182,12 @@ def test_settings_feature_options(fm3d, tmp_path):
     assert (s.detectorType, s.detectorMode) == (fm3d.FEAT_STAR, 1)
     assert (s.starMaxSize, s.starResponse, s.starLineThreshold, s.starLineBinarized, s.starSuppression) == \
         (45, 30, 10, 8, 5)
+    s = load("FeatureOptions:\n   DetectorType: SURF\n   DetectorMode: STATIC\n   BriskDetector:\n"
+             "      Threshold: 25\n      Octaves: 0\n   ExtractorType: BRISK\n")  # build/settings.yml:46-48
+    assert (s.extractorType, s.briskThreshold, s.briskOctaves) == (fm3d.FEAT_BRISK, 25, 0)
+    assert (fm3d.Settings.default().briskThreshold, fm3d.Settings.default().briskOctaves) == (30, 3)
+    assert load("FeatureOptions:\n   DetectorType: BRISK\n").detectorType == fm3d.FEAT_OTHER  # no BRISK detector
+    assert load("FeatureOptions:\n   ExtractorType: FREAK\n").extractorType == fm3d.FEAT_OTHER
     for mode, det in (("ADAPTIVE", "ORB"), ("STATIC", "MSER"), ("OTHER", "SURF")):
         s = load(f"FeatureOptions:\n   DetectorMode: {mode}\n   DetectorType: {det}\n")
         assert s.detectorType == fm3d.FEAT_OTHER, (mode, det)
