@@ -1,6 +1,6 @@
 """Drive the kernels outside the C4 bench for rocprofv3 --kernel-trace --stats:
 SURF detect + describe on the VGA frames (Upright 1 = the reference's settings, and Upright 0),
-extractDescriptorsFromPatches, ORB detect + describe and compute (2,000 / 10,000 features), SIFT detect + describe and compute, STAR detection (static and ADAPTIVE), the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
+extractDescriptorsFromPatches, ORB detect + describe and compute (2,000 / 10,000 features), SIFT detect + describe and compute, STAR detection (static and ADAPTIVE), BRISK description, the C3 NCC leg (16 hypotheses at pixelsRay 32 over every DLT inlier
 of the 10k-ORB pair) and the circular neighbourhoods of the C4 inliers.  Product path only (no
 oracle); each leg timed with host wall clock after a warm-up call, printed as one JSON line.
 
@@ -88,6 +88,17 @@ def main():
         feats = fm3d.Features(ctx)
         k, ms = timed(lambda: feats.detect(pair.img1), 3)
         res["star_adaptive_vga_400_500"] = {"keypoints": int(len(k)), "ms": round(ms, 3)}
+    finally:
+        ctx.close()
+    # BRISK (ExtractorType BRISK) on the VGA frame's SURF keypoints
+    s = fm3d.Settings.default()
+    s.extractorType = fm3d.FEAT_BRISK
+    ctx = fm3d.Context(s)
+    try:
+        feats = fm3d.Features(ctx)
+        ks = feats.detect(pair.img1)
+        (kb, _, _), ms = timed(lambda: feats.compute(pair.img1, ks), 5)
+        res["brisk_compute_vga_surf_kpts"] = {"keypoints": int(len(kb)), "ms": round(ms, 3)}
     finally:
         ctx.close()
     # C3 NCC leg: the 10k-ORB pair's DLT inliers, 16 hypotheses, pixelsRay 32
