@@ -86,7 +86,7 @@ struct fm3d_ctx {
     // BRISK description
     DevBuf brImg, brSum, brKp, brIdx, brPat, brPairs, brDesc;
     // STAR detection
-    DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut;
+    DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut, starWork;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     DevBuf f32Work;           // the bf16 MFMA prefilter's scratch (rows, norms, bounds, candidates)
     int nCU = 0;
@@ -1341,8 +1341,11 @@ int star_patterns(int w, int h, int maxSize, fm3d::StarPat& P) {
 int star_responses(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, fm3d::StarPat& P) {
     if (!star_patterns(w, h, maxSize, P))
         return fail(c, FM3D_ERR_INVALID, "STAR: undefined for min(w, h) <= 6 or MaxSize > 128");
-    if (w > fm3d::star_tilted_max_width() || fm3d::star_tilted_lds_bytes(w) > 160 * 1024)
-        return fail(c, FM3D_ERR_INVALID, "STAR: image wider than 6,000 pixels");
+    // FM3D_STAR_TILT=rows: the one-workgroup row walk (A/B knob); default: the diagonal scans
+    const char* tilt = getenv("FM3D_STAR_TILT");
+    const bool rows = tilt && std::string(tilt) == "rows";
+    if (rows && (w > fm3d::star_tilted_max_width() || fm3d::star_tilted_lds_bytes(w) > 160 * 1024))
+        return fail(c, FM3D_ERR_INVALID, "STAR: image wider than 6,000 pixels for the row walk");
     const long long W1H1 = (long long)(w + 1) * (h + 1), WH = (long long)w * h;
     if (W1H1 > INT32_MAX / 4) return fail(c, FM3D_ERR_INVALID, "image too large for STAR");
     HIPCHK(c, c->starImg.ensure((size_t)WH));
@@ -1353,7 +1356,13 @@ int star_responses(fm3d_ctx* c, const uint8_t* img, int w, int h, int maxSize, f
     HIPCHK(c, c->starZ.ensure((size_t)WH * sizeof(short)));
     HIPCHK(c, hipMemcpyAsync(c->starImg.p, img, (size_t)WH, hipMemcpyHostToDevice, c->stream));
     fm3d::launch_integral(c->starImg.as<uint8_t>(), w, h, c->starS.as<int>(), c->stream);
-    fm3d::launch_star_tilted(c->starImg.as<uint8_t>(), w, h, c->starT.as<int>(), c->starF.as<int>(), c->stream);
+    if (rows) {
+        fm3d::launch_star_tilted(c->starImg.as<uint8_t>(), w, h, c->starT.as<int>(), c->starF.as<int>(), c->stream);
+    } else {
+        HIPCHK(c, c->starWork.ensure(fm3d::star_diag_bytes(w, h)));
+        fm3d::launch_star_tilted_diag(c->starImg.as<uint8_t>(), w, h, c->starWork.p, c->starT.as<int>(),
+                                      c->starF.as<int>(), c->stream);
+    }
     fm3d::launch_star_resp(c->starS.as<int>(), c->starT.as<int>(), c->starF.as<int>(), w, h, P, c->starR.as<float>(),
                            c->starZ.as<short>(), c->stream);
     HIPCHK(c, hipGetLastError());

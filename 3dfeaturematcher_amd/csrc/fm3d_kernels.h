@@ -168,6 +168,8 @@ struct SurfOri {
 };
 void launch_integral(const uint8_t* img, int w, int h, int* sum, hipStream_t s);
 // nb images of w x h back to back, their (w+1) x (h+1) sums back to back
+// the row pass alone: rows[(y + 1) * (w + 1) + k] = sum of image row y's first k pixels (row 0 untouched)
+void launch_integral_rows(const uint8_t* img, int w, int h, int* rows, hipStream_t s);
 void launch_integral_batch(const uint8_t* img, int w, int h, int nb, int* sum, hipStream_t s);
 // Upright 0: flag[q] / angle[q] of keypoint q = (x, y, size) at kp + q*kstride, on the integral
 // image sum + q*sumStride
@@ -329,6 +331,8 @@ struct StarNms {   // StarDetectorSuppressNonmax's tiling and thresholds
 size_t star_tilted_lds_bytes(int w);
 int star_tilted_max_width();
 void launch_star_tilted(const uint8_t* img, int w, int h, int* T, int* F, hipStream_t s);
+size_t star_diag_bytes(int w, int h);
+void launch_star_tilted_diag(const uint8_t* img, int w, int h, void* work, int* T, int* F, hipStream_t s);
 void launch_star_resp(const int* S, const int* T, const int* F, int w, int h, const StarPat& P, float* resp,
                       short* sizes, hipStream_t s);
 void launch_star_nms(const float* resp, const short* sizes, int w, int h, const StarNms& N, fm3d_keypoint* kp, int* flag,

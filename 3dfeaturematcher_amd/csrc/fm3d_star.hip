@@ -5,11 +5,11 @@
 // StarAdjuster of its ADAPTIVE mode (:185-200).  The algorithm is OpenCV 2.4.9's
 // features2d/src/stardetector.cpp, restated in oracle/orc_star.c; the GPU equals that oracle bit for bit:
 //   integral (fm3d_surf.hip)  the upright sum S
-//   star_tilted_kernel        the tilted sum T and the flat-tilted sum F: one workgroup walks the rows
-//                             (each row needs the two above it at x-1, x, x+1), a thread per column,
-//                             the last three rows of each in an LDS ring and the image rows staged in
-//                             LDS a block of rows at a time; OpenCV's row recursions with its own
-//                             formulas at columns 0, 1 and w.  Integer adds: exact.
+//   star_diag_*_kernel        the tilted sum T and the flat-tilted sum F from prefix sums down the
+//                             diagonals of the row prefix sums (below): every diagonal an independent
+//                             chunked scan, exact modulo 2^32
+//   star_tilted_kernel        (FM3D_STAR_TILT=rows) the same T and F by OpenCV's row recursions, one
+//                             workgroup walking the rows with the last three in an LDS ring
 //   star_resp_kernel          a thread per pixel: every pattern's box sum from 8 integral reads (int),
 //                             then the (inner, outer) pairs in OpenCV's order and float arithmetic, the
 //                             SSE2 block's float(vals) - float(inner) on its columns and the scalar
@@ -105,6 +105,70 @@ __global__ __launch_bounds__(kTiltThreads) void star_tilted_kernel(const uint8_t
             lds_barrier();
         }
     }
+}
+
+// ---- the same T and F without the row chain.  With R(y', k) the sum of image row y''s first k pixels,
+// clamped to k in [0, w] (Re), the zero-padded definitions give
+//   T(y, x) = P(y, x + y - 1) - N(y, x - y),   F(y, x) = P(y, x + y) - N(y, x - y),
+//   P(y, u) = sum_{y' < y} Re(y', u - y'),      N(y, v) = sum_{y' < y} Re(y', v + y'),
+// prefix sums down the anti-diagonals (P) and diagonals (N) of Re: independent columns of a scan over
+// y, done in chunks of kDiagRows rows (partial sums, a scan over the chunks, then the rows of each
+// chunk).  Modulo-2^32 arithmetic: exact wherever OpenCV's int sums are.  Column j of P is u = j - 1,
+// of N v = j - h; Wd = w + h + 2 columns.
+constexpr int kDiagRows = 16;
+
+__device__ __forceinline__ unsigned diag_re(const int* __restrict__ R, int w, int yp, int k) {
+    return (unsigned)R[(size_t)(yp + 1) * (w + 1) + min(max(k, 0), w)];
+}
+
+// part[z][c][j]: the chunk's sum of Re over its source rows y' in [c*B, min(c*B + B, h))
+__global__ __launch_bounds__(256) void star_diag_part_kernel(const int* __restrict__ R, int w, int h, int Wd, int C,
+                                                             unsigned* __restrict__ part) {
+    const int j = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y, z = blockIdx.z;
+    if (j >= Wd) return;
+    const int y0 = c * kDiagRows, y1 = min(y0 + kDiagRows, h);
+    unsigned acc = 0;
+    for (int yp = y0; yp < y1; yp++) acc += diag_re(R, w, yp, z == 0 ? (j - 1) - yp : (j - h) + yp);
+    part[((size_t)z * C + c) * Wd + j] = acc;
+}
+
+// part -> exclusive prefix over the chunks, in place
+__global__ __launch_bounds__(256) void star_diag_scan_kernel(int Wd, int C, unsigned* __restrict__ part) {
+    const int j = blockIdx.x * 256 + threadIdx.x, z = blockIdx.y;
+    if (j >= Wd) return;
+    unsigned run = 0;
+    for (int c = 0; c < C; c++) {
+        unsigned* p = part + ((size_t)z * C + c) * Wd + j;
+        const unsigned v = *p;
+        *p = run;
+        run += v;
+    }
+}
+
+// PN[z][y][j] for the rows y in [c*B, min(c*B + B, h + 1))
+__global__ __launch_bounds__(256) void star_diag_emit_kernel(const int* __restrict__ R, int w, int h, int Wd, int C,
+                                                             const unsigned* __restrict__ base,
+                                                             unsigned* __restrict__ PN) {
+    const int j = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y, z = blockIdx.z;
+    if (j >= Wd) return;
+    unsigned acc = base[((size_t)z * C + c) * Wd + j];
+    const int y0 = c * kDiagRows, y1 = min(y0 + kDiagRows, h + 1);
+    unsigned* out = PN + (size_t)z * (h + 1) * Wd + j;
+    for (int y = y0; y < y1; y++) {
+        out[(size_t)y * Wd] = acc;
+        if (y < h) acc += diag_re(R, w, y, z == 0 ? (j - 1) - y : (j - h) + y);
+    }
+}
+
+__global__ __launch_bounds__(256) void star_diag_final_kernel(const unsigned* __restrict__ PN, int w, int h, int Wd,
+                                                              int* __restrict__ T, int* __restrict__ F) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x > w || y > h) return;
+    const unsigned* P = PN + (size_t)y * Wd;
+    const unsigned* N = PN + ((size_t)(h + 1) + y) * Wd;
+    const unsigned n = N[x - y + h];
+    T[(size_t)y * (w + 1) + x] = (int)(P[x + y] - n);
+    F[(size_t)y * (w + 1) + x] = (int)(P[x + y + 1] - n);
 }
 
 __global__ __launch_bounds__(256) void star_resp_kernel(const int* __restrict__ S, const int* __restrict__ T,
@@ -251,6 +315,25 @@ void launch_star_tilted(const uint8_t* img, int w, int h, int* T, int* F, hipStr
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&star_tilted_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     star_tilted_kernel<<<1, kTiltThreads, lds, s>>>(img, w, h, bk, T, F);
+}
+
+size_t star_diag_bytes(int w, int h) {
+    const size_t Wd = (size_t)w + h + 2, C = (size_t)(h + 1 + kDiagRows - 1) / kDiagRows;
+    return ((size_t)(h + 1) * (w + 1) + 2 * C * Wd + 2 * (size_t)(h + 1) * Wd) * 4 + 256;
+}
+
+void launch_star_tilted_diag(const uint8_t* img, int w, int h, void* work, int* T, int* F, hipStream_t s) {
+    if (w <= 0 || h <= 0) return;
+    const int Wd = w + h + 2, C = (h + 1 + kDiagRows - 1) / kDiagRows;
+    int* R = static_cast<int*>(work);
+    unsigned* part = reinterpret_cast<unsigned*>(R + (size_t)(h + 1) * (w + 1));
+    unsigned* PN = part + 2 * (size_t)C * Wd;
+    launch_integral_rows(img, w, h, R, s);
+    const unsigned gx = (unsigned)((Wd + 255) / 256);
+    star_diag_part_kernel<<<dim3(gx, C, 2), 256, 0, s>>>(R, w, h, Wd, C, part);
+    star_diag_scan_kernel<<<dim3(gx, 2), 256, 0, s>>>(Wd, C, part);
+    star_diag_emit_kernel<<<dim3(gx, C, 2), 256, 0, s>>>(R, w, h, Wd, C, part, PN);
+    star_diag_final_kernel<<<dim3((w + 1 + 63) / 64, (h + 1 + 3) / 4), 256, 0, s>>>(PN, w, h, Wd, T, F);
 }
 
 void launch_star_resp(const int* S, const int* T, const int* F, int w, int h, const StarPat& P, float* resp,

@@ -733,6 +733,11 @@ void launch_integral(const uint8_t* img, int w, int h, int* sum, hipStream_t s) 
     integral_cols_kernel<<<(w + 1 + 63) / 64, 64 * kIntBands, 0, s>>>(w, h, sum);
 }
 
+void launch_integral_rows(const uint8_t* img, int w, int h, int* rows, hipStream_t s) {
+    if (w <= 0 || h <= 0) return;
+    integral_rows_kernel<<<h, 64, 0, s>>>(img, w, h, rows);
+}
+
 void launch_surf_hessian(const int* sum, int w, const SurfLayer* layers, int nL, long long total, float* det,
                          float* tr, hipStream_t s) {
     if (total <= 0) return;

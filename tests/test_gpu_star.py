@@ -37,9 +37,13 @@ def _images(synth):
     return {"vga": fp.img1, "vga2": fp.img2, "blobs": _blobs(333, 517, 5), "bright": bright}
 
 
+@pytest.mark.parametrize("tilt", ["diag", "rows"])
 @pytest.mark.parametrize("name,max_size", [("vga", 45), ("vga", 16), ("blobs", 23), ("blobs", 90), ("bright", 128),
                                            ("vga2", 8)])
-def test_star_responses_bitwise(fm3d, orc, synth, name, max_size):
+def test_star_responses_bitwise(fm3d, orc, synth, name, max_size, tilt, monkeypatch):
+    """both forms of the tilted integrals: the diagonal scans (default) and the row walk"""
+    if tilt == "rows":
+        monkeypatch.setenv("FM3D_STAR_TILT", "rows")
     img = _images(synth)[name]
     ctx, _ = _ctx(fm3d)
     try:
