@@ -35,7 +35,7 @@ EXPORTS = (
     "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
-    "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches",
+    "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches", "fm3d_extract_descriptors_from_patches_any",
     "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern", "fm3d_sift_detect", "fm3d_sift_compute",
     "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_star_detect", "fm3d_brisk_compute", "fm3d_star_responses", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
@@ -517,6 +517,19 @@ class Features:
                 return k[:n.value]
             cap = n.value
 
+
+    def extractDescriptorsFromPatches(self, patches: np.ndarray) -> np.ndarray:
+        """DescriptorsMatcher::extractDescriptorsFromPatches (descriptorsmatcher.cpp:133-174) with any of
+        the settings' extractors: (P, cols) rows of the extractor's type (zero rows where the extractor
+        drops the centred keypoint)"""
+        P = np.ascontiguousarray(patches, dtype=np.uint8)
+        if P.ndim != 3 or P.shape[1] != P.shape[2]:
+            raise ValueError("patches must be (P, size, size)")
+        cols, dt = self.descriptor_info()
+        out = np.zeros((P.shape[0], cols), dtype=dt)
+        self.ctx.check(lib().fm3d_extract_descriptors_from_patches_any(self.ctx.handle, _ptr(P, ctypes.c_uint8),
+                                                                       P.shape[0], P.shape[1], _vp(out)))
+        return out
 
     def star(self, image: np.ndarray, max_size: int = 45, response: int = 30, line_threshold: int = 10,
              line_binarized: int = 8, suppression: int = 5) -> np.ndarray:

@@ -2134,6 +2134,33 @@ int fm3d_surf_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_
     return FM3D_OK;
 }
 
+int fm3d_extract_descriptors_from_patches_any(fm3d_ctx* c, const uint8_t* patches, int P, int size, void* desc) {
+    if (!c || P < 0 || size <= 0 || (P && (!patches || !desc))) return FM3D_ERR_INVALID;
+    const int ex = c->s.extractorType;
+    if (ex == FM3D_FEAT_SURF || ex == FM3D_FEAT_SIFT)
+        return fm3d_extract_descriptors_from_patches(c, patches, P, size, static_cast<float*>(desc));
+    if (ex != FM3D_FEAT_ORB && ex != FM3D_FEAT_BRISK)
+        return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' extractor type has no GPU implementation");
+    // descriptorsmatcher.cpp:142-172: the centred keypoint per patch, compute on each patch; the rows
+    // start as Mat::zeros and a dropped keypoint's empty row copies nothing
+    const int cols = ex == FM3D_FEAT_ORB ? 32 : 64;
+    uint8_t* d = static_cast<uint8_t*>(desc);
+    std::memset(d, 0, (size_t)P * cols);
+    const float center = (float)(int)std::floor(size / 2);
+    const fm3d_keypoint k{center, center, (float)size, -1.f, 1.f, 0, 0};
+    for (int p = 0; p < P; p++) {
+        fm3d_keypoint ko;
+        int m = 0, r;
+        const uint8_t* img = patches + (size_t)p * size * size;
+        r = ex == FM3D_FEAT_ORB ? fm3d_orb_compute(c, img, size, size, &k, 1, &ko, nullptr, &m, d + (size_t)p * cols)
+                                : fm3d_brisk_compute(c, img, size, size, &k, 1, &ko, nullptr, &m, d + (size_t)p * cols);
+        if (r) return r;
+        if (p == 0 && m == 0 && ex == FM3D_FEAT_ORB)
+            return fail(c, FM3D_ERR_INVALID, "ORB drops the first patch's keypoint (the reference's rows would have 0 columns)");
+    }
+    return FM3D_OK;
+}
+
 int fm3d_extract_descriptors_from_patches(fm3d_ctx* c, const uint8_t* patches, int P, int size, float* desc) {
     if (!c || P < 0 || size <= 0 || (P && (!patches || !desc))) return FM3D_ERR_INVALID;
     const fm3d_settings& S = c->s;

@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
                                                     imagePointsVector);
         for (size_t i = 0; i < patchesVector.size(); i++)  // singlecameratriangulator.cpp:843-846
             cv::imwrite("patch_" + std::to_string(i) + ".pgm", patchesVector[i]);
-        // main.cpp:182-183 (the settings' SURF extractor on the GPU; other extractors are not built)
+        // main.cpp:182-183 (the settings' extractor on the GPU: SURF, SIFT, ORB or BRISK)
         cv::Mat descriptors;
         if (!patchesVector.empty()) {
             try {
@@ -115,7 +115,8 @@ int main(int argc, char** argv) {
         dump("out_matches.bin", matches.data(), matches.size() * sizeof(cv::DMatch));
         dump("out_points.f64", triagulated.data(), triagulated.size() * sizeof(cv::Vec3d));
         dump("out_normals.f64", normalsVector.data(), normalsVector.size() * sizeof(cv::Vec3d));
-        dump("out_patch_desc.f32", descriptors.data, descriptors.empty() ? 0 : (size_t)descriptors.rows * descriptors.cols * 4);
+        dump(descriptors.depth() == CV_8U ? "out_patch_desc.u8" : "out_patch_desc.f32", descriptors.data,
+             descriptors.empty() ? 0 : (size_t)descriptors.rows * descriptors.cols * descriptors.elemSize());
         dump("out_neighborhoods.f64", neighborhoodsVector.empty() ? nullptr : neighborhoodsVector[0].data(),
              neighborhoodsVector.empty() ? 0 : neighborhoodsVector[0].size() * sizeof(cv::Vec3d));
         std::cout << matches.size() << " matches, " << triagulated.size() << " points with normals, gravity "

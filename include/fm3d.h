@@ -306,6 +306,13 @@ int fm3d_surf_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, 
    level 0, as SIFT::operator() with that keypoint builds it); the reference's descriptors Mat, one
    row per patch. */
 int fm3d_extract_descriptors_from_patches(fm3d_ctx *ctx, const uint8_t *patches, int P, int size, float *desc);
+/* The same for any extractor of the settings, rows laid out as fm3d_descriptor_info says: SURF / SIFT
+   as above (floats), ORB (32 bytes) and BRISK (64 bytes) per patch through their compute on the patch
+   (fm3d_orb_compute / fm3d_brisk_compute).  A patch whose keypoint the extractor drops keeps a zero
+   row, as the reference's Mat::zeros + copyTo of an empty row leaves it (BRISK drops every centred
+   patch keypoint: its pattern reaches ~1.5 x size); FM3D_ERR_INVALID when the first patch's row is
+   dropped by ORB (the reference's matrix would have 0 columns). */
+int fm3d_extract_descriptors_from_patches_any(fm3d_ctx *ctx, const uint8_t *patches, int P, int size, void *desc);
 
 /* ---------------- feature detection + description (ORB, OpenCV 2.4) ---------------- */
 /* FeatureDetector::detect of the settings' ORB detector (descriptorsmatcher.cpp:273-279:

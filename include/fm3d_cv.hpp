@@ -36,7 +36,7 @@
  *     <image>.desc.f32 (N x 128 float32) -- FeatureOptions.ExtractorType ORB / BRISK / FREAK
  *     selects Hamming matching on <image>.desc.u8 rows of 32 / 64 bytes (descriptorsmatcher.cpp:64-71);
  *   - the matcher is exact brute force, ties to the lowest train index;
- *   - extractDescriptorsFromPatches runs the settings' SURF or SIFT extractor on the GPU;
+ *   - extractDescriptorsFromPatches runs the settings' SURF, SIFT, ORB or BRISK extractor on the GPU;
  *   - the PCL viewer is visual only: start/stopVisualizerThread and the view* functions are
  *     no-ops; drawMatches / drawBackProjectedPoints draw with plain loops, in the reference's
  *     colours (cv::RNG(0xFFF0FF0F), random_color);
@@ -494,11 +494,12 @@ public:
                 throw fm3d::compat::Error(FM3D_ERR_INVALID, "patches must be equal-size square 8-bit images");
             std::memcpy(&all[i * (size_t)size * size], m.data, (size_t)size * size);
         }
-        const int dsize = s_.extractorType == FM3D_FEAT_SIFT ? 128 : (s_.surfExtended ? 128 : 64);
-        descriptors.create((int)patchesVector.size(), dsize, CV_32FC1);
         fm3d_ctx* c = fm3d::cvshim::device(s_).ctx();
-        fm3d::compat::check(c, fm3d_extract_descriptors_from_patches(c, all.data(), (int)patchesVector.size(), size,
-                                                                     reinterpret_cast<float*>(descriptors.data)));
+        int cols = 0, type = 0;
+        fm3d::compat::check(c, fm3d_descriptor_info(c, &cols, &type));
+        descriptors.create((int)patchesVector.size(), cols, type == FM3D_DESC_BITS ? CV_8UC1 : CV_32FC1);
+        fm3d::compat::check(c, fm3d_extract_descriptors_from_patches_any(c, all.data(), (int)patchesVector.size(), size,
+                                                                         descriptors.data));
     }
 
 private:

@@ -282,8 +282,9 @@ def _python_chain(fm3d, s, img1, img2):
         kept, normals = no.computeOptimizedNormals(P)
         frames = no.computeFeaturesFrames(kept, normals)
         patches = sct.projectReferencePointsToImageWithFrames(None, frames)
-        ex = fm3d.SIFT(ctx) if s.extractorType == fm3d.FEAT_SIFT else fm3d.SURF(ctx)
-        desc = ex.extractDescriptorsFromPatches(patches) if len(patches) else np.zeros((0, 128), np.float32)
+        feats = fm3d.Features(ctx)
+        cols, dt = feats.descriptor_info()
+        desc = feats.extractDescriptorsFromPatches(patches) if len(patches) else np.zeros((0, cols), dt)
     finally:
         ctx.close()
     return m, kept, normals, patches, desc
@@ -408,6 +409,46 @@ def test_dropin_main_star_detection(fm3d, synth, orc, tmp_path):
     q, t, _ = orc.match_nndr(dk.astype(np.uint8), orc.sift_compute(
         pair.img2, orc.star_detect(pair.img2, 45, 20, 10, 8, 5))[2].astype(np.uint8), orc.U8, s.nndrEpsilon)
     assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("det,ex", [("ORB", "ORB"), ("FAST", "BRISK")])
+def test_dropin_main_binary_extractors(fm3d, synth, orc, tmp_path, det, ex):
+    """main_dropin -s settings.yml with a binary extractor (ORB; BRISK, whose BriskDetector block the
+    reference's settings.yml carries): Hamming matching, the pipeline and the patch descriptors of
+    main.cpp:182-183 equal the Python mirror's; ORB's patch rows equal the ORB oracle on each patch,
+    BRISK's are zero (its pattern reaches past every centred patch keypoint, so OpenCV's rows stay
+    Mat::zeros)."""
+    pair = synth.make_frame_pair(1500, seed=28)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.8)
+    yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
+    yml += (f"FeatureOptions:\n   DetectorType: {det}\n   DetectorMode: STATIC\n   BriskDetector:\n"
+            f"      Threshold: 25\n      Octaves: 0\n   ExtractorType: {ex}\n")
+    (d / "settings.yml").write_text(yml)
+    r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
+    assert r.returncode == 0, r.stderr + r.stdout
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    m, kept, normals, patches, desc = _python_chain(fm3d, s, pair.img1, pair.img2)
+    assert np.fromfile(d / "out_matches.bin", dtype=fm3d.DMATCH).tobytes() == m.tobytes()
+    assert np.array_equal(np.fromfile(d / "out_points.f64").reshape(-1, 3), kept)
+    assert np.array_equal(np.fromfile(d / "out_normals.f64").reshape(-1, 3), normals)
+    assert len(m) > 10 and len(kept) > 3
+    cols = 32 if ex == "ORB" else 64
+    pd = np.fromfile(d / "out_patch_desc.u8", dtype=np.uint8).reshape(-1, cols)
+    assert pd.shape == (len(patches), cols) and np.array_equal(pd, desc)
+    if ex == "BRISK":
+        assert not pd.any()
+    else:
+        kp = np.zeros(1, dtype=fm3d.KEYPOINT)
+        kp["x"] = kp["y"] = 64
+        kp["size"] = 128
+        kp["angle"] = -1
+        kp["response"] = 1
+        ref = np.stack([orc.orb_compute(p, kp)[2][0] for p in patches[:6]])
+        assert np.array_equal(pd[:6], ref)
 
 
 @pytest.mark.gpu
