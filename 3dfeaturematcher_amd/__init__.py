@@ -952,8 +952,10 @@ class MOSAIC:
         return np.float32
 
     def compute(self) -> np.ndarray:
-        """The patch descriptors: (kept features, 128) float32."""
-        ex = SIFT(self.ctx) if self.ctx.settings.extractorType == FEAT_SIFT else SURF(self.ctx)
+        """The patch descriptors: (kept features, cols) rows of the settings' extractor (float32 for
+        SURF / SIFT, uint8 for ORB / BRISK)."""
+        feats = Features(self.ctx)
         if len(self.patches) == 0:
-            return np.zeros((0, ex.descriptorSize), dtype=np.float32)
-        return ex.extractDescriptorsFromPatches(self.patches)
+            cols, dt = feats.descriptor_info()
+            return np.zeros((0, cols), dtype=dt)
+        return feats.extractDescriptorsFromPatches(self.patches)
