@@ -98,6 +98,7 @@ struct fm3d_ctx {
     DevBuf lmProj;  // camera-2 projection constants for the LM kernel (fm3d::ProjConst)
     // staged pipeline inputs
     int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
+    int stK = 0, stP = 0;  // matches and inliers of the last fm3d_pipeline_run_dlt
     bool staged = false;
     hipEvent_t ev[8];
     std::string err;
@@ -1724,9 +1725,11 @@ int fm3d_pipeline_upload(fm3d_ctx* c, const void* descA, int nA, const void* des
     return FM3D_OK;
 }
 
-int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pipeline_stats* stats) {
-    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
-    hipSetDevice(c->device);
+}  // extern "C"
+namespace {
+// match -> NNDR -> compaction -> DLT triangulation -> compaction on the staged inputs (ev[2..5]):
+// K matches, P inliers (c->matches, c->pts, c->srcIdx)
+int pipeline_front(fm3d_ctx* c, int& K, int& P) {
     const int nA = c->stNA, nB = c->stNB;
     int r;
     hipEvent_t* ev = c->ev;
@@ -1738,7 +1741,7 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
     HIPCHK(c, c->matches.ensure((size_t)(nA + 1) * sizeof(fm3d_dmatch)));
     fm3d::launch_compact_dmatch(c->cand.as<fm3d_dmatch>(), c->flag.as<int>(), nA, c->matches.as<fm3d_dmatch>(),
                                 c->count.as<int>(), c->scanTmp.p, c->stream);
-    int K = 0;
+    K = 0;
     HIPCHK(c, hipMemcpyAsync(&K, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventRecord(ev[4], c->stream));
@@ -1765,10 +1768,24 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
     fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), K, c->pts.as<double>(),
                                 c->count.as<int>(), c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
-    int P = 0;
+    P = 0;
     HIPCHK(c, hipMemcpyAsync(&P, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventRecord(ev[5], c->stream));
+    return FM3D_OK;
+}
+}  // namespace
+extern "C" {
+
+int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pipeline_stats* stats) {
+    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    hipSetDevice(c->device);
+    const int nA = c->stNA, nB = c->stNB;
+    hipEvent_t* ev = c->ev;
+    int r, K = 0, P = 0;
+    if ((r = pipeline_front(c, K, P))) return r;
+    c->stK = K;
+    c->stP = P;
     // a6-a15: normals (pyramids were built at upload: images are inputs of the path)
     fm3d_lm_stats ls{};
     if ((r = run_lm(c, P, &ls, ev[6], ev[7]))) return r;
@@ -1831,6 +1848,45 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
         stats->lm.kernel_ms = stats->lm_ms;
         fill_lm_cycles(c, cnt, &stats->lm);
     }
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats) {
+    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    hipSetDevice(c->device);
+    hipEvent_t* ev = c->ev;
+    int r, K = 0, P = 0;
+    if ((r = pipeline_front(c, K, P))) return r;
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stK = K;
+    c->stP = P;
+    if (nInliers) *nInliers = P;
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->queries = c->stNA;
+        stats->trains = c->stNB;
+        stats->matches = K;
+        stats->inliers = P;
+        float ms;
+        hipEventElapsedTime(&ms, ev[2], ev[3]);
+        stats->match_ms = ms;
+        hipEventElapsedTime(&ms, ev[3], ev[4]);
+        stats->nndr_ms = ms;
+        hipEventElapsedTime(&ms, ev[4], ev[5]);
+        stats->triangulate_ms = ms;
+        hipEventElapsedTime(&ms, ev[2], ev[1]);
+        stats->total_ms = ms;
+    }
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_dlt_download(fm3d_ctx* c, fm3d_dmatch* matches, double* points, int32_t* matchIdx) {
+    if (!c || !c->staged) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    if (matches && c->stK) HIPCHK(c, hipMemcpy(matches, c->matches.p, (size_t)c->stK * sizeof(fm3d_dmatch), hipMemcpyDeviceToHost));
+    if (points && c->stP) HIPCHK(c, hipMemcpy(points, c->pts.p, (size_t)c->stP * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    if (matchIdx && c->stP) HIPCHK(c, hipMemcpy(matchIdx, c->srcIdx.p, (size_t)c->stP * sizeof(int), hipMemcpyDeviceToHost));
     return FM3D_OK;
 }
 

@@ -49,7 +49,9 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector peak, an FMA counted as 2 flops
 FP64_PEAK_NO_FMA = 39.3     # the same issue rate for 1-flop instructions (-ffp-contract=off: no FMA)
 HBM_PEAK_GBS = 8000.0
 WORKLOADS = {"c4": dict(keypoints=100_000, width=640, height=480),
-             "c5": dict(keypoints=1_000_000, width=640, height=480)}
+             "c5": dict(keypoints=1_000_000, width=640, height=480),
+             "c2": dict(keypoints=10_000, width=640, height=480)}
+INT8_PEAK_TOPS = 5000.0      # MI355X dense int8 MFMA (2x the ~2.5 PFLOP/s dense bf16; MI355X_MICROARCH.md)
 
 
 def parse():
@@ -57,8 +59,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("auto", "c4", "c5"), default="auto",
-                    help="auto: C4 at one GPU, C5 (one sharded 1M-keypoint frame pair) at N > 1")
+    ap.add_argument("--workload", choices=("auto", "c4", "c5", "c2"), default="auto",
+                    help="auto: C4 at one GPU, C5 (one sharded 1M-keypoint frame pair) at N > 1; c2: BASELINE's "
+                         "C2 (10k SIFT per frame, match + DLT triangulate only, one GPU)")
     ap.add_argument("--weak", action="store_true", help="every rank its own C4 frame pair (weak scaling)")
     ap.add_argument("--keypoints", type=int, default=0)
     ap.add_argument("--width", type=int, default=0)
@@ -96,6 +99,8 @@ def main():
         workload = "c5" if world > 1 and not args.weak else "c4"
     if args.weak:
         workload = "c4"
+    if workload == "c2":
+        return run_c2(args)
     wl = dict(WORKLOADS[workload])
     for k in ("keypoints", "width", "height"):
         if getattr(args, k):
@@ -264,6 +269,101 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_c2(args):
+    """BASELINE.json configs[1] (C2): 10k SIFT-128 keypoints per 640x480 frame, brute-force L2 match
+    (exact u8 path) + NNDR + DLT triangulation, no normals; one GPU.  A step is fm3d_pipeline_run_dlt on
+    HBM-resident inputs; the value is the triangulated inliers (matched + triangulated keypoints) per
+    second.  The roofline is the match stage's (int8 MFMA), timed by HIP events around it.  Every
+    step's matches and points are checked against the CPU oracle (knn2 + NNDR + triangulate)."""
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    synth = importlib.import_module("3dfeaturematcher_amd.synth")
+    wl = dict(WORKLOADS["c2"])
+    for k in ("keypoints", "width", "height"):
+        if getattr(args, k):
+            wl[k] = getattr(args, k)
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=args.seed, desc="sift")
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon = args.nndr
+    ctx = fm3d.Context(s)
+    sct = fm3d.SingleCameraTriangulator(ctx)
+    sct.set_g12(pair.g12)
+    pipe = fm3d.Pipeline(ctx)
+    pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+    for _ in range(args.warmup):
+        pipe.run_dlt()
+    stats = []
+    t0 = time.perf_counter()
+    total = 0
+    for _ in range(args.steps):
+        n, st = pipe.run_dlt()
+        total += n
+        stats.append(st)
+    elapsed = time.perf_counter() - t0
+    last = stats[-1]
+    m, pts, src = pipe.dlt_results(last["matches"], last["inliers"])
+    ctx.close()
+    # the cpu_baseline leg: the oracle's C2 path on the host cores, whose outputs also check the GPU's
+    cpu, (q, t, dist, opts) = (None, (None,) * 4) if args.no_cpu else c2_cpu_baseline(pair, s, args)
+    verified = None if q is None else bool(
+        np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t) and np.array_equal(m["distance"], dist)
+        and np.array_equal(pts, opts))
+    n_q, n_t, d = len(pair.desc1), len(pair.desc2), pair.desc1.shape[1]
+    match_ms = float(np.mean([x["match_ms"] for x in stats]))
+    achieved = 2.0 * n_q * n_t * d / (match_ms * 1e-3) / 1e12
+    out = {
+        "metric": "matched+triangulated keypoints/sec (BASELINE C2: match + DLT triangulate only)",
+        "value": total / elapsed,
+        "unit": "keypoints/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8 (exact int32 distances), f64 triangulation",
+        "data": "synthetic (ray-cast facet scene, seeded; 3dfeaturematcher_amd/synth.py)",
+        "config": {"workload": f"C2: {wl['keypoints'] // 1000}k SIFT-128 (u8) keypoints per {wl['width']}x{wl['height']} "
+                               f"frame pair, knnMatch k=2 + NNDR {args.nndr} + DLT triangulation",
+                   "keypoints_per_frame": wl["keypoints"], "parallelism": "1 GPU",
+                   "timed": "match -> NNDR -> compaction -> DLT -> compaction on HBM-resident inputs, host syncs "
+                            "for the two counts included"},
+        "roofline": {"kernel": "match stage (row constants + knn2_i8_kernel + part merge + NNDR), HIP events",
+                     "bound": "mfma", "compute": "int8 MFMA (v_mfma_i32_32x32x32_i8) + VALU top-2 epilogue",
+                     "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TOP/s", "frac": achieved / INT8_PEAK_TOPS,
+                     "traffic": None, "algorithmic": f"2 x {n_q} x {n_t} x {d} int8 ops per launch",
+                     "avg_launch_ms": match_ms},
+        "cpu_baseline": cpu,
+        "stages_ms": {k: last[k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "total_ms")},
+        "counts": {"queries": n_q, "matches": int(last["matches"]), "inliers": int(last["inliers"])},
+        "verified": verified,
+        "verification": "matches (query, train, distance) and inlier points byte-equal to the cpu_baseline "
+                        "leg's oracle outputs",
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+def c2_cpu_baseline(pair, s, args):
+    """The oracle's C2 path (knn2 + NNDR + DLT, C with OpenMP on the granted cores) on the whole 10k
+    frame pair: (baseline dict, its outputs)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    quota = cpu_quota()
+    cores = len(os.sched_getaffinity(0))
+    if quota:
+        cores = max(1, min(cores, int(quota)))
+    t0 = time.perf_counter()
+    q, t, dist = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, args.nndr, cores)
+    opts, _ = orc.triangulate(pair.cam, pair.g12, s.zThresholdMin, s.zThresholdMax, pair.kp1, pair.kp2, q, t)
+    el = time.perf_counter() - t0
+    base = {"value": len(opts) / el, "unit": "keypoints/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"the whole C2 frame pair: oracle knn2 of {len(pair.desc1)} x {len(pair.desc2)} u8 rows + "
+                      f"NNDR + DLT of {len(q)} matches, {el:.2f} s"}
+    return base, (q, t, dist, opts)
 
 
 def verify_against_fixture(args, wl, workload, pair, rec):

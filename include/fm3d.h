@@ -406,6 +406,13 @@ int fm3d_pipeline_upload(fm3d_ctx *ctx, const void *descA, int nA, const void *d
    recordsDev: device buffer with capacity nA records (NULL: internal); *nKept: survivors.
    Synchronises the context stream before returning. */
 int fm3d_pipeline_run(fm3d_ctx *ctx, fm3d_record *recordsDev, int *nKept, fm3d_pipeline_stats *stats);
+/* BASELINE.json's C2 ("brute-force L2 match + DLT triangulate only"): match -> NNDR -> triangulate on
+   the staged inputs, no normals; *nInliers = the triangulated points kept by the z filter (stats:
+   match / NNDR-compaction / triangulate / total HIP-event times). */
+int fm3d_pipeline_run_dlt(fm3d_ctx *ctx, int *nInliers, fm3d_pipeline_stats *stats);
+/* after fm3d_pipeline_run(_dlt): the compacted matches (K), the inlier points (P x 3 doubles, the
+   z-filtered triangulation in match order) and each point's match index (P); any may be NULL */
+int fm3d_pipeline_dlt_download(fm3d_ctx *ctx, fm3d_dmatch *matches, double *points, int32_t *matchIdx);
 /* copy n records from a device record buffer (NULL = internal) to host */
 int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, fm3d_record *out);
 
