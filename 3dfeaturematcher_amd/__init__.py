@@ -35,7 +35,8 @@ EXPORTS = (
     "fm3d_get_pyramid_level", "fm3d_optimize_normals", "fm3d_pipeline_upload", "fm3d_pipeline_run",
     "fm3d_records_download", "fm3d_pyrdown", "fm3d_neighborhood", "fm3d_undistort", "fm3d_version",
     "fm3d_gravity", "fm3d_features_frames", "fm3d_patch_size", "fm3d_export_patches", "fm3d_square_neighborhoods",
-    "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches", "fm3d_extract_descriptors_from_patches_any", "fm3d_pipeline_run_dlt", "fm3d_pipeline_dlt_download",
+    "fm3d_circular_neighborhoods", "fm3d_surf_detect", "fm3d_surf_compute", "fm3d_extract_descriptors_from_patches", "fm3d_extract_descriptors_from_patches_any", "fm3d_pipeline_run_dlt", "fm3d_pipeline_dlt_download", "fm3d_pipeline_run_ncc",
+    "fm3d_pipeline_ncc_download",
     "fm3d_orb_detect", "fm3d_orb_compute", "fm3d_orb_set_pattern", "fm3d_sift_detect", "fm3d_sift_compute",
     "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_star_detect", "fm3d_brisk_compute", "fm3d_star_responses", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
@@ -810,6 +811,23 @@ class Pipeline:
         st = PipelineStats()
         self.ctx.check(lib().fm3d_pipeline_run_dlt(self.ctx.handle, ctypes.byref(n), ctypes.byref(st)))
         return n.value, st.as_dict()
+
+    def run_ncc(self, hphi: int = 4, htheta: int = 4, span: float = 0.4):
+        """C3's path: match -> NNDR -> triangulate -> NCC scoring of hphi x htheta normals per inlier;
+        returns (n_points, stats dict)"""
+        n = ctypes.c_int(0)
+        st = PipelineStats()
+        self.ctx.check(lib().fm3d_pipeline_run_ncc(self.ctx.handle, hphi, htheta, ctypes.c_double(span), ctypes.byref(n),
+                                                   ctypes.byref(st)))
+        return n.value, st.as_dict()
+
+    def ncc_results(self, n_points: int, H: int):
+        """(scores (P, H), best normals (P, 3), best index (P,)) of the last run_ncc"""
+        sc = np.zeros((max(n_points, 1), H))
+        nr = np.zeros((max(n_points, 1), 3))
+        b = np.zeros(max(n_points, 1), dtype=np.int32)
+        self.ctx.check(lib().fm3d_pipeline_ncc_download(self.ctx.handle, _vp(sc), _vp(nr), _ptr(b, ctypes.c_int32)))
+        return sc[:n_points], nr[:n_points], b[:n_points]
 
     def dlt_results(self, n_matches: int, n_inliers: int):
         """(matches (K,) DMATCH, inlier points (P, 3), match index of each point) of the last run"""

@@ -87,6 +87,9 @@ struct fm3d_ctx {
     DevBuf brImg, brSum, brKp, brIdx, brPat, brPairs, brDesc;
     // STAR detection
     DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut, starWork;
+    // NCC hypotheses over the pipeline's inliers (fm3d_pipeline_run_ncc)
+    DevBuf nccS, nccN, nccB;
+    int nccH = 0;
     DevBuf bPairs;            // the f32 train rows in interleaved pairs
     DevBuf f32Work;           // the bf16 MFMA prefilter's scratch (rows, norms, bounds, candidates)
     int nCU = 0;
@@ -1878,6 +1881,85 @@ int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats
         hipEventElapsedTime(&ms, ev[2], ev[1]);
         stats->total_ms = ms;
     }
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* nPoints, fm3d_pipeline_stats* stats) {
+    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    if (Hphi <= 0 || Htheta <= 0 || Hphi * Htheta > 32) return fail(c, FM3D_ERR_INVALID, "1 <= Hphi * Htheta <= 32");
+    if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "fm3d_set_g12 / fm3d_setg12 not called");
+    hipSetDevice(c->device);
+    hipEvent_t* ev = c->ev;
+    int r, K = 0, P = 0;
+    if ((r = pipeline_front(c, K, P))) return r;
+    c->stK = K;
+    c->stP = P;
+    const int H = Hphi * Htheta;
+    c->nccH = H;
+    HIPCHK(c, hipEventRecord(ev[6], c->stream));
+    if (P > 0) {
+        if ((r = ensure_offsets(c))) return r;
+        HIPCHK(c, c->nccS.ensure((size_t)P * H * sizeof(double)));
+        HIPCHK(c, c->nccN.ensure((size_t)P * 3 * sizeof(double)));
+        HIPCHK(c, c->nccB.ensure((size_t)P * sizeof(int)));
+        fm3d::NccParams p{};
+        p.points = c->pts.as<double>();
+        p.P = P;
+        p.cam = c->cam;
+        std::memcpy(p.R2, c->R2, sizeof(p.R2));
+        std::memcpy(p.t2, c->t2, sizeof(p.t2));
+        p.img1 = c->pyr1[0].as<uint8_t>();
+        p.img2 = c->pyr2[0].as<uint8_t>();
+        p.w = c->lw[0];
+        p.h = c->lh[0];
+        p.offsets = c->offsets.as<int2>();
+        p.nOff = c->nOff;
+        p.nOffPad = c->nOffPad;
+        p.boundW = c->s.boundWidth;
+        p.boundH = c->s.boundHeight;
+        p.cmax = (int)(2 * c->s.zThresholdMax);
+        p.Hphi = Hphi;
+        p.Htheta = Htheta;
+        p.span = span;
+        p.scores = c->nccS.as<double>();
+        p.normals = c->nccN.as<double>();
+        p.best = c->nccB.as<int>();
+        fm3d::launch_ncc_hypotheses(p, c->stream);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipEventRecord(ev[7], c->stream));
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nPoints) *nPoints = P;
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->queries = c->stNA;
+        stats->trains = c->stNB;
+        stats->matches = K;
+        stats->inliers = P;
+        stats->kept = P;
+        float ms;
+        hipEventElapsedTime(&ms, ev[2], ev[3]);
+        stats->match_ms = ms;
+        hipEventElapsedTime(&ms, ev[3], ev[4]);
+        stats->nndr_ms = ms;
+        hipEventElapsedTime(&ms, ev[4], ev[5]);
+        stats->triangulate_ms = ms;
+        hipEventElapsedTime(&ms, ev[6], ev[7]);
+        stats->lm_ms = ms;  // the normal stage: here the NCC scoring
+        hipEventElapsedTime(&ms, ev[2], ev[1]);
+        stats->total_ms = ms;
+    }
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_ncc_download(fm3d_ctx* c, double* scores, double* normals, int32_t* best) {
+    if (!c || !c->staged) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    const size_t P = (size_t)c->stP;
+    if (P && scores) HIPCHK(c, hipMemcpy(scores, c->nccS.p, P * c->nccH * sizeof(double), hipMemcpyDeviceToHost));
+    if (P && normals) HIPCHK(c, hipMemcpy(normals, c->nccN.p, P * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    if (P && best) HIPCHK(c, hipMemcpy(best, c->nccB.p, P * sizeof(int), hipMemcpyDeviceToHost));
     return FM3D_OK;
 }
 

@@ -50,7 +50,8 @@ FP64_PEAK_NO_FMA = 39.3     # the same issue rate for 1-flop instructions (-ffp-
 HBM_PEAK_GBS = 8000.0
 WORKLOADS = {"c4": dict(keypoints=100_000, width=640, height=480),
              "c5": dict(keypoints=1_000_000, width=640, height=480),
-             "c2": dict(keypoints=10_000, width=640, height=480)}
+             "c2": dict(keypoints=10_000, width=640, height=480),
+             "c3": dict(keypoints=10_000, width=640, height=480)}
 INT8_PEAK_TOPS = 5000.0      # MI355X dense int8 MFMA (2x the ~2.5 PFLOP/s dense bf16; MI355X_MICROARCH.md)
 
 
@@ -59,9 +60,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("auto", "c4", "c5", "c2"), default="auto",
+    ap.add_argument("--workload", choices=("auto", "c4", "c5", "c2", "c3"), default="auto",
                     help="auto: C4 at one GPU, C5 (one sharded 1M-keypoint frame pair) at N > 1; c2: BASELINE's "
-                         "C2 (10k SIFT per frame, match + DLT triangulate only, one GPU)")
+                         "C2 (10k SIFT per frame, match + DLT triangulate only, one GPU); c3: BASELINE's C3 as "
+                         "worded (10k ORB, Hamming match + DLT + 64x64-patch NCC over 16 normal hypotheses)")
     ap.add_argument("--weak", action="store_true", help="every rank its own C4 frame pair (weak scaling)")
     ap.add_argument("--keypoints", type=int, default=0)
     ap.add_argument("--width", type=int, default=0)
@@ -101,6 +103,8 @@ def main():
         workload = "c4"
     if workload == "c2":
         return run_c2(args)
+    if workload == "c3":
+        return run_c3(args)
     wl = dict(WORKLOADS[workload])
     for k in ("keypoints", "width", "height"):
         if getattr(args, k):
@@ -338,6 +342,105 @@ def run_c2(args):
         "verified": verified,
         "verification": "matches (query, train, distance) and inlier points byte-equal to the cpu_baseline "
                         "leg's oracle outputs",
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+def run_c3(args):
+    """BASELINE.json configs[2] (C3) as worded: 10k ORB-256 keypoints per 640x480 frame, Hamming match
+    + NNDR 0.8 + DLT, then the NCC scoring of 16 candidate normals (4 x 4, half width 0.4 rad) over the
+    pixelsRay-32 neighbourhood (64 x 64) of every inlier -- fm3d_pipeline_run_ncc on HBM-resident
+    inputs.  The value is the NCC-scored inliers per second; the roofline is ncc_kernel's (fp64 VALU,
+    counted with the LM's 91 flops per pixel evaluation of the same geometry and sampling).  The
+    cpu_baseline leg runs the oracle's whole C3 path and its outputs check every score."""
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    synth = importlib.import_module("3dfeaturematcher_amd.synth")
+    wl = dict(WORKLOADS["c3"])
+    for k in ("keypoints", "width", "height"):
+        if getattr(args, k):
+            wl[k] = getattr(args, k)
+    nndr = 0.8 if args.nndr == 0.55 else args.nndr  # C3's ORB rows: the 0.8 ratio (0.55 is C4's SIFT)
+    ray = 32 if args.ray == 64 else args.ray
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=102, desc="orb")
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon = nndr
+    s.pixelsRay = ray
+    ctx = fm3d.Context(s)
+    sct = fm3d.SingleCameraTriangulator(ctx)
+    sct.set_g12(pair.g12)
+    pipe = fm3d.Pipeline(ctx)
+    pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2, binary=True)
+    for _ in range(args.warmup):
+        pipe.run_ncc(4, 4, 0.4)
+    stats = []
+    t0 = time.perf_counter()
+    total = 0
+    for _ in range(args.steps):
+        n, st = pipe.run_ncc(4, 4, 0.4)
+        total += n
+        stats.append(st)
+    elapsed = time.perf_counter() - t0
+    last = stats[-1]
+    P = int(last["inliers"])
+    sc, nb, best = pipe.ncc_results(P, 16)
+    _, pts, _ = pipe.dlt_results(int(last["matches"]), P)
+    ctx.close()
+    cpu, verified = None, None
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as orc
+        quota = cpu_quota()
+        cores = len(os.sched_getaffinity(0))
+        if quota:
+            cores = max(1, min(cores, int(quota)))
+        t1 = time.perf_counter()
+        q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.BITS, nndr, cores)
+        opts, _ = orc.triangulate(pair.cam, pair.g12, s.zThresholdMin, s.zThresholdMax, pair.kp1, pair.kp2, q, t)
+        R2, t2 = orc.camera2_from_g12(pair.g12)
+        rs, rn, rb = orc.ncc_hypotheses(pair.cam, R2, t2, pair.img1, pair.img2, opts, ray, 4, 4, 0.4,
+                                        bound=(s.boundWidth, s.boundHeight), zmax=s.zThresholdMax)
+        el = time.perf_counter() - t1
+        cpu = {"value": len(opts) / el, "unit": "keypoints/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
+               "sample": f"the whole C3 frame pair: oracle Hamming knn2 + NNDR + DLT + NCC of {len(opts)} points "
+                         f"x 16 hypotheses, {el:.2f} s"}
+        verified = bool(np.array_equal(pts, opts) and np.array_equal(sc, rs) and np.array_equal(best, rb) and
+                        np.array_equal(nb, rn, equal_nan=True))
+    ncc_ms = float(np.mean([x["lm_ms"] for x in stats]))
+    m_dat = sum(1 for i in range(-ray, ray + 1) for j in range(-ray, ray + 1) if i * i + j * j <= ray * ray)
+    pix = P * 16 * m_dat
+    achieved = FLOPS_PER_PIXEL_EVAL * pix / (ncc_ms * 1e-3) / 1e12 if ncc_ms > 0 else 0.0
+    out = {
+        "metric": "matched+triangulated+NCC-scored keypoints/sec (BASELINE C3: Hamming match + 64x64 patch NCC "
+                  "over 16 normal hypotheses)",
+        "value": total / elapsed, "unit": "keypoints/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (ray-cast facet scene, seeded; 3dfeaturematcher_amd/synth.py)",
+        "config": {"workload": f"C3: {wl['keypoints'] // 1000}k ORB-256 keypoints per {wl['width']}x{wl['height']} frame "
+                               f"pair, Hamming knnMatch k=2 + NNDR {nndr} + DLT + NCC of 4 x 4 normals (span 0.4 rad) "
+                               f"over the pixelsRay-{ray} neighbourhood",
+                   "keypoints_per_frame": wl["keypoints"], "parallelism": "1 GPU",
+                   "timed": "match -> NNDR -> DLT -> NCC scoring on HBM-resident inputs (scores stay on the device)"},
+        "roofline": {"kernel": "fm3d::ncc_kernel (NCC over candidate normals)", "bound": "fp64-valu",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "algorithmic": f"{FLOPS_PER_PIXEL_EVAL} flop per pixel evaluation (the LM's count for the "
+                                    f"same geometry + bilinear sample) x {P} points x 16 hypotheses x {m_dat} "
+                                    f"neighbourhood pixels (image-bounded pixels count too)",
+                     "avg_launch_ms": ncc_ms},
+        "cpu_baseline": cpu,
+        "stages_ms": {"match_ms": last["match_ms"], "nndr_ms": last["nndr_ms"], "triangulate_ms": last["triangulate_ms"],
+                      "ncc_ms": last["lm_ms"], "total_ms": last["total_ms"]},
+        "counts": {"queries": int(last["queries"]), "matches": int(last["matches"]), "inliers": P,
+                   "scored": int((best >= 0).sum())},
+        "verified": verified,
+        "verification": "inlier points, all 16 scores per point, best index and best normal byte-equal to the "
+                        "cpu_baseline leg's oracle outputs",
     }
     line = json.dumps(out)
     print(line, flush=True)

@@ -413,6 +413,13 @@ int fm3d_pipeline_run_dlt(fm3d_ctx *ctx, int *nInliers, fm3d_pipeline_stats *sta
 /* after fm3d_pipeline_run(_dlt): the compacted matches (K), the inlier points (P x 3 doubles, the
    z-filtered triangulation in match order) and each point's match index (P); any may be NULL */
 int fm3d_pipeline_dlt_download(fm3d_ctx *ctx, fm3d_dmatch *matches, double *points, int32_t *matchIdx);
+/* BASELINE.json's C3 as worded ("Hamming popcount match + 64x64 patch NCC over 16 normal hypotheses"):
+   match -> NNDR -> triangulate, then fm3d_ncc_hypotheses' scoring of every inlier on the device
+   (pixelsRay 32 gives the 64 x 64 neighbourhood); *nPoints = inliers scored; stats.lm_ms is the NCC
+   kernel's time.  Needs the camera-2 pose (fm3d_set_g12).  Results via fm3d_pipeline_ncc_download
+   (scores P x H, best normals P x 3, best index P; any may be NULL). */
+int fm3d_pipeline_run_ncc(fm3d_ctx *ctx, int Hphi, int Htheta, double span, int *nPoints, fm3d_pipeline_stats *stats);
+int fm3d_pipeline_ncc_download(fm3d_ctx *ctx, double *scores, double *normals, int32_t *best);
 /* copy n records from a device record buffer (NULL = internal) to host */
 int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, fm3d_record *out);
 

@@ -37,3 +37,32 @@ def test_pipeline_dlt_bitwise(fm3d, orc, synth, n, seed):
     assert np.array_equal(pts, opts) and np.array_equal(src, np.flatnonzero(mask))
     assert P2 == P and np.array_equal(pts2, pts)
     assert np.array_equal(m3, m) and np.array_equal(pts3, pts) and np.array_equal(src3, src) and kept <= P
+
+
+def test_pipeline_ncc_bitwise(fm3d, orc, synth):
+    """BASELINE's C3 as worded through the pipeline (fm3d_pipeline_run_ncc): Hamming match -> NNDR ->
+    DLT -> NCC of 4 x 4 normals at pixelsRay 32, every inlier's scores against the oracle on a sample"""
+    fp = synth.make_frame_pair(10_000, seed=102, desc="orb")
+    s = fm3d.Settings.default()
+    s.set_camera(fp.cam)
+    s.nndrEpsilon, s.pixelsRay = 0.8, 32
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(fp.g12)
+        R2, t2 = sct.camera2()
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2, binary=True)
+        P, st = pipe.run_ncc(4, 4, 0.4)
+        sc, nb, b = pipe.ncc_results(P, 16)
+        _, pts, _ = pipe.dlt_results(st["matches"], P)
+    finally:
+        ctx.close()
+    q, t, _ = orc.match_nndr(fp.desc1, fp.desc2, orc.BITS, 0.8, oracle_threads())
+    opts, _ = orc.triangulate(fp.cam, fp.g12, s.zThresholdMin, s.zThresholdMax, fp.kp1, fp.kp2, q, t)
+    assert P == len(opts) > 5000 and np.array_equal(pts, opts)
+    sel = np.sort(np.random.default_rng(34).choice(P, 800, replace=False))
+    rs, rn, rb = orc.ncc_hypotheses(fp.cam, R2, t2, fp.img1, fp.img2, opts[sel], 32, 4, 4, 0.4,
+                                    bound=(s.boundWidth, s.boundHeight), zmax=s.zThresholdMax)
+    assert np.array_equal(sc[sel], rs) and np.array_equal(b[sel], rb) and np.array_equal(nb[sel], rn, equal_nan=True)
+    assert (b >= 0).mean() > 0.3
