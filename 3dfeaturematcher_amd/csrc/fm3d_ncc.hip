@@ -12,8 +12,9 @@
 //   * per normal the evaluateNormal geometry (:65-149 through :421-470, :591-665): ray-plane
 //     intersection, bounding box, camera-2 projection, isPixelGood, image-2 sample; any failing pixel
 //     (or a flat patch) gives the score -2, else NCC(I1, I2) over the m_dat pixels.
-// One 256-thread workgroup per point: wave w scores hypotheses w, w+4, ...; lane l sums the entries
-// of offset index = l (mod 64) in order, then a fixed xor tree over the wave (the oracle's order).
+// One 256-thread workgroup per point: the rays and image-1 samples of 256 entries at a time in LDS
+// (each computed once, not once per wave); wave w scores hypotheses w, w+4, ...; lane l sums the
+// entries of offset index = l (mod 64) in order, then a fixed xor tree over the wave (the oracle's order).
 #include <hip/hip_runtime.h>
 
 #include "fm3d_device.h"
@@ -57,56 +58,84 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
             nh = k + 1;
         }
     }
-    double Sa[kNccMaxPerWave], Sb[kNccMaxPerWave], Saa[kNccMaxPerWave], Sbb[kNccMaxPerWave], Sab[kNccMaxPerWave];
+    // the image-1 sums are the same for every hypothesis that scores: one that fails anywhere scores -2
+    // whatever its sums, and one that never fails takes every in-bounds pixel, in the same order
+    double Sa = 0., Saa = 0.;
+    double Sb[kNccMaxPerWave], Sbb[kNccMaxPerWave], Sab[kNccMaxPerWave];
     bool bad[kNccMaxPerWave];
     for (int k = 0; k < kNccMaxPerWave; k++) {
-        Sa[k] = Sb[k] = Saa[k] = Sbb[k] = Sab[k] = 0.;
+        Sb[k] = Sbb[k] = Sab[k] = 0.;
         bad[k] = false;
     }
-    bool bad1 = false;
     int m = 0;
     const double cm = (double)p.cmax;
     const double xmax = (double)p.w, ymax = (double)p.h;  // isPixelGood at scale 1
-    for (int e = lane; e < p.nOffPad; e += 64) {
-        const int2 o = p.offsets[e];
-        const double px = ccx + (double)o.x, py = ccy + (double)o.y;
-        const bool in = e < p.nOff && !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
-        if (!in) continue;
-        m++;
-        double ux, uy;
-        undistort1(p.cam, px, py, ux, uy);
+    // the hypothesis-independent part of a pixel (its undistorted ray and image-1 sample) once per
+    // workgroup, 256 entries at a time in LDS; lane l of every wave then takes the entries l, l + 64,
+    // l + 128, l + 192 of each chunk -- the same entries in the same order as a lane-strided scan
+    __shared__ double Rx[256], Ry[256];
+    __shared__ float A1[256];
+    __shared__ int OK[256];
+    __shared__ int anyBad1S;
+    if (threadIdx.x == 0) anyBad1S = 0;
+    __syncthreads();
+    for (int base = 0; base < p.nOffPad; base += 256) {
+        const int e = base + threadIdx.x;
+        int in = 0;
+        double ux = 0., uy = 0.;
         float I1 = 0.f;
-        if (!pixel_good_b(px, py, xmax, ymax))
-            bad1 = true;
-        else
-            I1 = bilinear(p.img1, p.w, (float)px, (float)py);
-        const double a = (double)I1;
-        for (int k = 0; k < nh; k++) {
-            const double nn = n0[k] * ux + n1[k] * uy + n2[k] * 1.;
-            const double kk = mm[k] / nn;
-            const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-            const bool inbox = (P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm);  // NaN fails
-            double u, v;
-            project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
-            if (!inbox || !pixel_good_b(u, v, xmax, ymax)) {
-                bad[k] = true;
-                continue;
+        if (e < p.nOffPad) {
+            const int2 o = p.offsets[e];
+            const double px = ccx + (double)o.x, py = ccy + (double)o.y;
+            in = e < p.nOff && !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+            if (in) {
+                undistort1(p.cam, px, py, ux, uy);
+                if (!pixel_good_b(px, py, xmax, ymax))
+                    anyBad1S = 1;  // the same value from any thread
+                else
+                    I1 = bilinear(p.img1, p.w, (float)px, (float)py);
             }
-            const double b = (double)bilinear(p.img2, p.w, (float)u, (float)v);
-            Sa[k] += a;
-            Sb[k] += b;
-            Saa[k] += a * a;
-            Sbb[k] += b * b;
-            Sab[k] += a * b;
         }
+        Rx[threadIdx.x] = ux;
+        Ry[threadIdx.x] = uy;
+        A1[threadIdx.x] = I1;
+        OK[threadIdx.x] = in;
+        __syncthreads();
+        for (int j = 0; j < 4; j++) {
+            const int t = lane + 64 * j;
+            if (base + t >= p.nOffPad) break;
+            if (!OK[t]) continue;
+            m++;
+            const double ux = Rx[t], uy = Ry[t];
+            const double a = (double)A1[t];
+            Sa += a;
+            Saa += a * a;
+            for (int k = 0; k < nh; k++) {
+                const double nn = n0[k] * ux + n1[k] * uy + n2[k] * 1.;
+                const double kk = mm[k] / nn;
+                const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+                const bool inbox = (P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm);  // NaN fails
+                double u, v;
+                project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
+                if (!inbox || !pixel_good_b(u, v, xmax, ymax)) {
+                    bad[k] = true;
+                    continue;
+                }
+                const double b = (double)bilinear(p.img2, p.w, (float)u, (float)v);
+                Sb[k] += b;
+                Sbb[k] += b * b;
+                Sab[k] += a * b;
+            }
+        }
+        __syncthreads();
     }
     for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o);
-    const bool anyBad1 = __any(bad1);
+    const bool anyBad1 = anyBad1S != 0;
     __shared__ double score[32];
+    const double sa = xor_sum(Sa), saa = xor_sum(Saa);
     for (int k = 0; k < nh; k++) {
         const bool fail = anyBad1 || __any(bad[k]);
-        const double sa = xor_sum(Sa[k]), sb = xor_sum(Sb[k]), saa = xor_sum(Saa[k]), sbb = xor_sum(Sbb[k]),
-                     sab = xor_sum(Sab[k]);
+        const double sb = xor_sum(Sb[k]), sbb = xor_sum(Sbb[k]), sab = xor_sum(Sab[k]);
         if (lane == 0) {
             double s = -2.;
             if (!fail && m > 0) {
