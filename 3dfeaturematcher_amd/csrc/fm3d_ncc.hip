@@ -32,6 +32,9 @@ __device__ __forceinline__ double xor_sum(double v) {
     return v;
 }
 
+// KPW: hypotheses per wave the register arrays hold (H <= 4 * KPW); sized to H so that 16 hypotheses
+// keep 4 per wave in registers (225 VGPRs at 8, 2 waves per SIMD)
+template <int KPW>
 __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     const int pt = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (pt >= p.P) return;
@@ -46,8 +49,8 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     const double theta0 = fm3d_atan2(g2, sqrt(g0 * g0 + g1 * g1)), phi0 = fm3d_atan2(g1, g0);
     const int H = p.Hphi * p.Htheta;
     int nh = 0;
-    double n0[kNccMaxPerWave], n1[kNccMaxPerWave], n2[kNccMaxPerWave], mm[kNccMaxPerWave];
-    for (int k = 0; k < kNccMaxPerWave; k++) {
+    double n0[KPW], n1[KPW], n2[KPW], mm[KPW];
+    for (int k = 0; k < KPW; k++) {
         const int h = wave + 4 * k;
         if (h < H) {
             const int ip = h / p.Htheta, it = h - ip * p.Htheta;
@@ -61,9 +64,9 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     // the image-1 sums are the same for every hypothesis that scores: one that fails anywhere scores -2
     // whatever its sums, and one that never fails takes every in-bounds pixel, in the same order
     double Sa = 0., Saa = 0.;
-    double Sb[kNccMaxPerWave], Sbb[kNccMaxPerWave], Sab[kNccMaxPerWave];
-    bool bad[kNccMaxPerWave];
-    for (int k = 0; k < kNccMaxPerWave; k++) {
+    double Sb[KPW], Sbb[KPW], Sab[KPW];
+    bool bad[KPW];
+    for (int k = 0; k < KPW; k++) {
         Sb[k] = Sbb[k] = Sab[k] = 0.;
         bad[k] = false;
     }
@@ -173,7 +176,13 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
 
 void launch_ncc_hypotheses(const NccParams& p, hipStream_t s) {
     if (p.P <= 0) return;
-    ncc_kernel<<<p.P, 256, 0, s>>>(p);
+    const int H = p.Hphi * p.Htheta;
+    if (H <= 8)
+        ncc_kernel<2><<<p.P, 256, 0, s>>>(p);
+    else if (H <= 16)
+        ncc_kernel<4><<<p.P, 256, 0, s>>>(p);
+    else
+        ncc_kernel<kNccMaxPerWave><<<p.P, 256, 0, s>>>(p);
 }
 
 }  // namespace fm3d
