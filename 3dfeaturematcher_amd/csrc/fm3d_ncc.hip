@@ -34,7 +34,7 @@ __device__ __forceinline__ double xor_sum(double v) {
 
 // KPW: hypotheses per wave the register arrays hold (H <= 4 * KPW); sized to H so that 16 hypotheses
 // keep 4 per wave in registers (225 VGPRs at 8, 2 waves per SIMD)
-template <int KPW>
+template <int KPW, bool FULL>
 __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     const int pt = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (pt >= p.P) return;
@@ -113,7 +113,10 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
             const double a = (double)A1[t];
             Sa += a;
             Saa += a * a;
-            for (int k = 0; k < nh; k++) {
+            const int nk = FULL ? KPW : nh;  // FULL: H == 4 * KPW, every wave holds KPW hypotheses
+#pragma unroll
+            for (int k = 0; k < KPW; k++) {
+                if (k >= nk) break;
                 const double nn = n0[k] * ux + n1[k] * uy + n2[k] * 1.;
                 const double kk = mm[k] / nn;
                 const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
@@ -177,12 +180,16 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
 void launch_ncc_hypotheses(const NccParams& p, hipStream_t s) {
     if (p.P <= 0) return;
     const int H = p.Hphi * p.Htheta;
-    if (H <= 8)
-        ncc_kernel<2><<<p.P, 256, 0, s>>>(p);
+    if (H == 16)
+        ncc_kernel<4, true><<<p.P, 256, 0, s>>>(p);
+    else if (H == 32)
+        ncc_kernel<kNccMaxPerWave, true><<<p.P, 256, 0, s>>>(p);
+    else if (H <= 8)
+        ncc_kernel<2, false><<<p.P, 256, 0, s>>>(p);
     else if (H <= 16)
-        ncc_kernel<4><<<p.P, 256, 0, s>>>(p);
+        ncc_kernel<4, false><<<p.P, 256, 0, s>>>(p);
     else
-        ncc_kernel<kNccMaxPerWave><<<p.P, 256, 0, s>>>(p);
+        ncc_kernel<kNccMaxPerWave, false><<<p.P, 256, 0, s>>>(p);
 }
 
 }  // namespace fm3d
