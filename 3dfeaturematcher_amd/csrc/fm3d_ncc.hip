@@ -26,6 +26,7 @@ namespace fm3d {
 namespace {
 
 constexpr int kNccMaxPerWave = 8;  // hypotheses per wave (H <= 32)
+constexpr int kNccChunk = 512;     // neighbourhood entries staged in LDS at a time
 
 __device__ __forceinline__ double xor_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -74,37 +75,39 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     const double cm = (double)p.cmax;
     const double xmax = (double)p.w, ymax = (double)p.h;  // isPixelGood at scale 1
     // the hypothesis-independent part of a pixel (its undistorted ray and image-1 sample) once per
-    // workgroup, 256 entries at a time in LDS; lane l of every wave then takes the entries l, l + 64,
-    // l + 128, l + 192 of each chunk -- the same entries in the same order as a lane-strided scan
-    __shared__ double Rx[256], Ry[256];
-    __shared__ float A1[256];
-    __shared__ int OK[256];
+    // workgroup, kNccChunk entries at a time in LDS; lane l of every wave then takes the entries l,
+    // l + 64, l + 128, ... of each chunk -- the same entries in the same order as a lane-strided scan
+    __shared__ double Rx[kNccChunk], Ry[kNccChunk];
+    __shared__ float A1[kNccChunk];
+    __shared__ int OK[kNccChunk];
     __shared__ int anyBad1S;
     if (threadIdx.x == 0) anyBad1S = 0;
     __syncthreads();
-    for (int base = 0; base < p.nOffPad; base += 256) {
-        const int e = base + threadIdx.x;
-        int in = 0;
-        double ux = 0., uy = 0.;
-        float I1 = 0.f;
-        if (e < p.nOffPad) {
-            const int2 o = p.offsets[e];
-            const double px = ccx + (double)o.x, py = ccy + (double)o.y;
-            in = e < p.nOff && !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
-            if (in) {
-                undistort1(p.cam, px, py, ux, uy);
-                if (!pixel_good_b(px, py, xmax, ymax))
-                    anyBad1S = 1;  // the same value from any thread
-                else
-                    I1 = bilinear(p.img1, p.w, (float)px, (float)py);
+    for (int base = 0; base < p.nOffPad; base += kNccChunk) {
+        for (int r = 0; r < kNccChunk / 256; r++) {
+            const int sl = threadIdx.x + 256 * r, e = base + sl;
+            int in = 0;
+            double ux = 0., uy = 0.;
+            float I1 = 0.f;
+            if (e < p.nOffPad) {
+                const int2 o = p.offsets[e];
+                const double px = ccx + (double)o.x, py = ccy + (double)o.y;
+                in = e < p.nOff && !(px < 0 || py < 0 || px >= p.boundW || py >= p.boundH);
+                if (in) {
+                    undistort1(p.cam, px, py, ux, uy);
+                    if (!pixel_good_b(px, py, xmax, ymax))
+                        anyBad1S = 1;  // the same value from any thread
+                    else
+                        I1 = bilinear(p.img1, p.w, (float)px, (float)py);
+                }
             }
+            Rx[sl] = ux;
+            Ry[sl] = uy;
+            A1[sl] = I1;
+            OK[sl] = in;
         }
-        Rx[threadIdx.x] = ux;
-        Ry[threadIdx.x] = uy;
-        A1[threadIdx.x] = I1;
-        OK[threadIdx.x] = in;
         __syncthreads();
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < kNccChunk / 64; j++) {
             const int t = lane + 64 * j;
             if (base + t >= p.nOffPad) break;
             if (!OK[t]) continue;
