@@ -41,7 +41,8 @@ EXPORTS = (
     "fm3d_sift_pyramid", "fm3d_fast_detect", "fm3d_star_detect", "fm3d_brisk_compute", "fm3d_star_responses", "fm3d_detect", "fm3d_descriptor_info", "fm3d_compute",
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
-    "fm3d_plane_to_image2",
+    "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
+    "fm3d_mgpu_submit", "fm3d_mgpu_wait",
 )
 
 
@@ -805,6 +806,33 @@ class Pipeline:
                                                ctypes.byref(n), ctypes.byref(st)))
         return n.value, st.as_dict()
 
+    def submit(self, desc_a, desc_b, kp1, kp2, img1, img2, binary=False, query_offset=0):
+        """fm3d_pipeline_submit: stage one frame pair (H2D through pinned buffers, pyramids) and queue the
+        whole path on the context stream without waiting.  The arrays are copied before it returns."""
+        a = np.ascontiguousarray(desc_a)
+        b = np.ascontiguousarray(desc_b)
+        k1 = np.ascontiguousarray(kp1, dtype=np.float32)
+        k2 = np.ascontiguousarray(kp2, dtype=np.float32)
+        i1 = np.ascontiguousarray(img1, dtype=np.uint8)
+        i2 = np.ascontiguousarray(img2, dtype=np.uint8)
+        h, w = i1.shape
+        self.n_queries = a.shape[0]
+        self.ctx.check(lib().fm3d_pipeline_submit(self.ctx.handle, _vp(a), a.shape[0], _vp(b), b.shape[0],
+                                                  a.shape[1], _desc_type(a, binary), _vp(k1), _vp(k2),
+                                                  _ptr(i1, ctypes.c_uint8), _ptr(i2, ctypes.c_uint8), w, h,
+                                                  query_offset))
+
+    def wait(self, out: np.ndarray | None = None):
+        """fm3d_pipeline_wait: (survivor records (host), stats dict) of the submitted frame pair.  out: a
+        RECORD array with room for n_queries records (reused across calls), or None to allocate."""
+        if out is None:
+            out = np.zeros(max(self.n_queries, 1), dtype=RECORD)
+        n = ctypes.c_int(0)
+        st = PipelineStats()
+        self.ctx.check(lib().fm3d_pipeline_wait(self.ctx.handle, _vp(out), len(out), ctypes.byref(n),
+                                                ctypes.byref(st)))
+        return out[:n.value], st.as_dict()
+
     def run_dlt(self):
         """C2's path: match -> NNDR -> triangulate only; returns (n_inliers, stats dict)"""
         n = ctypes.c_int(0)
@@ -905,6 +933,29 @@ class MultiGPU:
         self.check(lib().fm3d_mgpu_pipeline_upload(self._h, _vp(a), a.shape[0], _vp(b), b.shape[0], a.shape[1],
                                                    _desc_type(a, binary), _vp(k1), _vp(k2), _ptr(i1, ctypes.c_uint8),
                                                    _ptr(i2, ctypes.c_uint8), w, h))
+
+    def submit(self, desc_a, desc_b, kp1, kp2, img1, img2, binary=False):
+        """fm3d_mgpu_submit: one frame pair staged on every device and queued (two may be in flight)."""
+        a = np.ascontiguousarray(desc_a)
+        b = np.ascontiguousarray(desc_b)
+        k1 = np.ascontiguousarray(kp1, dtype=np.float32)
+        k2 = np.ascontiguousarray(kp2, dtype=np.float32)
+        i1 = np.ascontiguousarray(img1, dtype=np.uint8)
+        i2 = np.ascontiguousarray(img2, dtype=np.uint8)
+        h, w = i1.shape
+        self.n_queries = a.shape[0]
+        self.check(lib().fm3d_mgpu_submit(self._h, _vp(a), a.shape[0], _vp(b), b.shape[0], a.shape[1],
+                                          _desc_type(a, binary), _vp(k1), _vp(k2), _ptr(i1, ctypes.c_uint8),
+                                          _ptr(i2, ctypes.c_uint8), w, h))
+
+    def wait(self, out: np.ndarray | None = None):
+        """fm3d_mgpu_wait: (merged records of the oldest submitted pair, stats dict)."""
+        if out is None:
+            out = np.zeros(max(self.n_queries, 1), dtype=RECORD)
+        n = ctypes.c_int(0)
+        st = PipelineStats()
+        self.check(lib().fm3d_mgpu_wait(self._h, _vp(out), len(out), ctypes.byref(n), ctypes.byref(st)))
+        return out[:n.value], st.as_dict()
 
     def run(self):
         """One pass over all devices: (records in query order, stats dict)."""

@@ -51,6 +51,38 @@ struct DevBuf {
 
 constexpr size_t kGuard(int w) { return (size_t)4 * w + 64; }
 
+// page-locked host staging (hipHostMalloc): the H2D copies of the inputs run asynchronously from
+// it, at full PCIe rate, and the host may return before they execute (fm3d_pipeline_submit)
+struct HostBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t alloc = n < 4096 ? 4096 : n;
+        hipError_t e = hipHostMalloc(&p, alloc, hipHostMallocDefault);
+        if (e == hipSuccess) bytes = alloc;
+        return e;
+    }
+    void release() {
+        if (p) hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const {
+        return (T*)p;
+    }
+};
+
+// the pipeline's small device -> host results of one frame pair (one D2H, pinned)
+struct PipeSmall {
+    int32_t cnt[4];                 // matches K, inliers P, kept, pad
+    unsigned long long lm[26];      // the LM kernel's counters (fm3d_lm2.hip statPass layout)
+};
+
 }  // namespace
 
 struct fm3d_ctx {
@@ -99,11 +131,20 @@ struct fm3d_ctx {
     DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, slab, slabI1;
     DevBuf records, recTmp, recFlag;
     DevBuf lmProj;  // camera-2 projection constants for the LM kernel (fm3d::ProjConst)
+    DevBuf pcnt;    // the pipeline's device counts: [0] matches K, [1] inliers P, [2] kept
+    // pinned staging: descriptors A / B (padded rows), keypoints, images, small tables, results
+    HostBuf hA, hB, hK1, hK2, hImg, hTab, hProj, hSmall;
+    hipEvent_t evStage = nullptr;  // after the last H2D copy from the staging buffers
+    hipEvent_t evProj = nullptr;   // after the last H2D copy of the LM constants (hProj)
+    bool pending = false;          // a fm3d_pipeline_submit awaiting fm3d_pipeline_wait
+    fm3d_lm_stats subLm{};         // the pending submit's LM launch data
+    fm3d_record* pendOut = nullptr;  // the device records of the pending / last run
     // staged pipeline inputs
     int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
     int stK = 0, stP = 0;  // matches and inliers of the last fm3d_pipeline_run_dlt
+    int nccP = 0;          // points of the last successful fm3d_pipeline_run_ncc (its score rows)
     bool staged = false;
-    hipEvent_t ev[8];
+    hipEvent_t ev[10];     // [0..1] standalone LM, [2..7] pipeline stages, [8] submit start, [1] end
     std::string err;
 };
 
@@ -295,23 +336,49 @@ bool f32_is_u8(const float* x, size_t n) {
     return true;
 }
 
-// pad rows of bytes to dimPad (multiple of 128) with value 128 (x - 128 == 0: no effect on d2)
-std::vector<uint8_t> pad_u8(const uint8_t* x, int n, int dim, int dimPad) {
-    std::vector<uint8_t> o((size_t)n * dimPad, 128);
-    for (int i = 0; i < n; i++) std::memcpy(&o[(size_t)i * dimPad], x + (size_t)i * dim, dim);
-    return o;
-}
-std::vector<uint8_t> f32_to_u8(const float* x, int n, int dim, int dimPad) {
-    std::vector<uint8_t> o((size_t)n * dimPad, 128);
-    for (int i = 0; i < n; i++)
-        for (int d = 0; d < dim; d++) o[(size_t)i * dimPad + d] = (uint8_t)x[(size_t)i * dim + d];
-    return o;
+// The staging buffers are refilled only after the H2D copies of the previous call out of them
+// have run (c->evStage, recorded after them on the context stream).
+int staging_wait(fm3d_ctx* c) {
+    HIPCHK(c, hipEventSynchronize(c->evStage));
+    return FM3D_OK;
 }
 
-// stage descriptors on the device; returns the effective kernel type
+// bytes from a host array to a device buffer through the pinned staging buffer h
+int upload_pinned(fm3d_ctx* c, DevBuf& dst, HostBuf& h, const void* src, size_t bytes) {
+    HIPCHK(c, dst.ensure(bytes));
+    if (!bytes) return FM3D_OK;
+    HIPCHK(c, h.ensure(bytes));
+    std::memcpy(h.p, src, bytes);
+    HIPCHK(c, hipMemcpyAsync(dst.p, h.p, bytes, hipMemcpyHostToDevice, c->stream));
+    return FM3D_OK;
+}
+
+// rows of bytes padded to dimPad (multiple of 128) with value 128 (x - 128 == 0: no effect on d2),
+// from u8 rows or from integer-valued f32 rows
+void pad_u8(uint8_t* o, const uint8_t* x, int n, int dim, int dimPad) {
+    if (dim == dimPad) {
+        std::memcpy(o, x, (size_t)n * dim);
+        return;
+    }
+    for (int i = 0; i < n; i++) {
+        std::memcpy(o + (size_t)i * dimPad, x + (size_t)i * dim, dim);
+        std::memset(o + (size_t)i * dimPad + dim, 128, dimPad - dim);
+    }
+}
+void f32_to_u8(uint8_t* o, const float* x, int n, int dim, int dimPad) {
+    for (int i = 0; i < n; i++) {
+        for (int d = 0; d < dim; d++) o[(size_t)i * dimPad + d] = (uint8_t)x[(size_t)i * dim + d];
+        std::memset(o + (size_t)i * dimPad + dim, 128, dimPad - dim);
+    }
+}
+
+// stage descriptors on the device (asynchronous H2D from the pinned staging buffers; the stream
+// orders every later use); returns the effective kernel type
 int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
                       int* effType, int* dimPad) {
     if (dim <= 0 || nA < 0 || nB < 0) return fail(c, FM3D_ERR_INVALID, "bad descriptor shape");
+    int r;
+    if ((r = staging_wait(c))) return r;
     int t = type;
     // integer-valued f32 rows take the u8 kernel only where it supports the width (padded <= 256)
     if (type == FM3D_DESC_F32 && ((dim + 127) / 128) * 128 <= 256 && f32_is_u8((const float*)descA, (size_t)nA * dim) &&
@@ -320,35 +387,45 @@ int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB,
     if (t == FM3D_DESC_U8) {
         int dp = ((dim + 127) / 128) * 128;
         if (dp > 256) return fail(c, FM3D_ERR_UNSUPPORTED, "u8 descriptors longer than 256 bytes");
-        std::vector<uint8_t> a = type == FM3D_DESC_F32 ? f32_to_u8((const float*)descA, nA, dim, dp)
-                                                        : pad_u8((const uint8_t*)descA, nA, dim, dp);
-        std::vector<uint8_t> b = type == FM3D_DESC_F32 ? f32_to_u8((const float*)descB, nB, dim, dp)
-                                                        : pad_u8((const uint8_t*)descB, nB, dim, dp);
-        int r;
-        if ((r = upload(c, c->A, a.data(), a.size()))) return r;
-        if ((r = upload(c, c->B, b.data(), b.size()))) return r;
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const size_t ba = (size_t)nA * dp, bb = (size_t)nB * dp;
+        HIPCHK(c, c->hA.ensure(ba + 1));
+        HIPCHK(c, c->hB.ensure(bb + 1));
+        if (type == FM3D_DESC_F32) {
+            f32_to_u8(c->hA.as<uint8_t>(), (const float*)descA, nA, dim, dp);
+            f32_to_u8(c->hB.as<uint8_t>(), (const float*)descB, nB, dim, dp);
+        } else {
+            pad_u8(c->hA.as<uint8_t>(), (const uint8_t*)descA, nA, dim, dp);
+            pad_u8(c->hB.as<uint8_t>(), (const uint8_t*)descB, nB, dim, dp);
+        }
+        HIPCHK(c, c->A.ensure(ba));
+        HIPCHK(c, c->B.ensure(bb));
+        if (ba) HIPCHK(c, hipMemcpyAsync(c->A.p, c->hA.p, ba, hipMemcpyHostToDevice, c->stream));
+        if (bb) HIPCHK(c, hipMemcpyAsync(c->B.p, c->hB.p, bb, hipMemcpyHostToDevice, c->stream));
         *dimPad = dp;
     } else if (t == FM3D_DESC_F32) {
-        int r;
-        if ((r = upload(c, c->A, descA, (size_t)nA * dim * 4))) return r;
-        if ((r = upload(c, c->B, descB, (size_t)nB * dim * 4))) return r;
+        if ((r = upload_pinned(c, c->A, c->hA, descA, (size_t)nA * dim * 4))) return r;
+        if ((r = upload_pinned(c, c->B, c->hB, descB, (size_t)nB * dim * 4))) return r;
         *dimPad = dim;
     } else if (t == FM3D_DESC_BITS) {
         int words = (dim + 3) / 4;
         int wp = (words == 4 || words == 8 || words == 16) ? words : 16;
         if (words > 16) return fail(c, FM3D_ERR_UNSUPPORTED, "binary descriptors longer than 64 bytes");
-        std::vector<uint8_t> a((size_t)nA * wp * 4, 0), b((size_t)nB * wp * 4, 0);
-        for (int i = 0; i < nA; i++) std::memcpy(&a[(size_t)i * wp * 4], (const uint8_t*)descA + (size_t)i * dim, dim);
-        for (int i = 0; i < nB; i++) std::memcpy(&b[(size_t)i * wp * 4], (const uint8_t*)descB + (size_t)i * dim, dim);
-        int r;
-        if ((r = upload(c, c->A, a.data(), a.size()))) return r;
-        if ((r = upload(c, c->B, b.data(), b.size()))) return r;
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const size_t ba = (size_t)nA * wp * 4, bb = (size_t)nB * wp * 4;
+        HIPCHK(c, c->hA.ensure(ba + 1));
+        HIPCHK(c, c->hB.ensure(bb + 1));
+        std::memset(c->hA.p, 0, ba);
+        std::memset(c->hB.p, 0, bb);
+        for (int i = 0; i < nA; i++) std::memcpy(c->hA.as<uint8_t>() + (size_t)i * wp * 4, (const uint8_t*)descA + (size_t)i * dim, dim);
+        for (int i = 0; i < nB; i++) std::memcpy(c->hB.as<uint8_t>() + (size_t)i * wp * 4, (const uint8_t*)descB + (size_t)i * dim, dim);
+        HIPCHK(c, c->A.ensure(ba));
+        HIPCHK(c, c->B.ensure(bb));
+        if (ba) HIPCHK(c, hipMemcpyAsync(c->A.p, c->hA.p, ba, hipMemcpyHostToDevice, c->stream));
+        if (bb) HIPCHK(c, hipMemcpyAsync(c->B.p, c->hB.p, bb, hipMemcpyHostToDevice, c->stream));
         *dimPad = wp * 4;
     } else {
         return fail(c, FM3D_ERR_INVALID, "unknown descriptor type");
     }
+    HIPCHK(c, hipEventRecord(c->evStage, c->stream));
     *effType = t;
     return FM3D_OK;
 }
@@ -500,17 +577,30 @@ void fill_lm_cycles(const fm3d_ctx* c, const unsigned long long* cnt, fm3d_lm_st
     st->queue_empty_ticks = cnt[25] ? (int64_t)(cnt[25] - cnt[20]) : 0;
 }
 
-// LM normals over nPts device points (c->pts), outputs in c->lm*
-int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
+// The LM kernel's camera: the settings' camera with a principal point of -0.0 replaced by +0.0.
+// The kernel's isPixelGood compares bit patterns (0 <= u <= xmax as bits(u) <= bits(xmax)), which
+// differs from the reference's comparison only for u == -0.0; u = xd*fx + cx (and the image-1
+// centre, the same sum) is -0.0 only when cx is -0.0 and xd*fx is -0.0.  With +0.0 that sum is
+// +0.0: the reference's test is true for both zeros, and the bilinear sample at a +-0 coordinate is
+// the same.  Every other principal point (zero, negative, outside the image) gives the reference's
+// bits: a negative u or NaN lies above bits(xmax) as the reference's comparison is false, and the
+// fused a2 = r2 + 2x^2 differs only where x*x is subnormal, where u's float sample coordinate
+// rounds to the same value (tests/test_gpu_parity.py::test_principal_point_zero_and_negative).
+fm3d::Camera lm_camera(const fm3d::Camera& cam) {
+    fm3d::Camera k = cam;
+    if (k.cx == 0.) k.cx = 0.;  // -0.0 -> +0.0
+    if (k.cy == 0.) k.cy = 0.;
+    return k;
+}
+
+// LM normals over the device points c->pts, outputs in c->lm*.  P: the point count, or its bound
+// when Pdev holds the count on the device (the pipeline: no host sync before the launch)
+int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
     int r;
     if ((r = ensure_offsets(c))) return r;
     if (c->pyr1.empty()) return fail(c, FM3D_ERR_INVALID, "fm3d_set_images (NormalOptimizer::setImages) not called");
     if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "g12 not set (SingleCameraTriangulator::setg12)");
-    // the kernel's isPixelGood compares bit patterns (u = xd*fx + cx is never -0) and its
-    // distortion terms round like the reference's only where u, v are dominated by cx, cy near the
-    // optical axis (fm3d_lm2.hip, geometry2): a principal point inside the image
-    if (!(c->cam.cx >= 1e-3 && c->cam.cy >= 1e-3))
-        return fail(c, FM3D_ERR_UNSUPPORTED, "computeOptimizedNormals needs a principal point with cx, cy > 0");
+    const fm3d::Camera cam = lm_camera(c->cam);
     const int levels = c->s.pyramids;
     HIPCHK(c, c->lmNormals.ensure((size_t)(P + 1) * 3 * sizeof(double)));
     HIPCHK(c, c->lmStatus.ensure((size_t)(P + 1) * sizeof(int)));
@@ -551,14 +641,17 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     fm3d::LMParams p{};
     p.points = c->pts.as<double>();
     p.P = P;
-    p.cam = c->cam;
+    p.Pdev = Pdev;
+    p.cam = cam;
     std::memcpy(p.R2, c->R2, sizeof(p.R2));
     std::memcpy(p.t2, c->t2, sizeof(p.t2));
     {   // the same constants as a small global table (re-read per chunk by the LM kernel)
-        fm3d::ProjConst pc;
+        HIPCHK(c, hipEventSynchronize(c->evProj));  // the previous launch's copy out of hProj ran
+        HIPCHK(c, c->hProj.ensure(sizeof(fm3d::ProjConst)));
+        fm3d::ProjConst& pc = *c->hProj.as<fm3d::ProjConst>();  // pinned: the copy may run later
         std::memcpy(pc.R, c->R2, sizeof(pc.R));
         std::memcpy(pc.t, c->t2, sizeof(pc.t));
-        pc.cam = c->cam;
+        pc.cam = cam;
         const size_t Gn = (size_t)groups * slots * c->nOffPad;  // entries per slab array
         pc.slabRX = (const char*)c->slab.p;
         pc.slabRY = FM3D_RAY_AOS ? pc.slabRX + sizeof(double) : pc.slabRX + Gn * sizeof(double);
@@ -568,6 +661,7 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
         pc.slabDJ1 = pc.slabDJ0 + Gn * 4;
         HIPCHK(c, c->lmProj.ensure(sizeof(pc)));
         HIPCHK(c, hipMemcpyAsync(c->lmProj.p, &pc, sizeof(pc), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipEventRecord(c->evProj, c->stream));
         p.proj = c->lmProj.as<fm3d::ProjConst>();
     }
     p.lvl = c->lvlDesc.as<LevelDesc>();
@@ -631,11 +725,16 @@ int run_lm(fm3d_ctx* c, int P, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e
     return FM3D_OK;
 }
 
-int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int width, int height, int stride) {
+// the two images into pinned staging and their pyramids (pyrDown chain) on the context stream;
+// sync: wait for them before returning (fm3d_set_images: the caller may read them back at once)
+int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int width, int height, int stride,
+                    bool sync = true) {
     if (!img1 || !img2 || width <= 0 || height <= 0 || stride < width)
         return fail(c, FM3D_ERR_INVALID, "bad image arguments");
     const int levels = c->s.pyramids;
     if (levels < 0 || levels > 7) return fail(c, FM3D_ERR_UNSUPPORTED, "pyramids must be in [0, 7]");
+    int r;
+    if ((r = staging_wait(c))) return r;
     c->w = width;
     c->h = height;
     c->lw.assign(levels + 1, 0);
@@ -652,11 +751,19 @@ int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int w
         size_t bytes = (size_t)c->lw[L] * c->lh[L] + kGuard(c->lw[L]);
         HIPCHK(c, c->pyr1[L].ensure(bytes));
         HIPCHK(c, c->pyr2[L].ensure(bytes));
-        HIPCHK(c, hipMemsetAsync(c->pyr1[L].p, 0, bytes, c->stream));
-        HIPCHK(c, hipMemsetAsync(c->pyr2[L].p, 0, bytes, c->stream));
+        // level 0 is overwritten by the copy below: only its zero guard needs clearing
+        const size_t skip = L == 0 ? (size_t)width * height : 0;
+        HIPCHK(c, hipMemsetAsync((char*)c->pyr1[L].p + skip, 0, bytes - skip, c->stream));
+        HIPCHK(c, hipMemsetAsync((char*)c->pyr2[L].p + skip, 0, bytes - skip, c->stream));
     }
-    HIPCHK(c, hipMemcpy2DAsync(c->pyr1[0].p, width, img1, stride, width, height, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpy2DAsync(c->pyr2[0].p, width, img2, stride, width, height, hipMemcpyHostToDevice, c->stream));
+    const size_t wh = (size_t)width * height;
+    HIPCHK(c, c->hImg.ensure(2 * wh));
+    for (int y = 0; y < height; y++) {
+        std::memcpy(c->hImg.as<uint8_t>() + (size_t)y * width, img1 + (size_t)y * stride, width);
+        std::memcpy(c->hImg.as<uint8_t>() + wh + (size_t)y * width, img2 + (size_t)y * stride, width);
+    }
+    HIPCHK(c, hipMemcpyAsync(c->pyr1[0].p, c->hImg.p, wh, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->pyr2[0].p, c->hImg.as<uint8_t>() + wh, wh, hipMemcpyHostToDevice, c->stream));
     for (int L = 1; L <= levels; L++) {
         fm3d::launch_pyrdown(c->pyr1[L - 1].as<uint8_t>(), c->lw[L - 1], c->lh[L - 1], c->pyr1[L].as<uint8_t>(),
                              c->stream);
@@ -664,11 +771,13 @@ int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int w
                              c->stream);
     }
     HIPCHK(c, hipGetLastError());
-    std::vector<LevelDesc> d(levels + 1);
+    HIPCHK(c, c->hTab.ensure((levels + 1) * sizeof(LevelDesc)));
+    LevelDesc* d = c->hTab.as<LevelDesc>();
     for (int L = 0; L <= levels; L++) d[L] = LevelDesc{c->pyr1[L].as<uint8_t>(), c->pyr2[L].as<uint8_t>(), c->lw[L], c->lh[L]};
-    HIPCHK(c, c->lvlDesc.ensure(d.size() * sizeof(LevelDesc)));
-    HIPCHK(c, hipMemcpyAsync(c->lvlDesc.p, d.data(), d.size() * sizeof(LevelDesc), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, c->lvlDesc.ensure((levels + 1) * sizeof(LevelDesc)));
+    HIPCHK(c, hipMemcpyAsync(c->lvlDesc.p, d, (levels + 1) * sizeof(LevelDesc), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->evStage, c->stream));
+    if (sync) HIPCHK(c, hipStreamSynchronize(c->stream));
     return FM3D_OK;
 }
 
@@ -1450,6 +1559,8 @@ int fm3d_ctx_create(const fm3d_settings* s, int device, fm3d_ctx** out) {
     }
     c->ownStream = true;
     for (auto& e : c->ev) hipEventCreate(&e);
+    hipEventCreateWithFlags(&c->evStage, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->evProj, hipEventDisableTiming);
     c->cam.fx = s->Fx;
     c->cam.fy = s->Fy;
     c->cam.cx = s->Cx;
@@ -1478,8 +1589,15 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->orbPyr, &c->orbTab, &c->orbLev, &c->orbMap, &c->orbFlag, &c->orbPos, &c->orbKp, &c->orbR,
                       &c->orbBlur, &c->orbDesc, &c->orbPat, &c->siftImg, &c->siftBase, &c->siftG, &c->siftD,
                       &c->siftGL, &c->siftDL, &c->siftTaps, &c->siftScan, &c->siftFlag, &c->siftPos, &c->siftCand,
-                      &c->siftAng, &c->siftNpk, &c->siftKp, &c->siftDesc};
+                      &c->siftAng, &c->siftNpk, &c->siftKp, &c->siftDesc, &c->brImg, &c->brSum, &c->brKp,
+                      &c->brIdx, &c->brPat, &c->brPairs, &c->brDesc, &c->starImg, &c->starS, &c->starT, &c->starF,
+                      &c->starR, &c->starZ, &c->starKp, &c->starFlag, &c->starPos, &c->starOut, &c->starWork,
+                      &c->nccS, &c->nccN, &c->nccB, &c->pcnt};
     for (DevBuf* b : bufs) b->release();
+    HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall};
+    for (HostBuf* b : hbufs) b->release();
+    hipEventDestroy(c->evStage);
+    hipEventDestroy(c->evProj);
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();
     for (auto& e : c->ev) hipEventDestroy(e);
@@ -1615,8 +1733,8 @@ int fm3d_triangulate(fm3d_ctx* c, const fm3d_point2f* kpts1, int n1, const fm3d_
     p.mask = c->triMask.as<int>();
     p.mask8 = c->triMask8.as<uint8_t>();
     fm3d::launch_triangulate(p, c->stream);
-    fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), K, c->pts.as<double>(), c->count.as<int>(),
-                                c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
+    fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), K, nullptr, c->pts.as<double>(),
+                                c->count.as<int>(), c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
     int n = 0;
     HIPCHK(c, hipMemcpyAsync(&n, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1652,7 +1770,7 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
     hipSetDevice(c->device);
     int r;
     if ((r = upload(c, c->pts, points, (size_t)P * 3 * sizeof(double)))) return r;
-    if ((r = run_lm(c, P, stats, c->ev[0], c->ev[1]))) return r;
+    if ((r = run_lm(c, P, nullptr, stats, c->ev[0], c->ev[1]))) return r;
     std::vector<double> nrm((size_t)P * 3);
     std::vector<int> st(P), inf((size_t)P * 8), nf((size_t)P * 8);
     unsigned long long cnt[26] = {};
@@ -1702,16 +1820,25 @@ int fm3d_optimize_normals(fm3d_ctx* c, double* points, int P, double* normals, i
 }
 
 // ---------------- whole pipeline, device resident ----------------
-int fm3d_pipeline_upload(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
-                         const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
-                         int width, int height, int queryOffset) {
-    if (!c || !kpts1 || !kpts2) return fail(c, FM3D_ERR_INVALID, "null argument");
-    hipSetDevice(c->device);
+}  // extern "C"
+namespace {
+#define PENDING_CHECK(c)                                                                            \
+    do {                                                                                            \
+        if ((c)->pending)                                                                           \
+            return fail((c), FM3D_ERR_INVALID, "a submitted frame pair is pending: fm3d_pipeline_wait first"); \
+    } while (0)
+
+// the inputs of one frame pair into HBM on the context stream (pinned staging, asynchronous):
+// descriptors, keypoints, both images and their pyramids (a6, normaloptimizer.cpp:206-221)
+int stage_pipeline(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                   const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
+                   int width, int height, int queryOffset) {
+    if (!kpts1 || !kpts2) return fail(c, FM3D_ERR_INVALID, "null argument");
     int t, dp, r;
     if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp))) return r;
-    if ((r = upload(c, c->kp1, kpts1, (size_t)nA * sizeof(fm3d_point2f)))) return r;
-    if ((r = upload(c, c->kp2, kpts2, (size_t)nB * sizeof(fm3d_point2f)))) return r;
-    if ((r = set_images_impl(c, img1, img2, width, height, width))) return r;
+    if ((r = upload_pinned(c, c->kp1, c->hK1, kpts1, (size_t)nA * sizeof(fm3d_point2f)))) return r;
+    if ((r = upload_pinned(c, c->kp2, c->hK2, kpts2, (size_t)nB * sizeof(fm3d_point2f)))) return r;
+    if ((r = set_images_impl(c, img1, img2, width, height, width, false))) return r;  // records evStage
     if (!c->haveG12) {
         double g[16];
         if ((r = fm3d_setg12(c, c->s.pos1, c->s.pos2, c->s.pos1 + 3, c->s.pos2 + 3, g))) return r;
@@ -1724,36 +1851,33 @@ int fm3d_pipeline_upload(fm3d_ctx* c, const void* descA, int nA, const void* des
     c->stDimPad = dp;
     c->stQueryOffset = queryOffset;
     c->staged = true;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     return FM3D_OK;
 }
 
-}  // extern "C"
-namespace {
-// match -> NNDR -> compaction -> DLT triangulation -> compaction on the staged inputs (ev[2..5]):
-// K matches, P inliers (c->matches, c->pts, c->srcIdx)
-int pipeline_front(fm3d_ctx* c, int& K, int& P) {
+// match -> NNDR -> compaction -> DLT triangulation -> compaction on the staged inputs (ev[2..5]),
+// sized by the query count: the match count K and the inlier count P stay on the device
+// (c->pcnt[0], [1]) and bound nothing the host launches, so the stages queue without a host
+// round trip (c->matches, c->pts, c->srcIdx hold K / P entries)
+int pipeline_front(fm3d_ctx* c) {
     const int nA = c->stNA, nB = c->stNB;
     int r;
     hipEvent_t* ev = c->ev;
+    HIPCHK(c, c->pcnt.ensure(64));
+    int* cnt = c->pcnt.as<int>();
     HIPCHK(c, hipEventRecord(ev[2], c->stream));
     // a1: match + NNDR
     if ((r = run_match(c, nA, nB, c->stType, c->stDimPad, c->s.nndrEpsilon, c->stQueryOffset, false))) return r;
     HIPCHK(c, hipEventRecord(ev[3], c->stream));
     if ((r = ensure_scan_tmp(c, nA))) return r;
     HIPCHK(c, c->matches.ensure((size_t)(nA + 1) * sizeof(fm3d_dmatch)));
-    fm3d::launch_compact_dmatch(c->cand.as<fm3d_dmatch>(), c->flag.as<int>(), nA, c->matches.as<fm3d_dmatch>(),
-                                c->count.as<int>(), c->scanTmp.p, c->stream);
-    K = 0;
-    HIPCHK(c, hipMemcpyAsync(&K, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fm3d::launch_compact_dmatch(c->cand.as<fm3d_dmatch>(), c->flag.as<int>(), nA, c->matches.as<fm3d_dmatch>(), cnt + 0,
+                                c->scanTmp.p, c->stream);
     HIPCHK(c, hipEventRecord(ev[4], c->stream));
-    // a4, a5: triangulate (matches are device resident)
-    HIPCHK(c, c->triPts.ensure((size_t)(K + 1) * 3 * sizeof(double)));
-    HIPCHK(c, c->triMask.ensure((size_t)(K + 1) * sizeof(int)));
-    HIPCHK(c, c->pts.ensure((size_t)(K + 1) * 3 * sizeof(double)));
-    HIPCHK(c, c->srcIdx.ensure((size_t)(K + 1) * sizeof(int)));
-    if ((r = ensure_scan_tmp(c, K > nA ? K : nA))) return r;
+    // a4, a5: triangulate (matches are device resident; K <= nA)
+    HIPCHK(c, c->triPts.ensure((size_t)(nA + 1) * 3 * sizeof(double)));
+    HIPCHK(c, c->triMask.ensure((size_t)(nA + 1) * sizeof(int)));
+    HIPCHK(c, c->pts.ensure((size_t)(nA + 1) * 3 * sizeof(double)));
+    HIPCHK(c, c->srcIdx.ensure((size_t)(nA + 1) * sizeof(int)));
     fm3d::TriParams tp{};
     tp.cam = c->cam;
     std::memcpy(tp.g12, c->g12, sizeof(tp.g12));
@@ -1762,59 +1886,63 @@ int pipeline_front(fm3d_ctx* c, int& K, int& P) {
     tp.kp1 = c->kp1.as<fm3d_point2f>();
     tp.kp2 = c->kp2.as<fm3d_point2f>();
     tp.matches = c->matches.as<fm3d_dmatch>();
-    tp.K = K;
+    tp.K = nA;
+    tp.Kdev = cnt + 0;
     tp.queryOffset = c->stQueryOffset;
     tp.pts = c->triPts.as<double>();
     tp.mask = c->triMask.as<int>();
     tp.mask8 = nullptr;
     fm3d::launch_triangulate(tp, c->stream);
-    fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), K, c->pts.as<double>(),
-                                c->count.as<int>(), c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
+    fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), nA, cnt + 0, c->pts.as<double>(), cnt + 1,
+                                c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
-    P = 0;
-    HIPCHK(c, hipMemcpyAsync(&P, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventRecord(ev[5], c->stream));
     return FM3D_OK;
 }
-}  // namespace
-extern "C" {
 
-int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pipeline_stats* stats) {
-    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
-    hipSetDevice(c->device);
-    const int nA = c->stNA, nB = c->stNB;
+// the whole path on the staged inputs, queued on the context stream: front half, LM normals over
+// the device-counted inliers (a6-a15; the pyramids were built at staging: images are inputs of the
+// path), survivor records (compacted into out, or the internal buffer), then one D2H of the counts
+// and the LM counters into pinned memory.  Nothing here waits for the device.
+int enqueue_full(fm3d_ctx* c, fm3d_record* out, fm3d_lm_stats* ls) {
+    const int nA = c->stNA;
     hipEvent_t* ev = c->ev;
-    int r, K = 0, P = 0;
-    if ((r = pipeline_front(c, K, P))) return r;
-    c->stK = K;
-    c->stP = P;
-    // a6-a15: normals (pyramids were built at upload: images are inputs of the path)
-    fm3d_lm_stats ls{};
-    if ((r = run_lm(c, P, &ls, ev[6], ev[7]))) return r;
-    // records of the survivors
-    HIPCHK(c, c->recTmp.ensure((size_t)(P + 1) * sizeof(fm3d_record)));
-    HIPCHK(c, c->recFlag.ensure((size_t)(P + 1) * sizeof(int)));
-    fm3d_record* out = recordsDev;
+    int r;
+    if ((r = pipeline_front(c))) return r;
+    int* cnt = c->pcnt.as<int>();
+    if ((r = run_lm(c, nA, cnt + 1, ls, ev[6], ev[7]))) return r;
+    HIPCHK(c, c->recTmp.ensure((size_t)(nA + 1) * sizeof(fm3d_record)));
+    HIPCHK(c, c->recFlag.ensure((size_t)(nA + 1) * sizeof(int)));
     if (!out) {
         HIPCHK(c, c->records.ensure((size_t)(nA + 1) * sizeof(fm3d_record)));
         out = c->records.as<fm3d_record>();
     }
-    if ((r = ensure_scan_tmp(c, P > nA ? P : nA))) return r;
-    fm3d::launch_make_records(c->matches.as<fm3d_dmatch>(), c->srcIdx.as<int>(), P, c->pts.as<double>(),
+    c->pendOut = out;
+    fm3d::launch_make_records(c->matches.as<fm3d_dmatch>(), c->srcIdx.as<int>(), nA, cnt + 1, c->pts.as<double>(),
                               c->lmNormals.as<double>(), c->lmStatus.as<int>(), c->recTmp.as<fm3d_record>(),
                               c->recFlag.as<int>(), c->stream);
-    fm3d::launch_compact_records(c->recTmp.as<fm3d_record>(), c->recFlag.as<int>(), P, out, c->count.as<int>(),
+    fm3d::launch_compact_records(c->recTmp.as<fm3d_record>(), c->recFlag.as<int>(), nA, cnt + 1, out, cnt + 2,
                                  c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
-    int kept = 0;
-    unsigned long long cnt[26] = {};
-    HIPCHK(c, hipMemcpyAsync(&kept, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(cnt, c->lmStat.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, c->hSmall.ensure(sizeof(PipeSmall)));
+    PipeSmall* hs = c->hSmall.as<PipeSmall>();
+    HIPCHK(c, hipMemcpyAsync(hs->cnt, cnt, sizeof(hs->cnt), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(hs->lm, c->lmStat.p, sizeof(hs->lm), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    return FM3D_OK;
+}
+
+// after the stream ran enqueue_full: guards, counts and stats (t0: the event the total starts at)
+int finalize_full(fm3d_ctx* c, const fm3d_lm_stats& ls, hipEvent_t t0, bool staged_in_step, int* nKept,
+                  fm3d_pipeline_stats* stats) {
+    hipEvent_t* ev = c->ev;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    const PipeSmall* hs = c->hSmall.as<PipeSmall>();
+    const int K = hs->cnt[0], P = hs->cnt[1], kept = hs->cnt[2];
+    c->stK = K;
+    c->stP = P;
     // the LM watchdog (maxIter / FM3D_LM_MAX_SECONDS) leaves points in kLMRunning: an error, not drops
-    if (cnt[2]) return fail(c, FM3D_ERR_HIP, "LM kernel iteration guard tripped (internal error)");
+    if (hs->lm[2]) return fail(c, FM3D_ERR_HIP, "LM kernel iteration guard tripped (internal error)");
     if (c->s.strictNanExit && P > 0) {  // reference exit(-6) on a NaN plane hit (:465-469)
         std::vector<int> st(P);
         HIPCHK(c, hipMemcpy(st.data(), c->lmStatus.p, (size_t)P * sizeof(int), hipMemcpyDeviceToHost));
@@ -1825,8 +1953,8 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
     if (nKept) *nKept = kept;
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
-        stats->queries = nA;
-        stats->trains = nB;
+        stats->queries = c->stNA;
+        stats->trains = c->stNB;
         stats->matches = K;
         stats->inliers = P;
         stats->kept = kept;
@@ -1837,31 +1965,141 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
         stats->nndr_ms = ms;
         hipEventElapsedTime(&ms, ev[4], ev[5]);
         stats->triangulate_ms = ms;
-        stats->pyramid_ms = 0;
         ms = 0;
-        if (P) hipEventElapsedTime(&ms, ev[6], ev[7]);
+        if (staged_in_step) hipEventElapsedTime(&ms, ev[8], ev[2]);
+        stats->pyramid_ms = ms;  // the inputs' H2D + pyramids (fm3d_pipeline_submit only)
+        ms = 0;
+        hipEventElapsedTime(&ms, ev[6], ev[7]);
         stats->lm_ms = ms;
-        hipEventElapsedTime(&ms, ev[2], ev[1]);
+        hipEventElapsedTime(&ms, t0, ev[1]);
         stats->total_ms = ms;
         stats->lm = ls;
         stats->lm.points_in = P;
         stats->lm.points_kept = kept;
-        stats->lm.evaluations = (int64_t)cnt[0];
-        stats->lm.pixel_evaluations = (int64_t)cnt[1];
+        stats->lm.evaluations = (int64_t)hs->lm[0];
+        stats->lm.pixel_evaluations = (int64_t)hs->lm[1];
         stats->lm.kernel_ms = stats->lm_ms;
-        fill_lm_cycles(c, cnt, &stats->lm);
+        fill_lm_cycles(c, hs->lm, &stats->lm);
     }
     return FM3D_OK;
 }
+}  // namespace
+extern "C" {
+
+int fm3d_pipeline_upload(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                         const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
+                         int width, int height, int queryOffset) {
+    if (!c) return FM3D_ERR_INVALID;
+    PENDING_CHECK(c);
+    hipSetDevice(c->device);
+    int r;
+    if ((r = stage_pipeline(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, queryOffset)))
+        return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pipeline_stats* stats) {
+    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    PENDING_CHECK(c);
+    hipSetDevice(c->device);
+    fm3d_lm_stats ls{};
+    int r;
+    if ((r = enqueue_full(c, recordsDev, &ls))) return r;
+    return finalize_full(c, ls, c->ev[2], false, nKept, stats);
+}
+
+int fm3d_pipeline_submit(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                         const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
+                         int width, int height, int queryOffset) {
+    if (!c) return FM3D_ERR_INVALID;
+    PENDING_CHECK(c);
+    hipSetDevice(c->device);
+    HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
+    int r;
+    if ((r = stage_pipeline(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, queryOffset)))
+        return r;
+    c->subLm = fm3d_lm_stats{};
+    if ((r = enqueue_full(c, nullptr, &c->subLm))) return r;
+    c->pending = true;
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_wait(fm3d_ctx* c, fm3d_record* out, int cap, int* nKept, fm3d_pipeline_stats* stats) {
+    if (!c) return FM3D_ERR_INVALID;
+    if (!c->pending) return fail(c, FM3D_ERR_INVALID, "no frame pair submitted (fm3d_pipeline_submit)");
+    hipSetDevice(c->device);
+    c->pending = false;
+    int kept = 0, r;
+    if ((r = finalize_full(c, c->subLm, c->ev[8], true, &kept, stats))) return r;
+    if (out && kept > cap) return fail(c, FM3D_ERR_INVALID, "record buffer too small");
+    if (out && kept)
+        HIPCHK(c, hipMemcpy(out, c->pendOut, (size_t)kept * sizeof(fm3d_record), hipMemcpyDeviceToHost));
+    if (nKept) *nKept = kept;
+    return FM3D_OK;
+}
+
+}  // extern "C"
+
+// ---- internal entry points of the multi-GPU host (fm3d_mgpu.cpp; fm3d_internal.h, not the C ABI)
+int fm3d_internal_submit_to(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                            const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1,
+                            const uint8_t* img2, int width, int height, fm3d_record* recordsDev) {
+    if (!c) return FM3D_ERR_INVALID;
+    PENDING_CHECK(c);
+    hipSetDevice(c->device);
+    HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
+    int r;
+    if ((r = stage_pipeline(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, 0))) return r;
+    c->subLm = fm3d_lm_stats{};
+    if ((r = enqueue_full(c, recordsDev, &c->subLm))) return r;
+    c->pending = true;
+    return FM3D_OK;
+}
+
+int fm3d_internal_enqueue(fm3d_ctx* c, fm3d_record* recordsDev) {
+    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    PENDING_CHECK(c);
+    hipSetDevice(c->device);
+    HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
+    c->subLm = fm3d_lm_stats{};
+    int r;
+    if ((r = enqueue_full(c, recordsDev, &c->subLm))) return r;
+    c->pending = true;
+    return FM3D_OK;
+}
+
+int fm3d_internal_finish(fm3d_ctx* c, int* nKept, fm3d_pipeline_stats* stats) {
+    if (!c || !c->pending) return fail(c, FM3D_ERR_INVALID, "nothing pending");
+    hipSetDevice(c->device);
+    c->pending = false;
+    return finalize_full(c, c->subLm, c->ev[8], true, nKept, stats);
+}
+
+const int* fm3d_internal_kept_dev(fm3d_ctx* c) { return c->pcnt.as<int>() + 2; }
+hipStream_t fm3d_internal_stream(fm3d_ctx* c) { return c->stream; }
+int fm3d_internal_device(fm3d_ctx* c) { return c->device; }
+int fm3d_internal_prepare(fm3d_ctx* c) {  // the device count buffer, before a collective names it
+    hipSetDevice(c->device);
+    HIPCHK(c, c->pcnt.ensure(64));
+    return FM3D_OK;
+}
+
+extern "C" {
 
 int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats) {
     if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    PENDING_CHECK(c);
     hipSetDevice(c->device);
     hipEvent_t* ev = c->ev;
-    int r, K = 0, P = 0;
-    if ((r = pipeline_front(c, K, P))) return r;
+    int r;
+    if ((r = pipeline_front(c))) return r;
+    HIPCHK(c, c->hSmall.ensure(sizeof(PipeSmall)));
+    PipeSmall* hs = c->hSmall.as<PipeSmall>();
+    HIPCHK(c, hipMemcpyAsync(hs->cnt, c->pcnt.p, sizeof(hs->cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int K = hs->cnt[0], P = hs->cnt[1];
     c->stK = K;
     c->stP = P;
     if (nInliers) *nInliers = P;
@@ -1886,25 +2124,26 @@ int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats
 
 int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* nPoints, fm3d_pipeline_stats* stats) {
     if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    PENDING_CHECK(c);
     if (Hphi <= 0 || Htheta <= 0 || Hphi * Htheta > 32) return fail(c, FM3D_ERR_INVALID, "1 <= Hphi * Htheta <= 32");
     if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "fm3d_set_g12 / fm3d_setg12 not called");
     hipSetDevice(c->device);
     hipEvent_t* ev = c->ev;
-    int r, K = 0, P = 0;
-    if ((r = pipeline_front(c, K, P))) return r;
-    c->stK = K;
-    c->stP = P;
+    int r;
+    c->nccP = 0;
+    if ((r = pipeline_front(c))) return r;
+    const int nA = c->stNA;
     const int H = Hphi * Htheta;
-    c->nccH = H;
     HIPCHK(c, hipEventRecord(ev[6], c->stream));
-    if (P > 0) {
+    if (nA > 0) {
         if ((r = ensure_offsets(c))) return r;
-        HIPCHK(c, c->nccS.ensure((size_t)P * H * sizeof(double)));
-        HIPCHK(c, c->nccN.ensure((size_t)P * 3 * sizeof(double)));
-        HIPCHK(c, c->nccB.ensure((size_t)P * sizeof(int)));
+        HIPCHK(c, c->nccS.ensure((size_t)nA * H * sizeof(double)));
+        HIPCHK(c, c->nccN.ensure((size_t)nA * 3 * sizeof(double)));
+        HIPCHK(c, c->nccB.ensure((size_t)nA * sizeof(int)));
         fm3d::NccParams p{};
         p.points = c->pts.as<double>();
-        p.P = P;
+        p.P = nA;  // the bound; the inlier count is on the device
+        p.Pdev = c->pcnt.as<int>() + 1;
         p.cam = c->cam;
         std::memcpy(p.R2, c->R2, sizeof(p.R2));
         std::memcpy(p.t2, c->t2, sizeof(p.t2));
@@ -1928,8 +2167,16 @@ int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* n
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(ev[7], c->stream));
+    HIPCHK(c, c->hSmall.ensure(sizeof(PipeSmall)));
+    PipeSmall* hs = c->hSmall.as<PipeSmall>();
+    HIPCHK(c, hipMemcpyAsync(hs->cnt, c->pcnt.p, sizeof(hs->cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int K = hs->cnt[0], P = hs->cnt[1];
+    c->stK = K;
+    c->stP = P;
+    c->nccH = H;
+    c->nccP = P;  // the score rows fm3d_pipeline_ncc_download returns (set only by a successful run)
     if (nPoints) *nPoints = P;
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
@@ -1955,8 +2202,10 @@ int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* n
 
 int fm3d_pipeline_ncc_download(fm3d_ctx* c, double* scores, double* normals, int32_t* best) {
     if (!c || !c->staged) return FM3D_ERR_INVALID;
+    PENDING_CHECK(c);
     hipSetDevice(c->device);
-    const size_t P = (size_t)c->stP;
+    // the rows of the last successful fm3d_pipeline_run_ncc (a later run / run_dlt does not resize them)
+    const size_t P = (size_t)c->nccP;
     if (P && scores) HIPCHK(c, hipMemcpy(scores, c->nccS.p, P * c->nccH * sizeof(double), hipMemcpyDeviceToHost));
     if (P && normals) HIPCHK(c, hipMemcpy(normals, c->nccN.p, P * 3 * sizeof(double), hipMemcpyDeviceToHost));
     if (P && best) HIPCHK(c, hipMemcpy(best, c->nccB.p, P * sizeof(int), hipMemcpyDeviceToHost));
@@ -1965,6 +2214,7 @@ int fm3d_pipeline_ncc_download(fm3d_ctx* c, double* scores, double* normals, int
 
 int fm3d_pipeline_dlt_download(fm3d_ctx* c, fm3d_dmatch* matches, double* points, int32_t* matchIdx) {
     if (!c || !c->staged) return FM3D_ERR_INVALID;
+    PENDING_CHECK(c);
     hipSetDevice(c->device);
     if (matches && c->stK) HIPCHK(c, hipMemcpy(matches, c->matches.p, (size_t)c->stK * sizeof(fm3d_dmatch), hipMemcpyDeviceToHost));
     if (points && c->stP) HIPCHK(c, hipMemcpy(points, c->pts.p, (size_t)c->stP * 3 * sizeof(double), hipMemcpyDeviceToHost));

@@ -36,7 +36,8 @@ struct ProjConst {
 
 struct LMParams {
     const double* points;  // P x 3
-    int P;
+    int P;                 // points, or their bound when Pdev is set
+    const int* Pdev;       // the point count on the device (may be null: P)
     Camera cam;
     double R2[9], t2[3];
     const ProjConst* proj;  // the same R2, t2, cam in global memory
@@ -124,7 +125,8 @@ void launch_nndr(int type, const int* idx, const int* key, const float* fkey, in
 // ---------------- NCC normal hypotheses (fm3d_ncc.hip) ----------------
 struct NccParams {
     const double* points;  // P x 3
-    int P;
+    int P;                 // points, or their bound when Pdev is set (one workgroup each)
+    const int* Pdev;       // the point count on the device (may be null)
     Camera cam;
     double R2[9], t2[3];
     const uint8_t *img1, *img2;  // pyramid level 0 (+ zero guard)
@@ -261,8 +263,9 @@ void launch_sift_desc(const float* gp, const SiftLevel* GL, int L, int firstOcta
 size_t scan_tmp_bytes(int n);
 void launch_compact_dmatch(const fm3d_dmatch* in, const int* flag, int n, fm3d_dmatch* out, int* count, void* tmp,
                            hipStream_t s);
-void launch_compact_points(const double* in, const int* flag, int n, double* out, int* count, int* srcIndex,
-                           void* tmp, hipStream_t s);
+// nDev (may be null): the item count on the device, n its bound (device-sized launches: no host sync)
+void launch_compact_points(const double* in, const int* flag, int n, const int* nDev, double* out, int* count,
+                           int* srcIndex, void* tmp, hipStream_t s);
 void launch_exclusive_scan(const int* flag, int n, int* offsets, int* total, void* tmp, hipStream_t s);
 
 // ---------------- triangulation ----------------
@@ -273,7 +276,8 @@ struct TriParams {
     const fm3d_point2f* kp1;
     const fm3d_point2f* kp2;
     const fm3d_dmatch* matches;
-    int K;
+    int K;            // matches, or their bound when Kdev is set
+    const int* Kdev;  // the match count on the device (may be null)
     int queryOffset;  // matches[].queryIdx - queryOffset indexes kp1
     double* pts;      // K x 3 (match order, not compacted)
     int* mask;        // K
@@ -313,10 +317,11 @@ void launch_export_patches(const double* frames, int P, int size, double eps, do
                            hipStream_t s);
 
 // ---------------- records ----------------
-void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int nInl, const double* pts,
+// nDev (may be null): the count on the device, nInl / n its bound
+void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int nInl, const int* nDev, const double* pts,
                          const double* normals, const int* status, fm3d_record* rec, int* flag, hipStream_t s);
-void launch_compact_records(const fm3d_record* in, const int* flag, int n, fm3d_record* out, int* count, void* tmp,
-                            hipStream_t s);
+void launch_compact_records(const fm3d_record* in, const int* flag, int n, const int* nDev, fm3d_record* out,
+                            int* count, void* tmp, hipStream_t s);
 
 // ---------------------------------------------------------------- STAR (fm3d_star.hip)
 struct StarPat {   // StarDetectorComputeResponses' pattern set (oracle/orc_star.c orc_star_patterns)

@@ -148,7 +148,7 @@ struct Ctl2 {
 
     __device__ void fetch(SlotS2& S, SlotP2& P) {
         const int q = atomicAdd(p->queue, 1);
-        if (q >= p->P) {
+        if (q >= (p->Pdev ? *p->Pdev : p->P)) {  // the inlier count on the device (pipeline) or given
             P.pass = Q_DONE;
             return;
         }

@@ -3,21 +3,24 @@
 //
 // The reference runs its three stages in one process on one thread (main.cpp:91-155) and has no
 // distributed component.  Every stage is independent per query keypoint once frame B's
-// descriptors and both image pyramids are on a device, so one frame pair splits into logical
-// shares of query blocks (BLOCK queries each, dealt round-robin over the shares: every share sees
-// the same mix of queries), share s running on devices[s % ndev]:
-//   * upload: each share's queries gathered into one array (local queryIdx), frame B, keypoints
-//     of frame B and both images replicated to its device (host uploads, one context per share);
-//   * run: one host thread per device runs that device's shares one after the other (the LM
-//     kernel is persistent and fills the GPU), each writing its survivor records straight into
-//     its slot of the device's all-gather send buffer;
+// descriptors and both image pyramids are on a device, so one frame pair splits into blocks of
+// BLOCK queries dealt round-robin over `shares` logical shares, share s belonging to device
+// s % ndev.  Per device:
+//   * ONE replica: the device's queries (the union of its shares' blocks, in increasing order:
+//     local queryIdx) gathered into one array, frame B, its keypoints and both images staged once
+//     (pinned H2D) into one context, and ONE pass of the whole path -- one LM launch over all the
+//     device's points, so the device pays one end-of-launch tail, not one per share;
 //   * exchange: ncclAllGather over xGMI (RCCL, one communicator per device from ncclCommInitAll)
-//     of the per-share survivor counts and of the fixed-capacity 64-byte record slots, so every
-//     device holds every share's records (north_star: "RCCL all-gather of per-shard 3D
-//     points/normals");
-//   * merge (fm3d_merge_shares, plain C++ on the host): local query indices mapped back to
-//     global ones in closed form, records ordered by query -- byte-identical to one
+//     of the device's survivor count and its fixed-capacity 64-byte record slot, queued on the
+//     device's pipeline stream right after the records (north_star: "RCCL all-gather of per-shard
+//     3D points/normals");
+//   * merge (plain C++ on the host): device 0's gathered copy, local query indices mapped back
+//     through each device's query list, records ordered by query -- byte-identical to one
 //     fm3d_pipeline_run of the whole frame pair.
+// Two context sets take frame pairs in turn (fm3d_mgpu_submit / fm3d_mgpu_wait): the next pair's
+// staging, front half and LM workgroups fill the CUs the previous LM launch frees in its tail, as
+// on one GPU (bench.py --gpus N).  Every submit is host-asynchronous: one host thread per device
+// gathers its queries and queues its pipeline, then the collectives are queued behind them.
 // RCCL is loaded with dlopen on first use, so libfm3d.so itself does not depend on it (a process
 // that also loads PyTorch's bundled RCCL keeps one copy per user).
 #include <dlfcn.h>
@@ -31,6 +34,7 @@
 #include <vector>
 
 #include "fm3d.h"
+#include "fm3d_internal.h"
 
 namespace {
 
@@ -73,7 +77,26 @@ Rccl& rccl() {
     return r;
 }
 
+// ncclGroupStart ... ncclGroupEnd: the group is closed on every path out of the scope, so a failed
+// collective never leaves later ones batched into a broken group on this thread
+struct RcclGroup {
+    bool open = false;
+    ncclResult_t start() {
+        ncclResult_t r = rccl().groupStart();
+        open = r == ncclSuccess;
+        return r;
+    }
+    ncclResult_t end() {
+        open = false;
+        return rccl().groupEnd();
+    }
+    ~RcclGroup() {
+        if (open) rccl().groupEnd();
+    }
+};
+
 constexpr int kDefaultBlock = 4096;
+constexpr int kSets = 2;  // frame pairs in flight (context sets)
 
 // number of queries of share s under the block-cyclic partition
 int64_t share_count(int64_t nA, int shares, int s, int block) {
@@ -89,15 +112,19 @@ struct fm3d_mgpu {
     fm3d_settings s{};
     int ndev = 0, shares = 0, block = kDefaultBlock;
     std::vector<int> devices;
-    std::vector<fm3d_ctx*> ctx;           // one per share
-    std::vector<ncclComm_t> comms;        // one per device
-    std::vector<hipStream_t> streams;     // one per device (the collectives)
-    std::vector<void*> send, recv;        // per device: L slots x cap records / ndev x L slots
-    std::vector<int32_t*> cntSend, cntRecv;
-    int64_t nA = 0, cap = 0;              // queries; records per share slot
-    std::vector<int> nq;                  // queries per share
-    int L = 0;                            // share slots per device (ceil(shares / ndev))
-    bool staged = false;
+    fm3d_ctx* ctx[kSets][16] = {};                 // one context per set and device
+    std::vector<ncclComm_t> comms;                  // one per device
+    void* send[kSets][16] = {};                     // per set and device: the records (capDev)
+    void* recv[kSets][16] = {};                     // ndev x capDev gathered records
+    int32_t* cntRecv[kSets][16] = {};               // ndev gathered counts
+    int64_t nA = 0, capDev = 0;                     // queries; record capacity per device
+    std::vector<std::vector<int32_t>> idx;          // per device: its global query indices (increasing)
+    std::vector<std::vector<uint8_t>> rowsA;        // per device: its gathered query rows (host)
+    std::vector<std::vector<fm3d_point2f>> kpA;     // per device: its gathered keypoints
+    bool staged = false;                            // fm3d_mgpu_pipeline_upload ran (set 0)
+    bool pending[kSets] = {};
+    int next = 0;                                   // the set the next submit takes
+    int waitNext = 0;                               // the set the next wait takes
     std::string err;
 };
 
@@ -114,25 +141,140 @@ int mfail(fm3d_mgpu* m, int code, const std::string& msg) {
         if (e_ != hipSuccess) return mfail(m, FM3D_ERR_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-#define MNCCL(m, x)                                                                             \
-    do {                                                                                        \
-        ncclResult_t r_ = (x);                                                                  \
-        if (r_ != ncclSuccess) return mfail(m, FM3D_ERR_HIP, std::string(#x ": ") + rccl().errStr(r_)); \
-    } while (0)
-
 void free_buffers(fm3d_mgpu* m) {
-    for (int d = 0; d < (int)m->send.size(); d++) {
-        hipSetDevice(m->devices[d]);
-        if (m->send[d]) hipFree(m->send[d]);
-        if (m->recv[d]) hipFree(m->recv[d]);
-        if (m->cntSend[d]) hipFree(m->cntSend[d]);
-        if (m->cntRecv[d]) hipFree(m->cntRecv[d]);
-        m->send[d] = m->recv[d] = nullptr;
-        m->cntSend[d] = m->cntRecv[d] = nullptr;
-    }
+    for (int k = 0; k < kSets; k++)
+        for (int d = 0; d < m->ndev; d++) {
+            hipSetDevice(m->devices[d]);
+            if (m->send[k][d]) hipFree(m->send[k][d]);
+            if (m->recv[k][d]) hipFree(m->recv[k][d]);
+            if (m->cntRecv[k][d]) hipFree(m->cntRecv[k][d]);
+            m->send[k][d] = m->recv[k][d] = nullptr;
+            m->cntRecv[k][d] = nullptr;
+        }
+    m->capDev = 0;
 }
 
 size_t row_bytes(int dim, int type) { return type == FM3D_DESC_F32 ? (size_t)dim * 4 : (size_t)dim; }
+
+// the device of block b: share b % shares lives on device share % ndev
+int device_of_block(const fm3d_mgpu* m, int64_t b) { return (int)((b % m->shares) % m->ndev); }
+
+// per-device query lists for nA queries; (re)allocates the exchange buffers when they grow
+int plan(fm3d_mgpu* m, int64_t nA) {
+    m->nA = nA;
+    m->idx.assign(m->ndev, {});
+    const int64_t nb = (nA + m->block - 1) / m->block;
+    for (int64_t b = 0; b < nb; b++) {
+        auto& v = m->idx[device_of_block(m, b)];
+        for (int64_t q = b * m->block; q < std::min<int64_t>((b + 1) * m->block, nA); q++) v.push_back((int32_t)q);
+    }
+    int64_t cap = 1;
+    for (auto& v : m->idx) cap = std::max<int64_t>(cap, (int64_t)v.size());
+    if (cap > m->capDev) {
+        free_buffers(m);
+        const size_t slot = (size_t)cap * sizeof(fm3d_record);
+        for (int k = 0; k < kSets; k++)
+            for (int d = 0; d < m->ndev; d++) {
+                MHIP(m, hipSetDevice(m->devices[d]));
+                MHIP(m, hipMalloc(&m->send[k][d], slot));
+                MHIP(m, hipMalloc(&m->recv[k][d], slot * m->ndev));
+                MHIP(m, hipMalloc((void**)&m->cntRecv[k][d], sizeof(int32_t) * m->ndev));
+            }
+        m->capDev = cap;
+    }
+    return FM3D_OK;
+}
+
+// device d's queries gathered into host arrays (local queryIdx = position in m->idx[d])
+void gather_device(fm3d_mgpu* m, int d, const void* descA, size_t rb, const fm3d_point2f* kpts1) {
+    const auto& ix = m->idx[d];
+    m->rowsA[d].resize(ix.size() * rb + 1);
+    m->kpA[d].resize(ix.size() + 1);
+    for (size_t i = 0; i < ix.size(); i++) {
+        std::memcpy(m->rowsA[d].data() + i * rb, (const uint8_t*)descA + (size_t)ix[i] * rb, rb);
+        m->kpA[d][i] = kpts1[ix[i]];
+    }
+}
+
+// the collectives of set k, queued on every device's pipeline stream behind its records
+int queue_allgather(fm3d_mgpu* m, int k) {
+    const size_t slot = (size_t)m->capDev * sizeof(fm3d_record);
+    RcclGroup g;
+    ncclResult_t r = g.start();
+    if (r != ncclSuccess) return mfail(m, FM3D_ERR_HIP, std::string("ncclGroupStart: ") + rccl().errStr(r));
+    for (int d = 0; d < m->ndev; d++) {
+        fm3d_ctx* c = m->ctx[k][d];
+        hipStream_t st = fm3d_internal_stream(c);
+        r = rccl().allGather(fm3d_internal_kept_dev(c), m->cntRecv[k][d], 1, ncclInt32, m->comms[d], st);
+        if (r == ncclSuccess) r = rccl().allGather(m->send[k][d], m->recv[k][d], slot, ncclUint8, m->comms[d], st);
+        if (r != ncclSuccess)
+            return mfail(m, FM3D_ERR_HIP, "ncclAllGather on device " + std::to_string(m->devices[d]) + ": " +
+                                              rccl().errStr(r));
+    }
+    r = g.end();
+    if (r != ncclSuccess) return mfail(m, FM3D_ERR_HIP, std::string("ncclGroupEnd: ") + rccl().errStr(r));
+    return FM3D_OK;
+}
+
+// wait for set k, then device 0's gathered records -> out in query order
+int finish_set(fm3d_mgpu* m, int k, fm3d_record* out, int cap, int* nKept, fm3d_pipeline_stats* stats) {
+    std::vector<fm3d_pipeline_stats> st(m->ndev);
+    std::vector<int> kept(m->ndev, 0);
+    int rc = FM3D_OK;
+    for (int d = 0; d < m->ndev; d++) {  // every device's finish runs, so none stays pending
+        int r = fm3d_internal_finish(m->ctx[k][d], &kept[d], &st[d]);
+        if (r && !rc) rc = mfail(m, r, "device " + std::to_string(m->devices[d]) + ": " + fm3d_last_error(m->ctx[k][d]));
+    }
+    m->pending[k] = false;
+    if (rc) return rc;
+    MHIP(m, hipSetDevice(m->devices[0]));
+    std::vector<int32_t> cnt(m->ndev);
+    MHIP(m, hipMemcpy(cnt.data(), m->cntRecv[k][0], sizeof(int32_t) * m->ndev, hipMemcpyDeviceToHost));
+    int64_t total = 0;
+    for (int d = 0; d < m->ndev; d++) {
+        if (cnt[d] != kept[d]) return mfail(m, FM3D_ERR_HIP, "all-gathered survivor count differs from the device's");
+        total += cnt[d];
+    }
+    if (total > cap) return mfail(m, FM3D_ERR_INVALID, "record buffer too small");
+    int64_t o = 0;
+    for (int d = 0; d < m->ndev; d++) {
+        if (!cnt[d]) continue;
+        const char* src = (const char*)m->recv[k][0] + (size_t)d * m->capDev * sizeof(fm3d_record);
+        MHIP(m, hipMemcpy(out + o, src, (size_t)cnt[d] * sizeof(fm3d_record), hipMemcpyDeviceToHost));
+        const auto& ix = m->idx[d];
+        int32_t prev = -1;
+        for (int i = 0; i < cnt[d]; i++) {
+            const int32_t l = out[o + i].queryIdx;
+            if (l < 0 || l >= (int32_t)ix.size() || l <= prev)
+                return mfail(m, FM3D_ERR_HIP, "a gathered record carries a bad local query index");
+            prev = l;
+            out[o + i].queryIdx = ix[l];
+        }
+        o += cnt[d];
+    }
+    // each device's list is in increasing query order and the query sets are disjoint
+    std::sort(out, out + o, [](const fm3d_record& a, const fm3d_record& b) { return a.queryIdx < b.queryIdx; });
+    if (nKept) *nKept = (int)o;
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        for (int d = 0; d < m->ndev; d++) {
+            stats->queries += st[d].queries;
+            stats->matches += st[d].matches;
+            stats->inliers += st[d].inliers;
+            stats->kept += st[d].kept;
+            stats->lm.evaluations += st[d].lm.evaluations;
+            stats->lm.pixel_evaluations += st[d].lm.pixel_evaluations;
+            stats->trains = std::max(stats->trains, st[d].trains);
+            // the slowest device (HIP events on its stream: submit -> records)
+            stats->total_ms = std::max(stats->total_ms, st[d].total_ms);
+            stats->lm_ms = std::max(stats->lm_ms, st[d].lm_ms);
+            stats->match_ms = std::max(stats->match_ms, st[d].match_ms);
+            stats->pyramid_ms = std::max(stats->pyramid_ms, st[d].pyramid_ms);
+        }
+        stats->lm.kernel_ms = stats->lm_ms;
+    }
+    return FM3D_OK;
+}
 
 }  // namespace
 
@@ -181,21 +323,20 @@ int fm3d_merge_shares(int nA, int shares, int block, const fm3d_record* const* r
 }
 
 int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int shares, int block, fm3d_mgpu** out) {
-    if (!s || !out || ndev <= 0 || shares < ndev || block < 0) return FM3D_ERR_INVALID;
+    if (!s || !out || ndev <= 0 || ndev > 16 || shares < ndev || block < 0) return FM3D_ERR_INVALID;
     *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
     fm3d_mgpu* m = new fm3d_mgpu();
     m->s = *s;
     m->ndev = ndev;
     m->shares = shares;
     m->block = block ? block : kDefaultBlock;
-    m->L = (shares + ndev - 1) / ndev;
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
     for (int d = 0; d < ndev; d++) {
         const int dev = devices ? devices[d] : d;
-        if (dev < 0 || dev >= count) {
+        if (dev < 0 || dev >= count || std::count(m->devices.begin(), m->devices.end(), dev)) {
             delete m;
-            return FM3D_ERR_INVALID;
+            return FM3D_ERR_INVALID;  // fewer devices visible than asked for, or a device twice
         }
         m->devices.push_back(dev);
     }
@@ -204,46 +345,36 @@ int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int s
         fm3d_mgpu_destroy(m);
         return FM3D_ERR_UNSUPPORTED;
     }
-    m->ctx.assign(shares, nullptr);
-    for (int j = 0; j < shares; j++) {
-        int r = fm3d_ctx_create(s, m->devices[j % ndev], &m->ctx[j]);
-        if (r) {
-            fm3d_mgpu_destroy(m);
-            return r;
+    for (int k = 0; k < kSets; k++)
+        for (int d = 0; d < ndev; d++) {
+            int r = fm3d_ctx_create(s, m->devices[d], &m->ctx[k][d]);
+            if (!r) r = fm3d_internal_prepare(m->ctx[k][d]);
+            if (r) {
+                fm3d_mgpu_destroy(m);
+                return r;
+            }
         }
-    }
     m->comms.assign(ndev, nullptr);
     if (rccl().commInitAll(m->comms.data(), ndev, m->devices.data()) != ncclSuccess) {
         fm3d_mgpu_destroy(m);
         return FM3D_ERR_HIP;
     }
-    m->streams.assign(ndev, nullptr);
-    m->send.assign(ndev, nullptr);
-    m->recv.assign(ndev, nullptr);
-    m->cntSend.assign(ndev, nullptr);
-    m->cntRecv.assign(ndev, nullptr);
-    for (int d = 0; d < ndev; d++) {
-        hipSetDevice(m->devices[d]);
-        if (hipStreamCreateWithFlags(&m->streams[d], hipStreamNonBlocking) != hipSuccess) {
-            fm3d_mgpu_destroy(m);
-            return FM3D_ERR_HIP;
-        }
-    }
+    m->rowsA.resize(ndev);
+    m->kpA.resize(ndev);
     *out = m;
     return FM3D_OK;
 }
 
 void fm3d_mgpu_destroy(fm3d_mgpu* m) {
     if (!m) return;
+    for (int k = 0; k < kSets; k++)
+        for (int d = 0; d < m->ndev; d++)
+            if (m->ctx[k][d]) hipStreamSynchronize(fm3d_internal_stream(m->ctx[k][d]));
     free_buffers(m);
-    for (size_t d = 0; d < m->streams.size(); d++)
-        if (m->streams[d]) {
-            hipSetDevice(m->devices[d]);
-            hipStreamDestroy(m->streams[d]);
-        }
     for (auto c : m->comms)
         if (c) rccl().commDestroy(c);
-    for (auto c : m->ctx) fm3d_ctx_destroy(c);
+    for (int k = 0; k < kSets; k++)
+        for (int d = 0; d < m->ndev; d++) fm3d_ctx_destroy(m->ctx[k][d]);
     delete m;
 }
 
@@ -251,10 +382,11 @@ const char* fm3d_mgpu_last_error(const fm3d_mgpu* m) { return m ? m->err.c_str()
 
 int fm3d_mgpu_set_g12(fm3d_mgpu* m, const double g12[16]) {
     if (!m || !g12) return FM3D_ERR_INVALID;
-    for (auto c : m->ctx) {
-        int r = fm3d_set_g12(c, g12);
-        if (r) return mfail(m, r, fm3d_last_error(c));
-    }
+    for (int k = 0; k < kSets; k++)
+        for (int d = 0; d < m->ndev; d++) {
+            int r = fm3d_set_g12(m->ctx[k][d], g12);
+            if (r) return mfail(m, r, fm3d_last_error(m->ctx[k][d]));
+        }
     return FM3D_OK;
 }
 
@@ -262,41 +394,17 @@ int fm3d_mgpu_pipeline_upload(fm3d_mgpu* m, const void* descA, int nA, const voi
                               const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1,
                               const uint8_t* img2, int width, int height) {
     if (!m || nA < 0 || nB < 0 || dim <= 0 || (nA && (!descA || !kpts1)) || !kpts2) return mfail(m, FM3D_ERR_INVALID, "bad argument");
+    if (m->pending[0] || m->pending[1]) return mfail(m, FM3D_ERR_INVALID, "a submitted frame pair is pending");
     const size_t rb = row_bytes(dim, type);
-    free_buffers(m);
     m->staged = false;
-    m->nA = nA;
-    m->cap = 1;
-    for (int j = 0; j < m->shares; j++) m->cap = std::max<int64_t>(m->cap, share_count(nA, m->shares, j, m->block));
-    m->nq.assign(m->shares, 0);
-    std::vector<int32_t> idx;
-    std::vector<uint8_t> a;
-    std::vector<fm3d_point2f> k1;
-    for (int j = 0; j < m->shares; j++) {
-        int n = 0;
-        fm3d_share_queries(nA, m->shares, j, m->block, nullptr, 0, &n);
-        m->nq[j] = n;
-        if (n == 0) continue;  // more shares than blocks: nothing to stage or run
-        idx.resize(n);
-        fm3d_share_queries(nA, m->shares, j, m->block, idx.data(), n, &n);
-        a.resize((size_t)n * rb + 1);
-        k1.resize((size_t)n + 1);
-        for (int i = 0; i < n; i++) {
-            std::memcpy(a.data() + (size_t)i * rb, (const uint8_t*)descA + (size_t)idx[i] * rb, rb);
-            k1[i] = kpts1[idx[i]];
-        }
-        int r = fm3d_pipeline_upload(m->ctx[j], a.data(), n, descB, nB, dim, type, k1.data(), kpts2, img1, img2, width,
-                                     height, 0);
-        if (r) return mfail(m, r, fm3d_last_error(m->ctx[j]));
-    }
-    const size_t slot = (size_t)m->cap * sizeof(fm3d_record);
+    int r;
+    if ((r = plan(m, nA))) return r;
     for (int d = 0; d < m->ndev; d++) {
-        hipSetDevice(m->devices[d]);
-        MHIP(m, hipMalloc(&m->send[d], slot * m->L));
-        MHIP(m, hipMalloc(&m->recv[d], slot * m->L * m->ndev));
-        MHIP(m, hipMalloc((void**)&m->cntSend[d], sizeof(int32_t) * m->L));
-        MHIP(m, hipMalloc((void**)&m->cntRecv[d], sizeof(int32_t) * m->L * m->ndev));
-        MHIP(m, hipMemset(m->cntSend[d], 0, sizeof(int32_t) * m->L));
+        gather_device(m, d, descA, rb, kpts1);
+        const int n = (int)m->idx[d].size();
+        r = fm3d_pipeline_upload(m->ctx[0][d], m->rowsA[d].data(), n, descB, nB, dim, type, m->kpA[d].data(), kpts2,
+                                 img1, img2, width, height, 0);
+        if (r) return mfail(m, r, fm3d_last_error(m->ctx[0][d]));
     }
     m->staged = true;
     return FM3D_OK;
@@ -304,78 +412,64 @@ int fm3d_mgpu_pipeline_upload(fm3d_mgpu* m, const void* descA, int nA, const voi
 
 int fm3d_mgpu_pipeline_run(fm3d_mgpu* m, fm3d_record* out, int* nKept, fm3d_pipeline_stats* stats) {
     if (!m || !m->staged) return mfail(m, FM3D_ERR_INVALID, "fm3d_mgpu_pipeline_upload not called");
-    const size_t slot = (size_t)m->cap * sizeof(fm3d_record);
-    std::vector<int> kept(m->shares, 0), rc(m->shares, 0);
-    std::vector<fm3d_pipeline_stats> st(m->shares);
-    std::vector<double> devMs(m->ndev, 0.0);
-    // one host thread per device; a device's shares run one after the other
+    if (m->pending[0] || m->pending[1]) return mfail(m, FM3D_ERR_INVALID, "a submitted frame pair is pending");
+    for (int d = 0; d < m->ndev; d++) {
+        int r = fm3d_internal_enqueue(m->ctx[0][d], (fm3d_record*)m->send[0][d]);
+        if (r) {
+            for (int e = 0; e < d; e++) fm3d_internal_finish(m->ctx[0][e], nullptr, nullptr);
+            return mfail(m, r, fm3d_last_error(m->ctx[0][d]));
+        }
+    }
+    m->pending[0] = true;
+    int r = queue_allgather(m, 0);
+    int r2 = finish_set(m, 0, out, (int)m->nA, nKept, stats);
+    return r ? r : r2;
+}
+
+int fm3d_mgpu_submit(fm3d_mgpu* m, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                     const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
+                     int width, int height) {
+    if (!m || nA < 0 || nB < 0 || dim <= 0 || (nA && (!descA || !kpts1)) || !kpts2) return mfail(m, FM3D_ERR_INVALID, "bad argument");
+    const int k = m->next;
+    if (m->pending[k]) return mfail(m, FM3D_ERR_INVALID, "both frame pairs in flight: fm3d_mgpu_wait first");
+    if (m->pending[k ^ 1] && nA != m->nA) return mfail(m, FM3D_ERR_INVALID, "frame pairs in flight must have the same query count");
+    const size_t rb = row_bytes(dim, type);
+    int r;
+    if (!m->pending[k ^ 1] && (r = plan(m, nA))) return r;
+    // one host thread per device: gather its queries, stage and queue its whole path
+    std::vector<int> rc(m->ndev, 0);
     std::vector<std::thread> th;
     for (int d = 0; d < m->ndev; d++)
-        th.emplace_back([m, d, slot, &kept, &rc, &st, &devMs]() {
-            for (int j = d, l = 0; j < m->shares; j += m->ndev, l++) {
-                fm3d_record* dst = (fm3d_record*)((char*)m->send[d] + (size_t)l * slot);
-                if (m->nq[j] == 0) continue;
-                rc[j] = fm3d_pipeline_run(m->ctx[j], dst, &kept[j], &st[j]);
-                if (rc[j]) return;
-                devMs[d] += st[j].total_ms;
-            }
+        th.emplace_back([&, d]() {
+            gather_device(m, d, descA, rb, kpts1);
+            rc[d] = fm3d_internal_submit_to(m->ctx[k][d], m->rowsA[d].data(), (int)m->idx[d].size(), descB, nB, dim,
+                                            type, m->kpA[d].data(), kpts2, img1, img2, width, height,
+                                            (fm3d_record*)m->send[k][d]);
         });
     for (auto& t : th) t.join();
-    for (int j = 0; j < m->shares; j++)
-        if (rc[j]) return mfail(m, rc[j], fm3d_last_error(m->ctx[j]));
-    // counts per slot (empty slots of the last device keep 0), then the RCCL all-gathers
-    for (int d = 0; d < m->ndev; d++) {
-        std::vector<int32_t> c(m->L, 0);
-        for (int j = d, l = 0; j < m->shares; j += m->ndev, l++) c[l] = kept[j];
-        hipSetDevice(m->devices[d]);
-        MHIP(m, hipMemcpyAsync(m->cntSend[d], c.data(), sizeof(int32_t) * m->L, hipMemcpyHostToDevice, m->streams[d]));
-        MHIP(m, hipStreamSynchronize(m->streams[d]));
+    int bad = -1;
+    for (int d = 0; d < m->ndev; d++)
+        if (rc[d] && bad < 0) bad = d;
+    if (bad >= 0) {
+        for (int d = 0; d < m->ndev; d++)
+            if (!rc[d]) fm3d_internal_finish(m->ctx[k][d], nullptr, nullptr);
+        return mfail(m, rc[bad], "device " + std::to_string(m->devices[bad]) + ": " + fm3d_last_error(m->ctx[k][bad]));
     }
-    MNCCL(m, rccl().groupStart());
-    for (int d = 0; d < m->ndev; d++) {
-        MNCCL(m, rccl().allGather(m->cntSend[d], m->cntRecv[d], (size_t)m->L, ncclInt32, m->comms[d], m->streams[d]));
-        MNCCL(m, rccl().allGather(m->send[d], m->recv[d], slot * m->L, ncclUint8, m->comms[d], m->streams[d]));
+    m->pending[k] = true;
+    if ((r = queue_allgather(m, k))) {
+        finish_set(m, k, nullptr, 0, nullptr, nullptr);
+        return r;
     }
-    MNCCL(m, rccl().groupEnd());
-    for (int d = 0; d < m->ndev; d++) {
-        hipSetDevice(m->devices[d]);
-        MHIP(m, hipStreamSynchronize(m->streams[d]));
-    }
-    // device 0's copy of every share's records -> host, merged in query order
-    hipSetDevice(m->devices[0]);
-    std::vector<int32_t> cnt((size_t)m->L * m->ndev);
-    MHIP(m, hipMemcpy(cnt.data(), m->cntRecv[0], sizeof(int32_t) * cnt.size(), hipMemcpyDeviceToHost));
-    std::vector<std::vector<fm3d_record>> part(m->shares);
-    std::vector<const fm3d_record*> ptrs(m->shares);
-    std::vector<int> counts(m->shares);
-    for (int j = 0; j < m->shares; j++) {
-        const int d = j % m->ndev, l = j / m->ndev;
-        const int c = cnt[(size_t)d * m->L + l];
-        if (c != kept[j]) return mfail(m, FM3D_ERR_HIP, "all-gathered survivor count differs from the share's");
-        part[j].resize((size_t)c + 1);
-        const char* src = (const char*)m->recv[0] + ((size_t)d * m->L + l) * slot;
-        if (c) MHIP(m, hipMemcpy(part[j].data(), src, (size_t)c * sizeof(fm3d_record), hipMemcpyDeviceToHost));
-        ptrs[j] = part[j].data();
-        counts[j] = c;
-    }
-    int n = 0;
-    int r = fm3d_merge_shares((int)m->nA, m->shares, m->block, ptrs.data(), counts.data(), out, &n);
-    if (r) return mfail(m, r, "merge of the gathered shares failed");
-    if (nKept) *nKept = n;
-    if (stats) {
-        std::memset(stats, 0, sizeof(*stats));
-        for (int j = 0; j < m->shares; j++) {
-            stats->queries += st[j].queries;
-            stats->matches += st[j].matches;
-            stats->inliers += st[j].inliers;
-            stats->kept += st[j].kept;
-            stats->lm.evaluations += st[j].lm.evaluations;
-            stats->lm.pixel_evaluations += st[j].lm.pixel_evaluations;
-        }
-        for (int j = 0; j < m->shares; j++) stats->trains = std::max(stats->trains, st[j].trains);
-        stats->total_ms = *std::max_element(devMs.begin(), devMs.end());  // the slowest device
-    }
+    m->next = k ^ 1;
     return FM3D_OK;
+}
+
+int fm3d_mgpu_wait(fm3d_mgpu* m, fm3d_record* out, int cap, int* nKept, fm3d_pipeline_stats* stats) {
+    if (!m) return FM3D_ERR_INVALID;
+    const int k = m->waitNext;
+    if (!m->pending[k]) return mfail(m, FM3D_ERR_INVALID, "no frame pair submitted (fm3d_mgpu_submit)");
+    m->waitNext = k ^ 1;
+    return finish_set(m, k, out, cap, nKept, stats);
 }
 
 }  // extern "C"

@@ -62,7 +62,7 @@ __device__ inline void dlt_nullvec(double* A, double* v) {
 // thread per match: gather, undistortPoints, cvTriangulatePoints, z filter.
 __global__ void triangulate_kernel(TriParams p) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p.K) return;
+    if (i >= (p.Kdev ? *p.Kdev : p.K)) return;  // the match count on the device (grid: its bound)
     const fm3d_dmatch mt = p.matches[i];
     const fm3d_point2f k1 = p.kp1[mt.queryIdx - p.queryOffset];
     const fm3d_point2f k2 = p.kp2[mt.trainIdx];
@@ -160,8 +160,18 @@ __global__ void plane_project_kernel(PlaneProjParams p) {
 // ---------------- stable compaction (three-phase scan) ----------------
 constexpr int kScanBlock = 1024;  // items per block (256 threads x 4)
 
-__global__ void scan_count_kernel(const int* __restrict__ flag, int n, int* __restrict__ blockSums) {
+// n: the item count, or its bound when nDev holds the count on the device (the grid is sized by
+// the bound; items past the count read as unflagged, so the extra blocks count 0)
+__device__ __forceinline__ int dev_count(const int* nDev, int n) {
+    if (!nDev) return n;
+    const int d = *nDev;
+    return d < n ? d : n;
+}
+
+__global__ void scan_count_kernel(const int* __restrict__ flag, int n, const int* __restrict__ nDev,
+                                  int* __restrict__ blockSums) {
     __shared__ int red[256];
+    n = dev_count(nDev, n);
     const int base = blockIdx.x * kScanBlock;
     int c = 0;
     for (int k = 0; k < 4; k++) {
@@ -224,8 +234,10 @@ __device__ inline int block_local_offset(const int* flag, int n, int base, int* 
 
 template <typename T>
 __global__ void scatter_kernel(const T* __restrict__ in, const int* __restrict__ flag, int n,
-                               const int* __restrict__ blockOff, T* __restrict__ out, int* __restrict__ srcIndex) {
+                               const int* __restrict__ nDev, const int* __restrict__ blockOff, T* __restrict__ out,
+                               int* __restrict__ srcIndex) {
     __shared__ int sh[256];
+    n = dev_count(nDev, n);
     const int base = blockIdx.x * kScanBlock;
     int c4, f[4];
     int o = blockOff[blockIdx.x] + block_local_offset(flag, n, base, sh, c4, f);
@@ -257,24 +269,25 @@ __global__ void offsets_kernel(const int* __restrict__ flag, int n, const int* _
 }
 
 template <typename T>
-void compact(const T* in, const int* flag, int n, T* out, int* count, int* srcIndex, void* tmp, hipStream_t s) {
+void compact(const T* in, const int* flag, int n, const int* nDev, T* out, int* count, int* srcIndex, void* tmp,
+             hipStream_t s) {
     const int nb = (n + kScanBlock - 1) / kScanBlock;
     int* blockSums = (int*)tmp;
     if (n <= 0) {
         hipMemsetAsync(count, 0, sizeof(int), s);
         return;
     }
-    scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, blockSums);
+    scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, nDev, blockSums);
     scan_blocks_kernel<<<1, 1024, 0, s>>>(blockSums, nb, count);
-    scatter_kernel<T><<<nb, 256, 0, s>>>(in, flag, n, blockSums, out, srcIndex);
+    scatter_kernel<T><<<nb, 256, 0, s>>>(in, flag, n, nDev, blockSums, out, srcIndex);
 }
 
 __global__ void make_records_kernel(const fm3d_dmatch* __restrict__ matches, const int* __restrict__ inlierSrc,
-                                    int nInl, const double* __restrict__ pts, const double* __restrict__ normals,
-                                    const int* __restrict__ status, fm3d_record* __restrict__ rec,
-                                    int* __restrict__ flag) {
+                                    int nInl, const int* __restrict__ nDev, const double* __restrict__ pts,
+                                    const double* __restrict__ normals, const int* __restrict__ status,
+                                    fm3d_record* __restrict__ rec, int* __restrict__ flag) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nInl) return;
+    if (i >= dev_count(nDev, nInl)) return;
     const fm3d_dmatch m = matches[inlierSrc[i]];
     fm3d_record r;
     r.queryIdx = m.queryIdx;
@@ -315,12 +328,12 @@ size_t scan_tmp_bytes(int n) { return sizeof(int) * ((size_t)(n + kScanBlock - 1
 
 void launch_compact_dmatch(const fm3d_dmatch* in, const int* flag, int n, fm3d_dmatch* out, int* count, void* tmp,
                            hipStream_t s) {
-    compact<fm3d_dmatch>(in, flag, n, out, count, nullptr, tmp, s);
+    compact<fm3d_dmatch>(in, flag, n, nullptr, out, count, nullptr, tmp, s);
 }
 
-void launch_compact_points(const double* in, const int* flag, int n, double* out, int* count, int* srcIndex,
-                           void* tmp, hipStream_t s) {
-    compact<Point3>((const Point3*)in, flag, n, (Point3*)out, count, srcIndex, tmp, s);
+void launch_compact_points(const double* in, const int* flag, int n, const int* nDev, double* out, int* count,
+                           int* srcIndex, void* tmp, hipStream_t s) {
+    compact<Point3>((const Point3*)in, flag, n, nDev, (Point3*)out, count, srcIndex, tmp, s);
 }
 
 void launch_exclusive_scan(const int* flag, int n, int* offsets, int* total, void* tmp, hipStream_t s) {
@@ -330,20 +343,21 @@ void launch_exclusive_scan(const int* flag, int n, int* offsets, int* total, voi
         hipMemsetAsync(total, 0, sizeof(int), s);
         return;
     }
-    scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, blockSums);
+    scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, nullptr, blockSums);
     scan_blocks_kernel<<<1, 1024, 0, s>>>(blockSums, nb, total);
     offsets_kernel<<<nb, 256, 0, s>>>(flag, n, blockSums, offsets);
 }
 
-void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int nInl, const double* pts,
+void launch_make_records(const fm3d_dmatch* matches, const int* inlierSrc, int nInl, const int* nDev, const double* pts,
                          const double* normals, const int* status, fm3d_record* rec, int* flag, hipStream_t s) {
     if (nInl <= 0) return;
-    make_records_kernel<<<(nInl + 255) / 256, 256, 0, s>>>(matches, inlierSrc, nInl, pts, normals, status, rec, flag);
+    make_records_kernel<<<(nInl + 255) / 256, 256, 0, s>>>(matches, inlierSrc, nInl, nDev, pts, normals, status, rec,
+                                                            flag);
 }
 
-void launch_compact_records(const fm3d_record* in, const int* flag, int n, fm3d_record* out, int* count, void* tmp,
-                            hipStream_t s) {
-    compact<fm3d_record>(in, flag, n, out, count, nullptr, tmp, s);
+void launch_compact_records(const fm3d_record* in, const int* flag, int n, const int* nDev, fm3d_record* out,
+                            int* count, void* tmp, hipStream_t s) {
+    compact<fm3d_record>(in, flag, n, nDev, out, count, nullptr, tmp, s);
 }
 
 }  // namespace fm3d

@@ -38,7 +38,7 @@ __device__ __forceinline__ double xor_sum(double v) {
 template <int KPW, bool FULL>
 __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     const int pt = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (pt >= p.P) return;
+    if (pt >= (p.Pdev ? *p.Pdev : p.P)) return;  // the inlier count on the device (pipeline), or P
     const double X0 = p.points[3 * pt], X1 = p.points[3 * pt + 1], X2 = p.points[3 * pt + 2];
     static const double Ident[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     static const double Zero[3] = {0, 0, 0};

@@ -76,6 +76,12 @@ def parse():
                          "--keypoints 10000 --seed 102 --nndr 0.8 --ray 32|64)")
     ap.add_argument("--nndr", type=float, default=0.55)
     ap.add_argument("--lm-waves", type=int, default=0)
+    ap.add_argument("--mode", choices=("stream", "resident"), default="stream",
+                    help="stream (C4 headline): every step a frame pair from host memory to host memory, "
+                         "--inflight pairs in flight; resident: inputs uploaded once, one step in flight")
+    ap.add_argument("--inflight", type=int, default=2, help="frame pairs in flight in the stream mode")
+    ap.add_argument("--mgpu", action="store_true",
+                    help="the one-process multi-GPU path (fm3d_mgpu, C5) also at --gpus 1 (its reference point)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the C5 byte-identity check against one GPU")
@@ -94,17 +100,332 @@ def records_digest(rec_bytes: bytes) -> str:
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     workload = args.workload
     if workload == "auto":
-        workload = "c5" if world > 1 and not args.weak else "c4"
+        workload = "c5" if (world > 1 or args.gpus > 1 or args.mgpu) and not args.weak else "c4"
     if args.weak:
         workload = "c4"
+    if world == 1 and (args.gpus > 1 or args.mgpu):
+        # the driver's `bench.py --gpus N` without a torchrun environment: this one process drives
+        # N GPUs through the C ABI's multi-GPU host (fm3d_mgpu)
+        return run_mgpu(args, workload)
     if workload == "c2":
         return run_c2(args)
     if workload == "c3":
         return run_c3(args)
+    if world == 1 and workload == "c4" and args.mode == "stream":
+        return run_c4_stream(args)
+    return run_resident(args, workload)
+
+
+def emit(out, args):
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+def lm_workload(args):
+    return {"pixelsRay": args.ray, "pyramids": args.levels}
+
+
+def c4_settings(fm3d, pair, args):
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon = args.nndr
+    s.pixelsRay = args.ray
+    s.pyramids = args.levels
+    s.lmWaves = args.lm_waves
+    return s
+
+
+def run_c4_stream(args):
+    """The headline (BASELINE configs[3], C4) as a stream of frame pairs, SURVEY.md §8(d)'s timed
+    region: every step takes one frame pair from host memory through the whole path and back --
+    H2D of descriptors, keypoints and both images (pinned staging), the a6 pyramids, match -> NNDR
+    -> DLT -> LM normals -> survivor records, D2H of the records -- with `inflight` frame pairs in
+    flight on as many contexts (one HIP stream each; fm3d_pipeline_submit / fm3d_pipeline_wait).
+    The next pair's front half and LM workgroups take the CUs the previous LM launch frees in its
+    tail, which a single launch leaves idle.  value = kept keypoints of the K timed
+    pairs / the host wall time of the K steps (fill and drain of the pipeline included)."""
+    import torch
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    synth = importlib.import_module("3dfeaturematcher_amd.synth")
+    wl = dict(WORKLOADS["c4"])
+    for k in ("keypoints", "width", "height"):
+        if getattr(args, k):
+            wl[k] = getattr(args, k)
+    t_gen = time.time()
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=args.seed, desc=args.desc)
+    t_gen = time.time() - t_gen
+    s = c4_settings(fm3d, pair, args)
+    nf = max(1, args.inflight)
+    streams = [torch.cuda.Stream(device=0) for _ in range(nf)]
+    ctxs, pipes = [], []
+    for st in streams:
+        ctx = fm3d.Context(s, device=0)
+        ctx.set_stream(st.cuda_stream)
+        fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
+        ctxs.append(ctx)
+        pipes.append(fm3d.Pipeline(ctx))
+    binary = args.desc == "orb"
+    bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(nf)]
+    inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+
+    def stream_run(n_steps, timed):
+        """n_steps frame pairs through the pipeline; returns per-pair (kept, stats, latency s, digest)."""
+        res = []
+        pend = [None] * nf
+        ends = [None] * nf
+        t_sub = [0.0] * nf
+
+        def drain(j):
+            rec, st = pipes[j].wait(bufs[j])
+            res.append((len(rec), st, time.perf_counter() - t_sub[j], records_digest(rec.tobytes())))
+            pend[j] = None
+            return rec
+
+        last = None
+        for k in range(n_steps):
+            j = k % nf
+            if pend[j] is not None:
+                last = drain(j)
+            t_sub[j] = time.perf_counter()
+            pipes[j].submit(*inputs, binary=binary)
+            if timed:
+                ends[j] = torch.cuda.Event(enable_timing=True)
+                ends[j].record(streams[j])
+            pend[j] = True
+        for k in range(n_steps, n_steps + nf):  # drain in submission order
+            j = k % nf
+            if pend[j] is not None:
+                last = drain(j)
+        return res, ends, last
+
+    stream_run(args.warmup, False)
+    torch.cuda.synchronize()
+    start = torch.cuda.Event(enable_timing=True)
+    start.record(streams[0])
+    for st in streams[1:]:
+        st.wait_stream(streams[0])
+    t0 = time.perf_counter()
+    res, ends, last_rec = stream_run(args.steps, True)
+    elapsed = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    span_ms = max(start.elapsed_time(e) for e in ends if e is not None)
+    kept_total = sum(r[0] for r in res)
+    stats = [r[1] for r in res]
+    lat = [r[2] * 1e3 for r in res]
+    digests = sorted(set(r[3] for r in res))
+    last_st = stats[-1]
+    # the same frame pair HBM-resident, one launch at a time (the pre-round-4 headline): inputs
+    # uploaded once, pipe.run() per step -- the per-launch roofline of lm2_kernel
+    res_steps = max(1, min(3, args.steps))
+    pipes[0].upload(*inputs, binary=binary)
+    pipes[0].run()
+    t1 = time.perf_counter()
+    rstats = [pipes[0].run()[1] for _ in range(res_steps)]
+    res_elapsed = time.perf_counter() - t1
+    for c in ctxs:
+        c.close()
+    pix = float(np.mean([st["lm"]["pixel_evaluations"] for st in stats]))
+    evals = float(np.mean([st["lm"]["evaluations"] for st in stats]))
+    cpu = None
+    if not args.no_cpu and args.desc == "sift":
+        cpu = cpu_baseline(pair, s, last_st, args)
+    rlm_ms = float(np.mean([st["lm_ms"] for st in rstats]))
+    roof = roofline(stats, span_ms / args.steps, pix, evals, args, pair, s)
+    roof.update({
+        "kernel": "fm3d::lm2_kernel (LM normal refinement), launches overlapped two at a time",
+        "avg_launch_ms": span_ms / args.steps,
+        "achieved_basis": (f"{FLOPS_PER_PIXEL_EVAL} flop x the pixel evaluations of the {args.steps} timed LM launches / "
+                           f"the device span of the timed region ({span_ms:.1f} ms, HIP events on the context "
+                           f"streams: first submit -> last pair's records); avg_launch_ms = that span / launches"),
+        "overlapped_launch_ms_each": float(np.mean([st["lm_ms"] for st in stats])),
+        "single_launch": {
+            "avg_launch_ms": rlm_ms,
+            "achieved": FLOPS_PER_PIXEL_EVAL * pix / (rlm_ms * 1e-3) / 1e12,
+            "frac": FLOPS_PER_PIXEL_EVAL * pix / (rlm_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+            "note": "one launch in flight (HBM-resident inputs, fm3d_pipeline_run), HIP events on its stream",
+        },
+    })
+    kp_k = wl["keypoints"] // 1000
+    desc = (f"C4: {kp_k}k SIFT-128 (u8) keypoints per {wl['width']}x{wl['height']} frame pair, full pipeline, "
+            f"pixelsRay {args.ray}, pyramids {args.levels}") if args.desc == "sift" else (
+            f"C3-like: {kp_k}k ORB-256 (Hamming) keypoints per {wl['width']}x{wl['height']} frame pair, NNDR "
+            f"{args.nndr}, full pipeline, pixelsRay {args.ray}, pyramids {args.levels}")
+    frame_s = elapsed / args.steps
+    out = {
+        "metric": METRIC,
+        "value": kept_total / elapsed,
+        "unit": "keypoints/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": frame_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (ray-cast facet scene, seeded; 3dfeaturematcher_amd/synth.py)",
+        "config": {
+            "workload": desc,
+            "keypoints_per_frame": wl["keypoints"], "width": wl["width"], "height": wl["height"],
+            "pixelsRay": args.ray, "pyramids": args.levels, "parallelism": "1 GPU",
+            "mode": f"stream: {nf} frame pairs in flight (one context + HIP stream each, fm3d_pipeline_submit/wait)",
+            "timed": ("per step, from host memory to host memory: H2D of descriptors, keypoints and images (pinned "
+                      "staging), pyramids (a6), match -> NNDR -> DLT -> LM normals -> survivor records, D2H of the "
+                      "records; the K steps' wall time includes filling and draining the pipeline"),
+        },
+        "latency_ms": {"mean": float(np.mean(lat)), "max": float(np.max(lat)),
+                       "note": "per frame pair, submit call -> its records on the host"},
+        "device_resident_value": sum(st["kept"] for st in rstats) / res_elapsed,
+        "device_resident_note": (f"the same pair, inputs HBM-resident, one step in flight ({res_steps} steps of "
+                                 f"fm3d_pipeline_run, {res_elapsed / res_steps * 1e3:.1f} ms each)"),
+        "input_keypoints_per_s": wl["keypoints"] / frame_s,
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "stages_ms": {k: last_st[k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "lm_ms", "total_ms")},
+        "h2d_pyramids_ms": last_st["pyramid_ms"],
+        "counts": {k: last_st[k] for k in ("queries", "matches", "inliers", "kept")},
+        "lm_profile": lm_profile(rstats[-1]["lm"]),
+        "lm_profile_overlapped": lm_profile(last_st["lm"]),
+        "setup_s": {"synthetic_generation": round(t_gen, 2)},
+        "records_sha256": digests[0] if len(digests) == 1 else digests,
+        "records_identical_across_steps": len(digests) == 1,
+    }
+    out.update(verify_against_fixture(args, wl, "c4", pair, last_rec))
+    if len(digests) != 1:
+        out["verified"] = False
+    emit(out, args)
+
+
+def run_mgpu(args, workload):
+    """`bench.py --gpus N` without a torchrun environment (the driver's command shape): this one
+    process drives N GPUs through the C ABI's multi-GPU host (fm3d_mgpu, csrc/fm3d_mgpu.cpp).  C5
+    (BASELINE configs[4]): ONE 1M-keypoint frame pair per step, its 4,096-query blocks dealt
+    round-robin over the N devices, one replica of frame B and the images per device and one pass
+    (one LM launch) per device, RCCL all-gather of the survivor records over xGMI, merged in query
+    order on the host; two frame pairs in flight (fm3d_mgpu_submit / fm3d_mgpu_wait), every step
+    from host memory to host memory as at one GPU.  Strong scaling: value = kept keypoints of the K
+    pairs / wall time.  Exits non-zero when fewer than N GPUs are visible."""
+    import torch
+    n = args.gpus
+    vis = torch.cuda.device_count()
+    if vis < n:
+        print(f"bench.py --gpus {n}: only {vis} GPU(s) visible", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    if workload != "c5":
+        print(f"bench.py --gpus {n}: the one-process multi-GPU run is C5 (--workload auto / c5); use torchrun "
+              f"for --weak or other workloads", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    synth = importlib.import_module("3dfeaturematcher_amd.synth")
+    wl = dict(WORKLOADS["c5"])
+    for k in ("keypoints", "width", "height"):
+        if getattr(args, k):
+            wl[k] = getattr(args, k)
+    t_gen = time.time()
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=args.seed, desc=args.desc)
+    t_gen = time.time() - t_gen
+    s = c4_settings(fm3d, pair, args)
+    mg = fm3d.MultiGPU(s, devices=list(range(n)), shares=n)
+    mg.set_g12(pair.g12)
+    binary = args.desc == "orb"
+    inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+    bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(2)]
+
+    def stream_run(n_steps):
+        res, pend, last = [], 0, None
+        t_sub = []
+        for k in range(n_steps):
+            if pend == 2:
+                rec, st = mg.wait(bufs[len(res) % 2])
+                res.append((len(rec), st, time.perf_counter() - t_sub[len(res)], records_digest(rec.tobytes())))
+                last, pend = rec, pend - 1
+            t_sub.append(time.perf_counter())
+            mg.submit(*inputs, binary=binary)
+            pend += 1
+        while pend:
+            rec, st = mg.wait(bufs[len(res) % 2])
+            res.append((len(rec), st, time.perf_counter() - t_sub[len(res)], records_digest(rec.tobytes())))
+            last, pend = rec, pend - 1
+        return res, last
+
+    stream_run(args.warmup)
+    t0 = time.perf_counter()
+    res, last_rec = stream_run(args.steps)
+    elapsed = time.perf_counter() - t0
+    mg.close()
+    kept_total = sum(r[0] for r in res)
+    stats = [r[1] for r in res]
+    lat = [r[2] * 1e3 for r in res]
+    digests = sorted(set(r[3] for r in res))
+    last_st = stats[-1]
+    frame_s = elapsed / args.steps
+    pix = float(np.mean([st["lm"]["pixel_evaluations"] for st in stats]))
+    kp_k = wl["keypoints"] // 1000
+    out = {
+        "metric": METRIC,
+        "value": kept_total / elapsed,
+        "unit": "keypoints/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": frame_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (ray-cast facet scene, seeded; 3dfeaturematcher_amd/synth.py)",
+        "config": {
+            "workload": (f"C5: one {kp_k}k-keypoint SIFT-128 (u8) frame pair ({wl['width']}x{wl['height']}, sub-pixel "
+                         f"keypoints) per step, full pipeline, pixelsRay {args.ray}, pyramids {args.levels}, query "
+                         f"blocks over {n} GPUs, RCCL all-gather of survivor records"),
+            "keypoints_per_frame": wl["keypoints"], "width": wl["width"], "height": wl["height"],
+            "pixelsRay": args.ray, "pyramids": args.levels,
+            "parallelism": (f"dp{n} in one process (fm3d_mgpu): 4,096-query blocks dealt round-robin over the "
+                            f"devices, one replica of frame B + images and one LM launch per device, RCCL "
+                            f"all-gather of counts + 64-B survivor records every step"),
+            "mode": "stream: 2 frame pairs in flight (fm3d_mgpu_submit / fm3d_mgpu_wait)",
+            "timed": ("per step, from host memory to host memory: per-device query gather + H2D (pinned), pyramids, "
+                      "match -> NNDR -> DLT -> LM -> records, RCCL all-gather, D2H of device 0's gathered "
+                      "records, host merge in query order"),
+        },
+        "latency_ms": {"mean": float(np.mean(lat)), "max": float(np.max(lat)),
+                       "note": "per frame pair, submit call -> merged records on the host"},
+        "input_keypoints_per_s": wl["keypoints"] / frame_s,
+        "roofline": {
+            "kernel": "fm3d::lm2_kernel on every device, launches overlapped two at a time",
+            "bound": "fp64-valu",
+            "achieved": FLOPS_PER_PIXEL_EVAL * pix / frame_s / 1e12,
+            "peak": FP64_PEAK_TFLOPS * n, "unit": "TFLOP/s",
+            "frac": FLOPS_PER_PIXEL_EVAL * pix / frame_s / 1e12 / (FP64_PEAK_TFLOPS * n),
+            "traffic": None,
+            "algorithmic": f"{FLOPS_PER_PIXEL_EVAL} flop x {pix:.4g} pixel evaluations per frame pair (all devices) "
+                           f"/ the wall time per step; peak = {n} x {FP64_PEAK_TFLOPS}",
+            "avg_launch_ms": frame_s * 1e3,
+        },
+        "cpu_baseline": None,
+        "stages_ms": {k: last_st[k] for k in ("match_ms", "lm_ms", "total_ms", "pyramid_ms")},
+        "counts": {k: last_st[k] for k in ("queries", "matches", "inliers", "kept")},
+        "setup_s": {"synthetic_generation": round(t_gen, 2)},
+        "records_sha256": digests[0] if len(digests) == 1 else digests,
+        "records_identical_across_steps": len(digests) == 1,
+    }
+    out.update(verify_against_fixture(args, wl, "c5", pair, last_rec))
+    if len(digests) != 1:
+        out["verified"] = False
+    emit(out, args)
+
+
+def run_resident(args, workload):
+    """Inputs uploaded once, one step in flight (fm3d_pipeline_run): --mode resident at one GPU, and
+    the torchrun route (WORLD_SIZE > 1: one process per GPU, C5 sharded or --weak)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     wl = dict(WORKLOADS[workload])
     for k in ("keypoints", "width", "height"):
         if getattr(args, k):

@@ -406,6 +406,18 @@ int fm3d_pipeline_upload(fm3d_ctx *ctx, const void *descA, int nA, const void *d
    recordsDev: device buffer with capacity nA records (NULL: internal); *nKept: survivors.
    Synchronises the context stream before returning. */
 int fm3d_pipeline_run(fm3d_ctx *ctx, fm3d_record *recordsDev, int *nKept, fm3d_pipeline_stats *stats);
+/* The same path for a stream of frame pairs (a serving loop keeps two contexts, i.e. two pairs, in
+   flight): fm3d_pipeline_submit stages one frame pair's inputs through page-locked buffers (H2D of
+   descriptors, keypoints and images, the pyramids) and queues match -> NNDR -> triangulate -> LM
+   normals -> survivor records on the context stream, then returns without waiting: every count
+   stays on the device and sizes nothing the host launches.  fm3d_pipeline_wait waits for it and
+   copies the survivor records to out (host, capacity cap; may be NULL); stats.pyramid_ms = the
+   inputs' H2D + pyramids, total_ms = submit to results.  One submit per context may be pending; the
+   other pipeline calls on that context fail with FM3D_ERR_INVALID until it is waited for. */
+int fm3d_pipeline_submit(fm3d_ctx *ctx, const void *descA, int nA, const void *descB, int nB, int dim, int type,
+                         const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1,
+                         const uint8_t *img2, int width, int height, int queryOffset);
+int fm3d_pipeline_wait(fm3d_ctx *ctx, fm3d_record *out, int cap, int *nKept, fm3d_pipeline_stats *stats);
 /* BASELINE.json's C2 ("brute-force L2 match + DLT triangulate only"): match -> NNDR -> triangulate on
    the staged inputs, no normals; *nInliers = the triangulated points kept by the z filter (stats:
    match / NNDR-compaction / triangulate / total HIP-event times). */
@@ -426,12 +438,14 @@ int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, f
 /* ---------------- several GPUs of one node, one process ---------------- */
 /* The reference runs main.cpp:91-155 in one process on one device; these calls are the same
    pipeline over ndev devices.  The queries split into `shares` logical shares (blocks of `block`
-   queries, 0 = 4096, dealt round-robin; share s runs on devices[s % ndev], shares >= ndev); frame B,
-   its keypoints and both images are replicated to every device; every device runs the whole path
-   on its shares; the survivor counts and 64-byte records are all-gathered with RCCL over xGMI
-   (ncclCommInitAll, ncclAllGather); the host merge (fm3d_merge_shares) returns the records in query
-   order, byte-identical to fm3d_pipeline_run of the whole frame pair.  devices may be NULL (0..ndev-1).
-   FM3D_ERR_UNSUPPORTED when RCCL (librccl.so.1) cannot be loaded. */
+   queries, 0 = 4096, dealt round-robin; share s belongs to devices[s % ndev], shares >= ndev).  Each
+   device holds ONE replica -- its shares' queries gathered in increasing order, frame B, its
+   keypoints and both images, staged once -- and runs the whole path over them in one pass (one LM
+   launch); the survivor counts and 64-byte records are all-gathered with RCCL over xGMI
+   (ncclCommInitAll, ncclAllGather, queued behind each device's records); the host merge returns the
+   records in query order, byte-identical to fm3d_pipeline_run of the whole frame pair.  devices may
+   be NULL (0..ndev-1); FM3D_ERR_INVALID when a device index is not visible (fewer GPUs than asked
+   for) or repeats; FM3D_ERR_UNSUPPORTED when RCCL (librccl.so.1) cannot be loaded. */
 typedef struct fm3d_mgpu fm3d_mgpu;
 int fm3d_mgpu_create(const fm3d_settings *s, int ndev, const int *devices, int shares, int block, fm3d_mgpu **out);
 void fm3d_mgpu_destroy(fm3d_mgpu *m);
@@ -441,9 +455,17 @@ int fm3d_mgpu_set_g12(fm3d_mgpu *m, const double g12[16]);
 int fm3d_mgpu_pipeline_upload(fm3d_mgpu *m, const void *descA, int nA, const void *descB, int nB, int dim, int type,
                               const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1,
                               const uint8_t *img2, int width, int height);
-/* out: host buffer, capacity nA records; stats: counts summed over the shares, total_ms = the
-   slowest device's pipeline time */
+/* out: host buffer, capacity nA records; stats: counts summed over the devices, total_ms / lm_ms =
+   the slowest device's */
 int fm3d_mgpu_pipeline_run(fm3d_mgpu *m, fm3d_record *out, int *nKept, fm3d_pipeline_stats *stats);
+/* A stream of frame pairs over the devices (two in flight, as fm3d_pipeline_submit / _wait on one
+   GPU): submit stages one frame pair on every device (host-asynchronous, one host thread per device)
+   and queues its path and all-gather; wait returns the oldest submitted pair's merged records (out:
+   capacity cap).  Pairs in flight together must have the same query count. */
+int fm3d_mgpu_submit(fm3d_mgpu *m, const void *descA, int nA, const void *descB, int nB, int dim, int type,
+                     const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1, const uint8_t *img2,
+                     int width, int height);
+int fm3d_mgpu_wait(fm3d_mgpu *m, fm3d_record *out, int cap, int *nKept, fm3d_pipeline_stats *stats);
 /* the block-cyclic partition: global query indices of share s (increasing); idx NULL asks for *n */
 int fm3d_share_queries(int nA, int shares, int s, int block, int32_t *idx, int cap, int *n);
 /* the merge (host only, no GPU): recs[s] holds counts[s] records of share s with LOCAL query

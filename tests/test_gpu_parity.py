@@ -477,7 +477,8 @@ def test_circular_neighborhoods_bitwise(fm3d, orc, pair, given_normals):
         ctx.close()
 
 
-@pytest.mark.parametrize("ray,hphi,htheta", [(16, 4, 4), (32, 8, 4), (8, 1, 3)])
+# (3, 4) and (5, 5): the partial instances (H 9..15 four hypotheses per wave, H 17..31 eight)
+@pytest.mark.parametrize("ray,hphi,htheta", [(16, 4, 4), (32, 8, 4), (8, 1, 3), (16, 3, 4), (16, 5, 5)])
 def test_ncc_hypotheses_bitwise(fm3d, orc, pair, ray, hphi, htheta):
     """NCC scoring of candidate normals (fm3d_ncc_hypotheses) on the GPU against the oracle, bit for
     bit: scores of every hypothesis, the best normal and its index (16 and 32 hypotheses, VGA bounds
@@ -837,20 +838,175 @@ def test_mgpu_one_device_shares_equal_pipeline_run(fm3d, synth, n, block, shares
         assert k > 50
 
 
-def test_principal_point_limit(fm3d, pair):
-    """a principal point on or outside the image's top/left edge (cx or cy < 1e-3) is
-    an explicit FM3D_ERR_UNSUPPORTED of computeOptimizedNormals, not a wrong
-    result."""
-    s = _settings(fm3d, pair.cam, pixelsRay=8)
-    s.Cx = 0.0
+@pytest.mark.parametrize("cx,cy", [(0.0, 0.0), (-0.0, -0.0), (-20.0, 10.0)])
+def test_principal_point_zero_and_negative(fm3d, orc, pair, cx, cy):
+    """computeOptimizedNormals with a principal point on or outside the image's
+    top/left edge (the reference has no limit there) -- bit-exact against the oracle, which runs the
+    reference's comparisons with the same camera.  The kernel's bit-pattern isPixelGood differs
+    from `0 <= u` only for u == -0.0, which only cx == -0.0 can produce; the host hands the kernel
+    +0.0 there (fm3d_host.cpp lm_camera)."""
+    import dataclasses
+    cam = dataclasses.replace(pair.cam, cx=cx, cy=cy)
+    q, t, _ = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    pts, _ = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, q, t)
+    # points around the optical axis: with cx = cy = 0 their neighbourhoods straddle u = 0 / v = 0
+    extra = np.array([[0.0, 0.0, 2.0], [1e-3, 1e-3, 2.0], [0.05, 0.02, 2.0], [0.2, 0.15, 2.1], [0.4, 0.3, 1.9]])
+    P = np.concatenate([np.abs(pts[:40]), extra])
+    s = _settings(fm3d, cam, pixelsRay=8, pyramids=1)
     ctx = fm3d.Context(s)
     try:
         sct = fm3d.SingleCameraTriangulator(ctx)
         sct.set_g12(pair.g12)
+        R2, t2 = sct.camera2()
         no = fm3d.NormalOptimizer(ctx, sct)
         no.setImages(pair.img1, pair.img2)
-        with pytest.raises(fm3d.Fm3dError) as e:
-            no.computeOptimizedNormals(np.array([[0.1, 0.1, 2.0]]))
-        assert e.value.code == fm3d.ERR_UNSUPPORTED
+        kept, normals = no.computeOptimizedNormals(P)
+        st, info, nfev = no.last_status, no.last_info, no.last_nfev
     finally:
         ctx.close()
+    ref = orc.optimize_normals(cam, R2, t2, pair.img1, pair.img2, 1, P, 8, mode=orc.DETMATH,
+                               nthreads=oracle_threads())
+    assert np.array_equal(st, ref["status"])
+    assert np.array_equal(info[:, :2], ref["info"][:, :2])
+    assert np.array_equal(nfev[:, :2], ref["nfev"][:, :2])
+    ok = ref["status"] == 0
+    assert np.array_equal(normals, ref["normals"][ok])
+    assert np.array_equal(kept, P[ok])
+    assert ok.sum() > 0
+
+
+def _pipe_ctx(fm3d, s, g12):
+    ctx = fm3d.Context(s)
+    fm3d.SingleCameraTriangulator(ctx).set_g12(g12)
+    return ctx, fm3d.Pipeline(ctx)
+
+
+def test_pipeline_submit_wait_stream_equals_run(fm3d, synth):
+    """fm3d_pipeline_submit / fm3d_pipeline_wait (the headline's stream: inputs from host memory,
+    device-side counts, two contexts in flight) give the records of fm3d_pipeline_run, byte for byte,
+    for two different frame pairs taken in turn; the pending guards fail loudly."""
+    pairs = [synth.make_frame_pair(3000, seed=11), synth.make_frame_pair(2500, seed=12)]
+    s = _settings(fm3d, pairs[0].cam, pixelsRay=12, pyramids=2)
+    ref = []
+    ctx, pipe = _pipe_ctx(fm3d, s, pairs[0].g12)
+    try:
+        for fp in pairs:
+            pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            k, st = pipe.run()
+            ref.append((pipe.records(k), st))
+    finally:
+        ctx.close()
+    cs = [_pipe_ctx(fm3d, s, pairs[0].g12) for _ in range(2)]
+    try:
+        got = []
+        order = [0, 1, 0, 1, 1]
+        pend = [None, None]
+        for i, w in enumerate(order):
+            j = i % 2
+            if pend[j] is not None:
+                got.append((pend[j], cs[j][1].wait()))
+            fp = pairs[w]
+            cs[j][1].submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            pend[j] = w
+        for i in range(len(order), len(order) + 2):
+            j = i % 2
+            got.append((pend[j], cs[j][1].wait()))
+        with pytest.raises(fm3d.Fm3dError):
+            cs[0][1].wait()  # nothing pending
+        fp = pairs[0]
+        cs[0][1].submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        with pytest.raises(fm3d.Fm3dError):
+            cs[0][1].run()  # a submit is pending
+        got.append((0, cs[0][1].wait()))
+    finally:
+        for c, _ in cs:
+            c.close()
+    assert len(got) == len(order) + 1
+    for w, (rec, st) in got:
+        assert rec.tobytes() == ref[w][0].tobytes()
+        for key in ("matches", "inliers", "kept"):
+            assert st[key] == ref[w][1][key]
+        assert st["lm"]["pixel_evaluations"] == ref[w][1]["lm"]["pixel_evaluations"]
+        assert st["pyramid_ms"] > 0 and st["total_ms"] >= st["lm_ms"]
+    assert len(ref[0][0]) > 50
+
+
+def test_pipeline_ncc_download_after_other_runs(fm3d, synth):
+    """fm3d_pipeline_ncc_download returns the rows of the last successful run_ncc,
+    even after a run_dlt / run on a larger pair (which rewrite the inlier count)."""
+    small, big = synth.make_frame_pair(1200, seed=41), synth.make_frame_pair(4000, seed=42)
+    s = _settings(fm3d, small.cam, pixelsRay=8)
+    ctx, pipe = _pipe_ctx(fm3d, s, small.g12)
+    try:
+        pipe.upload(small.desc1, small.desc2, small.kp1, small.kp2, small.img1, small.img2)
+        P1, _ = pipe.run_ncc(4, 4, 0.4)
+        sc1, nb1, b1 = pipe.ncc_results(P1, 16)
+        pipe.upload(big.desc1, big.desc2, big.kp1, big.kp2, big.img1, big.img2)
+        P2, _ = pipe.run_dlt()
+        assert P2 > P1 > 0
+        sc2, nb2, b2 = pipe.ncc_results(P1, 16)
+        pipe.run()
+        sc3, _, _ = pipe.ncc_results(P1, 16)
+    finally:
+        ctx.close()
+    assert np.array_equal(sc1, sc2) and np.array_equal(b1, b2) and np.array_equal(nb1, nb2, equal_nan=True)
+    assert np.array_equal(sc1, sc3)
+
+
+def test_mgpu_submit_wait_stream_equals_run(fm3d, synth):
+    """fm3d_mgpu_submit / fm3d_mgpu_wait (bench.py --gpus N's path) on one device with three logical
+    shares (one replica, one LM launch, RCCL all-gather, host merge): byte-identical to
+    fm3d_pipeline_run of the whole frame pair, pair after pair with two in flight."""
+    fp = synth.make_frame_pair(9000, seed=31)
+    s = _settings(fm3d, fp.cam, pixelsRay=12, pyramids=1)
+    ctx, pipe = _pipe_ctx(fm3d, s, fp.g12)
+    try:
+        pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        k, st = pipe.run()
+        full = pipe.records(k)
+    finally:
+        ctx.close()
+    mg = fm3d.MultiGPU(s, devices=[0], shares=3, block=1024)
+    try:
+        mg.set_g12(fp.g12)
+        outs = []
+        for i in range(4):
+            if i >= 2:
+                outs.append(mg.wait())
+            mg.submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        outs += [mg.wait(), mg.wait()]
+        with pytest.raises(fm3d.Fm3dError):
+            mg.wait()
+    finally:
+        mg.close()
+    assert k > 50
+    for rec, mst in outs:
+        assert rec.tobytes() == full.tobytes()
+        assert mst["kept"] == k and mst["inliers"] == st["inliers"]
+
+
+def test_mgpu_more_devices_than_visible_fails(fm3d, pair):
+    """fm3d_mgpu_create over more devices than the box has: FM3D_ERR_INVALID, never a silent
+    one-GPU run (bench.py --gpus N relies on it)."""
+    s = _settings(fm3d, pair.cam)
+    import torch
+    vis = torch.cuda.device_count()
+    with pytest.raises(fm3d.Fm3dError) as e:
+        fm3d.MultiGPU(s, devices=list(range(vis + 1)))
+    assert e.value.code == fm3d.ERR_INVALID
+
+
+def test_bench_gpus_more_than_visible_exits_nonzero():
+    """`bench.py --gpus N` with fewer than N GPUs visible exits non-zero with a clear
+    message, never a one-GPU line labelled otherwise."""
+    import os
+    import subprocess
+    import sys
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = torch.cuda.device_count() + 1
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--steps", "1", "--warmup",
+                        "0", "--no-cpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert f"--gpus {n}" in r.stderr and "visible" in r.stderr
+    assert '"metric"' not in r.stdout
