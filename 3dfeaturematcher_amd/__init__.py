@@ -42,7 +42,7 @@ EXPORTS = (
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
-    "fm3d_mgpu_submit", "fm3d_mgpu_wait",
+    "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link",
 )
 
 
@@ -821,6 +821,10 @@ class Pipeline:
                                                   a.shape[1], _desc_type(a, binary), _vp(k1), _vp(k2),
                                                   _ptr(i1, ctypes.c_uint8), _ptr(i2, ctypes.c_uint8), w, h,
                                                   query_offset))
+
+    def link(self, leader: "Pipeline"):
+        """fm3d_pipeline_link(self, leader): this context's pairs join the leader's LM launches."""
+        self.ctx.check(lib().fm3d_pipeline_link(self.ctx.handle, leader.ctx.handle))
 
     def wait(self, out: np.ndarray | None = None):
         """fm3d_pipeline_wait: (survivor records (host), stats dict) of the submitted frame pair.  out: a

@@ -79,8 +79,9 @@ struct HostBuf {
 
 // the pipeline's small device -> host results of one frame pair (one D2H, pinned)
 struct PipeSmall {
-    int32_t cnt[4];                 // matches K, inliers P, kept, pad
-    unsigned long long lm[26];      // the LM kernel's counters (fm3d_lm2.hip statPass layout)
+    int32_t cnt[4];                 // matches K, inliers P, kept, pad (c->pcnt bytes 0..15)
+    unsigned long long prob[2];     // this pair's residual / pixel evaluations (c->pcnt bytes 16..31)
+    unsigned long long lm[26];      // the LM launch's counters (fm3d_lm2.hip statPass layout)
 };
 
 }  // namespace
@@ -137,6 +138,13 @@ struct fm3d_ctx {
     hipEvent_t evStage = nullptr;  // after the last H2D copy from the staging buffers
     hipEvent_t evProj = nullptr;   // after the last H2D copy of the LM constants (hProj)
     bool pending = false;          // a fm3d_pipeline_submit awaiting fm3d_pipeline_wait
+    // fm3d_pipeline_link: a member's submit queues its front half only; the leader's next submit
+    // queues ONE LM launch over both pairs' points and the member's records behind it
+    fm3d_ctx* linkLeader = nullptr;  // (member) the context that launches its LM
+    fm3d_ctx* linkMember = nullptr;  // (leader) the context whose pair joins its launches
+    bool frontOnly = false;          // (member) submitted, its LM not queued yet
+    hipEvent_t evFront = nullptr;    // (member) after its front half
+    hipEvent_t evLm = nullptr;       // (leader) after a joint LM launch
     fm3d_lm_stats subLm{};         // the pending submit's LM launch data
     fm3d_record* pendOut = nullptr;  // the device records of the pending / last run
     // staged pipeline inputs
@@ -593,36 +601,65 @@ fm3d::Camera lm_camera(const fm3d::Camera& cam) {
     return k;
 }
 
-// LM normals over the device points c->pts, outputs in c->lm*.  P: the point count, or its bound
-// when Pdev holds the count on the device (the pipeline: no host sync before the launch)
-int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
+// One frame pair's points for an LM launch: its context (pyramids c->lvlDesc, pose c->R2/t2,
+// outputs c->lm*, per-pair counters c->pcnt + 16 bytes) and the points (c->pts): P of them, or
+// P their bound when Pdev holds the count on the device (the pipeline: no host sync)
+struct LMSrc {
+    fm3d_ctx* c;
+    int P;
+    const int* Pdev;
+};
+
+// LM normals over the points of nProb frame pairs in ONE launch on c's stream (c's slabs, queue
+// and launch counters): the slots that find one pair's points used up take the next pair's, so
+// a second pair fills the launch's end-of-queue tail (fm3d_pipeline_link).  Every problem's
+// context must be ordered before this stream by the caller (its points, pyramids).
+int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
     int r;
+    if (nProb < 1 || nProb > fm3d::kLMMaxProblems) return fail(c, FM3D_ERR_INVALID, "bad LM problem count");
     if ((r = ensure_offsets(c))) return r;
-    if (c->pyr1.empty()) return fail(c, FM3D_ERR_INVALID, "fm3d_set_images (NormalOptimizer::setImages) not called");
-    if (!c->haveG12) return fail(c, FM3D_ERR_INVALID, "g12 not set (SingleCameraTriangulator::setg12)");
     const fm3d::Camera cam = lm_camera(c->cam);
     const int levels = c->s.pyramids;
-    HIPCHK(c, c->lmNormals.ensure((size_t)(P + 1) * 3 * sizeof(double)));
-    HIPCHK(c, c->lmStatus.ensure((size_t)(P + 1) * sizeof(int)));
-    HIPCHK(c, c->lmInfo.ensure((size_t)(P + 1) * 8 * sizeof(int)));
-    HIPCHK(c, c->lmNfev.ensure((size_t)(P + 1) * 8 * sizeof(int)));
-    HIPCHK(c, c->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
+    long Ptot = 0;
+    for (int j = 0; j < nProb; j++) {
+        fm3d_ctx* q = src[j].c;
+        if (q->pyr1.empty()) return fail(c, FM3D_ERR_INVALID, "fm3d_set_images (NormalOptimizer::setImages) not called");
+        if (!q->haveG12) return fail(c, FM3D_ERR_INVALID, "g12 not set (SingleCameraTriangulator::setg12)");
+        if (q != c && (q->device != c->device || q->s.pyramids != levels || q->s.pixelsRay != c->s.pixelsRay ||
+                       std::memcmp(&q->cam, &c->cam, sizeof(c->cam)) != 0 || q->s.boundWidth != c->s.boundWidth ||
+                       q->s.boundHeight != c->s.boundHeight || q->s.zThresholdMax != c->s.zThresholdMax ||
+                       q->s.epsilonLMMIN != c->s.epsilonLMMIN))
+            return fail(c, FM3D_ERR_INVALID, "linked contexts need one device, camera and LM settings");
+        const int P = src[j].P;
+        HIPCHK(c, q->lmNormals.ensure((size_t)(P + 1) * 3 * sizeof(double)));
+        HIPCHK(c, q->lmStatus.ensure((size_t)(P + 1) * sizeof(int)));
+        HIPCHK(c, q->lmInfo.ensure((size_t)(P + 1) * 8 * sizeof(int)));
+        HIPCHK(c, q->lmNfev.ensure((size_t)(P + 1) * 8 * sizeof(int)));
+        HIPCHK(c, q->lmMdat.ensure((size_t)(P + 1) * sizeof(int)));
+        HIPCHK(c, q->pcnt.ensure(64));
+        Ptot += P;
+    }
     HIPCHK(c, c->lmQueue.ensure(64 * sizeof(int)));
     HIPCHK(c, c->lmStat.ensure(256));
     // persistent workgroups of fm3d::kLM2Slots term waves (one point each) + a chain wave;
     // slots refill from the queue (fm3d_lm2.hip)
     const int slots = fm3d::kLM2Slots;
-    const void* kptr = reinterpret_cast<const void*>(fm3d::lm2_kernel);
+    // one pose for all problems: the single-pose kernel (entry 0 of the table serves them all)
+    bool multiPose = false;
+    for (int j = 1; j < nProb; j++)
+        multiPose |= std::memcmp(src[j].c->R2, src[0].c->R2, sizeof(c->R2)) != 0 ||
+                     std::memcmp(src[j].c->t2, src[0].c->t2, sizeof(c->t2)) != 0;
+    const void* kptr = multiPose ? reinterpret_cast<const void*>(fm3d::lm2_kernel<true>)
+                                 : reinterpret_cast<const void*>(fm3d::lm2_kernel<false>);
     long groups = c->s.lmWaves;
     if (groups <= 0) {
-        int dev = 0, cus = 0, perCU = 0;
-        HIPCHK(c, hipGetDevice(&dev));
-        HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        int cus = 0, perCU = 0;
+        HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kptr, fm3d::kLM2Threads, 0));
         if (perCU < 1) perCU = 1;
         groups = (long)cus * perCU;
     }
-    const long needed = (P + slots - 1) / slots;
+    const long needed = (Ptot + slots - 1) / slots;
     if (groups > needed) groups = needed;
     const size_t ents = (size_t)c->nOffPad * slots;
     // per slot and entry: rays (2 doubles) + I1, fvec dI, two Jacobian dI (float) + compact index
@@ -639,32 +676,48 @@ int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t
     HIPCHK(c, c->slab.ensure(ents * 2 * sizeof(double) * groups + 16384));
     HIPCHK(c, c->slabI1.ensure(ents * 5 * 4 * groups + 16384));
     fm3d::LMParams p{};
-    p.points = c->pts.as<double>();
-    p.P = P;
-    p.Pdev = Pdev;
+    p.nProb = nProb;
     p.cam = cam;
-    std::memcpy(p.R2, c->R2, sizeof(p.R2));
-    std::memcpy(p.t2, c->t2, sizeof(p.t2));
-    {   // the same constants as a small global table (re-read per chunk by the LM kernel)
-        HIPCHK(c, hipEventSynchronize(c->evProj));  // the previous launch's copy out of hProj ran
-        HIPCHK(c, c->hProj.ensure(sizeof(fm3d::ProjConst)));
-        fm3d::ProjConst& pc = *c->hProj.as<fm3d::ProjConst>();  // pinned: the copy may run later
-        std::memcpy(pc.R, c->R2, sizeof(pc.R));
-        std::memcpy(pc.t, c->t2, sizeof(pc.t));
-        pc.cam = cam;
+    {   // per problem: its pose as a small global table (re-read per chunk by the LM kernel), and
+        // the problem table; both from pinned memory (the copies may run after this returns)
+        HIPCHK(c, hipEventSynchronize(c->evProj));  // the previous launch's copies out of hProj ran
+        const size_t pcBytes = (sizeof(fm3d::ProjConst) + 255) / 256 * 256;
+        HIPCHK(c, c->hProj.ensure(pcBytes * nProb + sizeof(fm3d::LMProblem) * nProb));
+        char* hp = c->hProj.as<char>();
+        fm3d::LMProblem* hpr = (fm3d::LMProblem*)(hp + pcBytes * nProb);
+        HIPCHK(c, c->lmProj.ensure(pcBytes * nProb + sizeof(fm3d::LMProblem) * nProb));
         const size_t Gn = (size_t)groups * slots * c->nOffPad;  // entries per slab array
-        pc.slabRX = (const char*)c->slab.p;
-        pc.slabRY = FM3D_RAY_AOS ? pc.slabRX + sizeof(double) : pc.slabRX + Gn * sizeof(double);
-        pc.slabI1 = (const char*)c->slabI1.p;
-        pc.slabDF = (char*)c->slabI1.p + Gn * 4;
-        pc.slabDJ0 = pc.slabDF + Gn * 4;
-        pc.slabDJ1 = pc.slabDJ0 + Gn * 4;
-        HIPCHK(c, c->lmProj.ensure(sizeof(pc)));
-        HIPCHK(c, hipMemcpyAsync(c->lmProj.p, &pc, sizeof(pc), hipMemcpyHostToDevice, c->stream));
+        for (int j = 0; j < nProb; j++) {
+            fm3d_ctx* q = src[j].c;
+            fm3d::ProjConst& pc = *(fm3d::ProjConst*)(hp + pcBytes * j);
+            std::memcpy(pc.R, q->R2, sizeof(pc.R));
+            std::memcpy(pc.t, q->t2, sizeof(pc.t));
+            pc.cam = cam;
+            pc.slabRX = (const char*)c->slab.p;
+            pc.slabRY = FM3D_RAY_AOS ? pc.slabRX + sizeof(double) : pc.slabRX + Gn * sizeof(double);
+            pc.slabI1 = (const char*)c->slabI1.p;
+            pc.slabDF = (char*)c->slabI1.p + Gn * 4;
+            pc.slabDJ0 = pc.slabDF + Gn * 4;
+            pc.slabDJ1 = pc.slabDJ0 + Gn * 4;
+            fm3d::LMProblem& pr = hpr[j];
+            pr.points = q->pts.as<double>();
+            pr.Pdev = src[j].Pdev;
+            pr.P = src[j].P;
+            pr.lvl = q->lvlDesc.as<LevelDesc>();
+            pr.normals = q->lmNormals.as<double>();
+            pr.status = q->lmStatus.as<int>();
+            pr.info = q->lmInfo.as<int>();
+            pr.nfev = q->lmNfev.as<int>();
+            pr.mdat = q->lmMdat.as<int>();
+            pr.stat = (unsigned long long*)(q->pcnt.as<char>() + 16);
+            pr.projOff = (unsigned)(pcBytes * j);
+        }
+        HIPCHK(c, hipMemcpyAsync(c->lmProj.p, hp, pcBytes * nProb + sizeof(fm3d::LMProblem) * nProb,
+                                 hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipEventRecord(c->evProj, c->stream));
         p.proj = c->lmProj.as<fm3d::ProjConst>();
+        p.prob = (const fm3d::LMProblem*)(c->lmProj.as<char>() + pcBytes * nProb);
     }
-    p.lvl = c->lvlDesc.as<LevelDesc>();
     p.levels = levels;
     p.offsets = c->offsets.as<int2>();
     p.nOff = c->nOff;
@@ -677,11 +730,6 @@ int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t
     p.slab = c->slab.as<double>();
     p.slabI1 = c->slabI1.as<float>();
     p.nWaves = groups;
-    p.normals = c->lmNormals.as<double>();
-    p.status = c->lmStatus.as<int>();
-    p.info = c->lmInfo.as<int>();
-    p.nfev = c->lmNfev.as<int>();
-    p.mdat = c->lmMdat.as<int>();
     p.statEval = c->lmStat.as<unsigned long long>();
     p.statPix = c->lmStat.as<unsigned long long>() + 1;
     p.overflow = (int*)(c->lmStat.as<unsigned long long>() + 2);
@@ -689,11 +737,10 @@ int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t
     c->lmGroups = groups;
     {   // guards against a broken state machine (never expected to trigger): passes per slot
         // <= its points x levels x (300 evaluations + QR passes), and a wall-clock limit
-        const long long perSlot = (P + groups * slots - 1) / (groups * slots) + 1;
+        const long long perSlot = (Ptot + groups * slots - 1) / (groups * slots) + 1;
         p.maxIter = perSlot * (long long)(levels + 1) * 1600 + 10000;
-        int dev = 0, khz = 0;
-        HIPCHK(c, hipGetDevice(&dev));
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
         const char* ms = getenv("FM3D_LM_MAX_SECONDS");  // watchdog (tests lower it; fractions allowed)
         const double secs = ms && atof(ms) > 0 ? atof(ms) : 300.;
         p.maxTicks = (long long)((double)khz * 1000. * secs);
@@ -705,24 +752,40 @@ int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t
     }
     // the counters (incl. the overflow word) are reset for every call, also for P == 0
     HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 256, c->stream));
-    if (P > 0) {
+    for (int j = 0; j < nProb; j++) HIPCHK(c, hipMemsetAsync(src[j].c->pcnt.as<char>() + 16, 0, 16, c->stream));
+    if (Ptot > 0) {
         HIPCHK(c, hipEventRecord(e0, c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64 * sizeof(int), c->stream));
         HIPCHK(c, hipMemsetAsync(c->lmStat.as<unsigned long long>() + 20, 0xff, 8, c->stream));  // min start
-        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->lmStatus.p, fm3d::kLMRunning, P, c->stream));
-        HIPCHK(c, hipMemsetAsync(c->lmInfo.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
-        HIPCHK(c, hipMemsetAsync(c->lmNfev.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
+        for (int j = 0; j < nProb; j++) {
+            fm3d_ctx* q = src[j].c;
+            const int P = src[j].P;
+            if (P <= 0) continue;
+            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)q->lmStatus.p, fm3d::kLMRunning, P, c->stream));
+            HIPCHK(c, hipMemsetAsync(q->lmInfo.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
+            HIPCHK(c, hipMemsetAsync(q->lmNfev.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
+        }
         // one launch: every slot runs its point through all levels, coarsest first
         // (optimize_pyramid :225-241)
-        hipLaunchKernelGGL(fm3d::lm2_kernel, dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream, p);
+        if (multiPose)
+            hipLaunchKernelGGL(fm3d::lm2_kernel<true>, dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream, p);
+        else
+            hipLaunchKernelGGL(fm3d::lm2_kernel<false>, dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream,
+                               p);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(e1, c->stream));
     }
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
-        stats->points_in = P;
+        stats->points_in = Ptot;
     }
     return FM3D_OK;
+}
+
+// LM normals over c's own points (c->pts: P, or the bound P with the count at Pdev)
+int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
+    const LMSrc one{c, P, Pdev};
+    return run_lm_multi(c, &one, 1, stats, e0, e1);
 }
 
 // the two images into pinned staging and their pyramids (pyrDown chain) on the context stream;
@@ -1561,6 +1624,8 @@ int fm3d_ctx_create(const fm3d_settings* s, int device, fm3d_ctx** out) {
     for (auto& e : c->ev) hipEventCreate(&e);
     hipEventCreateWithFlags(&c->evStage, hipEventDisableTiming);
     hipEventCreateWithFlags(&c->evProj, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->evFront, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->evLm, hipEventDisableTiming);
     c->cam.fx = s->Fx;
     c->cam.fy = s->Fy;
     c->cam.cx = s->Cx;
@@ -1598,6 +1663,10 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
     for (HostBuf* b : hbufs) b->release();
     hipEventDestroy(c->evStage);
     hipEventDestroy(c->evProj);
+    hipEventDestroy(c->evFront);
+    hipEventDestroy(c->evLm);
+    if (c->linkLeader) c->linkLeader->linkMember = nullptr;
+    if (c->linkMember) c->linkMember->linkLeader = nullptr;
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();
     for (auto& e : c->ev) hipEventDestroy(e);
@@ -1900,17 +1969,11 @@ int pipeline_front(fm3d_ctx* c) {
     return FM3D_OK;
 }
 
-// the whole path on the staged inputs, queued on the context stream: front half, LM normals over
-// the device-counted inliers (a6-a15; the pyramids were built at staging: images are inputs of the
-// path), survivor records (compacted into out, or the internal buffer), then one D2H of the counts
-// and the LM counters into pinned memory.  Nothing here waits for the device.
-int enqueue_full(fm3d_ctx* c, fm3d_record* out, fm3d_lm_stats* ls) {
+// the survivor records of c's pair (after its LM normals, in stream order), then one D2H of the
+// counts, the pair's LM counters and the LM launch's counters (lmStat: the launching context's)
+int enqueue_epilogue(fm3d_ctx* c, fm3d_record* out, const void* lmStat) {
     const int nA = c->stNA;
-    hipEvent_t* ev = c->ev;
-    int r;
-    if ((r = pipeline_front(c))) return r;
     int* cnt = c->pcnt.as<int>();
-    if ((r = run_lm(c, nA, cnt + 1, ls, ev[6], ev[7]))) return r;
     HIPCHK(c, c->recTmp.ensure((size_t)(nA + 1) * sizeof(fm3d_record)));
     HIPCHK(c, c->recFlag.ensure((size_t)(nA + 1) * sizeof(int)));
     if (!out) {
@@ -1926,9 +1989,42 @@ int enqueue_full(fm3d_ctx* c, fm3d_record* out, fm3d_lm_stats* ls) {
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, c->hSmall.ensure(sizeof(PipeSmall)));
     PipeSmall* hs = c->hSmall.as<PipeSmall>();
-    HIPCHK(c, hipMemcpyAsync(hs->cnt, cnt, sizeof(hs->cnt), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(hs->lm, c->lmStat.p, sizeof(hs->lm), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    HIPCHK(c, hipMemcpyAsync(hs->cnt, cnt, sizeof(hs->cnt) + sizeof(hs->prob), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(hs->lm, lmStat, sizeof(hs->lm), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    return FM3D_OK;
+}
+
+// the whole path on the staged inputs, queued on the context stream: front half, LM normals over
+// the device-counted inliers (a6-a15; the pyramids were built at staging: images are inputs of the
+// path), survivor records (compacted into out, or the internal buffer), then one D2H of the counts
+// and the LM counters into pinned memory.  Nothing here waits for the device.
+int enqueue_full(fm3d_ctx* c, fm3d_record* out, fm3d_lm_stats* ls) {
+    int r;
+    if ((r = pipeline_front(c))) return r;
+    if ((r = run_lm(c, c->stNA, c->pcnt.as<int>() + 1, ls, c->ev[6], c->ev[7]))) return r;
+    return enqueue_epilogue(c, out, c->lmStat.p);
+}
+
+// the leader's pair with its member's queued front half: ONE LM launch over both pairs' points on
+// the leader's stream (after the member's front half), then each pair's records on its own stream
+int enqueue_linked(fm3d_ctx* c, fm3d_ctx* m, fm3d_lm_stats* ls) {
+    int r;
+    if ((r = pipeline_front(c))) return r;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, m->evFront, 0));
+    const LMSrc src[2] = {{m, m->stNA, m->pcnt.as<int>() + 1}, {c, c->stNA, c->pcnt.as<int>() + 1}};
+    HIPCHK(c, hipEventRecord(m->ev[6], c->stream));
+    if ((r = run_lm_multi(c, src, 2, ls, c->ev[6], c->ev[7]))) return r;
+    HIPCHK(c, hipEventRecord(m->ev[7], c->stream));
+    HIPCHK(c, hipEventRecord(c->evLm, c->stream));
+    m->subLm = *ls;
+    m->lmGroups = c->lmGroups;
+    m->wallKhz = c->wallKhz;
+    if ((r = enqueue_epilogue(c, nullptr, c->lmStat.p))) return r;
+    hipSetDevice(m->device);
+    HIPCHK(m, hipStreamWaitEvent(m->stream, c->evLm, 0));
+    if ((r = enqueue_epilogue(m, nullptr, c->lmStat.p))) return r;
+    m->frontOnly = false;
     return FM3D_OK;
 }
 
@@ -1976,8 +2072,8 @@ int finalize_full(fm3d_ctx* c, const fm3d_lm_stats& ls, hipEvent_t t0, bool stag
         stats->lm = ls;
         stats->lm.points_in = P;
         stats->lm.points_kept = kept;
-        stats->lm.evaluations = (int64_t)hs->lm[0];
-        stats->lm.pixel_evaluations = (int64_t)hs->lm[1];
+        stats->lm.evaluations = (int64_t)hs->prob[0];  // this pair's (a launch may hold two)
+        stats->lm.pixel_evaluations = (int64_t)hs->prob[1];
         stats->lm.kernel_ms = stats->lm_ms;
         fill_lm_cycles(c, hs->lm, &stats->lm);
     }
@@ -2020,8 +2116,27 @@ int fm3d_pipeline_submit(fm3d_ctx* c, const void* descA, int nA, const void* des
     if ((r = stage_pipeline(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, queryOffset)))
         return r;
     c->subLm = fm3d_lm_stats{};
-    if ((r = enqueue_full(c, nullptr, &c->subLm))) return r;
+    if (c->linkLeader) {  // member: the front half now, the LM with the leader's next pair
+        if ((r = pipeline_front(c))) return r;
+        HIPCHK(c, hipEventRecord(c->evFront, c->stream));
+        c->frontOnly = true;
+    } else if (c->linkMember && c->linkMember->frontOnly) {
+        if ((r = enqueue_linked(c, c->linkMember, &c->subLm))) return r;
+    } else {
+        if ((r = enqueue_full(c, nullptr, &c->subLm))) return r;
+    }
     c->pending = true;
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_link(fm3d_ctx* member, fm3d_ctx* leader) {
+    if (!member || !leader || member == leader) return FM3D_ERR_INVALID;
+    if (member->pending || leader->pending) return fail(member, FM3D_ERR_INVALID, "a submitted frame pair is pending");
+    if (member->linkLeader || member->linkMember || leader->linkLeader || leader->linkMember)
+        return fail(member, FM3D_ERR_INVALID, "a context is linked already");
+    if (member->device != leader->device) return fail(member, FM3D_ERR_INVALID, "linked contexts need one device");
+    member->linkLeader = leader;
+    leader->linkMember = member;
     return FM3D_OK;
 }
 
@@ -2029,8 +2144,14 @@ int fm3d_pipeline_wait(fm3d_ctx* c, fm3d_record* out, int cap, int* nKept, fm3d_
     if (!c) return FM3D_ERR_INVALID;
     if (!c->pending) return fail(c, FM3D_ERR_INVALID, "no frame pair submitted (fm3d_pipeline_submit)");
     hipSetDevice(c->device);
+    int r;
+    if (c->frontOnly) {  // a member whose leader took no pair since: its LM alone, on its own stream
+        if ((r = run_lm(c, c->stNA, c->pcnt.as<int>() + 1, &c->subLm, c->ev[6], c->ev[7]))) return r;
+        if ((r = enqueue_epilogue(c, nullptr, c->lmStat.p))) return r;
+        c->frontOnly = false;
+    }
     c->pending = false;
-    int kept = 0, r;
+    int kept = 0;
     if ((r = finalize_full(c, c->subLm, c->ev[8], true, &kept, stats))) return r;
     if (out && kept > cap) return fail(c, FM3D_ERR_INVALID, "record buffer too small");
     if (out && kept)

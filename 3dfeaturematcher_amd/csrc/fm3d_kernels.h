@@ -34,14 +34,32 @@ struct ProjConst {
     char *slabDF, *slabDJ0, *slabDJ1;
 };
 
+// one frame pair's points in an LM launch (a launch may take the points of several: the slots
+// of a workgroup whose first pair runs dry take the next pair's points)
+struct LMProblem {
+    const double* points;     // P x 3
+    const int* Pdev;          // the point count on the device (may be null: P)
+    const LevelDesc* lvl;     // its pyramids, levels+1 entries
+    double* normals;          // P x 3
+    int* status;              // P
+    int* info;                // P x 8
+    int* nfev;                // P x 8
+    int* mdat;                // P
+    unsigned long long* stat; // [residual evaluations, pixel evaluations] of its points
+    int P;                    // points, or their bound when Pdev is set
+    unsigned projOff;         // byte offset of its ProjConst (camera-2 pose) in LMParams::proj
+};
+
 struct LMParams {
-    const double* points;  // P x 3
-    int P;                 // points, or their bound when Pdev is set
-    const int* Pdev;       // the point count on the device (may be null: P)
-    Camera cam;
-    double R2[9], t2[3];
-    const ProjConst* proj;  // the same R2, t2, cam in global memory
-    const LevelDesc* lvl;   // device array, levels+1 entries
+    // (the field order of the single-problem layout is kept: the kernel's register allocation
+    // follows the kernarg layout; points .. mdat are unused, the problem table holds them)
+    const double* points_;
+    int P_;
+    const int* Pdev_;
+    Camera cam;                 // shared by the problems (one camera)
+    double R2_[9], t2_[3];
+    const ProjConst* proj;      // per problem: R2, t2, cam (+ the slab bases, the same in each)
+    const LevelDesc* lvl_;
     int levels;
     const int2* offsets;  // circle offsets (i, j) in reference order, padded to nOffPad
     int nOff, nOffPad;
@@ -52,11 +70,11 @@ struct LMParams {
     double* slab;    // rays: 2 arrays x (groups*kLM2Slots) slots x nOffPad entries
     float* slabI1;   // I1, fvec dI, 2 Jacobian dI, compact index: 5 arrays, same shape
     long nWaves;     // number of workgroups
-    double* normals;  // P x 3
-    int* status;      // P
-    int* info;        // P x 8
-    int* nfev;        // P x 8
-    int* mdat;        // P
+    double* normals_;
+    int* status_;
+    int* info_;
+    int* nfev_;
+    int* mdat_;
     unsigned long long* statEval;
     unsigned long long* statPix;
     long long maxIter;       // safety bound on passes per slot
@@ -67,7 +85,10 @@ struct LMParams {
     // [passes, cycles terms, cycles chain, cycles control, cycles total, wall ticks sum, wall ticks
     //  max, class passes x4, class cycles x4, max start, max end, min start, ..., producer waits]
     unsigned long long* statPass;
+    int nProb;                  // frame pairs of the launch (problems, <= kLMMaxProblems)
+    const LMProblem* prob;      // device table
 };
+constexpr int kLMMaxProblems = 4;
 
 constexpr int kLMRunning = 0x100;  // status of a point still in flight
 
@@ -76,6 +97,8 @@ constexpr int kLMRunning = 0x100;  // status of a point still in flight
 constexpr int kLM2Slots = 15;
 constexpr int kLM2Ring = 8;  // chunks of 64 entries in flight per slot
 constexpr int kLM2Threads = 64 * (kLM2Slots + 1);
+// MULTI: the problems' ProjConst entries differ (per-pass pose offset); false: entry 0 for all
+template <bool MULTI>
 __global__ void lm2_kernel(LMParams p);
 
 // ---------------- matching ----------------

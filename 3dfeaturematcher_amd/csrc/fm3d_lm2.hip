@@ -79,6 +79,7 @@ typedef __attribute__((address_space(1), aligned(1))) const uint16_t gu16u;  // 
 // the slot's current pass, written by lane 0 of the slot's term wave
 struct SlotP2 {
     int pass, ekind, nev, len, pivot, t0, t1, q0, lw;
+    unsigned projOff;  // byte offset of the point's frame pair's ProjConst in the table (p.proj)
     double n0[2], n1[2], n2[2], mm[2], w[2], hj[2];
     double scale, xmax, ymax, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant, wF;
     const uint8_t* img1;
@@ -91,6 +92,8 @@ struct SlotS2 {
     double X0, X1, X2, ccx, ccy, nrm0, nrm1, nrm2;
     double apf, aqf, ff, aps, fs, vfirst, r01, tq0, qtf0, wa4s, usecond, ajn0s, tq, ajn1s;
     double wF, wJ[2];  // weights of the evaluations behind the stored fvec / Jacobian dI values
+    long long pev, ppix;  // the point's residual / pixel evaluations (its problem's counters)
+    int prob;             // the point's problem (frame pair) in p->prob
     int pidx, m, L, i1ok, ekind, t0, q0, t1, bNaN;
 };
 
@@ -146,17 +149,30 @@ struct Ctl2 {
     double eps;
     long long cnt_eval, cnt_pix;
 
+    // the next point of the launch's queue: the problems' points one after the other (each
+    // problem one frame pair; its point count on the device or given)
     __device__ void fetch(SlotS2& S, SlotP2& P) {
-        const int q = atomicAdd(p->queue, 1);
-        if (q >= (p->Pdev ? *p->Pdev : p->P)) {  // the inlier count on the device (pipeline) or given
+        int loc = atomicAdd(p->queue, 1), j = 0;
+        for (; j < p->nProb; j++) {
+            const LMProblem& pr = p->prob[j];
+            const int n = pr.Pdev ? *pr.Pdev : pr.P;
+            if (loc < n) break;
+            loc -= n;
+        }
+        if (j >= p->nProb) {
             P.pass = Q_DONE;
             return;
         }
-        S.pidx = q;
+        const LMProblem& pr = p->prob[j];
+        S.prob = j;
+        S.pidx = loc;
+        S.pev = 0;
+        S.ppix = 0;
+        P.projOff = pr.projOff;
         atomicMax(p->statPass + 22, wall_clock64());  // the last point handed out: the queue runs dry
-        S.X0 = p->points[3 * q + 0];
-        S.X1 = p->points[3 * q + 1];
-        S.X2 = p->points[3 * q + 2];
+        S.X0 = pr.points[3 * loc + 0];
+        S.X1 = pr.points[3 * loc + 1];
+        S.X2 = pr.points[3 * loc + 2];
         const double Ident[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         const double Zero[3] = {0, 0, 0};
         double cx, cy;
@@ -169,7 +185,7 @@ struct Ctl2 {
         P.ccy = cy;
     }
     __device__ void start_level(SlotS2& S, SlotP2& P) {
-        const LevelDesc lv = p->lvl[S.L];
+        const LevelDesc lv = p->prob[S.prob].lvl[S.L];
         P.pass = Q_LEVEL;
         P.len = S.m;
         P.scale = ldexp(1.0, -S.L);  // 1.0 / float(2^L)  (optimize_pyramid, :225-241)
@@ -182,16 +198,20 @@ struct Ctl2 {
         P.ccy = S.ccy;
     }
     __device__ void finish_point(SlotS2& S, SlotP2& P, int code) {
-        p->status[S.pidx] = code;
-        p->normals[3 * S.pidx + 0] = S.nrm0;
-        p->normals[3 * S.pidx + 1] = S.nrm1;
-        p->normals[3 * S.pidx + 2] = S.nrm2;
-        p->mdat[S.pidx] = S.m;
+        const LMProblem& pr = p->prob[S.prob];
+        pr.status[S.pidx] = code;
+        pr.normals[3 * S.pidx + 0] = S.nrm0;
+        pr.normals[3 * S.pidx + 1] = S.nrm1;
+        pr.normals[3 * S.pidx + 2] = S.nrm2;
+        pr.mdat[S.pidx] = S.m;
+        atomicAdd(pr.stat + 0, (unsigned long long)S.pev);
+        atomicAdd(pr.stat + 1, (unsigned long long)S.ppix);
         fetch(S, P);
     }
     __device__ void level_done(SlotS2& S, SlotP2& P, int info) {
-        p->info[8 * S.pidx + S.L] = info;
-        p->nfev[8 * S.pidx + S.L] = S.s.nfev;
+        const LMProblem& pr = p->prob[S.prob];
+        pr.info[8 * S.pidx + S.L] = info;
+        pr.nfev[8 * S.pidx + S.L] = S.s.nfev;
         sph2car_det(S.s.x[0], S.s.x[1], S.nrm0, S.nrm1, S.nrm2);
         S.L--;
         if (S.L < 0)
@@ -200,8 +220,9 @@ struct Ctl2 {
             start_level(S, P);
     }
     __device__ void abort_level(SlotS2& S, SlotP2& P, int code) {
-        p->info[8 * S.pidx + S.L] = -code;
-        p->nfev[8 * S.pidx + S.L] = S.s.nfev;
+        const LMProblem& pr = p->prob[S.prob];
+        pr.info[8 * S.pidx + S.L] = -code;
+        pr.nfev[8 * S.pidx + S.L] = S.s.nfev;
         finish_point(S, P, code);
     }
     // evaluateNormal (normaloptimizer.cpp:65-149), per-call part, for evaluation ev.
@@ -227,6 +248,8 @@ struct Ctl2 {
         S.s.nfev++;
         cnt_eval++;
         cnt_pix += S.m;
+        S.pev++;
+        S.ppix += S.m;
     }
     __device__ void eval_pass(SlotS2& S, SlotP2& P, int kind, double a, double b) {
         count_eval(S);
@@ -623,11 +646,17 @@ typedef __attribute__((address_space(4))) const ProjConst cProjConst;
 
 // The projection constants re-read (scalar loads, scalar cache) at every use: 21 uniform
 // doubles kept live across the pass loops would not fit the SGPR budget and get spilled
-// to VGPR lanes (a v_readlane per use).  The zero is opaque to the compiler, so the loads
-// are not hoisted out of the loop.
+// to VGPR lanes (a v_readlane per use).  The offset (0, or the pass's frame pair's entry of
+// the table, SlotP2::projOff) is opaque to the compiler, so the loads are not hoisted out
+// of the loop.  Every entry holds the same slab bases.
 __device__ __forceinline__ const cProjConst* proj_consts(const ProjConst* p) {
     int z;
     asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return (const cProjConst*)((const __attribute__((address_space(4))) char*)p + z);
+}
+__device__ __forceinline__ const cProjConst* proj_consts(const ProjConst* p, unsigned off) {
+    unsigned z;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(z) : "s"(off));
     return (const cProjConst*)((const __attribute__((address_space(4))) char*)p + z);
 }
 
@@ -674,11 +703,14 @@ struct Geo2 {
 // a2 = r2 + 2*x*x and a3 = r2 + 2*y*y are single FMAs: 2*RN(x*x) == RN(2x*x) (a power-of-two
 // scaling) wherever x*x is normal, so fma(xx, 2, r2) rounds the same exact sum; where x*x is
 // subnormal, |x|, |y| < 1e-150 and u, v round to cx, cy either way.
-template <bool MMOK>
-__device__ __forceinline__ Geo2 geometry2(const LMParams& p, double ux, double uy, double n0, double n1, double n2,
-                                          double mm, double scale, unsigned long long xmaxb,
-                                          unsigned long long ymaxb, int lw, double cm) {
-    const cProjConst* pc = proj_consts(p.proj);
+// MULTI: the launch's problems have different poses -- the pass's entry of the table (projOff,
+// one more scalar register live across the pass loops: +3-6 % cycles per evaluation pass,
+// measured); otherwise entry 0
+template <bool MMOK, bool MULTI>
+__device__ __forceinline__ Geo2 geometry2(const LMParams& p, unsigned projOff, double ux, double uy, double n0,
+                                          double n1, double n2, double mm, double scale,
+                                          unsigned long long xmaxb, unsigned long long ymaxb, int lw, double cm) {
+    const cProjConst* pc = MULTI ? proj_consts(p.proj, projOff) : proj_consts(p.proj);
     Geo2 r;
     const double nn = n0 * ux + n1 * uy + n2 * 1.;
     const double kk = MMOK ? div_nn(mm, nn, true) : mm / nn;
@@ -892,6 +924,7 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
 }  // namespace
 
 // 4 waves per SIMD: one workgroup of 16 waves per CU (128 VGPRs)
+template <bool MULTI>
 __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     Shared& sh = g_sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1107,6 +1140,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     const unsigned long long ymaxb = (unsigned long long)__double_as_longlong(SP.ymax);
                     const uint8_t* img2 = SP.img2;
                     const int lw = rfl(SP.lw);
+                    const unsigned projOff = MULTI ? (unsigned)rfl((int)SP.projOff) : 0u;
                     const bool i1ok = rfl(SS.i1ok) != 0;
                     const gu8* img2b = (const gu8*)rfl_ptr(img2);
                     // The fast form (FAST): the ray-plane quotients take div_nn's fast sequence
@@ -1148,8 +1182,10 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             float i1;
                         };
                         auto geo = [&](double ux, double uy, double n0, double n1, double n2, double mm) {
-                            return FAST ? geometry2<true>(p, ux, uy, n0, n1, n2, mm, scale, xmaxb, ymaxb, lw, cm)
-                                        : geometry2<false>(p, ux, uy, n0, n1, n2, mm, scale, xmaxb, ymaxb, lw, cm);
+                            return FAST ? geometry2<true, MULTI>(p, projOff, ux, uy, n0, n1, n2, mm, scale, xmaxb,
+                                                                 ymaxb, lw, cm)
+                                        : geometry2<false, MULTI>(p, projOff, ux, uy, n0, n1, n2, mm, scale, xmaxb,
+                                                                  ymaxb, lw, cm);
                         };
                         auto jdiv = [&](double a, double h, double y, bool mok) {
                             return FAST ? mdiv_fast(a, h, y) : mdiv(a, h, y, mok);
@@ -1721,5 +1757,10 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
         atomicMin(p.statPass + 17, tStart);
     }
 }
+
+// one pose for every problem of the launch (one frame pair, or linked pairs of one rig pose), and
+// a pose per problem
+template __global__ void lm2_kernel<false>(LMParams p);
+template __global__ void lm2_kernel<true>(LMParams p);
 
 }  // namespace fm3d

@@ -59,8 +59,12 @@ __device__ inline void dlt_nullvec(double* A, double* v) {
 }
 
 // setKeypoints (singlecameratriangulator.cpp:145-171) + triangulate (:173-230), one
-// thread per match: gather, undistortPoints, cvTriangulatePoints, z filter.
-__global__ void triangulate_kernel(TriParams p) {
+// thread per match: gather, undistortPoints, cvTriangulatePoints, z filter.  A thread's A and V
+// (32 doubles) and the sweep's temporaries need ~150 VGPRs: 64-thread workgroups (launch bound)
+// give it the registers; under the default 1024-thread bound (128 VGPRs) the sweeps spilled to
+// scratch and the kernel lasted 27-33 us at any match count (rocprofv3, round 3).
+constexpr int kTriThreads = 64;
+__global__ __launch_bounds__(kTriThreads) void triangulate_kernel(TriParams p) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (p.Kdev ? *p.Kdev : p.K)) return;  // the match count on the device (grid: its bound)
     const fm3d_dmatch mt = p.matches[i];
@@ -306,7 +310,7 @@ __global__ void make_records_kernel(const fm3d_dmatch* __restrict__ matches, con
 
 void launch_triangulate(const TriParams& p, hipStream_t s) {
     if (p.K <= 0) return;
-    triangulate_kernel<<<(p.K + 255) / 256, 256, 0, s>>>(p);
+    triangulate_kernel<<<(p.K + kTriThreads - 1) / kTriThreads, kTriThreads, 0, s>>>(p);
 }
 
 void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s) {

@@ -79,7 +79,9 @@ def parse():
     ap.add_argument("--mode", choices=("stream", "resident"), default="stream",
                     help="stream (C4 headline): every step a frame pair from host memory to host memory, "
                          "--inflight pairs in flight; resident: inputs uploaded once, one step in flight")
-    ap.add_argument("--inflight", type=int, default=2, help="frame pairs in flight in the stream mode")
+    ap.add_argument("--inflight", type=int, default=2, help="LM launches in flight in the stream mode")
+    ap.add_argument("--lm-pairs", type=int, default=1,
+                    help="frame pairs per LM launch in the stream mode (2: fm3d_pipeline_link)")
     ap.add_argument("--mgpu", action="store_true",
                     help="the one-process multi-GPU path (fm3d_mgpu, C5) also at --gpus 1 (its reference point)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
@@ -160,7 +162,8 @@ def run_c4_stream(args):
     pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=args.seed, desc=args.desc)
     t_gen = time.time() - t_gen
     s = c4_settings(fm3d, pair, args)
-    nf = max(1, args.inflight)
+    nl = max(1, args.lm_pairs)
+    nf = max(1, args.inflight) * nl  # contexts: `inflight` LM launches of `lm_pairs` frame pairs each
     streams = [torch.cuda.Stream(device=0) for _ in range(nf)]
     ctxs, pipes = [], []
     for st in streams:
@@ -169,6 +172,11 @@ def run_c4_stream(args):
         fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
         ctxs.append(ctx)
         pipes.append(fm3d.Pipeline(ctx))
+    if nl == 2:  # context 2i's pairs join the LM launches of context 2i + 1 (fm3d_pipeline_link)
+        for i in range(0, nf, 2):
+            pipes[i].link(pipes[i + 1])
+    elif nl != 1:
+        raise SystemExit("--lm-pairs: 1 or 2")
     binary = args.desc == "orb"
     bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(nf)]
     inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
@@ -273,7 +281,8 @@ def run_c4_stream(args):
             "workload": desc,
             "keypoints_per_frame": wl["keypoints"], "width": wl["width"], "height": wl["height"],
             "pixelsRay": args.ray, "pyramids": args.levels, "parallelism": "1 GPU",
-            "mode": f"stream: {nf} frame pairs in flight (one context + HIP stream each, fm3d_pipeline_submit/wait)",
+            "mode": (f"stream: {nf} frame pairs in flight (one context + HIP stream each, fm3d_pipeline_submit/wait), "
+                     f"{nl} frame pair(s) per LM launch" + (" (fm3d_pipeline_link)" if nl > 1 else "")),
             "timed": ("per step, from host memory to host memory: H2D of descriptors, keypoints and images (pinned "
                       "staging), pyramids (a6), match -> NNDR -> DLT -> LM normals -> survivor records, D2H of the "
                       "records; the K steps' wall time includes filling and draining the pipeline"),

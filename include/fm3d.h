@@ -418,6 +418,14 @@ int fm3d_pipeline_submit(fm3d_ctx *ctx, const void *descA, int nA, const void *d
                          const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1,
                          const uint8_t *img2, int width, int height, int queryOffset);
 int fm3d_pipeline_wait(fm3d_ctx *ctx, fm3d_record *out, int cap, int *nKept, fm3d_pipeline_stats *stats);
+/* Join two contexts' LM launches (same device, camera and LM settings): after the link a submit on
+   `member` queues its pair's front half only, and the next submit on `leader` queues ONE LM launch
+   over both pairs' points -- the workgroups whose slots run out of one pair's points take the
+   other's, so the pair fills the launch's end-of-queue tail -- followed by each pair's records on
+   its own stream.  A member waited for before its leader's next submit runs its LM alone.  Each
+   pair's results are those of its own fm3d_pipeline_run, bit for bit.  fm3d_pipeline_run and the
+   other calls of a linked context run unlinked. */
+int fm3d_pipeline_link(fm3d_ctx *member, fm3d_ctx *leader);
 /* BASELINE.json's C2 ("brute-force L2 match + DLT triangulate only"): match -> NNDR -> triangulate on
    the staged inputs, no normals; *nInliers = the triangulated points kept by the z filter (stats:
    match / NNDR-compaction / triangulate / total HIP-event times). */

@@ -931,6 +931,88 @@ def test_pipeline_submit_wait_stream_equals_run(fm3d, synth):
     assert len(ref[0][0]) > 50
 
 
+def test_pipeline_linked_lm_launch_equals_run(fm3d, synth):
+    """fm3d_pipeline_link: two contexts' frame pairs in ONE LM launch (the slots of a workgroup that
+    run out of one pair's points take the other's): each pair's records, counts and evaluation
+    counts equal its own fm3d_pipeline_run, bit for bit -- in both orders of different pairs, and
+    for a member waited for before its leader's submit (its LM alone)."""
+    pairs = [synth.make_frame_pair(3000, seed=11), synth.make_frame_pair(2500, seed=12)]
+    s = _settings(fm3d, pairs[0].cam, pixelsRay=12, pyramids=2)
+    ref = []
+    ctx, pipe = _pipe_ctx(fm3d, s, pairs[0].g12)
+    try:
+        for fp in pairs:
+            pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            k, st = pipe.run()
+            ref.append((pipe.records(k), st))
+    finally:
+        ctx.close()
+    cs = [_pipe_ctx(fm3d, s, pairs[0].g12) for _ in range(2)]
+    member, leader = cs[0][1], cs[1][1]
+    try:
+        member.link(leader)
+        got = []
+        for wm, wl in ((0, 1), (1, 0), (1, 1)):
+            a, b = pairs[wm], pairs[wl]
+            member.submit(a.desc1, a.desc2, a.kp1, a.kp2, a.img1, a.img2)
+            leader.submit(b.desc1, b.desc2, b.kp1, b.kp2, b.img1, b.img2)
+            got += [(wm, member.wait()), (wl, leader.wait())]
+        a = pairs[0]
+        member.submit(a.desc1, a.desc2, a.kp1, a.kp2, a.img1, a.img2)
+        got.append((0, member.wait()))  # no leader submit: the member's LM alone
+        with pytest.raises(fm3d.Fm3dError):
+            leader.link(member)  # linked already
+    finally:
+        for c, _ in cs:
+            c.close()
+    for w, (rec, st) in got:
+        assert rec.tobytes() == ref[w][0].tobytes()
+        for key in ("matches", "inliers", "kept"):
+            assert st[key] == ref[w][1][key]
+        assert st["lm"]["pixel_evaluations"] == ref[w][1]["lm"]["pixel_evaluations"]
+        assert st["lm"]["evaluations"] == ref[w][1]["lm"]["evaluations"]
+
+
+def test_pipeline_linked_lm_two_poses(fm3d, synth):
+    """Linked frame pairs with different camera-2 poses take the LM kernel's per-problem pose
+    (lm2_kernel<true>): each pair's records equal its own fm3d_pipeline_run."""
+    g12b = synth.reference_g12() @ _small_motion()
+    pairs = [synth.make_frame_pair(3000, seed=11), synth.make_frame_pair(3000, seed=14, g12=g12b)]
+    s = _settings(fm3d, pairs[0].cam, pixelsRay=12, pyramids=2)
+    ref = []
+    for fp in pairs:
+        ctx, pipe = _pipe_ctx(fm3d, s, fp.g12)
+        try:
+            pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            k, st = pipe.run()
+            ref.append((pipe.records(k), st))
+        finally:
+            ctx.close()
+    cs = [_pipe_ctx(fm3d, s, fp.g12) for fp in pairs]
+    try:
+        cs[1][1].link(cs[0][1])  # pair 1's context (pose b) joins pair 0's launches (pose a)
+        for _ in range(2):
+            b, a = pairs[1], pairs[0]
+            cs[1][1].submit(b.desc1, b.desc2, b.kp1, b.kp2, b.img1, b.img2)
+            cs[0][1].submit(a.desc1, a.desc2, a.kp1, a.kp2, a.img1, a.img2)
+            got = [cs[0][1].wait(), cs[1][1].wait()]
+            for w in (0, 1):
+                assert got[w][0].tobytes() == ref[w][0].tobytes()
+                assert got[w][1]["lm"]["pixel_evaluations"] == ref[w][1]["lm"]["pixel_evaluations"]
+    finally:
+        for c, _ in cs:
+            c.close()
+    assert len(ref[0][0]) > 50 and len(ref[1][0]) > 50
+
+
+def _small_motion():
+    c, s_ = np.cos(0.03), np.sin(0.03)
+    M = np.eye(4)
+    M[:3, :3] = [[c, 0, s_], [0, 1, 0], [-s_, 0, c]]
+    M[:3, 3] = [0.02, -0.01, 0.0]
+    return M
+
+
 def test_pipeline_ncc_download_after_other_runs(fm3d, synth):
     """fm3d_pipeline_ncc_download returns the rows of the last successful run_ncc,
     even after a run_dlt / run on a larger pair (which rewrite the inlier count)."""
