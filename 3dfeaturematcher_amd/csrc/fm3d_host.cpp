@@ -140,9 +140,10 @@ struct fm3d_ctx {
     bool pending = false;          // a fm3d_pipeline_submit awaiting fm3d_pipeline_wait
     // fm3d_pipeline_link: a member's submit queues its front half only; the leader's next submit
     // queues ONE LM launch over both pairs' points and the member's records behind it
-    fm3d_ctx* linkLeader = nullptr;  // (member) the context that launches its LM
-    fm3d_ctx* linkMember = nullptr;  // (leader) the context whose pair joins its launches
+    fm3d_ctx* linkLeader = nullptr;        // (member) the context that launches its LM
+    std::vector<fm3d_ctx*> linkMembers;    // (leader) the contexts whose pairs join its launches
     bool frontOnly = false;          // (member) submitted, its LM not queued yet
+    fm3d_record* subOut = nullptr;   // the submitted pair's record destination (device; null: internal)
     hipEvent_t evFront = nullptr;    // (member) after its front half
     hipEvent_t evLm = nullptr;       // (leader) after a joint LM launch
     fm3d_lm_stats subLm{};         // the pending submit's LM launch data
@@ -1665,8 +1666,11 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
     hipEventDestroy(c->evProj);
     hipEventDestroy(c->evFront);
     hipEventDestroy(c->evLm);
-    if (c->linkLeader) c->linkLeader->linkMember = nullptr;
-    if (c->linkMember) c->linkMember->linkLeader = nullptr;
+    if (c->linkLeader) {
+        auto& v = c->linkLeader->linkMembers;
+        v.erase(std::remove(v.begin(), v.end(), c), v.end());
+    }
+    for (fm3d_ctx* m : c->linkMembers) m->linkLeader = nullptr;
     for (auto& b : c->pyr1) b.release();
     for (auto& b : c->pyr2) b.release();
     for (auto& e : c->ev) hipEventDestroy(e);
@@ -2006,25 +2010,32 @@ int enqueue_full(fm3d_ctx* c, fm3d_record* out, fm3d_lm_stats* ls) {
     return enqueue_epilogue(c, out, c->lmStat.p);
 }
 
-// the leader's pair with its member's queued front half: ONE LM launch over both pairs' points on
-// the leader's stream (after the member's front half), then each pair's records on its own stream
-int enqueue_linked(fm3d_ctx* c, fm3d_ctx* m, fm3d_lm_stats* ls) {
+// the leader's pair with its members' queued front halves: ONE LM launch over all these pairs'
+// points on the leader's stream (after every member's front half), then each pair's records on
+// its own stream
+int enqueue_linked(fm3d_ctx* c, const std::vector<fm3d_ctx*>& ms, fm3d_lm_stats* ls) {
     int r;
     if ((r = pipeline_front(c))) return r;
-    HIPCHK(c, hipStreamWaitEvent(c->stream, m->evFront, 0));
-    const LMSrc src[2] = {{m, m->stNA, m->pcnt.as<int>() + 1}, {c, c->stNA, c->pcnt.as<int>() + 1}};
-    HIPCHK(c, hipEventRecord(m->ev[6], c->stream));
-    if ((r = run_lm_multi(c, src, 2, ls, c->ev[6], c->ev[7]))) return r;
-    HIPCHK(c, hipEventRecord(m->ev[7], c->stream));
+    std::vector<LMSrc> src;
+    for (fm3d_ctx* m : ms) {
+        HIPCHK(c, hipStreamWaitEvent(c->stream, m->evFront, 0));
+        src.push_back({m, m->stNA, m->pcnt.as<int>() + 1});
+        HIPCHK(c, hipEventRecord(m->ev[6], c->stream));
+    }
+    src.push_back({c, c->stNA, c->pcnt.as<int>() + 1});
+    if ((r = run_lm_multi(c, src.data(), (int)src.size(), ls, c->ev[6], c->ev[7]))) return r;
     HIPCHK(c, hipEventRecord(c->evLm, c->stream));
-    m->subLm = *ls;
-    m->lmGroups = c->lmGroups;
-    m->wallKhz = c->wallKhz;
-    if ((r = enqueue_epilogue(c, nullptr, c->lmStat.p))) return r;
-    hipSetDevice(m->device);
-    HIPCHK(m, hipStreamWaitEvent(m->stream, c->evLm, 0));
-    if ((r = enqueue_epilogue(m, nullptr, c->lmStat.p))) return r;
-    m->frontOnly = false;
+    if ((r = enqueue_epilogue(c, c->subOut, c->lmStat.p))) return r;
+    for (fm3d_ctx* m : ms) {
+        HIPCHK(c, hipEventRecord(m->ev[7], c->stream));
+        m->subLm = *ls;
+        m->lmGroups = c->lmGroups;
+        m->wallKhz = c->wallKhz;
+        hipSetDevice(m->device);
+        HIPCHK(m, hipStreamWaitEvent(m->stream, c->evLm, 0));
+        if ((r = enqueue_epilogue(m, m->subOut, c->lmStat.p))) return r;
+        m->frontOnly = false;
+    }
     return FM3D_OK;
 }
 
@@ -2105,10 +2116,13 @@ int fm3d_pipeline_run(fm3d_ctx* c, fm3d_record* recordsDev, int* nKept, fm3d_pip
     return finalize_full(c, ls, c->ev[2], false, nKept, stats);
 }
 
-int fm3d_pipeline_submit(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
-                         const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
-                         int width, int height, int queryOffset) {
-    if (!c) return FM3D_ERR_INVALID;
+}  // extern "C"
+namespace {
+// one frame pair staged and queued on c's stream (records into out: device, or null = internal);
+// a link member queues its front half only, a leader joins its queued members' pairs
+int submit_impl(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
+                int width, int height, int queryOffset, fm3d_record* out) {
     PENDING_CHECK(c);
     hipSetDevice(c->device);
     HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
@@ -2116,27 +2130,54 @@ int fm3d_pipeline_submit(fm3d_ctx* c, const void* descA, int nA, const void* des
     if ((r = stage_pipeline(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, queryOffset)))
         return r;
     c->subLm = fm3d_lm_stats{};
+    c->subOut = out;
     if (c->linkLeader) {  // member: the front half now, the LM with the leader's next pair
         if ((r = pipeline_front(c))) return r;
         HIPCHK(c, hipEventRecord(c->evFront, c->stream));
         c->frontOnly = true;
-    } else if (c->linkMember && c->linkMember->frontOnly) {
-        if ((r = enqueue_linked(c, c->linkMember, &c->subLm))) return r;
+    } else if (!c->linkMembers.empty()) {
+        std::vector<fm3d_ctx*> ms;  // the members with a pair queued since this leader's last launch
+        for (fm3d_ctx* m : c->linkMembers)
+            if (m->frontOnly) ms.push_back(m);
+        if ((r = ms.empty() ? enqueue_full(c, out, &c->subLm) : enqueue_linked(c, ms, &c->subLm))) return r;
     } else {
-        if ((r = enqueue_full(c, nullptr, &c->subLm))) return r;
+        if ((r = enqueue_full(c, out, &c->subLm))) return r;
     }
     c->pending = true;
     return FM3D_OK;
 }
 
+// a member whose leader took no pair since its submit: its LM alone, on its own stream
+int flush_member(fm3d_ctx* c) {
+    if (!c->frontOnly) return FM3D_OK;
+    hipSetDevice(c->device);
+    int r;
+    if ((r = run_lm(c, c->stNA, c->pcnt.as<int>() + 1, &c->subLm, c->ev[6], c->ev[7]))) return r;
+    if ((r = enqueue_epilogue(c, c->subOut, c->lmStat.p))) return r;
+    c->frontOnly = false;
+    return FM3D_OK;
+}
+}  // namespace
+extern "C" {
+
+int fm3d_pipeline_submit(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
+                         const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
+                         int width, int height, int queryOffset) {
+    if (!c) return FM3D_ERR_INVALID;
+    return submit_impl(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, queryOffset,
+                       nullptr);
+}
+
 int fm3d_pipeline_link(fm3d_ctx* member, fm3d_ctx* leader) {
     if (!member || !leader || member == leader) return FM3D_ERR_INVALID;
     if (member->pending || leader->pending) return fail(member, FM3D_ERR_INVALID, "a submitted frame pair is pending");
-    if (member->linkLeader || member->linkMember || leader->linkLeader || leader->linkMember)
+    if (member->linkLeader || !member->linkMembers.empty() || leader->linkLeader)
         return fail(member, FM3D_ERR_INVALID, "a context is linked already");
+    if ((int)leader->linkMembers.size() + 1 >= fm3d::kLMMaxProblems)
+        return fail(member, FM3D_ERR_INVALID, "a leader takes at most 3 members");
     if (member->device != leader->device) return fail(member, FM3D_ERR_INVALID, "linked contexts need one device");
     member->linkLeader = leader;
-    leader->linkMember = member;
+    leader->linkMembers.push_back(member);
     return FM3D_OK;
 }
 
@@ -2145,11 +2186,7 @@ int fm3d_pipeline_wait(fm3d_ctx* c, fm3d_record* out, int cap, int* nKept, fm3d_
     if (!c->pending) return fail(c, FM3D_ERR_INVALID, "no frame pair submitted (fm3d_pipeline_submit)");
     hipSetDevice(c->device);
     int r;
-    if (c->frontOnly) {  // a member whose leader took no pair since: its LM alone, on its own stream
-        if ((r = run_lm(c, c->stNA, c->pcnt.as<int>() + 1, &c->subLm, c->ev[6], c->ev[7]))) return r;
-        if ((r = enqueue_epilogue(c, nullptr, c->lmStat.p))) return r;
-        c->frontOnly = false;
-    }
+    if ((r = flush_member(c))) return r;
     c->pending = false;
     int kept = 0;
     if ((r = finalize_full(c, c->subLm, c->ev[8], true, &kept, stats))) return r;
@@ -2167,16 +2204,11 @@ int fm3d_internal_submit_to(fm3d_ctx* c, const void* descA, int nA, const void* 
                             const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1,
                             const uint8_t* img2, int width, int height, fm3d_record* recordsDev) {
     if (!c) return FM3D_ERR_INVALID;
-    PENDING_CHECK(c);
-    hipSetDevice(c->device);
-    HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
-    int r;
-    if ((r = stage_pipeline(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, 0))) return r;
-    c->subLm = fm3d_lm_stats{};
-    if ((r = enqueue_full(c, recordsDev, &c->subLm))) return r;
-    c->pending = true;
-    return FM3D_OK;
+    return submit_impl(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, img1, img2, width, height, 0, recordsDev);
 }
+
+int fm3d_internal_flush(fm3d_ctx* c) { return c ? flush_member(c) : FM3D_ERR_INVALID; }
+bool fm3d_internal_front_only(const fm3d_ctx* c) { return c && c->frontOnly; }
 
 int fm3d_internal_enqueue(fm3d_ctx* c, fm3d_record* recordsDev) {
     if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
@@ -2265,7 +2297,7 @@ int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* n
         p.points = c->pts.as<double>();
         p.P = nA;  // the bound; the inlier count is on the device
         p.Pdev = c->pcnt.as<int>() + 1;
-        p.cam = c->cam;
+        p.cam = lm_camera(c->cam);  // the kernel's bit-pattern isPixelGood (fm3d_ncc.hip ncc_geometry)
         std::memcpy(p.R2, c->R2, sizeof(p.R2));
         std::memcpy(p.t2, c->t2, sizeof(p.t2));
         p.img1 = c->pyr1[0].as<uint8_t>();
@@ -3437,7 +3469,7 @@ int fm3d_ncc_hypotheses(fm3d_ctx* c, const double* points, int P, int Hphi, int 
     fm3d::NccParams p{};
     p.points = X.as<double>();
     p.P = P;
-    p.cam = c->cam;
+    p.cam = lm_camera(c->cam);  // the kernel's bit-pattern isPixelGood (fm3d_ncc.hip ncc_geometry)
     std::memcpy(p.R2, c->R2, sizeof(p.R2));
     std::memcpy(p.t2, c->t2, sizeof(p.t2));
     p.img1 = c->pyr1[0].as<uint8_t>();

@@ -17,10 +17,12 @@
 //   * merge (plain C++ on the host): device 0's gathered copy, local query indices mapped back
 //     through each device's query list, records ordered by query -- byte-identical to one
 //     fm3d_pipeline_run of the whole frame pair.
-// Two context sets take frame pairs in turn (fm3d_mgpu_submit / fm3d_mgpu_wait): the next pair's
-// staging, front half and LM workgroups fill the CUs the previous LM launch frees in its tail, as
-// on one GPU (bench.py --gpus N).  Every submit is host-asynchronous: one host thread per device
-// gathers its queries and queues its pipeline, then the collectives are queued behind them.
+// Four context sets take frame pairs in turn (fm3d_mgpu_submit / fm3d_mgpu_wait), linked in two
+// couples (fm3d_pipeline_link: sets 0 -> 1 and 2 -> 3): each device's LM launch takes two frame
+// pairs' points, and one couple's staging, front halves and LM workgroups fill the CUs the other's
+// launch frees in its tail, as on one GPU (bench.py --gpus N).  Every submit is host-asynchronous:
+// one host thread per device gathers its queries and queues its pipeline, then the collectives are
+// queued behind the records.
 // RCCL is loaded with dlopen on first use, so libfm3d.so itself does not depend on it (a process
 // that also loads PyTorch's bundled RCCL keeps one copy per user).
 #include <dlfcn.h>
@@ -96,7 +98,7 @@ struct RcclGroup {
 };
 
 constexpr int kDefaultBlock = 4096;
-constexpr int kSets = 2;  // frame pairs in flight (context sets)
+constexpr int kSets = 4;  // frame pairs in flight (context sets; set 2i joins set 2i + 1's LM launches)
 
 // number of queries of share s under the block-cyclic partition
 int64_t share_count(int64_t nA, int shares, int s, int block) {
@@ -123,6 +125,7 @@ struct fm3d_mgpu {
     std::vector<std::vector<fm3d_point2f>> kpA;     // per device: its gathered keypoints
     bool staged = false;                            // fm3d_mgpu_pipeline_upload ran (set 0)
     bool pending[kSets] = {};
+    bool gathered[kSets] = {};                      // the set's all-gather is queued
     int next = 0;                                   // the set the next submit takes
     int waitNext = 0;                               // the set the next wait takes
     std::string err;
@@ -349,6 +352,7 @@ int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int s
         for (int d = 0; d < ndev; d++) {
             int r = fm3d_ctx_create(s, m->devices[d], &m->ctx[k][d]);
             if (!r) r = fm3d_internal_prepare(m->ctx[k][d]);
+            if (!r && (k & 1)) r = fm3d_pipeline_link(m->ctx[k - 1][d], m->ctx[k][d]);
             if (r) {
                 fm3d_mgpu_destroy(m);
                 return r;
@@ -394,7 +398,8 @@ int fm3d_mgpu_pipeline_upload(fm3d_mgpu* m, const void* descA, int nA, const voi
                               const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1,
                               const uint8_t* img2, int width, int height) {
     if (!m || nA < 0 || nB < 0 || dim <= 0 || (nA && (!descA || !kpts1)) || !kpts2) return mfail(m, FM3D_ERR_INVALID, "bad argument");
-    if (m->pending[0] || m->pending[1]) return mfail(m, FM3D_ERR_INVALID, "a submitted frame pair is pending");
+    for (int k = 0; k < kSets; k++)
+        if (m->pending[k]) return mfail(m, FM3D_ERR_INVALID, "a submitted frame pair is pending");
     const size_t rb = row_bytes(dim, type);
     m->staged = false;
     int r;
@@ -412,7 +417,8 @@ int fm3d_mgpu_pipeline_upload(fm3d_mgpu* m, const void* descA, int nA, const voi
 
 int fm3d_mgpu_pipeline_run(fm3d_mgpu* m, fm3d_record* out, int* nKept, fm3d_pipeline_stats* stats) {
     if (!m || !m->staged) return mfail(m, FM3D_ERR_INVALID, "fm3d_mgpu_pipeline_upload not called");
-    if (m->pending[0] || m->pending[1]) return mfail(m, FM3D_ERR_INVALID, "a submitted frame pair is pending");
+    for (int k = 0; k < kSets; k++)
+        if (m->pending[k]) return mfail(m, FM3D_ERR_INVALID, "a submitted frame pair is pending");
     for (int d = 0; d < m->ndev; d++) {
         int r = fm3d_internal_enqueue(m->ctx[0][d], (fm3d_record*)m->send[0][d]);
         if (r) {
@@ -431,12 +437,16 @@ int fm3d_mgpu_submit(fm3d_mgpu* m, const void* descA, int nA, const void* descB,
                      int width, int height) {
     if (!m || nA < 0 || nB < 0 || dim <= 0 || (nA && (!descA || !kpts1)) || !kpts2) return mfail(m, FM3D_ERR_INVALID, "bad argument");
     const int k = m->next;
-    if (m->pending[k]) return mfail(m, FM3D_ERR_INVALID, "both frame pairs in flight: fm3d_mgpu_wait first");
-    if (m->pending[k ^ 1] && nA != m->nA) return mfail(m, FM3D_ERR_INVALID, "frame pairs in flight must have the same query count");
+    if (m->pending[k]) return mfail(m, FM3D_ERR_INVALID, "every context set holds a frame pair: fm3d_mgpu_wait first");
+    bool others = false;
+    for (int j = 0; j < kSets; j++) others |= m->pending[j];
+    if (others && nA != m->nA) return mfail(m, FM3D_ERR_INVALID, "frame pairs in flight must have the same query count");
     const size_t rb = row_bytes(dim, type);
     int r;
-    if (!m->pending[k ^ 1] && (r = plan(m, nA))) return r;
-    // one host thread per device: gather its queries, stage and queue its whole path
+    if (!others && (r = plan(m, nA))) return r;
+    // one host thread per device: gather its queries, stage and queue its path (a member set: its
+    // front half; a leader set: the front half, one LM launch with the member set's queued pair,
+    // both pairs' records)
     std::vector<int> rc(m->ndev, 0);
     std::vector<std::thread> th;
     for (int d = 0; d < m->ndev; d++)
@@ -452,15 +462,22 @@ int fm3d_mgpu_submit(fm3d_mgpu* m, const void* descA, int nA, const void* descB,
         if (rc[d] && bad < 0) bad = d;
     if (bad >= 0) {
         for (int d = 0; d < m->ndev; d++)
-            if (!rc[d]) fm3d_internal_finish(m->ctx[k][d], nullptr, nullptr);
+            if (!rc[d]) {
+                fm3d_internal_flush(m->ctx[k][d]);
+                fm3d_internal_finish(m->ctx[k][d], nullptr, nullptr);
+            }
         return mfail(m, rc[bad], "device " + std::to_string(m->devices[bad]) + ": " + fm3d_last_error(m->ctx[k][bad]));
     }
     m->pending[k] = true;
-    if ((r = queue_allgather(m, k))) {
-        finish_set(m, k, nullptr, 0, nullptr, nullptr);
-        return r;
+    m->gathered[k] = false;
+    m->next = (k + 1) % kSets;
+    // the all-gathers behind the records now queued: the member set's (its records were queued with
+    // this leader's launch) and this set's
+    for (int j : {k - 1, k}) {
+        if (j < 0 || !m->pending[j] || m->gathered[j] || fm3d_internal_front_only(m->ctx[j][0])) continue;
+        if ((r = queue_allgather(m, j))) return r;
+        m->gathered[j] = true;
     }
-    m->next = k ^ 1;
     return FM3D_OK;
 }
 
@@ -468,7 +485,16 @@ int fm3d_mgpu_wait(fm3d_mgpu* m, fm3d_record* out, int cap, int* nKept, fm3d_pip
     if (!m) return FM3D_ERR_INVALID;
     const int k = m->waitNext;
     if (!m->pending[k]) return mfail(m, FM3D_ERR_INVALID, "no frame pair submitted (fm3d_mgpu_submit)");
-    m->waitNext = k ^ 1;
+    m->waitNext = (k + 1) % kSets;
+    if (!m->gathered[k]) {  // a member set whose leader set took no pair since: its LM alone
+        for (int d = 0; d < m->ndev; d++) {
+            int r = fm3d_internal_flush(m->ctx[k][d]);
+            if (r) return mfail(m, r, fm3d_last_error(m->ctx[k][d]));
+        }
+        int r = queue_allgather(m, k);
+        if (r) return r;
+        m->gathered[k] = true;
+    }
     return finish_set(m, k, out, cap, nKept, stats);
 }
 

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fm3d_device.h"
+#include "fm3d_fastdiv.h"
 #include "fm3d_kernels.h"
 #include "fm3d_lmdif.h"
 
@@ -31,6 +32,61 @@ constexpr int kNccChunk = 512;     // neighbourhood entries staged in LDS at a t
 __device__ __forceinline__ double xor_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
+}
+
+// The evaluateNormal geometry of one neighbourhood entry through one hypothesis' plane (ray-plane
+// intersection :421-470, isInBoundingBox :646-655, projectPointsToImage2 :591-644, isPixelGood
+// :657-665) in the LM kernel's arithmetic forms (fm3d_lm2.hip geometry2), each the
+// same bits as project1 + pixel_good wherever the pixel is good -- the only case its u, v are used:
+//  * mm / nn by div_nn's fast sequence when the hypothesis-uniform numerator passes div_nn_ok: the
+//    quotient is exact below 2^100 and NaN or >= 2^100 elsewhere, so the bounding box decides alike;
+//  * 1/z by recip_z_lo (one guard); a2 = r2 + 2x^2 as fma(x*x, 2, r2) (2*RN(x*x) == RN(2x*x));
+//  * project1's NaN for an infinite r6 dropped (such a u or v is infinite or NaN: not good);
+//  * 0 <= u <= xmax as bits(u) <= bits(xmax): u is never -0.0 (the host hands the kernel a
+//    principal point of +0.0 for -0.0, fm3d_host.cpp lm_camera), negatives and NaNs lie above.
+// Returns good; fx, fy: the float sample coordinates; off: the bilinear window's byte offset.
+__device__ __forceinline__ bool ncc_geometry(const NccParams& p, double ux, double uy, double n0, double n1,
+                                             double n2, double mm, bool mok, double cm, unsigned long long xmaxb,
+                                             unsigned long long ymaxb, float& fx, float& fy, unsigned& off) {
+    const double nn = n0 * ux + n1 * uy + n2 * 1.;
+    const double kk = mok ? div_nn(mm, nn, true) : mm / nn;
+    const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
+    const bool inbox = (fabs(P0) < cm) & (fabs(P1) < cm) & (P2 > 0.) & (P2 < cm);  // NaN fails
+    double x = p.R2[0] * P0 + p.R2[1] * P1 + p.R2[2] * P2 + p.t2[0];
+    double y = p.R2[3] * P0 + p.R2[4] * P1 + p.R2[5] * P2 + p.t2[1];
+    const double z = recip_z_lo(p.R2[6] * P0 + p.R2[7] * P1 + p.R2[8] * P2 + p.t2[2]);
+    x *= z;
+    y *= z;
+    const double xx = x * x, yy = y * y;
+    const double r2 = xx + yy;
+    const double r4 = r2 * r2;
+    const double r6 = r4 * r2;
+    const double a1 = (x + x) * y;
+    const double a2 = __builtin_fma(xx, 2., r2);
+    const double a3 = __builtin_fma(yy, 2., r2);
+    const double cdist = 1 + p.cam.k[0] * r2 + p.cam.k[1] * r4 + p.cam.k[4] * r6;
+    const double xd = x * cdist + p.cam.k[2] * a1 + p.cam.k[3] * a2;
+    const double yd = y * cdist + p.cam.k[2] * a3 + p.cam.k[3] * a1;
+    const double u = xd * p.cam.fx + p.cam.cx;
+    const double v = yd * p.cam.fy + p.cam.cy;
+    const bool good = inbox & ((unsigned long long)__double_as_longlong(u) <= xmaxb) &
+                      ((unsigned long long)__double_as_longlong(v) <= ymaxb);
+    fx = (float)u;
+    fy = (float)v;
+    off = good ? (unsigned)((int)floorf(fy) * p.w + (int)floorf(fx)) : 0u;
+    return good;
+}
+
+// getBilinearInterpPix32f on the gathered window (bilinear(): the same operations)
+__device__ __forceinline__ float ncc_bilinear(const uint8_t* img, unsigned off, int w, float x, float y) {
+    typedef __attribute__((aligned(1))) const uint16_t u16u;
+    const unsigned lo = *(u16u*)(img + off), hi = *(u16u*)(img + off + w);
+    const float x0 = floorf(x), y0 = floorf(y);
+    const float b00 = (float)(lo & 0xff), b01 = (float)(lo >> 8);
+    const float b10 = (float)(hi & 0xff), b11 = (float)(hi >> 8);
+    const float xm0 = 1.0f - (x - x0), xm1 = (x - x0);
+    const float ym0 = 1.0f - (y - y0), ym1 = (y - y0);
+    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
 }
 
 // KPW: hypotheses per wave the register arrays hold (H <= 4 * KPW); sized to H so that 16 hypotheses
@@ -74,6 +130,13 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     int m = 0;
     const double cm = (double)p.cmax;
     const double xmax = (double)p.w, ymax = (double)p.h;  // isPixelGood at scale 1
+    const unsigned long long xmaxb = (unsigned long long)__double_as_longlong(xmax);
+    const unsigned long long ymaxb = (unsigned long long)__double_as_longlong(ymax);
+    bool mok[KPW];
+    for (int k = 0; k < KPW; k++) mok[k] = k < nh && div_nn_ok(mm[k]);
+    // hypotheses of this wave that already failed on some entry (wave-uniform): they score -2
+    // whatever their sums, so their geometry is not computed again
+    unsigned dead = 0;
     // the hypothesis-independent part of a pixel (its undistorted ray and image-1 sample) once per
     // workgroup, kNccChunk entries at a time in LDS; lane l of every wave then takes the entries l,
     // l + 64, l + 128, ... of each chunk -- the same entries in the same order as a lane-strided scan
@@ -83,6 +146,7 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     __shared__ int anyBad1S;
     if (threadIdx.x == 0) anyBad1S = 0;
     __syncthreads();
+    const int nk = FULL ? KPW : nh;  // FULL: H == 4 * KPW, every wave holds KPW hypotheses
     for (int base = 0; base < p.nOffPad; base += kNccChunk) {
         for (int r = 0; r < kNccChunk / 256; r++) {
             const int sl = threadIdx.x + 256 * r, e = base + sl;
@@ -107,43 +171,47 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
             OK[sl] = in;
         }
         __syncthreads();
+        if (anyBad1S) dead = ~0u;  // an image-1 pixel fails: every hypothesis scores -2
         for (int j = 0; j < kNccChunk / 64; j++) {
             const int t = lane + 64 * j;
-            if (base + t >= p.nOffPad) break;
-            if (!OK[t]) continue;
-            m++;
-            const double ux = Rx[t], uy = Ry[t];
-            const double a = (double)A1[t];
-            Sa += a;
-            Saa += a * a;
-            const int nk = FULL ? KPW : nh;  // FULL: H == 4 * KPW, every wave holds KPW hypotheses
+            if (base + 64 * j >= p.nOffPad) break;  // wave-uniform
+            const bool ok = OK[t] != 0;
+            unsigned badNow = 0;
+            if (ok) {
+                m++;
+                const double ux = Rx[t], uy = Ry[t];
+                const double a = (double)A1[t];
+                Sa += a;
+                Saa += a * a;
 #pragma unroll
-            for (int k = 0; k < KPW; k++) {
-                if (k >= nk) break;
-                const double nn = n0[k] * ux + n1[k] * uy + n2[k] * 1.;
-                const double kk = mm[k] / nn;
-                const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-                const bool inbox = (P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm);  // NaN fails
-                double u, v;
-                project1(p.cam, p.R2, p.t2, P0, P1, P2, u, v);
-                if (!inbox || !pixel_good_b(u, v, xmax, ymax)) {
-                    bad[k] = true;
-                    continue;
+                for (int k = 0; k < KPW; k++) {
+                    if (k >= nk) break;
+                    if ((dead >> k) & 1) continue;  // wave-uniform
+                    float fx, fy;
+                    unsigned off;
+                    if (!ncc_geometry(p, ux, uy, n0[k], n1[k], n2[k], mm[k], mok[k], cm, xmaxb, ymaxb, fx, fy, off)) {
+                        badNow |= 1u << k;
+                        continue;
+                    }
+                    const double b = (double)ncc_bilinear(p.img2, off, p.w, fx, fy);
+                    Sb[k] += b;
+                    Sbb[k] += b * b;
+                    Sab[k] += a * b;
                 }
-                const double b = (double)bilinear(p.img2, p.w, (float)u, (float)v);
-                Sb[k] += b;
-                Sbb[k] += b * b;
-                Sab[k] += a * b;
             }
+#pragma unroll
+            for (int k = 0; k < KPW; k++)
+                if (__ballot((badNow >> k) & 1)) dead |= 1u << k;
         }
         __syncthreads();
     }
+    for (int k = 0; k < KPW; k++) bad[k] = (dead >> k) & 1;
     for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o);
     const bool anyBad1 = anyBad1S != 0;
     __shared__ double score[32];
     const double sa = xor_sum(Sa), saa = xor_sum(Saa);
     for (int k = 0; k < nh; k++) {
-        const bool fail = anyBad1 || __any(bad[k]);
+        const bool fail = anyBad1 || bad[k];  // wave-uniform
         const double sb = xor_sum(Sb[k]), sbb = xor_sum(Sbb[k]), sab = xor_sum(Sab[k]);
         if (lane == 0) {
             double s = -2.;

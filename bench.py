@@ -80,8 +80,8 @@ def parse():
                     help="stream (C4 headline): every step a frame pair from host memory to host memory, "
                          "--inflight pairs in flight; resident: inputs uploaded once, one step in flight")
     ap.add_argument("--inflight", type=int, default=2, help="LM launches in flight in the stream mode")
-    ap.add_argument("--lm-pairs", type=int, default=1,
-                    help="frame pairs per LM launch in the stream mode (2: fm3d_pipeline_link)")
+    ap.add_argument("--lm-pairs", type=int, default=2,
+                    help="frame pairs per LM launch in the stream mode (2-4: fm3d_pipeline_link)")
     ap.add_argument("--mgpu", action="store_true",
                     help="the one-process multi-GPU path (fm3d_mgpu, C5) also at --gpus 1 (its reference point)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
@@ -172,11 +172,12 @@ def run_c4_stream(args):
         fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
         ctxs.append(ctx)
         pipes.append(fm3d.Pipeline(ctx))
-    if nl == 2:  # context 2i's pairs join the LM launches of context 2i + 1 (fm3d_pipeline_link)
-        for i in range(0, nf, 2):
-            pipes[i].link(pipes[i + 1])
-    elif nl != 1:
-        raise SystemExit("--lm-pairs: 1 or 2")
+    if not 1 <= nl <= 4:
+        raise SystemExit("--lm-pairs: 1 to 4")
+    # contexts nl*i .. nl*i + nl - 2 join the LM launches of context nl*i + nl - 1 (fm3d_pipeline_link)
+    for i in range(0, nf, nl):
+        for j in range(i, i + nl - 1):
+            pipes[j].link(pipes[i + nl - 1])
     binary = args.desc == "orb"
     bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(nf)]
     inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
@@ -343,13 +344,13 @@ def run_mgpu(args, workload):
     mg.set_g12(pair.g12)
     binary = args.desc == "orb"
     inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
-    bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(2)]
+    bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(2)]  # the last two waits' records
 
     def stream_run(n_steps):
         res, pend, last = [], 0, None
         t_sub = []
         for k in range(n_steps):
-            if pend == 2:
+            if pend == 4:  # fm3d_mgpu's four context sets: two LM launches of two frame pairs each
                 rec, st = mg.wait(bufs[len(res) % 2])
                 res.append((len(rec), st, time.perf_counter() - t_sub[len(res)], records_digest(rec.tobytes())))
                 last, pend = rec, pend - 1
@@ -397,7 +398,8 @@ def run_mgpu(args, workload):
             "parallelism": (f"dp{n} in one process (fm3d_mgpu): 4,096-query blocks dealt round-robin over the "
                             f"devices, one replica of frame B + images and one LM launch per device, RCCL "
                             f"all-gather of counts + 64-B survivor records every step"),
-            "mode": "stream: 2 frame pairs in flight (fm3d_mgpu_submit / fm3d_mgpu_wait)",
+            "mode": ("stream: 4 frame pairs in flight, 2 per LM launch on every device (fm3d_mgpu_submit / "
+                     "fm3d_mgpu_wait, context sets linked by fm3d_pipeline_link)"),
             "timed": ("per step, from host memory to host memory: per-device query gather + H2D (pinned), pyramids, "
                       "match -> NNDR -> DLT -> LM -> records, RCCL all-gather, D2H of device 0's gathered "
                       "records, host merge in query order"),
@@ -406,7 +408,7 @@ def run_mgpu(args, workload):
                        "note": "per frame pair, submit call -> merged records on the host"},
         "input_keypoints_per_s": wl["keypoints"] / frame_s,
         "roofline": {
-            "kernel": "fm3d::lm2_kernel on every device, launches overlapped two at a time",
+            "kernel": "fm3d::lm2_kernel on every device, two frame pairs per launch, launches overlapped",
             "bound": "fp64-valu",
             "achieved": FLOPS_PER_PIXEL_EVAL * pix / frame_s / 1e12,
             "peak": FP64_PEAK_TFLOPS * n, "unit": "TFLOP/s",

@@ -418,13 +418,14 @@ int fm3d_pipeline_submit(fm3d_ctx *ctx, const void *descA, int nA, const void *d
                          const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1,
                          const uint8_t *img2, int width, int height, int queryOffset);
 int fm3d_pipeline_wait(fm3d_ctx *ctx, fm3d_record *out, int cap, int *nKept, fm3d_pipeline_stats *stats);
-/* Join two contexts' LM launches (same device, camera and LM settings): after the link a submit on
-   `member` queues its pair's front half only, and the next submit on `leader` queues ONE LM launch
-   over both pairs' points -- the workgroups whose slots run out of one pair's points take the
-   other's, so the pair fills the launch's end-of-queue tail -- followed by each pair's records on
-   its own stream.  A member waited for before its leader's next submit runs its LM alone.  Each
-   pair's results are those of its own fm3d_pipeline_run, bit for bit.  fm3d_pipeline_run and the
-   other calls of a linked context run unlinked. */
+/* Join contexts' LM launches (same device, camera and LM settings; up to 3 members per leader):
+   after the link a submit on `member` queues its pair's front half only, and the next submit on
+   `leader` queues ONE LM launch over its pair's and every queued member pair's points -- the
+   workgroups whose slots run out of one pair's points take the next's, so the pairs fill each
+   other's end-of-queue tail -- followed by each pair's records on its own stream.  A member waited
+   for before its leader's next submit runs its LM alone.  Each pair's results are those of its own
+   fm3d_pipeline_run, bit for bit.  fm3d_pipeline_run and the other calls of a linked context run
+   unlinked. */
 int fm3d_pipeline_link(fm3d_ctx *member, fm3d_ctx *leader);
 /* BASELINE.json's C2 ("brute-force L2 match + DLT triangulate only"): match -> NNDR -> triangulate on
    the staged inputs, no normals; *nInliers = the triangulated points kept by the z filter (stats:
@@ -466,10 +467,11 @@ int fm3d_mgpu_pipeline_upload(fm3d_mgpu *m, const void *descA, int nA, const voi
 /* out: host buffer, capacity nA records; stats: counts summed over the devices, total_ms / lm_ms =
    the slowest device's */
 int fm3d_mgpu_pipeline_run(fm3d_mgpu *m, fm3d_record *out, int *nKept, fm3d_pipeline_stats *stats);
-/* A stream of frame pairs over the devices (two in flight, as fm3d_pipeline_submit / _wait on one
-   GPU): submit stages one frame pair on every device (host-asynchronous, one host thread per device)
-   and queues its path and all-gather; wait returns the oldest submitted pair's merged records (out:
-   capacity cap).  Pairs in flight together must have the same query count. */
+/* A stream of frame pairs over the devices (up to four in flight, as fm3d_pipeline_submit / _wait
+   on one GPU, two pairs per LM launch through fm3d_pipeline_link): submit stages one frame pair on
+   every device (host-asynchronous, one host thread per device) and queues its path and all-gather;
+   wait returns the oldest submitted pair's merged records (out: capacity cap).  Pairs in flight
+   together must have the same query count. */
 int fm3d_mgpu_submit(fm3d_mgpu *m, const void *descA, int nA, const void *descB, int nB, int dim, int type,
                      const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1, const uint8_t *img2,
                      int width, int height);

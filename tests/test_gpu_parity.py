@@ -501,6 +501,29 @@ def test_ncc_hypotheses_bitwise(fm3d, orc, pair, ray, hphi, htheta):
     assert (b >= 0).mean() > 0.5
 
 
+@pytest.mark.parametrize("cx,cy", [(0.0, 0.0), (-20.0, 10.0)])
+def test_ncc_hypotheses_principal_point(fm3d, orc, pair, cx, cy):
+    """NCC scoring with a principal point on / outside the image edge: the kernel's bit-pattern
+    isPixelGood and fast divisions give the oracle's scores bit for bit."""
+    import dataclasses
+    cam = dataclasses.replace(pair.cam, cx=cx, cy=cy)
+    s = _settings(fm3d, cam, pixelsRay=12, boundWidth=640, boundHeight=480)
+    ctx = fm3d.Context(s)
+    try:
+        sct = fm3d.SingleCameraTriangulator(ctx)
+        sct.set_g12(pair.g12)
+        R2, t2 = sct.camera2()
+        no = fm3d.NormalOptimizer(ctx, sct)
+        no.setImages(pair.img1, pair.img2)
+        X = np.concatenate([np.abs(pair.points[:200]), [[0.0, 0.0, 2.0], [0.05, 0.02, 2.0]]])
+        sc, nb, b = no.nccHypotheses(X, 4, 4, 0.4)
+    finally:
+        ctx.close()
+    rs, rn, rb = orc.ncc_hypotheses(cam, R2, t2, pair.img1, pair.img2, X, 12, 4, 4, 0.4, bound=(640, 480))
+    assert np.array_equal(b, rb) and np.array_equal(sc, rs) and np.array_equal(nb, rn, equal_nan=True)
+    assert (b >= 0).sum() > 0
+
+
 def test_c2_sift10k_match_and_dlt(fm3d, orc, synth):
     """BASELINE configs[1] (C2): 10k SIFT-128 per frame, brute-force L2 match + NNDR + DLT --
     match indices, distances, inlier mask and points bit-exact against the oracle."""
@@ -973,6 +996,45 @@ def test_pipeline_linked_lm_launch_equals_run(fm3d, synth):
         assert st["lm"]["evaluations"] == ref[w][1]["lm"]["evaluations"]
 
 
+def test_pipeline_linked_four_pairs(fm3d, synth):
+    """A leader with three members: four frame pairs in one LM launch, each pair's records equal
+    its own fm3d_pipeline_run; a member without a queued pair is skipped by its leader."""
+    pairs = [synth.make_frame_pair(2000, seed=11), synth.make_frame_pair(1500, seed=12)]
+    s = _settings(fm3d, pairs[0].cam, pixelsRay=10, pyramids=1)
+    ref = []
+    ctx, pipe = _pipe_ctx(fm3d, s, pairs[0].g12)
+    try:
+        for fp in pairs:
+            pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            k, st = pipe.run()
+            ref.append(pipe.records(k))
+    finally:
+        ctx.close()
+    cs = [_pipe_ctx(fm3d, s, pairs[0].g12) for _ in range(4)]
+    ps = [p for _, p in cs]
+    try:
+        for m in ps[:3]:
+            m.link(ps[3])
+        with pytest.raises(fm3d.Fm3dError):
+            cs2 = _pipe_ctx(fm3d, s, pairs[0].g12)
+            try:
+                cs2[1].link(ps[3])  # a fourth member
+            finally:
+                cs2[0].close()
+        for order, members in (((0, 1, 0, 1), (0, 1, 2)), ((1, 1, 0, 0), (0, 2))):
+            for j in members:
+                fp = pairs[order[j]]
+                ps[j].submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            fp = pairs[order[3]]
+            ps[3].submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            for j in list(members) + [3]:
+                rec, _ = ps[j].wait()
+                assert rec.tobytes() == ref[order[j]].tobytes(), (order, j)
+    finally:
+        for c, _ in cs:
+            c.close()
+
+
 def test_pipeline_linked_lm_two_poses(fm3d, synth):
     """Linked frame pairs with different camera-2 poses take the LM kernel's per-problem pose
     (lm2_kernel<true>): each pair's records equal its own fm3d_pipeline_run."""
@@ -1037,8 +1099,8 @@ def test_pipeline_ncc_download_after_other_runs(fm3d, synth):
 
 def test_mgpu_submit_wait_stream_equals_run(fm3d, synth):
     """fm3d_mgpu_submit / fm3d_mgpu_wait (bench.py --gpus N's path) on one device with three logical
-    shares (one replica, one LM launch, RCCL all-gather, host merge): byte-identical to
-    fm3d_pipeline_run of the whole frame pair, pair after pair with two in flight."""
+    shares (one replica, linked context sets: two pairs per LM launch, RCCL all-gather, host merge):
+    byte-identical to fm3d_pipeline_run of the whole frame pair, pair after pair."""
     fp = synth.make_frame_pair(9000, seed=31)
     s = _settings(fm3d, fp.cam, pixelsRay=12, pyramids=1)
     ctx, pipe = _pipe_ctx(fm3d, s, fp.g12)
@@ -1059,6 +1121,9 @@ def test_mgpu_submit_wait_stream_equals_run(fm3d, synth):
         outs += [mg.wait(), mg.wait()]
         with pytest.raises(fm3d.Fm3dError):
             mg.wait()
+        # a pair on a member set waited for before its leader set takes one: its LM alone
+        mg.submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        outs.append(mg.wait())
     finally:
         mg.close()
     assert k > 50
