@@ -89,7 +89,7 @@ def parse():
     ap.add_argument("--no-check", action="store_true", help="skip the C5 byte-identity check against one GPU")
     ap.add_argument("--out", type=str, default="")
     ap.add_argument("--pmc-json", type=str, default=next(
-        (p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_c4.json") for r in (3, 2)) if os.path.exists(p)),
+        (p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_c4.json") for r in (4, 3, 2)) if os.path.exists(p)),
         os.path.join(ROOT, "profiles", "r02_pmc_c4.json")),
                     help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()
