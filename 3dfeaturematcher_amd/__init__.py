@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
-FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_STAR, FEAT_BRISK, FEAT_OTHER = 0, 1, 2, 3, 4, 5, -1  # fm3d_settings.detectorType / extractorType
+FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_STAR, FEAT_BRISK, FEAT_FREAK, FEAT_OTHER = 0, 1, 2, 3, 4, 5, 6, -1  # fm3d_settings.detectorType / extractorType
 DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
@@ -42,7 +42,7 @@ EXPORTS = (
     "fm3d_ncc_hypotheses", "fm3d_mgpu_create", "fm3d_mgpu_destroy", "fm3d_mgpu_last_error", "fm3d_mgpu_set_g12",
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
-    "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link",
+    "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link", "fm3d_freak_compute", "fm3d_freak_set_pairs",
 )
 
 
@@ -247,7 +247,7 @@ class DescriptorsMatcher:
             feats = Features(self.ctx)
             ka, _, da = feats.compute(image_a, feats.detect(image_a))
             kb, _, db = feats.compute(image_b, feats.detect(image_b))
-            binary = S.extractorType in (FEAT_ORB, FEAT_BRISK)
+            binary = S.extractorType in (FEAT_ORB, FEAT_BRISK, FEAT_FREAK)
             m = DescriptorsMatcher(self.ctx, binary=binary).compareWithNNDR(epsilon, da, db, matches)
             return m, ka, kb, da, db
         if S.detectorType == FEAT_ORB and S.extractorType == FEAT_ORB:
@@ -463,8 +463,8 @@ class SIFT:
 
 class Features:
     """The settings' detector and extractor, whatever their types (descriptorsmatcher.cpp:176-359):
-    STATIC SURF / ORB / SIFT / FAST / STAR or ADAPTIVE FAST / SURF / STAR detection (fm3d_detect), SURF / SIFT / ORB / BRISK
-    description (fm3d_compute) on any keypoints."""
+    STATIC SURF / ORB / SIFT / FAST / STAR or ADAPTIVE FAST / SURF / STAR detection (fm3d_detect), SURF / SIFT / ORB / BRISK /
+    FREAK description (fm3d_compute) on any keypoints."""
 
     def __init__(self, ctx: Context):
         self.ctx = ctx
@@ -504,6 +504,15 @@ class Features:
         self.ctx.check(lib().fm3d_compute(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, _vp(kin), n, _vp(kout),
                                           _ptr(kept, ctypes.c_int32), ctypes.byref(m), _vp(desc)))
         return kout[:m.value], kept[:m.value], desc[:m.value]
+
+    def set_freak_pairs(self, pairs=None):
+        """fm3d_freak_set_pairs: FREAK's 512 selected pairs (indices into the 903 point pairs); None restores
+        the default table (include/fm3d_freak.h)"""
+        if pairs is None:
+            self.ctx.check(lib().fm3d_freak_set_pairs(self.ctx.handle, None, 0))
+        else:
+            a = np.ascontiguousarray(pairs, dtype=np.int32)
+            self.ctx.check(lib().fm3d_freak_set_pairs(self.ctx.handle, _ptr(a, ctypes.c_int32), len(a)))
 
     def fast(self, image: np.ndarray, threshold: int = 10, nonmax: bool = True) -> np.ndarray:
         """cv::FastFeatureDetector(threshold, nonmax).detect: KEYPOINT records in raster order"""

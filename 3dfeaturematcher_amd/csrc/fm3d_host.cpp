@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "fm3d.h"
+#include "fm3d_freak.h"
 #include "fm3d_kernels.h"
 
 using fm3d::Camera;
@@ -118,6 +119,9 @@ struct fm3d_ctx {
         siftNpk, siftKp, siftDesc;
     // BRISK description
     DevBuf brImg, brSum, brKp, brIdx, brPat, brPairs, brDesc;
+    // FREAK description (frLut: the whole default pattern, uploaded once)
+    DevBuf frImg, frSum, frKp, frScale, frLut, frOp, frPairs, frAng, frDesc;
+    std::vector<int> freakUserPairs;  // fm3d_freak_set_pairs (empty: FM3D_FREAK_DEF_PAIRS)
     // STAR detection
     DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut, starWork;
     // NCC hypotheses over the pipeline's inliers (fm3d_pipeline_run_ncc)
@@ -1658,7 +1662,8 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->siftAng, &c->siftNpk, &c->siftKp, &c->siftDesc, &c->brImg, &c->brSum, &c->brKp,
                       &c->brIdx, &c->brPat, &c->brPairs, &c->brDesc, &c->starImg, &c->starS, &c->starT, &c->starF,
                       &c->starR, &c->starZ, &c->starKp, &c->starFlag, &c->starPos, &c->starOut, &c->starWork,
-                      &c->nccS, &c->nccN, &c->nccB, &c->pcnt};
+                      &c->nccS, &c->nccN, &c->nccB, &c->pcnt, &c->frImg, &c->frSum, &c->frKp, &c->frScale,
+                      &c->frLut, &c->frOp, &c->frPairs, &c->frAng, &c->frDesc};
     for (DevBuf* b : bufs) b->release();
     HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall};
     for (HostBuf* b : hbufs) b->release();
@@ -2680,7 +2685,7 @@ int fm3d_extract_descriptors_from_patches_any(fm3d_ctx* c, const uint8_t* patche
     const int ex = c->s.extractorType;
     if (ex == FM3D_FEAT_SURF || ex == FM3D_FEAT_SIFT)
         return fm3d_extract_descriptors_from_patches(c, patches, P, size, static_cast<float*>(desc));
-    if (ex != FM3D_FEAT_ORB && ex != FM3D_FEAT_BRISK)
+    if (ex != FM3D_FEAT_ORB && ex != FM3D_FEAT_BRISK && ex != FM3D_FEAT_FREAK)
         return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' extractor type has no GPU implementation");
     // descriptorsmatcher.cpp:142-172: the centred keypoint per patch, compute on each patch; the rows
     // start as Mat::zeros and a dropped keypoint's empty row copies nothing
@@ -2693,8 +2698,9 @@ int fm3d_extract_descriptors_from_patches_any(fm3d_ctx* c, const uint8_t* patche
         fm3d_keypoint ko;
         int m = 0, r;
         const uint8_t* img = patches + (size_t)p * size * size;
-        r = ex == FM3D_FEAT_ORB ? fm3d_orb_compute(c, img, size, size, &k, 1, &ko, nullptr, &m, d + (size_t)p * cols)
-                                : fm3d_brisk_compute(c, img, size, size, &k, 1, &ko, nullptr, &m, d + (size_t)p * cols);
+        r = ex == FM3D_FEAT_ORB     ? fm3d_orb_compute(c, img, size, size, &k, 1, &ko, nullptr, &m, d + (size_t)p * cols)
+            : ex == FM3D_FEAT_BRISK ? fm3d_brisk_compute(c, img, size, size, &k, 1, &ko, nullptr, &m, d + (size_t)p * cols)
+                                    : fm3d_freak_compute(c, img, size, size, &k, 1, &ko, nullptr, &m, d + (size_t)p * cols);
         if (r) return r;
         if (p == 0 && m == 0 && ex == FM3D_FEAT_ORB)
             return fail(c, FM3D_ERR_INVALID, "ORB drops the first patch's keypoint (the reference's rows would have 0 columns)");
@@ -3194,7 +3200,157 @@ int brisk_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keyp
     return FM3D_OK;
 }
 
+// ---------------------------------------------------------------- FREAK extractor
+// cv::FREAK() on given keypoints (OpenCV 2.4.9 freak.cpp; oracle/orc_freak.c): FREAK::buildPattern's
+// tables (the 43 points of each of the 64 scales and 256 orientations in glibc's double cos / sin, the
+// pattern sizes, the orientation weights) and the per-keypoint scale and border filter stay on the
+// host in the same float / double expressions and glibc calls; intensities, orientation and bits run
+// on the GPU (fm3d_freak.hip).
+namespace freak {
+constexpr float kPatternScale = 22.0f;  // cv::FREAK() defaults
+constexpr int kOctaves = 4;
+struct Pattern {
+    std::vector<float4> lut;  // (x, y, sigma, 0) per (scale, orientation, point)
+    int sizes[fm3d::kFreakScales];
+    int op[4 * fm3d::kFreakOrientPairs];  // (i, j, weight_dx, weight_dy)
+};
+const Pattern& pattern() {
+    static const Pattern P = [] {
+        Pattern p;
+        const int n[8] = {6, 6, 6, 6, 6, 6, 6, 1};
+        const double bigR = 2.0 / 3.0, smallR = 2.0 / 24.0;
+        const double unitSpace = (bigR - smallR) / 21.0;
+        const double radius[8] = {bigR, bigR - 6 * unitSpace, bigR - 11 * unitSpace, bigR - 15 * unitSpace,
+                                  bigR - 18 * unitSpace, bigR - 20 * unitSpace, smallR, 0.0};
+        const double sigma[8] = {radius[0] / 2.0, radius[1] / 2.0, radius[2] / 2.0, radius[3] / 2.0,
+                                 radius[4] / 2.0, radius[5] / 2.0, radius[6] / 2.0, radius[6] / 2.0};
+        const double scaleStep = std::pow(2.0, (double)kOctaves / fm3d::kFreakScales);
+        p.lut.resize((size_t)fm3d::kFreakScales * fm3d::kFreakOrient * fm3d::kFreakPoints);
+        for (int s = 0; s < fm3d::kFreakScales; s++) {
+            const double scalingFactor = std::pow(scaleStep, (double)s);
+            p.sizes[s] = 0;
+            for (int r = 0; r < fm3d::kFreakOrient; r++) {
+                const double theta = (double)r * 2 * M_PI / (double)fm3d::kFreakOrient;
+                int q = 0;
+                for (int i = 0; i < 8; i++)
+                    for (int k = 0; k < n[i]; k++) {
+                        const double beta = M_PI / n[i] * (i % 2);
+                        const double alpha = (double)k * 2 * M_PI / (double)n[i] + beta + theta;
+                        float4& pt = p.lut[((size_t)s * fm3d::kFreakOrient + r) * fm3d::kFreakPoints + q];
+                        pt.x = (float)(radius[i] * std::cos(alpha) * scalingFactor * kPatternScale);
+                        pt.y = (float)(radius[i] * std::sin(alpha) * scalingFactor * kPatternScale);
+                        pt.z = (float)(sigma[i] * scalingFactor * kPatternScale);
+                        pt.w = 0.f;
+                        const int sizeMax = (int)std::ceil((radius[i] + sigma[i]) * scalingFactor * kPatternScale) + 1;
+                        if (p.sizes[s] < sizeMax) p.sizes[s] = sizeMax;
+                        q++;
+                    }
+            }
+        }
+        for (int m = fm3d::kFreakOrientPairs; m--;) {
+            const int i = FM3D_FREAK_ORIENT_PAIRS[2 * m], j = FM3D_FREAK_ORIENT_PAIRS[2 * m + 1];
+            const float dx = p.lut[i].x - p.lut[j].x, dy = p.lut[i].y - p.lut[j].y;
+            const float norm_sq = dx * dx + dy * dy;
+            p.op[4 * m] = i;
+            p.op[4 * m + 1] = j;
+            p.op[4 * m + 2] = (int)((dx / norm_sq) * 4096.0 + 0.5);
+            p.op[4 * m + 3] = (int)((dy / norm_sq) * 4096.0 + 0.5);
+        }
+        return p;
+    }();
+    return P;
+}
+int kscale(float size) {
+    const float sizeCst = (float)(fm3d::kFreakScales / (0.693147180559945 * kOctaves));
+    int s = (int)(logf(size / 7) * sizeCst + 0.5);
+    return std::min(std::max(s, 0), fm3d::kFreakScales - 1);
+}
+// the compressed pair index (FREAK::DEF_PAIRS) -> (i, j < i) of the 903 pairs in generation order
+int2 pair_of(int k) {
+    int a = 1;
+    while (k >= a) k -= a++;
+    return make_int2(a, k);
+}
+}  // namespace freak
+
+int freak_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n, fm3d_keypoint* kout,
+                  int32_t* kept, int* nOut, uint8_t* desc) {
+    const freak::Pattern& P = freak::pattern();
+    *nOut = 0;
+    // runByKeypointSize(FLT_EPSILON) (NaN dropped), then FREAK's scale-dependent border, order kept
+    std::vector<fm3d_keypoint> K;
+    std::vector<int> src, scl;
+    for (int q = 0; q < n; q++) {
+        const fm3d_keypoint& k = kpts[q];
+        if (!(k.size >= FLT_EPSILON && k.size <= FLT_MAX)) continue;
+        const int s = freak::kscale(k.size);
+        const float ps = (float)P.sizes[s];
+        if (k.x <= ps || k.y <= ps || k.x >= w - ps || k.y >= h - ps) continue;
+        K.push_back(k);
+        src.push_back(q);
+        scl.push_back(s);
+    }
+    const int m = (int)K.size();
+    if (m == 0) return FM3D_OK;
+    const long long W1H1 = (long long)(w + 1) * (h + 1);
+    if (W1H1 > INT32_MAX / 4) return fail(c, FM3D_ERR_INVALID, "image too large for FREAK");
+    std::vector<int2> pairs(FM3D_FREAK_NB_PAIRS);
+    for (int k = 0; k < FM3D_FREAK_NB_PAIRS; k++)
+        pairs[k] = freak::pair_of(c->freakUserPairs.empty() ? FM3D_FREAK_DEF_PAIRS[k] : c->freakUserPairs[k]);
+    if (c->frLut.bytes == 0) {  // the whole pattern, once per context (8.4 MB)
+        HIPCHK(c, c->frLut.ensure(P.lut.size() * sizeof(float4)));
+        HIPCHK(c, c->frOp.ensure(sizeof(P.op)));
+        HIPCHK(c, hipMemcpy(c->frLut.p, P.lut.data(), P.lut.size() * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->frOp.p, P.op, sizeof(P.op), hipMemcpyHostToDevice));
+    }
+    HIPCHK(c, c->frImg.ensure((size_t)w * h));
+    HIPCHK(c, c->frSum.ensure((size_t)W1H1 * sizeof(int)));
+    HIPCHK(c, c->frKp.ensure((size_t)m * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->frScale.ensure((size_t)m * sizeof(int)));
+    HIPCHK(c, c->frPairs.ensure(pairs.size() * sizeof(int2)));
+    HIPCHK(c, c->frAng.ensure((size_t)m * sizeof(float)));
+    HIPCHK(c, c->frDesc.ensure((size_t)m * 64));
+    HIPCHK(c, hipMemcpyAsync(c->frImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->frKp.p, K.data(), (size_t)m * sizeof(fm3d_keypoint), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->frScale.p, scl.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->frPairs.p, pairs.data(), pairs.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_integral(c->frImg.as<uint8_t>(), w, h, c->frSum.as<int>(), c->stream);
+    fm3d::launch_freak_desc(c->frImg.as<uint8_t>(), c->frSum.as<int>(), w, c->frKp.as<fm3d_keypoint>(),
+                            c->frScale.as<int>(), m, c->frLut.as<float4>(), c->frOp.as<int4>(), c->frPairs.as<int2>(),
+                            c->frAng.as<float>(), c->frDesc.as<uint8_t>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    std::vector<float> ang(m);
+    HIPCHK(c, hipMemcpyAsync(desc, c->frDesc.p, (size_t)m * 64, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ang.data(), c->frAng.p, (size_t)m * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < m; i++) {
+        kout[i] = K[i];
+        kout[i].angle = ang[i];  // FREAK's orientation normalisation sets the keypoint angle
+        if (kept) kept[i] = src[i];
+    }
+    *nOut = m;
+    return FM3D_OK;
+}
+
 extern "C" {
+int fm3d_freak_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,
+                       fm3d_keypoint* kout, int32_t* kept, int* nOut, uint8_t* desc) {
+    if (!c || !img || !nOut || w <= 0 || h <= 0 || n < 0 || (n > 0 && (!kpts || !kout || !desc)))
+        return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    return freak_compute(c, img, w, h, kpts, n, kout, kept, nOut, desc);
+}
+
+int fm3d_freak_set_pairs(fm3d_ctx* c, const int32_t* pairs, int n) {
+    if (!c || (pairs && n != FM3D_FREAK_NB_PAIRS)) return FM3D_ERR_INVALID;
+    if (pairs)
+        for (int k = 0; k < n; k++)
+            if (pairs[k] < 0 || pairs[k] >= 903) return fail(c, FM3D_ERR_INVALID, "a FREAK pair index outside [0, 903)");
+    c->freakUserPairs.clear();
+    if (pairs) c->freakUserPairs.assign(pairs, pairs + n);
+    return FM3D_OK;
+}
+
 int fm3d_brisk_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,
                        fm3d_keypoint* kout, int32_t* kept, int* nOut, uint8_t* desc) {
     if (!c || !img || !nOut || w <= 0 || h <= 0 || n < 0 || (n > 0 && (!kpts || !kout || !desc)))
@@ -3351,6 +3507,7 @@ int fm3d_descriptor_info(const fm3d_ctx* c, int* cols, int* type) {
         *type = FM3D_DESC_BITS;
         return FM3D_OK;
     case FM3D_FEAT_BRISK:
+    case FM3D_FEAT_FREAK:
         *cols = 64;
         *type = FM3D_DESC_BITS;
         return FM3D_OK;
@@ -3370,6 +3527,8 @@ int fm3d_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypo
         return fm3d_orb_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<uint8_t*>(desc));
     case FM3D_FEAT_BRISK:
         return fm3d_brisk_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<uint8_t*>(desc));
+    case FM3D_FEAT_FREAK:
+        return fm3d_freak_compute(c, img, w, h, kpts, n, kout, kept, nOut, static_cast<uint8_t*>(desc));
     default:
         return c ? fail(c, FM3D_ERR_UNSUPPORTED, "the settings' extractor type has no GPU implementation")
                  : FM3D_ERR_INVALID;

@@ -368,6 +368,14 @@ void launch_star_nms(const float* resp, const short* sizes, int w, int h, const 
 void launch_star_scatter(const fm3d_keypoint* kp, const int* flag, const int* pos, int n, fm3d_keypoint* out,
                          hipStream_t s);
 
+// ---------------------------------------------------------------- FREAK (fm3d_freak.hip)
+constexpr int kFreakScales = 64, kFreakOrient = 256, kFreakPoints = 43, kFreakOrientPairs = 45;
+// lut: (x, y, sigma, 0) per (scale, orientation, point); opairs: (i, j, weight_dx, weight_dy); pairs: the
+// 512 (i, j); scale: each keypoint's pattern scale; angle / desc: n floats / n x 64 bytes
+void launch_freak_desc(const uint8_t* img, const int* sum, int w, const fm3d_keypoint* kp, const int* scale, int n,
+                       const float4* lut, const int4* opairs, const int2* pairs, float* angle, uint8_t* desc,
+                       hipStream_t s);
+
 // ---------------------------------------------------------------- BRISK (fm3d_brisk.hip)
 // pat: 60 (x, y, sigma, 0) pattern points per (scale, rotation) in use; pidx: each keypoint's row of pat;
 // pairs: the short pairs (i, j); desc: n x 64 bytes

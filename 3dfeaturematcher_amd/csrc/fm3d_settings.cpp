@@ -241,6 +241,7 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
                                : ex == "ORB"   ? FM3D_FEAT_ORB
                                : ex == "SIFT"  ? FM3D_FEAT_SIFT
                                : ex == "BRISK" ? FM3D_FEAT_BRISK
+                               : ex == "FREAK" ? FM3D_FEAT_FREAK
                                                : FM3D_FEAT_OTHER;
         get_i(kv, "FeatureOptions.BriskDetector.Threshold", &s->briskThreshold);
         get_i(kv, "FeatureOptions.BriskDetector.Octaves", &s->briskOctaves);

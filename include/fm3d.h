@@ -113,6 +113,7 @@ typedef struct fm3d_settings {
 #define FM3D_FEAT_FAST 3
 #define FM3D_FEAT_STAR 4
 #define FM3D_FEAT_BRISK 5 /* extractor only: the reference's generateDetector has no BRISK branch */
+#define FM3D_FEAT_FREAK 6 /* extractor only (cv::FREAK(), descriptorsmatcher.cpp:350-353) */
 #define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
@@ -373,6 +374,17 @@ int fm3d_fast_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, i
    bytes (512 bits) per kept keypoint. */
 int fm3d_brisk_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const fm3d_keypoint *kpts, int n,
                        fm3d_keypoint *kout, int32_t *kept, int *nOut, uint8_t *desc);
+/* descriptor_extractor_->compute(img, kpts, desc) of the settings' FREAK extractor
+   (descriptorsmatcher.cpp:350-353: cv::FREAK() -- orientation and scale normalised, patternScale 22,
+   4 octaves; OpenCV 2.4.9 freak.cpp): keypoints of size < FLT_EPSILON and those within their scale's
+   pattern size of the border dropped (order kept; kept[] = input index, may be NULL), kout's angle set
+   to FREAK's orientation, then 64 bytes (512 bits, the SSE2 build's bit order) per kept keypoint. */
+int fm3d_freak_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const fm3d_keypoint *kpts, int n,
+                       fm3d_keypoint *kout, int32_t *kept, int *nOut, uint8_t *desc);
+/* the 512 selected pairs, as indices into the 903 pairs (i, j < i) of the 43 pattern points in
+   generation order: OpenCV's FREAK::DEF_PAIRS is restated in include/fm3d_freak.h (unverified: OpenCV
+   is not in this image) -- pass OpenCV's own table here for parity with it; NULL restores the default. */
+int fm3d_freak_set_pairs(fm3d_ctx *ctx, const int32_t *pairs, int n);
 /* cv::StarFeatureDetector(maxSize, response, lineThreshold, lineBinarized, suppression).detect
    (descriptorsmatcher.cpp:204-213; OpenCV 2.4.9 StarDetector, CenSurE): KeyPoint(x, y, size, -1,
    response) in tile order.  FM3D_ERR_INVALID where OpenCV's result is undefined (min(w, h) <= 6,
@@ -388,8 +400,8 @@ int fm3d_star_responses(fm3d_ctx *ctx, const uint8_t *img, int width, int height
    DynamicAdaptedFeatureDetector).  *n = all; min(*n, cap) written.  FM3D_ERR_UNSUPPORTED for the
    detector types without a GPU implementation (STAR, MSER, the STAR adjuster). */
 int fm3d_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, fm3d_keypoint *kpts, int cap, int *n);
-/* the row layout of the settings' extractor: SURF 64 | 128 and SIFT 128 (FM3D_DESC_F32), ORB 32 bytes
-   (FM3D_DESC_BITS); FM3D_ERR_UNSUPPORTED for BRISK / FREAK. */
+/* the row layout of the settings' extractor: SURF 64 | 128 and SIFT 128 (FM3D_DESC_F32), ORB 32 bytes,
+   BRISK and FREAK 64 bytes (FM3D_DESC_BITS). */
 int fm3d_descriptor_info(const fm3d_ctx *ctx, int *cols, int *type);
 /* descriptor_extractor_->compute(img, kpts, desc) of generateExtractor (:113-114, 295-359): the
    settings' SURF / SIFT / ORB extractor on any keypoints (fm3d_surf_compute / fm3d_sift_compute /

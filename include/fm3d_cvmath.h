@@ -173,6 +173,8 @@ FM3D_HD float fm3d_cv_atan2_deg(float y, float x)
 /* the reference's cosf / sinf / powf(2.f, y), deterministic */
 FM3D_HD float fm3d_cv_cosf(float x) { return (float)fm3d_cos((double)x); }
 FM3D_HD float fm3d_cv_sinf(float x) { return (float)fm3d_sin((double)x); }
+/* atan2f (FREAK's orientation): the float of the deterministic double atan2 */
+FM3D_HD float fm3d_cv_atan2f(float y, float x) { return (float)fm3d_atan2((double)y, (double)x); }
 FM3D_HD float fm3d_cv_exp2f(float y)
 {
     const float k = floorf(y);

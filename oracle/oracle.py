@@ -870,3 +870,57 @@ def brisk_compute(img, kpts):
     m = lib().orc_brisk_compute(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _kp(kin), ctypes.c_int(n),
                                 _kp(kout), _p(kept, ctypes.c_int), _p(desc, ctypes.c_uint8))
     return kout[:m], kept[:m], desc[:m]
+
+
+# ---------------------------------------------------------------- FREAK (orc_freak.c)
+def freak_point(scale, rot, i):
+    """FREAK buildPattern's point i at (scale, orientation) of the default pattern: (x, y, sigma) float32"""
+    x, y, s = ctypes.c_float(0), ctypes.c_float(0), ctypes.c_float(0)
+    lib().orc_freak_point(ctypes.c_int(scale), ctypes.c_int(rot), ctypes.c_int(i), ctypes.byref(x), ctypes.byref(y),
+                          ctypes.byref(s))
+    return np.float32(x.value), np.float32(y.value), np.float32(s.value)
+
+
+def freak_size(scale):
+    return int(lib().orc_freak_size(ctypes.c_int(scale)))
+
+
+def freak_kscale(size, octaves=4):
+    return int(lib().orc_freak_kscale(ctypes.c_float(size), ctypes.c_int(octaves)))
+
+
+def freak_weights():
+    """the 45 orientation pairs' (weight_dx, weight_dy) of the default pattern"""
+    lut = np.zeros(64 * 256 * 43 * 3, np.float32)
+    sizes = np.zeros(64, np.int32)
+    lib().orc_freak_pattern(ctypes.c_float(22.0), ctypes.c_int(4), _p(lut, ctypes.c_float), _p(sizes, ctypes.c_int))
+    wx = np.zeros(45, np.int32)
+    wy = np.zeros(45, np.int32)
+    lib().orc_freak_weights(_p(lut, ctypes.c_float), _p(wx, ctypes.c_int), _p(wy, ctypes.c_int))
+    return wx, wy
+
+
+def freak_mean_intensity(img, kx, ky, px, py, sigma):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    s = np.zeros((h + 1) * (w + 1), np.int32)
+    lib().orc_freak_integral(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _p(s, ctypes.c_int))
+    return int(lib().orc_freak_mean_intensity(_p(img, ctypes.c_uint8), _p(s, ctypes.c_int), ctypes.c_int(w),
+                                              ctypes.c_float(kx), ctypes.c_float(ky), ctypes.c_float(px),
+                                              ctypes.c_float(py), ctypes.c_float(sigma)))
+
+
+def freak_compute(img, kpts, pairs=None):
+    """DescriptorExtractor::compute with cv::FREAK() (defaults): (kept keypoints with their angles, input
+    index of each, (m, 64) uint8 descriptors); pairs: 512 pair indices (None: the default table)"""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    kin = np.ascontiguousarray(kpts, dtype=KEYPOINT)
+    n = len(kin)
+    kout = np.zeros(max(n, 1), dtype=KEYPOINT)
+    kept = np.zeros(max(n, 1), dtype=np.int32)
+    desc = np.zeros((max(n, 1), 64), dtype=np.uint8)
+    pp = None if pairs is None else _p(np.ascontiguousarray(pairs, dtype=np.int32), ctypes.c_int)
+    m = lib().orc_freak_compute(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _kp(kin), ctypes.c_int(n),
+                                pp, _kp(kout), _p(kept, ctypes.c_int), _p(desc, ctypes.c_uint8))
+    return kout[:m], kept[:m], desc[:m]

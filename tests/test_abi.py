@@ -187,7 +187,7 @@ def test_settings_feature_options(fm3d, tmp_path):
     assert (s.extractorType, s.briskThreshold, s.briskOctaves) == (fm3d.FEAT_BRISK, 25, 0)
     assert (fm3d.Settings.default().briskThreshold, fm3d.Settings.default().briskOctaves) == (30, 3)
     assert load("FeatureOptions:\n   DetectorType: BRISK\n").detectorType == fm3d.FEAT_OTHER  # no BRISK detector
-    assert load("FeatureOptions:\n   ExtractorType: FREAK\n").extractorType == fm3d.FEAT_OTHER
+    assert load("FeatureOptions:\n   ExtractorType: FREAK\n").extractorType == fm3d.FEAT_FREAK
     for mode, det in (("ADAPTIVE", "ORB"), ("STATIC", "MSER"), ("OTHER", "SURF")):
         s = load(f"FeatureOptions:\n   DetectorMode: {mode}\n   DetectorType: {det}\n")
         assert s.detectorType == fm3d.FEAT_OTHER, (mode, det)
