@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("FM3D_LIB") or os.path.join(_HERE, "libfm3d.so")
 
 FM3D_OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_PARSE, ERR_NAN_PLANE = -1, -2, -3, -4, -5, -6
-FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_STAR, FEAT_BRISK, FEAT_FREAK, FEAT_OTHER = 0, 1, 2, 3, 4, 5, 6, -1  # fm3d_settings.detectorType / extractorType
+FEAT_SURF, FEAT_ORB, FEAT_SIFT, FEAT_FAST, FEAT_STAR, FEAT_BRISK, FEAT_FREAK, FEAT_MSER, FEAT_OTHER = 0, 1, 2, 3, 4, 5, 6, 7, -1  # fm3d_settings.detectorType / extractorType
 DESC_F32, DESC_U8, DESC_BITS = 0, 1, 2
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
@@ -43,6 +43,7 @@ EXPORTS = (
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
     "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link", "fm3d_freak_compute", "fm3d_freak_set_pairs",
+    "fm3d_mser_detect", "fm3d_mser_regions",
 )
 
 
@@ -77,6 +78,10 @@ class Settings(ctypes.Structure):
         ("starMaxSize", ctypes.c_int), ("starResponse", ctypes.c_int), ("starLineThreshold", ctypes.c_int),
         ("starLineBinarized", ctypes.c_int), ("starSuppression", ctypes.c_int),
         ("briskThreshold", ctypes.c_int), ("briskOctaves", ctypes.c_int),
+        ("mserDelta", ctypes.c_int), ("mserMinArea", ctypes.c_int), ("mserMaxArea", ctypes.c_int),
+        ("mserMaxVariation", ctypes.c_double), ("mserMinDiversity", ctypes.c_double),
+        ("mserMaxEvolution", ctypes.c_int), ("mserAreaThreshold", ctypes.c_double),
+        ("mserMinMargin", ctypes.c_double), ("mserEdgeBlurSize", ctypes.c_int),
     ]
 
     @staticmethod
@@ -570,6 +575,48 @@ class Features:
         self.ctx.check(lib().fm3d_star_responses(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, max_size,
                                                  _ptr(R, ctypes.c_float), _ptr(Z, ctypes.c_int16), ctypes.byref(b)))
         return b.value, R, Z
+
+    def mser(self, image: np.ndarray, delta: int = 5, min_area: int = 60, max_area: int = 14400,
+             max_variation: float = 0.25, min_diversity: float = 0.2) -> np.ndarray:
+        """cv::MserFeatureDetector(delta, minArea, maxArea, maxVariation, minDiversity, ...).detect:
+        KEYPOINT records in region order"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap = 4096
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            n = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_mser_detect(self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, delta, min_area,
+                                                  max_area, ctypes.c_double(max_variation),
+                                                  ctypes.c_double(min_diversity), _vp(k), cap, ctypes.byref(n)))
+            if n.value <= cap:
+                return k[:n.value]
+            cap = n.value
+
+    def mser_regions(self, image: np.ndarray, delta: int = 5, min_area: int = 60, max_area: int = 14400,
+                     max_variation: float = 0.25, min_diversity: float = 0.2):
+        """MSER::operator()(img, msers): [(colour -1 | +1, (k, 2) int32 points (x, y) in region-list order)]"""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap, pcap = 1024, 1 << 18
+        while True:
+            color = np.zeros(cap, np.int32)
+            count = np.zeros(cap, np.int32)
+            pts = np.zeros((pcap, 2), np.int32)
+            nr, npt = ctypes.c_int(0), ctypes.c_int64(0)
+            self.ctx.check(lib().fm3d_mser_regions(
+                self.ctx.handle, _ptr(img, ctypes.c_uint8), w, h, delta, min_area, max_area,
+                ctypes.c_double(max_variation), ctypes.c_double(min_diversity), _ptr(color, ctypes.c_int32),
+                _ptr(count, ctypes.c_int32), cap, _ptr(pts, ctypes.c_int32), ctypes.c_int64(pcap), ctypes.byref(nr),
+                ctypes.byref(npt)))
+            if nr.value <= cap and npt.value <= pcap:
+                break
+            cap, pcap = max(cap, nr.value), max(pcap, npt.value)
+        out, off = [], 0
+        for i in range(nr.value):
+            out.append((int(color[i]), pts[off:off + count[i]].copy()))
+            off += int(count[i])
+        return out
 
 
 class SingleCameraTriangulator:

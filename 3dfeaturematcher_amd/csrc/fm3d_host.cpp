@@ -121,6 +121,7 @@ struct fm3d_ctx {
     DevBuf brImg, brSum, brKp, brIdx, brPat, brPairs, brDesc;
     // FREAK description (frLut: the whole default pattern, uploaded once)
     DevBuf frImg, frSum, frKp, frScale, frLut, frOp, frPairs, frAng, frDesc;
+    DevBuf msImg, msWork, msHeap, msNode, msHist, msReg, msCnt, msOff, msXY, msScr, msKp, msFlag, msPos, msOut;
     std::vector<int> freakUserPairs;  // fm3d_freak_set_pairs (empty: FM3D_FREAK_DEF_PAIRS)
     // STAR detection
     DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut, starWork;
@@ -1663,7 +1664,9 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->brIdx, &c->brPat, &c->brPairs, &c->brDesc, &c->starImg, &c->starS, &c->starT, &c->starF,
                       &c->starR, &c->starZ, &c->starKp, &c->starFlag, &c->starPos, &c->starOut, &c->starWork,
                       &c->nccS, &c->nccN, &c->nccB, &c->pcnt, &c->frImg, &c->frSum, &c->frKp, &c->frScale,
-                      &c->frLut, &c->frOp, &c->frPairs, &c->frAng, &c->frDesc};
+                      &c->frLut, &c->frOp, &c->frPairs, &c->frAng, &c->frDesc, &c->msImg, &c->msWork,
+                      &c->msHeap, &c->msNode, &c->msHist, &c->msReg, &c->msCnt, &c->msOff, &c->msXY, &c->msScr,
+                      &c->msKp, &c->msFlag, &c->msPos, &c->msOut};
     for (DevBuf* b : bufs) b->release();
     HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall};
     for (HostBuf* b : hbufs) b->release();
@@ -3332,7 +3335,151 @@ int freak_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keyp
     return FM3D_OK;
 }
 
+// MSER (fm3d_mser.hip): the two floods, then the regions' records and point offsets.  regs: pass 0's
+// regions then pass 1's ({colour, head node, count, 0}); off: their prefix (points before each).
+int mser_flood(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserParams& P, fm3d::MserLayout& L,
+               std::vector<int4>& regs, int& n0, std::vector<long long>& off) {
+    if (w <= 0 || h <= 0) return fail(c, FM3D_ERR_INVALID, "MSER: empty image");
+    if ((long long)w * h > (1LL << 28) || (long long)(h + 2) * 2 * (w + 2) > (1LL << 30))
+        return fail(c, FM3D_ERR_INVALID, "MSER: image too large");
+    L = fm3d::mser_layout(w, h);
+    HIPCHK(c, c->msImg.ensure((size_t)w * h));
+    HIPCHK(c, c->msWork.ensure((size_t)2 * L.imgInts * sizeof(int)));
+    HIPCHK(c, c->msHeap.ensure((size_t)2 * L.heapInts * sizeof(int)));
+    HIPCHK(c, c->msNode.ensure((size_t)2 * L.nodes * sizeof(int2)));
+    HIPCHK(c, c->msHist.ensure((size_t)2 * L.hists * sizeof(fm3d::MserHist)));
+    HIPCHK(c, c->msReg.ensure((size_t)2 * L.regCap * sizeof(int4)));
+    HIPCHK(c, c->msCnt.ensure(2 * sizeof(int)));
+    HIPCHK(c, hipMemcpyAsync(c->msImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_mser_flood(c->msImg.as<uint8_t>(), L, P, c->msWork.as<int>(), c->msHeap.as<int>(),
+                            c->msNode.as<int2>(), c->msHist.as<fm3d::MserHist>(), c->msReg.as<int4>(),
+                            c->msCnt.as<int>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    int cnt[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(cnt, c->msCnt.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (cnt[0] < 0 || cnt[1] < 0 || cnt[0] > L.regCap || cnt[1] > L.regCap)
+        return fail(c, FM3D_ERR_HIP, "MSER: region count out of range");
+    n0 = cnt[0];
+    regs.resize((size_t)cnt[0] + cnt[1]);
+    if (cnt[0])
+        HIPCHK(c, hipMemcpyAsync(regs.data(), c->msReg.p, (size_t)cnt[0] * sizeof(int4), hipMemcpyDeviceToHost, c->stream));
+    if (cnt[1])
+        HIPCHK(c, hipMemcpyAsync(regs.data() + cnt[0], c->msReg.as<int4>() + L.regCap, (size_t)cnt[1] * sizeof(int4),
+                                 hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    off.assign(regs.size() + 1, 0);
+    for (size_t i = 0; i < regs.size(); i++) {
+        if (regs[i].z <= 0 || regs[i].z > (long long)w * h) return fail(c, FM3D_ERR_HIP, "MSER: bad region size");
+        off[i + 1] = off[i] + regs[i].z;
+    }
+    return FM3D_OK;
+}
+
+// the region points (walked from the node lists) and each region's fitEllipse keypoint + kept flag
+int mser_fit(fm3d_ctx* c, const fm3d::MserLayout& L, const std::vector<int4>& regs, int n0,
+             const std::vector<long long>& off) {
+    const int n = (int)regs.size();
+    if (n == 0) return FM3D_OK;
+    const long long tot = off[n];
+    HIPCHK(c, c->msOff.ensure((size_t)(n + 1) * sizeof(long long)));
+    HIPCHK(c, c->msXY.ensure((size_t)tot * sizeof(int2)));
+    HIPCHK(c, c->msScr.ensure((size_t)tot * 5 * sizeof(double)));
+    HIPCHK(c, c->msKp.ensure((size_t)(n + 1) * sizeof(fm3d_keypoint)));
+    HIPCHK(c, c->msFlag.ensure((size_t)(n + 1) * sizeof(int)));
+    HIPCHK(c, hipMemcpyAsync(c->msOff.p, off.data(), (size_t)(n + 1) * sizeof(long long), hipMemcpyHostToDevice,
+                             c->stream));
+    fm3d::launch_mser_fit(c->msReg.as<int4>(), L.regCap, n0, n, c->msNode.as<int2>(), L.nodes,
+                          c->msOff.as<long long>(), L, c->msXY.as<int2>(), c->msScr.as<double>(),
+                          c->msKp.as<fm3d_keypoint>(), c->msFlag.as<int>(), nullptr, c->stream);
+    HIPCHK(c, hipGetLastError());
+    return FM3D_OK;
+}
+
+fm3d::MserParams mser_params(int delta, int minArea, int maxArea, double maxVariation, double minDiversity) {
+    fm3d::MserParams P;
+    P.delta = delta;
+    P.minArea = minArea;
+    P.maxArea = maxArea;
+    P.maxVariation = maxVariation;
+    P.minDiversity = minDiversity;
+    return P;
+}
+
+// MserFeatureDetector::detect: the kept keypoints in region order
+int mser_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserParams& P,
+                std::vector<fm3d_keypoint>& k) {
+    k.clear();
+    fm3d::MserLayout L;
+    std::vector<int4> regs;
+    std::vector<long long> off;
+    int n0 = 0, r;
+    if ((r = mser_flood(c, img, w, h, P, L, regs, n0, off))) return r;
+    const int n = (int)regs.size();
+    for (int i = 0; i < n; i++)
+        if (regs[i].z < 5) return fail(c, FM3D_ERR_INVALID, "MSER: a region under 5 points (fitEllipse throws)");
+    if (n == 0) return FM3D_OK;
+    if ((r = mser_fit(c, L, regs, n0, off))) return r;
+    if ((r = ensure_scan_tmp(c, n))) return r;
+    HIPCHK(c, c->msPos.ensure((size_t)(n + 1) * sizeof(int)));
+    fm3d::launch_exclusive_scan(c->msFlag.as<int>(), n, c->msPos.as<int>(), c->count.as<int>(), c->scanTmp.p, c->stream);
+    HIPCHK(c, hipGetLastError());
+    int nk = 0;
+    HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nk == 0) return FM3D_OK;
+    HIPCHK(c, c->msOut.ensure((size_t)nk * sizeof(fm3d_keypoint)));
+    fm3d::launch_star_scatter(c->msKp.as<fm3d_keypoint>(), c->msFlag.as<int>(), c->msPos.as<int>(), n,
+                              c->msOut.as<fm3d_keypoint>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    k.resize(nk);
+    HIPCHK(c, hipMemcpyAsync(k.data(), c->msOut.p, (size_t)nk * sizeof(fm3d_keypoint), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FM3D_OK;
+}
+
 extern "C" {
+int fm3d_mser_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int delta, int minArea, int maxArea,
+                     double maxVariation, double minDiversity, fm3d_keypoint* kpts, int cap, int* n) {
+    if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    std::vector<fm3d_keypoint> k;
+    int r;
+    if ((r = mser_detect(c, img, w, h, mser_params(delta, minArea, maxArea, maxVariation, minDiversity), k))) return r;
+    for (int i = 0; i < (int)k.size() && i < cap; i++) kpts[i] = k[i];
+    *n = (int)k.size();
+    return FM3D_OK;
+}
+
+int fm3d_mser_regions(fm3d_ctx* c, const uint8_t* img, int w, int h, int delta, int minArea, int maxArea,
+                      double maxVariation, double minDiversity, int32_t* color, int32_t* count, int cap, int32_t* pts,
+                      int64_t ptsCap, int* nRegions, int64_t* nPoints) {
+    if (!c || !img || !nRegions || !nPoints || w <= 0 || h <= 0 || cap < 0 || ptsCap < 0 ||
+        (cap > 0 && (!color || !count)) || (ptsCap > 0 && !pts))
+        return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    fm3d::MserLayout L;
+    std::vector<int4> regs;
+    std::vector<long long> off;
+    int n0 = 0, r;
+    const fm3d::MserParams P = mser_params(delta, minArea, maxArea, maxVariation, minDiversity);
+    if ((r = mser_flood(c, img, w, h, P, L, regs, n0, off))) return r;
+    const int n = (int)regs.size();
+    if ((r = mser_fit(c, L, regs, n0, off))) return r;  // walks the lists into msXY
+    const long long tot = off[n];
+    for (int i = 0; i < n && i < cap; i++) {
+        color[i] = regs[i].x;
+        count[i] = regs[i].z;
+    }
+    const long long m = std::min<long long>(tot, ptsCap);
+    if (m > 0)
+        HIPCHK(c, hipMemcpyAsync(pts, c->msXY.p, (size_t)m * sizeof(int2), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *nRegions = n;
+    *nPoints = tot;
+    return FM3D_OK;
+}
+
 int fm3d_freak_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keypoint* kpts, int n,
                        fm3d_keypoint* kout, int32_t* kept, int* nOut, uint8_t* desc) {
     if (!c || !img || !nOut || w <= 0 || h <= 0 || n < 0 || (n > 0 && (!kpts || !kout || !desc)))
@@ -3417,6 +3564,11 @@ int detect_static(fm3d_ctx* c, const uint8_t* img, int w, int h, std::vector<fm3
     case FM3D_FEAT_STAR:
         return star_detect(c, img, w, h, S.starMaxSize, S.starResponse, S.starLineThreshold, S.starLineBinarized,
                            S.starSuppression, k);
+    case FM3D_FEAT_MSER:
+        return mser_detect(c, img, w, h,
+                           mser_params(S.mserDelta, S.mserMinArea, S.mserMaxArea, S.mserMaxVariation,
+                                       S.mserMinDiversity),
+                           k);
     default:
         return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' detector type has no GPU implementation");
     }

@@ -376,6 +376,35 @@ void launch_freak_desc(const uint8_t* img, const int* sum, int w, const fm3d_key
                        const float4* lut, const int4* opairs, const int2* pairs, float* angle, uint8_t* desc,
                        hipStream_t s);
 
+// ---------------------------------------------------------------- MSER (fm3d_mser.hip)
+struct MserParams {
+    int delta, minArea, maxArea;
+    double maxVariation, minDiversity;
+};
+struct MserHist {  // MSERGrowHistory by index
+    int shortcut, child, stable, val, size;
+};
+// the workspace of one pass over a w x h image (both passes: twice, pass-major)
+struct MserLayout {
+    int w, h, step, stepgap;
+    long long imgInts;   // (h + 2) * step
+    long long heapInts;  // w * h + 256
+    long long nodes;     // w * h: {next node, pixel offset}
+    long long hists;     // 2 w h (a bound: one per raise and per merge)
+    long long regCap;    // region records per pass
+};
+MserLayout mser_layout(int w, int h);
+// both flood passes, one workgroup each (pass 0 on 255 - I, colour -1; pass 1 on I, colour +1):
+// reg[pass * regCap + r] = {colour, head node, point count, 0}; nreg[pass] = regions (all, even past regCap)
+void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, int* work, int* heap, int2* node,
+                       MserHist* hist, int4* reg, int* nreg, hipStream_t s);
+// fitEllipse per region (one lane each): region r of the concatenated list (pass 0's n0 then pass 1's),
+// its points at off[r] in xy (walked from the node list) and 5 * count doubles of scratch at 5 * off[r];
+// kp[r] = KeyPoint(centre, sqrt(w h)), flag[r] = kept (diameter > FLT_EPSILON, rounded centre inside)
+void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const int2* node, long long nodes,
+                     const long long* off, const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag,
+                     float* box, hipStream_t s);
+
 // ---------------------------------------------------------------- BRISK (fm3d_brisk.hip)
 // pat: 60 (x, y, sigma, 0) pattern points per (scale, rotation) in use; pidx: each keypoint's row of pat;
 // pairs: the short pairs (i, j); desc: n x 64 bytes

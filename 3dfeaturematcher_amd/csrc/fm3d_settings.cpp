@@ -161,6 +161,15 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->starSuppression = 5;
     s->briskThreshold = 30;  // cv::BRISK's defaults
     s->briskOctaves = 3;
+    s->mserDelta = 5;  // cv::MSER's defaults
+    s->mserMinArea = 60;
+    s->mserMaxArea = 14400;
+    s->mserMaxVariation = 0.25;
+    s->mserMinDiversity = 0.2;
+    s->mserMaxEvolution = 200;
+    s->mserAreaThreshold = 1.01;
+    s->mserMinMargin = 0.003;
+    s->mserEdgeBlurSize = 5;
     return FM3D_OK;
 }
 
@@ -214,6 +223,7 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
                                   : det == "SIFT" ? FM3D_FEAT_SIFT
                                   : det == "FAST" ? FM3D_FEAT_FAST
                                   : det == "STAR" ? FM3D_FEAT_STAR
+                                  : det == "MSER" ? FM3D_FEAT_MSER
                                                   : FM3D_FEAT_OTHER;
             else  // ADAPTIVE: the FAST / SURF / STAR adjusters
                 s->detectorType = mode != "ADAPTIVE" ? FM3D_FEAT_OTHER
@@ -233,6 +243,15 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
         get_i(kv, "FeatureOptions.StarDetector.LineThreshold", &s->starLineThreshold);
         get_i(kv, "FeatureOptions.StarDetector.LineBinarized", &s->starLineBinarized);
         get_i(kv, "FeatureOptions.StarDetector.Suppression", &s->starSuppression);
+        get_i(kv, "FeatureOptions.MSERDetector.Delta", &s->mserDelta);
+        get_i(kv, "FeatureOptions.MSERDetector.MinArea", &s->mserMinArea);
+        get_i(kv, "FeatureOptions.MSERDetector.MaxArea", &s->mserMaxArea);
+        get_d(kv, "FeatureOptions.MSERDetector.MaxVariation", &s->mserMaxVariation);
+        get_d(kv, "FeatureOptions.MSERDetector.MinDiversity", &s->mserMinDiversity);
+        get_i(kv, "FeatureOptions.MSERDetector.MaxEvolution", &s->mserMaxEvolution);
+        get_d(kv, "FeatureOptions.MSERDetector.AreaThreshold", &s->mserAreaThreshold);
+        get_d(kv, "FeatureOptions.MSERDetector.MinMargin", &s->mserMinMargin);
+        get_i(kv, "FeatureOptions.MSERDetector.EdgeBlurSize", &s->mserEdgeBlurSize);
         get_i(kv, "FeatureOptions.Adaptive.MinFeatures", &s->adaptiveMinFeatures);
         get_i(kv, "FeatureOptions.Adaptive.MaxFeatures", &s->adaptiveMaxFeatures);
         get_i(kv, "FeatureOptions.Adaptive.MaxIters", &s->adaptiveMaxIters);

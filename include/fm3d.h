@@ -105,6 +105,15 @@ typedef struct fm3d_settings {
     /* FeatureOptions.BriskDetector.Threshold / Octaves (:345-347, build/settings.yml:46-48): cv::BRISK's
        detection parameters, which its descriptor does not use (OpenCV defaults 30 / 3) */
     int briskThreshold, briskOctaves;
+    /* FeatureOptions.MSERDetector.Delta / MinArea / MaxArea / MaxVariation / MinDiversity / MaxEvolution /
+       AreaThreshold / MinMargin / EdgeBlurSize (:258-272, cv::MSER's nine arguments; OpenCV's defaults
+       5 / 60 / 14400 / 0.25 / 0.2 / 200 / 1.01 / 0.003 / 5).  On grey images only the first five
+       steer the result (the last four drive OpenCV's colour-image MSCR). */
+    int mserDelta, mserMinArea, mserMaxArea;
+    double mserMaxVariation, mserMinDiversity;
+    int mserMaxEvolution;
+    double mserAreaThreshold, mserMinMargin;
+    int mserEdgeBlurSize;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
@@ -114,6 +123,7 @@ typedef struct fm3d_settings {
 #define FM3D_FEAT_STAR 4
 #define FM3D_FEAT_BRISK 5 /* extractor only: the reference's generateDetector has no BRISK branch */
 #define FM3D_FEAT_FREAK 6 /* extractor only (cv::FREAK(), descriptorsmatcher.cpp:350-353) */
+#define FM3D_FEAT_MSER 7  /* detector only (cv::MserFeatureDetector, descriptorsmatcher.cpp:258-272) */
 #define FM3D_FEAT_OTHER (-1)
 
 /* cv::DMatch layout */
@@ -395,10 +405,25 @@ int fm3d_star_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, i
    the signed pattern size (0 in the border), w*h each; *border the pattern border. */
 int fm3d_star_responses(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int maxSize, float *resp,
                         int16_t *sizes, int *border);
+/* cv::MserFeatureDetector(delta, minArea, maxArea, maxVariation, minDiversity, ...).detect
+   (descriptorsmatcher.cpp:258-272; OpenCV 2.4.9 mser.cpp on a grey image): per maximally stable region
+   (pass 1 on 255 - I, then pass 2 on I, each in the flood's order) KeyPoint(centre, sqrt(w * h)) of its
+   fitEllipse, kept when the diameter exceeds FLT_EPSILON and the rounded centre is inside the image
+   (angle -1, response 0).  FM3D_ERR_INVALID where OpenCV throws (a region under 5 points, MinArea < 4).
+   Each flood pass is sequential by construction (its order is part of the output) and runs as one GPU
+   lane; fitEllipse runs one lane per region. */
+int fm3d_mser_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int delta, int minArea, int maxArea,
+                     double maxVariation, double minDiversity, fm3d_keypoint *kpts, int cap, int *n);
+/* MSER::operator()(img, msers): *nRegions regions, color[i] -1 (pass 1) or +1, count[i] points, the
+   points (x, y) concatenated in pts in each region's list order (MSERToContour); *nPoints = all points.
+   min(regions, cap) and min(points, ptsCap) written. */
+int fm3d_mser_regions(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int delta, int minArea, int maxArea,
+                      double maxVariation, double minDiversity, int32_t *color, int32_t *count, int cap, int32_t *pts,
+                      int64_t ptsCap, int *nRegions, int64_t *nPoints);
 /* feature_detector_->detect(img, kpts) of generateDetector (descriptorsmatcher.cpp:110-111, 176-293):
-   STATIC SURF / ORB / SIFT / FAST, or ADAPTIVE with the FAST or SURF adjuster (the threshold walk of
-   DynamicAdaptedFeatureDetector).  *n = all; min(*n, cap) written.  FM3D_ERR_UNSUPPORTED for the
-   detector types without a GPU implementation (STAR, MSER, the STAR adjuster). */
+   STATIC SURF / ORB / SIFT / FAST / STAR / MSER, or ADAPTIVE with the FAST, SURF or STAR adjuster (the
+   threshold walk of DynamicAdaptedFeatureDetector).  *n = all; min(*n, cap) written.
+   FM3D_ERR_UNSUPPORTED for a type the reference does not build (FM3D_FEAT_OTHER). */
 int fm3d_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, fm3d_keypoint *kpts, int cap, int *n);
 /* the row layout of the settings' extractor: SURF 64 | 128 and SIFT 128 (FM3D_DESC_F32), ORB 32 bytes,
    BRISK and FREAK 64 bytes (FM3D_DESC_BITS). */

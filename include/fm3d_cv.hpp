@@ -29,9 +29,9 @@
  * What differs, and why:
  *   - feature detection/description (descriptorsmatcher.cpp:110-115): when main.cpp:94 passes
  *     empty vectors, the settings' detector / extractor runs on the GPU (SURF of
- *     build/settings.yml, fm3d_surf_detect; ORB, SIFT, FAST, STAR, ADAPTIVE and the BRISK
- *     extractor too, any pair of them, see fm3d.h); a type without a GPU implementation (MSER,
- *     FREAK) falls back to the image's feature side files:
+ *     build/settings.yml, fm3d_surf_detect; ORB, SIFT, FAST, STAR, MSER, ADAPTIVE and the BRISK
+ *     and FREAK extractors too, any pair of them, see fm3d.h); a type the reference does not build
+ *     (FM3D_FEAT_OTHER) falls back to the image's feature side files:
  *     <image>.kpts.f32 (N x 2 float32 positions) and <image>.desc.u8 (N x 128 uint8) or
  *     <image>.desc.f32 (N x 128 float32) -- FeatureOptions.ExtractorType ORB / BRISK / FREAK
  *     selects Hamming matching on <image>.desc.u8 rows of 32 / 64 bytes (descriptorsmatcher.cpp:64-71);
@@ -503,9 +503,9 @@ public:
     }
 
 private:
-    // the detector + extractor (:110-115): the settings' pair on the GPU (SURF, ORB, SIFT, FAST, STAR,
-    // ADAPTIVE, the BRISK extractor, mixed pairs); a type with no GPU implementation (MSER, FREAK) takes its output
-    // from the images' side files
+    // the detector + extractor (:110-115): the settings' pair on the GPU (SURF, ORB, SIFT, FAST, STAR, MSER,
+    // ADAPTIVE, the BRISK and FREAK extractors, mixed pairs); a type the reference does not build takes its
+    // output from the images' side files
     // (<image>.kpts.f32 and <image>.desc.u8 / .desc.f32), or from the caller's keypoints + descriptors
     void features(const cv::Mat& img, std::vector<cv::KeyPoint>& kpts, cv::Mat& d) {
         if (s_.detectorType == FM3D_FEAT_SURF && s_.extractorType == FM3D_FEAT_SURF) {

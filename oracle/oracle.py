@@ -924,3 +924,62 @@ def freak_compute(img, kpts, pairs=None):
     m = lib().orc_freak_compute(_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), _kp(kin), ctypes.c_int(n),
                                 pp, _kp(kout), _p(kept, ctypes.c_int), _p(desc, ctypes.c_uint8))
     return kout[:m], kept[:m], desc[:m]
+
+
+# ---------------------------------------------------------------- MSER (orc_mser.c)
+MSER_DEFAULTS = dict(delta=5, min_area=60, max_area=14400, max_variation=0.25, min_diversity=0.2)
+
+
+def _mser_args(img, delta, min_area, max_area, max_variation, min_diversity):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    return img, (_p(img, ctypes.c_uint8), ctypes.c_int(w), ctypes.c_int(h), ctypes.c_int(delta), ctypes.c_int(min_area),
+                 ctypes.c_int(max_area), ctypes.c_double(max_variation), ctypes.c_double(min_diversity))
+
+
+def mser_regions(img, delta=5, min_area=60, max_area=14400, max_variation=0.25, min_diversity=0.2):
+    """MSER::operator()(img, msers): [(colour -1 | +1, (k, 2) int32 points (x, y) in region-list order)]"""
+    img, a = _mser_args(img, delta, min_area, max_area, max_variation, min_diversity)
+    npts = ctypes.c_longlong(0)
+    n = lib().orc_mser_regions(*a, None, None, ctypes.c_int(0), None, ctypes.c_longlong(0), ctypes.byref(npts))
+    if n < 0:
+        raise ValueError("MSER: bad input")
+    color = np.zeros(max(n, 1), np.int32)
+    count = np.zeros(max(n, 1), np.int32)
+    pts = np.zeros((max(npts.value, 1), 2), np.int32)
+    lib().orc_mser_regions(*a, _p(color, ctypes.c_int), _p(count, ctypes.c_int), ctypes.c_int(n), _p(pts, ctypes.c_int),
+                           ctypes.c_longlong(npts.value), ctypes.byref(npts))
+    out, off = [], 0
+    for i in range(n):
+        out.append((int(color[i]), pts[off:off + count[i]].copy()))
+        off += int(count[i])
+    return out
+
+
+def fit_ellipse(points):
+    """cvFitEllipse2 on integer points: (cx, cy, width, height, angle) float32"""
+    p = np.ascontiguousarray(points, dtype=np.int32).reshape(-1, 2)
+    box = np.zeros(5, np.float32)
+    if lib().orc_fit_ellipse(_p(p, ctypes.c_int), ctypes.c_int(len(p)), _p(box, ctypes.c_float)) < 0:
+        raise ValueError("fitEllipse: fewer than 5 points")
+    return box
+
+
+def mser_detect(img, delta=5, min_area=60, max_area=14400, max_variation=0.25, min_diversity=0.2):
+    """MserFeatureDetector(...).detect(img): KEYPOINT records in region order"""
+    img, a = _mser_args(img, delta, min_area, max_area, max_variation, min_diversity)
+    n = lib().orc_mser_detect(*a, None, ctypes.c_int(0))
+    if n < 0:
+        raise ValueError("MSER: a region below 5 points (fitEllipse throws) or bad input")
+    out = np.zeros(max(n, 1), dtype=KEYPOINT)
+    lib().orc_mser_detect(*a, _kp(out), ctypes.c_int(n))
+    return out[:n]
+
+
+def fit_ellipse_solves(points):
+    """cvFitEllipse2's solves: (cx, cy, conic A..E (5), centre (2), re-fit A..C (3)) float64"""
+    p = np.ascontiguousarray(points, dtype=np.int32).reshape(-1, 2)
+    sol = np.zeros(12, np.float64)
+    if lib().orc_fit_ellipse_solves(_p(p, ctypes.c_int), ctypes.c_int(len(p)), _p(sol)) < 0:
+        raise ValueError("fitEllipse: fewer than 5 points")
+    return sol

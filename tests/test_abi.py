@@ -188,7 +188,16 @@ def test_settings_feature_options(fm3d, tmp_path):
     assert (fm3d.Settings.default().briskThreshold, fm3d.Settings.default().briskOctaves) == (30, 3)
     assert load("FeatureOptions:\n   DetectorType: BRISK\n").detectorType == fm3d.FEAT_OTHER  # no BRISK detector
     assert load("FeatureOptions:\n   ExtractorType: FREAK\n").extractorType == fm3d.FEAT_FREAK
-    for mode, det in (("ADAPTIVE", "ORB"), ("STATIC", "MSER"), ("OTHER", "SURF")):
+    assert load("FeatureOptions:\n   DetectorMode: STATIC\n   DetectorType: MSER\n").detectorType == fm3d.FEAT_MSER
+    s = load("FeatureOptions:\n   DetectorType: MSER\n   MSERDetector:\n      Delta: 3\n      MinArea: 30\n"
+             "      MaxArea: 5000\n      MaxVariation: 0.4\n      MinDiversity: 0.1\n      MaxEvolution: 100\n"
+             "      AreaThreshold: 1.2\n      MinMargin: 0.01\n      EdgeBlurSize: 3\n")
+    assert (s.mserDelta, s.mserMinArea, s.mserMaxArea, s.mserMaxVariation, s.mserMinDiversity, s.mserMaxEvolution,
+            s.mserAreaThreshold, s.mserMinMargin, s.mserEdgeBlurSize) == (3, 30, 5000, 0.4, 0.1, 100, 1.2, 0.01, 3)
+    d = fm3d.Settings.default()  # cv::MSER's defaults
+    assert (d.mserDelta, d.mserMinArea, d.mserMaxArea, d.mserMaxVariation, d.mserMinDiversity, d.mserMaxEvolution,
+            d.mserAreaThreshold, d.mserMinMargin, d.mserEdgeBlurSize) == (5, 60, 14400, 0.25, 0.2, 200, 1.01, 0.003, 5)
+    for mode, det in (("ADAPTIVE", "ORB"), ("ADAPTIVE", "MSER"), ("STATIC", "GFTT"), ("OTHER", "SURF")):
         s = load(f"FeatureOptions:\n   DetectorMode: {mode}\n   DetectorType: {det}\n")
         assert s.detectorType == fm3d.FEAT_OTHER, (mode, det)
     d = fm3d.Settings.default()

@@ -216,8 +216,8 @@ def test_dropin_main_matches_python_api(fm3d, synth, orc, tmp_path):
     pair.desc2.tofile(d / "img2.pgm.desc.u8")
     yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.55)
     yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
-    # a detector type with no GPU implementation (MSER): the side files are read
-    yml += "FeatureOptions:\n   DetectorType: MSER\n   ExtractorType: SIFT\n"
+    # a detector type the reference does not build (GFTT): the side files are read
+    yml += "FeatureOptions:\n   DetectorType: GFTT\n   ExtractorType: SIFT\n"
     (d / "settings.yml").write_text(yml)
     r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d)
     assert r.returncode == 0, r.stderr + r.stdout
