@@ -43,7 +43,7 @@ EXPORTS = (
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
     "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link", "fm3d_freak_compute", "fm3d_freak_set_pairs",
-    "fm3d_mser_detect", "fm3d_mser_regions",
+    "fm3d_mser_detect", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt", "fm3d_pipeline_wait_dlt",
 )
 
 
@@ -898,6 +898,17 @@ class Pipeline:
         n = ctypes.c_int(0)
         st = PipelineStats()
         self.ctx.check(lib().fm3d_pipeline_run_dlt(self.ctx.handle, ctypes.byref(n), ctypes.byref(st)))
+        return n.value, st.as_dict()
+
+    def submit_dlt(self) -> None:
+        """fm3d_pipeline_submit_dlt: C2's path queued on the context stream (returns at once)"""
+        self.ctx.check(lib().fm3d_pipeline_submit_dlt(self.ctx.handle))
+
+    def wait_dlt(self):
+        """fm3d_pipeline_wait_dlt: (n_inliers, stats dict) of the submitted front half"""
+        n = ctypes.c_int(0)
+        st = PipelineStats()
+        self.ctx.check(lib().fm3d_pipeline_wait_dlt(self.ctx.handle, ctypes.byref(n), ctypes.byref(st)))
         return n.value, st.as_dict()
 
     def run_ncc(self, hphi: int = 4, htheta: int = 4, span: float = 0.4):

@@ -152,6 +152,7 @@ struct fm3d_ctx {
     hipEvent_t evFront = nullptr;    // (member) after its front half
     hipEvent_t evLm = nullptr;       // (leader) after a joint LM launch
     fm3d_lm_stats subLm{};         // the pending submit's LM launch data
+    bool pendingDlt = false;       // the pending submit is fm3d_pipeline_submit_dlt's front half
     fm3d_record* pendOut = nullptr;  // the device records of the pending / last run
     // staged pipeline inputs
     int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
@@ -2192,6 +2193,7 @@ int fm3d_pipeline_link(fm3d_ctx* member, fm3d_ctx* leader) {
 int fm3d_pipeline_wait(fm3d_ctx* c, fm3d_record* out, int cap, int* nKept, fm3d_pipeline_stats* stats) {
     if (!c) return FM3D_ERR_INVALID;
     if (!c->pending) return fail(c, FM3D_ERR_INVALID, "no frame pair submitted (fm3d_pipeline_submit)");
+    if (c->pendingDlt) return fail(c, FM3D_ERR_INVALID, "a front half is pending: fm3d_pipeline_wait_dlt");
     hipSetDevice(c->device);
     int r;
     if ((r = flush_member(c))) return r;
@@ -2248,18 +2250,30 @@ int fm3d_internal_prepare(fm3d_ctx* c) {  // the device count buffer, before a c
 
 extern "C" {
 
-int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats) {
+int fm3d_pipeline_submit_dlt(fm3d_ctx* c) {
     if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
     PENDING_CHECK(c);
     hipSetDevice(c->device);
-    hipEvent_t* ev = c->ev;
     int r;
     if ((r = pipeline_front(c))) return r;
     HIPCHK(c, c->hSmall.ensure(sizeof(PipeSmall)));
     PipeSmall* hs = c->hSmall.as<PipeSmall>();
     HIPCHK(c, hipMemcpyAsync(hs->cnt, c->pcnt.p, sizeof(hs->cnt), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipEventRecord(ev[1], c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    c->pending = true;
+    c->pendingDlt = true;
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_wait_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats) {
+    if (!c) return FM3D_ERR_INVALID;
+    if (!c->pendingDlt) return fail(c, FM3D_ERR_INVALID, "no front half submitted (fm3d_pipeline_submit_dlt)");
+    hipSetDevice(c->device);
+    hipEvent_t* ev = c->ev;
+    c->pending = false;
+    c->pendingDlt = false;
+    HIPCHK(c, hipEventSynchronize(ev[1]));
+    const PipeSmall* hs = c->hSmall.as<PipeSmall>();
     const int K = hs->cnt[0], P = hs->cnt[1];
     c->stK = K;
     c->stP = P;
@@ -2281,6 +2295,12 @@ int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats
         stats->total_ms = ms;
     }
     return FM3D_OK;
+}
+
+int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats) {
+    int r;
+    if ((r = fm3d_pipeline_submit_dlt(c))) return r;
+    return fm3d_pipeline_wait_dlt(c, nInliers, stats);
 }
 
 int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* nPoints, fm3d_pipeline_stats* stats) {

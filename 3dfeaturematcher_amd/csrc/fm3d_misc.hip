@@ -272,6 +272,57 @@ __global__ void offsets_kernel(const int* __restrict__ flag, int n, const int* _
     }
 }
 
+// up to kSmallCompact items: one workgroup walks them in chunks of 4096 (4 per thread: a wave
+// prefix by shuffles, the 16 wave sums through LDS), carrying the running count -- one launch
+// instead of three; with offsets the per-item exclusive offsets are written, with out the flagged
+// items (and srcIndex) scattered in order.  count: the total.
+constexpr int kSmallCompact = 16384;
+
+template <typename T>
+__global__ __launch_bounds__(1024) void compact_small_kernel(const T* __restrict__ in, const int* __restrict__ flag,
+                                                             int n, const int* __restrict__ nDev, T* __restrict__ out,
+                                                             int* __restrict__ count, int* __restrict__ srcIndex,
+                                                             int* __restrict__ offsets) {
+    __shared__ int wsum[16];
+    n = dev_count(nDev, n);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int carry = 0;
+    for (int base = 0; base < n; base += 4096) {
+        int f[4], c4 = 0;
+        for (int k = 0; k < 4; k++) {
+            const int i = base + tid * 4 + k;
+            f[k] = (i < n && flag[i]) ? 1 : 0;
+            c4 += f[k];
+        }
+        int x = c4;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        int wbase = 0, tot = 0;
+        for (int w = 0; w < 16; w++) {
+            const int v = wsum[w];
+            wbase += w < wid ? v : 0;
+            tot += v;
+        }
+        int o = carry + wbase + x - c4;
+        for (int k = 0; k < 4; k++) {
+            const int i = base + tid * 4 + k;
+            if (offsets && i < n) offsets[i] = o;
+            if (out && f[k]) {
+                out[o] = in[i];
+                if (srcIndex) srcIndex[o] = i;
+            }
+            o += f[k];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0 && count) *count = carry;
+}
+
 template <typename T>
 void compact(const T* in, const int* flag, int n, const int* nDev, T* out, int* count, int* srcIndex, void* tmp,
              hipStream_t s) {
@@ -279,6 +330,10 @@ void compact(const T* in, const int* flag, int n, const int* nDev, T* out, int* 
     int* blockSums = (int*)tmp;
     if (n <= 0) {
         hipMemsetAsync(count, 0, sizeof(int), s);
+        return;
+    }
+    if (n <= kSmallCompact) {
+        compact_small_kernel<T><<<1, 1024, 0, s>>>(in, flag, n, nDev, out, count, srcIndex, nullptr);
         return;
     }
     scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, nDev, blockSums);
@@ -345,6 +400,10 @@ void launch_exclusive_scan(const int* flag, int n, int* offsets, int* total, voi
     int* blockSums = (int*)tmp;
     if (n <= 0) {
         hipMemsetAsync(total, 0, sizeof(int), s);
+        return;
+    }
+    if (n <= kSmallCompact) {
+        compact_small_kernel<int><<<1, 1024, 0, s>>>(nullptr, flag, n, nullptr, nullptr, total, nullptr, offsets);
         return;
     }
     scan_count_kernel<<<nb, 256, 0, s>>>(flag, n, nullptr, blockSums);

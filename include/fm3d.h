@@ -468,6 +468,12 @@ int fm3d_pipeline_link(fm3d_ctx *member, fm3d_ctx *leader);
    the staged inputs, no normals; *nInliers = the triangulated points kept by the z filter (stats:
    match / NNDR-compaction / triangulate / total HIP-event times). */
 int fm3d_pipeline_run_dlt(fm3d_ctx *ctx, int *nInliers, fm3d_pipeline_stats *stats);
+/* fm3d_pipeline_run_dlt as submit / wait (a serving loop keeps two contexts in flight): submit queues the
+   staged pair's front half (match -> NNDR -> compaction -> DLT -> compaction) on the context stream with
+   its counts copied to page-locked memory and returns; wait blocks on that copy and reports as
+   fm3d_pipeline_run_dlt.  Until the wait the other pipeline calls on the context fail. */
+int fm3d_pipeline_submit_dlt(fm3d_ctx *ctx);
+int fm3d_pipeline_wait_dlt(fm3d_ctx *ctx, int *nInliers, fm3d_pipeline_stats *stats);
 /* after fm3d_pipeline_run(_dlt): the compacted matches (K), the inlier points (P x 3 doubles, the
    z-filtered triangulation in match order) and each point's match index (P); any may be NULL */
 int fm3d_pipeline_dlt_download(fm3d_ctx *ctx, fm3d_dmatch *matches, double *points, int32_t *matchIdx);

@@ -9,7 +9,8 @@ from conftest import oracle_threads
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,seed", [(10_000, 7), (2_500, 3)])
+# 2,500 and 10,000 queries: the one-workgroup compaction; 20,000: the three-kernel one
+@pytest.mark.parametrize("n,seed", [(10_000, 7), (2_500, 3), (20_000, 5)])
 def test_pipeline_dlt_bitwise(fm3d, orc, synth, n, seed):
     pair = synth.make_frame_pair(n, seed=seed)
     s = fm3d.Settings.default()
@@ -37,6 +38,43 @@ def test_pipeline_dlt_bitwise(fm3d, orc, synth, n, seed):
     assert np.array_equal(pts, opts) and np.array_equal(src, np.flatnonzero(mask))
     assert P2 == P and np.array_equal(pts2, pts)
     assert np.array_equal(m3, m) and np.array_equal(pts3, pts) and np.array_equal(src3, src) and kept <= P
+
+
+def test_pipeline_submit_wait_dlt_two_in_flight(fm3d, orc, synth):
+    """fm3d_pipeline_submit_dlt / wait_dlt on two contexts in flight (the C2 serving loop) equal
+    fm3d_pipeline_run_dlt; a pending front half blocks the other pipeline calls"""
+    pair = synth.make_frame_pair(6000, seed=11)
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon = 0.55
+    ctxs = [fm3d.Context(s) for _ in range(2)]
+    try:
+        pipes = []
+        for c in ctxs:
+            fm3d.SingleCameraTriangulator(c).set_g12(pair.g12)
+            p = fm3d.Pipeline(c)
+            p.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+            pipes.append(p)
+        P0, st0 = pipes[0].run_dlt()
+        ref = pipes[0].dlt_results(st0["matches"], st0["inliers"])
+        for _ in range(3):
+            pipes[0].submit_dlt()
+            pipes[1].submit_dlt()
+            with pytest.raises(fm3d.Fm3dError):
+                pipes[0].run_dlt()
+            with pytest.raises(fm3d.Fm3dError):
+                pipes[1].submit_dlt()
+            for p in pipes:
+                P, st = p.wait_dlt()
+                got = p.dlt_results(st["matches"], st["inliers"])
+                assert P == P0 and st["matches"] == st0["matches"]
+                for a, b in zip(got, ref):
+                    assert np.array_equal(a, b)
+        with pytest.raises(fm3d.Fm3dError):
+            pipes[0].wait_dlt()  # nothing pending
+    finally:
+        for c in ctxs:
+            c.close()
 
 
 def test_pipeline_ncc_bitwise(fm3d, orc, synth):
