@@ -272,10 +272,11 @@ __global__ void offsets_kernel(const int* __restrict__ flag, int n, const int* _
     }
 }
 
-// up to kSmallCompact items: one workgroup walks them in chunks of 4096 (4 per thread: a wave
-// prefix by shuffles, the 16 wave sums through LDS), carrying the running count -- one launch
-// instead of three; with offsets the per-item exclusive offsets are written, with out the flagged
-// items (and srcIndex) scattered in order.  count: the total.
+// up to kSmallCompact items: one workgroup of 1024 threads, item i = 1024 * it + thread (coalesced,
+// every flag loaded at once), the (iteration, wave) counts by ballots, their exclusive scan over 256
+// entries in (iteration, wave) order by the first four waves -- one launch instead of three.  With
+// offsets the per-item exclusive offsets are written, with out the flagged items (and srcIndex)
+// scattered in order.  count: the total.
 constexpr int kSmallCompact = 16384;
 
 template <typename T>
@@ -283,44 +284,58 @@ __global__ __launch_bounds__(1024) void compact_small_kernel(const T* __restrict
                                                              int n, const int* __restrict__ nDev, T* __restrict__ out,
                                                              int* __restrict__ count, int* __restrict__ srcIndex,
                                                              int* __restrict__ offsets) {
-    __shared__ int wsum[16];
+    __shared__ int wt[256];
+    __shared__ int ws4[4];
+    __shared__ int totS;
     n = dev_count(nDev, n);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    int carry = 0;
-    for (int base = 0; base < n; base += 4096) {
-        int f[4], c4 = 0;
-        for (int k = 0; k < 4; k++) {
-            const int i = base + tid * 4 + k;
-            f[k] = (i < n && flag[i]) ? 1 : 0;
-            c4 += f[k];
-        }
-        int x = c4;
+    const int ipt = (n + 1023) >> 10;  // iterations, <= 16
+    bool f[16];
+#pragma unroll
+    for (int it = 0; it < 16; it++) {
+        const int i = it * 1024 + tid;
+        f[it] = it < ipt && i < n && flag[i] != 0;
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int pre[16];
+#pragma unroll
+    for (int it = 0; it < 16; it++) {
+        const unsigned long long b = __ballot(f[it]);
+        pre[it] = __popcll(b & below);
+        if (lane == 0) wt[it * 16 + wid] = __popcll(b);
+    }
+    __syncthreads();
+    int v = 0, x = 0;
+    if (tid < 256) {
+        v = wt[tid];
+        x = v;
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(x, o);
             if (lane >= o) x += y;
         }
-        if (lane == 63) wsum[wid] = x;
-        __syncthreads();
-        int wbase = 0, tot = 0;
-        for (int w = 0; w < 16; w++) {
-            const int v = wsum[w];
-            wbase += w < wid ? v : 0;
-            tot += v;
-        }
-        int o = carry + wbase + x - c4;
-        for (int k = 0; k < 4; k++) {
-            const int i = base + tid * 4 + k;
-            if (offsets && i < n) offsets[i] = o;
-            if (out && f[k]) {
-                out[o] = in[i];
+        if (lane == 63) ws4[wid] = x;
+    }
+    __syncthreads();
+    if (tid < 256) {
+        int add = 0;
+        for (int w = 0; w < wid; w++) add += ws4[w];
+        wt[tid] = add + x - v;  // exclusive
+        if (tid == 255) totS = add + x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 16; it++) {
+        const int i = it * 1024 + tid;
+        if (it < ipt && i < n) {
+            const int o = wt[it * 16 + wid] + pre[it];
+            if (offsets) offsets[i] = o;
+            if (f[it]) {
+                if (out) out[o] = in[i];
                 if (srcIndex) srcIndex[o] = i;
             }
-            o += f[k];
         }
-        carry += tot;
-        __syncthreads();
     }
-    if (tid == 0 && count) *count = carry;
+    if (tid == 0 && count) *count = totS;
 }
 
 template <typename T>
