@@ -55,6 +55,15 @@ WORKLOADS = {"c4": dict(keypoints=100_000, width=640, height=480),
 INT8_PEAK_TOPS = 5000.0      # MI355X dense int8 MFMA (2x the ~2.5 PFLOP/s dense bf16; MI355X_MICROARCH.md)
 
 
+WORKLOAD_DEFAULTS = {
+    "c4": {"ray": 64, "nndr": 0.55, "seed": 7},
+    "c5": {"ray": 64, "nndr": 0.55, "seed": 7},
+    "c2": {"ray": 64, "nndr": 0.55, "seed": 7},
+    # C3's ORB rows: the 0.8 ratio and the 64 x 64 neighbourhood of BASELINE's wording
+    "c3": {"ray": 32, "nndr": 0.8, "seed": 102},
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -68,13 +77,14 @@ def parse():
     ap.add_argument("--keypoints", type=int, default=0)
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
-    ap.add_argument("--ray", type=int, default=64)
+    # None: the workload's own value (C2 / C4 / C5: pixelsRay 64, NNDR 0.55, seed 7; C3: 32, 0.8, 102)
+    ap.add_argument("--ray", type=int, default=None)
     ap.add_argument("--levels", type=int, default=3)
-    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--desc", choices=("sift", "orb"), default="sift",
                     help="descriptor kind of the synthetic pair (orb: 256-bit, Hamming; BASELINE C3 with "
                          "--keypoints 10000 --seed 102 --nndr 0.8 --ray 32|64)")
-    ap.add_argument("--nndr", type=float, default=0.55)
+    ap.add_argument("--nndr", type=float, default=None)
     ap.add_argument("--lm-waves", type=int, default=0)
     ap.add_argument("--mode", choices=("stream", "resident"), default="stream",
                     help="stream (C4 headline): every step a frame pair from host memory to host memory, "
@@ -107,6 +117,9 @@ def main():
         workload = "c5" if (world > 1 or args.gpus > 1 or args.mgpu) and not args.weak else "c4"
     if args.weak:
         workload = "c4"
+    for k, v in WORKLOAD_DEFAULTS.get(workload, WORKLOAD_DEFAULTS["c4"]).items():
+        if getattr(args, k) is None:  # only what the command line left open
+            setattr(args, k, v)
     if world == 1 and (args.gpus > 1 or args.mgpu):
         # the driver's `bench.py --gpus N` without a torchrun environment: this one process drives
         # N GPUs through the C ABI's multi-GPU host (fm3d_mgpu)
@@ -732,9 +745,8 @@ def run_c3(args):
     for k in ("keypoints", "width", "height"):
         if getattr(args, k):
             wl[k] = getattr(args, k)
-    nndr = 0.8 if args.nndr == 0.55 else args.nndr  # C3's ORB rows: the 0.8 ratio (0.55 is C4's SIFT)
-    ray = 32 if args.ray == 64 else args.ray
-    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=102, desc="orb")
+    nndr, ray = args.nndr, args.ray  # C3's own defaults (WORKLOAD_DEFAULTS) unless given
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=args.seed, desc="orb")
     s = fm3d.Settings.default()
     s.set_camera(pair.cam)
     s.nndrEpsilon = nndr

@@ -418,20 +418,56 @@ private:
 namespace fm3d {
 namespace cvshim {
 
-// one GPU context per process, shared by the reference classes (the reference's classes share
-// state through the SingleCameraTriangulator pointer and the images they are given)
-inline fm3d::compat::Device& device(const fm3d_settings& s) {
-    static std::unique_ptr<fm3d::compat::Device> dev;
-    if (!dev) dev.reset(new fm3d::compat::Device(s, 0));
-    return *dev;
-}
-
 template <class T>
 inline std::vector<T> read_side(const std::string& path, bool& ok) {
     std::vector<char> b = cv::detail::slurp(path, ok);
     std::vector<T> v(ok ? b.size() / sizeof(T) : 0);
     if (!v.empty()) std::memcpy(v.data(), b.data(), v.size() * sizeof(T));
     return v;
+}
+
+// OpenCV's data tables that the library cannot ship: ORB's bit_pattern_31_ (orb.cpp) and FREAK's
+// DEF_PAIRS (freak.cpp).  FM3D_ORB_PATTERN names a raw file of 512 (x, y) int32 test points,
+// FM3D_FREAK_PAIRS one of 512 int32 pair indices; without them the drop-in's ORB at patchSize 31
+// runs on makeRandomPattern(31) and FREAK on the library's restated table, and one warning per
+// process says so (the descriptors then differ from OpenCV's).
+inline void load_tables(fm3d_ctx* c, const fm3d_settings& s) {
+    bool ok = false;
+    if (const char* p = std::getenv("FM3D_ORB_PATTERN")) {
+        std::vector<int32_t> v = read_side<int32_t>(p, ok);
+        ok = ok && v.size() == 1024;
+        if (ok)
+            fm3d::compat::check(c, fm3d_orb_set_pattern(c, v.data(), 512));
+        else
+            std::fprintf(stderr, "fm3d: FM3D_ORB_PATTERN=%s is not 512 int32 (x, y) points: ignored\n", p);
+    }
+    if (!ok && s.orbPatchSize == 31 && (s.detectorType == FM3D_FEAT_ORB || s.extractorType == FM3D_FEAT_ORB))
+        std::fprintf(stderr, "fm3d: ORB runs on makeRandomPattern(31), not OpenCV's bit_pattern_31_: its descriptors "
+                             "differ from OpenCV's (FM3D_ORB_PATTERN: a file of the table's 512 int32 (x, y) "
+                             "points)\n");
+    ok = false;
+    if (const char* p = std::getenv("FM3D_FREAK_PAIRS")) {
+        std::vector<int32_t> v = read_side<int32_t>(p, ok);
+        ok = ok && v.size() == 512;
+        if (ok)
+            fm3d::compat::check(c, fm3d_freak_set_pairs(c, v.data(), 512));
+        else
+            std::fprintf(stderr, "fm3d: FM3D_FREAK_PAIRS=%s is not 512 int32 pair indices: ignored\n", p);
+    }
+    if (!ok && s.extractorType == FM3D_FEAT_FREAK)
+        std::fprintf(stderr, "fm3d: FREAK runs on the library's restated DEF_PAIRS table, unverified against "
+                             "OpenCV's (FM3D_FREAK_PAIRS: a file of OpenCV's 512 int32 pair indices)\n");
+}
+
+// one GPU context per process, shared by the reference classes (the reference's classes share
+// state through the SingleCameraTriangulator pointer and the images they are given)
+inline fm3d::compat::Device& device(const fm3d_settings& s) {
+    static std::unique_ptr<fm3d::compat::Device> dev;
+    if (!dev) {
+        dev.reset(new fm3d::compat::Device(s, 0));
+        load_tables(dev->ctx(), s);
+    }
+    return *dev;
 }
 
 inline std::string upper(std::string s) {

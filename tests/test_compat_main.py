@@ -452,6 +452,45 @@ def test_dropin_main_binary_extractors(fm3d, synth, orc, tmp_path, det, ex):
 
 
 @pytest.mark.gpu
+def test_dropin_main_orb_pattern_from_env(fm3d, synth, orc, tmp_path):
+    """the drop-in takes OpenCV's tables from FM3D_ORB_PATTERN / FM3D_FREAK_PAIRS; without
+    them ORB at patchSize 31 warns once that it runs on makeRandomPattern(31).  With a table given the
+    patch descriptors are the ORB oracle's on that table, and nothing is printed."""
+    pair = synth.make_frame_pair(1500, seed=28)
+    d = tmp_path
+    write_pgm(d / "img1.pgm", pair.img1)
+    write_pgm(d / "img2.pgm", pair.img2)
+    yml = settings_yml(pair.cam, synth.REF_POS1, synth.REF_POS2, 10, 2, 0.8)
+    yml = yml.replace("img1: img1.pgm", f"img1: {d / 'img1.pgm'}").replace("img2: img2.pgm", f"img2: {d / 'img2.pgm'}")
+    yml += "FeatureOptions:\n   DetectorType: ORB\n   DetectorMode: STATIC\n   ExtractorType: ORB\n"
+    (d / "settings.yml").write_text(yml)
+    env = {k: v for k, v in os.environ.items() if k not in ("FM3D_ORB_PATTERN", "FM3D_FREAK_PAIRS")}
+    r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d,
+                       env=env)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert r.stderr.count("makeRandomPattern(31)") == 1
+    # another valid 512-point table: the default one with its tests reversed
+    pat = np.ascontiguousarray(orc.orb_random_pattern(31).reshape(256, 2, 2)[::-1].reshape(512, 2), dtype=np.int32)
+    pat.tofile(d / "pattern.i32")
+    r = subprocess.run([DROPIN, "-s", str(d / "settings.yml")], capture_output=True, text=True, timeout=120, cwd=d,
+                       env=dict(env, FM3D_ORB_PATTERN=str(d / "pattern.i32")))
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "makeRandomPattern" not in r.stderr and "ignored" not in r.stderr
+    pd = np.fromfile(d / "out_patch_desc.u8", dtype=np.uint8).reshape(-1, 32)
+    kp = np.zeros(1, dtype=fm3d.KEYPOINT)
+    kp["x"] = kp["y"] = 64
+    kp["size"] = 128
+    kp["angle"] = -1
+    kp["response"] = 1
+    s = fm3d.Settings.load(str(d / "settings.yml"))
+    _, _, _, patches, _ = _python_chain(fm3d, s, pair.img1, pair.img2)
+    assert len(pd) == len(patches) > 3
+    ref = np.stack([orc.orb_compute(p, kp, pattern=pat)[2][0] for p in patches[:6]])
+    assert np.array_equal(pd[:6], ref)
+    assert not np.array_equal(ref, np.stack([orc.orb_compute(p, kp)[2][0] for p in patches[:6]]))
+
+
+@pytest.mark.gpu
 def test_mosaic_python_and_cpp(fm3d, synth, tmp_path):
     """MOSAIC (mosaic.h:47-70, mosaic.cpp:32-73): the Python class and the C++ one (mosaic_demo,
     include/fm3d_cv.hpp) run the same pipeline; their patch descriptors and points equal the
