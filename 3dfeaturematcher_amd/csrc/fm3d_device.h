@@ -18,8 +18,33 @@ struct Camera {
     double k[5];  // OpenCV order k1,k2,p1,p2,k3 (settings k0,k1,p1,p2,k2; singlecameratriangulator.cpp:99-105)
 };
 
+// 1 / d, correctly rounded.  On the device for 2^-700 <= |d| <= 2^700 the hardware reciprocal with
+// Newton steps and one Markstein correction (the division operator's steps without its operand
+// scaling and fix-up, which change nothing in that range; fm3d_fastdiv.h recip_fast, checked against
+// the operator by tools/micro/div_check.hip), else the operator.
+__host__ __device__ inline double recip_exact(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double ad = fabs(d);
+    if (ad >= 0x1p-700 && ad <= 0x1p700) {
+        double r = __builtin_amdgcn_rcp(d);
+        double e = __builtin_fma(-d, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        e = __builtin_fma(-d, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        const double rem = __builtin_fma(-d, r, 1.0);
+        return __builtin_fma(rem, r, r);
+    }
+#endif
+    return 1. / d;
+}
+
 // cv::undistortPoints (OpenCV 2.4 cvUndistortPoints), 5 iterations, R = I.
 // Reference call sites: singlecameratriangulator.cpp:169-170 (keypoints), :542 (neighbourhood).
+// OpenCV evaluates icdist = (1 + ((k7 r2 + k6) r2 + k5) r2) / (1 + ((k3 r2 + k2) r2 + k1) r2) with
+// the rational coefficients k5..k7 = 0, and then applies R = I and the identity P as
+// (1 x + 0 y + 0, 0 x + 1 y + 0) * 1 / (0 x + 0 y + 1).  For a finite r2 the numerator is exactly 1,
+// and for finite x, y the transform is x + 0, y + 0 (which turns -0 into +0, as 1 x + 0 y + 0 does)
+// times 1: the same bits with fewer operations.  A non-finite r2, x or y takes the literal forms.
 __host__ __device__ inline void undistort1(const Camera& c, double x, double y, double& ox, double& oy) {
     const double ifx = 1. / c.fx, ify = 1. / c.fy;
     double x0, y0;
@@ -27,11 +52,21 @@ __host__ __device__ inline void undistort1(const Camera& c, double x, double y, 
     y0 = y = (y - c.cy) * ify;
     for (int j = 0; j < 5; j++) {
         double r2 = x * x + y * y;
-        double icdist = (1 + ((0. * r2 + 0.) * r2 + 0.) * r2) / (1 + ((c.k[4] * r2 + c.k[1]) * r2 + c.k[0]) * r2);
+        const double den = 1 + ((c.k[4] * r2 + c.k[1]) * r2 + c.k[0]) * r2;
+        double icdist;
+        if (r2 <= DBL_MAX)
+            icdist = recip_exact(den);
+        else
+            icdist = (1 + ((0. * r2 + 0.) * r2 + 0.) * r2) / den;
         double deltaX = 2 * c.k[2] * x * y + c.k[3] * (r2 + 2 * x * x);
         double deltaY = c.k[2] * (r2 + 2 * y * y) + 2 * c.k[3] * x * y;
         x = (x0 - deltaX) * icdist;
         y = (y0 - deltaY) * icdist;
+    }
+    if (fabs(x) <= DBL_MAX && fabs(y) <= DBL_MAX) {
+        ox = x + 0.;
+        oy = y + 0.;
+        return;
     }
     double xx = 1. * x + 0. * y + 0.;
     double yy = 0. * x + 1. * y + 0.;

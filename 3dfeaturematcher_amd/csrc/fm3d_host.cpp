@@ -3360,18 +3360,18 @@ int freak_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keyp
 int mser_flood(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserParams& P, fm3d::MserLayout& L,
                std::vector<int4>& regs, int& n0, std::vector<long long>& off) {
     if (w <= 0 || h <= 0) return fail(c, FM3D_ERR_INVALID, "MSER: empty image");
-    if ((long long)w * h > (1LL << 28) || (long long)(h + 2) * 2 * (w + 2) > (1LL << 30))
+    if ((long long)w * h >= (1LL << 28) - 1 || w > 65535 || h > 65535)
         return fail(c, FM3D_ERR_INVALID, "MSER: image too large");
     L = fm3d::mser_layout(w, h);
     HIPCHK(c, c->msImg.ensure((size_t)w * h));
-    HIPCHK(c, c->msWork.ensure((size_t)2 * L.imgInts * sizeof(int)));
-    HIPCHK(c, c->msHeap.ensure((size_t)2 * L.heapInts * sizeof(int)));
+    HIPCHK(c, c->msWork.ensure(L.visInLds ? 16 : (size_t)2 * L.visWords * sizeof(unsigned)));
+    HIPCHK(c, c->msHeap.ensure((size_t)2 * L.heapEntries * sizeof(int2)));
     HIPCHK(c, c->msNode.ensure((size_t)2 * L.nodes * sizeof(int2)));
     HIPCHK(c, c->msHist.ensure((size_t)2 * L.hists * sizeof(fm3d::MserHist)));
     HIPCHK(c, c->msReg.ensure((size_t)2 * L.regCap * sizeof(int4)));
     HIPCHK(c, c->msCnt.ensure(2 * sizeof(int)));
     HIPCHK(c, hipMemcpyAsync(c->msImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
-    fm3d::launch_mser_flood(c->msImg.as<uint8_t>(), L, P, c->msWork.as<int>(), c->msHeap.as<int>(),
+    fm3d::launch_mser_flood(c->msImg.as<uint8_t>(), L, P, c->msWork.as<unsigned>(), c->msHeap.as<int2>(),
                             c->msNode.as<int2>(), c->msHist.as<fm3d::MserHist>(), c->msReg.as<int4>(),
                             c->msCnt.as<int>(), c->stream);
     HIPCHK(c, hipGetLastError());

@@ -386,18 +386,20 @@ struct MserHist {  // MSERGrowHistory by index
 };
 // the workspace of one pass over a w x h image (both passes: twice, pass-major)
 struct MserLayout {
-    int w, h, step, stepgap;
-    long long imgInts;   // (h + 2) * step
-    long long heapInts;  // w * h + 256
-    long long nodes;     // w * h: {next node, pixel offset}
-    long long hists;     // 2 w h (a bound: one per raise and per merge)
+    int w, h;
+    int visInLds;        // the visited bitmap in LDS (w * h <= kMserLdsBits), else in HBM
+    long long visWords;  // ceil(w * h / 32)
+    long long heapEntries;  // w * h + 256: {pixel + 1 | direction << 28, x | y << 16}
+    long long nodes;     // w * h: {next node, x | y << 16}
+    long long hists;     // 2 w h + 2 (a bound: one per raise and per merge)
     long long regCap;    // region records per pass
 };
+constexpr long long kMserLdsBits = 120 * 1024 * 8;
 MserLayout mser_layout(int w, int h);
 // both flood passes, one workgroup each (pass 0 on 255 - I, colour -1; pass 1 on I, colour +1):
 // reg[pass * regCap + r] = {colour, head node, point count, 0}; nreg[pass] = regions (all, even past regCap)
-void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, int* work, int* heap, int2* node,
-                       MserHist* hist, int4* reg, int* nreg, hipStream_t s);
+void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, unsigned* vis, int2* heap,
+                       int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s);
 // fitEllipse per region (one lane each): region r of the concatenated list (pass 0's n0 then pass 1's),
 // its points at off[r] in xy (walked from the node list) and 5 * count doubles of scratch at 5 * off[r];
 // kp[r] = KeyPoint(centre, sqrt(w h)), flag[r] = kept (diameter > FLT_EPSILON, rounded centre inside)

@@ -10,11 +10,19 @@
 // pass whose visiting order decides which component's history continues at equal-size merges, which
 // point list comes first, and the order the regions come out in -- all part of the detector's output.
 // It is sequential by construction, so each pass is one lane (the two passes run side by side, one
-// workgroup each); the rest of the workgroup lays out the padded int image and the grey-level
-// histogram first.  The component stack (257 entries) and the 256 bucket tops live in LDS; the padded
-// image, the bucket heap, the point nodes and the histories in HBM (L2-resident at VGA sizes).
-// fitEllipse then runs one lane per region (its three least-squares solves are OpenCV's scalar
-// one-sided Jacobi SVD, sums in the region list's order), all regions in parallel.
+// workgroup each; the rest of the workgroup builds the grey-level histogram and clears the state
+// first).  The lane is latency-bound, so the state is laid out for one memory round trip per pixel:
+//   * mser.cpp's padded int image (value, visited bit, next direction) is split: the grey values
+//     are read from the 8-bit input (read-only, cache-resident), the visited bits are a bitmap in
+//     LDS (up to kMserLdsBits pixels; HBM beyond), and the next direction travels in the bucket
+//     entry of a pixel pushed back by a descent ({pixel + 1 | direction << 28, x | y << 16});
+//   * the top entry of every grey-level bucket is cached in LDS, so a pop reads LDS and the refill
+//     of that bucket's new top from HBM is issued with the neighbours' value loads;
+//   * the top component of the stack stays in registers (size, tail, history), the ones below it in
+//     LDS.
+// The point lists (node = {next, x | y << 16}) and the histories are in HBM.  fitEllipse then runs
+// one lane per region (its three least-squares solves are OpenCV's scalar one-sided Jacobi SVD, sums
+// in the region list's order), all regions in parallel.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
@@ -28,15 +36,10 @@ MserLayout mser_layout(int w, int h) {
     MserLayout L;
     L.w = w;
     L.h = h;
-    L.step = 8;
-    L.stepgap = 3;
-    while (L.step < w + 2) {
-        L.step <<= 1;
-        L.stepgap++;
-    }
     const long long N = (long long)w * h;
-    L.imgInts = (long long)(h + 2) * L.step;
-    L.heapInts = N + 256;
+    L.visInLds = N <= kMserLdsBits;
+    L.visWords = (N + 31) / 32;
+    L.heapEntries = N + 256;
     L.nodes = N;
     L.hists = 2 * N + 2;
     L.regCap = N + 1;
@@ -141,144 +144,175 @@ __device__ __forceinline__ bool stable_check(Comp& c, MserHist* hist, const Mser
     return stable;
 }
 
+// one bucket entry: {pixel + 1 | next direction << 28, x | y << 16}; {0, 0} is a bucket's base
+__device__ __forceinline__ int2 mser_entry(int p, int x, int y, int dir) {
+    return make_int2((p + 1) | (dir << 28), x | (y << 16));
+}
+
+template <bool LDSVIS>
 __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t* __restrict__ src, MserLayout L,
-                                                                   MserParams P, int* work, int* heapAll,
+                                                                   MserParams P, unsigned* visAll, int2* heapAll,
                                                                    int2* nodeAll, MserHist* histAll, int4* regAll,
                                                                    int* nreg) {
     const int pass = blockIdx.x, tid = threadIdx.x;
-    int* img = work + (size_t)pass * L.imgInts;
-    int* heap = heapAll + (size_t)pass * L.heapInts;
+    const int w = L.w, h = L.h;
+    const int N = w * h;
+    int2* heap = heapAll + (size_t)pass * L.heapEntries;
     int2* node = nodeAll + (size_t)pass * L.nodes;
     MserHist* hist = histAll + (size_t)pass * L.hists;
     int4* reg = regAll + (size_t)pass * L.regCap;
+    extern __shared__ unsigned visLds[];
+    unsigned* vis = LDSVIS ? visLds : visAll + (size_t)pass * L.visWords;
     __shared__ int hcur[256];
     __shared__ int lsize[256];
+    __shared__ int2 topE[256];
     __shared__ Comp comp[257];
     for (int i = tid; i < 256; i += kMserThreads) lsize[i] = 0;
+    for (long long i = tid; i < L.visWords; i += kMserThreads) vis[i] = 0u;
     __syncthreads();
-    // preprocessMSER_8UC1: -1 border, grey value (255 - I on pass 0) inside, the level histogram
-    const int smask = L.step - 1;
-    for (long long i = tid; i < L.imgInts; i += kMserThreads) {
-        const int y = (int)(i >> L.stepgap), x = (int)(i & smask);
-        int v = -1;
-        if (y >= 1 && y <= L.h && x >= 1 && x <= L.w) {
-            const int g = src[(size_t)(y - 1) * L.w + (x - 1)];
-            v = pass == 0 ? 255 - g : g;
-            atomicAdd(&lsize[v], 1);
-        }
-        img[i] = v;
+    // preprocessMSER_8UC1's level histogram (pass 0 floods 255 - I, pass 1 I)
+    for (int i = tid; i < N; i += kMserThreads) {
+        const int g = src[i];
+        atomicAdd(&lsize[pass == 0 ? 255 - g : g], 1);
     }
     __syncthreads();
     if (tid != 0) return;
     {
         int base = 0;
-        hcur[0] = 0;
-        heap[0] = 0;
-        for (int i = 1; i < 256; i++) {
-            base += lsize[i - 1] + 1;
+        for (int i = 0; i < 256; i++) {
+            if (i) base += lsize[i - 1] + 1;
             hcur[i] = base;
-            heap[base] = 0;
+            heap[base] = make_int2(0, 0);
+            topE[i] = make_int2(0, 0);
         }
     }
-    const int color = pass == 0 ? -1 : 1, ioff = L.step + 1;
+    const int color = pass == 0 ? -1 : 1;
     const long long regCap = L.regCap;
+    const unsigned inv = pass == 0 ? 255u : 0u;  // value = g ^ inv (255 - g for pass 0)
     int nnode = 0, nhist = 0, nr = 0;
-    int cur = ioff;
-    int cv = img[cur];
+    // the current pixel
+    int p = 0, x = 0, y = 0, dir = 0;
+    int v = (int)(src[0] ^ inv);
+    vis[0] |= 1u;
+    // the stack: comp[1 .. top - 1] in LDS, the top one in T; comp[0] the 256 sentinel
     int top = 1;
     comp[0].level = 256;
-    comp_init(comp[1]);
-    comp[1].level = cv & 0xff;
-    cv |= (int)0x80000000;
-    img[cur] = cv;
-    int lev = cv & 0xff;
+    Comp T;
+    comp_init(T);
+    T.level = v;
+    int belowLevel = 256;  // comp[top - 1].level
+    // a pop's bucket refill in flight: topE[pendB] = pendE once it has arrived
+    int pendB = -1;
+    int2 pendE = make_int2(0, 0);
     for (;;) {
-        bool descended = false;
-        while ((cv & 0x70000) < 0x40000) {
-            const int d = (cv & 0x70000) >> 16;
-            const int nb = cur + (d == 0 ? 1 : d == 1 ? L.step : d == 2 ? -1 : -L.step);
-            int nv = img[nb];
-            if (nv >= 0) {
-                nv |= (int)0x80000000;
-                img[nb] = nv;
-                if ((nv & 0xff) < (cv & 0xff)) {
-                    // push the current pixel back and open a component at the neighbour's level
-                    const int t = ++hcur[lev];
-                    heap[t] = cur;
-                    cv += 0x10000;
-                    img[cur] = cv;
-                    lev = nv & 0xff;
-                    cur = nb;
-                    cv = nv;
-                    top++;
-                    comp_init(comp[top]);
-                    comp[top].level = lev;
-                    descended = true;
+        // --- the remaining neighbours of p, from direction dir (right, down, left, up) ---
+        int np[4], nv[4];
+        bool cand[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int nx = x + (d == 0 ? 1 : d == 2 ? -1 : 0), ny = y + (d == 1 ? 1 : d == 3 ? -1 : 0);
+            const bool in = d >= dir && nx >= 0 && nx < w && ny >= 0 && ny < h;
+            np[d] = in ? p + (d == 0 ? 1 : d == 1 ? w : d == 2 ? -1 : -w) : p;
+            cand[d] = in && !((vis[np[d] >> 5] >> (np[d] & 31)) & 1u);
+        }
+#pragma unroll
+        for (int d = 0; d < 4; d++) nv[d] = (int)(src[np[d]] ^ inv);  // issued together
+        if (pendB >= 0) {  // the previous pop's refill (issued before these loads)
+            topE[pendB] = pendE;
+            pendB = -1;
+        }
+        int descend = -1;
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            if (descend >= 0 || !cand[d]) continue;
+            vis[np[d] >> 5] |= 1u << (np[d] & 31);
+            const int nx = x + (d == 0 ? 1 : d == 2 ? -1 : 0), ny = y + (d == 1 ? 1 : d == 3 ? -1 : 0);
+            if (nv[d] < v) {
+                descend = d;
+            } else {
+                const int b = nv[d];
+                const int t = ++hcur[b];
+                const int2 e = mser_entry(np[d], nx, ny, 0);
+                heap[t] = e;
+                topE[b] = e;
+            }
+        }
+        if (descend >= 0) {
+            // push p back (resuming after `descend`) and open a component at the neighbour's level
+            const int d = descend;
+            const int t = ++hcur[v];
+            const int2 e = mser_entry(p, x, y, d + 1);
+            heap[t] = e;
+            topE[v] = e;
+            x += d == 0 ? 1 : d == 2 ? -1 : 0;
+            y += d == 1 ? 1 : d == 3 ? -1 : 0;
+            p = np[d];
+            v = nv[d];
+            dir = 0;
+            comp[top] = T;
+            belowLevel = T.level;
+            top++;
+            comp_init(T);
+            T.level = v;
+            continue;
+        }
+        // accumulateMSERComp: the finished pixel joins the top component's list
+        node[nnode] = make_int2(-1, x | (y << 16));
+        if (T.size > 0)
+            node[T.tail].x = nnode;
+        else
+            T.head = nnode;
+        T.tail = nnode;
+        T.size++;
+        nnode++;
+        // the next pixel: this level's bucket, else the next non-empty level
+        int2 e = topE[v];
+        int pv = v;
+        if (!e.x) {
+            pv = 0;
+            for (int i = v + 1; i < 256; i++)
+                if (topE[i].x) {
+                    pv = i;
                     break;
                 }
-                const int b = nv & 0xff;
-                const int t = ++hcur[b];
-                heap[t] = nb;
-            }
-            cv += 0x10000;
-        }
-        if (descended) continue;
-        // accumulateMSERComp: the finished pixel joins the top component's list
-        {
-            Comp& c = comp[top];
-            node[nnode] = make_int2(-1, cur - ioff);
-            if (c.size > 0)
-                node[c.tail].x = nnode;
-            else
-                c.head = nnode;
-            c.tail = nnode;
-            c.size++;
-            nnode++;
+            if (!pv) break;
+            e = topE[pv];
         }
         {
-            const int t = hcur[lev];
-            const int nx = heap[t];
-            if (nx) {
-                cur = nx;
-                hcur[lev] = t - 1;
-                cv = img[cur];
-                continue;
-            }
+            const int t = --hcur[pv];
+            pendE = heap[t];  // the bucket's next top, consumed after the neighbour loads
+            pendB = pv;
         }
-        int pv = 0;
-        for (int i = (cv & 0xff) + 1; i < 256; i++)
-            if (heap[hcur[i]]) {
-                pv = i;
-                break;
-            }
-        if (!pv) break;
-        lev = pv;
-        {
-            const int t = hcur[lev];
-            cur = heap[t];
-            hcur[lev] = t - 1;
-            cv = img[cur];
-        }
-        if (pv < comp[top - 1].level) {
-            if (stable_check(comp[top], hist, P)) {
-                if (nr < regCap) reg[nr] = make_int4(color, comp[top].head, hist[comp[top].hist].size, 0);
-                nr++;
-            }
-            new_history(comp[top], hist, nhist++);
-            comp[top].level = pv;
-        } else {
-            for (;;) {
-                top--;
-                merge(comp[top + 1], comp[top], hist, node, nhist++);
-                if (pv <= comp[top].level) break;
-                if (pv < comp[top - 1].level) {
-                    if (stable_check(comp[top], hist, P)) {
-                        if (nr < regCap) reg[nr] = make_int4(color, comp[top].head, hist[comp[top].hist].size, 0);
-                        nr++;
+        p = (e.x & 0x0fffffff) - 1;
+        dir = (int)((unsigned)e.x >> 28);
+        x = e.y & 0xffff;
+        y = (int)((unsigned)e.y >> 16);
+        if (pv != v) {
+            v = pv;
+            if (pv < belowLevel) {
+                if (stable_check(T, hist, P)) {
+                    if (nr < regCap) reg[nr] = make_int4(color, T.head, hist[T.hist].size, 0);
+                    nr++;
+                }
+                new_history(T, hist, nhist++);
+                T.level = pv;
+            } else {
+                for (;;) {
+                    top--;
+                    Comp B = comp[top];
+                    merge(T, B, hist, node, nhist++);
+                    T = B;
+                    belowLevel = comp[top - 1].level;
+                    if (pv <= T.level) break;
+                    if (pv < belowLevel) {
+                        if (stable_check(T, hist, P)) {
+                            if (nr < regCap) reg[nr] = make_int4(color, T.head, hist[T.hist].size, 0);
+                            nr++;
+                        }
+                        new_history(T, hist, nhist++);
+                        T.level = pv;
+                        break;
                     }
-                    new_history(comp[top], hist, nhist++);
-                    comp[top].level = pv;
-                    break;
                 }
             }
         }
@@ -286,13 +320,35 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     nreg[pass] = nr;
 }
 
-// cv::solve(A, b, DECOMP_SVD) with At = A^T (n rows of m), b constant (bval): JacobiSVDImpl_ + SVBkSbImpl_
-__device__ void svd_solve(double* At, int m, int n, double bval, double* x) {
+// lane l's double, on every lane (two v_readlane: the index is wave-uniform)
+__device__ __forceinline__ double lane_get(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// s + t[0] + t[1] + ... + t[cnt - 1] in that order (t[l] on lane l), on every lane
+__device__ __forceinline__ double seq_add(double s, double t, int cnt) {
+    for (int l = 0; l < cnt; l++) s += lane_get(t, l);
+    return s;
+}
+
+// cv::solve(A, b, DECOMP_SVD) with At = A^T (n rows of m), b constant (bval): JacobiSVDImpl_ +
+// SVBkSbImpl_ by one wave.  The element-wise steps run lane-parallel (lane l takes k = l, l + 64,
+// ...); every sum runs over k in order, its terms computed by the lanes and added one by one
+// (seq_add), so each sum has the scalar loop's bits.  Every lane holds W, Vt and x.
+__device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x) {
+    const int lane = threadIdx.x & 63;
     double W[5], Vt[25];
     const double eps = DBL_EPSILON * 10;
     for (int i = 0; i < n; i++) {
         double sd = 0;
-        for (int k = 0; k < m; k++) sd += At[i * m + k] * At[i * m + k];
+        for (int base = 0; base < m; base += 64) {
+            const int k = base + lane;
+            const double t = k < m ? At[i * m + k] : 0.;
+            sd = seq_add(sd, t * t, min(64, m - base));
+        }
         W[i] = sd;
         for (int k = 0; k < n; k++) Vt[i * n + k] = 0;
         Vt[i * n + i] = 1;
@@ -305,7 +361,11 @@ __device__ void svd_solve(double* At, int m, int n, double bval, double* x) {
                 double* Ai = At + i * m;
                 double* Aj = At + j * m;
                 double a = W[i], pp = 0, bb = W[j];
-                for (int k = 0; k < m; k++) pp += Ai[k] * Aj[k];
+                for (int base = 0; base < m; base += 64) {
+                    const int k = base + lane;
+                    const double t = k < m ? Ai[k] * Aj[k] : 0.;
+                    pp = seq_add(pp, t, min(64, m - base));
+                }
                 if (fabs(pp) <= eps * sqrt(a * bb)) continue;
                 pp *= 2;
                 const double beta = a - bb, gamma = sqrt(pp * pp + beta * beta);
@@ -319,13 +379,22 @@ __device__ void svd_solve(double* At, int m, int n, double bval, double* x) {
                     s = pp / (gamma * c * 2);
                 }
                 a = bb = 0;
-                for (int k = 0; k < m; k++) {
-                    const double t0 = c * Ai[k] + s * Aj[k];
-                    const double t1 = -s * Ai[k] + c * Aj[k];
-                    Ai[k] = t0;
-                    Aj[k] = t1;
-                    a += t0 * t0;
-                    bb += t1 * t1;
+                for (int base = 0; base < m; base += 64) {
+                    const int k = base + lane;
+                    double t0 = 0., t1 = 0.;
+                    if (k < m) {
+                        const double ai = Ai[k], aj = Aj[k];
+                        t0 = c * ai + s * aj;
+                        t1 = -s * ai + c * aj;
+                        Ai[k] = t0;
+                        Aj[k] = t1;
+                    }
+                    const double q0 = t0 * t0, q1 = t1 * t1;
+                    const int cnt = min(64, m - base);
+                    for (int l = 0; l < cnt; l++) {  // the two sums interleaved, each in k order
+                        a += lane_get(q0, l);
+                        bb += lane_get(q1, l);
+                    }
                 }
                 W[i] = a;
                 W[j] = bb;
@@ -341,7 +410,11 @@ __device__ void svd_solve(double* At, int m, int n, double bval, double* x) {
     }
     for (int i = 0; i < n; i++) {
         double sd = 0;
-        for (int k = 0; k < m; k++) sd += At[i * m + k] * At[i * m + k];
+        for (int base = 0; base < m; base += 64) {
+            const int k = base + lane;
+            const double t = k < m ? At[i * m + k] : 0.;
+            sd = seq_add(sd, t * t, min(64, m - base));
+        }
         W[i] = sqrt(sd);
     }
     for (int i = 0; i < n - 1; i++) {
@@ -352,7 +425,7 @@ __device__ void svd_solve(double* At, int m, int n, double bval, double* x) {
             double t = W[i];
             W[i] = W[j];
             W[j] = t;
-            for (int k = 0; k < m; k++) {
+            for (int k = lane; k < m; k += 64) {
                 t = At[i * m + k];
                 At[i * m + k] = At[j * m + k];
                 At[j * m + k] = t;
@@ -367,7 +440,7 @@ __device__ void svd_solve(double* At, int m, int n, double bval, double* x) {
     for (int i = 0; i < n; i++) {
         if (W[i] <= DBL_MIN) continue;  // OpenCV's random left vector: unused below
         const double t = 1. / W[i];
-        for (int k = 0; k < m; k++) At[i * m + k] *= t;
+        for (int k = lane; k < m; k += 64) At[i * m + k] *= t;
     }
     double threshold = 0;
     for (int i = 0; i < n; i++) x[i] = 0;
@@ -377,7 +450,11 @@ __device__ void svd_solve(double* At, int m, int n, double bval, double* x) {
         double wi = W[i], s = 0;
         if (fabs(wi) <= threshold) continue;
         wi = 1 / wi;
-        for (int k = 0; k < m; k++) s += At[i * m + k] * bval;
+        for (int base = 0; base < m; base += 64) {
+            const int k = base + lane;
+            const double t = k < m ? At[i * m + k] * bval : 0.;
+            s = seq_add(s, t, min(64, m - base));
+        }
         s *= wi;
         for (int k = 0; k < n; k++) x[k] = x[k] + s * Vt[i * n + k];
     }
@@ -387,7 +464,7 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
                                                       const int2* __restrict__ nodeAll, long long nodes,
                                                       const long long* __restrict__ off, MserLayout L, int2* xyAll,
                                                       double* scratch, fm3d_keypoint* kp, int* flag, float* boxOut) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.x, lane = threadIdx.x;  // one wave per region
     if (r >= n) return;
     const int pass = r < n0 ? 0 : 1;
     const int4 R = reg[pass * regCap + (pass ? r - n0 : r)];
@@ -395,22 +472,29 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
     const int m = R.z;
     int2* xy = xyAll + off[r];
     double* At = scratch + 5 * off[r];
-    {
+    if (lane == 0) {  // the region's list: one dependent walk
         int q = R.y;
         for (int k = 0; k < m; k++) {
             const int2 nd = node[q];
-            xy[k] = make_int2(nd.y & (L.step - 1), nd.y >> L.stepgap);
+            xy[k] = make_int2(nd.y & 0xffff, (int)((unsigned)nd.y >> 16));
             q = nd.x;
         }
     }
+    __threadfence_block();
+    __syncthreads();
+    // the float centroid: integer coordinates below 2^24 in every partial sum, so exact in any order
     float cx = 0.f, cy = 0.f;
-    for (int k = 0; k < m; k++) {
+    for (int k = lane; k < m; k += 64) {
         cx = __fadd_rn(cx, (float)xy[k].x);
         cy = __fadd_rn(cy, (float)xy[k].y);
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        cx = __fadd_rn(cx, __shfl_xor(cx, o));
+        cy = __fadd_rn(cy, __shfl_xor(cy, o));
+    }
     cx = cx / (float)m;
     cy = cy / (float)m;
-    for (int k = 0; k < m; k++) {
+    for (int k = lane; k < m; k += 64) {
         const float px = __fsub_rn((float)xy[k].x, cx), py = __fsub_rn((float)xy[k].y, cy);
         At[0 * m + k] = -(double)px * (double)px;
         At[1 * m + k] = -(double)py * (double)py;
@@ -419,7 +503,7 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
         At[4 * m + k] = py;
     }
     double gfp[5], rp[5];
-    svd_solve(At, m, 5, 10000.0, gfp);
+    svd_solve_wave(At, m, 5, 10000.0, gfp);
     {
         double A2[4], x2[2];
         A2[0] = 2 * gfp[0];
@@ -517,14 +601,14 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
         rp[0] = x2[0];
         rp[1] = x2[1];
     }
-    for (int k = 0; k < m; k++) {
+    for (int k = lane; k < m; k += 64) {
         const float px = __fsub_rn((float)xy[k].x, cx), py = __fsub_rn((float)xy[k].y, cy);
         At[0 * m + k] = ((double)px - rp[0]) * ((double)px - rp[0]);
         At[1 * m + k] = ((double)py - rp[1]) * ((double)py - rp[1]);
         At[2 * m + k] = ((double)px - rp[0]) * ((double)py - rp[1]);
     }
     double g[3];
-    svd_solve(At, m, 3, 1.0, g);
+    svd_solve_wave(At, m, 3, 1.0, g);
     const double min_eps = 1e-6;
     rp[4] = -0.5 * fm3d_atan2(g[2], g[1] - g[0]);
     double t = fm3d_sin(-2.0 * rp[4]);
@@ -556,6 +640,7 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
     k.response = 0.f;
     k.octave = 0;
     k.class_id = -1;
+    if (lane != 0) return;
     kp[r] = k;
     flag[r] = diam > FLT_EPSILON && rx >= 0 && rx < L.w && ry >= 0 && ry < L.h;
     if (boxOut) {
@@ -569,16 +654,23 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
 
 }  // namespace
 
-void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, int* work, int* heap, int2* node,
-                       MserHist* hist, int4* reg, int* nreg, hipStream_t s) {
-    mser_flood_kernel<<<2, kMserThreads, 0, s>>>(img, L, P, work, heap, node, hist, reg, nreg);
+void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, unsigned* vis, int2* heap,
+                       int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s) {
+    if (L.visInLds) {
+        const size_t lds = (size_t)L.visWords * sizeof(unsigned);
+        hipFuncSetAttribute((const void*)mser_flood_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        mser_flood_kernel<true><<<2, kMserThreads, lds, s>>>(img, L, P, vis, heap, node, hist, reg, nreg);
+    } else {
+        mser_flood_kernel<false><<<2, kMserThreads, 0, s>>>(img, L, P, vis, heap, node, hist, reg, nreg);
+    }
 }
 
 void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const int2* node, long long nodes,
                      const long long* off, const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag,
                      float* box, hipStream_t s) {
     if (n <= 0) return;
-    mser_fit_kernel<<<(n + 63) / 64, 64, 0, s>>>(reg, regCap, n0, n, node, nodes, off, L, xy, scratch, kp, flag, box);
+    mser_fit_kernel<<<n, 64, 0, s>>>(reg, regCap, n0, n, node, nodes, off, L, xy, scratch, kp, flag, box);
 }
 
 }  // namespace fm3d

@@ -98,6 +98,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the C5 byte-identity check against one GPU")
     ap.add_argument("--out", type=str, default="")
+    ap.add_argument("--dump-records", type=str, default="",
+                    help="torchrun C5: rank 0 saves the last step's merged survivor records (.npy)")
     ap.add_argument("--pmc-json", type=str, default=next(
         (p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_c4.json") for r in (4, 3, 2)) if os.path.exists(p)),
         os.path.join(ROOT, "profiles", "r02_pmc_c4.json")),
@@ -130,6 +132,8 @@ def main():
         return run_c3(args)
     if world == 1 and workload == "c4" and args.mode == "stream":
         return run_c4_stream(args)
+    if world > 1 and not args.weak and args.mode == "stream":
+        return run_torchrun_stream(args, workload)
     return run_resident(args, workload)
 
 
@@ -442,6 +446,175 @@ def run_mgpu(args, workload):
     if len(digests) != 1:
         out["verified"] = False
     emit(out, args)
+
+
+def run_torchrun_stream(args, workload):
+    """The torchrun route (WORLD_SIZE > 1, one process per GPU), C5 as north_star states it: ONE 1M-
+    keypoint frame pair per step, the same on every rank; rank r takes the 4,096-query blocks
+    shard.query_blocks(1M, N, r) (frame B and both images replicated) and keeps frame pairs in flight
+    as at one GPU (`inflight` LM launches of `lm_pairs` linked pairs, fm3d_pipeline_submit / wait, one
+    context + HIP stream each); every finished step's survivor records are all-gathered over RCCL
+    (torch.distributed, backend nccl) and rank 0 merges the last one in query order and checks it
+    against the committed fixture.  Each step runs from host memory to host memory as at one GPU.
+    Strong scaling: value = kept keypoints of the K frame pairs (all ranks) / the max-over-ranks wall
+    time.  FM3D_BENCH_BACKEND=gloo with FM3D_BENCH_SHARE_DEVICE=1 runs the ranks on one GPU with a CPU
+    all-gather (the multi-rank logic on a one-GPU box; tests/test_gpu_parity.py)."""
+    import torch
+    import torch.distributed as tdist
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("FM3D_BENCH_BACKEND", "nccl")
+    vis = torch.cuda.device_count()
+    dev = 0 if os.environ.get("FM3D_BENCH_SHARE_DEVICE") == "1" else local
+    if dev >= vis:
+        print(f"bench.py rank {rank}: device {dev} not visible ({vis} GPU(s))", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    torch.cuda.set_device(dev)
+    tdist.init_process_group(backend)  # nccl: RCCL over xGMI
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
+    synth = importlib.import_module("3dfeaturematcher_amd.synth")
+    shard = importlib.import_module("3dfeaturematcher_amd.shard")
+    wl = dict(WORKLOADS[workload])
+    for k in ("keypoints", "width", "height"):
+        if getattr(args, k):
+            wl[k] = getattr(args, k)
+    t_gen = time.time()
+    pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=args.seed, desc=args.desc)
+    t_gen = time.time() - t_gen
+    s = c4_settings(fm3d, pair, args)
+    n = len(pair.desc1)
+    qidx = shard.query_blocks(n, world, rank)
+    inputs = (pair.desc1[qidx], pair.desc2, pair.kp1[qidx], pair.kp2, pair.img1, pair.img2)
+    nl = max(1, args.lm_pairs)
+    nf = max(1, args.inflight) * nl
+    streams = [torch.cuda.Stream(device=dev) for _ in range(nf)]
+    ctxs, pipes = [], []
+    for st in streams:
+        ctx = fm3d.Context(s, device=dev)
+        ctx.set_stream(st.cuda_stream)
+        fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
+        ctxs.append(ctx)
+        pipes.append(fm3d.Pipeline(ctx))
+    for i in range(0, nf, nl):
+        for j in range(i, i + nl - 1):
+            pipes[j].link(pipes[i + nl - 1])
+    binary = args.desc == "orb"
+    bufs = [np.zeros(len(qidx), dtype=fm3d.RECORD) for _ in range(nf)]
+    cap = shard.blocks_capacity(n, world)
+    rec_t = torch.zeros((cap, shard.RECORD_BYTES), dtype=torch.uint8,
+                        device="cpu" if backend == "gloo" else f"cuda:{dev}")
+
+    def gather(rec):
+        k = len(rec)
+        if k:
+            rec_t[:k].copy_(torch.from_numpy(rec.view(np.uint8).reshape(k, shard.RECORD_BYTES)))
+        return shard.all_gather_device(rec_t, k)
+
+    def stream_run(n_steps):
+        res, pend, t_sub, last = [], [None] * nf, [0.0] * nf, None
+
+        def drain(j):
+            rec, st = pipes[j].wait(bufs[j])
+            g = gather(rec)
+            res.append((len(rec), st, time.perf_counter() - t_sub[j]))
+            pend[j] = None
+            return g
+
+        for k in range(n_steps):
+            j = k % nf
+            if pend[j] is not None:
+                last = drain(j)
+            t_sub[j] = time.perf_counter()
+            pipes[j].submit(*inputs, binary=binary)
+            pend[j] = True
+        for k in range(n_steps, n_steps + nf):
+            j = k % nf
+            if pend[j] is not None:
+                last = drain(j)
+        return res, last
+
+    def sync():
+        torch.cuda.synchronize()
+        tdist.barrier()
+        torch.cuda.synchronize()
+
+    stream_run(args.warmup)
+    sync()
+    t0 = time.perf_counter()
+    res, last = stream_run(args.steps)
+    sync()
+    elapsed = time.perf_counter() - t0
+    for c in ctxs:
+        c.close()
+    red = torch.tensor([elapsed, float(sum(r[0] for r in res))], dtype=torch.float64, device=rec_t.device)
+    t_max = red[:1].clone()
+    tdist.all_reduce(t_max, op=tdist.ReduceOp.MAX)
+    kept = red[1:].clone()
+    tdist.all_reduce(kept, op=tdist.ReduceOp.SUM)
+    elapsed, all_kept = float(t_max.item()), int(kept.item())
+    stats = [r[1] for r in res]
+    lat = [r[2] * 1e3 for r in res]
+    if rank == 0:
+        merged = shard.merge_gathered_shares(last[0], last[1], n)
+        frame_s = elapsed / args.steps
+        pix_local = float(np.mean([st["lm"]["pixel_evaluations"] for st in stats]))
+        kp_k = wl["keypoints"] // 1000
+        last_st = stats[-1]
+        out = {
+            "metric": METRIC,
+            "value": all_kept / elapsed,
+            "unit": "keypoints/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": frame_s * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (ray-cast facet scene, seeded; 3dfeaturematcher_amd/synth.py)",
+            "config": {
+                "workload": (f"C5: one {kp_k}k-keypoint SIFT-128 (u8) frame pair ({wl['width']}x{wl['height']}, "
+                             f"sub-pixel keypoints) per step, full pipeline, pixelsRay {args.ray}, pyramids "
+                             f"{args.levels}, query blocks over {world} GPUs, RCCL all-gather of survivor records"),
+                "keypoints_per_frame": wl["keypoints"], "width": wl["width"], "height": wl["height"],
+                "pixelsRay": args.ray, "pyramids": args.levels,
+                "parallelism": (f"dp{world}: one process per GPU (torchrun), 4,096-query blocks of one frame pair "
+                                f"dealt round-robin over the ranks, frame B + images replicated, RCCL all-gather "
+                                f"of counts + 64-B survivor records every step ({backend})"),
+                "mode": (f"stream: {nf} frame pairs in flight per rank, {nl} per LM launch (fm3d_pipeline_submit / "
+                         f"wait / link)"),
+                "timed": ("per step on every rank, from host memory to host memory: its query share's H2D (pinned), "
+                          "pyramids, match -> NNDR -> DLT -> LM -> records, D2H, the all-gather; barrier + "
+                          "synchronize on both sides, max over ranks"),
+            },
+            "latency_ms": {"mean": float(np.mean(lat)), "max": float(np.max(lat)),
+                           "note": "rank 0, per frame pair, submit call -> its gathered records"},
+            "input_keypoints_per_s": wl["keypoints"] / frame_s,
+            "roofline": {
+                "kernel": "fm3d::lm2_kernel on every rank's GPU, launches overlapped",
+                "bound": "fp64-valu",
+                "achieved": FLOPS_PER_PIXEL_EVAL * pix_local / frame_s / 1e12,
+                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": FLOPS_PER_PIXEL_EVAL * pix_local / frame_s / 1e12 / FP64_PEAK_TFLOPS,
+                "traffic": None,
+                "algorithmic": (f"{FLOPS_PER_PIXEL_EVAL} flop x rank 0's {pix_local:.4g} pixel evaluations per frame "
+                                f"pair / the wall time per step, against one GPU's peak"),
+                "avg_launch_ms": frame_s * 1e3,
+            },
+            "cpu_baseline": None,
+            "stages_ms": {k: last_st[k] for k in ("match_ms", "lm_ms", "total_ms", "pyramid_ms")},
+            "counts_rank0": {k: last_st[k] for k in ("queries", "matches", "inliers", "kept")},
+            "kept_per_frame_pair": int(len(merged)),
+            "setup_s": {"synthetic_generation": round(t_gen, 2)},
+        }
+        out.update(verify_against_fixture(args, wl, "c5", pair, merged))
+        if args.dump_records:
+            np.save(args.dump_records, merged)
+        emit(out, args)
+    tdist.barrier()
+    tdist.destroy_process_group()
 
 
 def run_resident(args, workload):

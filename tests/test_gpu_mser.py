@@ -81,6 +81,22 @@ def test_mser_vga_bitwise(fm3d, orc, synth, seed):
     _same_regions(r, orc.mser_regions(img))
 
 
+def test_mser_large_image_hbm_bitmap(fm3d, orc):
+    """an image past the LDS bitmap (kMserLdsBits = 983,040 pixels): the visited bits in HBM"""
+    img = _blurred(1000, 1024, 3.0, 9)
+    kw = dict(min_area=30, max_area=20000)
+    ctx, _ = _ctx(fm3d)
+    try:
+        F = fm3d.Features(ctx)
+        r = F.mser_regions(img, **kw)
+        k = F.mser(img, **kw)
+    finally:
+        ctx.close()
+    _same_regions(r, orc.mser_regions(img, **kw))
+    _same_kpts(k, orc.mser_detect(img, **kw))
+    assert len(r) > 50
+
+
 def test_mser_settings_through_detect(fm3d, orc, synth):
     """DetectorType MSER with the nine MSERDetector keys (the last four do not steer grey images)"""
     img = synth.make_frame_pair(1500, seed=75).img2

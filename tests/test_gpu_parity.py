@@ -1157,3 +1157,42 @@ def test_bench_gpus_more_than_visible_exits_nonzero():
     assert r.returncode != 0
     assert f"--gpus {n}" in r.stderr and "visible" in r.stderr
     assert '"metric"' not in r.stdout
+
+
+@pytest.mark.timeout(500)
+def test_bench_torchrun_stream_two_ranks_one_gpu(fm3d, synth, tmp_path):
+    """bench.py's torchrun route (one process per GPU, frame pairs in flight, all-gather of every
+    step's records, rank-0 merge) with two ranks on this one GPU and a gloo all-gather
+    (FM3D_BENCH_BACKEND / FM3D_BENCH_SHARE_DEVICE): the merged records of the last step equal one
+    fm3d_pipeline_run of the whole frame pair, byte for byte."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dump = tmp_path / "merged.npy"
+    env = dict(os.environ, FM3D_BENCH_BACKEND="gloo", FM3D_BENCH_SHARE_DEVICE="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29631", os.path.join(root, "bench.py"), "--gpus", "2", "--workload", "c5",
+           "--keypoints", "30000", "--steps", "3", "--warmup", "1", "--dump-records", str(dump)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
+    merged = np.load(dump)
+    # the same frame pair whole, one run
+    pair = synth.make_frame_pair(30000, 640, 480, seed=7, desc="sift")
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon, s.pixelsRay, s.pyramids = 0.55, 64, 3
+    ctx = fm3d.Context(s)
+    try:
+        fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+        k, st = pipe.run()
+        ref = pipe.records(k)
+    finally:
+        ctx.close()
+    assert len(merged) == k > 1000
+    assert merged.tobytes() == ref.tobytes()
