@@ -77,10 +77,10 @@ __device__ __forceinline__ bool ncc_geometry(const NccParams& p, double ux, doub
     return good;
 }
 
-// getBilinearInterpPix32f on the gathered window (bilinear(): the same operations); lo / hi: the two
-// bytes at off and off + w
-typedef __attribute__((aligned(1))) const uint16_t u16u;
-__device__ __forceinline__ float ncc_bilinear(unsigned lo, unsigned hi, float x, float y) {
+// getBilinearInterpPix32f on the gathered window (bilinear(): the same operations)
+__device__ __forceinline__ float ncc_bilinear(const uint8_t* img, unsigned off, int w, float x, float y) {
+    typedef __attribute__((aligned(1))) const uint16_t u16u;
+    const unsigned lo = *(u16u*)(img + off), hi = *(u16u*)(img + off + w);
     const float x0 = floorf(x), y0 = floorf(y);
     const float b00 = (float)(lo & 0xff), b01 = (float)(lo >> 8);
     const float b10 = (float)(hi & 0xff), b11 = (float)(hi >> 8);
@@ -183,33 +183,17 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
                 const double a = (double)A1[t];
                 Sa += a;
                 Saa += a * a;
-                // the live hypotheses' geometry first, then all their gathers together (a failed
-                // pixel gathers the image's first bytes), then the samples and sums: no branch between
-                // a gather and the next hypothesis' geometry, so the gathers overlap.  A hypothesis
-                // whose pixel fails is dead (score -2), so what its sums take in does not matter.
-                float fx[KPW], fy[KPW];
-                unsigned off[KPW];
-                bool good[KPW];
 #pragma unroll
                 for (int k = 0; k < KPW; k++) {
-                    good[k] = false;
-                    off[k] = 0u;
-                    fx[k] = fy[k] = 0.f;
-                    if (k < nk && !((dead >> k) & 1))  // wave-uniform
-                        good[k] = ncc_geometry(p, ux, uy, n0[k], n1[k], n2[k], mm[k], mok[k], cm, xmaxb, ymaxb, fx[k],
-                                               fy[k], off[k]);
-                }
-                unsigned lo[KPW], hi[KPW];
-#pragma unroll
-                for (int k = 0; k < KPW; k++) {
-                    lo[k] = *(u16u*)(p.img2 + off[k]);
-                    hi[k] = *(u16u*)(p.img2 + off[k] + p.w);
-                }
-#pragma unroll
-                for (int k = 0; k < KPW; k++) {
-                    if (k >= nk || ((dead >> k) & 1)) continue;  // wave-uniform
-                    if (!good[k]) badNow |= 1u << k;
-                    const double b = (double)ncc_bilinear(lo[k], hi[k], fx[k], fy[k]);
+                    if (k >= nk) break;
+                    if ((dead >> k) & 1) continue;  // wave-uniform
+                    float fx, fy;
+                    unsigned off;
+                    if (!ncc_geometry(p, ux, uy, n0[k], n1[k], n2[k], mm[k], mok[k], cm, xmaxb, ymaxb, fx, fy, off)) {
+                        badNow |= 1u << k;
+                        continue;
+                    }
+                    const double b = (double)ncc_bilinear(p.img2, off, p.w, fx, fy);
                     Sb[k] += b;
                     Sbb[k] += b * b;
                     Sab[k] += a * b;
