@@ -965,6 +965,17 @@ def run_c3(args):
         verified = bool(np.array_equal(pts, opts) and np.array_equal(sc, rs) and np.array_equal(best, rb) and
                         np.array_equal(nb, rn, equal_nan=True))
     ncc_ms = float(np.mean([x["lm_ms"] for x in stats]))
+    # HBM bytes and VALU busy of ncc_kernel from the committed rocprofv3 PMC passes of this command
+    # (tools/r04_final_prof.sh -> profiles/r04_pmc_c3.json), when they are for the same workload
+    pmc = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "r04_pmc_c3.json")) as f:
+            d = json.load(f)
+        w = d.get("workload", {})
+        if (w.get("keypoints"), w.get("ray")) == (wl["keypoints"], ray):
+            pmc = d
+    except (OSError, ValueError):
+        pass
     m_dat = sum(1 for i in range(-ray, ray + 1) for j in range(-ray, ray + 1) if i * i + j * j <= ray * ray)
     pix = P * 16 * m_dat
     achieved = FLOPS_PER_PIXEL_EVAL * pix / (ncc_ms * 1e-3) / 1e12 if ncc_ms > 0 else 0.0
@@ -982,7 +993,12 @@ def run_c3(args):
                    "timed": "match -> NNDR -> DLT -> NCC scoring on HBM-resident inputs (scores stay on the device)"},
         "roofline": {"kernel": "fm3d::ncc_kernel (NCC over candidate normals)", "bound": "fp64-valu",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved / FP64_PEAK_TFLOPS,
+                     "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                     "traffic_source": "profiles/r04_pmc_c3.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
+                                       if pmc else None,
+                     "valu_busy_per_simd": pmc.get("valu_busy_per_simd") if pmc else None,
+                     "l2_hit": pmc.get("l2_hit") if pmc else None,
                      "algorithmic": f"{FLOPS_PER_PIXEL_EVAL} flop per pixel evaluation (the LM's count for the "
                                     f"same geometry + bilinear sample) x {P} points x 16 hypotheses x {m_dat} "
                                     f"neighbourhood pixels (image-bounded pixels count too)",
