@@ -631,7 +631,10 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
     if (ang < -180) ang = __fadd_rn(ang, 360.f);
     if (ang > 360) ang = __fsub_rn(ang, 360.f);
     const float diam = sqrtf(bh * bw);
-    const int rx = (int)rintf(bx), ry = (int)rintf(by);
+    // Rect::contains(Point(cvRound(cx), cvRound(cy))): cvRound of a NaN, an infinity or a value past
+    // the int range is INT_MIN (SSE2), never inside; compared as floats (v_cvt_i32 would give 0 for NaN)
+    const float rxf = rintf(bx), ryf = rintf(by);
+    const bool inside = rxf >= 0.f && rxf < (float)L.w && ryf >= 0.f && ryf < (float)L.h;
     fm3d_keypoint k;
     k.x = bx;
     k.y = by;
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
     k.class_id = -1;
     if (lane != 0) return;
     kp[r] = k;
-    flag[r] = diam > FLT_EPSILON && rx >= 0 && rx < L.w && ry >= 0 && ry < L.h;
+    flag[r] = diam > FLT_EPSILON && inside;
     if (boxOut) {
         boxOut[5 * r + 0] = bx;
         boxOut[5 * r + 1] = by;

@@ -610,9 +610,14 @@ int orc_mser_detect(const uint8_t *img, int w, int h, int delta, int minArea, in
         }
         off += count[i];
         diam = sqrtf(box[3] * box[2]);
-        rx = (int)rintf(box[0]);
-        ry = (int)rintf(box[1]);
-        if (diam > FLT_EPSILON && rx >= 0 && rx < w && ry >= 0 && ry < h) {
+        /* Rect::contains(Point(cvRound(cx), cvRound(cy))): cvRound of a NaN, an infinity or a value
+         * past the int range is INT_MIN (SSE2 conversion), never inside; compared as floats here */
+        {
+            const float fx = rintf(box[0]), fy = rintf(box[1]);
+            rx = fx >= 0.f && fx < (float)w;
+            ry = fy >= 0.f && fy < (float)h;
+        }
+        if (diam > FLT_EPSILON && rx && ry) {
             if (nk < cap) {
                 kp[nk].x = box[0];
                 kp[nk].y = box[1];

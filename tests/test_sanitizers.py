@@ -16,7 +16,7 @@ NATIVE = os.path.join(ROOT, "tests", "native")
 @pytest.fixture(scope="module")
 def build_dir(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("san"))
-    targets = [f"{out}/san_oracle", f"{out}/san_star", f"{out}/san_parse"]
+    targets = [f"{out}/san_oracle", f"{out}/san_star", f"{out}/san_mser", f"{out}/san_parse"]
     csrc = os.path.join(ROOT, "3dfeaturematcher_amd", "csrc", "_build")
     if all(os.path.exists(os.path.join(csrc, f"{k}.hip.o")) for k in ("fm3d_match", "fm3d_misc", "fm3d_lm2", "fm3d_patch")):
         targets.append(f"{out}/san_host")
@@ -42,6 +42,10 @@ def test_oracle_under_asan_ubsan(build_dir):
 
 def test_star_oracle_under_asan_ubsan(build_dir):
     assert "san_star: ok" in _run(f"{build_dir}/san_star")
+
+
+def test_mser_oracle_under_asan_ubsan(build_dir):
+    assert "san_mser: ok" in _run(f"{build_dir}/san_mser")
 
 
 def test_settings_and_pgm_parsers_malformed_inputs(build_dir, tmp_path):
