@@ -121,7 +121,7 @@ struct fm3d_ctx {
     DevBuf brImg, brSum, brKp, brIdx, brPat, brPairs, brDesc;
     // FREAK description (frLut: the whole default pattern, uploaded once)
     DevBuf frImg, frSum, frKp, frScale, frLut, frOp, frPairs, frAng, frDesc;
-    DevBuf msImg, msWork, msHeap, msNode, msHist, msReg, msCnt, msOff, msXY, msScr, msKp, msFlag, msPos, msOut;
+    DevBuf msImg, msWork, msHeap, msNode, msHist, msReg, msCnt, msOff, msXY, msScr, msKp, msFlag, msPos, msOut, msRank;
     std::vector<int> freakUserPairs;  // fm3d_freak_set_pairs (empty: FM3D_FREAK_DEF_PAIRS)
     // STAR detection
     DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut, starWork;
@@ -1666,7 +1666,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->starR, &c->starZ, &c->starKp, &c->starFlag, &c->starPos, &c->starOut, &c->starWork,
                       &c->nccS, &c->nccN, &c->nccB, &c->pcnt, &c->frImg, &c->frSum, &c->frKp, &c->frScale,
                       &c->frLut, &c->frOp, &c->frPairs, &c->frAng, &c->frDesc, &c->msImg, &c->msWork,
-                      &c->msHeap, &c->msNode, &c->msHist, &c->msReg, &c->msCnt, &c->msOff, &c->msXY, &c->msScr,
+                      &c->msHeap, &c->msNode, &c->msHist, &c->msReg, &c->msCnt, &c->msOff, &c->msXY, &c->msScr, &c->msRank,
                       &c->msKp, &c->msFlag, &c->msPos, &c->msOut};
     for (DevBuf* b : bufs) b->release();
     HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall};
@@ -3363,7 +3363,7 @@ int mser_flood(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserPa
     if ((long long)w * h >= (1LL << 28) - 1 || w > 65535 || h > 65535)
         return fail(c, FM3D_ERR_INVALID, "MSER: image too large");
     L = fm3d::mser_layout(w, h);
-    HIPCHK(c, c->msImg.ensure((size_t)w * h));
+    HIPCHK(c, c->msImg.ensure(((size_t)w * h + 3) & ~(size_t)3));  // read as dwords by the flood
     HIPCHK(c, c->msWork.ensure(L.visInLds ? 16 : (size_t)2 * L.visWords * sizeof(unsigned)));
     HIPCHK(c, c->msHeap.ensure((size_t)2 * L.heapEntries * sizeof(int2)));
     HIPCHK(c, c->msNode.ensure((size_t)2 * L.nodes * sizeof(int2)));
@@ -3396,7 +3396,7 @@ int mser_flood(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserPa
     return FM3D_OK;
 }
 
-// the region points (walked from the node lists) and each region's fitEllipse keypoint + kept flag
+// the region points (gathered from the ranked node lists) and each region's fitEllipse keypoint + kept flag
 int mser_fit(fm3d_ctx* c, const fm3d::MserLayout& L, const std::vector<int4>& regs, int n0,
              const std::vector<long long>& off) {
     const int n = (int)regs.size();
@@ -3409,7 +3409,9 @@ int mser_fit(fm3d_ctx* c, const fm3d::MserLayout& L, const std::vector<int4>& re
     HIPCHK(c, c->msFlag.ensure((size_t)(n + 1) * sizeof(int)));
     HIPCHK(c, hipMemcpyAsync(c->msOff.p, off.data(), (size_t)(n + 1) * sizeof(long long), hipMemcpyHostToDevice,
                              c->stream));
-    fm3d::launch_mser_fit(c->msReg.as<int4>(), L.regCap, n0, n, c->msNode.as<int2>(), L.nodes,
+    HIPCHK(c, c->msRank.ensure(fm3d::mser_rank_bytes(L.nodes)));
+    const fm3d::MserRank K = fm3d::launch_mser_rank(c->msNode.as<int2>(), L.nodes, c->msRank.as<int>(), c->stream);
+    fm3d::launch_mser_fit(c->msReg.as<int4>(), L.regCap, n0, n, K, L.nodes,
                           c->msOff.as<long long>(), L, c->msXY.as<int2>(), c->msScr.as<double>(),
                           c->msKp.as<fm3d_keypoint>(), c->msFlag.as<int>(), nullptr, c->stream);
     HIPCHK(c, hipGetLastError());
@@ -3485,7 +3487,7 @@ int fm3d_mser_regions(fm3d_ctx* c, const uint8_t* img, int w, int h, int delta, 
     const fm3d::MserParams P = mser_params(delta, minArea, maxArea, maxVariation, minDiversity);
     if ((r = mser_flood(c, img, w, h, P, L, regs, n0, off))) return r;
     const int n = (int)regs.size();
-    if ((r = mser_fit(c, L, regs, n0, off))) return r;  // walks the lists into msXY
+    if ((r = mser_fit(c, L, regs, n0, off))) return r;  // gathers the region points into msXY
     const long long tot = off[n];
     for (int i = 0; i < n && i < cap; i++) {
         color[i] = regs[i].x;

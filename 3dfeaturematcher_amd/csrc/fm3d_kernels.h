@@ -400,10 +400,18 @@ MserLayout mser_layout(int w, int h);
 // reg[pass * regCap + r] = {colour, head node, point count, 0}; nreg[pass] = regions (all, even past regCap)
 void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, unsigned* vis, int2* heap,
                        int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s);
-// fitEllipse per region (one lane each): region r of the concatenated list (pass 0's n0 then pass 1's),
-// its points at off[r] in xy (walked from the node list) and 5 * count doubles of scratch at 5 * off[r];
-// kp[r] = KeyPoint(centre, sqrt(w h)), flag[r] = kept (diameter > FLT_EPSILON, rounded centre inside)
-void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const int2* node, long long nodes,
+// the point lists of both passes ranked (list ranking): node g = pass * nodes + i sits at
+// pts[base[last[g]] + rank[g]] (its list's points stored backwards from the end); work: mser_rank_bytes
+struct MserRank {
+    const int *rank, *last, *base, *pts;
+};
+size_t mser_rank_bytes(long long nodes);
+MserRank launch_mser_rank(const int2* node, long long nodes, int* work, hipStream_t s);
+// fitEllipse per region (one wave each): region r of the concatenated list (pass 0's n0 then pass 1's),
+// its points at off[r] in xy (gathered from the ranked lists) and 5 * count doubles of scratch at
+// 5 * off[r]; kp[r] = KeyPoint(centre, sqrt(w h)), flag[r] = kept (diameter > FLT_EPSILON, rounded
+// centre inside)
+void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const MserRank& K, long long nodes,
                      const long long* off, const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag,
                      float* box, hipStream_t s);
 

@@ -82,7 +82,8 @@ __device__ __forceinline__ void new_history(Comp& c, MserHist* hist, int hi) {
 
 // MSERMergeComp(top, below, below, history): the larger keeps its history (the top one on a tie);
 // its point list comes first
-__device__ __forceinline__ void merge(const Comp& top, Comp& below, MserHist* hist, int2* node, int hi) {
+// the link of the winner's tail to the other list (tail, head) is returned in `link` (x = -1: none)
+__device__ __forceinline__ void merge(const Comp& top, Comp& below, MserHist* hist, int2& link, int hi) {
     const bool topWins = top.size >= below.size;
     const Comp win = topWins ? top : below, lose = topWins ? below : top;
     MserHist r;
@@ -102,7 +103,7 @@ __device__ __forceinline__ void merge(const Comp& top, Comp& below, MserHist* hi
     r.val = win.level;
     r.size = win.size;
     hist[hi] = r;
-    if (top.size > 0 && below.size > 0) node[win.tail].x = lose.head;
+    link = (top.size > 0 && below.size > 0) ? make_int2(win.tail, lose.head) : make_int2(-1, 0);
     Comp m;
     m.level = below.level;
     m.var = win.var;
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     unsigned* vis = LDSVIS ? visLds : visAll + (size_t)pass * L.visWords;
     __shared__ int hcur[256];
     __shared__ int lsize[256];
-    __shared__ int2 topE[256];
+    __shared__ int2 topE[257];  // [256]: the no-refill sink
     __shared__ Comp comp[257];
     for (int i = tid; i < 256; i += kMserThreads) lsize[i] = 0;
     for (long long i = tid; i < L.visWords; i += kMserThreads) vis[i] = 0u;
@@ -192,7 +193,15 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     int nnode = 0, nhist = 0, nr = 0;
     // the current pixel
     int p = 0, x = 0, y = 0, dir = 0;
-    int v = (int)(src[0] ^ inv);
+    // grey values through the scalar cache (the image read as aligned dwords; the buffer is padded):
+    // scalar loads count in lgkmcnt, so they do not wait for the lane's earlier vector stores
+    const unsigned* __restrict__ src4 = (const unsigned*)src;
+    auto grey = [&](int q) -> int {
+        const int qs = __builtin_amdgcn_readfirstlane(q);
+        const unsigned wd = src4[qs >> 2];
+        return (int)(((wd >> ((qs & 3) << 3)) & 255u) ^ inv);
+    };
+    int v = grey(0);
     vis[0] |= 1u;
     // the stack: comp[1 .. top - 1] in LDS, the top one in T; comp[0] the 256 sentinel
     int top = 1;
@@ -201,31 +210,42 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     comp_init(T);
     T.level = v;
     int belowLevel = 256;  // comp[top - 1].level
-    // a pop's bucket refill in flight: topE[pendB] = pendE once it has arrived
-    int pendB = -1;
+    // a pop's bucket refill in flight: topE[pendB] = pendE once it has arrived (256: none)
+    int pendB = 256;
     int2 pendE = make_int2(0, 0);
     for (;;) {
         // --- the remaining neighbours of p, from direction dir (right, down, left, up) ---
         int np[4], nv[4];
-        bool cand[4];
+        bool in[4];
 #pragma unroll
         for (int d = 0; d < 4; d++) {
             const int nx = x + (d == 0 ? 1 : d == 2 ? -1 : 0), ny = y + (d == 1 ? 1 : d == 3 ? -1 : 0);
-            const bool in = d >= dir && nx >= 0 && nx < w && ny >= 0 && ny < h;
-            np[d] = in ? p + (d == 0 ? 1 : d == 1 ? w : d == 2 ? -1 : -w) : p;
-            cand[d] = in && !((vis[np[d] >> 5] >> (np[d] & 31)) & 1u);
+            in[d] = (d >= dir) & (nx >= 0) & (nx < w) & (ny >= 0) & (ny < h);
+            np[d] = in[d] ? p + (d == 0 ? 1 : d == 1 ? w : d == 2 ? -1 : -w) : p;
         }
+        // one batch of loads, used unconditionally (none is sunk into a branch)
+        unsigned vw[4], gw[4];
 #pragma unroll
-        for (int d = 0; d < 4; d++) nv[d] = (int)(src[np[d]] ^ inv);  // issued together
-        if (pendB >= 0) {  // the previous pop's refill (issued before these loads)
-            topE[pendB] = pendE;
-            pendB = -1;
-        }
+        for (int d = 0; d < 4; d++) gw[d] = src4[__builtin_amdgcn_readfirstlane(np[d]) >> 2];
+#pragma unroll
+        for (int d = 0; d < 4; d++) vw[d] = vis[np[d] >> 5];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < 4; d++) nv[d] = (int)(((gw[d] >> ((np[d] & 3) << 3)) & 255u) ^ inv);
+        bool cand[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) cand[d] = in[d] & !((vw[d] >> (np[d] & 31)) & 1u);
+        topE[pendB] = pendE;  // the previous pop's refill (issued before these loads; branch-free)
+        pendB = 256;
         int descend = -1;
 #pragma unroll
         for (int d = 0; d < 4; d++) {
             if (descend >= 0 || !cand[d]) continue;
-            vis[np[d] >> 5] |= 1u << (np[d] & 31);
+            if (LDSVIS)  // no wait: LDS operations complete in order
+                __hip_atomic_fetch_or(&vis[np[d] >> 5], 1u << (np[d] & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                vis[np[d] >> 5] |= 1u << (np[d] & 31);
             const int nx = x + (d == 0 ? 1 : d == 2 ? -1 : 0), ny = y + (d == 1 ? 1 : d == 3 ? -1 : 0);
             if (nv[d] < v) {
                 descend = d;
@@ -300,7 +320,9 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
                 for (;;) {
                     top--;
                     Comp B = comp[top];
-                    merge(T, B, hist, node, nhist++);
+                    int2 link;
+                    merge(T, B, hist, link, nhist++);
+                    if (link.x >= 0) node[link.x].x = link.y;
                     T = B;
                     belowLevel = comp[top - 1].level;
                     if (pv <= T.level) break;
@@ -320,6 +342,118 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     nreg[pass] = nr;
 }
 
+// ---------------------------------------------------------------- the point lists, ranked
+// After the floods every region is a run of some node list (a node's successor changes only while it
+// is its list's tail).  Wyllie's list ranking puts every node of both passes (global index
+// pass * N + node) at base[end of its list] + (its distance to that end), so a region's points are
+// one contiguous, backwards run and fitEllipse reads them in parallel instead of walking the list.
+__global__ void mser_rank_init_kernel(const int2* __restrict__ node, int N, int* jump, int* rank, int* last,
+                                      int* len, int* pred) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * N) return;
+    const int s = node[i].x;
+    const int g = s >= 0 ? s + (i >= N ? N : 0) : -1;
+    jump[i] = g;
+    rank[i] = g >= 0 ? 1 : 0;
+    last[i] = g >= 0 ? g : i;
+    len[i] = 0;
+    pred[i] = 0;
+}
+
+// pred[j] = 1 for every node with a predecessor (a node has at most one)
+__global__ void mser_rank_pred_kernel(const int* __restrict__ jump, int* pred, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && jump[i] >= 0) pred[jump[i]] = 1;
+}
+
+__global__ void mser_rank_round_kernel(const int* __restrict__ jIn, const int* __restrict__ rIn,
+                                       const int* __restrict__ lIn, int* jOut, int* rOut, int* lOut, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int j = jIn[i];
+    if (j >= 0) {
+        rOut[i] = rIn[i] + rIn[j];
+        lOut[i] = lIn[j];
+        jOut[i] = jIn[j];
+    } else {
+        rOut[i] = rIn[i];
+        lOut[i] = lIn[i];
+        jOut[i] = -1;
+    }
+}
+
+// each list's length, written at its end by its head
+__global__ void mser_rank_len_kernel(const int* __restrict__ rank, const int* __restrict__ last,
+                                     const int* __restrict__ pred, int* len, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && !pred[i]) len[last[i]] = rank[i] + 1;
+}
+
+constexpr int kRankScan = 1024;  // items per scan block (256 threads x 4)
+
+__device__ __forceinline__ int block_excl_scan256(int v, int* sh, int& total) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const int a = t >= o ? sh[t - o] : 0;
+        __syncthreads();
+        sh[t] += a;
+        __syncthreads();
+    }
+    total = sh[255];
+    const int r = sh[t] - v;
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(256) void mser_scan_sums_kernel(const int* __restrict__ v, int n, int* sums) {
+    __shared__ int sh[256];
+    const int b = blockIdx.x * kRankScan + threadIdx.x * 4;
+    int c = 0;
+    for (int k = 0; k < 4; k++) c += b + k < n ? v[b + k] : 0;
+    int tot;
+    block_excl_scan256(c, sh, tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void mser_scan_top_kernel(int* sums, int nb) {
+    __shared__ int sh[256];
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += 256) {
+        const int i = b0 + threadIdx.x;
+        const int c = i < nb ? sums[i] : 0;
+        int tot;
+        const int e = block_excl_scan256(c, sh, tot);
+        if (i < nb) sums[i] = carry + e;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void mser_scan_out_kernel(const int* __restrict__ v, int n,
+                                                            const int* __restrict__ sums, int* out) {
+    __shared__ int sh[256];
+    const int b = blockIdx.x * kRankScan + threadIdx.x * 4;
+    int f[4], c = 0;
+    for (int k = 0; k < 4; k++) {
+        f[k] = b + k < n ? v[b + k] : 0;
+        c += f[k];
+    }
+    int tot;
+    int o = sums[blockIdx.x] + block_excl_scan256(c, sh, tot);
+    for (int k = 0; k < 4; k++) {
+        if (b + k < n) out[b + k] = o;
+        o += f[k];
+    }
+}
+
+__global__ void mser_rank_scatter_kernel(const int2* __restrict__ node, const int* __restrict__ rank,
+                                         const int* __restrict__ last, const int* __restrict__ base, int* pts,
+                                         int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) pts[base[last[i]] + rank[i]] = node[i].y;
+}
+
 // lane l's double, on every lane (two v_readlane: the index is wave-uniform)
 __device__ __forceinline__ double lane_get(double v, int l) {
     const long long b = __double_as_longlong(v);
@@ -328,17 +462,58 @@ __device__ __forceinline__ double lane_get(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// s + t[0] + t[1] + ... + t[cnt - 1] in that order (t[l] on lane l), on every lane
-__device__ __forceinline__ double seq_add(double s, double t, int cnt) {
-    for (int l = 0; l < cnt; l++) s += lane_get(t, l);
+// s + t[0] + t[1] + ... + t[cnt - 1] in that order (t[l] on lane l), on every lane: the terms go
+// through LDS (buf: 64 doubles of the wave's own) and every lane reads them back two at a time
+// (broadcast), so a term costs half a read and one add instead of two v_readlane and an add
+__device__ __forceinline__ double seq_add(double s, double t, int cnt, double* buf) {
+    buf[threadIdx.x & 63] = t;
+    const double2* b2 = (const double2*)buf;
+    int l = 0;
+    for (; l + 16 <= cnt; l += 16) {  // 8 reads in flight, then 16 adds
+        double2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = b2[(l >> 1) + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            s += v[j].x;
+            s += v[j].y;
+        }
+    }
+    for (; l < cnt; l++) s += buf[l];
+    __builtin_amdgcn_wave_barrier();  // every lane's reads before the next chunk's writes
     return s;
+}
+
+// the two sums s0 += t0[l], s1 += t1[l] interleaved, each in lane order (buf: 128 doubles)
+__device__ __forceinline__ void seq_add2(double& s0, double& s1, double t0, double t1, int cnt, double* buf) {
+    const int lane = threadIdx.x & 63;
+    buf[2 * lane] = t0;
+    buf[2 * lane + 1] = t1;
+    const double2* b2 = (const double2*)buf;
+    int l = 0;
+    for (; l + 8 <= cnt; l += 8) {
+        double2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = b2[l + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            s0 += v[j].x;
+            s1 += v[j].y;
+        }
+    }
+    for (; l < cnt; l++) {
+        const double2 v = b2[l];
+        s0 += v.x;
+        s1 += v.y;
+    }
+    __builtin_amdgcn_wave_barrier();
 }
 
 // cv::solve(A, b, DECOMP_SVD) with At = A^T (n rows of m), b constant (bval): JacobiSVDImpl_ +
 // SVBkSbImpl_ by one wave.  The element-wise steps run lane-parallel (lane l takes k = l, l + 64,
 // ...); every sum runs over k in order, its terms computed by the lanes and added one by one
 // (seq_add), so each sum has the scalar loop's bits.  Every lane holds W, Vt and x.
-__device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x) {
+__device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x, double* buf) {
     const int lane = threadIdx.x & 63;
     double W[5], Vt[25];
     const double eps = DBL_EPSILON * 10;
@@ -347,7 +522,7 @@ __device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x)
         for (int base = 0; base < m; base += 64) {
             const int k = base + lane;
             const double t = k < m ? At[i * m + k] : 0.;
-            sd = seq_add(sd, t * t, min(64, m - base));
+            sd = seq_add(sd, t * t, min(64, m - base), buf);
         }
         W[i] = sd;
         for (int k = 0; k < n; k++) Vt[i * n + k] = 0;
@@ -364,7 +539,7 @@ __device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x)
                 for (int base = 0; base < m; base += 64) {
                     const int k = base + lane;
                     const double t = k < m ? Ai[k] * Aj[k] : 0.;
-                    pp = seq_add(pp, t, min(64, m - base));
+                    pp = seq_add(pp, t, min(64, m - base), buf);
                 }
                 if (fabs(pp) <= eps * sqrt(a * bb)) continue;
                 pp *= 2;
@@ -390,11 +565,7 @@ __device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x)
                         Aj[k] = t1;
                     }
                     const double q0 = t0 * t0, q1 = t1 * t1;
-                    const int cnt = min(64, m - base);
-                    for (int l = 0; l < cnt; l++) {  // the two sums interleaved, each in k order
-                        a += lane_get(q0, l);
-                        bb += lane_get(q1, l);
-                    }
+                    seq_add2(a, bb, q0, q1, min(64, m - base), buf);  // interleaved, each in k order
                 }
                 W[i] = a;
                 W[j] = bb;
@@ -413,7 +584,7 @@ __device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x)
         for (int base = 0; base < m; base += 64) {
             const int k = base + lane;
             const double t = k < m ? At[i * m + k] : 0.;
-            sd = seq_add(sd, t * t, min(64, m - base));
+            sd = seq_add(sd, t * t, min(64, m - base), buf);
         }
         W[i] = sqrt(sd);
     }
@@ -453,7 +624,7 @@ __device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x)
         for (int base = 0; base < m; base += 64) {
             const int k = base + lane;
             const double t = k < m ? At[i * m + k] * bval : 0.;
-            s = seq_add(s, t, min(64, m - base));
+            s = seq_add(s, t, min(64, m - base), buf);
         }
         s *= wi;
         for (int k = 0; k < n; k++) x[k] = x[k] + s * Vt[i * n + k];
@@ -461,23 +632,23 @@ __device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x)
 }
 
 __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ reg, long long regCap, int n0, int n,
-                                                      const int2* __restrict__ nodeAll, long long nodes,
-                                                      const long long* __restrict__ off, MserLayout L, int2* xyAll,
-                                                      double* scratch, fm3d_keypoint* kp, int* flag, float* boxOut) {
+                                                      MserRank K, long long nodes, const long long* __restrict__ off,
+                                                      MserLayout L, int2* xyAll, double* scratch, fm3d_keypoint* kp,
+                                                      int* flag, float* boxOut) {
     const int r = blockIdx.x, lane = threadIdx.x;  // one wave per region
+    __shared__ double sbuf[128];                   // the sequential sums' terms
     if (r >= n) return;
     const int pass = r < n0 ? 0 : 1;
     const int4 R = reg[pass * regCap + (pass ? r - n0 : r)];
-    const int2* node = nodeAll + pass * nodes;
     const int m = R.z;
     int2* xy = xyAll + off[r];
     double* At = scratch + 5 * off[r];
-    if (lane == 0) {  // the region's list: one dependent walk
-        int q = R.y;
-        for (int k = 0; k < m; k++) {
-            const int2 nd = node[q];
-            xy[k] = make_int2(nd.y & 0xffff, (int)((unsigned)nd.y >> 16));
-            q = nd.x;
+    {  // the region's first m list points: a run of its list, stored backwards from the head's slot
+        const long long g = R.y + pass * nodes;
+        const long long start = (long long)K.base[K.last[g]] + K.rank[g];
+        for (int k = lane; k < m; k += 64) {
+            const int q = K.pts[start - k];
+            xy[k] = make_int2(q & 0xffff, (int)((unsigned)q >> 16));
         }
     }
     __threadfence_block();
@@ -503,7 +674,7 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
         At[4 * m + k] = py;
     }
     double gfp[5], rp[5];
-    svd_solve_wave(At, m, 5, 10000.0, gfp);
+    svd_solve_wave(At, m, 5, 10000.0, gfp, sbuf);
     {
         double A2[4], x2[2];
         A2[0] = 2 * gfp[0];
@@ -608,7 +779,7 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
         At[2 * m + k] = ((double)px - rp[0]) * ((double)py - rp[1]);
     }
     double g[3];
-    svd_solve_wave(At, m, 3, 1.0, g);
+    svd_solve_wave(At, m, 3, 1.0, g, sbuf);
     const double min_eps = 1e-6;
     rp[4] = -0.5 * fm3d_atan2(g[2], g[1] - g[0]);
     double t = fm3d_sin(-2.0 * rp[4]);
@@ -669,11 +840,44 @@ void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams
     }
 }
 
-void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const int2* node, long long nodes,
+size_t mser_rank_bytes(long long nodes) { return (size_t)(10 * 2 * nodes + (2 * nodes + kRankScan) / kRankScan + 8) * 4; }
+
+MserRank launch_mser_rank(const int2* node, long long nodes, int* work, hipStream_t s) {
+    const int n = (int)(2 * nodes), N = (int)nodes;
+    int* jr[2][3] = {{work, work + n, work + 2 * n}, {work + 3 * n, work + 4 * n, work + 5 * n}};
+    int* len = work + 6 * n;
+    int* base = work + 7 * n;
+    int* pts = work + 8 * n;
+    int* pred = work + 9 * n;
+    int* sums = work + 10 * n;
+    const int g = (n + 255) / 256;
+    mser_rank_init_kernel<<<g, 256, 0, s>>>(node, N, jr[0][0], jr[0][1], jr[0][2], len, pred);
+    mser_rank_pred_kernel<<<g, 256, 0, s>>>(jr[0][0], pred, n);
+    int cur = 0;
+    for (long long span = 1; span < nodes; span <<= 1) {  // ceil(log2 N) doublings reach every list's end
+        mser_rank_round_kernel<<<g, 256, 0, s>>>(jr[cur][0], jr[cur][1], jr[cur][2], jr[cur ^ 1][0], jr[cur ^ 1][1],
+                                                 jr[cur ^ 1][2], n);
+        cur ^= 1;
+    }
+    mser_rank_len_kernel<<<g, 256, 0, s>>>(jr[cur][1], jr[cur][2], pred, len, n);
+    const int nb = (n + kRankScan - 1) / kRankScan;
+    mser_scan_sums_kernel<<<nb, 256, 0, s>>>(len, n, sums);
+    mser_scan_top_kernel<<<1, 256, 0, s>>>(sums, nb);
+    mser_scan_out_kernel<<<nb, 256, 0, s>>>(len, n, sums, base);
+    mser_rank_scatter_kernel<<<g, 256, 0, s>>>(node, jr[cur][1], jr[cur][2], base, pts, n);
+    MserRank K;
+    K.rank = jr[cur][1];
+    K.last = jr[cur][2];
+    K.base = base;
+    K.pts = pts;
+    return K;
+}
+
+void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const MserRank& K, long long nodes,
                      const long long* off, const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag,
                      float* box, hipStream_t s) {
     if (n <= 0) return;
-    mser_fit_kernel<<<n, 64, 0, s>>>(reg, regCap, n0, n, node, nodes, off, L, xy, scratch, kp, flag, box);
+    mser_fit_kernel<<<n, 64, 0, s>>>(reg, regCap, n0, n, K, nodes, off, L, xy, scratch, kp, flag, box);
 }
 
 }  // namespace fm3d
