@@ -121,7 +121,8 @@ struct fm3d_ctx {
     DevBuf brImg, brSum, brKp, brIdx, brPat, brPairs, brDesc;
     // FREAK description (frLut: the whole default pattern, uploaded once)
     DevBuf frImg, frSum, frKp, frScale, frLut, frOp, frPairs, frAng, frDesc;
-    DevBuf msImg, msWork, msHeap, msNode, msHist, msReg, msCnt, msOff, msXY, msScr, msKp, msFlag, msPos, msOut, msRank;
+    DevBuf msImg, msWork, msHeap, msNode, msHist, msReg, msCnt, msOff, msXY, msScr, msKp, msFlag, msPos, msOut, msRank,
+        msPad;
     std::vector<int> freakUserPairs;  // fm3d_freak_set_pairs (empty: FM3D_FREAK_DEF_PAIRS)
     // STAR detection
     DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut, starWork;
@@ -1667,7 +1668,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->nccS, &c->nccN, &c->nccB, &c->pcnt, &c->frImg, &c->frSum, &c->frKp, &c->frScale,
                       &c->frLut, &c->frOp, &c->frPairs, &c->frAng, &c->frDesc, &c->msImg, &c->msWork,
                       &c->msHeap, &c->msNode, &c->msHist, &c->msReg, &c->msCnt, &c->msOff, &c->msXY, &c->msScr, &c->msRank,
-                      &c->msKp, &c->msFlag, &c->msPos, &c->msOut};
+                      &c->msKp, &c->msFlag, &c->msPos, &c->msOut, &c->msPad};
     for (DevBuf* b : bufs) b->release();
     HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall};
     for (HostBuf* b : hbufs) b->release();
@@ -3360,10 +3361,11 @@ int freak_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keyp
 int mser_flood(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserParams& P, fm3d::MserLayout& L,
                std::vector<int4>& regs, int& n0, std::vector<long long>& off) {
     if (w <= 0 || h <= 0) return fail(c, FM3D_ERR_INVALID, "MSER: empty image");
-    if ((long long)w * h >= (1LL << 28) - 1 || w > 65535 || h > 65535)
+    if ((long long)(w + 2) * (h + 2) >= (1LL << 28) - 1 || w > 65535 || h > 65535)
         return fail(c, FM3D_ERR_INVALID, "MSER: image too large");
     L = fm3d::mser_layout(w, h);
-    HIPCHK(c, c->msImg.ensure(((size_t)w * h + 3) & ~(size_t)3));  // read as dwords by the flood
+    HIPCHK(c, c->msImg.ensure((size_t)w * h));
+    HIPCHK(c, c->msPad.ensure((size_t)2 * L.padBytes));
     HIPCHK(c, c->msWork.ensure(L.visInLds ? 16 : (size_t)2 * L.visWords * sizeof(unsigned)));
     HIPCHK(c, c->msHeap.ensure((size_t)2 * L.heapEntries * sizeof(int2)));
     HIPCHK(c, c->msNode.ensure((size_t)2 * L.nodes * sizeof(int2)));
@@ -3371,7 +3373,8 @@ int mser_flood(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserPa
     HIPCHK(c, c->msReg.ensure((size_t)2 * L.regCap * sizeof(int4)));
     HIPCHK(c, c->msCnt.ensure(2 * sizeof(int)));
     HIPCHK(c, hipMemcpyAsync(c->msImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
-    fm3d::launch_mser_flood(c->msImg.as<uint8_t>(), L, P, c->msWork.as<unsigned>(), c->msHeap.as<int2>(),
+    fm3d::launch_mser_flood(c->msImg.as<uint8_t>(), L, P, c->msPad.as<uint8_t>(), c->msWork.as<unsigned>(),
+                            c->msHeap.as<int2>(),
                             c->msNode.as<int2>(), c->msHist.as<fm3d::MserHist>(), c->msReg.as<int4>(),
                             c->msCnt.as<int>(), c->stream);
     HIPCHK(c, hipGetLastError());

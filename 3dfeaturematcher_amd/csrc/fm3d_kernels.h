@@ -387,9 +387,11 @@ struct MserHist {  // MSERGrowHistory by index
 // the workspace of one pass over a w x h image (both passes: twice, pass-major)
 struct MserLayout {
     int w, h;
-    int visInLds;        // the visited bitmap in LDS (w * h <= kMserLdsBits), else in HBM
-    long long visWords;  // ceil(w * h / 32)
-    long long heapEntries;  // w * h + 256: {pixel + 1 | direction << 28, x | y << 16}
+    int pw;              // the padded width w + 2 (the flood works on the (w + 2) x (h + 2) grid)
+    int visInLds;        // the visited bitmap in LDS ((w + 2)(h + 2) <= kMserLdsBits), else in HBM
+    long long visWords;  // ceil((w + 2)(h + 2) / 32)
+    long long padBytes;  // one pass's padded grey image, rounded up to whole dwords
+    long long heapEntries;  // w * h + 256: {padded pixel + 1 | direction << 28, x | y << 16}
     long long nodes;     // w * h: {next node, x | y << 16}
     long long hists;     // 2 w h + 2 (a bound: one per raise and per merge)
     long long regCap;    // region records per pass
@@ -398,8 +400,9 @@ constexpr long long kMserLdsBits = 120 * 1024 * 8;
 MserLayout mser_layout(int w, int h);
 // both flood passes, one workgroup each (pass 0 on 255 - I, colour -1; pass 1 on I, colour +1):
 // reg[pass * regCap + r] = {colour, head node, point count, 0}; nreg[pass] = regions (all, even past regCap)
-void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, unsigned* vis, int2* heap,
-                       int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s);
+// pad: 2 * padBytes of scratch (each pass's grey values on the padded grid, pass 0 inverted)
+void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, uint8_t* pad, unsigned* vis,
+                       int2* heap, int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s);
 // the point lists of both passes ranked (list ranking): node g = pass * nodes + i sits at
 // pts[base[last[g]] + rank[g]] (its list's points stored backwards from the end); work: mser_rank_bytes
 struct MserRank {

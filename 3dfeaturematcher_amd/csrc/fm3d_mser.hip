@@ -36,9 +36,11 @@ MserLayout mser_layout(int w, int h) {
     MserLayout L;
     L.w = w;
     L.h = h;
-    const long long N = (long long)w * h;
-    L.visInLds = N <= kMserLdsBits;
-    L.visWords = (N + 31) / 32;
+    const long long N = (long long)w * h, NP = (long long)(w + 2) * (h + 2);
+    L.pw = w + 2;
+    L.visInLds = NP <= kMserLdsBits;
+    L.visWords = (NP + 31) / 32;
+    L.padBytes = (NP + 3) & ~3LL;
     L.heapEntries = N + 256;
     L.nodes = N;
     L.hists = 2 * N + 2;
@@ -146,13 +148,33 @@ __device__ __forceinline__ bool stable_check(Comp& c, MserHist* hist, const Mser
 }
 
 // one bucket entry: {pixel + 1 | next direction << 28, x | y << 16}; {0, 0} is a bucket's base
-__device__ __forceinline__ int2 mser_entry(int p, int x, int y, int dir) {
-    return make_int2((p + 1) | (dir << 28), x | (y << 16));
+__device__ __forceinline__ int2 mser_entry(unsigned q, int x, int y, int dir) {
+    return make_int2((int)(q + 1) | (dir << 28), x | (y << 16));
+}
+
+// each pass's grey values on the padded (w + 2) x (h + 2) grid (pass 0: 255 - I), border 0; the flood
+// never reads a border value (the border is marked visited), it only needs no bounds tests
+__global__ void mser_pad_kernel(const uint8_t* __restrict__ src, MserLayout L, uint8_t* pad) {
+    const long long NP = (long long)L.pw * (L.h + 2);
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * L.padBytes) return;
+    const int pass = i >= L.padBytes;
+    const long long q = i - pass * L.padBytes;
+    uint8_t v = 0;
+    if (q < NP) {
+        const int px = (int)(q % L.pw) - 1, py = (int)(q / L.pw) - 1;
+        if (px >= 0 && px < L.w && py >= 0 && py < L.h) {
+            const uint8_t g = src[(size_t)py * L.w + px];
+            v = pass == 0 ? (uint8_t)(255 - g) : g;
+        }
+    }
+    pad[i] = v;
 }
 
 template <bool LDSVIS>
 __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t* __restrict__ src, MserLayout L,
-                                                                   MserParams P, unsigned* visAll, int2* heapAll,
+                                                                   MserParams P, const uint8_t* __restrict__ padAll,
+                                                                   unsigned* visAll, int2* heapAll,
                                                                    int2* nodeAll, MserHist* histAll, int4* regAll,
                                                                    int* nreg) {
     const int pass = blockIdx.x, tid = threadIdx.x;
@@ -171,6 +193,11 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     for (int i = tid; i < 256; i += kMserThreads) lsize[i] = 0;
     for (long long i = tid; i < L.visWords; i += kMserThreads) vis[i] = 0u;
     __syncthreads();
+    const unsigned W = (unsigned)L.pw, H = (unsigned)(h + 2);
+    for (unsigned i = tid; i < 2 * W + 2 * (H - 2); i += kMserThreads) {  // the border: visited
+        const unsigned q = i < W ? i : i < 2 * W ? (H - 1) * W + (i - W) : ((i - 2 * W) / 2 + 1) * W + ((i & 1) ? W - 1 : 0);
+        atomicOr(&vis[q >> 5], 1u << (q & 31));
+    }
     // preprocessMSER_8UC1's level histogram (pass 0 floods 255 - I, pass 1 I)
     for (int i = tid; i < N; i += kMserThreads) {
         const int g = src[i];
@@ -189,20 +216,15 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     }
     const int color = pass == 0 ? -1 : 1;
     const long long regCap = L.regCap;
-    const unsigned inv = pass == 0 ? 255u : 0u;  // value = g ^ inv (255 - g for pass 0)
     int nnode = 0, nhist = 0, nr = 0;
-    // the current pixel
-    int p = 0, x = 0, y = 0, dir = 0;
-    // grey values through the scalar cache (the image read as aligned dwords; the buffer is padded):
-    // scalar loads count in lgkmcnt, so they do not wait for the lane's earlier vector stores
-    const unsigned* __restrict__ src4 = (const unsigned*)src;
-    auto grey = [&](int q) -> int {
-        const int qs = __builtin_amdgcn_readfirstlane(q);
-        const unsigned wd = src4[qs >> 2];
-        return (int)(((wd >> ((qs & 3) << 3)) & 255u) ^ inv);
-    };
-    int v = grey(0);
-    vis[0] |= 1u;
+    // the current pixel: q on the padded grid, (x, y) in the image
+    unsigned q = W + 1;
+    int x = 0, y = 0, dir = 0;
+    // grey values through the scalar cache (the padded image read as aligned dwords): scalar loads
+    // count in lgkmcnt, so they do not wait for the lane's earlier vector stores
+    const unsigned* __restrict__ pad4 = (const unsigned*)(padAll + (size_t)pass * L.padBytes);
+    int v = (int)((pad4[q >> 2] >> ((q & 3) << 3)) & 255u);
+    vis[q >> 5] |= 1u << (q & 31);
     // the stack: comp[1 .. top - 1] in LDS, the top one in T; comp[0] the 256 sentinel
     int top = 1;
     comp[0].level = 256;
@@ -215,23 +237,26 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     int2 pendE = make_int2(0, 0);
     for (;;) {
         // --- the remaining neighbours of p, from direction dir (right, down, left, up) ---
-        int np[4], nv[4];
+        unsigned np[4];
+        int nv[4];
         bool in[4];
 #pragma unroll
         for (int d = 0; d < 4; d++) {
-            const int nx = x + (d == 0 ? 1 : d == 2 ? -1 : 0), ny = y + (d == 1 ? 1 : d == 3 ? -1 : 0);
-            in[d] = (d >= dir) & (nx >= 0) & (nx < w) & (ny >= 0) & (ny < h);
-            np[d] = in[d] ? p + (d == 0 ? 1 : d == 1 ? w : d == 2 ? -1 : -w) : p;
+            in[d] = d >= dir;  // the padded border is visited: no bounds tests
+            np[d] = d == 0 ? q + 1 : d == 1 ? q + W : d == 2 ? q - 1 : q - W;
         }
         // one batch of loads, used unconditionally (none is sunk into a branch)
         unsigned vw[4], gw[4];
 #pragma unroll
-        for (int d = 0; d < 4; d++) gw[d] = src4[__builtin_amdgcn_readfirstlane(np[d]) >> 2];
+        for (int d = 0; d < 4; d++) {  // a 32-bit byte offset from the pass's base (the SGPR-offset form)
+            const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(np[d] & ~3u));
+            gw[d] = *(const unsigned*)((const uint8_t*)pad4 + off);
+        }
 #pragma unroll
         for (int d = 0; d < 4; d++) vw[d] = vis[np[d] >> 5];
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int d = 0; d < 4; d++) nv[d] = (int)(((gw[d] >> ((np[d] & 3) << 3)) & 255u) ^ inv);
+        for (int d = 0; d < 4; d++) nv[d] = (int)((gw[d] >> ((np[d] & 3) << 3)) & 255u);
         bool cand[4];
 #pragma unroll
         for (int d = 0; d < 4; d++) cand[d] = in[d] & !((vw[d] >> (np[d] & 31)) & 1u);
@@ -261,12 +286,12 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
             // push p back (resuming after `descend`) and open a component at the neighbour's level
             const int d = descend;
             const int t = ++hcur[v];
-            const int2 e = mser_entry(p, x, y, d + 1);
+            const int2 e = mser_entry(q, x, y, d + 1);
             heap[t] = e;
             topE[v] = e;
             x += d == 0 ? 1 : d == 2 ? -1 : 0;
             y += d == 1 ? 1 : d == 3 ? -1 : 0;
-            p = np[d];
+            q = np[d];
             v = nv[d];
             dir = 0;
             comp[top] = T;
@@ -303,7 +328,7 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
             pendE = heap[t];  // the bucket's next top, consumed after the neighbour loads
             pendB = pv;
         }
-        p = (e.x & 0x0fffffff) - 1;
+        q = (unsigned)(e.x & 0x0fffffff) - 1u;
         dir = (int)((unsigned)e.x >> 28);
         x = e.y & 0xffff;
         y = (int)((unsigned)e.y >> 16);
@@ -828,15 +853,16 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
 
 }  // namespace
 
-void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, unsigned* vis, int2* heap,
-                       int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s) {
+void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, uint8_t* pad, unsigned* vis,
+                       int2* heap, int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s) {
+    mser_pad_kernel<<<(unsigned)((2 * L.padBytes + 255) / 256), 256, 0, s>>>(img, L, pad);
     if (L.visInLds) {
         const size_t lds = (size_t)L.visWords * sizeof(unsigned);
         hipFuncSetAttribute((const void*)mser_flood_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-        mser_flood_kernel<true><<<2, kMserThreads, lds, s>>>(img, L, P, vis, heap, node, hist, reg, nreg);
+        mser_flood_kernel<true><<<2, kMserThreads, lds, s>>>(img, L, P, pad, vis, heap, node, hist, reg, nreg);
     } else {
-        mser_flood_kernel<false><<<2, kMserThreads, 0, s>>>(img, L, P, vis, heap, node, hist, reg, nreg);
+        mser_flood_kernel<false><<<2, kMserThreads, 0, s>>>(img, L, P, pad, vis, heap, node, hist, reg, nreg);
     }
 }
 
