@@ -148,6 +148,10 @@ __device__ __forceinline__ bool stable_check(Comp& c, MserHist* hist, const Mser
 }
 
 // one bucket entry: {pixel + 1 | next direction << 28, x | y << 16}; {0, 0} is a bucket's base
+// element i of an 8-byte array through a 32-bit byte offset (the SGPR-base + VGPR-offset address
+// form: no 64-bit address arithmetic; every index here is below 2^28)
+__device__ __forceinline__ int2& at8(int2* base, int i) { return *(int2*)((uint8_t*)base + ((unsigned)i << 3)); }
+
 __device__ __forceinline__ int2 mser_entry(unsigned q, int x, int y, int dir) {
     return make_int2((int)(q + 1) | (dir << 28), x | (y << 16));
 }
@@ -266,28 +270,33 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
 #pragma unroll
         for (int d = 0; d < 4; d++) {
             if (descend >= 0 || !cand[d]) continue;
-            if (LDSVIS)  // no wait: LDS operations complete in order
-                __hip_atomic_fetch_or(&vis[np[d] >> 5], 1u << (np[d] & 31), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-                vis[np[d] >> 5] |= 1u << (np[d] & 31);
+            {  // the visited bit: a plain store of the word read above (no wait); a later neighbour
+               // in the same word stores the word with both bits
+                const unsigned nw = vw[d] | (1u << (np[d] & 31));
+#pragma unroll
+                for (int d2 = d + 1; d2 < 4; d2++)
+                    if ((np[d2] >> 5) == (np[d] >> 5)) vw[d2] = nw;
+                vis[np[d] >> 5] = nw;
+            }
             const int nx = x + (d == 0 ? 1 : d == 2 ? -1 : 0), ny = y + (d == 1 ? 1 : d == 3 ? -1 : 0);
             if (nv[d] < v) {
                 descend = d;
             } else {
                 const int b = nv[d];
-                const int t = ++hcur[b];
+                const int t = hcur[b] + 1;
+                hcur[b] = t;
                 const int2 e = mser_entry(np[d], nx, ny, 0);
-                heap[t] = e;
+                at8(heap, t) = e;
                 topE[b] = e;
             }
         }
         if (descend >= 0) {
             // push p back (resuming after `descend`) and open a component at the neighbour's level
             const int d = descend;
-            const int t = ++hcur[v];
+            const int t = hcur[v] + 1;
+            hcur[v] = t;
             const int2 e = mser_entry(q, x, y, d + 1);
-            heap[t] = e;
+            at8(heap, t) = e;
             topE[v] = e;
             x += d == 0 ? 1 : d == 2 ? -1 : 0;
             y += d == 1 ? 1 : d == 3 ? -1 : 0;
@@ -302,9 +311,9 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
             continue;
         }
         // accumulateMSERComp: the finished pixel joins the top component's list
-        node[nnode] = make_int2(-1, x | (y << 16));
+        at8(node, nnode) = make_int2(-1, x | (y << 16));
         if (T.size > 0)
-            node[T.tail].x = nnode;
+            at8(node, T.tail).x = nnode;
         else
             T.head = nnode;
         T.tail = nnode;
@@ -324,8 +333,9 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
             e = topE[pv];
         }
         {
-            const int t = --hcur[pv];
-            pendE = heap[t];  // the bucket's next top, consumed after the neighbour loads
+            const int t = hcur[pv] - 1;
+            hcur[pv] = t;
+            pendE = at8(heap, t);  // the bucket's next top, consumed after the neighbour loads
             pendB = pv;
         }
         q = (unsigned)(e.x & 0x0fffffff) - 1u;
@@ -347,7 +357,7 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
                     Comp B = comp[top];
                     int2 link;
                     merge(T, B, hist, link, nhist++);
-                    if (link.x >= 0) node[link.x].x = link.y;
+                    if (link.x >= 0) at8(node, link.x).x = link.y;
                     T = B;
                     belowLevel = comp[top - 1].level;
                     if (pv <= T.level) break;
