@@ -43,7 +43,7 @@ EXPORTS = (
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
     "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link", "fm3d_freak_compute", "fm3d_freak_set_pairs",
-    "fm3d_mser_detect", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt", "fm3d_pipeline_wait_dlt",
+    "fm3d_mser_detect", "fm3d_mser_detect_batch", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt", "fm3d_pipeline_wait_dlt",
 )
 
 
@@ -592,6 +592,30 @@ class Features:
             if n.value <= cap:
                 return k[:n.value]
             cap = n.value
+
+    def mser_batch(self, images, delta: int = 5, min_area: int = 60, max_area: int = 14400,
+                   max_variation: float = 0.25, min_diversity: float = 0.2):
+        """mser() on several images of one size in one call (fm3d_mser_detect_batch: every image's floods
+        side by side): a list of KEYPOINT arrays, each equal to mser(image)"""
+        imgs = np.ascontiguousarray(np.stack([np.asarray(i, dtype=np.uint8) for i in images]))
+        count, h, w = imgs.shape
+        cap = 4096 * count
+        counts = np.zeros(count, np.int32)
+        while True:
+            k = np.zeros(cap, dtype=KEYPOINT)
+            tot = ctypes.c_int(0)
+            self.ctx.check(lib().fm3d_mser_detect_batch(
+                self.ctx.handle, _ptr(imgs, ctypes.c_uint8), count, w, h, delta, min_area, max_area,
+                ctypes.c_double(max_variation), ctypes.c_double(min_diversity), _vp(k), cap,
+                _ptr(counts, ctypes.c_int32), ctypes.byref(tot)))
+            if tot.value <= cap:
+                break
+            cap = tot.value
+        out, off = [], 0
+        for c in counts:
+            out.append(k[off:off + int(c)].copy())
+            off += int(c)
+        return out
 
     def mser_regions(self, image: np.ndarray, delta: int = 5, min_area: int = 60, max_area: int = 14400,
                      max_variation: float = 0.25, min_diversity: float = 0.2):

@@ -122,7 +122,7 @@ struct fm3d_ctx {
     // FREAK description (frLut: the whole default pattern, uploaded once)
     DevBuf frImg, frSum, frKp, frScale, frLut, frOp, frPairs, frAng, frDesc;
     DevBuf msImg, msWork, msHeap, msNode, msHist, msReg, msCnt, msOff, msXY, msScr, msKp, msFlag, msPos, msOut, msRank,
-        msPad;
+        msPad, msRegC;
     std::vector<int> freakUserPairs;  // fm3d_freak_set_pairs (empty: FM3D_FREAK_DEF_PAIRS)
     // STAR detection
     DevBuf starImg, starS, starT, starF, starR, starZ, starKp, starFlag, starPos, starOut, starWork;
@@ -1668,7 +1668,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->nccS, &c->nccN, &c->nccB, &c->pcnt, &c->frImg, &c->frSum, &c->frKp, &c->frScale,
                       &c->frLut, &c->frOp, &c->frPairs, &c->frAng, &c->frDesc, &c->msImg, &c->msWork,
                       &c->msHeap, &c->msNode, &c->msHist, &c->msReg, &c->msCnt, &c->msOff, &c->msXY, &c->msScr, &c->msRank,
-                      &c->msKp, &c->msFlag, &c->msPos, &c->msOut, &c->msPad};
+                      &c->msKp, &c->msFlag, &c->msPos, &c->msOut, &c->msPad, &c->msRegC};
     for (DevBuf* b : bufs) b->release();
     HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall};
     for (HostBuf* b : hbufs) b->release();
@@ -3356,67 +3356,74 @@ int freak_compute(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d_keyp
     return FM3D_OK;
 }
 
-// MSER (fm3d_mser.hip): the two floods, then the regions' records and point offsets.  regs: pass 0's
-// regions then pass 1's ({colour, head node, count, 0}); off: their prefix (points before each).
-int mser_flood(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserParams& P, fm3d::MserLayout& L,
-               std::vector<int4>& regs, int& n0, std::vector<long long>& off) {
-    if (w <= 0 || h <= 0) return fail(c, FM3D_ERR_INVALID, "MSER: empty image");
+// MSER (fm3d_mser.hip): the floods of `count` images (two per image, slot = 2 * image + pass), then the
+// regions' records and point offsets.  regs: every slot's regions in slot order ({colour, head node,
+// count, slot}); off: their prefix (points before each).
+int mser_flood(fm3d_ctx* c, const uint8_t* img, int count, int w, int h, const fm3d::MserParams& P,
+               fm3d::MserLayout& L, std::vector<int4>& regs, std::vector<long long>& off) {
+    if (w <= 0 || h <= 0 || count <= 0) return fail(c, FM3D_ERR_INVALID, "MSER: empty image");
     if ((long long)(w + 2) * (h + 2) >= (1LL << 28) - 1 || w > 65535 || h > 65535)
         return fail(c, FM3D_ERR_INVALID, "MSER: image too large");
+    if ((long long)2 * count * w * h >= (1LL << 30)) return fail(c, FM3D_ERR_INVALID, "MSER: batch too large");
+    const int slots = 2 * count;
     L = fm3d::mser_layout(w, h);
-    HIPCHK(c, c->msImg.ensure((size_t)w * h));
-    HIPCHK(c, c->msPad.ensure((size_t)2 * L.padBytes));
-    HIPCHK(c, c->msWork.ensure(L.visInLds ? 16 : (size_t)2 * L.visWords * sizeof(unsigned)));
-    HIPCHK(c, c->msHeap.ensure((size_t)2 * L.heapEntries * sizeof(int2)));
-    HIPCHK(c, c->msNode.ensure((size_t)2 * L.nodes * sizeof(int2)));
-    HIPCHK(c, c->msHist.ensure((size_t)2 * L.hists * sizeof(fm3d::MserHist)));
-    HIPCHK(c, c->msReg.ensure((size_t)2 * L.regCap * sizeof(int4)));
-    HIPCHK(c, c->msCnt.ensure(2 * sizeof(int)));
-    HIPCHK(c, hipMemcpyAsync(c->msImg.p, img, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
-    fm3d::launch_mser_flood(c->msImg.as<uint8_t>(), L, P, c->msPad.as<uint8_t>(), c->msWork.as<unsigned>(),
-                            c->msHeap.as<int2>(),
-                            c->msNode.as<int2>(), c->msHist.as<fm3d::MserHist>(), c->msReg.as<int4>(),
-                            c->msCnt.as<int>(), c->stream);
+    HIPCHK(c, c->msImg.ensure((size_t)count * w * h));
+    HIPCHK(c, c->msPad.ensure((size_t)slots * L.padBytes));
+    HIPCHK(c, c->msWork.ensure(L.visInLds ? 16 : (size_t)slots * L.visWords * sizeof(unsigned)));
+    HIPCHK(c, c->msHeap.ensure((size_t)slots * L.heapEntries * sizeof(int2)));
+    HIPCHK(c, c->msNode.ensure((size_t)slots * L.nodes * sizeof(int2)));
+    HIPCHK(c, c->msHist.ensure((size_t)slots * L.hists * sizeof(fm3d::MserHist)));
+    HIPCHK(c, c->msReg.ensure((size_t)slots * L.regCap * sizeof(int4)));
+    HIPCHK(c, c->msCnt.ensure((size_t)slots * sizeof(int)));
+    HIPCHK(c, hipMemcpyAsync(c->msImg.p, img, (size_t)count * w * h, hipMemcpyHostToDevice, c->stream));
+    fm3d::launch_mser_flood(c->msImg.as<uint8_t>(), count, L, P, c->msPad.as<uint8_t>(), c->msWork.as<unsigned>(),
+                            c->msHeap.as<int2>(), c->msNode.as<int2>(), c->msHist.as<fm3d::MserHist>(),
+                            c->msReg.as<int4>(), c->msCnt.as<int>(), c->stream);
     HIPCHK(c, hipGetLastError());
-    int cnt[2] = {0, 0};
-    HIPCHK(c, hipMemcpyAsync(cnt, c->msCnt.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    std::vector<int> cnt(slots, 0);
+    HIPCHK(c, hipMemcpyAsync(cnt.data(), c->msCnt.p, (size_t)slots * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (cnt[0] < 0 || cnt[1] < 0 || cnt[0] > L.regCap || cnt[1] > L.regCap)
-        return fail(c, FM3D_ERR_HIP, "MSER: region count out of range");
-    n0 = cnt[0];
-    regs.resize((size_t)cnt[0] + cnt[1]);
-    if (cnt[0])
-        HIPCHK(c, hipMemcpyAsync(regs.data(), c->msReg.p, (size_t)cnt[0] * sizeof(int4), hipMemcpyDeviceToHost, c->stream));
-    if (cnt[1])
-        HIPCHK(c, hipMemcpyAsync(regs.data() + cnt[0], c->msReg.as<int4>() + L.regCap, (size_t)cnt[1] * sizeof(int4),
-                                 hipMemcpyDeviceToHost, c->stream));
+    long long total = 0;
+    for (int k = 0; k < slots; k++) {
+        if (cnt[k] < 0 || cnt[k] > L.regCap) return fail(c, FM3D_ERR_HIP, "MSER: region count out of range");
+        total += cnt[k];
+    }
+    regs.resize((size_t)total);
+    for (int k = 0, at = 0; k < slots; at += cnt[k], k++)
+        if (cnt[k])
+            HIPCHK(c, hipMemcpyAsync(regs.data() + at, c->msReg.as<int4>() + (size_t)k * L.regCap,
+                                     (size_t)cnt[k] * sizeof(int4), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     off.assign(regs.size() + 1, 0);
-    for (size_t i = 0; i < regs.size(); i++) {
-        if (regs[i].z <= 0 || regs[i].z > (long long)w * h) return fail(c, FM3D_ERR_HIP, "MSER: bad region size");
-        off[i + 1] = off[i] + regs[i].z;
-    }
+    for (int k = 0, i = 0; k < slots; k++)
+        for (int j = 0; j < cnt[k]; j++, i++) {
+            if (regs[i].z <= 0 || regs[i].z > (long long)w * h) return fail(c, FM3D_ERR_HIP, "MSER: bad region size");
+            regs[i].w = k;
+            off[i + 1] = off[i] + regs[i].z;
+        }
     return FM3D_OK;
 }
 
 // the region points (gathered from the ranked node lists) and each region's fitEllipse keypoint + kept flag
-int mser_fit(fm3d_ctx* c, const fm3d::MserLayout& L, const std::vector<int4>& regs, int n0,
+int mser_fit(fm3d_ctx* c, const fm3d::MserLayout& L, int count, const std::vector<int4>& regs,
              const std::vector<long long>& off) {
     const int n = (int)regs.size();
     if (n == 0) return FM3D_OK;
     const long long tot = off[n];
     HIPCHK(c, c->msOff.ensure((size_t)(n + 1) * sizeof(long long)));
+    HIPCHK(c, c->msRegC.ensure((size_t)n * sizeof(int4)));
     HIPCHK(c, c->msXY.ensure((size_t)tot * sizeof(int2)));
     HIPCHK(c, c->msScr.ensure((size_t)tot * 5 * sizeof(double)));
     HIPCHK(c, c->msKp.ensure((size_t)(n + 1) * sizeof(fm3d_keypoint)));
     HIPCHK(c, c->msFlag.ensure((size_t)(n + 1) * sizeof(int)));
     HIPCHK(c, hipMemcpyAsync(c->msOff.p, off.data(), (size_t)(n + 1) * sizeof(long long), hipMemcpyHostToDevice,
                              c->stream));
-    HIPCHK(c, c->msRank.ensure(fm3d::mser_rank_bytes(L.nodes)));
-    const fm3d::MserRank K = fm3d::launch_mser_rank(c->msNode.as<int2>(), L.nodes, c->msRank.as<int>(), c->stream);
-    fm3d::launch_mser_fit(c->msReg.as<int4>(), L.regCap, n0, n, K, L.nodes,
-                          c->msOff.as<long long>(), L, c->msXY.as<int2>(), c->msScr.as<double>(),
-                          c->msKp.as<fm3d_keypoint>(), c->msFlag.as<int>(), nullptr, c->stream);
+    HIPCHK(c, hipMemcpyAsync(c->msRegC.p, regs.data(), (size_t)n * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->msRank.ensure(fm3d::mser_rank_bytes(L.nodes, 2 * count)));
+    const fm3d::MserRank K =
+        fm3d::launch_mser_rank(c->msNode.as<int2>(), L.nodes, 2 * count, c->msRank.as<int>(), c->stream);
+    fm3d::launch_mser_fit(c->msRegC.as<int4>(), n, K, L.nodes, c->msOff.as<long long>(), L, c->msXY.as<int2>(),
+                          c->msScr.as<double>(), c->msKp.as<fm3d_keypoint>(), c->msFlag.as<int>(), nullptr, c->stream);
     HIPCHK(c, hipGetLastError());
     return FM3D_OK;
 }
@@ -3432,26 +3439,41 @@ fm3d::MserParams mser_params(int delta, int minArea, int maxArea, double maxVari
 }
 
 // MserFeatureDetector::detect: the kept keypoints in region order
-int mser_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, const fm3d::MserParams& P,
-                std::vector<fm3d_keypoint>& k) {
+// MserFeatureDetector::detect on `count` images: the kept keypoints of each image in region order,
+// image after image; per[i] = image i's count
+int mser_detect(fm3d_ctx* c, const uint8_t* img, int count, int w, int h, const fm3d::MserParams& P,
+                std::vector<fm3d_keypoint>& k, std::vector<int>& per) {
     k.clear();
+    per.assign(count, 0);
     fm3d::MserLayout L;
     std::vector<int4> regs;
     std::vector<long long> off;
-    int n0 = 0, r;
-    if ((r = mser_flood(c, img, w, h, P, L, regs, n0, off))) return r;
+    int r;
+    if ((r = mser_flood(c, img, count, w, h, P, L, regs, off))) return r;
     const int n = (int)regs.size();
     for (int i = 0; i < n; i++)
         if (regs[i].z < 5) return fail(c, FM3D_ERR_INVALID, "MSER: a region under 5 points (fitEllipse throws)");
     if (n == 0) return FM3D_OK;
-    if ((r = mser_fit(c, L, regs, n0, off))) return r;
+    if ((r = mser_fit(c, L, count, regs, off))) return r;
     if ((r = ensure_scan_tmp(c, n))) return r;
     HIPCHK(c, c->msPos.ensure((size_t)(n + 1) * sizeof(int)));
     fm3d::launch_exclusive_scan(c->msFlag.as<int>(), n, c->msPos.as<int>(), c->count.as<int>(), c->scanTmp.p, c->stream);
     HIPCHK(c, hipGetLastError());
     int nk = 0;
+    std::vector<int> pos(n);
     HIPCHK(c, hipMemcpyAsync(&nk, c->count.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (count > 1) HIPCHK(c, hipMemcpyAsync(pos.data(), c->msPos.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (count == 1) {
+        per[0] = nk;
+    } else {  // image i's keypoints: the kept regions of slots 2i and 2i + 1
+        std::vector<int> first(count + 1, n);  // image i's first region (n: past the end)
+        for (int i = n - 1; i >= 0; i--) first[regs[i].w >> 1] = i;
+        for (int i = count - 1; i >= 0; i--)
+            if (first[i] == n) first[i] = first[i + 1];  // an image without regions
+        auto at = [&](int f) { return f < n ? pos[f] : nk; };
+        for (int i = 0; i < count; i++) per[i] = at(first[i + 1]) - at(first[i]);
+    }
     if (nk == 0) return FM3D_OK;
     HIPCHK(c, c->msOut.ensure((size_t)nk * sizeof(fm3d_keypoint)));
     fm3d::launch_star_scatter(c->msKp.as<fm3d_keypoint>(), c->msFlag.as<int>(), c->msPos.as<int>(), n,
@@ -3469,10 +3491,30 @@ int fm3d_mser_detect(fm3d_ctx* c, const uint8_t* img, int w, int h, int delta, i
     if (!c || !img || !n || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts)) return FM3D_ERR_INVALID;
     hipSetDevice(c->device);
     std::vector<fm3d_keypoint> k;
+    std::vector<int> per;
     int r;
-    if ((r = mser_detect(c, img, w, h, mser_params(delta, minArea, maxArea, maxVariation, minDiversity), k))) return r;
+    if ((r = mser_detect(c, img, 1, w, h, mser_params(delta, minArea, maxArea, maxVariation, minDiversity), k, per)))
+        return r;
     for (int i = 0; i < (int)k.size() && i < cap; i++) kpts[i] = k[i];
     *n = (int)k.size();
+    return FM3D_OK;
+}
+
+int fm3d_mser_detect_batch(fm3d_ctx* c, const uint8_t* imgs, int count, int w, int h, int delta, int minArea,
+                           int maxArea, double maxVariation, double minDiversity, fm3d_keypoint* kpts, int cap,
+                           int32_t* counts, int* total) {
+    if (!c || !imgs || !counts || !total || count <= 0 || w <= 0 || h <= 0 || cap < 0 || (cap > 0 && !kpts))
+        return FM3D_ERR_INVALID;
+    hipSetDevice(c->device);
+    std::vector<fm3d_keypoint> k;
+    std::vector<int> per;
+    int r;
+    if ((r = mser_detect(c, imgs, count, w, h, mser_params(delta, minArea, maxArea, maxVariation, minDiversity), k,
+                         per)))
+        return r;
+    for (int i = 0; i < (int)k.size() && i < cap; i++) kpts[i] = k[i];
+    for (int i = 0; i < count; i++) counts[i] = per[i];
+    *total = (int)k.size();
     return FM3D_OK;
 }
 
@@ -3486,11 +3528,11 @@ int fm3d_mser_regions(fm3d_ctx* c, const uint8_t* img, int w, int h, int delta, 
     fm3d::MserLayout L;
     std::vector<int4> regs;
     std::vector<long long> off;
-    int n0 = 0, r;
+    int r;
     const fm3d::MserParams P = mser_params(delta, minArea, maxArea, maxVariation, minDiversity);
-    if ((r = mser_flood(c, img, w, h, P, L, regs, n0, off))) return r;
+    if ((r = mser_flood(c, img, 1, w, h, P, L, regs, off))) return r;
     const int n = (int)regs.size();
-    if ((r = mser_fit(c, L, regs, n0, off))) return r;  // gathers the region points into msXY
+    if ((r = mser_fit(c, L, 1, regs, off))) return r;  // gathers the region points into msXY
     const long long tot = off[n];
     for (int i = 0; i < n && i < cap; i++) {
         color[i] = regs[i].x;
@@ -3590,10 +3632,13 @@ int detect_static(fm3d_ctx* c, const uint8_t* img, int w, int h, std::vector<fm3
         return star_detect(c, img, w, h, S.starMaxSize, S.starResponse, S.starLineThreshold, S.starLineBinarized,
                            S.starSuppression, k);
     case FM3D_FEAT_MSER:
-        return mser_detect(c, img, w, h,
+    {
+        std::vector<int> per;
+        return mser_detect(c, img, 1, w, h,
                            mser_params(S.mserDelta, S.mserMinArea, S.mserMaxArea, S.mserMaxVariation,
                                        S.mserMinDiversity),
-                           k);
+                           k, per);
+    }
     default:
         return fail(c, FM3D_ERR_UNSUPPORTED, "the settings' detector type has no GPU implementation");
     }

@@ -398,25 +398,26 @@ struct MserLayout {
 };
 constexpr long long kMserLdsBits = 120 * 1024 * 8;
 MserLayout mser_layout(int w, int h);
-// both flood passes, one workgroup each (pass 0 on 255 - I, colour -1; pass 1 on I, colour +1):
-// reg[pass * regCap + r] = {colour, head node, point count, 0}; nreg[pass] = regions (all, even past regCap)
-// pad: 2 * padBytes of scratch (each pass's grey values on the padded grid, pass 0 inverted)
-void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, uint8_t* pad, unsigned* vis,
-                       int2* heap, int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s);
-// the point lists of both passes ranked (list ranking): node g = pass * nodes + i sits at
+// both flood passes of `count` images of w x h (stored one after the other), one workgroup per slot
+// (slot = 2 * image + pass; pass 0 on 255 - I, colour -1; pass 1 on I, colour +1):
+// reg[slot * regCap + r] = {colour, head node, point count, 0}; nreg[slot] = regions (all, even past
+// regCap); pad: 2 * count * padBytes of scratch (each slot's grey values on the padded grid)
+void launch_mser_flood(const uint8_t* img, int count, const MserLayout& L, const MserParams& P, uint8_t* pad,
+                       unsigned* vis, int2* heap, int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s);
+// the point lists of all slots ranked (list ranking): node g = slot * nodes + i sits at
 // pts[base[last[g]] + rank[g]] (its list's points stored backwards from the end); work: mser_rank_bytes
 struct MserRank {
     const int *rank, *last, *base, *pts;
 };
-size_t mser_rank_bytes(long long nodes);
-MserRank launch_mser_rank(const int2* node, long long nodes, int* work, hipStream_t s);
-// fitEllipse per region (one wave each): region r of the concatenated list (pass 0's n0 then pass 1's),
-// its points at off[r] in xy (gathered from the ranked lists) and 5 * count doubles of scratch at
-// 5 * off[r]; kp[r] = KeyPoint(centre, sqrt(w h)), flag[r] = kept (diameter > FLT_EPSILON, rounded
-// centre inside)
-void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const MserRank& K, long long nodes,
-                     const long long* off, const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag,
-                     float* box, hipStream_t s);
+size_t mser_rank_bytes(long long nodes, int slots);
+MserRank launch_mser_rank(const int2* node, long long nodes, int slots, int* work, hipStream_t s);
+// fitEllipse per region (one wave each): reg[r] = {colour, head node, count, slot} (all slots' regions
+// in slot order), its points at off[r] in xy (gathered from the ranked lists) and 5 * count doubles
+// of scratch at 5 * off[r]; kp[r] = KeyPoint(centre, sqrt(w h)), flag[r] = kept (diameter >
+// FLT_EPSILON, rounded centre inside)
+void launch_mser_fit(const int4* reg, int n, const MserRank& K, long long nodes, const long long* off,
+                     const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag, float* box,
+                     hipStream_t s);
 
 // ---------------------------------------------------------------- BRISK (fm3d_brisk.hip)
 // pat: 60 (x, y, sigma, 0) pattern points per (scale, rotation) in use; pidx: each keypoint's row of pat;

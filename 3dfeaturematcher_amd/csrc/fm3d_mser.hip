@@ -158,17 +158,17 @@ __device__ __forceinline__ int2 mser_entry(unsigned q, int x, int y, int dir) {
 
 // each pass's grey values on the padded (w + 2) x (h + 2) grid (pass 0: 255 - I), border 0; the flood
 // never reads a border value (the border is marked visited), it only needs no bounds tests
-__global__ void mser_pad_kernel(const uint8_t* __restrict__ src, MserLayout L, uint8_t* pad) {
+__global__ void mser_pad_kernel(const uint8_t* __restrict__ src, MserLayout L, int slots, uint8_t* pad) {
     const long long NP = (long long)L.pw * (L.h + 2);
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 2 * L.padBytes) return;
-    const int pass = i >= L.padBytes;
-    const long long q = i - pass * L.padBytes;
+    if (i >= slots * L.padBytes) return;
+    const int slot = (int)(i / L.padBytes), pass = slot & 1;  // slot = 2 * image + pass
+    const long long q = i - slot * L.padBytes;
     uint8_t v = 0;
     if (q < NP) {
         const int px = (int)(q % L.pw) - 1, py = (int)(q / L.pw) - 1;
         if (px >= 0 && px < L.w && py >= 0 && py < L.h) {
-            const uint8_t g = src[(size_t)py * L.w + px];
+            const uint8_t g = src[(size_t)(slot >> 1) * L.w * L.h + (size_t)py * L.w + px];
             v = pass == 0 ? (uint8_t)(255 - g) : g;
         }
     }
@@ -181,15 +181,16 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
                                                                    unsigned* visAll, int2* heapAll,
                                                                    int2* nodeAll, MserHist* histAll, int4* regAll,
                                                                    int* nreg) {
-    const int pass = blockIdx.x, tid = threadIdx.x;
+    const int slot = blockIdx.x, pass = slot & 1, tid = threadIdx.x;  // slot = 2 * image + pass
     const int w = L.w, h = L.h;
     const int N = w * h;
-    int2* heap = heapAll + (size_t)pass * L.heapEntries;
-    int2* node = nodeAll + (size_t)pass * L.nodes;
-    MserHist* hist = histAll + (size_t)pass * L.hists;
-    int4* reg = regAll + (size_t)pass * L.regCap;
+    src += (size_t)(slot >> 1) * N;
+    int2* heap = heapAll + (size_t)slot * L.heapEntries;
+    int2* node = nodeAll + (size_t)slot * L.nodes;
+    MserHist* hist = histAll + (size_t)slot * L.hists;
+    int4* reg = regAll + (size_t)slot * L.regCap;
     extern __shared__ unsigned visLds[];
-    unsigned* vis = LDSVIS ? visLds : visAll + (size_t)pass * L.visWords;
+    unsigned* vis = LDSVIS ? visLds : visAll + (size_t)slot * L.visWords;
     __shared__ int hcur[256];
     __shared__ int lsize[256];
     __shared__ int2 topE[257];  // [256]: the no-refill sink
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     int x = 0, y = 0, dir = 0;
     // grey values through the scalar cache (the padded image read as aligned dwords): scalar loads
     // count in lgkmcnt, so they do not wait for the lane's earlier vector stores
-    const unsigned* __restrict__ pad4 = (const unsigned*)(padAll + (size_t)pass * L.padBytes);
+    const unsigned* __restrict__ pad4 = (const unsigned*)(padAll + (size_t)slot * L.padBytes);
     int v = (int)((pad4[q >> 2] >> ((q & 3) << 3)) & 255u);
     vis[q >> 5] |= 1u << (q & 31);
     // the stack: comp[1 .. top - 1] in LDS, the top one in T; comp[0] the 256 sentinel
@@ -374,20 +375,20 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
             }
         }
     }
-    nreg[pass] = nr;
+    nreg[slot] = nr;
 }
 
 // ---------------------------------------------------------------- the point lists, ranked
 // After the floods every region is a run of some node list (a node's successor changes only while it
-// is its list's tail).  Wyllie's list ranking puts every node of both passes (global index
-// pass * N + node) at base[end of its list] + (its distance to that end), so a region's points are
+// is its list's tail).  Wyllie's list ranking puts every node of every flood (global index
+// slot * N + node) at base[end of its list] + (its distance to that end), so a region's points are
 // one contiguous, backwards run and fitEllipse reads them in parallel instead of walking the list.
-__global__ void mser_rank_init_kernel(const int2* __restrict__ node, int N, int* jump, int* rank, int* last,
+__global__ void mser_rank_init_kernel(const int2* __restrict__ node, int N, int n, int* jump, int* rank, int* last,
                                       int* len, int* pred) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 2 * N) return;
+    if (i >= n) return;
     const int s = node[i].x;
-    const int g = s >= 0 ? s + (i >= N ? N : 0) : -1;
+    const int g = s >= 0 ? s + (i / N) * N : -1;  // the slot's nodes start at slot * N
     jump[i] = g;
     rank[i] = g >= 0 ? 1 : 0;
     last[i] = g >= 0 ? g : i;
@@ -666,20 +667,19 @@ __device__ void svd_solve_wave(double* At, int m, int n, double bval, double* x,
     }
 }
 
-__global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ reg, long long regCap, int n0, int n,
-                                                      MserRank K, long long nodes, const long long* __restrict__ off,
+__global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ reg, int n, MserRank K, long long nodes,
+                                                      const long long* __restrict__ off,
                                                       MserLayout L, int2* xyAll, double* scratch, fm3d_keypoint* kp,
                                                       int* flag, float* boxOut) {
     const int r = blockIdx.x, lane = threadIdx.x;  // one wave per region
     __shared__ double sbuf[128];                   // the sequential sums' terms
     if (r >= n) return;
-    const int pass = r < n0 ? 0 : 1;
-    const int4 R = reg[pass * regCap + (pass ? r - n0 : r)];
+    const int4 R = reg[r];  // {colour, head node, count, slot}
     const int m = R.z;
     int2* xy = xyAll + off[r];
     double* At = scratch + 5 * off[r];
     {  // the region's first m list points: a run of its list, stored backwards from the head's slot
-        const long long g = R.y + pass * nodes;
+        const long long g = R.y + R.w * nodes;
         const long long start = (long long)K.base[K.last[g]] + K.rank[g];
         for (int k = lane; k < m; k += 64) {
             const int q = K.pts[start - k];
@@ -863,23 +863,26 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
 
 }  // namespace
 
-void launch_mser_flood(const uint8_t* img, const MserLayout& L, const MserParams& P, uint8_t* pad, unsigned* vis,
-                       int2* heap, int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s) {
-    mser_pad_kernel<<<(unsigned)((2 * L.padBytes + 255) / 256), 256, 0, s>>>(img, L, pad);
+void launch_mser_flood(const uint8_t* img, int count, const MserLayout& L, const MserParams& P, uint8_t* pad,
+                       unsigned* vis, int2* heap, int2* node, MserHist* hist, int4* reg, int* nreg, hipStream_t s) {
+    const int slots = 2 * count;
+    mser_pad_kernel<<<(unsigned)((slots * L.padBytes + 255) / 256), 256, 0, s>>>(img, L, slots, pad);
     if (L.visInLds) {
         const size_t lds = (size_t)L.visWords * sizeof(unsigned);
-        hipFuncSetAttribute((const void*)mser_flood_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-        mser_flood_kernel<true><<<2, kMserThreads, lds, s>>>(img, L, P, pad, vis, heap, node, hist, reg, nreg);
+        (void)hipFuncSetAttribute((const void*)mser_flood_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        mser_flood_kernel<true><<<slots, kMserThreads, lds, s>>>(img, L, P, pad, vis, heap, node, hist, reg, nreg);
     } else {
-        mser_flood_kernel<false><<<2, kMserThreads, 0, s>>>(img, L, P, pad, vis, heap, node, hist, reg, nreg);
+        mser_flood_kernel<false><<<slots, kMserThreads, 0, s>>>(img, L, P, pad, vis, heap, node, hist, reg, nreg);
     }
 }
 
-size_t mser_rank_bytes(long long nodes) { return (size_t)(10 * 2 * nodes + (2 * nodes + kRankScan) / kRankScan + 8) * 4; }
+size_t mser_rank_bytes(long long nodes, int slots) {
+    return (size_t)(10 * slots * nodes + (slots * nodes + kRankScan) / kRankScan + 8) * 4;
+}
 
-MserRank launch_mser_rank(const int2* node, long long nodes, int* work, hipStream_t s) {
-    const int n = (int)(2 * nodes), N = (int)nodes;
+MserRank launch_mser_rank(const int2* node, long long nodes, int slots, int* work, hipStream_t s) {
+    const int n = (int)(slots * nodes), N = (int)nodes;
     int* jr[2][3] = {{work, work + n, work + 2 * n}, {work + 3 * n, work + 4 * n, work + 5 * n}};
     int* len = work + 6 * n;
     int* base = work + 7 * n;
@@ -887,7 +890,7 @@ MserRank launch_mser_rank(const int2* node, long long nodes, int* work, hipStrea
     int* pred = work + 9 * n;
     int* sums = work + 10 * n;
     const int g = (n + 255) / 256;
-    mser_rank_init_kernel<<<g, 256, 0, s>>>(node, N, jr[0][0], jr[0][1], jr[0][2], len, pred);
+    mser_rank_init_kernel<<<g, 256, 0, s>>>(node, N, n, jr[0][0], jr[0][1], jr[0][2], len, pred);
     mser_rank_pred_kernel<<<g, 256, 0, s>>>(jr[0][0], pred, n);
     int cur = 0;
     for (long long span = 1; span < nodes; span <<= 1) {  // ceil(log2 N) doublings reach every list's end
@@ -909,11 +912,11 @@ MserRank launch_mser_rank(const int2* node, long long nodes, int* work, hipStrea
     return K;
 }
 
-void launch_mser_fit(const int4* reg, long long regCap, int n0, int n, const MserRank& K, long long nodes,
-                     const long long* off, const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag,
-                     float* box, hipStream_t s) {
+void launch_mser_fit(const int4* reg, int n, const MserRank& K, long long nodes, const long long* off,
+                     const MserLayout& L, int2* xy, double* scratch, fm3d_keypoint* kp, int* flag, float* box,
+                     hipStream_t s) {
     if (n <= 0) return;
-    mser_fit_kernel<<<n, 64, 0, s>>>(reg, regCap, n0, n, K, nodes, off, L, xy, scratch, kp, flag, box);
+    mser_fit_kernel<<<n, 64, 0, s>>>(reg, n, K, nodes, off, L, xy, scratch, kp, flag, box);
 }
 
 }  // namespace fm3d

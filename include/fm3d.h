@@ -414,6 +414,14 @@ int fm3d_star_responses(fm3d_ctx *ctx, const uint8_t *img, int width, int height
    lane; fitEllipse runs one lane per region. */
 int fm3d_mser_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int delta, int minArea, int maxArea,
                      double maxVariation, double minDiversity, fm3d_keypoint *kpts, int cap, int *n);
+/* fm3d_mser_detect on `count` images of width x height stored one after the other (the reference's
+   detect(image_a), detect(image_b) of descriptorsmatcher.cpp:77-78 in one call): every image's two
+   floods run side by side (one workgroup each), so a batch takes about the time of one image.  The
+   keypoints of image 0, then image 1, ... (each exactly fm3d_mser_detect's); counts[i] = image i's,
+   *total = all; min(*total, cap) written.  FM3D_ERR_INVALID as fm3d_mser_detect for any image. */
+int fm3d_mser_detect_batch(fm3d_ctx *ctx, const uint8_t *imgs, int count, int width, int height, int delta,
+                           int minArea, int maxArea, double maxVariation, double minDiversity, fm3d_keypoint *kpts,
+                           int cap, int32_t *counts, int *total);
 /* MSER::operator()(img, msers): *nRegions regions, color[i] -1 (pass 1) or +1, count[i] points, the
    points (x, y) concatenated in pts in each region's list order (MSERToContour); *nPoints = all points.
    min(regions, cap) and min(points, ptsCap) written. */

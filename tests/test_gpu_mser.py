@@ -97,6 +97,31 @@ def test_mser_large_image_hbm_bitmap(fm3d, orc):
     assert len(r) > 50
 
 
+def test_mser_batch_equals_single(fm3d, orc, synth):
+    """fm3d_mser_detect_batch: every image's floods side by side; each image's keypoints equal its own
+    fm3d_mser_detect (and the oracle), including an image without regions in the middle"""
+    imgs = [synth.make_frame_pair(2000, seed=71).img1, np.full((480, 640), 90, np.uint8),
+            synth.make_frame_pair(2000, seed=72).img2, _blurred(480, 640, 2.5, 12)]
+    ctx, _ = _ctx(fm3d)
+    try:
+        F = fm3d.Features(ctx)
+        single = [F.mser(i) for i in imgs]
+        batch = F.mser_batch(imgs)
+        small = F.mser_batch([img for img, kw in SMALL[:3] if img.shape == (40, 50)] * 3, min_area=10,
+                             max_area=800)
+    finally:
+        ctx.close()
+    assert len(batch) == len(imgs)
+    for a, b in zip(batch, single):
+        _same_kpts(a, b)
+    assert len(batch[1]) == 0 and len(batch[0]) > 100
+    _same_kpts(batch[2], orc.mser_detect(imgs[2]))
+    want = orc.mser_detect(SMALL[0][0], min_area=10, max_area=800)
+    assert len(small) == 3
+    for k in small:
+        _same_kpts(k, want)
+
+
 def test_mser_settings_through_detect(fm3d, orc, synth):
     """DetectorType MSER with the nine MSERDetector keys (the last four do not steer grey images)"""
     img = synth.make_frame_pair(1500, seed=75).img2
