@@ -321,7 +321,11 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
         T.size++;
         nnode++;
         // the next pixel: this level's bucket, else the next non-empty level
+        // the top entry and the height read together (the compiler barrier keeps the height's load
+        // here instead of merging it with the level-change path's after the branch)
         int2 e = topE[v];
+        int hp = hcur[v];
+        asm volatile("" ::: "memory");
         int pv = v;
         if (!e.x) {
             pv = 0;
@@ -332,9 +336,10 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
                 }
             if (!pv) break;
             e = topE[pv];
+            hp = hcur[pv];
         }
         {
-            const int t = hcur[pv] - 1;
+            const int t = hp - 1;
             hcur[pv] = t;
             pendE = at8(heap, t);  // the bucket's next top, consumed after the neighbour loads
             pendB = pv;
