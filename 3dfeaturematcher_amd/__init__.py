@@ -43,7 +43,8 @@ EXPORTS = (
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
     "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link", "fm3d_freak_compute", "fm3d_freak_set_pairs",
-    "fm3d_mser_detect", "fm3d_mser_detect_batch", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt", "fm3d_pipeline_wait_dlt",
+    "fm3d_mser_detect", "fm3d_mser_detect_batch", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt",
+    "fm3d_pipeline_submit_ncc", "fm3d_pipeline_wait_ncc", "fm3d_pipeline_wait_dlt",
 )
 
 
@@ -942,6 +943,17 @@ class Pipeline:
         st = PipelineStats()
         self.ctx.check(lib().fm3d_pipeline_run_ncc(self.ctx.handle, hphi, htheta, ctypes.c_double(span), ctypes.byref(n),
                                                    ctypes.byref(st)))
+        return n.value, st.as_dict()
+
+    def submit_ncc(self, hphi: int = 4, htheta: int = 4, span: float = 0.4) -> None:
+        """fm3d_pipeline_submit_ncc: C3's path queued on the context stream (returns at once)"""
+        self.ctx.check(lib().fm3d_pipeline_submit_ncc(self.ctx.handle, hphi, htheta, ctypes.c_double(span)))
+
+    def wait_ncc(self):
+        """fm3d_pipeline_wait_ncc: (n_points, stats dict) of the submitted C3 path"""
+        n = ctypes.c_int(0)
+        st = PipelineStats()
+        self.ctx.check(lib().fm3d_pipeline_wait_ncc(self.ctx.handle, ctypes.byref(n), ctypes.byref(st)))
         return n.value, st.as_dict()
 
     def ncc_results(self, n_points: int, H: int):

@@ -154,6 +154,8 @@ struct fm3d_ctx {
     hipEvent_t evLm = nullptr;       // (leader) after a joint LM launch
     fm3d_lm_stats subLm{};         // the pending submit's LM launch data
     bool pendingDlt = false;       // the pending submit is fm3d_pipeline_submit_dlt's front half
+    bool pendingNcc = false;       // the pending submit is fm3d_pipeline_submit_ncc's front half + NCC
+    int nccHPending = 0;           // its hypotheses per point
     fm3d_record* pendOut = nullptr;  // the device records of the pending / last run
     // staged pipeline inputs
     int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
@@ -2195,6 +2197,7 @@ int fm3d_pipeline_wait(fm3d_ctx* c, fm3d_record* out, int cap, int* nKept, fm3d_
     if (!c) return FM3D_ERR_INVALID;
     if (!c->pending) return fail(c, FM3D_ERR_INVALID, "no frame pair submitted (fm3d_pipeline_submit)");
     if (c->pendingDlt) return fail(c, FM3D_ERR_INVALID, "a front half is pending: fm3d_pipeline_wait_dlt");
+    if (c->pendingNcc) return fail(c, FM3D_ERR_INVALID, "an NCC scoring is pending: fm3d_pipeline_wait_ncc");
     hipSetDevice(c->device);
     int r;
     if ((r = flush_member(c))) return r;
@@ -2304,7 +2307,7 @@ int fm3d_pipeline_run_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stats
     return fm3d_pipeline_wait_dlt(c, nInliers, stats);
 }
 
-int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* nPoints, fm3d_pipeline_stats* stats) {
+int fm3d_pipeline_submit_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span) {
     if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
     PENDING_CHECK(c);
     if (Hphi <= 0 || Htheta <= 0 || Hphi * Htheta > 32) return fail(c, FM3D_ERR_INVALID, "1 <= Hphi * Htheta <= 32");
@@ -2353,11 +2356,25 @@ int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* n
     PipeSmall* hs = c->hSmall.as<PipeSmall>();
     HIPCHK(c, hipMemcpyAsync(hs->cnt, c->pcnt.p, sizeof(hs->cnt), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->pending = true;
+    c->pendingNcc = true;
+    c->nccHPending = H;
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_wait_ncc(fm3d_ctx* c, int* nPoints, fm3d_pipeline_stats* stats) {
+    if (!c) return FM3D_ERR_INVALID;
+    if (!c->pendingNcc) return fail(c, FM3D_ERR_INVALID, "no NCC scoring submitted (fm3d_pipeline_submit_ncc)");
+    hipSetDevice(c->device);
+    hipEvent_t* ev = c->ev;
+    c->pending = false;
+    c->pendingNcc = false;
+    HIPCHK(c, hipEventSynchronize(ev[1]));
+    const PipeSmall* hs = c->hSmall.as<PipeSmall>();
     const int K = hs->cnt[0], P = hs->cnt[1];
     c->stK = K;
     c->stP = P;
-    c->nccH = H;
+    c->nccH = c->nccHPending;
     c->nccP = P;  // the score rows fm3d_pipeline_ncc_download returns (set only by a successful run)
     if (nPoints) *nPoints = P;
     if (stats) {
@@ -2380,6 +2397,12 @@ int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* n
         stats->total_ms = ms;
     }
     return FM3D_OK;
+}
+
+int fm3d_pipeline_run_ncc(fm3d_ctx* c, int Hphi, int Htheta, double span, int* nPoints, fm3d_pipeline_stats* stats) {
+    int r;
+    if ((r = fm3d_pipeline_submit_ncc(c, Hphi, Htheta, span))) return r;
+    return fm3d_pipeline_wait_ncc(c, nPoints, stats);
 }
 
 int fm3d_pipeline_ncc_download(fm3d_ctx* c, double* scores, double* normals, int32_t* best) {

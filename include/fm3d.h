@@ -491,6 +491,11 @@ int fm3d_pipeline_dlt_download(fm3d_ctx *ctx, fm3d_dmatch *matches, double *poin
    kernel's time.  Needs the camera-2 pose (fm3d_set_g12).  Results via fm3d_pipeline_ncc_download
    (scores P x H, best normals P x 3, best index P; any may be NULL). */
 int fm3d_pipeline_run_ncc(fm3d_ctx *ctx, int Hphi, int Htheta, double span, int *nPoints, fm3d_pipeline_stats *stats);
+/* fm3d_pipeline_run_ncc split for serving (as fm3d_pipeline_submit_dlt / wait_dlt): submit queues the
+   front half and the NCC scoring on the context stream and returns; wait blocks on the counts' copy
+   and reports as run_ncc.  Until the wait the other pipeline calls on the context fail. */
+int fm3d_pipeline_submit_ncc(fm3d_ctx *ctx, int Hphi, int Htheta, double span);
+int fm3d_pipeline_wait_ncc(fm3d_ctx *ctx, int *nPoints, fm3d_pipeline_stats *stats);
 int fm3d_pipeline_ncc_download(fm3d_ctx *ctx, double *scores, double *normals, int32_t *best);
 /* copy n records from a device record buffer (NULL = internal) to host */
 int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, fm3d_record *out);

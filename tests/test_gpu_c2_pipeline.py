@@ -77,6 +77,45 @@ def test_pipeline_submit_wait_dlt_two_in_flight(fm3d, orc, synth):
             c.close()
 
 
+def test_pipeline_submit_wait_ncc_two_in_flight(fm3d, synth):
+    """fm3d_pipeline_submit_ncc / wait_ncc on two contexts in flight (the C3 serving loop) equal
+    fm3d_pipeline_run_ncc bit for bit; a pending scoring blocks the other pipeline calls and the
+    DLT / full waits"""
+    pair = synth.make_frame_pair(4000, seed=102, desc="orb")
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon = 0.8
+    s.pixelsRay = 16
+    ctxs = [fm3d.Context(s) for _ in range(2)]
+    try:
+        pipes = []
+        for c in ctxs:
+            fm3d.SingleCameraTriangulator(c).set_g12(pair.g12)
+            p = fm3d.Pipeline(c)
+            p.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2, binary=True)
+            pipes.append(p)
+        P0, st0 = pipes[0].run_ncc(4, 4, 0.4)
+        ref = pipes[0].ncc_results(P0, 16)
+        assert P0 > 100
+        for _ in range(3):
+            pipes[0].submit_ncc(4, 4, 0.4)
+            pipes[1].submit_ncc(4, 4, 0.4)
+            with pytest.raises(fm3d.Fm3dError):
+                pipes[0].run_ncc(4, 4, 0.4)
+            with pytest.raises(fm3d.Fm3dError):
+                pipes[1].wait_dlt()
+            for p in pipes:
+                P, st = p.wait_ncc()
+                assert P == P0 and st["matches"] == st0["matches"]
+                for a, b in zip(p.ncc_results(P, 16), ref):
+                    assert np.array_equal(a, b, equal_nan=True)
+        with pytest.raises(fm3d.Fm3dError):
+            pipes[0].wait_ncc()  # nothing pending
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 def test_pipeline_ncc_bitwise(fm3d, orc, synth):
     """BASELINE's C3 as worded through the pipeline (fm3d_pipeline_run_ncc): Hamming match -> NNDR ->
     DLT -> NCC of 4 x 4 normals at pixelsRay 32, every inlier's scores against the oracle on a sample"""
