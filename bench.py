@@ -56,11 +56,13 @@ INT8_PEAK_TOPS = 5000.0      # MI355X dense int8 MFMA (2x the ~2.5 PFLOP/s dense
 
 
 WORKLOAD_DEFAULTS = {
-    "c4": {"ray": 64, "nndr": 0.55, "seed": 7},
-    "c5": {"ray": 64, "nndr": 0.55, "seed": 7},
-    "c2": {"ray": 64, "nndr": 0.55, "seed": 7},
-    # C3's ORB rows: the 0.8 ratio and the 64 x 64 neighbourhood of BASELINE's wording
-    "c3": {"ray": 32, "nndr": 0.8, "seed": 102},
+    "c4": {"ray": 64, "nndr": 0.55, "seed": 7, "inflight": 2},
+    "c5": {"ray": 64, "nndr": 0.55, "seed": 7, "inflight": 2},
+    # C2: three contexts in flight (one box, 400 steps each: 2 -> 0.070, 3 -> 0.055, 4 -> 0.060 ms)
+    "c2": {"ray": 64, "nndr": 0.55, "seed": 7, "inflight": 3},
+    # C3's ORB rows: the 0.8 ratio and the 64 x 64 neighbourhood of BASELINE's wording; four contexts
+    # in flight (one box, 60 steps each: 1 -> 1.66, 2 -> 1.52, 3 -> 1.49, 4 -> 1.47 ms per frame pair)
+    "c3": {"ray": 32, "nndr": 0.8, "seed": 102, "inflight": 4},
 }
 
 
@@ -89,7 +91,8 @@ def parse():
     ap.add_argument("--mode", choices=("stream", "resident"), default="stream",
                     help="stream (C4 headline): every step a frame pair from host memory to host memory, "
                          "--inflight pairs in flight; resident: inputs uploaded once, one step in flight")
-    ap.add_argument("--inflight", type=int, default=2, help="LM launches in flight in the stream mode")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="LM launches in flight in the stream mode (C4 / C5: 2); contexts in flight for C2 (3) / C3 (4)")
     ap.add_argument("--lm-pairs", type=int, default=2,
                     help="frame pairs per LM launch in the stream mode (2-4: fm3d_pipeline_link)")
     ap.add_argument("--mgpu", action="store_true",
