@@ -9,19 +9,22 @@
 // MSER's linear-time flood (Nister & Stewenius, as mser.cpp implements it) is one priority flood per
 // pass whose visiting order decides which component's history continues at equal-size merges, which
 // point list comes first, and the order the regions come out in -- all part of the detector's output.
-// It is sequential by construction, so each pass is one lane (the two passes run side by side, one
-// workgroup each; the rest of the workgroup builds the grey-level histogram and clears the state
-// first).  The lane is latency-bound, so the state is laid out for one memory round trip per pixel:
-//   * mser.cpp's padded int image (value, visited bit, next direction) is split: the grey values
-//     are read from the 8-bit input (read-only, cache-resident), the visited bits are a bitmap in
-//     LDS (up to kMserLdsBits pixels; HBM beyond), and the next direction travels in the bucket
-//     entry of a pixel pushed back by a descent ({pixel + 1 | direction << 28, x | y << 16});
+// It is sequential by construction, so each pass is one lane (the passes of every image in a batch
+// run side by side, one workgroup each; the rest of the workgroup builds the grey-level histogram and
+// clears the state first).  A lone wave issues one instruction every four cycles and waits on every
+// dependent load, so the state is laid out for few instructions and round trips per pixel:
+//   * mser.cpp's padded int image (value, visited bit, next direction) is split: each pass's grey
+//     values on the same (w + 2) x (h + 2) grid (mser_pad_kernel; read through the scalar cache), the
+//     visited bits a bitmap over that grid in LDS (up to kMserLdsBits cells; HBM beyond) with the
+//     border pre-marked (no bounds tests), and the next direction in the bucket entry of a pixel
+//     pushed back by a descent ({padded pixel + 1 | direction << 28, x | y << 16});
 //   * the top entry of every grey-level bucket is cached in LDS, so a pop reads LDS and the refill
 //     of that bucket's new top from HBM is issued with the neighbours' value loads;
 //   * the top component of the stack stays in registers (size, tail, history), the ones below it in
 //     LDS.
-// The point lists (node = {next, x | y << 16}) and the histories are in HBM.  fitEllipse then runs
-// one lane per region (its three least-squares solves are OpenCV's scalar one-sided Jacobi SVD, sums
+// The point lists (node = {next, x | y << 16}) and the histories are in HBM.  After the floods the
+// lists are ranked (Wyllie) so every region's points are one contiguous run, and fitEllipse runs one
+// wave per region (its three least-squares solves are OpenCV's scalar one-sided Jacobi SVD, every sum
 // in the region list's order), all regions in parallel.
 #include <hip/hip_runtime.h>
 #include <float.h>

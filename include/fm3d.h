@@ -411,7 +411,7 @@ int fm3d_star_responses(fm3d_ctx *ctx, const uint8_t *img, int width, int height
    fitEllipse, kept when the diameter exceeds FLT_EPSILON and the rounded centre is inside the image
    (angle -1, response 0).  FM3D_ERR_INVALID where OpenCV throws (a region under 5 points, MinArea < 4).
    Each flood pass is sequential by construction (its order is part of the output) and runs as one GPU
-   lane; fitEllipse runs one lane per region. */
+   lane; fitEllipse runs one wave per region (fm3d_mser_detect_batch: many images at once). */
 int fm3d_mser_detect(fm3d_ctx *ctx, const uint8_t *img, int width, int height, int delta, int minArea, int maxArea,
                      double maxVariation, double minDiversity, fm3d_keypoint *kpts, int cap, int *n);
 /* fm3d_mser_detect on `count` images of width x height stored one after the other (the reference's
