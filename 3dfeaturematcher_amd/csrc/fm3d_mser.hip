@@ -155,9 +155,8 @@ __device__ __forceinline__ bool stable_check(Comp& c, MserHist* hist, const Mser
 // form: no 64-bit address arithmetic; every index here is below 2^28)
 __device__ __forceinline__ int2& at8(int2* base, int i) { return *(int2*)((uint8_t*)base + ((unsigned)i << 3)); }
 
-__device__ __forceinline__ int2 mser_entry(unsigned q, int x, int y, int dir) {
-    return make_int2((int)(q + 1) | (dir << 28), x | (y << 16));
-}
+// the packed (x | y << 16) step to the neighbour in direction d (right, down, left, up)
+constexpr int kStep[4] = {1, 1 << 16, -1, -(1 << 16)};
 
 // each pass's grey values on the padded (w + 2) x (h + 2) grid (pass 0: 255 - I), border 0; the flood
 // never reads a border value (the border is marked visited), it only needs no bounds tests
@@ -225,9 +224,9 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
     const int color = pass == 0 ? -1 : 1;
     const long long regCap = L.regCap;
     int nnode = 0, nhist = 0, nr = 0;
-    // the current pixel: q on the padded grid, (x, y) in the image
+    // the current pixel: q on the padded grid, xy = x | y << 16 in the image
     unsigned q = W + 1;
-    int x = 0, y = 0, dir = 0;
+    int xy = 0, dir = 0;
     // grey values through the scalar cache (the padded image read as aligned dwords): scalar loads
     // count in lgkmcnt, so they do not wait for the lane's earlier vector stores
     const unsigned* __restrict__ pad4 = (const unsigned*)(padAll + (size_t)slot * L.padBytes);
@@ -282,14 +281,13 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
                     if ((np[d2] >> 5) == (np[d] >> 5)) vw[d2] = nw;
                 vis[np[d] >> 5] = nw;
             }
-            const int nx = x + (d == 0 ? 1 : d == 2 ? -1 : 0), ny = y + (d == 1 ? 1 : d == 3 ? -1 : 0);
             if (nv[d] < v) {
                 descend = d;
             } else {
                 const int b = nv[d];
                 const int t = hcur[b] + 1;
                 hcur[b] = t;
-                const int2 e = mser_entry(np[d], nx, ny, 0);
+                const int2 e = make_int2((int)(np[d] + 1), xy + kStep[d]);  // mser_entry, direction 0
                 at8(heap, t) = e;
                 topE[b] = e;
             }
@@ -299,11 +297,10 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
             const int d = descend;
             const int t = hcur[v] + 1;
             hcur[v] = t;
-            const int2 e = mser_entry(q, x, y, d + 1);
+            const int2 e = make_int2((int)(q + 1) | ((d + 1) << 28), xy);
             at8(heap, t) = e;
             topE[v] = e;
-            x += d == 0 ? 1 : d == 2 ? -1 : 0;
-            y += d == 1 ? 1 : d == 3 ? -1 : 0;
+            xy += kStep[d];
             q = np[d];
             v = nv[d];
             dir = 0;
@@ -315,7 +312,7 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
             continue;
         }
         // accumulateMSERComp: the finished pixel joins the top component's list
-        at8(node, nnode) = make_int2(-1, x | (y << 16));
+        at8(node, nnode) = make_int2(-1, xy);
         if (T.size > 0)
             at8(node, T.tail).x = nnode;
         else
@@ -349,8 +346,7 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
         }
         q = (unsigned)(e.x & 0x0fffffff) - 1u;
         dir = (int)((unsigned)e.x >> 28);
-        x = e.y & 0xffff;
-        y = (int)((unsigned)e.y >> 16);
+        xy = e.y;
         if (pv != v) {
             v = pv;
             if (pv < belowLevel) {
