@@ -138,6 +138,24 @@ def test_compute_without_gpu_fails_loudly(fm3d):
         assert "ERR" in out
 
 
+def test_new_entry_points_reject_bad_arguments(fm3d):
+    """The batch MSER and the NCC submit / wait entry points validate their arguments on the host
+    (FM3D_ERR_INVALID for a null context or sizes) before any device work -- no GPU needed"""
+    import ctypes
+    L = ctypes.CDLL(fm3d.LIB_PATH)
+    invalid = fm3d.ERR_INVALID
+    img = (ctypes.c_uint8 * 16)()
+    cnt = (ctypes.c_int32 * 2)()
+    tot = ctypes.c_int(0)
+    kp = (ctypes.c_uint8 * 64)()
+    r = L.fm3d_mser_detect_batch(None, img, 2, 4, 2, 5, 60, 14400, ctypes.c_double(0.25), ctypes.c_double(0.2),
+                                 kp, 0, cnt, ctypes.byref(tot))
+    assert r == invalid
+    n = ctypes.c_int(0)
+    assert L.fm3d_pipeline_submit_ncc(None, 4, 4, ctypes.c_double(0.4)) == invalid
+    assert L.fm3d_pipeline_wait_ncc(None, ctypes.byref(n), None) == invalid
+
+
 def test_gravity_and_patch_size_host(fm3d, orc):
     s = fm3d.Settings.default()
     g = np.zeros(3)
