@@ -273,8 +273,12 @@ __global__ __launch_bounds__(kMserThreads) void mser_flood_kernel(const uint8_t*
 #pragma unroll
         for (int d = 0; d < 4; d++) {
             if (descend >= 0 || !cand[d]) continue;
-            {  // the visited bit: a plain store of the word read above (no wait); a later neighbour
-               // in the same word stores the word with both bits
+            if (LDSVIS) {  // the visited bit: ds_or, no wait (the file is built without the atomic
+                           // optimizer, which would wrap a single lane's atomic in a lane election)
+                __hip_atomic_fetch_or(&vis[np[d] >> 5], 1u << (np[d] & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {  // a plain store of the word read above; a later neighbour in the same word
+                      // stores the word with both bits
                 const unsigned nw = vw[d] | (1u << (np[d] & 31));
 #pragma unroll
                 for (int d2 = d + 1; d2 < 4; d2++)
