@@ -122,6 +122,20 @@ def test_mser_batch_equals_single(fm3d, orc, synth):
         _same_kpts(k, want)
 
 
+def test_mser_batch_hbm_bitmap(fm3d, orc):
+    """a batch of images past the LDS bitmap: every slot's visited bits at its own offset in HBM"""
+    imgs = [_blurred(1000, 1024, 3.0, 9), _blurred(1000, 1024, 2.0, 10)]
+    kw = dict(min_area=30, max_area=20000)
+    ctx, _ = _ctx(fm3d)
+    try:
+        batch = fm3d.Features(ctx).mser_batch(imgs, **kw)
+    finally:
+        ctx.close()
+    for img, k in zip(imgs, batch):
+        _same_kpts(k, orc.mser_detect(img, **kw))
+    assert len(batch[0]) > 50 and len(batch[1]) > 50
+
+
 def test_mser_settings_through_detect(fm3d, orc, synth):
     """DetectorType MSER with the nine MSERDetector keys (the last four do not steer grey images)"""
     img = synth.make_frame_pair(1500, seed=75).img2
