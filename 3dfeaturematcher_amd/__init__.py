@@ -44,7 +44,7 @@ EXPORTS = (
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
     "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link", "fm3d_freak_compute", "fm3d_freak_set_pairs",
     "fm3d_mser_detect", "fm3d_mser_detect_batch", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt",
-    "fm3d_pipeline_submit_ncc", "fm3d_pipeline_wait_ncc", "fm3d_pipeline_wait_dlt",
+    "fm3d_pipeline_submit_ncc", "fm3d_pipeline_wait_ncc", "fm3d_pipeline_wait_dlt", "fm3d_device_count",
 )
 
 
@@ -83,6 +83,7 @@ class Settings(ctypes.Structure):
         ("mserMaxVariation", ctypes.c_double), ("mserMinDiversity", ctypes.c_double),
         ("mserMaxEvolution", ctypes.c_int), ("mserAreaThreshold", ctypes.c_double),
         ("mserMinMargin", ctypes.c_double), ("mserEdgeBlurSize", ctypes.c_int),
+        ("lmReduction", ctypes.c_int),
     ]
 
     @staticmethod
@@ -980,6 +981,13 @@ class Pipeline:
 
 
 SHARE_BLOCK = 4096  # queries per block of the block-cyclic partition (fm3d_mgpu, shard.py)
+
+
+def device_count() -> int:
+    """fm3d_device_count: the GPUs HIP sees (hipGetDeviceCount), without importing torch."""
+    n = ctypes.c_int(0)
+    _check(lib().fm3d_device_count(ctypes.byref(n)))
+    return n.value
 
 
 def share_queries(n: int, shares: int, s: int, block: int = SHARE_BLOCK) -> np.ndarray:

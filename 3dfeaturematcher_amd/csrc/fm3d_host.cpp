@@ -392,11 +392,12 @@ void f32_to_u8(uint8_t* o, const float* x, int n, int dim, int dimPad) {
 
 // stage descriptors on the device (asynchronous H2D from the pinned staging buffers; the stream
 // orders every later use); returns the effective kernel type
+// (waitStaging false: the caller waited for the staging buffers already, stage_pipeline)
 int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
-                      int* effType, int* dimPad) {
+                      int* effType, int* dimPad, bool waitStaging = true) {
     if (dim <= 0 || nA < 0 || nB < 0) return fail(c, FM3D_ERR_INVALID, "bad descriptor shape");
     int r;
-    if ((r = staging_wait(c))) return r;
+    if (waitStaging && (r = staging_wait(c))) return r;
     int t = type;
     // integer-valued f32 rows take the u8 kernel only where it supports the width (padded <= 256)
     if (type == FM3D_DESC_F32 && ((dim + 127) / 128) * 128 <= 256 && f32_is_u8((const float*)descA, (size_t)nA * dim) &&
@@ -638,7 +639,7 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
         if (q != c && (q->device != c->device || q->s.pyramids != levels || q->s.pixelsRay != c->s.pixelsRay ||
                        std::memcmp(&q->cam, &c->cam, sizeof(c->cam)) != 0 || q->s.boundWidth != c->s.boundWidth ||
                        q->s.boundHeight != c->s.boundHeight || q->s.zThresholdMax != c->s.zThresholdMax ||
-                       q->s.epsilonLMMIN != c->s.epsilonLMMIN))
+                       q->s.epsilonLMMIN != c->s.epsilonLMMIN || q->s.lmReduction != c->s.lmReduction))
             return fail(c, FM3D_ERR_INVALID, "linked contexts need one device, camera and LM settings");
         const int P = src[j].P;
         HIPCHK(c, q->lmNormals.ensure((size_t)(P + 1) * 3 * sizeof(double)));
@@ -651,16 +652,22 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
     }
     HIPCHK(c, c->lmQueue.ensure(64 * sizeof(int)));
     HIPCHK(c, c->lmStat.ensure(256));
-    // persistent workgroups of fm3d::kLM2Slots term waves (one point each) + a chain wave;
-    // slots refill from the queue (fm3d_lm2.hip)
-    const int slots = fm3d::kLM2Slots;
+    // persistent workgroups of fm3d::kLM2Slots term waves (one point each) + a chain wave, or in the
+    // tree-reduction mode kLM2Slots + 1 term waves; slots refill from the queue (fm3d_lm2.hip)
+    const char* te = getenv("FM3D_LM_TREE");  // A/B switch: overrides settings.lmReduction
+    if (c->s.lmReduction != 0 && c->s.lmReduction != 1)
+        return fail(c, FM3D_ERR_INVALID, "lmReduction must be 0 (pixel order) or 1 (tree)");
+    const bool tree = te ? atoi(te) != 0 : c->s.lmReduction != 0;
+    const int slots = fm3d::kLM2Slots + (tree ? 1 : 0);
     // one pose for all problems: the single-pose kernel (entry 0 of the table serves them all)
     bool multiPose = false;
     for (int j = 1; j < nProb; j++)
         multiPose |= std::memcmp(src[j].c->R2, src[0].c->R2, sizeof(c->R2)) != 0 ||
                      std::memcmp(src[j].c->t2, src[0].c->t2, sizeof(c->t2)) != 0;
-    const void* kptr = multiPose ? reinterpret_cast<const void*>(fm3d::lm2_kernel<true>)
-                                 : reinterpret_cast<const void*>(fm3d::lm2_kernel<false>);
+    const void* kptr = tree ? (multiPose ? reinterpret_cast<const void*>(fm3d::lm2_kernel<true, true>)
+                                         : reinterpret_cast<const void*>(fm3d::lm2_kernel<false, true>))
+                            : (multiPose ? reinterpret_cast<const void*>(fm3d::lm2_kernel<true, false>)
+                                         : reinterpret_cast<const void*>(fm3d::lm2_kernel<false, false>));
     long groups = c->s.lmWaves;
     if (groups <= 0) {
         int cus = 0, perCU = 0;
@@ -757,6 +764,7 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
         c->wallKhz = khz;
         const char* co = getenv("FM3D_LM_COOP");  // A/B switch for the tail help
         p.coop = co ? atoi(co) : 1;
+        if (tree) p.coop = 0;  // a helper's chunks would leave the lanes' chunk order of the tree
         const char* sf = getenv("FM3D_LM_SAFE");  // test switch: the guarded pass forms only
         p.safe = sf ? atoi(sf) : 0;
     }
@@ -777,11 +785,8 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
         }
         // one launch: every slot runs its point through all levels, coarsest first
         // (optimize_pyramid :225-241)
-        if (multiPose)
-            hipLaunchKernelGGL(fm3d::lm2_kernel<true>, dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream, p);
-        else
-            hipLaunchKernelGGL(fm3d::lm2_kernel<false>, dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream,
-                               p);
+        hipLaunchKernelGGL(reinterpret_cast<void (*)(fm3d::LMParams)>(const_cast<void*>(kptr)),
+                           dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream, p);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(e1, c->stream));
     }
@@ -801,13 +806,13 @@ int run_lm(fm3d_ctx* c, int P, const int* Pdev, fm3d_lm_stats* stats, hipEvent_t
 // the two images into pinned staging and their pyramids (pyrDown chain) on the context stream;
 // sync: wait for them before returning (fm3d_set_images: the caller may read them back at once)
 int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int width, int height, int stride,
-                    bool sync = true) {
+                    bool sync = true, bool waitStaging = true) {
     if (!img1 || !img2 || width <= 0 || height <= 0 || stride < width)
         return fail(c, FM3D_ERR_INVALID, "bad image arguments");
     const int levels = c->s.pyramids;
     if (levels < 0 || levels > 7) return fail(c, FM3D_ERR_UNSUPPORTED, "pyramids must be in [0, 7]");
     int r;
-    if ((r = staging_wait(c))) return r;
+    if (waitStaging && (r = staging_wait(c))) return r;
     c->w = width;
     c->h = height;
     c->lw.assign(levels + 1, 0);
@@ -1920,10 +1925,13 @@ int stage_pipeline(fm3d_ctx* c, const void* descA, int nA, const void* descB, in
                    int width, int height, int queryOffset) {
     if (!kpts1 || !kpts2) return fail(c, FM3D_ERR_INVALID, "null argument");
     int t, dp, r;
-    if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp))) return r;
+    // the previous pair's copies out of the staging buffers have run: one wait, then every H2D of
+    // this pair is queued without another (the call returns before they execute)
+    if ((r = staging_wait(c))) return r;
+    if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp, false))) return r;
     if ((r = upload_pinned(c, c->kp1, c->hK1, kpts1, (size_t)nA * sizeof(fm3d_point2f)))) return r;
     if ((r = upload_pinned(c, c->kp2, c->hK2, kpts2, (size_t)nB * sizeof(fm3d_point2f)))) return r;
-    if ((r = set_images_impl(c, img1, img2, width, height, width, false))) return r;  // records evStage
+    if ((r = set_images_impl(c, img1, img2, width, height, width, false, false))) return r;  // records evStage
     if (!c->haveG12) {
         double g[16];
         if ((r = fm3d_setg12(c, c->s.pos1, c->s.pos2, c->s.pos1 + 3, c->s.pos2 + 3, g))) return r;
@@ -2036,6 +2044,12 @@ int enqueue_linked(fm3d_ctx* c, const std::vector<fm3d_ctx*>& ms, fm3d_lm_stats*
     }
     src.push_back({c, c->stNA, c->pcnt.as<int>() + 1});
     if ((r = run_lm_multi(c, src.data(), (int)src.size(), ls, c->ev[6], c->ev[7]))) return r;
+    // each member gets its own copy of the launch's counters (on this stream, before evLm): the
+    // leader's next run_lm_multi resets c->lmStat, possibly before a member's epilogue has read it
+    for (fm3d_ctx* m : ms) {
+        HIPCHK(m, m->lmStat.ensure(256));
+        HIPCHK(c, hipMemcpyAsync(m->lmStat.p, c->lmStat.p, sizeof(PipeSmall::lm), hipMemcpyDeviceToDevice, c->stream));
+    }
     HIPCHK(c, hipEventRecord(c->evLm, c->stream));
     if ((r = enqueue_epilogue(c, c->subOut, c->lmStat.p))) return r;
     for (fm3d_ctx* m : ms) {
@@ -2045,7 +2059,7 @@ int enqueue_linked(fm3d_ctx* c, const std::vector<fm3d_ctx*>& ms, fm3d_lm_stats*
         m->wallKhz = c->wallKhz;
         hipSetDevice(m->device);
         HIPCHK(m, hipStreamWaitEvent(m->stream, c->evLm, 0));
-        if ((r = enqueue_epilogue(m, m->subOut, c->lmStat.p))) return r;
+        if ((r = enqueue_epilogue(m, m->subOut, m->lmStat.p))) return r;
         m->frontOnly = false;
     }
     return FM3D_OK;

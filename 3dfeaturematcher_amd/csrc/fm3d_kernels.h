@@ -97,8 +97,9 @@ constexpr int kLMRunning = 0x100;  // status of a point still in flight
 constexpr int kLM2Slots = 15;
 constexpr int kLM2Ring = 8;  // chunks of 64 entries in flight per slot
 constexpr int kLM2Threads = 64 * (kLM2Slots + 1);
-// MULTI: the problems' ProjConst entries differ (per-pass pose offset); false: entry 0 for all
-template <bool MULTI>
+// MULTI: the problems' ProjConst entries differ (per-pass pose offset); false: entry 0 for all.
+// TREE: the tree-summed reduction mode (kLM2Slots + 1 term waves, no chain wave)
+template <bool MULTI, bool TREE>
 __global__ void lm2_kernel(LMParams p);
 
 // ---------------- matching ----------------

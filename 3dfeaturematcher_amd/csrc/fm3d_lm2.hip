@@ -34,6 +34,17 @@
 //     norms) they are one multiply by the correctly rounded reciprocal and one Markstein
 //     correction;
 //   * one workgroup of kW = 15 term waves + the chain wave per CU (4 waves per SIMD).
+//
+// TREE (fm3d_settings.lmReduction = 1): every m_dat-long sum as a fixed blocked
+// tree instead -- each lane adds its entries (e = 64 k + lane) in chunk order, then an xor butterfly
+// over the 64 lanes (oracle/fm3d_oracle.c ORC_LM_TREE, bit for bit).  No chain wave and no ring:
+// the workgroup's 16th wave is a term wave too, and a pass's sums are the term wave's own.  The
+// Jacobian sweep also sums a_0.a_1, a_0.f, a_1.f, so the 2-column Householder QR comes from these
+// sums by the reflections' identities (ORC_LM_GRAM) where it is well conditioned; the three
+// Householder passes run (tree-summed) only where it is not.  A sum of squares with a component
+// outside enorm's intermediate range is replaced by MINPACK's sequential enorm (lane 0, from the
+// slabs; rare).  Not the reference's summation order: the normals differ from the sequential
+// mode's beyond 1e-4 on a fraction of points (profiles/r05_full_parity.json), so it is opt-in.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
@@ -52,6 +63,7 @@ namespace {
 using namespace lmdif;
 
 constexpr int kW = kLM2Slots;  // term waves (slots) per workgroup
+constexpr int kWA = kW + 1;    // per-slot LDS arrays: TREE runs kW + 1 term waves
 constexpr int kE = 64;         // entries per chunk: one per lane
 constexpr int kR = kLM2Ring;   // chunks in flight per slot (LDS ring depth)
 static_assert((kR & (kR - 1)) == 0, "ring depth: a power of two");
@@ -102,7 +114,10 @@ struct PassOut2 {
     double nrm[2];  // EVAL (per evaluation) / QR2: enorm of the pass's values
     double sum[2];  // QR1 (a_q and fvec products) / QR3 dot products
     double aqs1;    // QR2: transformed a_q at the second kept pixel
-    int cnt, fail[2], ph3[2], i1fail;
+    // TREE, Jacobian sweep: sq[j] = sum of a_j^2 (enorm: sqrt), g[0] = a_0.a_1, g[1 + j] = a_j.f;
+    // slow: bit j set when column j holds a component outside enorm's intermediate range
+    double sq[2], g[3];
+    int cnt, fail[2], ph3[2], i1fail, slow;
 };
 
 // what the chain lanes need to know about a pass (written before its first chunk)
@@ -122,8 +137,9 @@ struct Slab {
     gfloat* DJ1;
     gint* KI;  // compact entry -> neighbourhood offset index
 };
+template <int NS>
 __device__ inline Slab slab_of(const LMParams& p, long gslot) {
-    const size_t n = (size_t)p.nOffPad, G = (size_t)p.nWaves * kW;
+    const size_t n = (size_t)p.nOffPad, G = (size_t)p.nWaves * NS;
     Slab s;
 #if FM3D_RAY_AOS
     s.RX = (gdouble*)p.slab + gslot * n * 2;  // (ux, uy) pairs: one 16-byte record per entry
@@ -148,6 +164,7 @@ struct Ctl2 {
     Slab sl;
     double eps;
     long long cnt_eval, cnt_pix;
+    int tree;  // TREE launch: the Gram form of the QR where it applies (start_qr_tree)
 
     // the next point of the launch's queue: the problems' points one after the other (each
     // problem one frame pair; its point count on the device or given)
@@ -212,7 +229,7 @@ struct Ctl2 {
         const LMProblem& pr = p->prob[S.prob];
         pr.info[8 * S.pidx + S.L] = info;
         pr.nfev[8 * S.pidx + S.L] = S.s.nfev;
-        sph2car_det(S.s.x[0], S.s.x[1], S.nrm0, S.nrm1, S.nrm2);
+        sph2car_cr(S.s.x[0], S.s.x[1], S.nrm0, S.nrm1, S.nrm2);
         S.L--;
         if (S.L < 0)
             finish_point(S, P, FM3D_ST_OK);
@@ -229,12 +246,12 @@ struct Ctl2 {
     // Returns false if the normal is NaN (the call aborts before touching a pixel).
     __device__ bool setup_eval(SlotS2& S, SlotP2& P, int ev, double a, double b, double hj) {
         double n0, n1, n2;
-        sph2car_det(a, b, n0, n1, n2);  // par = (phi, theta)
+        sph2car_cr(a, b, n0, n1, n2);  // par = (phi, theta)
         if (n2 != n2 || n1 != n1 || n0 != n0) return false;
         double w_theta = 1.0, w_phi = 1.0;
         if (fabs(b) - M_PI / 2 > 0 || fabs(a) - M_PI > 0) {
-            w_theta = fm3d_exp(fabs(b) - M_PI / 2) + 1;
-            w_phi = fm3d_exp(fabs(a) - M_PI + 1) + 1;
+            w_theta = fm3d_exp_cr(fabs(b) - M_PI / 2) + 1;
+            w_phi = fm3d_exp_cr(fabs(a) - M_PI + 1) + 1;
         }
         P.n0[ev] = n0;
         P.n1[ev] = n1;
@@ -303,6 +320,9 @@ struct Ctl2 {
         S.s.r[3] = S.t1 ? -S.ajn1s : 0.;
         S.s.qtf[0] = S.qtf0;
         S.s.qtf[1] = qtf1;
+        after_qr(S, P);
+    }
+    __device__ void after_qr(SlotS2& S, SlotP2& P) {
         int info = lm_after_qr(S.s);
         if (info) {
             level_done(S, P, info);
@@ -347,6 +367,37 @@ struct Ctl2 {
             qr2(S, P);
         }
     }
+    // TREE: the 2-column QR from the Jacobian sweep's tree sums where it is well conditioned
+    // (oracle/fm3d_oracle.c orc_qr_tree, ORC_LM_GRAM: the same operations), else the Householder
+    // passes with tree sums
+    __device__ void start_qr_tree(SlotS2& S, SlotP2& P, const PassOut2& o) {
+        LM& s = S.s;
+        const int pc = (s.acnorm[1] > s.acnorm[0]) ? 1 : 0;
+        if (!o.slow && s.acnorm[pc] != 0.) {
+            const double apf = jcol_at(S, pc, 0), aqf = jcol_at(S, 1 - pc, 0);
+            const double Spq = o.g[0], Spf = o.g[1 + pc], Sqf = o.g[2 - pc], Sqq = o.sq[1 - pc];
+            const double s0 = apf < 0. ? -s.acnorm[pc] : s.acnorm[pc];
+            const double r01 = -(Spq / s0), qtf0 = -(Spf / s0), d = Sqq - r01 * r01;
+            if (__builtin_isfinite(Spq) && __builtin_isfinite(Spf) && __builtin_isfinite(Sqf) &&
+                __builtin_isfinite(Sqq) && d > 1e-6 * Sqq) {  // ORC_GRAM_C
+                const double v0 = apf / s0 + 1., v1 = jcol_at(S, pc, 1) / s0, t = (Spq / s0 + aqf) / v0;
+                const double a1 = jcol_at(S, 1 - pc, 1) - t * v1;
+                double s1 = sqrt(d);
+                if (a1 < 0.) s1 = -s1;
+                s.ipvt[0] = pc;
+                s.ipvt[1] = 1 - pc;
+                s.r[0] = -s0;
+                s.r[1] = 0.;
+                s.r[2] = r01;
+                s.r[3] = -s1;
+                s.qtf[0] = qtf0;
+                s.qtf[1] = -((Sqf - r01 * qtf0) / s1);
+                after_qr(S, P);
+                return;
+            }
+        }
+        start_qr(S, P);
+    }
     __device__ void qr2(SlotS2& S, SlotP2& P) {
         P.pass = Q_QR2;
         P.tq = S.tq;
@@ -358,6 +409,32 @@ struct Ctl2 {
         if (!i1ok) return FM3D_ST_ABORT_PIX1;
         if (ph3) return FM3D_ST_ABORT_PIX2;
         return 0;
+    }
+
+    // TREE: MINPACK's sequential enorm of a pass's values recomputed from the slabs, for a sum of
+    // squares with a component outside enorm's intermediate range (rare; orc_enorm_tree's
+    // fallback).  kind 0: the residual; 1 / 2: Jacobian column 0 / 1; 3: QR2's transformed a_q
+    // (entries 1 ..).  The same IEEE operations as the passes (their fast divisions round alike).
+    __device__ __noinline__ double seq_enorm(const SlotP2& P, int kind, int len) const {
+        Enorm en;
+        en.init(kind == 3 ? len - 1 : len);
+        const int pc = P.pivot;
+        for (int e = kind == 3 ? 1 : 0; e < len; e++) {
+            double v;
+            if (kind == 0) {
+                v = P.w[0] * (double)sl.DF[e];
+            } else if (kind < 3) {
+                const int j = kind - 1;
+                v = (P.w[j] * (double)(j ? sl.DJ1 : sl.DJ0)[e] - P.wF * (double)sl.DF[e]) / P.hj[j];
+            } else {
+                const double F = P.wF * (double)sl.DF[e];
+                const double ap = (P.w[pc] * (double)(pc ? sl.DJ1 : sl.DJ0)[e] - F) / P.hj[pc];
+                v = (P.w[1 - pc] * (double)(pc ? sl.DJ0 : sl.DJ1)[e] - F) / P.hj[1 - pc];
+                if (P.t0) v = v - P.tq * (ap / P.ajn0s);
+            }
+            en.add(v);
+        }
+        return en.finish();
     }
 
     __device__ __noinline__ void after_pass(SlotS2& S, SlotP2& P, const PassOut2& o) {
@@ -379,8 +456,8 @@ struct Ctl2 {
         } else if (ps == Q_LEVEL) {
             S.i1ok = o.i1fail ? 0 : 1;
             // car2sph (tools.cpp:767-771) -> lmdif from the current normal
-            S.s.x[1] = fm3d_atan2(S.nrm2, sqrt(S.nrm0 * S.nrm0 + S.nrm1 * S.nrm1));
-            S.s.x[0] = fm3d_atan2(S.nrm1, S.nrm0);
+            S.s.x[1] = fm3d_atan2_cr(S.nrm2, sqrt(S.nrm0 * S.nrm0 + S.nrm1 * S.nrm1));
+            S.s.x[0] = fm3d_atan2_cr(S.nrm1, S.nrm0);
             S.s.nfev = 0;
             S.s.iter = 1;
             S.s.par = 0.;
@@ -413,7 +490,10 @@ struct Ctl2 {
                     return;
                 }
                 s.acnorm[1] = o.nrm[1];
-                start_qr(S, P);
+                if (tree)
+                    start_qr_tree(S, P, o);
+                else
+                    start_qr(S, P);
             } else {
                 bool accepted;
                 int info = lm_after_trial(s, o.nrm[0], &accepted);
@@ -468,30 +548,30 @@ struct Shared {
     // position spans a multiple of 256 B, so in the chain's ds_read_b128 every lane of a 16-lane
     // group reads its own four banks whatever ring positions the slots are at (conflict-free).
     alignas(256) double ring[kR][kRS];
-    int rowTag[kW][kR];            // (chunk index << 2) | slow flags of the terms a ring position holds (published last)
-    int consumed[kW][2];           // chunks consumed, per chain lane (monotonic)
-    int resultId[kW][2];           // id of the last pass whose result is published
-    double result[kW][2];
+    int rowTag[kWA][kR];            // (chunk index << 2) | slow flags of the terms a ring position holds (published last)
+    int consumed[kWA][2];           // chunks consumed, per chain lane (monotonic)
+    int resultId[kWA][2];           // id of the last pass whose result is published
+    double result[kWA][2];
     Enorm chainEn[64];  // MINPACK enorm state of each chain lane (s2 lives in its register)
-    int done[kW];
+    int done[kWA];
     // tail help: a wave whose slot has no more points takes every other chunk of a busy slot's
     // summed passes (one helper per slot, attached for good)
-    int helper[kW];                // 1 once a helper is attached
-    int annSeq[kW];                // passes announced to the helper (monotonic)
-    int annBase[kW], annId[kW];    // the announced pass: first chunk index, pass id
-    int helpDone[kW];              // id of the last announced pass whose helper share is complete
-    int hfail[kW][2], hph3[kW][2]; // the helper share's failures (as fail0/fail1, ph30/ph31 != 0)
-    int hAtt[kW], hSeen[kW], hAnn[kW];  // per wave (lane 0): attached slot, passes taken, passes announced
+    int helper[kWA];                // 1 once a helper is attached
+    int annSeq[kWA];                // passes announced to the helper (monotonic)
+    int annBase[kWA], annId[kWA];    // the announced pass: first chunk index, pass id
+    int helpDone[kWA];              // id of the last announced pass whose helper share is complete
+    int hfail[kWA][2], hph3[kWA][2]; // the helper share's failures (as fail0/fail1, ph30/ph31 != 0)
+    int hAtt[kWA], hSeen[kWA], hAnn[kWA];  // per wave (lane 0): attached slot, passes taken, passes announced
     // per-wave statistics, kept in LDS (lane 0) so that they hold no scalar registers across
     // the pass loops: class passes / cycles, terms / control cycles, producer waits, passes
     struct WaveStat {
         unsigned long long cnt[4], cyc[4], terms, ctl, wait, nPass, iter, t0;
-    } ws[kW];
-    PassDesc pd[kW];
-    SlotP2 sp[kW];
-    SlotS2 ss[kW];
-    PassOut2 out[kW];
-    Ctl2 ctl[kW];
+    } ws[kWA];
+    PassDesc pd[kWA];
+    SlotP2 sp[kWA];
+    SlotS2 ss[kWA];
+    PassOut2 out[kWA];
+    Ctl2 ctl[kWA];
     LMParams P;
 };
 
@@ -924,13 +1004,14 @@ __device__ __noinline__ void chain_wave(int lane, unsigned long long tStart, lon
 }  // namespace
 
 // 4 waves per SIMD: one workgroup of 16 waves per CU (128 VGPRs)
-template <bool MULTI>
+template <bool MULTI, bool TREE>
 __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     Shared& sh = g_sh;
+    constexpr int NS = TREE ? kWA : kW;  // term waves (slots) of the workgroup
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long tStart = wall_clock64(), cyStart = clock64();
     if (tid == 0) sh.P = p;
-    if (tid < kW) {
+    if (tid < NS) {
         for (int k = 0; k < kR; k++) sh.rowTag[tid][k] = -1;
         sh.consumed[tid][0] = sh.consumed[tid][1] = 0;
         sh.resultId[tid][0] = sh.resultId[tid][1] = 0;
@@ -941,17 +1022,18 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     }
     __syncthreads();
 
-    if (wave < kW) {
+    if (wave < NS) {
         // ======================= term wave: slot w =======================
         const int w = rfl(wave);
-        const long gslot = (long)blockIdx.x * kW + w;
+        const long gslot = (long)blockIdx.x * NS + w;
         Ctl2& ctl = sh.ctl[w];
 
         // the summed passes address the slabs as grid-uniform array bases (ProjConst, scalar
         // loads) + one 32-bit byte offset per entry (global_load ... vOffset, sBase)
         if (lane == 0) {
             ctl.p = &sh.P;
-            ctl.sl = slab_of(p, gslot);
+            ctl.sl = slab_of<NS>(p, gslot);
+            ctl.tree = TREE;
             ctl.eps = sqrt(p.epsfcn > DBL_EPSILON ? p.epsfcn : DBL_EPSILON);
             ctl.cnt_eval = 0;
             ctl.cnt_pix = 0;
@@ -1107,13 +1189,13 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 cbase = rfl(cbase);
                 k0 = rfl(k0);
                 kS = rfl(kS);
-                const unsigned s8 = (unsigned)(((size_t)blockIdx.x * kW + tw) * p.nOffPad * 8);  // slot tw's, < 2^32 (host-checked)
+                const unsigned s8 = (unsigned)(((size_t)blockIdx.x * NS + tw) * p.nOffPad * 8);  // slot tw's, < 2^32 (host-checked)
                 const int ekind = rfl(SP.ekind);
                 const int nev = rfl(SP.nev);
                 const bool jac = pass == Q_EVAL && ekind == E_JAC;
                 cls = jac ? 0 : (pass == Q_EVAL ? 1 : 2);
                 const double agiant = SP.agiant;
-                if (own && lane == 0) {
+                if (!TREE && own && lane == 0) {
                     PassDesc& d = sh.pd[w];
                     d.nChunks = nCh;
                     d.id = passId;
@@ -1129,6 +1211,10 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 int fail0 = 0x7fffffff, fail1 = 0x7fffffff;
                 int ph30 = 0, ph31 = 0;  // image-2 failures seen (wave-uniform flags)
                 double aqs1 = 0.;
+                // TREE: the lane's partial sums of the pass (entries 64 k + lane in chunk order) and
+                // the wave-uniform enorm slow flags of sums 0 / 1
+                double ta0 = 0., ta1 = 0., ta2 = 0., ta3 = 0., ta4 = 0.;
+                bool tslow0 = false, tslow1 = false;
                 if (pass == Q_EVAL) {
                     const double n00 = SP.n0[0], n10 = SP.n1[0], n20 = SP.n2[0], mm0 = SP.mm[0], w0 = SP.w[0];
                     const double n01 = SP.n0[1], n11 = SP.n1[1], n21 = SP.n2[1], mm1 = SP.mm[1], w1 = SP.w[1];
@@ -1214,7 +1300,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             return make_uint2(*(const gu16u*)(img2b + off), *(const gu16u*)(img2b + (off + lw)));
                         };
                         auto chunk = [&](const Ld& L, int k, unsigned o4) {
-                            prod.reserve(cbase + k);
+                            if constexpr (!TREE) prod.reserve(cbase + k);
                             const LaneMask in = in_mask(k, len), ok = i1ok ? in : 0ull;
                             const Geo2 g0 = geo(L.ux, L.uy, n00, n10, n20, mm0);
                             Geo2 g1;
@@ -1262,7 +1348,20 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 *(gfloat*)(sb()->slabDJ1 + o4) = dI1;
                                 t1 = enorm_term2(v1, agiant, slow1);
                             }
-                            prod.write_terms<NEV == 2>(cbase + k, t0, v0, slow0, t1, v1, slow1);
+                            if constexpr (TREE) {
+                                ta0 += t0;
+                                tslow0 |= slow0;
+                                if (NEV == 2) {
+                                    const double Fm = sel_mask(wF * L.dF, in);
+                                    ta1 += t1;
+                                    ta2 += v0 * v1;
+                                    ta3 += v0 * Fm;
+                                    ta4 += v1 * Fm;
+                                    tslow1 |= slow1;
+                                }
+                            } else {
+                                prod.write_terms<NEV == 2>(cbase + k, t0, v0, slow0, t1, v1, slow1);
+                            }
                         };
                         // this wave's chunks: k0, k0 + kS, ...; st8 / st4: the offset step between them
                         unsigned o8 = s8 + lane * 8u + (unsigned)k0 * 512u, o4 = o8 >> 1;
@@ -1321,13 +1420,26 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 bool slow0, slow1;
                                 const double t0 = enorm_term2(v0, agiant, slow0);
                                 const double t1 = enorm_term2(v1, agiant, slow1);
-                                prod.reserve(cbase + k);
+                                if constexpr (!TREE) prod.reserve(cbase + k);
                                 {
                                     const auto* pc = sb();
                                     *(gfloat*)(pc->slabDJ0 + oo) = dI0;
                                     *(gfloat*)(pc->slabDJ1 + oo) = dI1;
                                 }
-                                prod.write_terms<true>(cbase + k, t0, v0, slow0, t1, v1, slow1);
+                                if constexpr (TREE) {
+                                    // the column norms and the Gram sums of the QR (start_qr_tree); F of
+                                    // the entries past len is slab padding: zeroed
+                                    const double Fm = sel_mask(F, S.ok0 | S.ok1);
+                                    ta0 += t0;
+                                    ta1 += t1;
+                                    ta2 += v0 * v1;
+                                    ta3 += v0 * Fm;
+                                    ta4 += v1 * Fm;
+                                    tslow0 |= slow0;
+                                    tslow1 |= slow1;
+                                } else {
+                                    prod.write_terms<true>(cbase + k, t0, v0, slow0, t1, v1, slow1);
+                                }
                             };
                             // A stage past the last chunk computes garbage from slab padding (its
                             // entries are not `in`: no failures); no branch between gathers and use
@@ -1419,7 +1531,12 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 }
                                 bool slow;
                                 const double t = enorm_term2(v, agiant, slow);
-                                prod.write_terms<false>(cbase + kk, t, v, slow, 0., 0., false);
+                                if constexpr (TREE) {
+                                    ta0 += t;
+                                    tslow0 |= slow;
+                                } else {
+                                    prod.write_terms<false>(cbase + kk, t, v, slow, 0., 0., false);
+                                }
                             };
                             // both chunks' values first (no branch between the gathers and their
                             // use), then the ring space, then the stores of the chunks that exist
@@ -1429,7 +1546,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 float dIA, dIB;
                                 const double vA = value(S.fxA, S.fyA, S.a, S.i1A, S.dFA, S.okA, dIA);
                                 const double vB = value(S.fxB, S.fyB, S.b, S.i1B, S.dFB, S.okB, dIB);
-                                prod.reserve(cbase + (two ? kB : k));  // space for both chunks
+                                if constexpr (!TREE) prod.reserve(cbase + (two ? kB : k));  // space for both chunks
                                 publish(vA, dIA, oo, k);
                                 if (two) publish(vB, dIB, oo + st4, kB);
                             };
@@ -1464,7 +1581,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             for (int k = k0; k < nCh; k += 2 * kS) {
                                 const int kB = k + kS;
                                 const bool two = kB < nCh;  // wave-uniform
-                                prod.reserve(cbase + (two ? kB : k));  // space for both chunks
+                                if constexpr (!TREE) prod.reserve(cbase + (two ? kB : k));  // space for both chunks
                                 const LaneMask inA = in_mask(k, len), inB = in_mask(kB, len);
                                 const Geo2 gA = geo(A.ux, A.uy, n00, n10, n20, mm0);
                                 // past the last chunk B holds slab padding: its entries are not
@@ -1497,7 +1614,12 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                     }
                                     bool slow;
                                     const double t = enorm_term2(v, agiant, slow);
-                                    prod.write_terms<false>(cbase + kk, t, v, slow, 0., 0., false);
+                                    if constexpr (TREE) {
+                                        ta0 += t;
+                                        tslow0 |= slow;
+                                    } else {
+                                        prod.write_terms<false>(cbase + kk, t, v, slow, 0., 0., false);
+                                    }
                                 };
                                 back1(gA, a, i1A, dFA, inA, o4, k);
                                 if (two) back1(gB, b, i1B, dFB, inB, o4 + st4, kB);
@@ -1654,8 +1776,14 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 if (kc < nCh) {
                                     const Terms T = (kc == 0 || kc == nCh - 1) ? chunk(buf[j], kc, std::true_type())
                                                                                : chunk(buf[j], kc, std::false_type());
-                                    prod.reserve(cbase + kc);
-                                    prod.write_terms<KIND == Q_QR1>(cbase + kc, T.t0, T.a, T.slow, T.t1, 0., false);
+                                    if constexpr (TREE) {
+                                        ta0 += T.t0;
+                                        if (KIND == Q_QR1) ta1 += T.t1;
+                                        tslow0 |= T.slow;
+                                    } else {
+                                        prod.reserve(cbase + kc);
+                                        prod.write_terms<KIND == Q_QR1>(cbase + kc, T.t0, T.a, T.slow, T.t1, 0., false);
+                                    }
                                     buf[j] = load(o4);
                                 }
                                 o4 += st4;
@@ -1688,6 +1816,41 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         sh.hph3[tw][0] = ph30 != 0;
                         sh.hph3[tw][1] = ph31 != 0;
                         lds_store_rel(&sh.helpDone[tw], sh.annId[tw]);
+                    }
+                } else if constexpr (TREE) {
+                    // ---- the pass's sums: the xor butterfly of the lanes' partial sums (every lane
+                    // ends with the same value; ORC_LM_TREE's orc_tree_finish)
+                    const bool two = pass == Q_QR1 || (pass == Q_EVAL && nev == 2);
+                    const bool gram = jac && nev == 2;
+                    for (int o = 32; o > 0; o >>= 1) {
+                        ta0 += __shfl_xor(ta0, o);
+                        if (two) ta1 += __shfl_xor(ta1, o);
+                        if (gram) {
+                            ta2 += __shfl_xor(ta2, o);
+                            ta3 += __shfl_xor(ta3, o);
+                            ta4 += __shfl_xor(ta4, o);
+                        }
+                    }
+                    const bool en = pass == Q_EVAL || pass == Q_QR2;  // sums of squares: enorm
+                    if (lane == 0) {
+                        double r0 = ta0, r1 = ta1;
+                        if (en) {
+                            r0 = tslow0 ? ctl.seq_enorm(SP, pass == Q_QR2 ? 3 : (jac ? 1 : 0), len) : sqrt(ta0);
+                            if (two) r1 = tslow1 ? ctl.seq_enorm(SP, 2, len) : sqrt(ta1);
+                        }
+                        OUT.nrm[0] = OUT.sum[0] = r0;
+                        OUT.nrm[1] = OUT.sum[1] = r1;
+                        OUT.sq[0] = ta0;
+                        OUT.sq[1] = ta1;
+                        OUT.g[0] = ta2;
+                        OUT.g[1] = ta3;
+                        OUT.g[2] = ta4;
+                        OUT.slow = (tslow0 ? 1 : 0) | (tslow1 ? 2 : 0);
+                        OUT.fail[0] = fail0;
+                        OUT.fail[1] = fail1;
+                        OUT.ph3[0] = ph30 != 0;
+                        OUT.ph3[1] = ph31 != 0;
+                        OUT.aqs1 = aqs1;
                     }
                 } else {
                     // ---- the chain lanes' results of this pass (and the helper share)
@@ -1760,7 +1923,9 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
 
 // one pose for every problem of the launch (one frame pair, or linked pairs of one rig pose), and
 // a pose per problem
-template __global__ void lm2_kernel<false>(LMParams p);
-template __global__ void lm2_kernel<true>(LMParams p);
+template __global__ void lm2_kernel<false, false>(LMParams p);
+template __global__ void lm2_kernel<true, false>(LMParams p);
+template __global__ void lm2_kernel<false, true>(LMParams p);
+template __global__ void lm2_kernel<true, true>(LMParams p);
 
 }  // namespace fm3d

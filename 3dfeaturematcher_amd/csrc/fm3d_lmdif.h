@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "fm3d_device.h"
+#include "fm3d_crmath.h"
 
 namespace fm3d {
 namespace lmdif {
@@ -283,10 +284,18 @@ __device__ inline float bilinear4(uint8_t b00_, uint8_t b01_, uint8_t b10_, uint
 }
 
 __device__ inline void sph2car_det(double phi, double theta, double& n0, double& n1, double& n2) {
-    // tools.cpp:772-777 with the deterministic transcendentals
+    // tools.cpp:772-777 with the 1-ulp deterministic transcendentals (the NCC hypotheses)
     n0 = fm3d_cos(theta) * fm3d_cos(phi);
     n1 = fm3d_cos(theta) * fm3d_sin(phi);
     n2 = fm3d_sin(theta);
+}
+// tools.cpp:772-777 with the correctly rounded transcendentals (fm3d_crmath.h): the LM path, whose
+// reference values are libm's, and libm is correctly rounded on ~99.8 % of the LM's arguments
+__device__ inline void sph2car_cr(double phi, double theta, double& n0, double& n1, double& n2) {
+    const double ct = fm3d_cos_cr(theta);
+    n0 = ct * fm3d_cos_cr(phi);
+    n1 = ct * fm3d_sin_cr(phi);
+    n2 = fm3d_sin_cr(theta);
 }
 
 }  // namespace lmdif

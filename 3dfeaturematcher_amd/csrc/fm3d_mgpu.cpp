@@ -325,6 +325,14 @@ int fm3d_merge_shares(int nA, int shares, int block, const fm3d_record* const* r
     return FM3D_OK;
 }
 
+int fm3d_device_count(int* n) {
+    if (!n) return FM3D_ERR_INVALID;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    *n = count;
+    return FM3D_OK;
+}
+
 int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int shares, int block, fm3d_mgpu** out) {
     if (!s || !out || ndev <= 0 || ndev > 16 || shares < ndev || block < 0) return FM3D_ERR_INVALID;
     *out = nullptr;
@@ -443,6 +451,9 @@ int fm3d_mgpu_submit(fm3d_mgpu* m, const void* descA, int nA, const void* descB,
     if (others && nA != m->nA) return mfail(m, FM3D_ERR_INVALID, "frame pairs in flight must have the same query count");
     const size_t rb = row_bytes(dim, type);
     int r;
+    // a submit restages set 0 and may re-plan idx / nA: fm3d_mgpu_pipeline_run needs a new upload
+    // 
+    m->staged = false;
     if (!others && (r = plan(m, nA))) return r;
     // one host thread per device: gather its queries, stage and queue its path (a member set: its
     // front half; a leader set: the front half, one LM launch with the member set's queued pair,

@@ -696,15 +696,31 @@ __global__ __launch_bounds__(64) void mser_fit_kernel(const int4* __restrict__ r
     }
     __threadfence_block();
     __syncthreads();
-    // the float centroid: integer coordinates below 2^24 in every partial sum, so exact in any order
+    // the float centroid (OpenCV: a sequential float sum in region-list order).  Where every partial
+    // sum stays below 2^24 (m * the largest coordinate), the integer-valued sums are exact in any
+    // order: lane-strided + xor tree.  Otherwise (a wide image with a large region) lane 0 adds the
+    // points in list order, as the reference.
     float cx = 0.f, cy = 0.f;
+    int cmax = 0;
     for (int k = lane; k < m; k += 64) {
         cx = __fadd_rn(cx, (float)xy[k].x);
         cy = __fadd_rn(cy, (float)xy[k].y);
+        cmax = max(cmax, max(xy[k].x, xy[k].y));
     }
     for (int o = 32; o > 0; o >>= 1) {
         cx = __fadd_rn(cx, __shfl_xor(cx, o));
         cy = __fadd_rn(cy, __shfl_xor(cy, o));
+        cmax = max(cmax, __shfl_xor(cmax, o));
+    }
+    if ((long long)m * (long long)cmax >= (1ll << 24)) {
+        float sx = 0.f, sy = 0.f;
+        if (lane == 0)
+            for (int k = 0; k < m; k++) {
+                sx = __fadd_rn(sx, (float)xy[k].x);
+                sy = __fadd_rn(sy, (float)xy[k].y);
+            }
+        cx = __shfl(sx, 0);
+        cy = __shfl(sy, 0);
     }
     cx = cx / (float)m;
     cy = cy / (float)m;

@@ -170,6 +170,7 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->mserAreaThreshold = 1.01;
     s->mserMinMargin = 0.003;
     s->mserEdgeBlurSize = 5;
+    s->lmReduction = 0;  // pixel-order sums (the reference's)
     return FM3D_OK;
 }
 
@@ -290,6 +291,7 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
     get_i(kv, "Fm3d.boundHeight", &s->boundHeight);
     get_i(kv, "Fm3d.strictNanExit", &s->strictNanExit);
     get_i(kv, "Fm3d.lmWaves", &s->lmWaves);
+    get_i(kv, "Fm3d.lmReduction", &s->lmReduction);
     return FM3D_OK;
 }
 

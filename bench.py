@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the C5 byte-identity check against one GPU")
+    ap.add_argument("--ref-steps", type=int, default=2,
+                    help="--gpus N > 1: frame pairs of the same C5 stream on device 0 alone after the timed steps "
+                         "(value_one_gpu, efficiency); 0 skips")
     ap.add_argument("--out", type=str, default="")
     ap.add_argument("--dump-records", type=str, default="",
                     help="torchrun C5: rank 0 saves the last step's merged survivor records (.npy)")
@@ -272,6 +275,10 @@ def run_c4_stream(args):
                            f"the device span of the timed region ({span_ms:.1f} ms, HIP events on the context "
                            f"streams: first submit -> last pair's records); avg_launch_ms = that span / launches"),
         "overlapped_launch_ms_each": float(np.mean([st["lm_ms"] for st in stats])),
+        # PMC bytes are measured on one resident launch: divide by that launch's time, not the span
+        "traffic_GBps": roof["traffic"] / (rlm_ms * 1e6) if roof.get("traffic") and rlm_ms > 0 else None,
+        "traffic_GBps_basis": ("HBM bytes of one resident launch (rocprofv3 PMC, traffic_source) / the resident "
+                               "launch's HIP-event time (single_launch.avg_launch_ms): both one launch at a time"),
         "single_launch": {
             "avg_launch_ms": rlm_ms,
             "achieved": FLOPS_PER_PIXEL_EVAL * pix / (rlm_ms * 1e-3) / 1e12,
@@ -339,10 +346,17 @@ def run_mgpu(args, workload):
     (one LM launch) per device, RCCL all-gather of the survivor records over xGMI, merged in query
     order on the host; two frame pairs in flight (fm3d_mgpu_submit / fm3d_mgpu_wait), every step
     from host memory to host memory as at one GPU.  Strong scaling: value = kept keypoints of the K
-    pairs / wall time.  Exits non-zero when fewer than N GPUs are visible."""
-    import torch
+    pairs / wall time.  Exits non-zero when fewer than N GPUs are visible.
+
+    The same workload on ONE GPU is measured after the timed steps (--ref-steps pairs through
+    fm3d_mgpu on device 0 alone, the same stream shape): `value_one_gpu` and
+    `efficiency = value / (N * value_one_gpu)` in the line, so the 1 -> N curve of C5 has its own
+    one-GPU point (the driver's `--gpus 1` line is C4, the headline).  torch is never imported on
+    this route: the visible-device count comes from libfm3d (hipGetDeviceCount), so the only RCCL in
+    the process is the one fm3d_mgpu loads."""
+    fm3d = importlib.import_module("3dfeaturematcher_amd")
     n = args.gpus
-    vis = torch.cuda.device_count()
+    vis = fm3d.device_count()
     if vis < n:
         print(f"bench.py --gpus {n}: only {vis} GPU(s) visible", file=sys.stderr, flush=True)
         raise SystemExit(2)
@@ -350,7 +364,6 @@ def run_mgpu(args, workload):
         print(f"bench.py --gpus {n}: the one-process multi-GPU run is C5 (--workload auto / c5); use torchrun "
               f"for --weak or other workloads", file=sys.stderr, flush=True)
         raise SystemExit(2)
-    fm3d = importlib.import_module("3dfeaturematcher_amd")
     synth = importlib.import_module("3dfeaturematcher_amd.synth")
     wl = dict(WORKLOADS["c5"])
     for k in ("keypoints", "width", "height"):
@@ -360,13 +373,14 @@ def run_mgpu(args, workload):
     pair = synth.make_frame_pair(wl["keypoints"], wl["width"], wl["height"], seed=args.seed, desc=args.desc)
     t_gen = time.time() - t_gen
     s = c4_settings(fm3d, pair, args)
+    torch_at_create = "torch" in sys.modules
     mg = fm3d.MultiGPU(s, devices=list(range(n)), shares=n)
     mg.set_g12(pair.g12)
     binary = args.desc == "orb"
     inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
     bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(2)]  # the last two waits' records
 
-    def stream_run(n_steps):
+    def stream_run(n_steps, mg=mg):
         res, pend, last = [], 0, None
         t_sub = []
         for k in range(n_steps):
@@ -389,6 +403,25 @@ def run_mgpu(args, workload):
     elapsed = time.perf_counter() - t0
     mg.close()
     kept_total = sum(r[0] for r in res)
+    value = kept_total / elapsed
+    # the same C5 stream on device 0 alone (untimed by the metric): the curve's one-GPU point
+    one = {"value_one_gpu": value, "efficiency": 1.0, "one_gpu_steps": args.steps,
+           "one_gpu_note": "this run is one GPU: value_one_gpu = value"}
+    if n > 1 and args.ref_steps > 0:
+        m1 = fm3d.MultiGPU(s, devices=[0], shares=1)
+        try:
+            m1.set_g12(pair.g12)
+            stream_run(1, m1)
+            t1 = time.perf_counter()
+            r1, rec1 = stream_run(args.ref_steps, m1)
+            v1 = sum(r[0] for r in r1) / (time.perf_counter() - t1)
+        finally:
+            m1.close()
+        one = {"value_one_gpu": v1, "efficiency": value / (n * v1), "one_gpu_steps": args.ref_steps,
+               "one_gpu_records_equal": bool(rec1.tobytes() == last_rec.tobytes()),
+               "one_gpu_note": (f"the same C5 frame pair through fm3d_mgpu on device 0 alone, {args.ref_steps} "
+                                f"pairs after 1 warmup pair, same stream shape; efficiency = value / "
+                                f"({n} x value_one_gpu)")}
     stats = [r[1] for r in res]
     lat = [r[2] * 1e3 for r in res]
     digests = sorted(set(r[3] for r in res))
@@ -398,7 +431,7 @@ def run_mgpu(args, workload):
     kp_k = wl["keypoints"] // 1000
     out = {
         "metric": METRIC,
-        "value": kept_total / elapsed,
+        "value": value,
         "unit": "keypoints/s",
         "n_gpus": n,
         "steps": args.steps,
@@ -444,6 +477,8 @@ def run_mgpu(args, workload):
         "setup_s": {"synthetic_generation": round(t_gen, 2)},
         "records_sha256": digests[0] if len(digests) == 1 else digests,
         "records_identical_across_steps": len(digests) == 1,
+        "torch_imported_at_mgpu_create": torch_at_create,
+        **one,
     }
     out.update(verify_against_fixture(args, wl, "c5", pair, last_rec))
     if len(digests) != 1:

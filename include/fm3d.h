@@ -114,6 +114,13 @@ typedef struct fm3d_settings {
     int mserMaxEvolution;
     double mserAreaThreshold, mserMinMargin;
     int mserEdgeBlurSize;
+    /* The LM's reduction order (not a reference key; Fm3d.lmReduction in the settings file):
+       0 = every m_dat-long sum (enorm of the residual, the Jacobian column norms, the Householder
+       products) in pixel order, MINPACK's and so the reference's -- the default, the parity
+       contract; 1 = the fixed blocked tree of DESIGN.md §3.4b (faster; bit-exact to the oracle's
+       ORC_LM_TREE | ORC_LM_GRAM mode, but the normals leave the reference's by more than 1e-4 on a
+       share of the points, profiles/r05_full_parity.json) */
+    int lmReduction;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
@@ -512,6 +519,9 @@ int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, f
    be NULL (0..ndev-1); FM3D_ERR_INVALID when a device index is not visible (fewer GPUs than asked
    for) or repeats; FM3D_ERR_UNSUPPORTED when RCCL (librccl.so.1) cannot be loaded. */
 typedef struct fm3d_mgpu fm3d_mgpu;
+/* the GPUs visible to this process (hipGetDeviceCount; 0 when HIP finds none): what a multi-GPU
+   host checks before fm3d_mgpu_create, without loading another runtime (bench.py --gpus N) */
+int fm3d_device_count(int *n);
 int fm3d_mgpu_create(const fm3d_settings *s, int ndev, const int *devices, int shares, int block, fm3d_mgpu **out);
 void fm3d_mgpu_destroy(fm3d_mgpu *m);
 const char *fm3d_mgpu_last_error(const fm3d_mgpu *m);

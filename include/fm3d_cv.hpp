@@ -36,7 +36,7 @@
  *     <image>.desc.f32 (N x 128 float32) -- FeatureOptions.ExtractorType ORB / BRISK / FREAK
  *     selects Hamming matching on <image>.desc.u8 rows of 32 / 64 bytes (descriptorsmatcher.cpp:64-71);
  *   - the matcher is exact brute force, ties to the lowest train index;
- *   - extractDescriptorsFromPatches runs the settings' SURF, SIFT, ORB or BRISK extractor on the GPU;
+ *   - extractDescriptorsFromPatches runs the settings' SURF, SIFT, ORB, BRISK or FREAK extractor on the GPU;
  *   - the PCL viewer is visual only: start/stopVisualizerThread and the view* functions are
  *     no-ops; drawMatches / drawBackProjectedPoints draw with plain loops, in the reference's
  *     colours (cv::RNG(0xFFF0FF0F), random_color);

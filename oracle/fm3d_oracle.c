@@ -34,7 +34,9 @@
  * Two LM modes, both MINPACK lmdif with Householder qrfac and every m_dat-long
  * sum in pixel (index) order:
  *   ORC_LM_STRICT  : libm transcendentals (sin/cos/atan2/exp) -- the reference's;
- *   ORC_LM_DETMATH : the deterministic transcendentals of include/fm3d_detmath.h.
+ *   ORC_LM_DETMATH : the correctly rounded transcendentals of include/fm3d_crmath.h (round 5;
+ *                    before, the 1-ulp polynomials of include/fm3d_detmath.h, which the NCC
+ *                    hypotheses keep: ORC_DET_1ULP).
  *                    THE GPU CONTRACT: the LM kernel (csrc/fm3d_lm2.hip) equals this
  *                    mode bit for bit (statuses, lmdif info / nfev per level, normals);
  *                    STRICT is the north_star's 1e-4 comparison.
@@ -49,6 +51,7 @@
 #include <omp.h>
 #endif
 #include "fm3d_detmath.h"
+#include "fm3d_crmath.h"
 
 #define ORC_API __attribute__((visibility("default")))
 
@@ -616,6 +619,15 @@ enum { ORC_LM_STRICT = 0, ORC_LM_DETMATH = 2 };
    The user-break mapping (evaluate sets *info < 0 -> lmdif returns -> status.info = 11) is the
    same in both. */
 enum { ORC_LMV_FDFLOOR = 4, ORC_LMV_ENORM = 8, ORC_LMV_DWARFEXIT = 16, ORC_LMV_TOL1E14 = 32 };
+/* Reduction modes.  Default: every m_dat-long sum in pixel order (MINPACK's, the
+   reference's).  ORC_LM_TREE: every m_dat-long sum as the fixed blocked tree of orc_tree_finish.
+   ORC_LM_GRAM (with TREE): the 2-column Householder QR from the tree sums of the Jacobian sweep
+   (column norms, a_p.a_q, a_p.f, a_q.f) where it is well conditioned, the Householder passes with
+   tree sums elsewhere (orc_qr_tree). */
+enum { ORC_LM_TREE = 64, ORC_LM_GRAM = 128 };
+/* the Gram form is used when ||a_q'||^2 = S_qq - r01^2 > ORC_GRAM_C * S_qq (relative cancellation error
+   below 2 eps / ORC_GRAM_C) */
+#define ORC_GRAM_C 1e-6
 static int orc_lmv_enorm = 0; /* set from the mode before the (parallel) point loop; read-only after */
 
 typedef struct {
@@ -663,28 +675,43 @@ static void orc_update_I1(orc_lmdata *D)
     }
 }
 
+/* DETMATH takes the correctly rounded functions of fm3d_crmath.h (the LM kernel's), or with
+   ORC_DET_1ULP the 1-ulp polynomials of fm3d_detmath.h (the NCC hypotheses: csrc/fm3d_ncc.hip).
+   Attribution switches (tools/full_parity.py): with ORC_LM_DETMATH, libm's function
+   for one transcendental at a time. */
+enum { ORC_LIBM_SIN = 256, ORC_LIBM_COS = 512, ORC_LIBM_ATAN2 = 1024, ORC_LIBM_EXP = 2048, ORC_DET_1ULP = 4096 };
+static double orc_fsin(int mode, double x)
+{
+    if (!(mode & ORC_LM_DETMATH) || (mode & ORC_LIBM_SIN)) return sin(x);
+    return (mode & ORC_DET_1ULP) ? fm3d_sin(x) : fm3d_sin_cr(x);
+}
+static double orc_fcos(int mode, double x)
+{
+    if (!(mode & ORC_LM_DETMATH) || (mode & ORC_LIBM_COS)) return cos(x);
+    return (mode & ORC_DET_1ULP) ? fm3d_cos(x) : fm3d_cos_cr(x);
+}
+static double orc_fatan2(int mode, double y, double x)
+{
+    if (!(mode & ORC_LM_DETMATH) || (mode & ORC_LIBM_ATAN2)) return atan2(y, x);
+    return (mode & ORC_DET_1ULP) ? fm3d_atan2(y, x) : fm3d_atan2_cr(y, x);
+}
+static double orc_fexp(int mode, double x)
+{
+    if (!(mode & ORC_LM_DETMATH) || (mode & ORC_LIBM_EXP)) return exp(x);
+    return (mode & ORC_DET_1ULP) ? fm3d_exp(x) : fm3d_exp_cr(x);
+}
+
 static void orc_sph2car(int mode, double phi, double theta, double n[3])
 {   /* tools.cpp:772-777 */
-    if (!(mode & ORC_LM_DETMATH)) {
-        n[0] = cos(theta) * cos(phi);
-        n[1] = cos(theta) * sin(phi);
-        n[2] = sin(theta);
-    } else {
-        n[0] = fm3d_cos(theta) * fm3d_cos(phi);
-        n[1] = fm3d_cos(theta) * fm3d_sin(phi);
-        n[2] = fm3d_sin(theta);
-    }
+    n[0] = orc_fcos(mode, theta) * orc_fcos(mode, phi);
+    n[1] = orc_fcos(mode, theta) * orc_fsin(mode, phi);
+    n[2] = orc_fsin(mode, theta);
 }
 
 static void orc_car2sph(int mode, const double v[3], double *phi, double *theta)
 {   /* tools.cpp:767-771 */
-    if (!(mode & ORC_LM_DETMATH)) {
-        *theta = atan2(v[2], sqrt(v[0] * v[0] + v[1] * v[1]));
-        *phi = atan2(v[1], v[0]);
-    } else {
-        *theta = fm3d_atan2(v[2], sqrt(v[0] * v[0] + v[1] * v[1]));
-        *phi = fm3d_atan2(v[1], v[0]);
-    }
+    *theta = orc_fatan2(mode, v[2], sqrt(v[0] * v[0] + v[1] * v[1]));
+    *phi = orc_fatan2(mode, v[1], v[0]);
 }
 
 /* evaluateNormal (normaloptimizer.cpp:65-149).  Returns 0 or a status code. */
@@ -711,13 +738,8 @@ static int orc_eval(orc_lmdata *D, const double *par, double *fvec)
     if (!D->I1_ok) return ORC_ST_ABORT_PIX1;
     /* weight (:125-142); abs() is std::abs(double) under the reference's <cmath> */
     if (fabs(theta) - M_PI / 2 > 0 || fabs(phi) - M_PI > 0) {
-        if (!(D->mode & ORC_LM_DETMATH)) {
-            w_theta = exp(fabs(theta) - M_PI / 2) + 1;
-            w_phi = exp(fabs(phi) - M_PI + 1) + 1;
-        } else {
-            w_theta = fm3d_exp(fabs(theta) - M_PI / 2) + 1;
-            w_phi = fm3d_exp(fabs(phi) - M_PI + 1) + 1;
-        }
+        w_theta = orc_fexp(D->mode, fabs(theta) - M_PI / 2) + 1;
+        w_phi = orc_fexp(D->mode, fabs(phi) - M_PI + 1) + 1;
     }
     w = w_phi * w_theta;
     /* projectPointsToImage2 (:591-644) and the residual (:145-148) */
@@ -808,6 +830,61 @@ static double orc_enorm(int n, const double *x)
         return sqrt(x3max * ((s2 / x3max) + (x3max * s3)));
     }
     return x3max * sqrt(s3);
+}
+
+/* ---- ORC_LM_TREE: every m_dat-long sum as the LM kernel's fixed blocked tree ----
+   (csrc/fm3d_lm2.hip, TREE).  Entry e (its absolute neighbourhood-entry index) belongs
+   to lane l = e % 64 of chunk e / 64.  acc[l] is the sequential sum, from +0, of the lane's terms in
+   chunk order; then the xor butterfly p[l] = p[l] + p[l ^ o] for o = 32, 16, ..., 1.  IEEE addition
+   is commutative, so every lane ends with the same value: the sum. */
+#define ORC_TL 64
+typedef struct {
+    double acc[ORC_TL];
+} orc_tree;
+static void orc_tree_init(orc_tree *t) { memset(t, 0, sizeof *t); }
+static inline void orc_tree_add(orc_tree *t, int e, double v) { t->acc[e % ORC_TL] += v; }
+static double orc_tree_finish(const orc_tree *t)
+{
+    double p[ORC_TL], q[ORC_TL];
+    int l, o;
+    memcpy(p, t->acc, sizeof p);
+    for (o = ORC_TL / 2; o > 0; o >>= 1) {
+        for (l = 0; l < ORC_TL; l++) q[l] = p[l] + p[l ^ o];
+        memcpy(p, q, sizeof p);
+    }
+    return p[0];
+}
+/* the enorm of x[j0..n) (entries at their absolute positions): sqrt of the tree sum of squares when
+   every component lies in MINPACK's intermediate range or is zero (enorm's own result there is
+   sqrt(s2)); otherwise MINPACK's sequential enorm (a chunk with a value outside that range: the
+   kernel's rare serial path) */
+static int orc_enorm_slow(int j0, int n, const double *x)
+{
+    const double rdwarf = orc_lmv_enorm ? sqrt(DBL_MIN) : 3.834e-20, rgiant = orc_lmv_enorm ? sqrt(DBL_MAX) : 1.304e19;
+    const double agiant = rgiant / (double)(n - j0);
+    int i;
+    for (i = j0; i < n; i++) {
+        double xa = fabs(x[i]);
+        if (!(xa < agiant) || (xa <= rdwarf && xa != 0.)) return 1;
+    }
+    return 0;
+}
+static double orc_enorm_tree(int j0, int n, const double *x)
+{
+    orc_tree t;
+    int i;
+    if (orc_enorm_slow(j0, n, x)) return orc_enorm(n - j0, x + j0);
+    orc_tree_init(&t);
+    for (i = j0; i < n; i++) orc_tree_add(&t, i, x[i] * x[i]);
+    return sqrt(orc_tree_finish(&t));
+}
+static double orc_dot_tree(int j0, int n, const double *a, const double *b)
+{
+    orc_tree t;
+    int i;
+    orc_tree_init(&t);
+    for (i = j0; i < n; i++) orc_tree_add(&t, i, a[i] * b[i]);
+    return orc_tree_finish(&t);
 }
 
 /* qrsolv (MINPACK), r column-major with leading dimension ldr */
@@ -945,6 +1022,72 @@ done:
 #undef R_
 }
 
+/* qrfac with column pivoting + lmdif's qtf for n = 2 with the tree sums (ORC_LM_TREE).  The same
+   steps as orc_jac_qr's Householder form, every m-long sum an orc_tree over absolute entry positions.
+   With ORC_LM_GRAM the Householder quantities come from the tree sums of the Jacobian sweep, by
+   exact identities of the reflections (H0 = I - v v^T / v0, v = a_p / s0 + e0, s0 = +-||a_p||):
+     r00 = -s0,  r01 = (H0 a_q)_0 = -(a_p.a_q) / s0,  qtf0 = (H0 f)_0 = -(a_p.f) / s0,
+     ||(H0 a_q)_{1..}||^2 = S_qq - r01^2,  s1 = +-sqrt(that) with the sign of (H0 a_q)_1,
+     r11 = -s1,  qtf1 = -((a_q.f) - r01 qtf0) / s1
+   where (H0 a_q)_1 = a_q1 - t v1, t = ((a_p.a_q) / s0 + a_q0) / v0.  Used when every column value is
+   in enorm's intermediate range (or zero), s0 != 0, the sums are finite and S_qq - r01^2 >
+   ORC_GRAM_C * S_qq; otherwise the Householder form. */
+static void orc_qr_tree(int mode, int m, double *fjac, const double *fvec, double *wa4, double r[4], double qtf[2],
+                        double acnorm[2], int ipvt[2])
+{
+    double rdiag[2], ajnorm, sum, temp;
+    int i, j, k, pc;
+    for (j = 0; j < 2; j++) acnorm[j] = orc_enorm_tree(0, m, &fjac[j * m]);
+    pc = acnorm[1] > acnorm[0] ? 1 : 0;
+    ipvt[0] = pc;
+    ipvt[1] = 1 - pc;
+    if (pc) {
+        for (i = 0; i < m; i++) { temp = fjac[i]; fjac[i] = fjac[m + i]; fjac[m + i] = temp; }
+    }
+    if ((mode & ORC_LM_GRAM) && !orc_enorm_slow(0, m, fjac) && !orc_enorm_slow(0, m, fjac + m) && acnorm[pc] != 0.) {
+        const double *ap = fjac, *aq = fjac + m;
+        double Spq = orc_dot_tree(0, m, ap, aq), Spf = orc_dot_tree(0, m, ap, fvec), Sqf = orc_dot_tree(0, m, aq, fvec);
+        double Sqq = orc_dot_tree(0, m, aq, aq);
+        double s0 = ap[0] < 0. ? -acnorm[pc] : acnorm[pc];
+        double r01 = -(Spq / s0), qtf0 = -(Spf / s0), d = Sqq - r01 * r01;
+        if (isfinite(Spq) && isfinite(Spf) && isfinite(Sqf) && isfinite(Sqq) && d > ORC_GRAM_C * Sqq) {
+            double v0 = ap[0] / s0 + 1., v1 = ap[1] / s0, t = (Spq / s0 + aq[0]) / v0, a1 = aq[1] - t * v1;
+            double s1 = sqrt(d);
+            if (a1 < 0.) s1 = -s1;
+            r[0] = -s0; r[1] = 0.; r[2] = r01; r[3] = -s1;
+            qtf[0] = qtf0;
+            qtf[1] = -((Sqf - r01 * qtf0) / s1);
+            return;
+        }
+    }
+    /* the Householder form (MINPACK qrfac, n = 2; the rdiag update of column 1 after step 0 does not
+       reach the result for n = 2) */
+    for (j = 0; j < 2; j++) {
+        ajnorm = j == 0 ? acnorm[pc] : orc_enorm_tree(1, m, &fjac[m]);
+        if (ajnorm == 0.) { rdiag[j] = 0.; continue; }
+        if (fjac[j * m + j] < 0.) ajnorm = -ajnorm;
+        for (i = j; i < m; i++) fjac[j * m + i] /= ajnorm;
+        fjac[j * m + j] += 1.;
+        for (k = j + 1; k < 2; k++) {
+            sum = orc_dot_tree(j, m, &fjac[j * m], &fjac[k * m]);
+            temp = sum / fjac[j * m + j];
+            for (i = j; i < m; i++) fjac[k * m + i] -= temp * fjac[j * m + i];
+        }
+        rdiag[j] = -ajnorm;
+    }
+    for (i = 0; i < m; i++) wa4[i] = fvec[i];
+    for (j = 0; j < 2; j++) {
+        if (fjac[j * m + j] != 0.) {
+            sum = orc_dot_tree(j, m, &fjac[j * m], wa4);
+            temp = -sum / fjac[j * m + j];
+            for (i = j; i < m; i++) wa4[i] += fjac[j * m + i] * temp;
+        }
+        fjac[j * m + j] = rdiag[j];
+        qtf[j] = wa4[j];
+    }
+    r[0] = fjac[0]; r[1] = 0.; r[2] = fjac[m + 0]; r[3] = fjac[m + 1];
+}
+
 /* Jacobian + QR.  Output: r (2x2 column-major upper triangle), qtf, acnorm,
    ipvt.  Returns 0 or a failure status of one of the two evaluations. */
 static int orc_jac_qr(orc_lmdata *D, double *x, const double *fvec, double eps,
@@ -965,6 +1108,10 @@ static int orc_jac_qr(orc_lmdata *D, double *x, const double *fvec, double eps,
         x[j] = temp;
         if (st) return st;
         for (i = 0; i < m; i++) fjac[j * m + i] = (wa4[i] - fvec[i]) / h[j];
+    }
+    if (D->mode & ORC_LM_TREE) {
+        orc_qr_tree(D->mode, m, fjac, fvec, wa4, r, qtf, acnorm, ipvt);
+        return 0;
     }
     {
         /* qrfac with column pivoting (MINPACK), n = 2 */
@@ -1047,7 +1194,7 @@ static int orc_lmdif(orc_lmdata *D, double *x, double epsfcn, double *fvec, doub
     if (D->m < n) { *nfev_out = 0; return 0; }
     st = orc_eval(D, x, fvec);
     if (st) { *nfev_out = (int)D->nfev; return -st; }
-    fnorm = orc_enorm(D->m, fvec);
+    fnorm = (D->mode & ORC_LM_TREE) ? orc_enorm_tree(0, D->m, fvec) : orc_enorm(D->m, fvec);
     if ((D->mode & ORC_LMV_DWARFEXIT) && fnorm <= LM_DWARF) { *nfev_out = (int)D->nfev; return 0; }
     for (;;) {
         st = orc_jac_qr(D, x, fvec, eps, fjac, wa4, tmp, r, qtf, acnorm, ipvt);
@@ -1090,7 +1237,7 @@ static int orc_lmdif(orc_lmdata *D, double *x, double epsfcn, double *fvec, doub
             if (iter == 1) delta = delta < pnorm ? delta : pnorm;
             st = orc_eval(D, wa2, wa4);
             if (st) { *nfev_out = (int)D->nfev; return -st; }
-            fnorm1 = orc_enorm(D->m, wa4);
+            fnorm1 = (D->mode & ORC_LM_TREE) ? orc_enorm_tree(0, D->m, wa4) : orc_enorm(D->m, wa4);
             actred = -1.;
             if (p1 * fnorm1 < fnorm) actred = 1. - (fnorm1 / fnorm) * (fnorm1 / fnorm);
             for (j = 0; j < n; j++) {
@@ -1272,14 +1419,14 @@ ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const
         orc_project1(cam, I, Z, X[0], X[1], X[2], &ccx, &ccy);
         inv = 1. / sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
         g[0] = X[0] * inv; g[1] = X[1] * inv; g[2] = X[2] * inv;
-        orc_car2sph(ORC_LM_DETMATH, g, &phi0, &theta0);
+        orc_car2sph(ORC_LM_DETMATH | ORC_DET_1ULP, g, &phi0, &theta0);
         for (hh = 0; hh < H; hh++) {
             const int ip = hh / Htheta, it = hh - ip * Htheta;
             const double dphi = span * (double)(2 * ip + 1 - Hphi) / Hphi;
             const double dtheta = span * (double)(2 * it + 1 - Htheta) / Htheta;
             double n[3], mm, S[5][64], T[5], sc = -2.;
             int m = 0, fail = 0, o;
-            orc_sph2car(ORC_LM_DETMATH, phi0 + dphi, theta0 + dtheta, n);
+            orc_sph2car(ORC_LM_DETMATH | ORC_DET_1ULP, phi0 + dphi, theta0 + dtheta, n);
             mm = n[0] * X[0] + n[1] * X[1] + n[2] * X[2];
             memset(S, 0, sizeof(S));
             e = 0;
@@ -1325,7 +1472,7 @@ ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const
         best[p] = bestH;
         if (bestH >= 0) {
             const int ip = bestH / Htheta, it = bestH - ip * Htheta;
-            orc_sph2car(ORC_LM_DETMATH, phi0 + span * (double)(2 * ip + 1 - Hphi) / Hphi,
+            orc_sph2car(ORC_LM_DETMATH | ORC_DET_1ULP, phi0 + span * (double)(2 * ip + 1 - Hphi) / Hphi,
                         theta0 + span * (double)(2 * it + 1 - Htheta) / Htheta, normals + 3 * (size_t)p);
         } else {
             normals[3 * p] = g[0]; normals[3 * p + 1] = g[1]; normals[3 * p + 2] = g[2];

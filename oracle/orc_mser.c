@@ -40,8 +40,9 @@
  *             run over the points in region-list order.  hypot is sqrt(p^2 + beta^2) and atan2 / sin are
  *             fm3d_detmath.h's (the GPU evaluates the same expressions); a zero singular value's left
  *             vector (OpenCV draws a random one) is never used by the back substitution and is left as is.
- * The centroid's float sums are exact (integer coordinates, sum < 2^24 for every region this detector
- * can emit at VGA sizes), so they are order independent.
+ * The centroid's float sums run in region-list order (OpenCV's).  The GPU sums lane-strided + tree
+ * where every partial sum stays below 2^24 (exact integers: any order gives these bits) and in list
+ * order on one lane elsewhere (wide images with large regions).
  */
 #include <float.h>
 #include <math.h>

@@ -27,6 +27,14 @@ def test_cmake_builds_library_oracle_and_examples(fm3d, tmp_path):
     missing = [s for s in fm3d.EXPORTS if s not in syms]
     assert not missing, missing
     assert (b / "liboracle.so").exists()
+    # the CMake-built oracle holds every restatement the Makefile's does, MSER included
+    onm = subprocess.run(["nm", "-D", "--defined-only", str(b / "liboracle.so")], capture_output=True,
+                         text=True).stdout
+    osyms = {line.split()[-1] for line in onm.splitlines() if line.strip()}
+    for sym in ("orc_optimize_normals", "orc_mser_detect", "orc_mser_regions", "orc_freak_compute", "orc_sift_detect"):
+        assert sym in osyms, sym
+    import ctypes
+    ctypes.CDLL(str(b / "liboracle.so")).orc_mser_detect  # loads, as tests/test_mser_oracle.py loads it
     for ex in ("fm3d_main", "main_dropin", "mosaic_demo"):
         assert (b / "examples" / ex).exists(), ex
     r = subprocess.run([str(b / "examples" / "main_dropin")], capture_output=True, text=True, timeout=60)

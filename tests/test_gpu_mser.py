@@ -97,6 +97,24 @@ def test_mser_large_image_hbm_bitmap(fm3d, orc):
     assert len(r) > 50
 
 
+def test_mser_wide_image_large_regions_centroid(fm3d, orc):
+    """a wide image with large regions, where a region's coordinate sum passes 2^24 (the
+    float centroid is then no longer exact in any order): the GPU sums such a region in list order,
+    as OpenCV and the oracle, and the keypoints stay bit-identical"""
+    img = _blurred(96, 3000, 10.0, 21)
+    kw = dict(min_area=1000, max_area=60000)
+    ctx, _ = _ctx(fm3d)
+    try:
+        k = fm3d.Features(ctx).mser(img, **kw)
+    finally:
+        ctx.close()
+    regs = orc.mser_regions(img, **kw)
+    big = [len(p) * int(p.max()) for _, p in regs]
+    assert max(big) >= 1 << 24, max(big)  # the case the sequential sum exists for
+    _same_kpts(k, orc.mser_detect(img, **kw))
+    assert len(k) > 3
+
+
 def test_mser_batch_equals_single(fm3d, orc, synth):
     """fm3d_mser_detect_batch: every image's floods side by side; each image's keypoints equal its own
     fm3d_mser_detect (and the oracle), including an image without regions in the middle"""

@@ -996,6 +996,42 @@ def test_pipeline_linked_lm_launch_equals_run(fm3d, synth):
         assert st["lm"]["evaluations"] == ref[w][1]["lm"]["evaluations"]
 
 
+def test_pipeline_linked_member_waited_after_leader_resubmit(fm3d, synth):
+    """submit(member), submit(leader), wait(leader), submit(leader), wait(member).  The
+    leader's second launch resets its own LM counters; the member's epilogue reads its own copy of
+    the linked launch's counters, so it reports that launch's (equal to what the leader reported for
+    it) and its records equal its own fm3d_pipeline_run."""
+    pairs = [synth.make_frame_pair(3000, seed=11), synth.make_frame_pair(2500, seed=12)]
+    s = _settings(fm3d, pairs[0].cam, pixelsRay=12, pyramids=2)
+    ctx, pipe = _pipe_ctx(fm3d, s, pairs[0].g12)
+    try:
+        ref = []
+        for fp in pairs:
+            pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+            k, _ = pipe.run()
+            ref.append(pipe.records(k))
+    finally:
+        ctx.close()
+    cs = [_pipe_ctx(fm3d, s, pairs[0].g12) for _ in range(2)]
+    member, leader = cs[0][1], cs[1][1]
+    try:
+        member.link(leader)
+        a, b = pairs[0], pairs[1]
+        member.submit(a.desc1, a.desc2, a.kp1, a.kp2, a.img1, a.img2)
+        leader.submit(b.desc1, b.desc2, b.kp1, b.kp2, b.img1, b.img2)
+        rec_l1, st_l1 = leader.wait()
+        leader.submit(a.desc1, a.desc2, a.kp1, a.kp2, a.img1, a.img2)  # its own launch: counters reset
+        rec_m, st_m = member.wait()
+        rec_l2, st_l2 = leader.wait()
+    finally:
+        for c, _ in cs:
+            c.close()
+    assert rec_m.tobytes() == ref[0].tobytes()
+    assert rec_l1.tobytes() == ref[1].tobytes() and rec_l2.tobytes() == ref[0].tobytes()
+    for key in ("passes", "cycles_total", "cycles_terms", "wall_ticks_max"):
+        assert st_m["lm"][key] == st_l1["lm"][key] > 0, key
+
+
 def test_pipeline_linked_four_pairs(fm3d, synth):
     """A leader with three members: four frame pairs in one LM launch, each pair's records equal
     its own fm3d_pipeline_run; a member without a queued pair is skipped by its leader."""
@@ -1124,6 +1160,11 @@ def test_mgpu_submit_wait_stream_equals_run(fm3d, synth):
         # a pair on a member set waited for before its leader set takes one: its LM alone
         mg.submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
         outs.append(mg.wait())
+        # a submit restaged set 0: run without a new upload fails loudly, with one it works
+        with pytest.raises(fm3d.Fm3dError):
+            mg.run()
+        mg.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        outs.append(mg.run())
     finally:
         mg.close()
     assert k > 50
@@ -1157,6 +1198,28 @@ def test_bench_gpus_more_than_visible_exits_nonzero():
     assert r.returncode != 0
     assert f"--gpus {n}" in r.stderr and "visible" in r.stderr
     assert '"metric"' not in r.stdout
+
+
+@pytest.mark.timeout(400)
+def test_bench_mgpu_one_gpu_line_without_torch(tmp_path):
+    """`bench.py --gpus 1 --mgpu` (the one-process multi-GPU route on this box's
+    one GPU) never imports torch before fm3d_mgpu_create (the visible-device count comes from
+    libfm3d's fm3d_device_count), and its line carries the same-workload one-GPU value and the
+    efficiency the N-GPU lines report."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "line.json"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--mgpu", "--keypoints",
+                        "200000", "--steps", "2", "--warmup", "1", "--no-cpu", "--out", str(out)],
+                       capture_output=True, text=True, timeout=380)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(out.read_text())
+    assert line["torch_imported_at_mgpu_create"] is False
+    assert line["n_gpus"] == 1 and line["efficiency"] == 1.0 and line["value_one_gpu"] == line["value"] > 0
+    assert line["records_identical_across_steps"] is True
 
 
 @pytest.mark.timeout(500)
