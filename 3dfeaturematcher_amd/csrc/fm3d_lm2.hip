@@ -74,7 +74,8 @@ constexpr int kRS = (2 * kLM2Slots * kRow * 8 + 255) / 256 * 256 / 8;
 #define FM3D_EVAL_PIPE 1
 #endif
 
-enum PassKind2 { Q_IDLE = 0, Q_INIT, Q_LEVEL, Q_EVAL, Q_QR1, Q_QR2, Q_QR3, Q_DONE };
+// Q_GRAM (TREE only): the Jacobian columns' norms and Gram sums, one sweep after the Jacobian's
+enum PassKind2 { Q_IDLE = 0, Q_INIT, Q_LEVEL, Q_EVAL, Q_QR1, Q_QR2, Q_QR3, Q_GRAM, Q_DONE };
 enum SumKind { S_NONE = 0, S_ENORM, S_DOT };
 
 typedef __attribute__((address_space(1))) double gdouble;
@@ -367,6 +368,18 @@ struct Ctl2 {
             qr2(S, P);
         }
     }
+    // TREE: one sweep over the stored Jacobian columns for their norms and Gram sums (Q_GRAM)
+    __device__ void gram_pass(SlotS2& S, SlotP2& P) {
+        P.pass = Q_GRAM;
+        P.len = S.m;
+        P.pivot = 0;
+        P.wF = S.wF;
+        P.w[0] = S.wJ[0];
+        P.w[1] = S.wJ[1];
+        P.hj[0] = S.s.h[0];
+        P.hj[1] = S.s.h[1];
+        P.agiant = 1.304e19 / (double)S.m;
+    }
     // TREE: the 2-column QR from the Jacobian sweep's tree sums where it is well conditioned
     // (oracle/fm3d_oracle.c orc_qr_tree, ORC_LM_GRAM: the same operations), else the Householder
     // passes with tree sums
@@ -478,7 +491,7 @@ struct Ctl2 {
                 s.fnorm = o.nrm[0];
                 jac_pass(S, P);
             } else if (S.ekind == E_JAC) {
-                s.acnorm[0] = o.nrm[0];
+                if (!tree) s.acnorm[0] = o.nrm[0];
                 count_eval(S);  // fdjac2's call for column 1
                 if (S.bNaN) {
                     abort_level(S, P, FM3D_ST_NAN_NORMAL);
@@ -489,11 +502,12 @@ struct Ctl2 {
                     abort_level(S, P, code);
                     return;
                 }
-                s.acnorm[1] = o.nrm[1];
-                if (tree)
-                    start_qr_tree(S, P, o);
-                else
+                if (tree) {
+                    gram_pass(S, P);
+                } else {
+                    s.acnorm[1] = o.nrm[1];
                     start_qr(S, P);
+                }
             } else {
                 bool accepted;
                 int info = lm_after_trial(s, o.nrm[0], &accepted);
@@ -534,6 +548,10 @@ struct Ctl2 {
             } else {
                 finalize_qr(S, P, S.wa4s);
             }
+        } else if (ps == Q_GRAM) {
+            S.s.acnorm[0] = o.nrm[0];
+            S.s.acnorm[1] = o.nrm[1];
+            start_qr_tree(S, P, o);
         } else if (ps == Q_QR3) {
             const double tq1 = -o.sum[0] / S.usecond;
             finalize_qr(S, P, S.wa4s + S.usecond * tq1);
@@ -1349,15 +1367,9 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 t1 = enorm_term2(v1, agiant, slow1);
                             }
                             if constexpr (TREE) {
-                                ta0 += t0;
-                                tslow0 |= slow0;
-                                if (NEV == 2) {
-                                    const double Fm = sel_mask(wF * L.dF, in);
-                                    ta1 += t1;
-                                    ta2 += v0 * v1;
-                                    ta3 += v0 * Fm;
-                                    ta4 += v1 * Fm;
-                                    tslow1 |= slow1;
+                                if (!JAC) {  // the Jacobian's sums come from the Q_GRAM sweep
+                                    ta0 += t0;
+                                    tslow0 |= slow0;
                                 }
                             } else {
                                 prod.write_terms<NEV == 2>(cbase + k, t0, v0, slow0, t1, v1, slow1);
@@ -1412,6 +1424,13 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 // evaluateNormal :145-148, fdjac2 forward differences
                                 const float dI0 = S.i1 - bilinear_f(S.a.x, S.a.y, S.xf0, S.yf0);
                                 const float dI1 = S.i1 - bilinear_f(S.c.x, S.c.y, S.xf1, S.yf1);
+                                if constexpr (TREE) {
+                                    // the columns' values and sums come from the Q_GRAM sweep
+                                    const auto* pc = sb();
+                                    *(gfloat*)(pc->slabDJ0 + oo) = dI0;
+                                    *(gfloat*)(pc->slabDJ1 + oo) = dI1;
+                                    return;
+                                }
                                 const double F = wF * (double)S.dF;
                                 double v0 = jdiv(w0 * (double)dI0 - F, h0, y0, mok0);
                                 double v1 = jdiv(w1 * (double)dI1 - F, h1, y1, mok1);
@@ -1420,26 +1439,13 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 bool slow0, slow1;
                                 const double t0 = enorm_term2(v0, agiant, slow0);
                                 const double t1 = enorm_term2(v1, agiant, slow1);
-                                if constexpr (!TREE) prod.reserve(cbase + k);
+                                prod.reserve(cbase + k);
                                 {
                                     const auto* pc = sb();
                                     *(gfloat*)(pc->slabDJ0 + oo) = dI0;
                                     *(gfloat*)(pc->slabDJ1 + oo) = dI1;
                                 }
-                                if constexpr (TREE) {
-                                    // the column norms and the Gram sums of the QR (start_qr_tree); F of
-                                    // the entries past len is slab padding: zeroed
-                                    const double Fm = sel_mask(F, S.ok0 | S.ok1);
-                                    ta0 += t0;
-                                    ta1 += t1;
-                                    ta2 += v0 * v1;
-                                    ta3 += v0 * Fm;
-                                    ta4 += v1 * Fm;
-                                    tslow0 |= slow0;
-                                    tslow1 |= slow1;
-                                } else {
-                                    prod.write_terms<true>(cbase + k, t0, v0, slow0, t1, v1, slow1);
-                                }
+                                prod.write_terms<true>(cbase + k, t0, v0, slow0, t1, v1, slow1);
                             };
                             // A stage past the last chunk computes garbage from slab padding (its
                             // entries are not `in`: no failures); no branch between gathers and use
@@ -1665,9 +1671,12 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                     // Entries past len compute garbage the edge chunks zero.
                     const double bnum = 256. * 1.01 * (wp + wq + 2. * wF);
                     const double bap = bnum / fabs(hp), baq = bnum / fabs(hq);
-                    const bool fast = !p.safe && t0f && q0f && mokp && mokq && moka0 && bnum < 1e99 && bap < 1e99 &&
-                                      baq < 1e99 && (pass != Q_QR3 || (t1f && moka1 &&
-                                      baq + fabs(tq) * (bap / fabs(ajn0s) + 1.) < 1e99));
+                    // (Q_GRAM: the columns themselves, no Householder quotient)
+                    bool fast = !p.safe && t0f && q0f && mokp && mokq && moka0 && bnum < 1e99 && bap < 1e99 &&
+                                baq < 1e99 && (pass != Q_QR3 || (t1f && moka1 &&
+                                baq + fabs(tq) * (bap / fabs(ajn0s) + 1.) < 1e99));
+                    if constexpr (TREE)
+                        if (pass == Q_GRAM) fast = !p.safe && mokp && mokq && bnum < 1e99 && bap < 1e99 && baq < 1e99;
                     auto run = [&](auto kindc, auto fastc) {
                         constexpr int KIND = decltype(kindc)::value;
                         constexpr bool FAST = decltype(fastc)::value;
@@ -1712,6 +1721,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                         struct Terms {
                             double t0, t1, a;  // a: QR2's raw value, published instead of t0 if slow
                             bool slow;
+                            double g0, g1, g2;  // Q_GRAM: a_0.a_1, a_0.f, a_1.f terms (t0, t1: a_0^2, a_1^2)
+                            bool slow1;
                         };
                         auto chunk = [&](const Ld& L, int k, auto edgec) {
                             constexpr bool EDGE = decltype(edgec)::value;
@@ -1721,16 +1732,26 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             const double F = wF * (double)L.f;
                             const double ap = dv(wp * (double)L.p - F, hp, yp, mokp);
                             const double aq = dv(wq * (double)L.q - F, hq, yq, mokq);
-                            double t0 = 0., t1 = 0., a = 0.;
-                            bool slow = false;
-                            if (KIND == Q_QR1) {
+                            double t0 = 0., t1 = 0., a = 0., g0 = 0., g1 = 0., g2 = 0.;
+                            bool slow = false, slow1 = false;
+                            if constexpr (KIND == Q_GRAM) {
+                                // the columns (pivot 0: ap = a_0, aq = a_1), their squares (enorm) and
+                                // the Gram sums of start_qr_tree; entries past len add +0
+                                const double a0 = (EDGE && !in) ? 0. : ap, a1 = (EDGE && !in) ? 0. : aq;
+                                const double f = (EDGE && !in) ? 0. : F;
+                                t0 = enorm_term2(a0, agiant, slow);
+                                t1 = enorm_term2(a1, agiant, slow1);
+                                g0 = a0 * a1;
+                                g1 = a0 * f;
+                                g2 = a1 * f;
+                            } else if constexpr (KIND == Q_QR1) {
                                 // qrfac column j = 0: v = a_p / ajnorm (+1 on the diagonal); v*a_q, v*f
                                 double v = dv(ap, ajn0s, ya0, moka0);
                                 if (EDGE && e == 0) v = v + 1.;
                                 t0 = v * aq;
                                 t1 = v * F;
                                 if (EDGE && !in) t0 = t1 = 0.;
-                            } else if (KIND == Q_QR2) {
+                            } else if constexpr (KIND == Q_QR2) {
                                 // a_q' = a_q - temp * v below the diagonal -> ajnorm of column 1
                                 a = aq;
                                 if (FAST || t0f) a = a - tq * dv(ap, ajn0s, ya0, moka0);
@@ -1751,7 +1772,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                 t0 = u * wa;
                                 if (EDGE && !(in && e > 0)) t0 = 0.;
                             }
-                            return Terms{t0, t1, a, slow};
+                            return Terms{t0, t1, a, slow, g0, g1, g2, slow1};
                         };
                         // kQD chunks of loads in flight: this pass computes little per entry.  A
                         // buffer is refilled after its chunk is consumed (no register copies)
@@ -1778,7 +1799,13 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                                                                                : chunk(buf[j], kc, std::false_type());
                                     if constexpr (TREE) {
                                         ta0 += T.t0;
-                                        if (KIND == Q_QR1) ta1 += T.t1;
+                                        if (KIND == Q_QR1 || KIND == Q_GRAM) ta1 += T.t1;
+                                        if (KIND == Q_GRAM) {
+                                            ta2 += T.g0;
+                                            ta3 += T.g1;
+                                            ta4 += T.g2;
+                                            tslow1 |= T.slow1;
+                                        }
                                         tslow0 |= T.slow;
                                     } else {
                                         prod.reserve(cbase + kc);
@@ -1790,7 +1817,14 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             }
                         }
                     };
-                    if (fast) {
+                    if (TREE && pass == Q_GRAM) {
+                        if constexpr (TREE) {
+                            if (fast)
+                                run(std::integral_constant<int, Q_GRAM>(), std::true_type());
+                            else
+                                run(std::integral_constant<int, Q_GRAM>(), std::false_type());
+                        }
+                    } else if (fast) {
                         if (pass == Q_QR1)
                             run(std::integral_constant<int, Q_QR1>(), std::true_type());
                         else if (pass == Q_QR2)
@@ -1820,8 +1854,8 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 } else if constexpr (TREE) {
                     // ---- the pass's sums: the xor butterfly of the lanes' partial sums (every lane
                     // ends with the same value; ORC_LM_TREE's orc_tree_finish)
-                    const bool two = pass == Q_QR1 || (pass == Q_EVAL && nev == 2);
-                    const bool gram = jac && nev == 2;
+                    const bool two = pass == Q_QR1 || pass == Q_GRAM;
+                    const bool gram = pass == Q_GRAM;
                     for (int o = 32; o > 0; o >>= 1) {
                         ta0 += __shfl_xor(ta0, o);
                         if (two) ta1 += __shfl_xor(ta1, o);
@@ -1831,11 +1865,13 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                             ta4 += __shfl_xor(ta4, o);
                         }
                     }
-                    const bool en = pass == Q_EVAL || pass == Q_QR2;  // sums of squares: enorm
+                    // sums of squares (enorm): the residual, QR2's a_q', the Gram sweep's columns (the
+                    // Jacobian pass itself has no sums in TREE)
+                    const bool en = (pass == Q_EVAL && !jac) || pass == Q_QR2 || pass == Q_GRAM;
                     if (lane == 0) {
                         double r0 = ta0, r1 = ta1;
                         if (en) {
-                            r0 = tslow0 ? ctl.seq_enorm(SP, pass == Q_QR2 ? 3 : (jac ? 1 : 0), len) : sqrt(ta0);
+                            r0 = tslow0 ? ctl.seq_enorm(SP, pass == Q_QR2 ? 3 : (pass == Q_GRAM ? 1 : 0), len) : sqrt(ta0);
                             if (two) r1 = tslow1 ? ctl.seq_enorm(SP, 2, len) : sqrt(ta1);
                         }
                         OUT.nrm[0] = OUT.sum[0] = r0;

@@ -858,6 +858,17 @@ static double orc_tree_finish(const orc_tree *t)
    every component lies in MINPACK's intermediate range or is zero (enorm's own result there is
    sqrt(s2)); otherwise MINPACK's sequential enorm (a chunk with a value outside that range: the
    kernel's rare serial path) */
+/* tree-mode path counters (tests/test_gpu_lm_tree.py, tools/full_parity.py): [0] Jacobians whose QR
+   took the Gram form, [1] the Householder form (ill conditioned, a slow column or non-finite sums),
+   [2] sums of squares that took the sequential enorm, [3] the Householder form for a zero Jacobian */
+ORC_API long long orc_tree_stats[4];
+static void orc_tree_count(int k)
+{
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    orc_tree_stats[k]++;
+}
 static int orc_enorm_slow(int j0, int n, const double *x)
 {
     const double rdwarf = orc_lmv_enorm ? sqrt(DBL_MIN) : 3.834e-20, rgiant = orc_lmv_enorm ? sqrt(DBL_MAX) : 1.304e19;
@@ -873,7 +884,10 @@ static double orc_enorm_tree(int j0, int n, const double *x)
 {
     orc_tree t;
     int i;
-    if (orc_enorm_slow(j0, n, x)) return orc_enorm(n - j0, x + j0);
+    if (orc_enorm_slow(j0, n, x)) {
+        orc_tree_count(2);
+        return orc_enorm(n - j0, x + j0);
+    }
     orc_tree_init(&t);
     for (i = j0; i < n; i++) orc_tree_add(&t, i, x[i] * x[i]);
     return sqrt(orc_tree_finish(&t));
@@ -1057,11 +1071,13 @@ static void orc_qr_tree(int mode, int m, double *fjac, const double *fvec, doubl
             r[0] = -s0; r[1] = 0.; r[2] = r01; r[3] = -s1;
             qtf[0] = qtf0;
             qtf[1] = -((Sqf - r01 * qtf0) / s1);
+            orc_tree_count(0);
             return;
         }
     }
     /* the Householder form (MINPACK qrfac, n = 2; the rdiag update of column 1 after step 0 does not
        reach the result for n = 2) */
+    orc_tree_count(acnorm[pc] == 0. ? 3 : 1);
     for (j = 0; j < 2; j++) {
         ajnorm = j == 0 ? acnorm[pc] : orc_enorm_tree(1, m, &fjac[m]);
         if (ajnorm == 0.) { rdiag[j] = 0.; continue; }

@@ -14,7 +14,21 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
 F32, U8, BITS = 0, 1, 2
-STRICT, DETMATH = 0, 2  # libm transcendentals / fm3d_detmath.h (the GPU contract)
+STRICT, DETMATH = 0, 2  # libm transcendentals / fm3d_crmath.h (the GPU contract)
+TREE, GRAM = 64, 128    # fm3d_oracle.c ORC_LM_TREE / ORC_LM_GRAM: the LM kernel's lmReduction = 1 is DETMATH|TREE|GRAM
+LIBM_SIN, LIBM_COS, LIBM_ATAN2, LIBM_EXP, DET_1ULP = 256, 512, 1024, 2048, 4096  # ORC_LIBM_* / ORC_DET_1ULP
+
+
+def tree_stats(reset=False):
+    """orc_tree_stats: [Gram-form QRs, Householder-form QRs, sequential-enorm fallbacks, Householder-form
+    QRs of a zero Jacobian] of the tree
+    mode since the last reset (test infrastructure)."""
+    arr = (ctypes.c_longlong * 4).in_dll(lib(), "orc_tree_stats")
+    out = [int(v) for v in arr]
+    if reset:
+        for i in range(4):
+            arr[i] = 0
+    return out
 
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
