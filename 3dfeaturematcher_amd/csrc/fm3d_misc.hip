@@ -9,53 +9,70 @@ namespace fm3d {
 namespace {
 
 // ---------------- DLT triangulation ----------------
-// Null vector of the 4x4 DLT system: one-sided (Hestenes) Jacobi SVD, cyclic pair
-// order, up to 30 sweeps; the same arithmetic as oracle/fm3d_oracle.c
-// (orc_dlt_nullvec).  OpenCV's cvSVD (JacobiSVD) is not reproducible bit for bit;
-// both agree with numpy.linalg.svd to ~1e-12 (tests/golden).
+// Null vector of the 4x4 DLT system: one-sided (Hestenes) Jacobi SVD in the round-robin pair
+// order (0,1)+(2,3), (0,2)+(1,3), (0,3)+(1,2), up to 30 sweeps; the same arithmetic as
+// oracle/fm3d_oracle.c (orc_dlt_nullvec).  The two rotations of a step touch disjoint columns:
+// independent, so their dependent chains (three divisions and two square roots each) run side by
+// side -- half the latency of the cyclic order, which bounds this kernel (one wave per SIMD, a
+// ~800-cycle chain per rotation; tools/micro/tri_bench.hip).  The column indices are compile-time
+// constants (registers, no indexed moves).  OpenCV's cvSVD (JacobiSVD) is not reproducible bit for
+// bit; both agree with numpy.linalg.svd to ~1e-12 (tests/golden).
+template <int P, int Q>
+__device__ __forceinline__ bool jacobi_pair(double* A, double* V) {
+    double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        double ap = A[i * 4 + P], aq = A[i * 4 + Q];
+        alpha += ap * ap;
+        beta += aq * aq;
+        gamma += ap * aq;
+    }
+    if (gamma != 0. && fabs(gamma) > 1e-15 * sqrt(alpha * beta)) {
+        double zeta = (beta - alpha) / (2. * gamma);
+        double t = (zeta >= 0. ? 1. : -1.) / (fabs(zeta) + sqrt(1. + zeta * zeta));
+        double cs = 1. / sqrt(1. + t * t);
+        double sn = cs * t;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            double ap = A[i * 4 + P], aq = A[i * 4 + Q];
+            A[i * 4 + P] = cs * ap - sn * aq;
+            A[i * 4 + Q] = sn * ap + cs * aq;
+            ap = V[i * 4 + P];
+            aq = V[i * 4 + Q];
+            V[i * 4 + P] = cs * ap - sn * aq;
+            V[i * 4 + Q] = sn * ap + cs * aq;
+        }
+        return true;
+    }
+    return false;
+}
 __device__ inline void dlt_nullvec(double* A, double* v) {
     double V[16];
+#pragma unroll
     for (int i = 0; i < 16; i++) V[i] = (i % 5 == 0) ? 1. : 0.;
     for (int sweep = 0; sweep < 30; sweep++) {
-        bool rotated = false;
-        for (int p = 0; p < 3; p++)
-            for (int q = p + 1; q < 4; q++) {
-                double alpha = 0, beta = 0, gamma = 0;
-                for (int i = 0; i < 4; i++) {
-                    double ap = A[i * 4 + p], aq = A[i * 4 + q];
-                    alpha += ap * ap;
-                    beta += aq * aq;
-                    gamma += ap * aq;
-                }
-                if (gamma != 0. && fabs(gamma) > 1e-15 * sqrt(alpha * beta)) {
-                    double zeta = (beta - alpha) / (2. * gamma);
-                    double t = (zeta >= 0. ? 1. : -1.) / (fabs(zeta) + sqrt(1. + zeta * zeta));
-                    double cs = 1. / sqrt(1. + t * t);
-                    double sn = cs * t;
-                    for (int i = 0; i < 4; i++) {
-                        double ap = A[i * 4 + p], aq = A[i * 4 + q];
-                        A[i * 4 + p] = cs * ap - sn * aq;
-                        A[i * 4 + q] = sn * ap + cs * aq;
-                        ap = V[i * 4 + p];
-                        aq = V[i * 4 + q];
-                        V[i * 4 + p] = cs * ap - sn * aq;
-                        V[i * 4 + q] = sn * ap + cs * aq;
-                    }
-                    rotated = true;
-                }
-            }
+        bool rotated = jacobi_pair<0, 1>(A, V);
+        rotated |= jacobi_pair<2, 3>(A, V);
+        rotated |= jacobi_pair<0, 2>(A, V);
+        rotated |= jacobi_pair<1, 3>(A, V);
+        rotated |= jacobi_pair<0, 3>(A, V);
+        rotated |= jacobi_pair<1, 2>(A, V);
         if (!rotated) break;
     }
     double nrm[4];
+#pragma unroll
     for (int p = 0; p < 4; p++) {
         double s = 0;
+#pragma unroll
         for (int i = 0; i < 4; i++) s += A[i * 4 + p] * A[i * 4 + p];
         nrm[p] = s;
     }
     int best = 0;
+#pragma unroll
     for (int p = 1; p < 4; p++)
         if (nrm[p] < nrm[best]) best = p;
-    for (int i = 0; i < 4; i++) v[i] = V[i * 4 + best];
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = best == 0 ? V[i * 4] : best == 1 ? V[i * 4 + 1] : best == 2 ? V[i * 4 + 2] : V[i * 4 + 3];
 }
 
 // setKeypoints (singlecameratriangulator.cpp:145-171) + triangulate (:173-230), one

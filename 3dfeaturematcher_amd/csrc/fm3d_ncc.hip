@@ -44,14 +44,29 @@ __device__ __forceinline__ double xor_sum(double v) {
 //  * project1's NaN for an infinite r6 dropped (such a u or v is infinite or NaN: not good);
 //  * 0 <= u <= xmax as bits(u) <= bits(xmax): u is never -0.0 (the host hands the kernel a
 //    principal point of +0.0 for -0.0, fm3d_host.cpp lm_camera), negatives and NaNs lie above.
-// Returns good; fx, fy: the float sample coordinates; off: the bilinear window's byte offset.
-__device__ __forceinline__ bool ncc_geometry(const NccParams& p, double ux, double uy, double n0, double n1,
-                                             double n2, double mm, bool mok, double cm, unsigned long long xmaxb,
-                                             unsigned long long ymaxb, float& fx, float& fy, unsigned& off) {
+// (ncc_geometry_m.)
+typedef unsigned long long LaneMask;
+// v where the lane's bit of m is set, else 0 (v_cndmask with the SGPR mask as selector)
+__device__ __forceinline__ unsigned ncc_sel_u32(unsigned v, LaneMask m) {
+    asm("v_cndmask_b32_e64 %0, 0, %0, %1" : "+v"(v) : "s"(m));
+    return v;
+}
+// The tests as lane masks (each the ballot of one compare, combined with scalar ANDs; fm3d_lm2.hip
+// geometry2's form): good, the float sample coordinates, and the bilinear window's byte offset (0
+// where not good: the gather then reads the image's first bytes)
+struct NccGeo {
+    float fx, fy;
+    unsigned off;
+    LaneMask good;
+};
+__device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, double uy, double n0, double n1,
+                                                 double n2, double mm, bool mok, double cm,
+                                                 unsigned long long xmaxb, unsigned long long ymaxb) {
+    NccGeo g;
     const double nn = n0 * ux + n1 * uy + n2 * 1.;
     const double kk = mok ? div_nn(mm, nn, true) : mm / nn;
     const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-    const bool inbox = (fabs(P0) < cm) & (fabs(P1) < cm) & (P2 > 0.) & (P2 < cm);  // NaN fails
+    const LaneMask inbox = __ballot(fabs(P0) < cm) & __ballot(fabs(P1) < cm) & __ballot(P2 > 0.) & __ballot(P2 < cm);
     double x = p.R2[0] * P0 + p.R2[1] * P1 + p.R2[2] * P2 + p.t2[0];
     double y = p.R2[3] * P0 + p.R2[4] * P1 + p.R2[5] * P2 + p.t2[1];
     const double z = recip_z_lo(p.R2[6] * P0 + p.R2[7] * P1 + p.R2[8] * P2 + p.t2[2]);
@@ -69,30 +84,39 @@ __device__ __forceinline__ bool ncc_geometry(const NccParams& p, double ux, doub
     const double yd = y * cdist + p.cam.k[2] * a3 + p.cam.k[3] * a1;
     const double u = xd * p.cam.fx + p.cam.cx;
     const double v = yd * p.cam.fy + p.cam.cy;
-    const bool good = inbox & ((unsigned long long)__double_as_longlong(u) <= xmaxb) &
-                      ((unsigned long long)__double_as_longlong(v) <= ymaxb);
-    fx = (float)u;
-    fy = (float)v;
-    off = good ? (unsigned)((int)floorf(fy) * p.w + (int)floorf(fx)) : 0u;
-    return good;
+    g.good = inbox & __ballot((unsigned long long)__double_as_longlong(u) <= xmaxb) &
+             __ballot((unsigned long long)__double_as_longlong(v) <= ymaxb);
+    g.fx = (float)u;
+    g.fy = (float)v;
+    const unsigned o = __umul24((unsigned)(int)floorf(g.fy), (unsigned)p.w) + (unsigned)(int)floorf(g.fx);
+    g.off = ncc_sel_u32(o, g.good);
+    return g;
 }
-
-// getBilinearInterpPix32f on the gathered window (bilinear(): the same operations)
-__device__ __forceinline__ float ncc_bilinear(const uint8_t* img, unsigned off, int w, float x, float y) {
+// getBilinearInterpPix32f (tools.cpp:129-142) on the gathered window, with the fractions
+// x - floor(x), y - floor(y), as two-lane float vectors (v_pk_mul_f32 / v_pk_add_f32: each component
+// rounded as the scalar operation; fm3d_lm2.hip bilinear_f)
+typedef float ncc_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float ncc_bilinear_f(const uint8_t* img, unsigned off, int w, float x, float y) {
     typedef __attribute__((aligned(1))) const uint16_t u16u;
     const unsigned lo = *(u16u*)(img + off), hi = *(u16u*)(img + off + w);
-    const float x0 = floorf(x), y0 = floorf(y);
-    const float b00 = (float)(lo & 0xff), b01 = (float)(lo >> 8);
-    const float b10 = (float)(hi & 0xff), b11 = (float)(hi >> 8);
-    const float xm0 = 1.0f - (x - x0), xm1 = (x - x0);
-    const float ym0 = 1.0f - (y - y0), ym1 = (y - y0);
-    return xm0 * (b00 * ym0 + b10 * ym1) + xm1 * (b01 * ym0 + b11 * ym1);
+    const float xf = x - floorf(x), yf = y - floorf(y);
+    const ncc_f32x2 b0 = {(float)(lo & 0xff), (float)(lo >> 8)};  // b00, b01
+    const ncc_f32x2 b1 = {(float)(hi & 0xff), (float)(hi >> 8)};  // b10, b11
+    const float ym0 = 1.0f - yf, ym1 = yf;
+    const ncc_f32x2 sc = b0 * ym0 + b1 * ym1;
+    const ncc_f32x2 xm = {1.0f - xf, xf};
+    const ncc_f32x2 q = xm * sc;
+    return q.x + q.y;
 }
 
 // KPW: hypotheses per wave the register arrays hold (H <= 4 * KPW); sized to H so that 16 hypotheses
 // keep 4 per wave in registers (225 VGPRs at 8, 2 waves per SIMD)
-template <int KPW, bool FULL>
-__global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
+// NW: waves per point (hypothesis h runs on wave h % NW).  Round 5 A/B at C3 (H = 16, one pair at a
+// time, tools/ncc_ab.sh): NW = 4, KPW = 4 1.497 ms; the plane constants made scalar (readfirstlane)
+// 1.498 ms; NW = 8, KPW = 2 (4 waves per SIMD instead of 3) 1.548 / 1.554 ms -- the kernel is VALU
+// issue bound, occupancy does not move it
+template <int KPW, bool FULL, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
     const int pt = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (pt >= (p.Pdev ? *p.Pdev : p.P)) return;  // the inlier count on the device (pipeline), or P
     const double X0 = p.points[3 * pt], X1 = p.points[3 * pt + 1], X2 = p.points[3 * pt + 2];
@@ -108,7 +132,7 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     int nh = 0;
     double n0[KPW], n1[KPW], n2[KPW], mm[KPW];
     for (int k = 0; k < KPW; k++) {
-        const int h = wave + 4 * k;
+        const int h = wave + NW * k;
         if (h < H) {
             const int ip = h / p.Htheta, it = h - ip * p.Htheta;
             const double dphi = p.span * (double)(2 * ip + 1 - p.Hphi) / p.Hphi;
@@ -146,10 +170,10 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
     __shared__ int anyBad1S;
     if (threadIdx.x == 0) anyBad1S = 0;
     __syncthreads();
-    const int nk = FULL ? KPW : nh;  // FULL: H == 4 * KPW, every wave holds KPW hypotheses
+    const int nk = FULL ? KPW : nh;  // FULL: H == NW * KPW, every wave holds KPW hypotheses
     for (int base = 0; base < p.nOffPad; base += kNccChunk) {
-        for (int r = 0; r < kNccChunk / 256; r++) {
-            const int sl = threadIdx.x + 256 * r, e = base + sl;
+        for (int r = 0; r < kNccChunk / (64 * NW); r++) {
+            const int sl = threadIdx.x + 64 * NW * r, e = base + sl;
             int in = 0;
             double ux = 0., uy = 0.;
             float I1 = 0.f;
@@ -175,33 +199,30 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
         for (int j = 0; j < kNccChunk / 64; j++) {
             const int t = lane + 64 * j;
             if (base + 64 * j >= p.nOffPad) break;  // wave-uniform
-            const bool ok = OK[t] != 0;
+            // branch-free over the lanes: an entry outside image 1 (OK 0) was staged with ray (0, 0)
+            // and sample 0, and its image-2 sample is zeroed, so it adds +0 to every sum (the partial
+            // sums are >= 0: +0 leaves them unchanged); a pixel that fails a hypothesis marks it dead,
+            // and a dead hypothesis scores -2 whatever its sums
+            const LaneMask okm = __ballot(OK[t] != 0);
+            m += (okm >> lane) & 1;
+            const double ux = Rx[t], uy = Ry[t];
+            const double a = (double)A1[t];
+            Sa += a;
+            Saa += a * a;
             unsigned badNow = 0;
-            if (ok) {
-                m++;
-                const double ux = Rx[t], uy = Ry[t];
-                const double a = (double)A1[t];
-                Sa += a;
-                Saa += a * a;
 #pragma unroll
-                for (int k = 0; k < KPW; k++) {
-                    if (k >= nk) break;
-                    if ((dead >> k) & 1) continue;  // wave-uniform
-                    float fx, fy;
-                    unsigned off;
-                    if (!ncc_geometry(p, ux, uy, n0[k], n1[k], n2[k], mm[k], mok[k], cm, xmaxb, ymaxb, fx, fy, off)) {
-                        badNow |= 1u << k;
-                        continue;
-                    }
-                    const double b = (double)ncc_bilinear(p.img2, off, p.w, fx, fy);
-                    Sb[k] += b;
-                    Sbb[k] += b * b;
-                    Sab[k] += a * b;
-                }
+            for (int k = 0; k < KPW; k++) {
+                if (k >= nk) break;
+                if ((dead >> k) & 1) continue;  // wave-uniform
+                const NccGeo g = ncc_geometry_m(p, ux, uy, n0[k], n1[k], n2[k], mm[k], mok[k], cm, xmaxb, ymaxb);
+                if (okm & ~g.good) badNow |= 1u << k;  // scalar
+                const float bf = ncc_bilinear_f(p.img2, g.off, p.w, g.fx, g.fy);
+                const double b = (double)__uint_as_float(ncc_sel_u32(__float_as_uint(bf), okm));
+                Sb[k] += b;
+                Sbb[k] += b * b;
+                Sab[k] += a * b;
             }
-#pragma unroll
-            for (int k = 0; k < KPW; k++)
-                if (__ballot((badNow >> k) & 1)) dead |= 1u << k;
+            dead |= badNow;
         }
         __syncthreads();
     }
@@ -219,8 +240,8 @@ __global__ __launch_bounds__(256) void ncc_kernel(NccParams p) {
                 const double cov = sab - sa * sb / m, va = saa - sa * sa / m, vb = sbb - sb * sb / m;
                 if (va > 0 && vb > 0) s = cov / sqrt(va * vb);
             }
-            score[wave + 4 * k] = s;
-            p.scores[(size_t)pt * H + wave + 4 * k] = s;
+            score[wave + NW * k] = s;
+            p.scores[(size_t)pt * H + wave + NW * k] = s;
         }
     }
     __syncthreads();

@@ -315,43 +315,51 @@ ORC_API void orc_camera2_from_g12(const double g12[16], double R2[9], double t2[
 /* ------------------------------------------------------------------ */
 /* DLT triangulation (a4, a5)                                          */
 /* ------------------------------------------------------------------ */
-/* Null vector of the 4x4 DLT system by one-sided (Hestenes) Jacobi SVD with a
-   fixed cyclic pair order, the same sweep rule as the GPU kernel.  OpenCV's
-   cvSVD (JacobiSVD) is not reproducible bit for bit; the null vector agrees
-   with numpy.linalg.svd to ~1e-12 (tests/golden). */
+/* one Jacobi rotation of columns (p, q) of A (and V) unless they are orthogonal to 1e-15 */
+static int orc_jacobi_pair(double A[16], double V[16], int p, int q)
+{
+    double alpha = 0, beta = 0, gamma = 0;
+    int i;
+    for (i = 0; i < 4; i++) {
+        double ap = A[i * 4 + p], aq = A[i * 4 + q];
+        alpha += ap * ap;
+        beta += aq * aq;
+        gamma += ap * aq;
+    }
+    if (gamma != 0. && fabs(gamma) > 1e-15 * sqrt(alpha * beta)) {
+        double zeta = (beta - alpha) / (2. * gamma);
+        double t = (zeta >= 0. ? 1. : -1.) / (fabs(zeta) + sqrt(1. + zeta * zeta));
+        double cs = 1. / sqrt(1. + t * t);
+        double sn = cs * t;
+        for (i = 0; i < 4; i++) {
+            double ap = A[i * 4 + p], aq = A[i * 4 + q];
+            A[i * 4 + p] = cs * ap - sn * aq;
+            A[i * 4 + q] = sn * ap + cs * aq;
+            ap = V[i * 4 + p];
+            aq = V[i * 4 + q];
+            V[i * 4 + p] = cs * ap - sn * aq;
+            V[i * 4 + q] = sn * ap + cs * aq;
+        }
+        return 1;
+    }
+    return 0;
+}
+
+/* Null vector of the 4x4 DLT system: one-sided (Hestenes) Jacobi SVD in the round-robin
+   (tournament) pair order -- (0,1)+(2,3), (0,2)+(1,3), (0,3)+(1,2): the two rotations of a step
+   touch disjoint columns, so they are independent and the GPU runs them side by side (half the
+   dependent chain of the cyclic order, round 5) -- up to 30 sweeps.  OpenCV's cvSVD (JacobiSVD) is
+   not reproducible bit for bit; the null vector agrees with numpy.linalg.svd to ~1e-12
+   (tests/golden). */
 static void orc_dlt_nullvec(double A[16], double v[4])
 {
+    static const int PQ[6][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {0, 3}, {1, 2}};
     double V[16];
-    int sweep, p, q, i, best;
+    int sweep, p, i, k, best;
     for (i = 0; i < 16; i++) V[i] = (i % 5 == 0) ? 1. : 0.;
     for (sweep = 0; sweep < 30; sweep++) {
         int rotated = 0;
-        for (p = 0; p < 3; p++)
-            for (q = p + 1; q < 4; q++) {
-                double alpha = 0, beta = 0, gamma = 0;
-                for (i = 0; i < 4; i++) {
-                    double ap = A[i * 4 + p], aq = A[i * 4 + q];
-                    alpha += ap * ap;
-                    beta += aq * aq;
-                    gamma += ap * aq;
-                }
-                if (gamma != 0. && fabs(gamma) > 1e-15 * sqrt(alpha * beta)) {
-                    double zeta = (beta - alpha) / (2. * gamma);
-                    double t = (zeta >= 0. ? 1. : -1.) / (fabs(zeta) + sqrt(1. + zeta * zeta));
-                    double cs = 1. / sqrt(1. + t * t);
-                    double sn = cs * t;
-                    for (i = 0; i < 4; i++) {
-                        double ap = A[i * 4 + p], aq = A[i * 4 + q];
-                        A[i * 4 + p] = cs * ap - sn * aq;
-                        A[i * 4 + q] = sn * ap + cs * aq;
-                        ap = V[i * 4 + p];
-                        aq = V[i * 4 + q];
-                        V[i * 4 + p] = cs * ap - sn * aq;
-                        V[i * 4 + q] = sn * ap + cs * aq;
-                    }
-                    rotated = 1;
-                }
-            }
+        for (k = 0; k < 6; k++) rotated |= orc_jacobi_pair(A, V, PQ[k][0], PQ[k][1]);
         if (!rotated) break;
     }
     {
