@@ -201,4 +201,48 @@ __device__ __forceinline__ float fast_atan2f(float y, float x) {
     return a;
 }
 
+// The decoupled look-back of one block (LookBack in fm3d_kernels.h), called by all 64 lanes of ONE wave
+// of the block: lane 0 publishes the block's count ("aggregate", flag 1); then the wave reads the
+// status words of its 64 nearest predecessors at once (one per lane), finds the nearest inclusive
+// prefix (flag 2) with a ballot, and -- once every word up to it carries this launch's epoch -- adds
+// the counts up to it; with no inclusive prefix in the window it moves 64 blocks further back.  Lane 0
+// publishes the block's inclusive prefix.  Returns (on every lane) the number of items of all earlier
+// blocks.  Status words are device-scope release / acquire atomics (vector memory).  A walk of one
+// word per step cost a memory round trip per predecessor (triangulate_compact 51 us at C2).
+__device__ inline int lookback_exclusive(unsigned long long* st, unsigned epoch, int bid, int agg) {
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    if (bid == 0) {
+        if (lane == 0)
+            __hip_atomic_store(&st[0], tag | (2ull << 30) | (unsigned)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0)
+        __hip_atomic_store(&st[bid], tag | (1ull << 30) | (unsigned)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    int ex = 0;
+    for (int base = bid - 1;;) {
+        const int b = base - lane;
+        // below block 0 (never reached: block 0's word is inclusive) reads as an empty inclusive prefix
+        const unsigned long long w =
+            b >= 0 ? __hip_atomic_load(&st[b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : (tag | (2ull << 30));
+        const bool ready = (unsigned)(w >> 32) == epoch;
+        const unsigned long long incl = __ballot(ready && ((w >> 30) & 3u) == 2u);
+        const unsigned long long notReady = __ballot(!ready);
+        const int l0 = incl ? __ffsll((long long)incl) - 1 : 63;
+        const unsigned long long need = l0 == 63 ? ~0ull : ((1ull << (l0 + 1)) - 1);
+        if (notReady & need) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        int v = lane <= l0 ? (int)(w & 0x3fffffffu) : 0;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        ex += v;
+        if (incl) break;
+        base -= 64;
+    }
+    if (lane == 0)
+        __hip_atomic_store(&st[bid], tag | (2ull << 30) | (unsigned)(ex + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return ex;
+}
+
 }  // namespace fm3d

@@ -136,6 +136,9 @@ struct fm3d_ctx {
     long lmGroups = 0;
     int wallKhz = 0;
     DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, slab, slabI1;
+    // the fused compactions' look-back state (fm3d_kernels.h LookBack): status words, block counter
+    DevBuf lbSt, lbCtr;
+    unsigned lbBase = 0, lbEpoch = 0;
     DevBuf records, recTmp, recFlag;
     DevBuf lmProj;  // camera-2 projection constants for the LM kernel (fm3d::ProjConst)
     DevBuf pcnt;    // the pipeline's device counts: [0] matches K, [1] inliers P, [2] kept
@@ -462,7 +465,32 @@ bool f32_mfma() {
 }
 
 // knn2 + NNDR flags on staged descriptors (device), results in c->idx/key/fkey/cand/flag
-int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int queryOffset, bool wantKnn) {
+// the look-back state of one fused-compaction launch of nBlocks blocks on c's stream
+int make_lookback(fm3d_ctx* c, int nBlocks, fm3d::LookBack* lb) {
+    if (!c->lbCtr.p) {
+        HIPCHK(c, c->lbCtr.ensure(64));
+        HIPCHK(c, hipMemsetAsync(c->lbCtr.p, 0, 64, c->stream));
+        c->lbBase = 0;
+    }
+    if (c->lbSt.bytes < (size_t)nBlocks * 8) {
+        HIPCHK(c, c->lbSt.ensure((size_t)nBlocks * 8 * 2));
+        HIPCHK(c, hipMemsetAsync(c->lbSt.p, 0, c->lbSt.bytes, c->stream));  // epoch 0: "not yet"
+    }
+    lb->st = c->lbSt.as<unsigned long long>();
+    lb->ctr = c->lbCtr.as<unsigned>();
+    lb->base = c->lbBase;
+    lb->epoch = ++c->lbEpoch;
+    c->lbBase += (unsigned)nBlocks;
+    return FM3D_OK;
+}
+
+// compactOut / compactCount (the pipeline): NNDR, the parts' merge (int keys) and the stable
+// compaction of the kept matches in one launch (launch_nndr_compact); else the NNDR flags and
+// candidates in c->flag / c->cand
+int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int queryOffset, bool wantKnn,
+              fm3d_dmatch* compactOut = nullptr, int* compactCount = nullptr) {
+    const bool fuse = compactOut != nullptr && !wantKnn;
+    int mergeParts = 1;  // > 1: the parts' lists are merged by launch_nndr_compact
     HIPCHK(c, c->idx.ensure((size_t)nA * 2 * sizeof(int) + 16));
     HIPCHK(c, c->key.ensure((size_t)nA * 2 * sizeof(int) + 16));
     HIPCHK(c, c->fkey.ensure((size_t)nA * 2 * sizeof(float) + 16));
@@ -485,9 +513,10 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
             HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
             HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
         }
+        if (fuse && parts > 1) mergeParts = parts;
         fm3d::launch_knn2_i8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, 0, c->cqA.as<int>(),
                              c->ctB.as<int>(), parts, c->partIdx.as<int>(), c->partKey.as<int>(), c->idx.as<int>(),
-                             c->key.as<int>(), c->stream);
+                             c->key.as<int>(), c->stream, mergeParts > 1);
     } else if (type == FM3D_DESC_F32 && (dimPad == 64 || dimPad == 128) && nB >= 64 &&
                (long long)nA * nB >= (1LL << 22) && f32_mfma()) {
         // float rows (SURF): the bf16 MFMA prefilter lists each query's possible top-2 rows, whose exact
@@ -548,9 +577,10 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
             HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
             HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
         }
+        if (fuse && parts > 1) mergeParts = parts;
         fm3d::launch_knn2_i8(c->A8.as<uint8_t>(), nA, c->B8.as<uint8_t>(), nB, 256, 1, nullptr, c->ctB.as<int>(),
                              parts, c->partIdx.as<int>(), c->partKey.as<int>(), c->idx.as<int>(), c->key.as<int>(),
-                             c->stream);
+                             c->stream, mergeParts > 1);
     } else {
         const int parts = fm3d::knn2_parts(nA, nB, dimPad, c->nCU);
         if (parts > 1) {
@@ -561,9 +591,18 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
                                c->partKey.as<int>(), c->idx.as<int>(), c->key.as<int>(), c->stream);
     }
     HIPCHK(c, hipGetLastError());
-    fm3d::launch_nndr(type, c->idx.as<int>(), c->key.as<int>(), c->fkey.as<float>(), nA, nB, eps, queryOffset,
-                      wantKnn ? c->knnOut.as<fm3d_dmatch>() : nullptr, c->cand.as<fm3d_dmatch>(), c->flag.as<int>(),
-                      c->stream);
+    if (fuse) {
+        fm3d::LookBack lb;
+        int r;
+        if ((r = make_lookback(c, fm3d::nndr_compact_blocks(nA), &lb))) return r;
+        fm3d::launch_nndr_compact(type, c->idx.as<int>(), c->key.as<int>(), c->fkey.as<float>(), c->partIdx.as<int>(),
+                                  c->partKey.as<int>(), mergeParts, nA, eps, queryOffset, compactOut, compactCount, lb,
+                                  c->stream);
+    } else {
+        fm3d::launch_nndr(type, c->idx.as<int>(), c->key.as<int>(), c->fkey.as<float>(), nA, nB, eps, queryOffset,
+                          wantKnn ? c->knnOut.as<fm3d_dmatch>() : nullptr, c->cand.as<fm3d_dmatch>(), c->flag.as<int>(),
+                          c->stream);
+    }
     HIPCHK(c, hipGetLastError());
     return FM3D_OK;
 }
@@ -1958,13 +1997,13 @@ int pipeline_front(fm3d_ctx* c) {
     HIPCHK(c, c->pcnt.ensure(64));
     int* cnt = c->pcnt.as<int>();
     HIPCHK(c, hipEventRecord(ev[2], c->stream));
-    // a1: match + NNDR
-    if ((r = run_match(c, nA, nB, c->stType, c->stDimPad, c->s.nndrEpsilon, c->stQueryOffset, false))) return r;
-    HIPCHK(c, hipEventRecord(ev[3], c->stream));
+    // a1: match + NNDR (+ the stable compaction of the kept matches, fused into the NNDR launch)
     if ((r = ensure_scan_tmp(c, nA))) return r;
     HIPCHK(c, c->matches.ensure((size_t)(nA + 1) * sizeof(fm3d_dmatch)));
-    fm3d::launch_compact_dmatch(c->cand.as<fm3d_dmatch>(), c->flag.as<int>(), nA, c->matches.as<fm3d_dmatch>(), cnt + 0,
-                                c->scanTmp.p, c->stream);
+    if ((r = run_match(c, nA, nB, c->stType, c->stDimPad, c->s.nndrEpsilon, c->stQueryOffset, false,
+                       c->matches.as<fm3d_dmatch>(), cnt + 0)))
+        return r;
+    HIPCHK(c, hipEventRecord(ev[3], c->stream));
     HIPCHK(c, hipEventRecord(ev[4], c->stream));
     // a4, a5: triangulate (matches are device resident; K <= nA)
     HIPCHK(c, c->triPts.ensure((size_t)(nA + 1) * 3 * sizeof(double)));
@@ -1985,9 +2024,11 @@ int pipeline_front(fm3d_ctx* c) {
     tp.pts = c->triPts.as<double>();
     tp.mask = c->triMask.as<int>();
     tp.mask8 = nullptr;
-    fm3d::launch_triangulate(tp, c->stream);
-    fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), nA, cnt + 0, c->pts.as<double>(), cnt + 1,
-                                c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
+    {   // DLT with the inliers' compaction fused (launch_triangulate_compact)
+        fm3d::LookBack lb;
+        if ((r = make_lookback(c, fm3d::triangulate_compact_blocks(nA), &lb))) return r;
+        fm3d::launch_triangulate_compact(tp, c->pts.as<double>(), c->srcIdx.as<int>(), cnt + 1, lb, c->stream);
+    }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(ev[5], c->stream));
     return FM3D_OK;

@@ -114,8 +114,10 @@ struct KnnOut {
 int knn2_u8_parts(int nA, int nB, int nCU);
 // int8-MFMA matcher for u8 rows (bits = 0) and for 32-byte binary rows unpacked by
 // launch_unpack_bits (bits = 1, dimPad 256); ctB = packed train row constants
+// deferMerge: with parts > 1 the parts' lists stay in partIdx / partKey (launch_nndr_compact merges them)
 void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int bits, const int* cqA,
-                    const int* ctB, int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s);
+                    const int* ctB, int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s,
+                    bool deferMerge = false);
 // row constants of both sides: cq = |a'|^2 per query row, ctp = packed train constants
 void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int* cq, int* ctp,
                         hipStream_t s);
@@ -308,6 +310,29 @@ struct TriParams {
     uint8_t* mask8;   // K (optional)
 };
 void launch_triangulate(const TriParams& p, hipStream_t s);
+
+// ---------------- stable compaction fused into its producer (decoupled look-back) ----------------
+// One launch produces the items and compacts them in order: each block counts its kept items,
+// publishes the count, and adds up its predecessors' (their inclusive prefix as soon as one is
+// published) to place its items.  Blocks take their index from a counter in launch order, so a block
+// only ever waits for blocks that started before it.
+struct LookBack {
+    unsigned long long* st;  // per block of the launch: (epoch << 32) | (flag << 30) | value
+    unsigned* ctr;           // block counter (never reset; base = its value at the launch's start)
+    unsigned base;
+    unsigned epoch;  // the launch's tag: status words of earlier launches read as "not yet"
+};
+// NNDR (descriptorsmatcher.cpp:119-129) with the parts' top-2 merge (int keys; parts = 1: idx / key
+// as merged lists) and the stable compaction of the kept matches: out[0 .. *count)
+void launch_nndr_compact(int type, const int* idx, const int* key, const float* fkey, const int* partIdx,
+                         const int* partKey, int parts, int nA, double eps, int queryOffset, fm3d_dmatch* out,
+                         int* count, const LookBack& lb, hipStream_t s);
+int nndr_compact_blocks(int nA);
+// setKeypoints + triangulate with the compaction of the inliers: out (P x 3), srcIdx (P), *count = P;
+// mask (K) as launch_triangulate
+void launch_triangulate_compact(const TriParams& p, double* out, int* srcIdx, int* count, const LookBack& lb,
+                                hipStream_t s);
+int triangulate_compact_blocks(int K);
 
 // ---------------- images ----------------
 void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s);

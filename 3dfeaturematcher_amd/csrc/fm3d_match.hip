@@ -564,6 +564,79 @@ __global__ void nndr_kernel(int type, const int* __restrict__ idx, const int* __
     cand[q] = fm3d_dmatch{q + queryOffset, i1, 0, d1};
 }
 
+// nndr_kernel with the parts' merge (knn2_int_merge's rule; int keys) and the stable compaction of the
+// kept matches in one launch (fm3d_kernels.h LookBack): the pipeline's a1 without two launches and
+// their round trips.  Block b's queries are b*256 .. b*256+255, b taken in launch order.
+__global__ __launch_bounds__(256) void nndr_compact_kernel(int type, const int* __restrict__ idx,
+                                                           const int* __restrict__ key, const float* __restrict__ fkey,
+                                                           const int* __restrict__ pIdx, const int* __restrict__ pKey,
+                                                           int parts, int nA, double eps, int queryOffset,
+                                                           fm3d_dmatch* __restrict__ out, int* __restrict__ count,
+                                                           LookBack lb) {
+    __shared__ int sBid, sEx, sWave[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) sBid = (int)(atomicAdd(lb.ctr, 1u) - lb.base);
+    __syncthreads();
+    const int bid = sBid;
+    const int q = bid * 256 + tid;
+    bool keep = false;
+    fm3d_dmatch cand{};
+    if (q < nA) {
+        int i1, i2;
+        float d1, d2;
+        if (parts > 1) {
+            int b1 = INT_MAX, b2 = INT_MAX;
+            i1 = i2 = -1;
+            for (int s = 0; s < parts; s++) {
+                const size_t o = ((size_t)s * nA + q) * 2;
+                int j0 = pIdx[o], j1 = pIdx[o + 1];
+                int k0 = pKey[o], k1 = pKey[o + 1];
+                if (j1 >= 0 && j1 < j0) {  // visit the part's two candidates in train index order
+                    const int tj = j0; j0 = j1; j1 = tj;
+                    const int tk = k0; k0 = k1; k1 = tk;
+                }
+                if (j0 >= 0) top2_insert(k0, j0, b1, i1, b2, i2);
+                if (j1 >= 0) top2_insert(k1, j1, b1, i1, b2, i2);
+            }
+            if (type == FM3D_DESC_U8) {
+                d1 = sqrtf((float)b1);
+                d2 = sqrtf((float)b2);
+            } else {
+                d1 = (float)b1;
+                d2 = (float)b2;
+            }
+        } else {
+            i1 = idx[2 * q];
+            i2 = idx[2 * q + 1];
+            if (type == FM3D_DESC_F32) {
+                d1 = sqrtf(fkey[2 * q]);
+                d2 = sqrtf(fkey[2 * q + 1]);
+            } else if (type == FM3D_DESC_U8) {
+                d1 = sqrtf((float)key[2 * q]);
+                d2 = sqrtf((float)key[2 * q + 1]);
+            } else {
+                d1 = (float)key[2 * q];
+                d2 = (float)key[2 * q + 1];
+            }
+        }
+        // descriptorsmatcher.cpp:121-128: size() >= 2 and distance0 <= epsilon * distance1 (double)
+        keep = (i1 >= 0 && i2 >= 0) && ((double)d1 <= eps * (double)d2);
+        cand = fm3d_dmatch{q + queryOffset, i1, 0, d1};
+    }
+    const unsigned long long bal = __ballot(keep);
+    if (lane == 0) sWave[wave] = __popcll(bal);
+    __syncthreads();
+    if (wave == 0) {
+        const int ex = lookback_exclusive(lb.st, lb.epoch, bid, sWave[0] + sWave[1] + sWave[2] + sWave[3]);
+        if (lane == 0) sEx = ex;
+    }
+    __syncthreads();
+    int o = sEx + __popcll(bal & ((1ull << lane) - 1));
+    for (int w = 0; w < wave; w++) o += sWave[w];
+    if (keep) out[o] = cand;
+    if (tid == 0 && bid == (int)gridDim.x - 1) *count = sEx + sWave[0] + sWave[1] + sWave[2] + sWave[3];
+}
+
 // ---------------- float rows: a bf16 MFMA prefilter, then the exact FLANN-order distances ----------------
 // s'_j = |b_j|^2 - 2 a_hi . b_hi,j (a_hi, b_hi = the rows rounded to bf16; the dot products on
 // v_mfma_f32_32x32x16_bf16, |b_j|^2 in fp32) ranks train row j for query a up to
@@ -948,7 +1021,8 @@ void launch_unpack_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, uint
 }
 
 void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int bits, const int* cqA,
-                    const int* ctB, int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s) {
+                    const int* ctB, int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s,
+                    bool deferMerge) {
     if (nA <= 0) return;
     size_t lds = 2 * (size_t)kT * dimPad + 2 * kT * sizeof(int);
     const int nTiles = (nB + kT - 1) / kT;
@@ -969,7 +1043,7 @@ void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
         go(knn2_i8_kernel<8, false>);
     else
         go(knn2_i8_kernel<0, false>);
-    if (parts > 1) knn2_int_merge<<<(nA + 255) / 256, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
+    if (parts > 1 && !deferMerge) knn2_int_merge<<<(nA + 255) / 256, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
 }
 
 size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts) {
@@ -1146,6 +1220,15 @@ void launch_knn2_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, int di
         default: knn2_bits_sgpr_kernel<16><<<g, 256, 0, s>>>(a, nA, b, nB, rowsPerPart, oi, ok); break;  // 64 B
     }
     if (parts > 1) knn2_int_merge<<<grid, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
+}
+
+int nndr_compact_blocks(int nA) { return nA > 0 ? (nA + 255) / 256 : 1; }
+
+void launch_nndr_compact(int type, const int* idx, const int* key, const float* fkey, const int* partIdx,
+                         const int* partKey, int parts, int nA, double eps, int queryOffset, fm3d_dmatch* out,
+                         int* count, const LookBack& lb, hipStream_t s) {
+    nndr_compact_kernel<<<nndr_compact_blocks(nA), 256, 0, s>>>(type, idx, key, fkey, partIdx, partKey, parts, nA, eps,
+                                                              queryOffset, out, count, lb);
 }
 
 void launch_nndr(int type, const int* idx, const int* key, const float* fkey, int nA, int nB, double eps,

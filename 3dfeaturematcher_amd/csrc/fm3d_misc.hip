@@ -81,9 +81,8 @@ __device__ inline void dlt_nullvec(double* A, double* v) {
 // give it the registers; under the default 1024-thread bound (128 VGPRs) the sweeps spilled to
 // scratch and the kernel lasted 27-33 us at any match count (rocprofv3, round 3).
 constexpr int kTriThreads = 64;
-__global__ __launch_bounds__(kTriThreads) void triangulate_kernel(TriParams p) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (p.Kdev ? *p.Kdev : p.K)) return;  // the match count on the device (grid: its bound)
+// match i: its homogeneous DLT point and whether it is an inlier (zThresholdMin <= Z/W < Max)
+__device__ __forceinline__ bool tri_one(const TriParams& p, int i, double* X) {
     const fm3d_dmatch mt = p.matches[i];
     const fm3d_point2f k1 = p.kp1[mt.queryIdx - p.queryOffset];
     const fm3d_point2f k2 = p.kp2[mt.trainIdx];
@@ -99,15 +98,45 @@ __global__ __launch_bounds__(kTriThreads) void triangulate_kernel(TriParams p) {
         A[2 * 4 + k] = u2x * p.g12[8 + k] - p.g12[0 + k];
         A[3 * 4 + k] = u2y * p.g12[8 + k] - p.g12[4 + k];
     }
-    double X[4];
     dlt_nullvec(A, X);
     // Z/W < zThresholdMin || Z/W >= zThresholdMax -> outlier (:200-216)
     const bool out = (X[2] / X[3] < p.zmin || X[2] / X[3] >= p.zmax);
     p.mask[i] = out ? 0 : 1;
     if (p.mask8) p.mask8[i] = out ? 0 : 1;
+    return !out;
+}
+__global__ __launch_bounds__(kTriThreads) void triangulate_kernel(TriParams p) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (p.Kdev ? *p.Kdev : p.K)) return;  // the match count on the device (grid: its bound)
+    double X[4];
+    tri_one(p, i, X);
     p.pts[3 * i + 0] = X[0] / X[3];
     p.pts[3 * i + 1] = X[1] / X[3];
     p.pts[3 * i + 2] = X[2] / X[3];
+}
+// the same with the inliers compacted in match order (fm3d_kernels.h LookBack): out, srcIdx, *count
+// -- the pipeline's a4/a5 without compact<Point3>'s launch (12 us at C2, one workgroup)
+__global__ __launch_bounds__(kTriThreads) void triangulate_compact_kernel(TriParams p, double* __restrict__ out,
+                                                                          int* __restrict__ srcIdx,
+                                                                          int* __restrict__ count, LookBack lb) {
+    __shared__ int sBid;
+    const int lane = threadIdx.x;
+    if (lane == 0) sBid = (int)(atomicAdd(lb.ctr, 1u) - lb.base);
+    __syncthreads();
+    const int bid = sBid;
+    const int i = bid * kTriThreads + lane;
+    double X[4];
+    const bool inl = i < (p.Kdev ? *p.Kdev : p.K) && tri_one(p, i, X);
+    const unsigned long long bal = __ballot(inl);
+    const int ex = lookback_exclusive(lb.st, lb.epoch, bid, __popcll(bal));  // one wave: kTriThreads == 64
+    const int o = ex + __popcll(bal & ((1ull << lane) - 1));
+    if (inl) {
+        out[3 * o + 0] = X[0] / X[3];
+        out[3 * o + 1] = X[1] / X[3];
+        out[3 * o + 2] = X[2] / X[3];
+        srcIdx[o] = i;
+    }
+    if (lane == 0 && bid == (int)gridDim.x - 1) *count = ex + __popcll(bal);
 }
 
 // ---------------- cv::pyrDown (8U) ----------------
@@ -398,6 +427,13 @@ __global__ void make_records_kernel(const fm3d_dmatch* __restrict__ matches, con
 void launch_triangulate(const TriParams& p, hipStream_t s) {
     if (p.K <= 0) return;
     triangulate_kernel<<<(p.K + kTriThreads - 1) / kTriThreads, kTriThreads, 0, s>>>(p);
+}
+
+int triangulate_compact_blocks(int K) { return K > 0 ? (K + kTriThreads - 1) / kTriThreads : 1; }
+
+void launch_triangulate_compact(const TriParams& p, double* out, int* srcIdx, int* count, const LookBack& lb,
+                                hipStream_t s) {
+    triangulate_compact_kernel<<<triangulate_compact_blocks(p.K), kTriThreads, 0, s>>>(p, out, srcIdx, count, lb);
 }
 
 void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s) {
