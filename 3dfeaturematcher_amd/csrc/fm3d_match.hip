@@ -31,6 +31,13 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int kQ = 128;     // queries per workgroup (4 waves x 32)
 constexpr int kT = 128;     // train rows per LDS tile
 constexpr int kThreads = 256;
+// 32-query groups per wave of the u8 kernel at 128-byte rows (knn2_i8_kernel's QG): 2 = 200 VGPRs,
+// two waves per SIMD; 100k x 100k 2.00 -> 1.85 ms, 10k x 10k 30.7 -> 29.6 us against QG 1 (150
+// VGPRs, three waves).  The 256-byte and binary variants keep 1 (a second group would spill).
+#ifndef FM3D_KNN_QG
+#define FM3D_KNN_QG 2
+#endif
+constexpr int kQG128 = FM3D_KNN_QG;
 
 __device__ inline int swz_chunk(int row, int ch) {
     // 16-byte chunk XOR swizzle inside each 128-byte segment: rows r..r+15 reading
@@ -143,8 +150,10 @@ __global__ void unpack_bits_kernel(const uint32_t* __restrict__ A, int nA, const
 
 // KS: dimPad / 32 when it is 4 (128-byte rows) or 8 (256), so the MFMA chain is straight-line
 // code; 0 reads it from dimPad.  BITS: rows are pre-unpacked int8 bits (no -128 offset, key
-// popc(b) - a.b', no query constant).
-template <int KS, bool BITS>
+// popc(b) - a.b', no query constant).  QG: 32-query groups per wave (a workgroup holds kQ * QG
+// queries); each A fragment read from LDS feeds QG MFMAs, and the per-tile staging, barrier and
+// merge are shared by QG groups.
+template <int KS, bool BITS, int QG>
 __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __restrict__ A, int nA,
                                                            const uint8_t* __restrict__ B, int nB, int dimPad,
                                                            const int* __restrict__ cqA, const int* __restrict__ ctB,
@@ -155,8 +164,7 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
     unsigned char* tiles = smem;                              // 2 x tileBytes
     uint32_t* ctl = (uint32_t*)(smem + 2 * (size_t)tileBytes);  // 2 x kT packed row constants
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q0 = blockIdx.x * kQ + wave * 32;
-    const int qrow = q0 + (lane & 31);
+    const int q0 = blockIdx.x * (kQ * QG) + wave * 32 * QG;
     const int half = lane >> 5;
     const int ksteps = KS ? KS : dimPad / 32;
     const int rowBytes = KS ? 32 * KS : dimPad;  // = dimPad (compile-time for KS != 0)
@@ -164,17 +172,26 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
     constexpr int kFlip = BITS ? 0 : (int)0x80808080;  // x ^ 0x80 == x - 128
     constexpr int kShift = BITS ? 7 : 8;                 // acc * MUL * 128 (key bits start at bit 7)
 
-    // B operand: this lane's query bytes as int8
-    v4i bq[8];  // up to dimPad = 256
+    // B operand: this lane's query bytes as int8, one set per query group
+    v4i bq[QG][8];  // up to dimPad = 256
 #pragma unroll
-    for (int kk = 0; kk < 8; kk++) {
-        if (kk < ksteps) {
-            v4i v = {0, 0, 0, 0};
-            if (qrow < nA) v = *(const v4i*)(A + (size_t)qrow * dimPad + 32 * kk + 16 * half);
-            bq[kk] = v ^ (v4i){kFlip, kFlip, kFlip, kFlip};
+    for (int g = 0; g < QG; g++) {
+        const int qrow = q0 + 32 * g + (lane & 31);
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            if (kk < ksteps) {
+                v4i v = {0, 0, 0, 0};
+                if (qrow < nA) v = *(const v4i*)(A + (size_t)qrow * dimPad + 32 * kk + 16 * half);
+                bq[g][kk] = v ^ (v4i){kFlip, kFlip, kFlip, kFlip};
+            }
         }
     }
-    int b1 = INT_MAX, i1 = -1, b2 = INT_MAX, i2 = -1;
+    int b1[QG], i1[QG], b2[QG], i2[QG];
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        b1[g] = b2[g] = INT_MAX;
+        i1[g] = i2[g] = -1;
+    }
     // train tiles of this part (blockIdx.y): [tBeg, tEnd); the parts' lists are merged by knn2_int_merge
     const int tBeg = blockIdx.y * tilesPerPart;
     const int tEnd = min((nB + kT - 1) / kT, tBeg + tilesPerPart);
@@ -215,6 +232,9 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
         }
         if (tid < kT) ctl[buf * kT + tid] = preCt;
     };
+    struct Acc {
+        v16i a[QG];
+    };
 
     if (tBeg < tEnd) {
         load_tile(tBeg);
@@ -226,45 +246,55 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
         if (t + 1 < tEnd) load_tile(t + 1);
         const unsigned char* tl = tiles + (size_t)buf * tileBytes;
         const uint32_t* ct = ctl + buf * kT;
-        // packed top-2 (largest) of this tile, two chains (even / odd row blocks) merged after the tile
-        uint32_t p1[2] = {0, 0}, p2[2] = {0, 0};
+        // packed top-2 (largest) of this tile per query group, two chains (even / odd row blocks)
+        // merged after the tile
+        uint32_t p1[QG][2], p2[QG][2];
+#pragma unroll
+        for (int g = 0; g < QG; g++) p1[g][0] = p1[g][1] = p2[g][0] = p2[g][1] = 0;
         // software pipeline over the four 32-row blocks: the MFMA chain of block rb + 1 is issued
         // between the epilogue instructions of block rb (both in flight in one wave)
         auto mma = [&](int rb) {
-            v16i acc = {0};
+            Acc acc;
+#pragma unroll
+            for (int g = 0; g < QG; g++) acc.a[g] = (v16i){0};
             const int arow = rb * 32 + (lane & 31);
 #pragma unroll
             for (int kk = 0; kk < 8; kk++) {
                 if (kk < ksteps) {
                     v4i a = *(const v4i*)(tl + (size_t)arow * rowBytes + 16 * swz_chunk(arow, 2 * kk + half));
-                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[kk], acc, 0, 0, 0);
+#pragma unroll
+                    for (int g = 0; g < QG; g++)
+                        acc.a[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[g][kk], acc.a[g], 0, 0, 0);
                 }
             }
             return acc;
         };
-        auto epi = [&](const v16i& acc, int rb, auto fullc) {
+        auto epi = [&](const Acc& acc, int rb, auto fullc) {
             // this lane's 16 train rows of the block; rows past nB exist only in the last tile,
             // tested against one per-lane limit (the row offsets stay compile-time constants)
             const int c = rb & 1;
             const int lim = nB - t * kT - 4 * half;
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                uint32_t v = ((uint32_t)acc[r] << kShift) + ct[row];
-                if (!decltype(fullc)::value) v = (rb * 32 + (r & 3) + 8 * (r >> 2) < lim) ? v : 0u;
-                p2[c] = med3u(p1[c], p2[c], v);
-                p1[c] = umax(p1[c], v);
+            for (int g = 0; g < QG; g++) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    uint32_t v = ((uint32_t)acc.a[g][r] << kShift) + ct[row];
+                    if (!decltype(fullc)::value) v = (rb * 32 + (r & 3) + 8 * (r >> 2) < lim) ? v : 0u;
+                    p2[g][c] = med3u(p1[g][c], p2[g][c], v);
+                    p1[g][c] = umax(p1[g][c], v);
+                }
             }
         };
         auto blocks = [&](auto fullc) {
-            v16i accCur = mma(0);
+            Acc accCur = mma(0);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int rb = 0; rb < kT / 32; rb++) {
-                v16i accNext;
+                Acc accNext;
                 if (rb + 1 < kT / 32) accNext = mma(rb + 1);
                 epi(accCur, rb, fullc);
-                // one scheduling region per block: at most two accumulators live (without the
+                // one scheduling region per block: at most two accumulator sets live (without the
                 // barriers the compiler hoists all sixteen MFMAs: 194 VGPRs instead of 150)
                 __builtin_amdgcn_sched_barrier(0);
                 if (rb + 1 < kT / 32) accCur = accNext;
@@ -276,23 +306,35 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
             blocks(std::false_type());
         // merge the chains, then fold the tile's two best into the running (key, index) list:
         // earlier tiles hold lower indices, and top2_insert keeps them on equal keys
-        const uint32_t m1 = umax(p1[0], p1[1]);
-        const uint32_t m2 = umax(umin(p1[0], p1[1]), umax(p2[0], p2[1]));
-        if (m1) top2_insert((int)kKeyBias - (int)(m1 >> 7), t * kT + 127 - (int)(m1 & 127), b1, i1, b2, i2);
-        if (m2) top2_insert((int)kKeyBias - (int)(m2 >> 7), t * kT + 127 - (int)(m2 & 127), b1, i1, b2, i2);
+#pragma unroll
+        for (int g = 0; g < QG; g++) {
+            const uint32_t m1 = umax(p1[g][0], p1[g][1]);
+            const uint32_t m2 = umax(umin(p1[g][0], p1[g][1]), umax(p2[g][0], p2[g][1]));
+            if (m1)
+                top2_insert((int)kKeyBias - (int)(m1 >> 7), t * kT + 127 - (int)(m1 & 127), b1[g], i1[g], b2[g],
+                            i2[g]);
+            if (m2)
+                top2_insert((int)kKeyBias - (int)(m2 >> 7), t * kT + 127 - (int)(m2 & 127), b1[g], i1[g], b2[g],
+                            i2[g]);
+        }
         if (t + 1 < tEnd) store_tile(buf ^ 1);
         __syncthreads();
     }
-    // lanes l and l+32 hold the same query (different train rows): merge
-    int c1 = __shfl_xor(b1, 32), j1 = __shfl_xor(i1, 32), c2 = __shfl_xor(b2, 32), j2 = __shfl_xor(i2, 32);
-    top2_merge(b1, i1, b2, i2, c1, j1, c2, j2);
-    if (half == 0 && qrow < nA) {
-        const int cq = BITS ? 0 : cqA[qrow];
-        const size_t o = ((size_t)blockIdx.y * nA + qrow) * 2;
-        idxOut[o] = i1;
-        idxOut[o + 1] = i2;
-        keyOut[o] = i1 >= 0 ? cq + b1 : INT_MAX;
-        keyOut[o + 1] = i2 >= 0 ? cq + b2 : INT_MAX;
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        // lanes l and l+32 hold the same query (different train rows): merge
+        int c1 = __shfl_xor(b1[g], 32), j1 = __shfl_xor(i1[g], 32), c2 = __shfl_xor(b2[g], 32),
+            j2 = __shfl_xor(i2[g], 32);
+        top2_merge(b1[g], i1[g], b2[g], i2[g], c1, j1, c2, j2);
+        const int qrow = q0 + 32 * g + (lane & 31);
+        if (half == 0 && qrow < nA) {
+            const int cq = BITS ? 0 : cqA[qrow];
+            const size_t o = ((size_t)blockIdx.y * nA + qrow) * 2;
+            idxOut[o] = i1[g];
+            idxOut[o + 1] = i2[g];
+            keyOut[o] = i1[g] >= 0 ? cq + b1[g] : INT_MAX;
+            keyOut[o + 1] = i2[g] >= 0 ? cq + b2[g] : INT_MAX;
+        }
     }
 }
 
@@ -1027,22 +1069,22 @@ void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
     size_t lds = 2 * (size_t)kT * dimPad + 2 * kT * sizeof(int);
     const int nTiles = (nB + kT - 1) / kT;
     const int tilesPerPart = parts > 1 ? (nTiles + parts - 1) / parts : (nTiles > 0 ? nTiles : 1);
-    const dim3 g((nA + kQ - 1) / kQ, parts);
     int* oi = parts > 1 ? partIdx : idx;
     int* ok = parts > 1 ? partKey : key;
-    auto go = [&](auto kernel) {
+    auto go = [&](auto kernel, int qg) {
         if (lds > 65536)
             (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const dim3 g((nA + kQ * qg - 1) / (kQ * qg), parts);
         kernel<<<g, kThreads, lds, s>>>(A, nA, B, nB, dimPad, cqA, ctB, tilesPerPart, oi, ok);
     };
     if (bits)
-        go(knn2_i8_kernel<8, true>);  // 32-byte binary rows unpacked to 256 int8
+        go(knn2_i8_kernel<8, true, 1>, 1);  // 32-byte binary rows unpacked to 256 int8
     else if (dimPad == 128)
-        go(knn2_i8_kernel<4, false>);
+        go(knn2_i8_kernel<4, false, kQG128>, kQG128);
     else if (dimPad == 256)
-        go(knn2_i8_kernel<8, false>);
+        go(knn2_i8_kernel<8, false, 1>, 1);
     else
-        go(knn2_i8_kernel<0, false>);
+        go(knn2_i8_kernel<0, false, 1>, 1);
     if (parts > 1 && !deferMerge) knn2_int_merge<<<(nA + 255) / 256, 256, 0, s>>>(partIdx, partKey, nA, parts, idx, key);
 }
 
@@ -1054,7 +1096,7 @@ size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts) {
 
 
 
-int knn2_f32_mfma_parts(int nA, int nB, int nCU) { return knn2_u8_parts(nA, nB, nCU); }
+int knn2_f32_mfma_parts(int nA, int nB, int nCU) { return knn2_u8_parts(nA, nB, nCU, 0); }
 
 void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, bool fused, void* work,
                           int* idx, float* key, hipStream_t s) {
@@ -1138,20 +1180,41 @@ void launch_knn2_f32_mfma_rescan(const float* A, const float* B, int nB, int dim
     knn2_f32_rescan_kernel<<<grid, 256, 0, s>>>(A, B, nB, dim, resc, nR, idx, key);
 }
 
-int knn2_u8_parts(int nA, int nB, int nCU) {
-    // Split the train tiles only when the 128-query blocks alone leave CUs idle (at 100k queries
-    // the extra staging of more, shorter blocks costs more than the balance gains).  Then aim at
-    // four blocks per CU, each part keeping >= 4 tiles: at 10k x 10k (79 query blocks) 16 parts
-    // take the u8 kernel 63 -> 29 us and the bits kernel 56 -> 43 us (rocprofv3, MI355X).
+int knn2_i8_queries_per_block(int dimPad, int bits) { return (!bits && dimPad == 128 ? kQG128 : 1) * kQ; }
+
+int knn2_u8_parts(int nA, int nB, int nCU, int qPerBlock) {
+    // Fewer query blocks than CUs: split the train tiles, aiming at four blocks per CU, each part
+    // keeping >= 4 tiles: at 10k x 10k (79 query blocks) 16 parts take the u8 kernel 63 -> 29 us and
+    // the bits kernel 56 -> 43 us (rocprofv3, MI355X).
+    // More query blocks than CUs (qPerBlock > 0: the kernel's queries per workgroup): a CU's time
+    // is its share of blocks times their length, so a last partial round of blocks costs almost a
+    // whole one (100k x 100k at 128 queries: 782 blocks on 256 CUs).  Pick the part count p <= 16
+    // (>= 4 tiles per part) minimising ceil(blocks * p / CUs) * ceil(tiles / p).  At 100k x 100k
+    // (u8, 256 queries per block) p = 4, 8, 16 measured 2.01, 1.88, 1.80 ms against the model's
+    // 1.12 : 1.04 : 1 (tools/knn_parts_sweep.py under rocprofv3; p = 1 at 128 queries: 2.87 ms).
     // FM3D_I8_PARTS overrides the part count (a tuning-only knob, read on every call so A/B runs in
-    // one process see changes); it is clamped to [1, tiles] and ignored when the query blocks
-    // already fill the CUs.
+    // one process see changes); it is clamped to [1, tiles].
     const char* e = getenv("FM3D_I8_PARTS");
     const int forced = e ? atoi(e) : 0;
-    const int nBlk = (nA + kQ - 1) / kQ;
+    const int qb = qPerBlock > 0 ? qPerBlock : kQ;
+    const int nBlk = (nA + qb - 1) / qb;
     const int nTiles = (nB + kT - 1) / kT;
-    if (nBlk <= 0 || nCU <= 0 || nBlk >= nCU) return 1;
+    if (nBlk <= 0 || nCU <= 0) return 1;
     if (forced > 0) return forced < (nTiles > 1 ? nTiles : 1) ? forced : (nTiles > 1 ? nTiles : 1);
+    if (nBlk >= nCU) {
+        if (qPerBlock <= 0) return 1;
+        int best = 1;
+        long long bestCost = 0;
+        for (int p = 1; p <= 16; p++) {
+            if (p > 1 && nTiles / p < 4) break;
+            const long long cost = (((long long)nBlk * p + nCU - 1) / nCU) * ((nTiles + p - 1) / p);
+            if (p == 1 || cost < bestCost) {
+                best = p;
+                bestCost = cost;
+            }
+        }
+        return best;
+    }
     int p = (4 * nCU + nBlk - 1) / nBlk;
     if (p > 16) p = 16;
     while (p > 1 && nTiles / p < 4) p--;
