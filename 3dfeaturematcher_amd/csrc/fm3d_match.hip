@@ -203,16 +203,22 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
     v4i pre[kPre];
     uint32_t preCt = 0;
     auto load_tile = [&](int t) {
+        // rows past nB only in the last tile: the others load without a per-chunk test
+        const uint8_t* tb = B + (size_t)t * kT * rowBytes;
+        if ((t + 1) * kT <= nB) {
 #pragma unroll
-        for (int i = 0; i < kPre; i++) {
-            const int c = tid + i * kThreads;
-            v4i v = {0, 0, 0, 0};
-            if (c < total) {
-                const int row = c / chunksPerRow, ch = c - row * chunksPerRow;
-                const int j = t * kT + row;
-                if (j < nB) v = *(const v4i*)(B + (size_t)j * rowBytes + 16 * ch);
+            for (int i = 0; i < kPre; i++) {
+                const int c = tid + i * kThreads;
+                if (c < total) pre[i] = *(const v4i*)(tb + (size_t)c * 16);
             }
-            pre[i] = v;
+        } else {
+#pragma unroll
+            for (int i = 0; i < kPre; i++) {
+                const int c = tid + i * kThreads;
+                v4i v = {0, 0, 0, 0};
+                if (c < total && t * kT + c / chunksPerRow < nB) v = *(const v4i*)(tb + (size_t)c * 16);
+                pre[i] = v;
+            }
         }
         if (tid < kT) {
             const int j = t * kT + tid;
