@@ -95,13 +95,10 @@ static void orc_undistort1(const orc_camera *c, double x, double y, double *ox, 
 /* cvProjectPoints2 (OpenCV 2.4) for one point with rotation matrix R (row-major)
    and translation t.  Call sites: singlecameratriangulator.cpp:388 (R=I,t=0) and
    :602 (R = Rodrigues(decompose(g12))). */
-static void orc_project1(const orc_camera *c, const double R[9], const double t[3],
-                         double X, double Y, double Z, double *u, double *v)
+/* cvProjectPoints2's distortion and intrinsics of a camera-frame point (x, y, z) */
+static void orc_project_xyz(const orc_camera *c, double x, double y, double z, double *u, double *v)
 {
     const double *k = c->k;
-    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
-    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
-    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
     double r2, r4, r6, a1, a2, a3, cdist, icdist2, xd, yd;
     z = z ? 1. / z : 1;
     x *= z;
@@ -118,6 +115,13 @@ static void orc_project1(const orc_camera *c, const double R[9], const double t[
     yd = y * cdist * icdist2 + k[2] * a3 + k[3] * a1;
     *u = xd * c->fx + c->cx;
     *v = yd * c->fy + c->cy;
+}
+
+static void orc_project1(const orc_camera *c, const double R[9], const double t[3],
+                         double X, double Y, double Z, double *u, double *v)
+{
+    orc_project_xyz(c, R[0] * X + R[1] * Y + R[2] * Z + t[0], R[3] * X + R[4] * Y + R[5] * Z + t[1],
+                    R[6] * X + R[7] * Y + R[8] * Z + t[2], u, v);
 }
 
 ORC_API void orc_undistort(const orc_camera *c, const double *xy, int n, double *out)
@@ -707,6 +711,15 @@ static double orc_fexp(int mode, double x)
 {
     if (!(mode & ORC_LM_DETMATH) || (mode & ORC_LIBM_EXP)) return exp(x);
     return (mode & ORC_DET_1ULP) ? fm3d_exp(x) : fm3d_exp_cr(x);
+}
+/* the four transcendentals elementwise in a mode (tests/test_crmath.py pins the correctly rounded
+   ones against mpmath): fn 0 sin(x), 1 cos(x), 2 atan2(x, y), 3 exp(x) */
+ORC_API void orc_math_eval(int fn, int mode, const double *x, const double *y, int n, double *out)
+{
+    int i;
+    for (i = 0; i < n; i++)
+        out[i] = fn == 0 ? orc_fsin(mode, x[i]) : fn == 1 ? orc_fcos(mode, x[i])
+               : fn == 2 ? orc_fatan2(mode, x[i], y[i]) : orc_fexp(mode, x[i]);
 }
 
 static void orc_sph2car(int mode, double phi, double theta, double n[3])
@@ -1421,7 +1434,8 @@ ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], cons
    deterministic transcendentals).  Per point: normals sph2car(phi0 + dphi, theta0 + dtheta) on an
    Hphi x Htheta grid of half width span around car2sph(X/|X|); per normal the level-0 samples
    I1 (image 1 at the pixel) and I2 (image 2 through the plane); score = NCC or -2 (a failing
-   pixel, a flat patch).  The five sums are accumulated per lane l = offset index mod 64 in offset
+   pixel, a flat patch).  Camera 2 sees the plane point P = k r of the ray r = (ux, uy, 1) at
+   k (R2 r) + t2 (round 5: R2 r once per entry, not R2 P once per hypothesis).  The five sums are accumulated per lane l = offset index mod 64 in offset
    order and combined by the xor tree over 64 lanes -- the GPU's order, so the scores are bit-equal.
    scores: P x H, normals: P x 3 (best, lowest h on ties; X/|X| if none), best: P (-1 if none). */
 ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const double t2[3], const uint8_t *img1,
@@ -1471,7 +1485,11 @@ ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const
                     k = mm / nn;
                     P0 = k * ux; P1 = k * uy; P2 = k * 1.;
                     if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm))) { fail = 1; continue; }
-                    orc_project1(cam, R2, t2, P0, P1, P2, &u, &v);
+                    /* R2 P + t2 = k (R2 r) + t2 for the ray r = (ux, uy, 1): R2 r is the same for
+                       every hypothesis (the GPU stages it once per entry) */
+                    orc_project_xyz(cam, k * (R2[0] * ux + R2[1] * uy + R2[2]) + t2[0],
+                                    k * (R2[3] * ux + R2[4] * uy + R2[5]) + t2[1],
+                                    k * (R2[6] * ux + R2[7] * uy + R2[8]) + t2[2], &u, &v);
                     if (!orc_pixel_good(u, v, 1.0, w, h)) { fail = 1; continue; }
                     b = (double)orc_bilinear(img2, w, h, (float)u, (float)v);
                     S[0][l] += a; S[1][l] += b; S[2][l] += a * a; S[3][l] += b * b; S[4][l] += a * b;

@@ -30,6 +30,20 @@ def tree_stats(reset=False):
             arr[i] = 0
     return out
 
+def math_eval(fn, x, y=None, mode=DETMATH):
+    """orc_math_eval: fn "sin", "cos", "exp" of x, or "atan2" of (x, y) = atan2(x, y), elementwise,
+    in an oracle mode (DETMATH: include/fm3d_crmath.h's correctly rounded functions; DETMATH |
+    DET_1ULP: fm3d_detmath.h's; 0: libm)."""
+    f = {"sin": 0, "cos": 1, "atan2": 2, "exp": 3}[fn]
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = x if y is None else np.ascontiguousarray(y, dtype=np.float64)
+    out = np.empty_like(x)
+    dp = ctypes.POINTER(ctypes.c_double)
+    lib().orc_math_eval(ctypes.c_int(f), ctypes.c_int(mode), x.ctypes.data_as(dp), y.ctypes.data_as(dp),
+                        ctypes.c_int(x.size), out.ctypes.data_as(dp))
+    return out
+
+
 ST_OK, ST_NO_PIXELS, ST_ABORT_BBOX, ST_ABORT_PIX1, ST_ABORT_PIX2, ST_NAN_PLANE, ST_NAN_NORMAL = range(7)
 
 

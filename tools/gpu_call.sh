@@ -2,7 +2,7 @@
 # gpurun wrapper for this container: retries ONLY when the box could not be prepared
 # (status "transient": nothing ran, nothing charged).  Usage: tools/gpu_call.sh TIMEOUT 'cmd'
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 ${GPU_CALL_ATTEMPTS:-8}); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" > /tmp/gpu_call.log 2>&1
   rc=$?
   if grep -q "status=transient" /tmp/gpu_call.log || [ $rc -eq 3 ]; then
