@@ -207,24 +207,27 @@ __device__ __forceinline__ float fast_atan2f(float y, float x) {
 // prefix (flag 2) with a ballot, and -- once every word up to it carries this launch's epoch -- adds
 // the counts up to it; with no inclusive prefix in the window it moves 64 blocks further back.  Lane 0
 // publishes the block's inclusive prefix.  Returns (on every lane) the number of items of all earlier
-// blocks.  Status words are device-scope release / acquire atomics (vector memory).  A walk of one
+// blocks.  Status words are device-scope RELAXED atomics (vector memory, past the per-XCD caches): a
+// word carries everything a successor needs (count, flag, epoch), and no block reads another's
+// other outputs, so nothing has to be ordered around them -- release / acquire would add an L2
+// writeback and invalidate per access (about 3.5 us each, MI355X_MICROARCH.md).  A walk of one
 // word per step cost a memory round trip per predecessor (triangulate_compact 51 us at C2).
 __device__ inline int lookback_exclusive(unsigned long long* st, unsigned epoch, int bid, int agg) {
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long tag = (unsigned long long)epoch << 32;
     if (bid == 0) {
         if (lane == 0)
-            __hip_atomic_store(&st[0], tag | (2ull << 30) | (unsigned)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&st[0], tag | (2ull << 30) | (unsigned)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
     if (lane == 0)
-        __hip_atomic_store(&st[bid], tag | (1ull << 30) | (unsigned)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st[bid], tag | (1ull << 30) | (unsigned)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ex = 0;
     for (int base = bid - 1;;) {
         const int b = base - lane;
         // below block 0 (never reached: block 0's word is inclusive) reads as an empty inclusive prefix
         const unsigned long long w =
-            b >= 0 ? __hip_atomic_load(&st[b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : (tag | (2ull << 30));
+            b >= 0 ? __hip_atomic_load(&st[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (tag | (2ull << 30));
         const bool ready = (unsigned)(w >> 32) == epoch;
         const unsigned long long incl = __ballot(ready && ((w >> 30) & 3u) == 2u);
         const unsigned long long notReady = __ballot(!ready);
@@ -241,7 +244,7 @@ __device__ inline int lookback_exclusive(unsigned long long* st, unsigned epoch,
         base -= 64;
     }
     if (lane == 0)
-        __hip_atomic_store(&st[bid], tag | (2ull << 30) | (unsigned)(ex + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st[bid], tag | (2ull << 30) | (unsigned)(ex + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return ex;
 }
 

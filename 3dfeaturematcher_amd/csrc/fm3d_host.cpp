@@ -163,6 +163,8 @@ struct fm3d_ctx {
     // staged pipeline inputs
     int stNA = 0, stNB = 0, stDim = 0, stType = 0, stDimPad = 0, stQueryOffset = 0;
     int stK = 0, stP = 0;  // matches and inliers of the last fm3d_pipeline_run_dlt
+    bool stageEv = true;   // the last pipeline_front recorded ev[3] / ev[5] (FM3D_STAGE_EVENTS)
+    int* frontHostCnt = nullptr;  // pipeline_front: the DLT kernel also stores (K, P) here (device pointer)
     int nccP = 0;          // points of the last successful fm3d_pipeline_run_ncc (its score rows)
     bool staged = false;
     hipEvent_t ev[10];     // [0..1] standalone LM, [2..7] pipeline stages, [8] submit start, [1] end
@@ -466,6 +468,23 @@ bool f32_mfma() {
 
 // knn2 + NNDR flags on staged descriptors (device), results in c->idx/key/fkey/cand/flag
 // the look-back state of one fused-compaction launch of nBlocks blocks on c's stream
+bool stage_events() {
+    const char* e = getenv("FM3D_STAGE_EVENTS");
+    return !(e && e[0] == '0');
+}
+
+// match_ms (row constants, knn, NNDR and its compaction: one stage since NNDR is fused into the
+// match's last launch; nndr_ms stays 0) and triangulate_ms, when the step recorded its stage events
+void stage_times(fm3d_ctx* c, fm3d_pipeline_stats* stats) {
+    float ms = 0;
+    if (!c->stageEv) return;
+    hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+    stats->match_ms = ms;
+    stats->nndr_ms = 0;
+    hipEventElapsedTime(&ms, c->ev[3], c->ev[5]);
+    stats->triangulate_ms = ms;
+}
+
 int make_lookback(fm3d_ctx* c, int nBlocks, fm3d::LookBack* lb) {
     if (!c->lbCtr.p) {
         HIPCHK(c, c->lbCtr.ensure(64));
@@ -2003,8 +2022,11 @@ int pipeline_front(fm3d_ctx* c) {
     if ((r = run_match(c, nA, nB, c->stType, c->stDimPad, c->s.nndrEpsilon, c->stQueryOffset, false,
                        c->matches.as<fm3d_dmatch>(), cnt + 0)))
         return r;
-    HIPCHK(c, hipEventRecord(ev[3], c->stream));
-    HIPCHK(c, hipEventRecord(ev[4], c->stream));
+    // the stage boundaries (ev[3]: match + NNDR done, ev[5]: DLT done) only when asked for: a timed
+    // event between two launches costs the C2 step 4-10 us of gap (rocprofv3 trace, round 5);
+    // FM3D_STAGE_EVENTS=0 leaves only the step's own ev[2] / ev[1]
+    c->stageEv = stage_events();
+    if (c->stageEv) HIPCHK(c, hipEventRecord(ev[3], c->stream));
     // a4, a5: triangulate (matches are device resident; K <= nA)
     HIPCHK(c, c->triPts.ensure((size_t)(nA + 1) * 3 * sizeof(double)));
     HIPCHK(c, c->triMask.ensure((size_t)(nA + 1) * sizeof(int)));
@@ -2027,10 +2049,11 @@ int pipeline_front(fm3d_ctx* c) {
     {   // DLT with the inliers' compaction fused (launch_triangulate_compact)
         fm3d::LookBack lb;
         if ((r = make_lookback(c, fm3d::triangulate_compact_blocks(nA), &lb))) return r;
-        fm3d::launch_triangulate_compact(tp, c->pts.as<double>(), c->srcIdx.as<int>(), cnt + 1, lb, c->stream);
+        fm3d::launch_triangulate_compact(tp, c->pts.as<double>(), c->srcIdx.as<int>(), cnt + 1, lb, c->stream,
+                                         c->frontHostCnt);
     }
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(ev[5], c->stream));
+    if (c->stageEv) HIPCHK(c, hipEventRecord(ev[5], c->stream));
     return FM3D_OK;
 }
 
@@ -2133,12 +2156,7 @@ int finalize_full(fm3d_ctx* c, const fm3d_lm_stats& ls, hipEvent_t t0, bool stag
         stats->inliers = P;
         stats->kept = kept;
         float ms;
-        hipEventElapsedTime(&ms, ev[2], ev[3]);
-        stats->match_ms = ms;
-        hipEventElapsedTime(&ms, ev[3], ev[4]);
-        stats->nndr_ms = ms;
-        hipEventElapsedTime(&ms, ev[4], ev[5]);
-        stats->triangulate_ms = ms;
+        stage_times(c, stats);
         ms = 0;
         if (staged_in_step) hipEventElapsedTime(&ms, ev[8], ev[2]);
         stats->pyramid_ms = ms;  // the inputs' H2D + pyramids (fm3d_pipeline_submit only)
@@ -2314,10 +2332,15 @@ int fm3d_pipeline_submit_dlt(fm3d_ctx* c) {
     PENDING_CHECK(c);
     hipSetDevice(c->device);
     int r;
-    if ((r = pipeline_front(c))) return r;
     HIPCHK(c, c->hSmall.ensure(sizeof(PipeSmall)));
     PipeSmall* hs = c->hSmall.as<PipeSmall>();
-    HIPCHK(c, hipMemcpyAsync(hs->cnt, c->pcnt.p, sizeof(hs->cnt), hipMemcpyDeviceToHost, c->stream));
+    // the counts reach the page-locked buffer from the DLT kernel itself (no copy launch)
+    void* dcnt = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer(&dcnt, hs->cnt, 0));
+    c->frontHostCnt = (int*)dcnt;
+    r = pipeline_front(c);
+    c->frontHostCnt = nullptr;
+    if (r) return r;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     c->pending = true;
     c->pendingDlt = true;
@@ -2344,12 +2367,7 @@ int fm3d_pipeline_wait_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stat
         stats->matches = K;
         stats->inliers = P;
         float ms;
-        hipEventElapsedTime(&ms, ev[2], ev[3]);
-        stats->match_ms = ms;
-        hipEventElapsedTime(&ms, ev[3], ev[4]);
-        stats->nndr_ms = ms;
-        hipEventElapsedTime(&ms, ev[4], ev[5]);
-        stats->triangulate_ms = ms;
+        stage_times(c, stats);
         hipEventElapsedTime(&ms, ev[2], ev[1]);
         stats->total_ms = ms;
     }
@@ -2440,12 +2458,7 @@ int fm3d_pipeline_wait_ncc(fm3d_ctx* c, int* nPoints, fm3d_pipeline_stats* stats
         stats->inliers = P;
         stats->kept = P;
         float ms;
-        hipEventElapsedTime(&ms, ev[2], ev[3]);
-        stats->match_ms = ms;
-        hipEventElapsedTime(&ms, ev[3], ev[4]);
-        stats->nndr_ms = ms;
-        hipEventElapsedTime(&ms, ev[4], ev[5]);
-        stats->triangulate_ms = ms;
+        stage_times(c, stats);
         hipEventElapsedTime(&ms, ev[6], ev[7]);
         stats->lm_ms = ms;  // the normal stage: here the NCC scoring
         hipEventElapsedTime(&ms, ev[2], ev[1]);

@@ -332,7 +332,7 @@ int nndr_compact_blocks(int nA);
 // setKeypoints + triangulate with the compaction of the inliers: out (P x 3), srcIdx (P), *count = P;
 // mask (K) as launch_triangulate
 void launch_triangulate_compact(const TriParams& p, double* out, int* srcIdx, int* count, const LookBack& lb,
-                                hipStream_t s);
+                                hipStream_t s, int* hostCnt = nullptr);
 int triangulate_compact_blocks(int K);
 
 // ---------------- images ----------------

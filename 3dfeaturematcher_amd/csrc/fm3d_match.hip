@@ -635,16 +635,32 @@ __global__ __launch_bounds__(256) void nndr_compact_kernel(int type, const int* 
         if (parts > 1) {
             int b1 = INT_MAX, b2 = INT_MAX;
             i1 = i2 = -1;
-            for (int s = 0; s < parts; s++) {
-                const size_t o = ((size_t)s * nA + q) * 2;
-                int j0 = pIdx[o], j1 = pIdx[o + 1];
-                int k0 = pKey[o], k1 = pKey[o + 1];
+            auto merge_part = [&](int j0, int j1, int k0, int k1) {
                 if (j1 >= 0 && j1 < j0) {  // visit the part's two candidates in train index order
                     const int tj = j0; j0 = j1; j1 = tj;
                     const int tk = k0; k0 = k1; k1 = tk;
                 }
                 if (j0 >= 0) top2_insert(k0, j0, b1, i1, b2, i2);
                 if (j1 >= 0) top2_insert(k1, j1, b1, i1, b2, i2);
+            };
+            // the first 16 parts' lists loaded before any is merged (one round of load latency, not
+            // one per part: 10.5 -> see DESIGN.md §3.2 at C2's 16 parts); knn2_u8_parts never makes
+            // more, FM3D_I8_PARTS may
+            int2 pj[16], pk[16];
+#pragma unroll
+            for (int s = 0; s < 16; s++) {
+                if (s < parts) {
+                    const size_t o = ((size_t)s * nA + q) * 2;
+                    pj[s] = *(const int2*)(pIdx + o);
+                    pk[s] = *(const int2*)(pKey + o);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < 16; s++)
+                if (s < parts) merge_part(pj[s].x, pj[s].y, pk[s].x, pk[s].y);
+            for (int s = 16; s < parts; s++) {
+                const size_t o = ((size_t)s * nA + q) * 2;
+                merge_part(pIdx[o], pIdx[o + 1], pKey[o], pKey[o + 1]);
             }
             if (type == FM3D_DESC_U8) {
                 d1 = sqrtf((float)b1);

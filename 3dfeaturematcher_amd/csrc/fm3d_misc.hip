@@ -116,9 +116,13 @@ __global__ __launch_bounds__(kTriThreads) void triangulate_kernel(TriParams p) {
 }
 // the same with the inliers compacted in match order (fm3d_kernels.h LookBack): out, srcIdx, *count
 // -- the pipeline's a4/a5 without compact<Point3>'s launch (12 us at C2, one workgroup)
+// hostCnt (page-locked host memory, or null): the last block also stores (match count, inlier count)
+// there with system-scope stores, so a caller that waits for the kernel reads them without a copy
+// launch (fm3d_pipeline_submit_dlt; 3.4 us of copy kernel and a 6 us gap at C2)
 __global__ __launch_bounds__(kTriThreads) void triangulate_compact_kernel(TriParams p, double* __restrict__ out,
                                                                           int* __restrict__ srcIdx,
-                                                                          int* __restrict__ count, LookBack lb) {
+                                                                          int* __restrict__ count, LookBack lb,
+                                                                          int* hostCnt) {
     __shared__ int sBid;
     const int lane = threadIdx.x;
     if (lane == 0) sBid = (int)(atomicAdd(lb.ctr, 1u) - lb.base);
@@ -136,7 +140,14 @@ __global__ __launch_bounds__(kTriThreads) void triangulate_compact_kernel(TriPar
         out[3 * o + 2] = X[2] / X[3];
         srcIdx[o] = i;
     }
-    if (lane == 0 && bid == (int)gridDim.x - 1) *count = ex + __popcll(bal);
+    if (lane == 0 && bid == (int)gridDim.x - 1) {
+        const int total = ex + __popcll(bal);
+        *count = total;
+        if (hostCnt) {
+            __hip_atomic_store(&hostCnt[0], p.Kdev ? *p.Kdev : p.K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hostCnt[1], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // ---------------- cv::pyrDown (8U) ----------------
@@ -432,8 +443,9 @@ void launch_triangulate(const TriParams& p, hipStream_t s) {
 int triangulate_compact_blocks(int K) { return K > 0 ? (K + kTriThreads - 1) / kTriThreads : 1; }
 
 void launch_triangulate_compact(const TriParams& p, double* out, int* srcIdx, int* count, const LookBack& lb,
-                                hipStream_t s) {
-    triangulate_compact_kernel<<<triangulate_compact_blocks(p.K), kTriThreads, 0, s>>>(p, out, srcIdx, count, lb);
+                                hipStream_t s, int* hostCnt) {
+    triangulate_compact_kernel<<<triangulate_compact_blocks(p.K), kTriThreads, 0, s>>>(p, out, srcIdx, count, lb,
+                                                                                      hostCnt);
 }
 
 void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s) {
