@@ -843,9 +843,10 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
         }
         // one launch: every slot runs its point through all levels, coarsest first
         // (optimize_pyramid :225-241)
-        hipLaunchKernelGGL(reinterpret_cast<void (*)(fm3d::LMParams)>(const_cast<void*>(kptr)),
-                           dim3((unsigned)groups), dim3(fm3d::kLM2Threads), 0, c->stream, p);
-        HIPCHK(c, hipGetLastError());
+        // through the runtime's launch by address (not a call through a cast function pointer, which
+        // the host sanitizers' function-type check rejects: tests/test_sanitizers.py)
+        void* kargs[] = {&p};
+        HIPCHK(c, hipLaunchKernel(kptr, dim3((unsigned)groups), dim3(fm3d::kLM2Threads), kargs, 0, c->stream));
         HIPCHK(c, hipEventRecord(e1, c->stream));
     }
     if (stats) {

@@ -814,7 +814,7 @@ def test_c5_1m_keypoints_query_blocks(fm3d, orc, synth):
     full = shard.run_shard(fp, s, 0, n)
     qsel = mod.subset_queries(mod.WORKLOADS["c5sub"], n)
     sub10 = full[np.isin(full["queryIdx"], qsel)]
-    assert len(sub10) == len(fx["records"]) == 36_448 and sub10.tobytes() == fx["records"].tobytes()
+    assert len(sub10) == len(fx["records"]) == 36_449 and sub10.tobytes() == fx["records"].tobytes()
     parts = [shard.run_shard_queries(fp, s, shard.query_blocks(n, 4, r)) for r in range(4)]
     merged = np.concatenate(parts)
     merged = merged[np.argsort(merged["queryIdx"], kind="stable")]
