@@ -36,15 +36,18 @@ __device__ __forceinline__ double xor_sum(double v) {
 
 // The evaluateNormal geometry of one neighbourhood entry through one hypothesis' plane (ray-plane
 // intersection :421-470, isInBoundingBox :646-655, projectPointsToImage2 :591-644, isPixelGood
-// :657-665) in the LM kernel's arithmetic forms (fm3d_lm2.hip geometry2), each the
-// same bits as project1 + pixel_good wherever the pixel is good -- the only case its u, v are used:
-//  * mm / nn by div_nn's fast sequence when the hypothesis-uniform numerator passes div_nn_ok: the
-//    quotient is exact below 2^100 and NaN or >= 2^100 elsewhere, so the bounding box decides alike;
-//  * 1/z by recip_z_lo (one guard); a2 = r2 + 2x^2 as fma(x*x, 2, r2) (2*RN(x*x) == RN(2x*x));
-//  * project1's NaN for an infinite r6 dropped (such a u or v is infinite or NaN: not good);
+// :657-665), without the ray-plane division (round 5; the oracle's orc_ncc_hypotheses states the
+// same arithmetic, this mode has no reference counterpart to keep the reference's order for):
+//  * the plane point is P = (mm / nn) r for the ray r = (ux, uy, 1), nn = n . r.  The bounding box
+//    |P0| < cm, |P1| < cm, 0 < P2 < cm reads |mm ux| < cm |nn|, |mm uy| < cm |nn|, |mm| < cm |nn| with
+//    mm and nn of one sign (nn = 0 fails every test, as P = inf / NaN did);
+//  * camera 2 sees P at (mm q + nn t2) / nn, q = R2 r staged once per entry (q0..q2), so the
+//    normalised coordinates are (mm q0 + nn t0) / (mm q2 + nn t2) and (mm q1 + nn t1) / (the same):
+//    one reciprocal (recip_z_lo, one guard), no quotient mm / nn;
+//  * r2 + 2x^2 as fma(x*x, 2, r2) (2*RN(x*x) == RN(2x*x)); project1's NaN for an infinite r6
+//    dropped (such a u or v is infinite or NaN: not good);
 //  * 0 <= u <= xmax as bits(u) <= bits(xmax): u is never -0.0 (the host hands the kernel a
 //    principal point of +0.0 for -0.0, fm3d_host.cpp lm_camera), negatives and NaNs lie above.
-// (ncc_geometry_m.)
 typedef unsigned long long LaneMask;
 // v where the lane's bit of m is set, else 0 (v_cndmask with the SGPR mask as selector)
 __device__ __forceinline__ unsigned ncc_sel_u32(unsigned v, LaneMask m) {
@@ -59,20 +62,20 @@ struct NccGeo {
     unsigned off;
     LaneMask good;
 };
-// Camera 2 sees the plane point P = kk r of the ray r = (ux, uy, 1) at kk (R2 r) + t2: q = R2 r is
-// hypothesis-independent and staged once per entry (q0..q2; round 5, 12 fp64 operations fewer per
-// pixel and hypothesis than R2 P + t2; the oracle's orc_ncc_hypotheses uses the same form).
+// sgn: the sign of mm as +1 / -1, 0 for mm = 0 or NaN (hypothesis-uniform); amm = |mm|.  The limit
+// cm (sgn nn) equals cm |nn| where mm and nn share a sign and is <= 0 (every test fails) elsewhere,
+// so the sign test costs one multiply
 __device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, double uy, double q0, double q1,
-                                                 double q2, double n0, double n1, double n2, double mm, bool mok,
-                                                 double cm, unsigned long long xmaxb, unsigned long long ymaxb) {
+                                                 double q2, double n0, double n1, double n2, double mm, double amm,
+                                                 double sgn, double cm, unsigned long long xmaxb,
+                                                 unsigned long long ymaxb) {
     NccGeo g;
     const double nn = n0 * ux + n1 * uy + n2 * 1.;
-    const double kk = mok ? div_nn(mm, nn, true) : mm / nn;
-    const double P0 = kk * ux, P1 = kk * uy, P2 = kk * 1.;
-    const LaneMask inbox = __ballot(fabs(P0) < cm) & __ballot(fabs(P1) < cm) & __ballot(P2 > 0.) & __ballot(P2 < cm);
-    double x = kk * q0 + p.t2[0];
-    double y = kk * q1 + p.t2[1];
-    const double z = recip_z_lo(kk * q2 + p.t2[2]);
+    const double lim = cm * (sgn * nn);
+    const LaneMask inbox = __ballot(fabs(mm * ux) < lim) & __ballot(fabs(mm * uy) < lim) & __ballot(amm < lim);
+    double x = mm * q0 + nn * p.t2[0];
+    double y = mm * q1 + nn * p.t2[1];
+    const double z = recip_z_lo(mm * q2 + nn * p.t2[2]);
     x *= z;
     y *= z;
     const double xx = x * x, yy = y * y;
@@ -159,8 +162,11 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
     const double xmax = (double)p.w, ymax = (double)p.h;  // isPixelGood at scale 1
     const unsigned long long xmaxb = (unsigned long long)__double_as_longlong(xmax);
     const unsigned long long ymaxb = (unsigned long long)__double_as_longlong(ymax);
-    bool mok[KPW];
-    for (int k = 0; k < KPW; k++) mok[k] = k < nh && div_nn_ok(mm[k]);
+    double sgn[KPW], amm[KPW];
+    for (int k = 0; k < KPW; k++) {
+        sgn[k] = mm[k] > 0. ? 1. : mm[k] < 0. ? -1. : 0.;
+        amm[k] = fabs(mm[k]);
+    }
     // hypotheses of this wave that already failed on some entry (wave-uniform): they score -2
     // whatever their sums, so their geometry is not computed again
     unsigned dead = 0;
@@ -220,7 +226,8 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
             for (int k = 0; k < KPW; k++) {
                 if (k >= nk) break;
                 if ((dead >> k) & 1) continue;  // wave-uniform
-                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], mok[k], cm, xmaxb, ymaxb);
+                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], amm[k], sgn[k], cm,
+                                                  xmaxb, ymaxb);
                 if (okm & ~g.good) badNow |= 1u << k;  // scalar
                 const float bf = ncc_bilinear_f(p.img2, g.off, p.w, g.fx, g.fy);
                 const double b = (double)__uint_as_float(ncc_sel_u32(__float_as_uint(bf), okm));

@@ -1434,8 +1434,9 @@ ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], cons
    deterministic transcendentals).  Per point: normals sph2car(phi0 + dphi, theta0 + dtheta) on an
    Hphi x Htheta grid of half width span around car2sph(X/|X|); per normal the level-0 samples
    I1 (image 1 at the pixel) and I2 (image 2 through the plane); score = NCC or -2 (a failing
-   pixel, a flat patch).  Camera 2 sees the plane point P = k r of the ray r = (ux, uy, 1) at
-   k (R2 r) + t2 (round 5: R2 r once per entry, not R2 P once per hypothesis).  The five sums are accumulated per lane l = offset index mod 64 in offset
+   pixel, a flat patch).  Round 5: the plane point P = (mm / nn) r of the ray r = (ux, uy, 1) is
+   tested against the bounding box and projected without the quotient (camera 2 sees it at
+   (mm R2 r + nn t2) / nn, so x = (mm q0 + nn t0) / (mm q2 + nn t2), q = R2 r).  The five sums are accumulated per lane l = offset index mod 64 in offset
    order and combined by the xor tree over 64 lanes -- the GPU's order, so the scores are bit-equal.
    scores: P x H, normals: P x 3 (best, lowest h on ties; X/|X| if none), best: P (-1 if none). */
 ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const double t2[3], const uint8_t *img1,
@@ -1470,7 +1471,7 @@ ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const
             e = 0;
             for (i = -ray; i <= ray; i++)
                 for (j = -ray; j <= ray; j++) {
-                    double px, py, ux, uy, nn, k, P0, P1, P2, u, v, a, b;
+                    double px, py, ux, uy, nn, lim, q0, q1, q2, u, v, a, b;
                     if (i * i + j * j > ray * ray) continue;
                     l = e++ & 63;  /* the offset index's lane */
                     px = ccx + i;
@@ -1482,14 +1483,17 @@ ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const
                     a = (double)orc_bilinear(img1, w, h, (float)px, (float)py);
                     orc_undistort1(cam, px, py, &ux, &uy);
                     nn = n[0] * ux + n[1] * uy + n[2] * 1.;
-                    k = mm / nn;
-                    P0 = k * ux; P1 = k * uy; P2 = k * 1.;
-                    if (!((P0 > -cm && P0 < cm) && (P1 > -cm && P1 < cm) && (P2 > 0. && P2 < cm))) { fail = 1; continue; }
-                    /* R2 P + t2 = k (R2 r) + t2 for the ray r = (ux, uy, 1): R2 r is the same for
-                       every hypothesis (the GPU stages it once per entry) */
-                    orc_project_xyz(cam, k * (R2[0] * ux + R2[1] * uy + R2[2]) + t2[0],
-                                    k * (R2[3] * ux + R2[4] * uy + R2[5]) + t2[1],
-                                    k * (R2[6] * ux + R2[7] * uy + R2[8]) + t2[2], &u, &v);
+                    /* the plane point P = (mm / nn) r without the division: |P0|, |P1| < cm and
+                       0 < P2 < cm as |mm ux|, |mm uy|, |mm| < cm |nn| with mm, nn of one sign */
+                    lim = cm * fabs(nn);
+                    if (!(fabs(mm * ux) < lim && fabs(mm * uy) < lim && fabs(mm) < lim &&
+                          ((mm > 0. && nn > 0.) || (mm < 0. && nn < 0.)))) { fail = 1; continue; }
+                    /* camera 2 sees P at (mm q + nn t2) / nn, q = R2 r (the GPU stages q once per
+                       entry): the normalised coordinates need one reciprocal */
+                    q0 = R2[0] * ux + R2[1] * uy + R2[2];
+                    q1 = R2[3] * ux + R2[4] * uy + R2[5];
+                    q2 = R2[6] * ux + R2[7] * uy + R2[8];
+                    orc_project_xyz(cam, mm * q0 + nn * t2[0], mm * q1 + nn * t2[1], mm * q2 + nn * t2[2], &u, &v);
                     if (!orc_pixel_good(u, v, 1.0, w, h)) { fail = 1; continue; }
                     b = (double)orc_bilinear(img2, w, h, (float)u, (float)v);
                     S[0][l] += a; S[1][l] += b; S[2][l] += a * a; S[3][l] += b * b; S[4][l] += a * b;
