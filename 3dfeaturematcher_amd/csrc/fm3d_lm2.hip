@@ -94,6 +94,10 @@ struct SlotP2 {
     int pass, ekind, nev, len, pivot, t0, t1, q0, lw;
     unsigned projOff;  // byte offset of the point's frame pair's ProjConst in the table (p.proj)
     double n0[2], n1[2], n2[2], mm[2], w[2], hj[2];
+    // setup_eval's sph2car deferred to the wave (resolve_trig): the angles (phi, theta) of the
+    // evaluations whose bit in tpend is set
+    double ta[2], tb[2];
+    int tpend;
     double scale, xmax, ymax, ccx, ccy, ajn0s, tq, ajn1s, tq0, agiant, wF;
     const uint8_t* img1;
     const uint8_t* img2;
@@ -245,22 +249,60 @@ struct Ctl2 {
     }
     // evaluateNormal (normaloptimizer.cpp:65-149), per-call part, for evaluation ev.
     // Returns false if the normal is NaN (the call aborts before touching a pixel).
+    // The normal sph2car(phi = a, theta = b) and mm = n . X: inside the reduction range of the
+    // correctly rounded sin / cos the four values are finite (no NaN check can fail), and the wave
+    // computes them after the bookkeeping, one function per lane (resolve_trig: the same bits);
+    // outside it (never on real data) lane 0 computes them here, as before.
     __device__ bool setup_eval(SlotS2& S, SlotP2& P, int ev, double a, double b, double hj) {
-        double n0, n1, n2;
-        sph2car_cr(a, b, n0, n1, n2);  // par = (phi, theta)
-        if (n2 != n2 || n1 != n1 || n0 != n0) return false;
+        if (fabs(a) < FM3D_CR_RANGE && fabs(b) < FM3D_CR_RANGE) {
+            P.ta[ev] = a;
+            P.tb[ev] = b;
+            P.tpend |= 1 << ev;
+        } else {
+            double n0, n1, n2;
+            sph2car_cr(a, b, n0, n1, n2);  // par = (phi, theta)
+            if (n2 != n2 || n1 != n1 || n0 != n0) return false;
+            P.n0[ev] = n0;
+            P.n1[ev] = n1;
+            P.n2[ev] = n2;
+            P.mm[ev] = n0 * S.X0 + n1 * S.X1 + n2 * S.X2;
+            P.tpend &= ~(1 << ev);
+        }
         double w_theta = 1.0, w_phi = 1.0;
         if (fabs(b) - M_PI / 2 > 0 || fabs(a) - M_PI > 0) {
             w_theta = fm3d_exp_cr(fabs(b) - M_PI / 2) + 1;
             w_phi = fm3d_exp_cr(fabs(a) - M_PI + 1) + 1;
         }
-        P.n0[ev] = n0;
-        P.n1[ev] = n1;
-        P.n2[ev] = n2;
-        P.mm[ev] = n0 * S.X0 + n1 * S.X1 + n2 * S.X2;
         P.w[ev] = w_phi * w_theta;
         P.hj[ev] = hj;
         return true;
+    }
+    // setup_eval's deferred normals, by the whole wave (all lanes call it): lane 4e + f computes
+    // function f of evaluation e -- cos(theta), sin(theta), cos(phi), sin(phi) -- and lane 0 forms
+    // sph2car_cr's n0 = cos(theta) cos(phi), n1 = cos(theta) sin(phi), n2 = sin(theta) and mm
+    __device__ void resolve_trig(const SlotS2& S, SlotP2& P, int lane) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const int pend = __builtin_amdgcn_readfirstlane(P.tpend);
+        if (!pend) return;
+        const int e = lane >> 2, f = lane & 3;
+        double v = 0.;
+        if (e < 2 && ((pend >> e) & 1)) v = fm3d_sincos_sel_cr(f < 2 ? P.tb[e] : P.ta[e], (f & 1) == 0);
+        for (int k = 0; k < 2; k++) {
+            if (!((pend >> k) & 1)) continue;
+            const double ct = __shfl(v, 4 * k), st = __shfl(v, 4 * k + 1), cp = __shfl(v, 4 * k + 2),
+                         sp = __shfl(v, 4 * k + 3);
+            if (lane == 0) {
+                const double n0 = ct * cp, n1 = ct * sp, n2 = st;
+                P.n0[k] = n0;
+                P.n1[k] = n1;
+                P.n2[k] = n2;
+                P.mm[k] = n0 * S.X0 + n1 * S.X1 + n2 * S.X2;
+            }
+        }
+        if (lane == 0) P.tpend = 0;
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
     __device__ void count_eval(SlotS2& S) {
         S.s.nfev++;
@@ -1068,8 +1110,10 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
         if (lane == 0) {
             for (int k = 0; k < 4; k++) WS.cnt[k] = WS.cyc[k] = 0;
             WS.terms = WS.ctl = WS.wait = WS.nPass = WS.iter = 0;
+            sh.sp[w].tpend = 0;
             ctl.fetch(sh.ss[w], sh.sp[w]);
         }
+        ctl.resolve_trig(sh.ss[w], sh.sp[w], lane);
         for (;;) {
             if ((long long)rfl_u64(lane == 0 ? ++WS.iter : 0) > p.maxIter ||
                 (long long)(wall_clock64() - tStart) > p.maxTicks) {
@@ -1927,6 +1971,7 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
                 WS.cnt[cls]++;
                 WS.cyc[cls] += tp2 - WS.t0;
             }
+            if (own) ctl.resolve_trig(SS, SP, lane);
             __builtin_amdgcn_s_waitcnt(0);
         }
         if (lane == 0) {

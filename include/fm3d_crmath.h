@@ -176,6 +176,22 @@ FM3D_HD double fm3d_cos_cr(double x)
     return fm3d_dd_round(v);
 }
 
+/* fm3d_sin_cr(x) (cosine 0) or fm3d_cos_cr(x) (cosine 1), the same operations and so the same bits:
+   cos(x) = sin(x + pi/2) takes the quadrant q + 1 of the same reduction.  For a wave whose lanes
+   compute different ones side by side (the LM kernel's sph2car of an evaluation: four lanes) */
+FM3D_HD double fm3d_sincos_sel_cr(double x, int cosine)
+{
+    int q;
+    fm3d_dd r, v;
+    if (!(fabs(x) < FM3D_CR_RANGE)) return cosine ? fm3d_cos(x) : fm3d_sin(x);
+    if (!cosine && x == 0.0) return x;
+    r = fm3d_cr_reduce(x, &q);
+    q += cosine;
+    v = (q & 1) ? fm3d_cr_cos_kernel(r) : fm3d_cr_sin_kernel(r);
+    if (q & 2) v = fm3d_dd_neg(v);
+    return fm3d_dd_round(v);
+}
+
 /* atan(t) for a double-double t in [0, 1]: atan(c) + atan((t - c) / (1 + t c)), c = j/16 the
    nearest sixteenth (|u| <= 1/32), the series through u^19 (double-double through u^5) */
 FM3D_HD fm3d_dd fm3d_cr_atan01(fm3d_dd t)
