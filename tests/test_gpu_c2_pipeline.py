@@ -40,6 +40,51 @@ def test_pipeline_dlt_bitwise(fm3d, orc, synth, n, seed):
     assert np.array_equal(m3, m) and np.array_equal(pts3, pts) and np.array_equal(src3, src) and kept <= P
 
 
+def test_pipeline_dlt_counts_without_copies_and_stage_events(fm3d, orc, synth, monkeypatch):
+    """Round 5: the DLT kernel stores (matches, inliers) straight into the page-locked buffer, and
+    FM3D_STAGE_EVENTS=0 drops the stage-boundary events.  Alternating pairs with many, few and no
+    matches (an NNDR ratio no pair passes) on one context: every step's counts are that pair's
+    (never a stale value of the step before: one context alternates the two pairs), its matches and
+    points equal the oracle's, and without
+    stage events match_ms / triangulate_ms are 0 while total_ms and the results are unchanged."""
+    pairs = [synth.make_frame_pair(3000, seed=21), synth.make_frame_pair(700, seed=22)]
+    s = fm3d.Settings.default()
+    s.set_camera(pairs[0].cam)
+    s.pixelsRay, s.pyramids = 8, 1
+    ref = {}
+    for i, fp in enumerate(pairs):
+        for eps in (0.55, 1e-6):
+            q, t, _ = orc.match_nndr(fp.desc1, fp.desc2, orc.U8, eps, oracle_threads())
+            pts, _ = orc.triangulate(fp.cam, fp.g12, s.zThresholdMin, s.zThresholdMax, fp.kp1, fp.kp2, q, t)
+            ref[i, eps] = (q, pts)
+    assert len(ref[1, 1e-6][0]) == 0 < len(ref[1, 0.55][0])
+    ctxs, pipes = {}, {}
+    for eps in (0.55, 1e-6):
+        s.nndrEpsilon = eps
+        ctxs[eps] = fm3d.Context(s)
+        fm3d.SingleCameraTriangulator(ctxs[eps]).set_g12(pairs[0].g12)
+        pipes[eps] = fm3d.Pipeline(ctxs[eps])
+    try:
+        for events in ("1", "0"):
+            monkeypatch.setenv("FM3D_STAGE_EVENTS", events)
+            for i, eps in [(0, 0.55), (1, 1e-6), (1, 0.55), (0, 1e-6), (0, 0.55), (1, 0.55)]:
+                fp = pairs[i]
+                pipes[eps].upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+                P, st = pipes[eps].run_dlt()
+                m, pts, _ = pipes[eps].dlt_results(st["matches"], st["inliers"])
+                q, opts = ref[i, eps]
+                assert st["matches"] == len(q) and P == st["inliers"] == len(opts)
+                assert np.array_equal(m["queryIdx"], q) and np.array_equal(pts, opts)
+                assert st["total_ms"] > 0
+                if events == "0":
+                    assert st["match_ms"] == 0 and st["triangulate_ms"] == 0
+                elif len(q):
+                    assert st["match_ms"] > 0 and st["triangulate_ms"] > 0
+    finally:
+        for c in ctxs.values():
+            c.close()
+
+
 def test_pipeline_submit_wait_dlt_two_in_flight(fm3d, orc, synth):
     """fm3d_pipeline_submit_dlt / wait_dlt on two contexts in flight (the C2 serving loop) equal
     fm3d_pipeline_run_dlt; a pending front half blocks the other pipeline calls"""
