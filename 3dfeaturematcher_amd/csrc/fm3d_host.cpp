@@ -527,7 +527,8 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         HIPCHK(c, c->ctB.ensure((size_t)(nBPad + 1) * sizeof(int)));
         fm3d::launch_rowconst_u8(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, dimPad, c->cqA.as<int>(),
                                  c->ctB.as<int>(), c->stream);
-        const int parts = fm3d::knn2_u8_parts(nA, nB, c->nCU, fm3d::knn2_i8_queries_per_block(dimPad, 0));
+        const int parts = fm3d::knn2_u8_parts(nA, nB, c->nCU, fm3d::knn2_i8_queries_per_block(dimPad, 0),
+                                              fm3d::knn2_i8_tile_rows(dimPad, 0));
         if (parts > 1) {
             HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
             HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
@@ -591,7 +592,8 @@ int run_match(fm3d_ctx* c, int nA, int nB, int type, int dimPad, double eps, int
         HIPCHK(c, c->ctB.ensure((size_t)(nB + 1) * sizeof(int)));
         fm3d::launch_unpack_bits(c->A.as<uint8_t>(), nA, c->B.as<uint8_t>(), nB, c->A8.as<uint8_t>(),
                                  c->B8.as<uint8_t>(), c->ctB.as<int>(), c->stream);
-        const int parts = fm3d::knn2_u8_parts(nA, nB, c->nCU, fm3d::knn2_i8_queries_per_block(256, 1));
+        const int parts = fm3d::knn2_u8_parts(nA, nB, c->nCU, fm3d::knn2_i8_queries_per_block(256, 1),
+                                              fm3d::knn2_i8_tile_rows(256, 1));
         if (parts > 1) {
             HIPCHK(c, c->partIdx.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));
             HIPCHK(c, c->partKey.ensure((size_t)parts * nA * 2 * sizeof(int) + 16));

@@ -111,8 +111,9 @@ struct KnnOut {
 
 // u8 rows (dim padded to a multiple of 128 with value 128 on both sides -> no effect)
 // u8 rows: `parts` train-tile ranges (knn2_u8_parts), merged through partIdx/partKey
-int knn2_u8_parts(int nA, int nB, int nCU, int qPerBlock);
+int knn2_u8_parts(int nA, int nB, int nCU, int qPerBlock, int tileRows);
 int knn2_i8_queries_per_block(int dimPad, int bits);
+int knn2_i8_tile_rows(int dimPad, int bits);
 // int8-MFMA matcher for u8 rows (bits = 0) and for 32-byte binary rows unpacked by
 // launch_unpack_bits (bits = 1, dimPad 256); ctB = packed train row constants
 // deferMerge: with parts > 1 the parts' lists stay in partIdx / partKey (launch_nndr_compact merges them)

@@ -89,6 +89,15 @@ __device__ inline void top2_merge(int& b1, int& i1, int& b2, int& i2, int c1, in
 // The packed row constant ctq = ((kKeyBias - c) << 7) | (127 - row) is formed once per train row;
 // the epilogue adds acc << 8 (u8: 2 a'.b') or acc << 7 (bits) to it.  0 marks "no row".
 constexpr uint32_t kKeyBias = (1u << 24) + (1u << 22) + 1;  // s in [-2^22, 2^24 + 2^22)
+// 128-byte u8 rows (SIFT) in 256-row tiles: eight row bits.  There |b'|^2 <= 2^21 and |2 a'.b'| <= 2^22,
+// so s lies in [-2^22, 2^21 + 2^22] and X = kKeyBias8 - s in [1, 2^23 + 2^21 + 1]: 24 bits
+constexpr uint32_t kKeyBias8 = (1u << 22) + (1u << 21) + 1;
+// train rows per LDS tile of the u8 kernel at 128-byte rows: 256 (one merge, one barrier and one
+// staging round per 256 rows; FM3D_KNN_TR256=0 keeps kT)
+#ifndef FM3D_KNN_TR256
+#define FM3D_KNN_TR256 1
+#endif
+constexpr int kTR128 = FM3D_KNN_TR256 ? 256 : 128;
 
 __device__ inline uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ inline uint32_t umax(uint32_t a, uint32_t b) { return a < b ? b : a; }
@@ -96,12 +105,13 @@ __device__ inline uint32_t umax(uint32_t a, uint32_t b) { return a < b ? b : a; 
 // reads inside asm)
 __device__ inline uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) { return umax(umin(a, b), umin(umax(a, b), c)); }
 __device__ inline uint32_t pack_row(uint32_t c, int r) { return ((kKeyBias - c) << 7) | (uint32_t)(127 - (r & 127)); }
+__device__ inline uint32_t pack_row8(uint32_t c, int r) { return ((kKeyBias8 - c) << 8) | (uint32_t)(255 - (r & 255)); }
 
 // per-row constants of both sides in one launch, 16 bytes per lane (v_dot4_i32_i8 of x' = x - 128
 // with itself), lanes of a row summed by shuffles: |x'|^2 for the query rows (cq), the packed
 // ranking constant for the train rows (ctp).  Padding bytes are 128 (x' = 0).
 __global__ void rowconst_u8_kernel(const uint8_t* __restrict__ A, int nA, const uint8_t* __restrict__ B, int nB,
-                                   int dimPad, int* __restrict__ cq, int* __restrict__ ctp) {
+                                   int dimPad, int* __restrict__ cq, int* __restrict__ ctp, int rowBits) {
     const int cpr = dimPad / 16;  // 8 or 16 lanes per row (power of two)
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t / cpr, k = t - r * cpr;
@@ -119,7 +129,7 @@ __global__ void rowconst_u8_kernel(const uint8_t* __restrict__ A, int nA, const 
         if (isA)
             cq[rr] = s;
         else
-            ctp[rr] = (int)pack_row((uint32_t)s, rr);
+            ctp[rr] = (int)(rowBits == 8 ? pack_row8((uint32_t)s, rr) : pack_row((uint32_t)s, rr));
     }
 }
 
@@ -153,16 +163,20 @@ __global__ void unpack_bits_kernel(const uint32_t* __restrict__ A, int nA, const
 // popc(b) - a.b', no query constant).  QG: 32-query groups per wave (a workgroup holds kQ * QG
 // queries); each A fragment read from LDS feeds QG MFMAs, and the per-tile staging, barrier and
 // merge are shared by QG groups.
-template <int KS, bool BITS, int QG>
+template <int KS, bool BITS, int QG, int TR = kT>
 __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __restrict__ A, int nA,
                                                            const uint8_t* __restrict__ B, int nB, int dimPad,
                                                            const int* __restrict__ cqA, const int* __restrict__ ctB,
                                                            int tilesPerPart, int* __restrict__ idxOut,
                                                            int* __restrict__ keyOut) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tileBytes = kT * (KS ? 32 * KS : dimPad);
+    static_assert(TR == 128 || (TR == 256 && KS == 4 && !BITS), "256-row tiles: 128-byte u8 rows only");
+    constexpr int kRB = TR == 256 ? 8 : 7;                 // row bits of a packed key
+    constexpr uint32_t kRowMask = (1u << kRB) - 1;
+    constexpr uint32_t kBias = TR == 256 ? kKeyBias8 : kKeyBias;
+    const int tileBytes = TR * (KS ? 32 * KS : dimPad);
     unsigned char* tiles = smem;                              // 2 x tileBytes
-    uint32_t* ctl = (uint32_t*)(smem + 2 * (size_t)tileBytes);  // 2 x kT packed row constants
+    uint32_t* ctl = (uint32_t*)(smem + 2 * (size_t)tileBytes);  // 2 x TR packed row constants
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int q0 = blockIdx.x * (kQ * QG) + wave * 32 * QG;
     const int half = lane >> 5;
@@ -170,7 +184,7 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
     const int rowBytes = KS ? 32 * KS : dimPad;  // = dimPad (compile-time for KS != 0)
     const int chunksPerRow = rowBytes / 16;
     constexpr int kFlip = BITS ? 0 : (int)0x80808080;  // x ^ 0x80 == x - 128
-    constexpr int kShift = BITS ? 7 : 8;                 // acc * MUL * 128 (key bits start at bit 7)
+    constexpr int kShift = BITS ? kRB : kRB + 1;         // acc * MUL << kRB (key bits start at bit kRB)
 
     // B operand: this lane's query bytes as int8, one set per query group
     v4i bq[QG][8];  // up to dimPad = 256
@@ -194,18 +208,18 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
     }
     // train tiles of this part (blockIdx.y): [tBeg, tEnd); the parts' lists are merged by knn2_int_merge
     const int tBeg = blockIdx.y * tilesPerPart;
-    const int tEnd = min((nB + kT - 1) / kT, tBeg + tilesPerPart);
+    const int tEnd = min((nB + TR - 1) / TR, tBeg + tilesPerPart);
 
     // train tiles: the global loads of tile t + 1 are issued into registers before tile t is
     // computed and written to LDS after it, so their latency overlaps the MFMA work
-    constexpr int kPre = 8;  // 16-byte chunks per thread and tile (kT * 256 / 16 / kThreads at most)
-    const int total = kT * chunksPerRow;
+    constexpr int kPre = 8;  // 16-byte chunks per thread and tile (TR * rowBytes / 16 / kThreads at most)
+    const int total = TR * chunksPerRow;
     v4i pre[kPre];
     uint32_t preCt = 0;
     auto load_tile = [&](int t) {
         // rows past nB only in the last tile: the others load without a per-chunk test
-        const uint8_t* tb = B + (size_t)t * kT * rowBytes;
-        if ((t + 1) * kT <= nB) {
+        const uint8_t* tb = B + (size_t)t * TR * rowBytes;
+        if ((t + 1) * TR <= nB) {
 #pragma unroll
             for (int i = 0; i < kPre; i++) {
                 const int c = tid + i * kThreads;
@@ -216,12 +230,12 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
             for (int i = 0; i < kPre; i++) {
                 const int c = tid + i * kThreads;
                 v4i v = {0, 0, 0, 0};
-                if (c < total && t * kT + c / chunksPerRow < nB) v = *(const v4i*)(tb + (size_t)c * 16);
+                if (c < total && t * TR + c / chunksPerRow < nB) v = *(const v4i*)(tb + (size_t)c * 16);
                 pre[i] = v;
             }
         }
-        if (tid < kT) {
-            const int j = t * kT + tid;
+        if (tid < TR) {
+            const int j = t * TR + tid;
             preCt = (j < nB) ? (uint32_t)ctB[j] : 0u;
         }
     };
@@ -236,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
                     pre[i] ^ (v4i){kFlip, kFlip, kFlip, kFlip};
             }
         }
-        if (tid < kT) ctl[buf * kT + tid] = preCt;
+        if (tid < TR) ctl[buf * TR + tid] = preCt;
     };
     struct Acc {
         v16i a[QG];
@@ -251,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
         const int buf = (t - tBeg) & 1;
         if (t + 1 < tEnd) load_tile(t + 1);
         const unsigned char* tl = tiles + (size_t)buf * tileBytes;
-        const uint32_t* ct = ctl + buf * kT;
+        const uint32_t* ct = ctl + buf * TR;
         // packed top-2 (largest) of this tile per query group, two chains (even / odd row blocks)
         // merged after the tile
         uint32_t p1[QG][2], p2[QG][2];
@@ -279,7 +293,7 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
             // this lane's 16 train rows of the block; rows past nB exist only in the last tile,
             // tested against one per-lane limit (the row offsets stay compile-time constants)
             const int c = rb & 1;
-            const int lim = nB - t * kT - 4 * half;
+            const int lim = nB - t * TR - 4 * half;
 #pragma unroll
             for (int g = 0; g < QG; g++) {
 #pragma unroll
@@ -296,17 +310,17 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
             Acc accCur = mma(0);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int rb = 0; rb < kT / 32; rb++) {
+            for (int rb = 0; rb < TR / 32; rb++) {
                 Acc accNext;
-                if (rb + 1 < kT / 32) accNext = mma(rb + 1);
+                if (rb + 1 < TR / 32) accNext = mma(rb + 1);
                 epi(accCur, rb, fullc);
                 // one scheduling region per block: at most two accumulator sets live (without the
                 // barriers the compiler hoists all sixteen MFMAs: 194 VGPRs instead of 150)
                 __builtin_amdgcn_sched_barrier(0);
-                if (rb + 1 < kT / 32) accCur = accNext;
+                if (rb + 1 < TR / 32) accCur = accNext;
             }
         };
-        if ((t + 1) * kT <= nB)
+        if ((t + 1) * TR <= nB)
             blocks(std::true_type());
         else
             blocks(std::false_type());
@@ -317,11 +331,11 @@ __global__ __launch_bounds__(kThreads) void knn2_i8_kernel(const uint8_t* __rest
             const uint32_t m1 = umax(p1[g][0], p1[g][1]);
             const uint32_t m2 = umax(umin(p1[g][0], p1[g][1]), umax(p2[g][0], p2[g][1]));
             if (m1)
-                top2_insert((int)kKeyBias - (int)(m1 >> 7), t * kT + 127 - (int)(m1 & 127), b1[g], i1[g], b2[g],
-                            i2[g]);
+                top2_insert((int)kBias - (int)(m1 >> kRB), t * TR + (int)kRowMask - (int)(m1 & kRowMask), b1[g], i1[g],
+                            b2[g], i2[g]);
             if (m2)
-                top2_insert((int)kKeyBias - (int)(m2 >> 7), t * kT + 127 - (int)(m2 & 127), b1[g], i1[g], b2[g],
-                            i2[g]);
+                top2_insert((int)kBias - (int)(m2 >> kRB), t * TR + (int)kRowMask - (int)(m2 & kRowMask), b1[g], i1[g],
+                            b2[g], i2[g]);
         }
         if (t + 1 < tEnd) store_tile(buf ^ 1);
         __syncthreads();
@@ -1074,7 +1088,8 @@ void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int 
                         hipStream_t s) {
     const size_t threads = (size_t)(nA + nB) * (dimPad / 16);
     if (threads == 0) return;
-    rowconst_u8_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(A, nA, B, nB, dimPad, cq, ctp);
+    const int rowBits = knn2_i8_tile_rows(dimPad, 0) == 256 ? 8 : 7;
+    rowconst_u8_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(A, nA, B, nB, dimPad, cq, ctp, rowBits);
 }
 
 void launch_unpack_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, uint8_t* outA, uint8_t* outB, int* ctp,
@@ -1088,8 +1103,9 @@ void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
                     const int* ctB, int parts, int* partIdx, int* partKey, int* idx, int* key, hipStream_t s,
                     bool deferMerge) {
     if (nA <= 0) return;
-    size_t lds = 2 * (size_t)kT * dimPad + 2 * kT * sizeof(int);
-    const int nTiles = (nB + kT - 1) / kT;
+    const int TRv = knn2_i8_tile_rows(dimPad, bits);
+    size_t lds = 2 * (size_t)TRv * dimPad + 2 * TRv * sizeof(int);
+    const int nTiles = (nB + TRv - 1) / TRv;
     const int tilesPerPart = parts > 1 ? (nTiles + parts - 1) / parts : (nTiles > 0 ? nTiles : 1);
     int* oi = parts > 1 ? partIdx : idx;
     int* ok = parts > 1 ? partKey : key;
@@ -1102,7 +1118,7 @@ void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
     if (bits)
         go(knn2_i8_kernel<8, true, 1>, 1);  // 32-byte binary rows unpacked to 256 int8
     else if (dimPad == 128)
-        go(knn2_i8_kernel<4, false, kQG128>, kQG128);
+        go(knn2_i8_kernel<4, false, kQG128, kTR128>, kQG128);
     else if (dimPad == 256)
         go(knn2_i8_kernel<8, false, 1>, 1);
     else
@@ -1118,7 +1134,7 @@ size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts) {
 
 
 
-int knn2_f32_mfma_parts(int nA, int nB, int nCU) { return knn2_u8_parts(nA, nB, nCU, 0); }
+int knn2_f32_mfma_parts(int nA, int nB, int nCU) { return knn2_u8_parts(nA, nB, nCU, 0, 0); }
 
 void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, bool fused, void* work,
                           int* idx, float* key, hipStream_t s) {
@@ -1203,8 +1219,9 @@ void launch_knn2_f32_mfma_rescan(const float* A, const float* B, int nB, int dim
 }
 
 int knn2_i8_queries_per_block(int dimPad, int bits) { return (!bits && dimPad == 128 ? kQG128 : 1) * kQ; }
+int knn2_i8_tile_rows(int dimPad, int bits) { return !bits && dimPad == 128 ? kTR128 : kT; }
 
-int knn2_u8_parts(int nA, int nB, int nCU, int qPerBlock) {
+int knn2_u8_parts(int nA, int nB, int nCU, int qPerBlock, int tileRows) {
     // Fewer query blocks than CUs: split the train tiles, aiming at four blocks per CU, each part
     // keeping >= 4 tiles: at 10k x 10k (79 query blocks) 16 parts take the u8 kernel 63 -> 29 us and
     // the bits kernel 56 -> 43 us (rocprofv3, MI355X).
@@ -1219,8 +1236,9 @@ int knn2_u8_parts(int nA, int nB, int nCU, int qPerBlock) {
     const char* e = getenv("FM3D_I8_PARTS");
     const int forced = e ? atoi(e) : 0;
     const int qb = qPerBlock > 0 ? qPerBlock : kQ;
+    const int tr = tileRows > 0 ? tileRows : kT;
     const int nBlk = (nA + qb - 1) / qb;
-    const int nTiles = (nB + kT - 1) / kT;
+    const int nTiles = (nB + tr - 1) / tr;
     if (nBlk <= 0 || nCU <= 0) return 1;
     if (forced > 0) return forced < (nTiles > 1 ? nTiles : 1) ? forced : (nTiles > 1 ? nTiles : 1);
     if (nBlk >= nCU) {
