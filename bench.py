@@ -107,7 +107,7 @@ def parse():
     ap.add_argument("--dump-records", type=str, default="",
                     help="torchrun C5: rank 0 saves the last step's merged survivor records (.npy)")
     ap.add_argument("--pmc-json", type=str, default=next(
-        (p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_c4.json") for r in (4, 3, 2)) if os.path.exists(p)),
+        (p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_c4.json") for r in (5, 4, 3, 2)) if os.path.exists(p)),
         os.path.join(ROOT, "profiles", "r02_pmc_c4.json")),
                     help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()
@@ -1031,16 +1031,19 @@ def run_c3(args):
                         np.array_equal(nb, rn, equal_nan=True))
     ncc_ms = float(np.mean([x["lm_ms"] for x in stats]))
     # HBM bytes and VALU busy of ncc_kernel from the committed rocprofv3 PMC passes of this command
-    # (tools/r04_final_prof.sh -> profiles/r04_pmc_c3.json), when they are for the same workload
-    pmc = None
-    try:
-        with open(os.path.join(ROOT, "profiles", "r04_pmc_c3.json")) as f:
-            d = json.load(f)
+    # (tools/r05_final_session.sh -> profiles/r05_pmc_c3.json; round 4's file before it), when they
+    # are for the same workload
+    pmc, pmc_file = None, None
+    for name in ("r05_pmc_c3.json", "r04_pmc_c3.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
         w = d.get("workload", {})
         if (w.get("keypoints"), w.get("ray")) == (wl["keypoints"], ray):
-            pmc = d
-    except (OSError, ValueError):
-        pass
+            pmc, pmc_file = d, name
+            break
     m_dat = sum(1 for i in range(-ray, ray + 1) for j in range(-ray, ray + 1) if i * i + j * j <= ray * ray)
     pix = P * 16 * m_dat
     achieved = FLOPS_PER_PIXEL_EVAL * pix / (ncc_ms * 1e-3) / 1e12 if ncc_ms > 0 else 0.0
@@ -1064,7 +1067,7 @@ def run_c3(args):
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS,
                      "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                     "traffic_source": "profiles/r04_pmc_c3.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
+                     "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
                                        if pmc else None,
                      "valu_busy_per_simd": pmc.get("valu_busy_per_simd") if pmc else None,
                      "l2_hit": pmc.get("l2_hit") if pmc else None,
