@@ -770,6 +770,8 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
             std::memcpy(pc.R, q->R2, sizeof(pc.R));
             std::memcpy(pc.t, q->t2, sizeof(pc.t));
             pc.cam = cam;
+            pc.k2d = 2. * cam.k[2];
+            pc.k3d = 2. * cam.k[3];
             pc.slabRX = (const char*)c->slab.p;
             pc.slabRY = FM3D_RAY_AOS ? pc.slabRX + sizeof(double) : pc.slabRX + Gn * sizeof(double);
             pc.slabI1 = (const char*)c->slabI1.p;

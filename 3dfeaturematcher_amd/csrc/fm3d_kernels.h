@@ -32,6 +32,8 @@ struct ProjConst {
     // with scalar loads and address entries by one 32-bit byte offset
     const char *slabRX, *slabRY, *slabI1;
     char *slabDF, *slabDJ0, *slabDJ1;
+    // 2 k[2], 2 k[3] (exact): the tangential 2xy terms as (2k) RN(xy), the same bits as k RN(2xy)
+    double k2d, k3d;
 };
 
 // one frame pair's points in an LM launch (a launch may take the points of several: the slots

@@ -842,7 +842,9 @@ struct Geo2 {
 // host-checked): negative values and NaNs have the sign or exponent bits that put them above.
 // a2 = r2 + 2*x*x and a3 = r2 + 2*y*y are single FMAs: 2*RN(x*x) == RN(2x*x) (a power-of-two
 // scaling) wherever x*x is normal, so fma(xx, 2, r2) rounds the same exact sum; where x*x is
-// subnormal, |x|, |y| < 1e-150 and u, v round to cx, cy either way.
+// subnormal, |x|, |y| < 1e-150 and u, v round to cx, cy either way.  Likewise k*(2xy) is
+// (2k)*RN(xy) (pc->k2d, k3d): one add fewer per evaluation; where xy is subnormal the term is far
+// below an ulp of x*cdist (or u, v round to cx, cy).
 // MULTI: the launch's problems have different poses -- the pass's entry of the table (projOff,
 // one more scalar register live across the pass loops: +3-6 % cycles per evaluation pass,
 // measured); otherwise entry 0
@@ -865,12 +867,12 @@ __device__ __forceinline__ Geo2 geometry2(const LMParams& p, unsigned projOff, d
     const double r2 = xx + yy;
     const double r4 = r2 * r2;
     const double r6 = r4 * r2;
-    const double a1 = (x + x) * y;
+    const double xy = x * y;
     const double a2 = __builtin_fma(xx, 2., r2);
     const double a3 = __builtin_fma(yy, 2., r2);
     const double cdist = 1 + pc->cam.k[0] * r2 + pc->cam.k[1] * r4 + pc->cam.k[4] * r6;
-    const double xd = x * cdist + pc->cam.k[2] * a1 + pc->cam.k[3] * a2;
-    const double yd = y * cdist + pc->cam.k[2] * a3 + pc->cam.k[3] * a1;
+    const double xd = x * cdist + pc->k2d * xy + pc->cam.k[3] * a2;
+    const double yd = y * cdist + pc->cam.k[2] * a3 + pc->k3d * xy;
     const double u = xd * pc->cam.fx + pc->cam.cx;
     const double v = yd * pc->cam.fy + pc->cam.cy;
     r.good = r.inbox & __ballot((unsigned long long)__double_as_longlong(u) <= xmaxb) &

@@ -44,7 +44,8 @@ __device__ __forceinline__ double xor_sum(double v) {
 //  * camera 2 sees P at (mm q + nn t2) / nn, q = R2 r staged once per entry (q0..q2), so the
 //    normalised coordinates are (mm q0 + nn t0) / (mm q2 + nn t2) and (mm q1 + nn t1) / (the same):
 //    one reciprocal (recip_z_lo, one guard), no quotient mm / nn;
-//  * r2 + 2x^2 as fma(x*x, 2, r2) (2*RN(x*x) == RN(2x*x)); project1's NaN for an infinite r6
+//  * r2 + 2x^2 as fma(x*x, 2, r2) (2*RN(x*x) == RN(2x*x)) and k 2xy as (2k) RN(xy) (k2d, k3d; the
+//    LM kernel's geometry2 states why the bits agree); project1's NaN for an infinite r6
 //    dropped (such a u or v is infinite or NaN: not good);
 //  * 0 <= u <= xmax as bits(u) <= bits(xmax): u is never -0.0 (the host hands the kernel a
 //    principal point of +0.0 for -0.0, fm3d_host.cpp lm_camera), negatives and NaNs lie above.
@@ -67,8 +68,8 @@ struct NccGeo {
 // so the sign test costs one multiply
 __device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, double uy, double q0, double q1,
                                                  double q2, double n0, double n1, double n2, double mm, double amm,
-                                                 double sgn, double cm, unsigned long long xmaxb,
-                                                 unsigned long long ymaxb) {
+                                                 double sgn, double cm, double k2d, double k3d,
+                                                 unsigned long long xmaxb, unsigned long long ymaxb) {
     NccGeo g;
     const double nn = n0 * ux + n1 * uy + n2 * 1.;
     const double lim = cm * (sgn * nn);
@@ -82,12 +83,12 @@ __device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, 
     const double r2 = xx + yy;
     const double r4 = r2 * r2;
     const double r6 = r4 * r2;
-    const double a1 = (x + x) * y;
+    const double xy = x * y;
     const double a2 = __builtin_fma(xx, 2., r2);
     const double a3 = __builtin_fma(yy, 2., r2);
     const double cdist = 1 + p.cam.k[0] * r2 + p.cam.k[1] * r4 + p.cam.k[4] * r6;
-    const double xd = x * cdist + p.cam.k[2] * a1 + p.cam.k[3] * a2;
-    const double yd = y * cdist + p.cam.k[2] * a3 + p.cam.k[3] * a1;
+    const double xd = x * cdist + k2d * xy + p.cam.k[3] * a2;
+    const double yd = y * cdist + p.cam.k[2] * a3 + k3d * xy;
     const double u = xd * p.cam.fx + p.cam.cx;
     const double v = yd * p.cam.fy + p.cam.cy;
     g.good = inbox & __ballot((unsigned long long)__double_as_longlong(u) <= xmaxb) &
@@ -159,6 +160,7 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
     }
     int m = 0;
     const double cm = (double)p.cmax;
+    const double k2d = 2. * p.cam.k[2], k3d = 2. * p.cam.k[3];
     const double xmax = (double)p.w, ymax = (double)p.h;  // isPixelGood at scale 1
     const unsigned long long xmaxb = (unsigned long long)__double_as_longlong(xmax);
     const unsigned long long ymaxb = (unsigned long long)__double_as_longlong(ymax);
@@ -226,8 +228,8 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
             for (int k = 0; k < KPW; k++) {
                 if (k >= nk) break;
                 if ((dead >> k) & 1) continue;  // wave-uniform
-                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], amm[k], sgn[k], cm,
-                                                  xmaxb, ymaxb);
+                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], amm[k], sgn[k], cm, k2d,
+                                                  k3d, xmaxb, ymaxb);
                 if (okm & ~g.good) badNow |= 1u << k;  // scalar
                 const float bf = ncc_bilinear_f(p.img2, g.off, p.w, g.fx, g.fy);
                 const double b = (double)__uint_as_float(ncc_sel_u32(__float_as_uint(bf), okm));
