@@ -622,7 +622,8 @@ def test_knn2_u8_train_parts_ties(fm3d, orc, ctx):
     rng = np.random.default_rng(21)
     nB = 9001
     B = rng.integers(0, 256, (nB, 128), dtype=np.uint8)
-    # 402 queries leave CUs idle: 4 parts of 18 tiles (2,304 rows) -- part 1 starts at row 2304
+    # 402 queries leave CUs idle, so the train tiles split into parts; row 2304 starts a tile at either
+    # tile size (18 x 128 = 9 x 256) and started part 1 with round 4's 128-row tiles
     B[5000:5100] = B[10:110]        # duplicates in a later part
     B[nB - 1] = B[3]                # and in the last, partial tile
     B[2304] = B[3]                  # and on the first row of part 1
@@ -633,6 +634,31 @@ def test_knn2_u8_train_parts_ties(fm3d, orc, ctx):
     assert np.array_equal(got["distance"], dist)
     assert (idx[:100, 0] == np.arange(10, 110)).all() and (idx[:100, 1] == np.arange(5000, 5100)).all()
     assert idx[100, 0] == 3 and idx[100, 1] == 2304
+
+
+@pytest.mark.parametrize("nA", [402, 3000])
+def test_knn2_u8_256_row_tiles_ties(fm3d, orc, ctx, nA):
+    """Round 5: 128-byte u8 rows run in 256-row train tiles with an 8-bit row index in the packed key
+    (knn2_i8_kernel<4, false, 2, 256>, 256 queries per workgroup).  Exact duplicates of one row in the
+    tile's upper half (row index > 127: the eighth bit), on the first row of the next tile, on the
+    first row of a part (402 queries: 9 parts of 4 tiles, part 1 from row 1024), in the last partial
+    tile, and distances at the 24-bit key's extremes (all-0 and all-255 rows) must resolve exactly as
+    the scan does: the lowest trainIdx first, for both neighbours."""
+    rng = np.random.default_rng(31 + nA)
+    nB = 9001
+    B = rng.integers(0, 256, (nB, 128), dtype=np.uint8)
+    for r in (200, 256, 1024, nB - 1):
+        B[r] = B[3]
+    B[700] = 0
+    B[701] = 255
+    A = np.concatenate([B[[3, 3, 200, 700, 701]], np.zeros((1, 128), np.uint8), np.full((1, 128), 255, np.uint8),
+                        rng.integers(0, 256, (nA - 7, 128), dtype=np.uint8)])
+    got = fm3d.DescriptorsMatcher(ctx).knn_match(A, B)
+    idx, dist = orc.knn2(A, B, orc.U8, oracle_threads())
+    assert np.array_equal(got["trainIdx"], idx)
+    assert np.array_equal(got["distance"], dist)
+    assert tuple(idx[0]) == (3, 200) and tuple(idx[2]) == (3, 200)
+    assert idx[5, 0] == 700 and idx[6, 0] == 701
 
 
 @pytest.mark.parametrize("mfma", ["1", "0"])
