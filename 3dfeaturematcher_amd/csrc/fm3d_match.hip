@@ -1134,6 +1134,10 @@ size_t knn2_f32_mfma_bytes(int nA, int nB, int dim, int parts) {
 
 
 
+// the bf16 prefilter kernel: parts only for query sets that leave CUs idle.  The int8 kernel's part
+// model for large sets (the last partial round of blocks) made the fused pass slower here (100k x
+// 100k SURF-128: 11.3 / 12.0 -> 17.7 / 17.8 ms, tools/r05_f32_parts_ab.sh): a part's running bound
+// starts loose again, so more rows enter the candidate lists
 int knn2_f32_mfma_parts(int nA, int nB, int nCU) { return knn2_u8_parts(nA, nB, nCU, 0, 0); }
 
 void launch_knn2_f32_mfma(const float* A, int nA, const float* B, int nB, int dim, int parts, bool fused, void* work,
