@@ -47,6 +47,9 @@ __device__ __forceinline__ double xor_sum(double v) {
 //  * r2 + 2x^2 as fma(x*x, 2, r2) (2*RN(x*x) == RN(2x*x)) and k 2xy as (2k) RN(xy) (k2d, k3d; the
 //    LM kernel's geometry2 states why the bits agree); project1's NaN for an infinite r6
 //    dropped (such a u or v is infinite or NaN: not good);
+//  * every product-and-sum after the undistortion fused (round 5): nn, the camera-2 coordinates, the
+//    distortion polynomial, xd / yd and the pixel coordinates (orc_ncc_project states the same
+//    fused operations on the host, C99 fma);
 //  * 0 <= u <= xmax as bits(u) <= bits(xmax): u is never -0.0 (the host hands the kernel a
 //    principal point of +0.0 for -0.0, fm3d_host.cpp lm_camera), negatives and NaNs lie above.
 typedef unsigned long long LaneMask;
@@ -63,22 +66,31 @@ struct NccGeo {
     unsigned off;
     LaneMask good;
 };
-// sgn: the sign of mm as +1 / -1, 0 for mm = 0 or NaN (hypothesis-uniform); amm = |mm|.  The limit
-// cm (sgn nn) equals cm |nn| where mm and nn share a sign and is <= 0 (every test fails) elsewhere,
-// so the sign test costs one multiply
-__device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, double uy, double q0, double q1,
-                                                 double q2, double n0, double n1, double n2, double mm, double amm,
-                                                 double sgn, double cm, double k2d, double k3d,
-                                                 unsigned long long xmaxb, unsigned long long ymaxb) {
+// csg = cm sgn, sgn the sign of mm as +1 / -1, 0 for mm = 0 or NaN (hypothesis-uniform); amm = |mm|.
+// The limit csg nn equals cm |nn| where mm and nn share a sign and is <= 0 or NaN (every test fails)
+// elsewhere, so the sign test costs one multiply
+// the part up to camera 2's homogeneous coordinates (X, Y, Z) = mm q + nn t2 and the box mask
+struct NccPre {
+    double nn, X, Y, Z;
+    LaneMask inbox;
+};
+__device__ __forceinline__ NccPre ncc_geo_pre(const NccParams& p, double ux, double uy, double q0, double q1, double q2,
+                                              double n0, double n1, double n2, double mm, double amm, double csg) {
+    NccPre r;
+    r.nn = __builtin_fma(n1, uy, __builtin_fma(n0, ux, n2));
+    const double lim = csg * r.nn;
+    r.inbox = __ballot(fabs(mm * ux) < lim) & __ballot(fabs(mm * uy) < lim) & __ballot(amm < lim);
+    r.X = __builtin_fma(r.nn, p.t2[0], mm * q0);
+    r.Y = __builtin_fma(r.nn, p.t2[1], mm * q1);
+    r.Z = __builtin_fma(r.nn, p.t2[2], mm * q2);
+    return r;
+}
+// the rest, given z = Z ? 1 / Z : 1
+__device__ __forceinline__ NccGeo ncc_geo_post(const NccParams& p, const NccPre& pr, double z, double k2d, double k3d,
+                                               unsigned long long xmaxb, unsigned long long ymaxb) {
     NccGeo g;
-    const double nn = n0 * ux + n1 * uy + n2 * 1.;
-    const double lim = cm * (sgn * nn);
-    const LaneMask inbox = __ballot(fabs(mm * ux) < lim) & __ballot(fabs(mm * uy) < lim) & __ballot(amm < lim);
-    double x = mm * q0 + nn * p.t2[0];
-    double y = mm * q1 + nn * p.t2[1];
-    const double z = recip_z_lo(mm * q2 + nn * p.t2[2]);
-    x *= z;
-    y *= z;
+    const LaneMask inbox = pr.inbox;
+    const double x = pr.X * z, y = pr.Y * z;
     const double xx = x * x, yy = y * y;
     const double r2 = xx + yy;
     const double r4 = r2 * r2;
@@ -86,27 +98,38 @@ __device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, 
     const double xy = x * y;
     const double a2 = __builtin_fma(xx, 2., r2);
     const double a3 = __builtin_fma(yy, 2., r2);
-    const double cdist = 1 + p.cam.k[0] * r2 + p.cam.k[1] * r4 + p.cam.k[4] * r6;
-    const double xd = x * cdist + k2d * xy + p.cam.k[3] * a2;
-    const double yd = y * cdist + p.cam.k[2] * a3 + k3d * xy;
-    const double u = xd * p.cam.fx + p.cam.cx;
-    const double v = yd * p.cam.fy + p.cam.cy;
+    const double cdist =
+        __builtin_fma(p.cam.k[4], r6, __builtin_fma(p.cam.k[1], r4, __builtin_fma(p.cam.k[0], r2, 1.)));
+    const double xd = __builtin_fma(p.cam.k[3], a2, __builtin_fma(k2d, xy, x * cdist));
+    const double yd = __builtin_fma(k3d, xy, __builtin_fma(p.cam.k[2], a3, y * cdist));
+    const double u = __builtin_fma(xd, p.cam.fx, p.cam.cx);
+    const double v = __builtin_fma(yd, p.cam.fy, p.cam.cy);
     g.good = inbox & __ballot((unsigned long long)__double_as_longlong(u) <= xmaxb) &
              __ballot((unsigned long long)__double_as_longlong(v) <= ymaxb);
     g.fx = (float)u;
     g.fy = (float)v;
-    const unsigned o = __umul24((unsigned)(int)floorf(g.fy), (unsigned)p.w) + (unsigned)(int)floorf(g.fx);
+    // truncation is floor on the good lanes (0 <= u, v); the others' offsets are zeroed
+    const unsigned o = __umul24((unsigned)(int)g.fy, (unsigned)p.w) + (unsigned)(int)g.fx;
     g.off = ncc_sel_u32(o, g.good);
     return g;
 }
+__device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, double uy, double q0, double q1,
+                                                 double q2, double n0, double n1, double n2, double mm, double amm,
+                                                 double csg, double k2d, double k3d,
+                                                 unsigned long long xmaxb, unsigned long long ymaxb) {
+    const NccPre pr = ncc_geo_pre(p, ux, uy, q0, q1, q2, n0, n1, n2, mm, amm, csg);
+    return ncc_geo_post(p, pr, recip_z_lo(pr.Z), k2d, k3d, xmaxb, ymaxb);
+}
 // getBilinearInterpPix32f (tools.cpp:129-142) on the gathered window, with the fractions
 // x - floor(x), y - floor(y), as two-lane float vectors (v_pk_mul_f32 / v_pk_add_f32: each component
-// rounded as the scalar operation; fm3d_lm2.hip bilinear_f)
+// rounded as the scalar operation; fm3d_lm2.hip bilinear_f).  The fractions as v_fract_f32: for a
+// good sample (x, y >= 0) x - floor(x) is exact and below 1, so fract's clamp never applies; the
+// other lanes' samples are discarded (not in image 1) or their hypothesis is dead
 typedef float ncc_f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float ncc_bilinear_f(const uint8_t* img, unsigned off, int w, float x, float y) {
-    typedef __attribute__((aligned(1))) const uint16_t u16u;
-    const unsigned lo = *(u16u*)(img + off), hi = *(u16u*)(img + off + w);
-    const float xf = x - floorf(x), yf = y - floorf(y);
+typedef __attribute__((aligned(1))) const uint16_t ncc_u16u;
+// the window's rows lo = (b00, b01), hi = (b10, b11) as loaded
+__device__ __forceinline__ float ncc_bilinear_w(unsigned lo, unsigned hi, float x, float y) {
+    const float xf = __builtin_amdgcn_fractf(x), yf = __builtin_amdgcn_fractf(y);
     const ncc_f32x2 b0 = {(float)(lo & 0xff), (float)(lo >> 8)};  // b00, b01
     const ncc_f32x2 b1 = {(float)(hi & 0xff), (float)(hi >> 8)};  // b10, b11
     const float ym0 = 1.0f - yf, ym1 = yf;
@@ -114,6 +137,10 @@ __device__ __forceinline__ float ncc_bilinear_f(const uint8_t* img, unsigned off
     const ncc_f32x2 xm = {1.0f - xf, xf};
     const ncc_f32x2 q = xm * sc;
     return q.x + q.y;
+}
+__device__ __forceinline__ float ncc_bilinear_f(const uint8_t* img, unsigned off, int w, float x, float y) {
+    // both rows by a 32-bit offset from the image base (the window lies inside the image)
+    return ncc_bilinear_w(*(ncc_u16u*)(img + off), *(ncc_u16u*)(img + (off + (unsigned)w)), x, y);
 }
 
 // KPW: hypotheses per wave the register arrays hold (H <= 4 * KPW); sized to H so that 16 hypotheses
@@ -164,14 +191,16 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
     const double xmax = (double)p.w, ymax = (double)p.h;  // isPixelGood at scale 1
     const unsigned long long xmaxb = (unsigned long long)__double_as_longlong(xmax);
     const unsigned long long ymaxb = (unsigned long long)__double_as_longlong(ymax);
-    double sgn[KPW], amm[KPW];
+    double csg[KPW], amm[KPW];
     for (int k = 0; k < KPW; k++) {
-        sgn[k] = mm[k] > 0. ? 1. : mm[k] < 0. ? -1. : 0.;
+        csg[k] = mm[k] > 0. ? cm : mm[k] < 0. ? -cm : 0.;
         amm[k] = fabs(mm[k]);
     }
     // hypotheses of this wave that already failed on some entry (wave-uniform): they score -2
-    // whatever their sums, so their geometry is not computed again
-    unsigned dead = 0;
+    // whatever their sums, so their geometry is not computed again.  Per hypothesis the lanes that
+    // failed it so far (a ballot OR, SGPRs): tests and updates stay scalar
+    LaneMask dead[KPW];
+    for (int k = 0; k < KPW; k++) dead[k] = 0;
     // the hypothesis-independent part of a pixel (its undistorted ray and image-1 sample) once per
     // workgroup, kNccChunk entries at a time in LDS; lane l of every wave then takes the entries l,
     // l + 64, l + 128, ... of each chunk -- the same entries in the same order as a lane-strided scan
@@ -209,7 +238,8 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
             OK[sl] = in;
         }
         __syncthreads();
-        if (anyBad1S) dead = ~0u;  // an image-1 pixel fails: every hypothesis scores -2
+        if (anyBad1S)  // an image-1 pixel fails: every hypothesis scores -2
+            for (int k = 0; k < KPW; k++) dead[k] = ~0ull;
         for (int j = 0; j < kNccChunk / 64; j++) {
             const int t = lane + 64 * j;
             if (base + 64 * j >= p.nOffPad) break;  // wave-uniform
@@ -222,26 +252,24 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
             const double ux = Rx[t], uy = Ry[t], q0 = Q0[t], q1 = Q1[t], q2 = Q2[t];
             const double a = (double)A1[t];
             Sa += a;
-            Saa += a * a;
-            unsigned badNow = 0;
+            Saa = __builtin_fma(a, a, Saa);  // a*a and a*b are exact (float samples): fusing keeps the bits
 #pragma unroll
             for (int k = 0; k < KPW; k++) {
                 if (k >= nk) break;
-                if ((dead >> k) & 1) continue;  // wave-uniform
-                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], amm[k], sgn[k], cm, k2d,
-                                                  k3d, xmaxb, ymaxb);
-                if (okm & ~g.good) badNow |= 1u << k;  // scalar
+                if (dead[k]) continue;  // wave-uniform
+                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], amm[k], csg[k], k2d, k3d,
+                                                  xmaxb, ymaxb);
+                dead[k] |= okm & ~g.good;
                 const float bf = ncc_bilinear_f(p.img2, g.off, p.w, g.fx, g.fy);
                 const double b = (double)__uint_as_float(ncc_sel_u32(__float_as_uint(bf), okm));
                 Sb[k] += b;
-                Sbb[k] += b * b;
-                Sab[k] += a * b;
+                Sbb[k] = __builtin_fma(b, b, Sbb[k]);
+                Sab[k] = __builtin_fma(a, b, Sab[k]);
             }
-            dead |= badNow;
         }
         __syncthreads();
     }
-    for (int k = 0; k < KPW; k++) bad[k] = (dead >> k) & 1;
+    for (int k = 0; k < KPW; k++) bad[k] = dead[k] != 0;
     for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o);
     const bool anyBad1 = anyBad1S != 0;
     __shared__ double score[32];

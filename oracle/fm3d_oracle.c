@@ -117,6 +117,29 @@ static void orc_project_xyz(const orc_camera *c, double x, double y, double z, d
     *v = yd * c->fy + c->cy;
 }
 
+/* the NCC kernel's camera-2 projection (csrc/fm3d_ncc.hip ncc_geometry_m): orc_project_xyz with every
+   product-and-sum fused (C99 fma, one rounding, as the GPU's fma) -- the NCC hypotheses are an
+   extension with no reference order to keep -- and 2 k xy as (2 k) RN(xy), the same bits as k RN(2 x y) */
+static void orc_ncc_project(const orc_camera *c, double x, double y, double z, double *u, double *v)
+{
+    const double *k = c->k;
+    double r2, r4, r6, xy, a2, a3, cdist, xd, yd;
+    z = z ? 1. / z : 1;
+    x *= z;
+    y *= z;
+    r2 = x * x + y * y;
+    r4 = r2 * r2;
+    r6 = r4 * r2;
+    xy = x * y;
+    a2 = fma(x * x, 2., r2);
+    a3 = fma(y * y, 2., r2);
+    cdist = fma(k[4], r6, fma(k[1], r4, fma(k[0], r2, 1.)));
+    xd = fma(k[3], a2, fma(2. * k[2], xy, x * cdist));
+    yd = fma(2. * k[3], xy, fma(k[2], a3, y * cdist));
+    *u = fma(xd, c->fx, c->cx);
+    *v = fma(yd, c->fy, c->cy);
+}
+
 static void orc_project1(const orc_camera *c, const double R[9], const double t[3],
                          double X, double Y, double Z, double *u, double *v)
 {
@@ -1436,7 +1459,8 @@ ORC_API int orc_optimize_normals(const orc_camera *cam, const double R2[9], cons
    I1 (image 1 at the pixel) and I2 (image 2 through the plane); score = NCC or -2 (a failing
    pixel, a flat patch).  Round 5: the plane point P = (mm / nn) r of the ray r = (ux, uy, 1) is
    tested against the bounding box and projected without the quotient (camera 2 sees it at
-   (mm R2 r + nn t2) / nn, so x = (mm q0 + nn t0) / (mm q2 + nn t2), q = R2 r).  The five sums are accumulated per lane l = offset index mod 64 in offset
+   (mm R2 r + nn t2) / nn, so x = (mm q0 + nn t0) / (mm q2 + nn t2), q = R2 r), and every
+   product-and-sum from nn to the pixel coordinates is one fma (orc_ncc_project).  The five sums are accumulated per lane l = offset index mod 64 in offset
    order and combined by the xor tree over 64 lanes -- the GPU's order, so the scores are bit-equal.
    scores: P x H, normals: P x 3 (best, lowest h on ties; X/|X| if none), best: P (-1 if none). */
 ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const double t2[3], const uint8_t *img1,
@@ -1482,7 +1506,7 @@ ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const
                     if (!orc_pixel_good(px, py, 1.0, w, h)) { fail = 1; continue; }
                     a = (double)orc_bilinear(img1, w, h, (float)px, (float)py);
                     orc_undistort1(cam, px, py, &ux, &uy);
-                    nn = n[0] * ux + n[1] * uy + n[2] * 1.;
+                    nn = fma(n[1], uy, fma(n[0], ux, n[2]));
                     /* the plane point P = (mm / nn) r without the division: |P0|, |P1| < cm and
                        0 < P2 < cm as |mm ux|, |mm uy|, |mm| < cm |nn| with mm, nn of one sign */
                     lim = cm * fabs(nn);
@@ -1493,7 +1517,8 @@ ORC_API void orc_ncc_hypotheses(const orc_camera *cam, const double R2[9], const
                     q0 = R2[0] * ux + R2[1] * uy + R2[2];
                     q1 = R2[3] * ux + R2[4] * uy + R2[5];
                     q2 = R2[6] * ux + R2[7] * uy + R2[8];
-                    orc_project_xyz(cam, mm * q0 + nn * t2[0], mm * q1 + nn * t2[1], mm * q2 + nn * t2[2], &u, &v);
+                    orc_ncc_project(cam, fma(nn, t2[0], mm * q0), fma(nn, t2[1], mm * q1), fma(nn, t2[2], mm * q2),
+                                    &u, &v);
                     if (!orc_pixel_good(u, v, 1.0, w, h)) { fail = 1; continue; }
                     b = (double)orc_bilinear(img2, w, h, (float)u, (float)v);
                     S[0][l] += a; S[1][l] += b; S[2][l] += a * a; S[3][l] += b * b; S[4][l] += a * b;
