@@ -29,6 +29,11 @@ namespace {
 constexpr int kNccMaxPerWave = 8;  // hypotheses per wave (H <= 32)
 constexpr int kNccChunk = 512;     // neighbourhood entries staged in LDS at a time
 
+__device__ __forceinline__ double ncc_uniform(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 __device__ __forceinline__ double xor_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
@@ -144,11 +149,12 @@ __device__ __forceinline__ float ncc_bilinear_f(const uint8_t* img, unsigned off
 }
 
 // KPW: hypotheses per wave the register arrays hold (H <= 4 * KPW); sized to H so that 16 hypotheses
-// keep 4 per wave in registers (225 VGPRs at 8, 2 waves per SIMD)
+// keep 4 per wave in registers
 // NW: waves per point (hypothesis h runs on wave h % NW).  Round 5 A/B at C3 (H = 16, one pair at a
-// time, tools/ncc_ab.sh): NW = 4, KPW = 4 1.497 ms; the plane constants made scalar (readfirstlane)
-// 1.498 ms; NW = 8, KPW = 2 (4 waves per SIMD instead of 3) 1.548 / 1.554 ms -- the kernel is VALU
-// issue bound, occupancy does not move it
+// time, tools/ncc_ab.sh), before the fused arithmetic: NW = 4, KPW = 4 1.497 ms; the plane constants
+// made scalar (readfirstlane) 1.498 ms; NW = 8, KPW = 2 (4 waves per SIMD instead of 3) 1.548 /
+// 1.554 ms.  With the fused arithmetic the scalar constants bring the kernel under 128 VGPRs, and
+// four waves per SIMD then pay (below)
 template <int KPW, bool FULL, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
     const int pt = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -195,6 +201,17 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
     for (int k = 0; k < KPW; k++) {
         csg[k] = mm[k] > 0. ? cm : mm[k] < 0. ? -cm : 0.;
         amm[k] = fabs(mm[k]);
+    }
+    // the plane constants are wave-uniform: scalar registers (round 5, with the fused arithmetic:
+    // 153 -> 113 VGPRs at H = 16, four waves per SIMD instead of three; same box 1.38 -> 1.33 ms
+    // at C3, and at H = 32 217 -> 138 VGPRs, 20.4 -> 18.4 ms over 20k points)
+    for (int k = 0; k < KPW; k++) {
+        n0[k] = ncc_uniform(n0[k]);
+        n1[k] = ncc_uniform(n1[k]);
+        n2[k] = ncc_uniform(n2[k]);
+        mm[k] = ncc_uniform(mm[k]);
+        csg[k] = ncc_uniform(csg[k]);
+        amm[k] = ncc_uniform(amm[k]);
     }
     // hypotheses of this wave that already failed on some entry (wave-uniform): they score -2
     // whatever their sums, so their geometry is not computed again.  Per hypothesis the lanes that
