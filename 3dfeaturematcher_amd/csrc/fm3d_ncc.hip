@@ -71,7 +71,7 @@ struct NccGeo {
     unsigned off;
     LaneMask good;
 };
-// csg = cm sgn, sgn the sign of mm as +1 / -1, 0 for mm = 0 or NaN (hypothesis-uniform); amm = |mm|.
+// csg = cm sgn, sgn the sign of mm as +1 / -1, 0 for mm = 0 or NaN (hypothesis-uniform).
 // The limit csg nn equals cm |nn| where mm and nn share a sign and is <= 0 or NaN (every test fails)
 // elsewhere, so the sign test costs one multiply
 // the part up to camera 2's homogeneous coordinates (X, Y, Z) = mm q + nn t2 and the box mask
@@ -80,11 +80,11 @@ struct NccPre {
     LaneMask inbox;
 };
 __device__ __forceinline__ NccPre ncc_geo_pre(const NccParams& p, double ux, double uy, double q0, double q1, double q2,
-                                              double n0, double n1, double n2, double mm, double amm, double csg) {
+                                              double n0, double n1, double n2, double mm, double csg) {
     NccPre r;
     r.nn = __builtin_fma(n1, uy, __builtin_fma(n0, ux, n2));
     const double lim = csg * r.nn;
-    r.inbox = __ballot(fabs(mm * ux) < lim) & __ballot(fabs(mm * uy) < lim) & __ballot(amm < lim);
+    r.inbox = __ballot(fabs(mm * ux) < lim) & __ballot(fabs(mm * uy) < lim) & __ballot(fabs(mm) < lim);
     r.X = __builtin_fma(r.nn, p.t2[0], mm * q0);
     r.Y = __builtin_fma(r.nn, p.t2[1], mm * q1);
     r.Z = __builtin_fma(r.nn, p.t2[2], mm * q2);
@@ -119,10 +119,10 @@ __device__ __forceinline__ NccGeo ncc_geo_post(const NccParams& p, const NccPre&
     return g;
 }
 __device__ __forceinline__ NccGeo ncc_geometry_m(const NccParams& p, double ux, double uy, double q0, double q1,
-                                                 double q2, double n0, double n1, double n2, double mm, double amm,
+                                                 double q2, double n0, double n1, double n2, double mm,
                                                  double csg, double k2d, double k3d,
                                                  unsigned long long xmaxb, unsigned long long ymaxb) {
-    const NccPre pr = ncc_geo_pre(p, ux, uy, q0, q1, q2, n0, n1, n2, mm, amm, csg);
+    const NccPre pr = ncc_geo_pre(p, ux, uy, q0, q1, q2, n0, n1, n2, mm, csg);
     return ncc_geo_post(p, pr, recip_z_lo(pr.Z), k2d, k3d, xmaxb, ymaxb);
 }
 // getBilinearInterpPix32f (tools.cpp:129-142) on the gathered window, with the fractions
@@ -197,10 +197,9 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
     const double xmax = (double)p.w, ymax = (double)p.h;  // isPixelGood at scale 1
     const unsigned long long xmaxb = (unsigned long long)__double_as_longlong(xmax);
     const unsigned long long ymaxb = (unsigned long long)__double_as_longlong(ymax);
-    double csg[KPW], amm[KPW];
+    double csg[KPW];
     for (int k = 0; k < KPW; k++) {
         csg[k] = mm[k] > 0. ? cm : mm[k] < 0. ? -cm : 0.;
-        amm[k] = fabs(mm[k]);
     }
     // the plane constants are wave-uniform: scalar registers (round 5, with the fused arithmetic:
     // 153 -> 113 VGPRs at H = 16, four waves per SIMD instead of three; same box 1.38 -> 1.33 ms
@@ -211,7 +210,6 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
         n2[k] = ncc_uniform(n2[k]);
         mm[k] = ncc_uniform(mm[k]);
         csg[k] = ncc_uniform(csg[k]);
-        amm[k] = ncc_uniform(amm[k]);
     }
     // hypotheses of this wave that already failed on some entry (wave-uniform): they score -2
     // whatever their sums, so their geometry is not computed again.  Per hypothesis the lanes that
@@ -274,7 +272,7 @@ __global__ __launch_bounds__(64 * NW) void ncc_kernel(NccParams p) {
             for (int k = 0; k < KPW; k++) {
                 if (k >= nk) break;
                 if (dead[k]) continue;  // wave-uniform
-                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], amm[k], csg[k], k2d, k3d,
+                const NccGeo g = ncc_geometry_m(p, ux, uy, q0, q1, q2, n0[k], n1[k], n2[k], mm[k], csg[k], k2d, k3d,
                                                   xmaxb, ymaxb);
                 dead[k] |= okm & ~g.good;
                 const float bf = ncc_bilinear_f(p.img2, g.off, p.w, g.fx, g.fy);
