@@ -84,6 +84,7 @@ class Settings(ctypes.Structure):
         ("mserMaxEvolution", ctypes.c_int), ("mserAreaThreshold", ctypes.c_double),
         ("mserMinMargin", ctypes.c_double), ("mserEdgeBlurSize", ctypes.c_int),
         ("lmReduction", ctypes.c_int),
+        ("dltSolver", ctypes.c_int),
     ]
 
     @staticmethod
@@ -866,17 +867,23 @@ class Pipeline:
         self.n_queries = 0
 
     def upload(self, desc_a, desc_b, kp1, kp2, img1, img2, binary=False, query_offset=0):
+        """fm3d_pipeline_upload; img1 = img2 = None stages no images (C2's match + DLT)"""
         a = np.ascontiguousarray(desc_a)
         b = np.ascontiguousarray(desc_b)
         k1 = np.ascontiguousarray(kp1, dtype=np.float32)
         k2 = np.ascontiguousarray(kp2, dtype=np.float32)
-        i1 = np.ascontiguousarray(img1, dtype=np.uint8)
-        i2 = np.ascontiguousarray(img2, dtype=np.uint8)
-        h, w = i1.shape
+        if img1 is None and img2 is None:
+            i1 = i2 = None
+            h = w = 0
+        else:
+            i1 = np.ascontiguousarray(img1, dtype=np.uint8)
+            i2 = np.ascontiguousarray(img2, dtype=np.uint8)
+            h, w = i1.shape
         self.n_queries = a.shape[0]
         self.ctx.check(lib().fm3d_pipeline_upload(self.ctx.handle, _vp(a), a.shape[0], _vp(b), b.shape[0],
                                                   a.shape[1], _desc_type(a, binary), _vp(k1), _vp(k2),
-                                                  _ptr(i1, ctypes.c_uint8), _ptr(i2, ctypes.c_uint8), w, h,
+                                                  None if i1 is None else _ptr(i1, ctypes.c_uint8),
+                                                  None if i2 is None else _ptr(i2, ctypes.c_uint8), w, h,
                                                   query_offset))
 
     def run(self, records_dev_ptr: int | None = None):

@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "fm3d_detmath.h"
+#include "fm3d_cvsvd.h"
 
 namespace fm3d {
 

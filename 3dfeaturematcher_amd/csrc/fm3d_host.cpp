@@ -107,7 +107,8 @@ struct fm3d_ctx {
     // work buffers
     DevBuf A, B, cqA, ctB, idx, key, fkey, knnOut, cand, flag, matches, count, scanTmp;
     DevBuf partIdx, partKey;  // per-part top-2 lists of the split matchers
-    DevBuf A8, B8;            // binary rows unpacked to int8 for the MFMA matcher
+    DevBuf A8, B8;            // binary rows unpacked to int8 for the MFMA matcher; u8 rows packed from floats
+    DevBuf u8Flag;            // launch_f32_pack_u8's "not integer-valued" flag
     // SURF detection / description
     DevBuf sfImg, sfSum, sfDet, sfTr, sfLayers, sfMids, sfCand, sfCount, sfSortTmp, sfFlag, sfPos, sfKp, sfKin, sfSrc,
         sfDesc, sfDW, sfAng;
@@ -138,12 +139,12 @@ struct fm3d_ctx {
     DevBuf lmNormals, lmStatus, lmInfo, lmNfev, lmMdat, lmQueue, lmStat, slab, slabI1;
     // the fused compactions' look-back state (fm3d_kernels.h LookBack): status words, block counter
     DevBuf lbSt, lbCtr;
-    unsigned lbBase = 0, lbEpoch = 0;
+    unsigned lbEpoch = 0;  // the last look-back launch's tag (fm3d_kernels.h LookBack)
     DevBuf records, recTmp, recFlag;
     DevBuf lmProj;  // camera-2 projection constants for the LM kernel (fm3d::ProjConst)
     DevBuf pcnt;    // the pipeline's device counts: [0] matches K, [1] inliers P, [2] kept
     // pinned staging: descriptors A / B (padded rows), keypoints, images, small tables, results
-    HostBuf hA, hB, hK1, hK2, hImg, hTab, hProj, hSmall;
+    HostBuf hA, hB, hK1, hK2, hImg, hTab, hProj, hSmall, hFlag;
     hipEvent_t evStage = nullptr;  // after the last H2D copy from the staging buffers
     hipEvent_t evProj = nullptr;   // after the last H2D copy of the LM constants (hProj)
     bool pending = false;          // a fm3d_pipeline_submit awaiting fm3d_pipeline_wait
@@ -203,37 +204,11 @@ void rodrigues_v2m(const double r[3], double R[9]) {
     for (int k = 0; k < 9; k++) R[k] = c * I[k] + c1 * rrt[k] + s * rxm[k];
 }
 
-void inv_t3(const double A[9], double out[9]) {
-    double c00 = A[4] * A[8] - A[5] * A[7];
-    double c01 = A[5] * A[6] - A[3] * A[8];
-    double c02 = A[3] * A[7] - A[4] * A[6];
-    double c10 = A[2] * A[7] - A[1] * A[8];
-    double c11 = A[0] * A[8] - A[2] * A[6];
-    double c12 = A[1] * A[6] - A[0] * A[7];
-    double c20 = A[1] * A[5] - A[2] * A[4];
-    double c21 = A[2] * A[3] - A[0] * A[5];
-    double c22 = A[0] * A[4] - A[1] * A[3];
-    double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
-    double id = 1. / det;
-    out[0] = c00 * id;
-    out[1] = c01 * id;
-    out[2] = c02 * id;
-    out[3] = c10 * id;
-    out[4] = c11 * id;
-    out[5] = c12 * id;
-    out[6] = c20 * id;
-    out[7] = c21 * id;
-    out[8] = c22 * id;
-}
-
-// cvRodrigues2 matrix -> vector; polar factor by three Newton steps (OpenCV: SVD U*V^T)
+// cvRodrigues2 matrix -> vector: R replaced by its polar factor U V^T from OpenCV 2.4's SVD
+// (include/fm3d_cvsvd.h, the same JacobiSVD the oracle restates), then the skew part and trace
 void rodrigues_m2v(const double Rin[9], double r[3]) {
-    double R[9], Y[9];
-    std::memcpy(R, Rin, sizeof(R));
-    for (int it = 0; it < 3; it++) {
-        inv_t3(R, Y);
-        for (int k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
-    }
+    double R[9];
+    fm3d_cv::polar3(Rin, R);
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
     double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
@@ -351,14 +326,6 @@ int upload(fm3d_ctx* c, DevBuf& b, const void* src, size_t bytes) {
     return FM3D_OK;
 }
 
-bool f32_is_u8(const float* x, size_t n) {
-    for (size_t i = 0; i < n; i++) {
-        float v = x[i];
-        if (!(v >= 0.f && v <= 255.f) || v != std::floor(v)) return false;
-    }
-    return true;
-}
-
 // The staging buffers are refilled only after the H2D copies of the previous call out of them
 // have run (c->evStage, recorded after them on the context stream).
 int staging_wait(fm3d_ctx* c) {
@@ -376,8 +343,7 @@ int upload_pinned(fm3d_ctx* c, DevBuf& dst, HostBuf& h, const void* src, size_t 
     return FM3D_OK;
 }
 
-// rows of bytes padded to dimPad (multiple of 128) with value 128 (x - 128 == 0: no effect on d2),
-// from u8 rows or from integer-valued f32 rows
+// rows of bytes padded to dimPad (multiple of 128) with value 128 (x - 128 == 0: no effect on d2)
 void pad_u8(uint8_t* o, const uint8_t* x, int n, int dim, int dimPad) {
     if (dim == dimPad) {
         std::memcpy(o, x, (size_t)n * dim);
@@ -388,13 +354,6 @@ void pad_u8(uint8_t* o, const uint8_t* x, int n, int dim, int dimPad) {
         std::memset(o + (size_t)i * dimPad + dim, 128, dimPad - dim);
     }
 }
-void f32_to_u8(uint8_t* o, const float* x, int n, int dim, int dimPad) {
-    for (int i = 0; i < n; i++) {
-        for (int d = 0; d < dim; d++) o[(size_t)i * dimPad + d] = (uint8_t)x[(size_t)i * dim + d];
-        std::memset(o + (size_t)i * dimPad + dim, 128, dimPad - dim);
-    }
-}
-
 // stage descriptors on the device (asynchronous H2D from the pinned staging buffers; the stream
 // orders every later use); returns the effective kernel type
 // (waitStaging false: the caller waited for the staging buffers already, stage_pipeline)
@@ -404,23 +363,47 @@ int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB,
     int r;
     if (waitStaging && (r = staging_wait(c))) return r;
     int t = type;
-    // integer-valued f32 rows take the u8 kernel only where it supports the width (padded <= 256)
-    if (type == FM3D_DESC_F32 && ((dim + 127) / 128) * 128 <= 256 && f32_is_u8((const float*)descA, (size_t)nA * dim) &&
-        f32_is_u8((const float*)descB, (size_t)nB * dim))
-        t = FM3D_DESC_U8;  // integer-valued rows: exact, identical ranking and distances
+    if (type == FM3D_DESC_F32 && ((dim + 127) / 128) * 128 <= 256) {
+        // float rows as the reference hands them to knnMatch (descriptorsmatcher.cpp:114-117): to the
+        // device as they are; one kernel packs them into padded u8 rows and flags any element that is not
+        // an integer in [0, 255].  Integer-valued rows (SIFT) take the u8 kernel -- exact, the same
+        // ranking and distances as the float scan -- others the float kernels.  The choice of kernels
+        // needs the flag: one host wait for this context's copies and the pack (the float path waits
+        // on the device once more anyway, run_match)
+        const int dp = ((dim + 127) / 128) * 128;
+        int r2;
+        if ((r2 = upload_pinned(c, c->A, c->hA, descA, (size_t)nA * dim * 4))) return r2;
+        if ((r2 = upload_pinned(c, c->B, c->hB, descB, (size_t)nB * dim * 4))) return r2;
+        HIPCHK(c, c->A8.ensure((size_t)nA * dp + 16));
+        HIPCHK(c, c->B8.ensure((size_t)nB * dp + 16));
+        HIPCHK(c, c->u8Flag.ensure(64));
+        HIPCHK(c, c->hFlag.ensure(64));
+        HIPCHK(c, hipMemsetAsync(c->u8Flag.p, 0, sizeof(int), c->stream));
+        fm3d::launch_f32_pack_u8(c->A.as<float>(), nA, c->B.as<float>(), nB, dim, dp, c->A8.as<uint8_t>(),
+                                 c->B8.as<uint8_t>(), c->u8Flag.as<int>(), c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->hFlag.p, c->u8Flag.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->evStage, c->stream));
+        HIPCHK(c, hipEventSynchronize(c->evStage));
+        if (*c->hFlag.as<int>() == 0) {
+            std::swap(c->A, c->A8);  // the packed rows become the matcher's inputs
+            std::swap(c->B, c->B8);
+            *dimPad = dp;
+            *effType = FM3D_DESC_U8;
+        } else {
+            *dimPad = dim;
+            *effType = FM3D_DESC_F32;
+        }
+        return FM3D_OK;
+    }
     if (t == FM3D_DESC_U8) {
         int dp = ((dim + 127) / 128) * 128;
         if (dp > 256) return fail(c, FM3D_ERR_UNSUPPORTED, "u8 descriptors longer than 256 bytes");
         const size_t ba = (size_t)nA * dp, bb = (size_t)nB * dp;
         HIPCHK(c, c->hA.ensure(ba + 1));
         HIPCHK(c, c->hB.ensure(bb + 1));
-        if (type == FM3D_DESC_F32) {
-            f32_to_u8(c->hA.as<uint8_t>(), (const float*)descA, nA, dim, dp);
-            f32_to_u8(c->hB.as<uint8_t>(), (const float*)descB, nB, dim, dp);
-        } else {
-            pad_u8(c->hA.as<uint8_t>(), (const uint8_t*)descA, nA, dim, dp);
-            pad_u8(c->hB.as<uint8_t>(), (const uint8_t*)descB, nB, dim, dp);
-        }
+        pad_u8(c->hA.as<uint8_t>(), (const uint8_t*)descA, nA, dim, dp);
+        pad_u8(c->hB.as<uint8_t>(), (const uint8_t*)descB, nB, dim, dp);
         HIPCHK(c, c->A.ensure(ba));
         HIPCHK(c, c->B.ensure(bb));
         if (ba) HIPCHK(c, hipMemcpyAsync(c->A.p, c->hA.p, ba, hipMemcpyHostToDevice, c->stream));
@@ -477,6 +460,7 @@ bool stage_events() {
 // match's last launch; nndr_ms stays 0) and triangulate_ms, when the step recorded its stage events
 void stage_times(fm3d_ctx* c, fm3d_pipeline_stats* stats) {
     float ms = 0;
+    stats->match_ms = stats->nndr_ms = stats->triangulate_ms = 0;  // 0 when the step recorded no stage events
     if (!c->stageEv) return;
     hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
     stats->match_ms = ms;
@@ -488,18 +472,21 @@ void stage_times(fm3d_ctx* c, fm3d_pipeline_stats* stats) {
 int make_lookback(fm3d_ctx* c, int nBlocks, fm3d::LookBack* lb) {
     if (!c->lbCtr.p) {
         HIPCHK(c, c->lbCtr.ensure(64));
-        HIPCHK(c, hipMemsetAsync(c->lbCtr.p, 0, 64, c->stream));
-        c->lbBase = 0;
+        HIPCHK(c, hipMemsetAsync(c->lbCtr.p, 0, 64, c->stream));  // each launch leaves it at 0
     }
+    bool zero = false;
     if (c->lbSt.bytes < (size_t)nBlocks * 8) {
         HIPCHK(c, c->lbSt.ensure((size_t)nBlocks * 8 * 2));
-        HIPCHK(c, hipMemsetAsync(c->lbSt.p, 0, c->lbSt.bytes, c->stream));  // epoch 0: "not yet"
+        zero = true;
     }
+    if (++c->lbEpoch == 0) {  // the 32-bit tag wrapped: 0 is the zeroed words' "not yet"
+        c->lbEpoch = 1;
+        zero = true;
+    }
+    if (zero) HIPCHK(c, hipMemsetAsync(c->lbSt.p, 0, c->lbSt.bytes, c->stream));  // epoch 0: "not yet"
     lb->st = c->lbSt.as<unsigned long long>();
     lb->ctr = c->lbCtr.as<unsigned>();
-    lb->base = c->lbBase;
-    lb->epoch = ++c->lbEpoch;
-    c->lbBase += (unsigned)nBlocks;
+    lb->epoch = c->lbEpoch;
     return FM3D_OK;
 }
 
@@ -685,6 +672,37 @@ struct LMSrc {
 // and launch counters): the slots that find one pair's points used up take the next pair's, so
 // a second pair fills the launch's end-of-queue tail (fm3d_pipeline_link).  Every problem's
 // context must be ordered before this stream by the caller (its points, pyramids).
+// the LM launch's workgroups for Ptot points (Ptot < 0: as many as the GPU holds): the settings'
+// lmWaves, or every CU at the kernel's occupancy, bounded by the points, the slabs' HBM budget and
+// their 32-bit offsets
+int lm_groups(fm3d_ctx* c, const void* kptr, int slots, long Ptot, long* out) {
+    long groups = c->s.lmWaves;
+    if (groups <= 0) {
+        int cus = 0, perCU = 0;
+        HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kptr, fm3d::kLM2Threads, 0));
+        if (perCU < 1) perCU = 1;
+        groups = (long)cus * perCU;
+    }
+    if (Ptot >= 0) {
+        const long needed = (Ptot + slots - 1) / slots;
+        if (groups > needed) groups = needed;
+    }
+    const size_t ents = (size_t)c->nOffPad * slots;
+    // per slot and entry: rays (2 doubles) + I1, fvec dI, two Jacobian dI (float) + compact index
+    const size_t perGroup = ents * (2 * sizeof(double) + 5 * 4);
+    const size_t budget = (size_t)48 << 30;  // HBM budget for the per-slot pixel slabs
+    long cap = (long)(budget / perGroup);
+    if (cap < 1) cap = 1;
+    if (groups > cap) groups = cap;
+    // the summed passes address a slab array with a 32-bit byte offset
+    const long cap32 = (long)((((size_t)1 << 32) - ((size_t)1 << 20)) / (ents * sizeof(double) * (FM3D_RAY_AOS ? 2 : 1)));
+    if (groups > cap32) groups = cap32;
+    if (groups < 1) groups = 1;
+    *out = groups;
+    return FM3D_OK;
+}
+
 int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats, hipEvent_t e0, hipEvent_t e1) {
     int r;
     if (nProb < 1 || nProb > fm3d::kLMMaxProblems) return fail(c, FM3D_ERR_INVALID, "bad LM problem count");
@@ -714,10 +732,11 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
     HIPCHK(c, c->lmStat.ensure(256));
     // persistent workgroups of fm3d::kLM2Slots term waves (one point each) + a chain wave, or in the
     // tree-reduction mode kLM2Slots + 1 term waves; slots refill from the queue (fm3d_lm2.hip)
-    const char* te = getenv("FM3D_LM_TREE");  // A/B switch: overrides settings.lmReduction
+    // the settings field alone picks the mode (no environment override: ADVICE r05; the tree mode
+    // fails the parity gate, profiles/r05_full_parity.json)
     if (c->s.lmReduction != 0 && c->s.lmReduction != 1)
         return fail(c, FM3D_ERR_INVALID, "lmReduction must be 0 (pixel order) or 1 (tree)");
-    const bool tree = te ? atoi(te) != 0 : c->s.lmReduction != 0;
+    const bool tree = c->s.lmReduction != 0;
     const int slots = fm3d::kLM2Slots + (tree ? 1 : 0);
     // one pose for all problems: the single-pose kernel (entry 0 of the table serves them all)
     bool multiPose = false;
@@ -728,27 +747,10 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
                                          : reinterpret_cast<const void*>(fm3d::lm2_kernel<false, true>))
                             : (multiPose ? reinterpret_cast<const void*>(fm3d::lm2_kernel<true, false>)
                                          : reinterpret_cast<const void*>(fm3d::lm2_kernel<false, false>));
-    long groups = c->s.lmWaves;
-    if (groups <= 0) {
-        int cus = 0, perCU = 0;
-        HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kptr, fm3d::kLM2Threads, 0));
-        if (perCU < 1) perCU = 1;
-        groups = (long)cus * perCU;
-    }
-    const long needed = (Ptot + slots - 1) / slots;
-    if (groups > needed) groups = needed;
+    long groups = 0;
+    int r0;
+    if ((r0 = lm_groups(c, kptr, slots, Ptot, &groups))) return r0;
     const size_t ents = (size_t)c->nOffPad * slots;
-    // per slot and entry: rays (2 doubles) + I1, fvec dI, two Jacobian dI (float) + compact index
-    const size_t perGroup = ents * (2 * sizeof(double) + 5 * 4);
-    const size_t budget = (size_t)48 << 30;  // HBM budget for the per-slot pixel slabs
-    long cap = (long)(budget / perGroup);
-    if (cap < 1) cap = 1;
-    if (groups > cap) groups = cap;
-    // the summed passes address a slab array with a 32-bit byte offset
-    const long cap32 = (long)((((size_t)1 << 32) - ((size_t)1 << 20)) / (ents * sizeof(double) * (FM3D_RAY_AOS ? 2 : 1)));
-    if (groups > cap32) groups = cap32;
-    if (groups < 1) groups = 1;
     // +8 KiB: the passes prefetch up to eight 64-entry chunks past a slot's last entry
     HIPCHK(c, c->slab.ensure(ents * 2 * sizeof(double) * groups + 16384));
     HIPCHK(c, c->slabI1.ensure(ents * 5 * 4 * groups + 16384));
@@ -1687,6 +1689,7 @@ const char* fm3d_version(void) { return "fm3d 0.1 (gfx950)"; }
 int fm3d_ctx_create(const fm3d_settings* s, int device, fm3d_ctx** out) {
     if (!s || !out) return FM3D_ERR_INVALID;
     *out = nullptr;
+    if (s->dltSolver != 0 && s->dltSolver != 1) return FM3D_ERR_INVALID;  // cvSVD or the legacy Jacobi
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return FM3D_ERR_HIP;
     if (device < 0 || device >= n) return FM3D_ERR_INVALID;
@@ -1699,6 +1702,8 @@ int fm3d_ctx_create(const fm3d_settings* s, int device, fm3d_ctx** out) {
         return FM3D_ERR_HIP;
     }
     c->ownStream = true;
+    // test hook: the look-back tag to start from (tests/test_gpu_c2_pipeline.py runs across its wrap)
+    if (const char* le = getenv("FM3D_DEBUG_LB_EPOCH")) c->lbEpoch = (unsigned)strtoul(le, nullptr, 0);
     for (auto& e : c->ev) hipEventCreate(&e);
     hipEventCreateWithFlags(&c->evStage, hipEventDisableTiming);
     hipEventCreateWithFlags(&c->evProj, hipEventDisableTiming);
@@ -1726,7 +1731,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->triPts, &c->triMask, &c->triMask8, &c->pts, &c->srcIdx, &c->lmNormals, &c->lmStatus,
                       &c->lmInfo, &c->lmNfev, &c->lmMdat, &c->lmQueue, &c->lmStat,
                       &c->slab, &c->slabI1,
-                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->f32Work, &c->A8, &c->B8,
+                      &c->records, &c->recTmp, &c->recFlag, &c->lmProj, &c->partIdx, &c->partKey, &c->bPairs, &c->f32Work, &c->A8, &c->B8, &c->u8Flag,
                       &c->sfImg, &c->sfSum, &c->sfDet, &c->sfTr, &c->sfLayers, &c->sfMids, &c->sfCand, &c->sfCount,
                       &c->sfSortTmp, &c->sfFlag, &c->sfPos, &c->sfKp, &c->sfKin, &c->sfSrc, &c->sfDesc, &c->sfDW, &c->sfAng,
                       &c->orbPyr, &c->orbTab, &c->orbLev, &c->orbMap, &c->orbFlag, &c->orbPos, &c->orbKp, &c->orbR,
@@ -1740,7 +1745,7 @@ void fm3d_ctx_destroy(fm3d_ctx* c) {
                       &c->msHeap, &c->msNode, &c->msHist, &c->msReg, &c->msCnt, &c->msOff, &c->msXY, &c->msScr, &c->msRank,
                       &c->msKp, &c->msFlag, &c->msPos, &c->msOut, &c->msPad, &c->msRegC};
     for (DevBuf* b : bufs) b->release();
-    HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall};
+    HostBuf* hbufs[] = {&c->hA, &c->hB, &c->hK1, &c->hK2, &c->hImg, &c->hTab, &c->hProj, &c->hSmall, &c->hFlag};
     for (HostBuf* b : hbufs) b->release();
     hipEventDestroy(c->evStage);
     hipEventDestroy(c->evProj);
@@ -1885,6 +1890,7 @@ int fm3d_triangulate(fm3d_ctx* c, const fm3d_point2f* kpts1, int n1, const fm3d_
     p.pts = c->triPts.as<double>();
     p.mask = c->triMask.as<int>();
     p.mask8 = c->triMask8.as<uint8_t>();
+    p.dltSolver = c->s.dltSolver;
     fm3d::launch_triangulate(p, c->stream);
     fm3d::launch_compact_points(c->triPts.as<double>(), c->triMask.as<int>(), K, nullptr, c->pts.as<double>(),
                                 c->count.as<int>(), c->srcIdx.as<int>(), c->scanTmp.p, c->stream);
@@ -1994,7 +2000,11 @@ int stage_pipeline(fm3d_ctx* c, const void* descA, int nA, const void* descB, in
     if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp, false))) return r;
     if ((r = upload_pinned(c, c->kp1, c->hK1, kpts1, (size_t)nA * sizeof(fm3d_point2f)))) return r;
     if ((r = upload_pinned(c, c->kp2, c->hK2, kpts2, (size_t)nB * sizeof(fm3d_point2f)))) return r;
-    if ((r = set_images_impl(c, img1, img2, width, height, width, false, false))) return r;  // records evStage
+    if (img1 || img2) {
+        if ((r = set_images_impl(c, img1, img2, width, height, width, false, false))) return r;  // records evStage
+    } else {  // no images (C2's match + DLT needs none): the context keeps the ones it has, if any
+        HIPCHK(c, hipEventRecord(c->evStage, c->stream));
+    }
     if (!c->haveG12) {
         double g[16];
         if ((r = fm3d_setg12(c, c->s.pos1, c->s.pos2, c->s.pos1 + 3, c->s.pos2 + 3, g))) return r;
@@ -2051,6 +2061,7 @@ int pipeline_front(fm3d_ctx* c) {
     tp.pts = c->triPts.as<double>();
     tp.mask = c->triMask.as<int>();
     tp.mask8 = nullptr;
+    tp.dltSolver = c->s.dltSolver;
     {   // DLT with the inliers' compaction fused (launch_triangulate_compact)
         fm3d::LookBack lb;
         if ((r = make_lookback(c, fm3d::triangulate_compact_blocks(nA), &lb))) return r;
@@ -2324,6 +2335,32 @@ int fm3d_internal_finish(fm3d_ctx* c, int* nKept, fm3d_pipeline_stats* stats) {
 const int* fm3d_internal_kept_dev(fm3d_ctx* c) { return c->pcnt.as<int>() + 2; }
 hipStream_t fm3d_internal_stream(fm3d_ctx* c) { return c->stream; }
 int fm3d_internal_device(fm3d_ctx* c) { return c->device; }
+// the device memory one context may take: its largest LM launch's slabs (every CU filled) plus the
+// per-pair buffers of nA queries against nB train rows of dim elements (a conservative estimate of
+// what the pipeline's DevBufs grow to: descriptors, their u8 / unpacked copies, per-query match,
+// triangulation, LM and record arrays, the matchers' part lists, pyramids)
+int fm3d_internal_memory_need(fm3d_ctx* c, int64_t nA, int64_t nB, int dim, int type, int width, int height,
+                              size_t* bytes) {
+    hipSetDevice(c->device);
+    int r;
+    if ((r = ensure_offsets(c))) return r;
+    const bool tree = c->s.lmReduction != 0;
+    const int slots = fm3d::kLM2Slots + (tree ? 1 : 0);
+    const void* kptr = tree ? reinterpret_cast<const void*>(fm3d::lm2_kernel<true, true>)
+                            : reinterpret_cast<const void*>(fm3d::lm2_kernel<true, false>);
+    long groups = 0;
+    if ((r = lm_groups(c, kptr, slots, -1, &groups))) return r;
+    const size_t ents = (size_t)c->nOffPad * slots;
+    size_t need = ents * (2 * sizeof(double) + 5 * 4) * groups + 32768;
+    const size_t rowIn = type == FM3D_DESC_F32 ? (size_t)dim * 4 : (size_t)dim;
+    const size_t rowWork = 256 + (type == FM3D_DESC_F32 ? (size_t)dim * 4 : 0);  // u8 / unpacked / pair copies
+    need += (size_t)(nA + nB) * (rowIn + rowWork) + (size_t)nB * 64;
+    need += (size_t)nA * 1536;  // per query: top-2 lists + 16 parts, matches, points, masks, LM arrays, records
+    need += (size_t)width * height * 4 + ((size_t)16 << 20);  // pyramids with guards, small buffers
+    *bytes = need;
+    return FM3D_OK;
+}
+
 int fm3d_internal_prepare(fm3d_ctx* c) {  // the device count buffer, before a collective names it
     hipSetDevice(c->device);
     HIPCHK(c, c->pcnt.ensure(64));

@@ -23,3 +23,7 @@ const int* fm3d_internal_kept_dev(fm3d_ctx* c);
 hipStream_t fm3d_internal_stream(fm3d_ctx* c);
 int fm3d_internal_device(fm3d_ctx* c);
 int fm3d_internal_prepare(fm3d_ctx* c);
+// the device memory one context of this settings may grow to for a frame pair of nA x nB rows:
+// its LM slabs (the largest launch) + a conservative estimate of the per-pair buffers
+int fm3d_internal_memory_need(fm3d_ctx* c, int64_t nA, int64_t nB, int dim, int type, int width, int height,
+                              size_t* bytes);

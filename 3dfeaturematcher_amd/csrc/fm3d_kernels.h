@@ -125,6 +125,10 @@ void launch_knn2_i8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimP
 // row constants of both sides: cq = |a'|^2 per query row, ctp = packed train constants
 void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int* cq, int* ctp,
                         hipStream_t s);
+// float rows (nA x dim, nB x dim) -> u8 rows padded to dimPad with 128, and *notU8 |= 1 when any element
+// is not an integer in [0, 255] (the caller zeroes it; (nA + nB) * dimPad / 4 < 2^32)
+void launch_f32_pack_u8(const float* A, int nA, const float* B, int nB, int dim, int dimPad, uint8_t* Au,
+                        uint8_t* Bu, int* notU8, hipStream_t s);
 // 32-byte binary rows -> 256 int8 (query 0/1, train -1/+1) + packed train constants popc(b)
 void launch_unpack_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, uint8_t* outA, uint8_t* outB, int* ctp,
                         hipStream_t s);
@@ -312,6 +316,7 @@ struct TriParams {
     double* pts;      // K x 3 (match order, not compacted)
     int* mask;        // K
     uint8_t* mask8;   // K (optional)
+    int dltSolver;    // fm3d_settings.dltSolver: 0 OpenCV 2.4's cvSVD (6 x 4), 1 the round-robin 4 x 4 Jacobi
 };
 void launch_triangulate(const TriParams& p, hipStream_t s);
 
@@ -322,10 +327,19 @@ void launch_triangulate(const TriParams& p, hipStream_t s);
 // only ever waits for blocks that started before it.
 struct LookBack {
     unsigned long long* st;  // per block of the launch: (epoch << 32) | (flag << 30) | value
-    unsigned* ctr;           // block counter (never reset; base = its value at the launch's start)
-    unsigned base;
-    unsigned epoch;  // the launch's tag: status words of earlier launches read as "not yet"
+    unsigned* ctr;           // block counter: 0 at every launch's start (lookback_block_id)
+    unsigned epoch;  // the launch's tag (never 0): status words of earlier launches read as "not yet"
 };
+// A block's index in launch order.  The block that takes the last index resets the counter for the
+// next launch on the stream: every other block of this launch took its index before it (one
+// modification order per address), so each launch's indices are 0 .. gridDim.x - 1 whatever the
+// earlier launches did -- a launch that never ran leaves the counter at 0 (no host-side
+// base to fall out of step with the device).
+__device__ inline int lookback_block_id(const LookBack& lb) {
+    const unsigned id = atomicAdd(lb.ctr, 1u);
+    if (id == gridDim.x - 1) __hip_atomic_store(lb.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (int)id;
+}
 // NNDR (descriptorsmatcher.cpp:119-129) with the parts' top-2 merge (int keys; parts = 1: idx / key
 // as merged lists) and the stable compaction of the kept matches: out[0 .. *count)
 void launch_nndr_compact(int type, const int* idx, const int* key, const float* fkey, const int* partIdx,

@@ -614,6 +614,7 @@ struct Shared {
     double result[kWA][2];
     Enorm chainEn[64];  // MINPACK enorm state of each chain lane (s2 lives in its register)
     int done[kWA];
+    int exited;  // TREE: term waves past their loop (the last one records the group's lifetime)
     // tail help: a wave whose slot has no more points takes every other chunk of a busy slot's
     // summed passes (one helper per slot, attached for good)
     int helper[kWA];                // 1 once a helper is attached
@@ -1072,7 +1073,10 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     constexpr int NS = TREE ? kWA : kW;  // term waves (slots) of the workgroup
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long tStart = wall_clock64(), cyStart = clock64();
-    if (tid == 0) sh.P = p;
+    if (tid == 0) {
+        sh.P = p;
+        sh.exited = 0;
+    }
     if (tid < NS) {
         for (int k = 0; k < kR; k++) sh.rowTag[tid][k] = -1;
         sh.consumed[tid][0] = sh.consumed[tid][1] = 0;
@@ -1992,8 +1996,11 @@ __global__ __launch_bounds__(kLM2Threads, 4) void lm2_kernel(LMParams p) {
     } else {
         chain_wave(lane, tStart, p.maxTicks, p.statPass + 2, p.statPass + 18);
     }
-    // the group's lifetime: the chain wave leaves last (once every slot is done)
-    if (wave == kW && lane == 0) {
+    // the group's lifetime, recorded by the wave that leaves last: the chain wave (it leaves once
+    // every slot is done), or in TREE mode, which has none, the last term wave past its loop
+    bool lastWave = false;
+    if (lane == 0) lastWave = TREE ? atomicAdd(&sh.exited, 1) == NS - 1 : wave == kW;
+    if (lastWave) {
         atomicAdd(p.statPass + 4, clock64() - cyStart);
         const unsigned long long wt = wall_clock64() - tStart;
         atomicAdd(p.statPass + 5, wt);

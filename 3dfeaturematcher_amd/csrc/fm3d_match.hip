@@ -637,7 +637,7 @@ __global__ __launch_bounds__(256) void nndr_compact_kernel(int type, const int* 
                                                            LookBack lb) {
     __shared__ int sBid, sEx, sWave[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) sBid = (int)(atomicAdd(lb.ctr, 1u) - lb.base);
+    if (tid == 0) sBid = lookback_block_id(lb);
     __syncthreads();
     const int bid = sBid;
     const int q = bid * 256 + tid;
@@ -1082,6 +1082,47 @@ __global__ __launch_bounds__(256) void knn2_f32_rescan_kernel(const float* __res
     }
 }
 
+// Float rows handed over as the reference's cv::Mat of SIFT descriptors (descriptorsmatcher.cpp:114-117)
+// that hold integers in [0, 255] (OpenCV's SIFT saturates to uchar before the float conversion): each
+// thread packs 4 bytes of a u8 row padded to dimPad (pad value 128) for the int8-MFMA kernel, both
+// sides in one launch, and *notU8 becomes 1 when any element is not such an integer (NaN included),
+// so the host keeps the float kernels.  (Until round 6 the host scanned and converted the rows on the
+// submitting thread.)
+__global__ __launch_bounds__(256) void f32_pack_u8_kernel(const float* __restrict__ A, unsigned nA,
+                                                          const float* __restrict__ B, unsigned nB, int dim,
+                                                          int dimPad, uint8_t* __restrict__ Au,
+                                                          uint8_t* __restrict__ Bu, int* __restrict__ notU8) {
+    const unsigned q = (unsigned)dimPad >> 2;  // 4-byte groups per padded row
+    const unsigned gA = nA * q, total = gA + nB * q;
+    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (t < total) {
+        const bool isA = t < gA;
+        const unsigned g = isA ? t : t - gA;
+        const unsigned row = g / q;
+        const int c0 = (int)(g - row * q) * 4;
+        const float* src = (isA ? A : B) + (size_t)row * dim;
+        float v[4];
+        if ((dim & 3) == 0 && c0 + 4 <= dim) {
+            const float4 f = *(const float4*)(src + c0);
+            v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = c0 + k < dim ? src[c0 + k] : 128.f;
+        }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool ok = v[k] >= 0.f && v[k] <= 255.f && v[k] == floorf(v[k]);
+            bad |= !ok;
+            packed |= (ok ? (uint32_t)v[k] : 0u) << (8 * k);
+        }
+        ((uint32_t*)(isA ? Au : Bu))[g] = packed;
+    }
+    const unsigned long long m = __ballot(bad);
+    if (m && (int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) atomicOr(notU8, 1);
+}
+
 }  // namespace
 
 void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int dimPad, int* cq, int* ctp,
@@ -1090,6 +1131,14 @@ void launch_rowconst_u8(const uint8_t* A, int nA, const uint8_t* B, int nB, int 
     if (threads == 0) return;
     const int rowBits = knn2_i8_tile_rows(dimPad, 0) == 256 ? 8 : 7;
     rowconst_u8_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(A, nA, B, nB, dimPad, cq, ctp, rowBits);
+}
+
+void launch_f32_pack_u8(const float* A, int nA, const float* B, int nB, int dim, int dimPad, uint8_t* Au,
+                        uint8_t* Bu, int* notU8, hipStream_t s) {
+    const size_t groups = ((size_t)nA + nB) * (dimPad / 4);
+    if (groups == 0) return;
+    f32_pack_u8_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, s>>>(A, (unsigned)nA, B, (unsigned)nB, dim, dimPad,
+                                                                       Au, Bu, notU8);
 }
 
 void launch_unpack_bits(const uint8_t* A, int nA, const uint8_t* B, int nB, uint8_t* outA, uint8_t* outB, int* ctp,

@@ -97,6 +97,12 @@ struct RcclGroup {
     }
 };
 
+// the failure text of this thread's last fm3d_mgpu_create (fm3d_mgpu_last_error(NULL))
+std::string& create_error() {
+    static thread_local std::string e;
+    return e;
+}
+
 constexpr int kDefaultBlock = 4096;
 constexpr int kSets = 4;  // frame pairs in flight (context sets; set 2i joins set 2i + 1's LM launches)
 
@@ -123,6 +129,8 @@ struct fm3d_mgpu {
     std::vector<std::vector<int32_t>> idx;          // per device: its global query indices (increasing)
     std::vector<std::vector<uint8_t>> rowsA;        // per device: its gathered query rows (host)
     std::vector<std::vector<fm3d_point2f>> kpA;     // per device: its gathered keypoints
+    std::vector<fm3d_record> mergeTmp;              // the devices' records before the merge
+    std::vector<size_t> memChecked;                 // per device: the memory need last pre-flighted
     bool staged = false;                            // fm3d_mgpu_pipeline_upload ran (set 0)
     bool pending[kSets] = {};
     bool gathered[kSets] = {};                      // the set's all-gather is queued
@@ -162,8 +170,55 @@ size_t row_bytes(int dim, int type) { return type == FM3D_DESC_F32 ? (size_t)dim
 // the device of block b: share b % shares lives on device share % ndev
 int device_of_block(const fm3d_mgpu* m, int64_t b) { return (int)((b % m->shares) % m->ndev); }
 
+// the k-way merge of per-list records (global query indices, each list increasing) under the
+// block-cyclic partition: block b's queries all belong to list owner(b), so the merged order is, for
+// b = 0, 1, ..., that list's next records below (b + 1) * block.  Returns the records written; a
+// record outside its list's blocks is left behind (the caller compares the count).
+template <class Owner>
+int64_t merge_blocks(const fm3d_record* recs, const int64_t* off, int lists, int64_t nA, int block, Owner owner,
+                     fm3d_record* out) {
+    std::vector<int64_t> pos(off, off + lists);
+    int64_t o = 0;
+    const int64_t nb = (nA + block - 1) / block;
+    for (int64_t b = 0; b < nb; b++) {
+        const int l = owner(b);
+        const int64_t lim = std::min<int64_t>((b + 1) * block, nA);
+        while (pos[l] < off[l + 1] && recs[pos[l]].queryIdx < lim) out[o++] = recs[pos[l]++];
+    }
+    return o;
+}
+
+// Pre-flight of device memory: before the contexts grow their buffers, every
+// device must have room for its four context sets -- each set's LM slabs (the largest launch: any set
+// may launch alone) and per-pair buffers (fm3d_internal_memory_need) -- and for the exchange
+// buffers, so too little memory is a clean FM3D_ERR_NOMEM, never an allocation failure mid-run.
+// `need` grows monotonically; only the growth since the last check must fit in the free memory.
+int preflight(fm3d_mgpu* m, int64_t nB, int dim, int type, int width, int height, int64_t capDev) {
+    if (m->memChecked.size() != (size_t)m->ndev) m->memChecked.assign(m->ndev, 0);
+    for (int d = 0; d < m->ndev; d++) {
+        const int64_t nAd = m->idx.empty() ? 0 : (int64_t)m->idx[d].size();
+        size_t per = 0;
+        int r = fm3d_internal_memory_need(m->ctx[0][d], nAd, nB, dim, type, width, height, &per);
+        if (r) return mfail(m, r, std::string("memory estimate: ") + fm3d_last_error(m->ctx[0][d]));
+        const size_t need = kSets * (per + (size_t)capDev * sizeof(fm3d_record) * (1 + m->ndev));
+        if (need <= m->memChecked[d]) continue;
+        size_t freeB = 0, totalB = 0;
+        MHIP(m, hipSetDevice(m->devices[d]));
+        MHIP(m, hipMemGetInfo(&freeB, &totalB));
+        const size_t grow = need - m->memChecked[d];
+        if (grow + ((size_t)256 << 20) > freeB)
+            return mfail(m, FM3D_ERR_NOMEM, "device " + std::to_string(m->devices[d]) + ": " +
+                                                std::to_string(grow >> 20) + " MiB more needed for " +
+                                                std::to_string(kSets) + " context sets (LM slabs + frame-pair "
+                                                "buffers), " + std::to_string(freeB >> 20) + " MiB free");
+        m->memChecked[d] = need;
+    }
+    return FM3D_OK;
+}
+
 // per-device query lists for nA queries; (re)allocates the exchange buffers when they grow
-int plan(fm3d_mgpu* m, int64_t nA) {
+// (nB, dim, type, width, height: the frame pair, for the memory pre-flight)
+int plan(fm3d_mgpu* m, int64_t nA, int64_t nB, int dim, int type, int width, int height) {
     m->nA = nA;
     m->idx.assign(m->ndev, {});
     const int64_t nb = (nA + m->block - 1) / m->block;
@@ -173,6 +228,8 @@ int plan(fm3d_mgpu* m, int64_t nA) {
     }
     int64_t cap = 1;
     for (auto& v : m->idx) cap = std::max<int64_t>(cap, (int64_t)v.size());
+    int r;
+    if ((r = preflight(m, nB, dim, type, width, height, std::max(cap, m->capDev)))) return r;
     if (cap > m->capDev) {
         free_buffers(m);
         const size_t slot = (size_t)cap * sizeof(fm3d_record);
@@ -239,24 +296,31 @@ int finish_set(fm3d_mgpu* m, int k, fm3d_record* out, int cap, int* nKept, fm3d_
         total += cnt[d];
     }
     if (total > cap) return mfail(m, FM3D_ERR_INVALID, "record buffer too small");
-    int64_t o = 0;
+    // every device's list to the host (device 0's gathered copy), local -> global query indices
+    std::vector<int64_t> off(m->ndev + 1, 0);
+    for (int d = 0; d < m->ndev; d++) off[d + 1] = off[d] + cnt[d];
+    m->mergeTmp.resize((size_t)total + 1);
     for (int d = 0; d < m->ndev; d++) {
         if (!cnt[d]) continue;
+        fm3d_record* dst = m->mergeTmp.data() + off[d];
         const char* src = (const char*)m->recv[k][0] + (size_t)d * m->capDev * sizeof(fm3d_record);
-        MHIP(m, hipMemcpy(out + o, src, (size_t)cnt[d] * sizeof(fm3d_record), hipMemcpyDeviceToHost));
+        MHIP(m, hipMemcpy(dst, src, (size_t)cnt[d] * sizeof(fm3d_record), hipMemcpyDeviceToHost));
         const auto& ix = m->idx[d];
         int32_t prev = -1;
         for (int i = 0; i < cnt[d]; i++) {
-            const int32_t l = out[o + i].queryIdx;
+            const int32_t l = dst[i].queryIdx;
             if (l < 0 || l >= (int32_t)ix.size() || l <= prev)
                 return mfail(m, FM3D_ERR_HIP, "a gathered record carries a bad local query index");
             prev = l;
-            out[o + i].queryIdx = ix[l];
+            dst[i].queryIdx = ix[l];
         }
-        o += cnt[d];
     }
-    // each device's list is in increasing query order and the query sets are disjoint
-    std::sort(out, out + o, [](const fm3d_record& a, const fm3d_record& b) { return a.queryIdx < b.queryIdx; });
+    // merge in query order without a sort: each device's list is increasing and holds exactly the
+    // queries of its blocks, so walking the blocks in order takes, for block b, its device's next
+    // records below the block's end (linear in records + blocks)
+    const int64_t o = merge_blocks(m->mergeTmp.data(), off.data(), m->ndev, m->nA, m->block,
+                                   [m](int64_t b) { return device_of_block(m, b); }, out);
+    if (o != total) return mfail(m, FM3D_ERR_HIP, "a gathered record lies outside its device's query blocks");
     if (nKept) *nKept = (int)o;
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
@@ -304,10 +368,14 @@ int fm3d_merge_shares(int nA, int shares, int block, const fm3d_record* const* r
         total += counts[s];
     }
     if (total > nA || (total && !out)) return FM3D_ERR_INVALID;
-    int64_t k = 0;
+    // the shares' records with global query indices, then merged in query order (merge_blocks:
+    // block b belongs to share b % shares; every share's list is increasing)
+    std::vector<fm3d_record> tmp((size_t)total + 1);
+    std::vector<int64_t> off(shares + 1, 0);
     for (int s = 0; s < shares; s++) {
         const int64_t mine = share_count(nA, shares, s, block);
         int32_t prev = -1;
+        off[s + 1] = off[s] + counts[s];
         for (int i = 0; i < counts[s]; i++) {
             fm3d_record r = recs[s][i];
             // local index within share s -> (block of the share, offset) -> global query
@@ -315,12 +383,12 @@ int fm3d_merge_shares(int nA, int shares, int block, const fm3d_record* const* r
             prev = r.queryIdx;
             const int64_t b = r.queryIdx / block, o = r.queryIdx % block;
             r.queryIdx = (int32_t)((b * shares + s) * block + o);
-            out[k++] = r;
+            tmp[off[s] + i] = r;
         }
     }
-    // every share's list is in increasing query order and the query sets are disjoint: the
-    // merged list is the records ordered by queryIdx (one record per query at most)
-    std::sort(out, out + k, [](const fm3d_record& a, const fm3d_record& b) { return a.queryIdx < b.queryIdx; });
+    const int64_t k = merge_blocks(tmp.data(), off.data(), shares, nA, block,
+                                   [shares](int64_t b) { return (int)(b % shares); }, out);
+    if (k != total) return FM3D_ERR_INVALID;
     *nOut = (int)k;
     return FM3D_OK;
 }
@@ -334,6 +402,7 @@ int fm3d_device_count(int* n) {
 }
 
 int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int shares, int block, fm3d_mgpu** out) {
+    create_error().clear();
     if (!s || !out || ndev <= 0 || ndev > 16 || shares < ndev || block < 0) return FM3D_ERR_INVALID;
     *out = nullptr;
     int count = 0;
@@ -366,6 +435,14 @@ int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int s
                 return r;
             }
         }
+    {   // the LM slabs of every context set must fit before anything else is set up
+        int r = preflight(m, 0, 128, FM3D_DESC_U8, 0, 0, 0);
+        if (r) {
+            create_error() = m->err;
+            fm3d_mgpu_destroy(m);
+            return r;
+        }
+    }
     m->comms.assign(ndev, nullptr);
     if (rccl().commInitAll(m->comms.data(), ndev, m->devices.data()) != ncclSuccess) {
         fm3d_mgpu_destroy(m);
@@ -390,7 +467,7 @@ void fm3d_mgpu_destroy(fm3d_mgpu* m) {
     delete m;
 }
 
-const char* fm3d_mgpu_last_error(const fm3d_mgpu* m) { return m ? m->err.c_str() : "null handle"; }
+const char* fm3d_mgpu_last_error(const fm3d_mgpu* m) { return m ? m->err.c_str() : create_error().c_str(); }
 
 int fm3d_mgpu_set_g12(fm3d_mgpu* m, const double g12[16]) {
     if (!m || !g12) return FM3D_ERR_INVALID;
@@ -411,7 +488,7 @@ int fm3d_mgpu_pipeline_upload(fm3d_mgpu* m, const void* descA, int nA, const voi
     const size_t rb = row_bytes(dim, type);
     m->staged = false;
     int r;
-    if ((r = plan(m, nA))) return r;
+    if ((r = plan(m, nA, nB, dim, type, width, height))) return r;
     for (int d = 0; d < m->ndev; d++) {
         gather_device(m, d, descA, rb, kpts1);
         const int n = (int)m->idx[d].size();
@@ -454,7 +531,8 @@ int fm3d_mgpu_submit(fm3d_mgpu* m, const void* descA, int nA, const void* descB,
     // a submit restages set 0 and may re-plan idx / nA: fm3d_mgpu_pipeline_run needs a new upload
     // 
     m->staged = false;
-    if (!others && (r = plan(m, nA))) return r;
+    if (!others && (r = plan(m, nA, nB, dim, type, width, height))) return r;
+    if (others && (r = preflight(m, nB, dim, type, width, height, m->capDev))) return r;
     // one host thread per device: gather its queries, stage and queue its path (a member set: its
     // front half; a leader set: the front half, one LM launch with the member set's queued pair,
     // both pairs' records)

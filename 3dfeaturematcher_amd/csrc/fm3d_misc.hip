@@ -9,14 +9,13 @@ namespace fm3d {
 namespace {
 
 // ---------------- DLT triangulation ----------------
-// Null vector of the 4x4 DLT system: one-sided (Hestenes) Jacobi SVD in the round-robin pair
-// order (0,1)+(2,3), (0,2)+(1,3), (0,3)+(1,2), up to 30 sweeps; the same arithmetic as
-// oracle/fm3d_oracle.c (orc_dlt_nullvec).  The two rotations of a step touch disjoint columns:
-// independent, so their dependent chains (three divisions and two square roots each) run side by
-// side -- half the latency of the cyclic order, which bounds this kernel (one wave per SIMD, a
-// ~800-cycle chain per rotation; tools/micro/tri_bench.hip).  The column indices are compile-time
-// constants (registers, no indexed moves).  OpenCV's cvSVD (JacobiSVD) is not reproducible bit for
-// bit; both agree with numpy.linalg.svd to ~1e-12 (tests/golden).
+// The default null vector is cvTriangulatePoints' (OpenCV 2.4): the 6 x 4 matrA and JacobiSVD, as
+// include/fm3d_cvsvd.h restates them (fm3d_cv::triangulate_point), bit for bit the oracle's
+// orc_triangulate1.  dltSolver = 1 (opt-in) keeps the solver of rounds 1-5 below: the 4-row system
+// and a one-sided (Hestenes) Jacobi SVD in the round-robin pair order (0,1)+(2,3), (0,2)+(1,3),
+// (0,3)+(1,2), up to 30 sweeps (oracle ORC_GEOM_DLT_LEGACY).  The two rotations of a step touch
+// disjoint columns: independent, so their dependent chains (three divisions and two square roots
+// each) run side by side.  Its points leave OpenCV's by up to ~1e-12 relative.
 template <int P, int Q>
 __device__ __forceinline__ bool jacobi_pair(double* A, double* V) {
     double alpha = 0, beta = 0, gamma = 0;
@@ -89,16 +88,20 @@ __device__ __forceinline__ bool tri_one(const TriParams& p, int i, double* X) {
     double u1x, u1y, u2x, u2y;
     undistort1(p.cam, (double)k1.x, (double)k1.y, u1x, u1y);
     undistort1(p.cam, (double)k2.x, (double)k2.y, u2x, u2y);
-    // P1 = [I|0], P2 = [I|0] * g12 (rows 0..2 of g12), A rows x*P.row2 - P.row0, y*P.row2 - P.row1
-    double A[16];
-    const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-    for (int k = 0; k < 4; k++) {
-        A[0 * 4 + k] = u1x * P1[8 + k] - P1[0 + k];
-        A[1 * 4 + k] = u1y * P1[8 + k] - P1[4 + k];
-        A[2 * 4 + k] = u2x * p.g12[8 + k] - p.g12[0 + k];
-        A[3 * 4 + k] = u2y * p.g12[8 + k] - p.g12[4 + k];
+    // P1 = [I|0], P2 = [I|0] * g12 (rows 0..2 of g12)
+    if (p.dltSolver == 0) {
+        fm3d_cv::triangulate_point(p.g12, u1x, u1y, u2x, u2y, X);
+    } else {  // rows x*P.row2 - P.row0, y*P.row2 - P.row1 per view
+        double A[16];
+        const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        for (int k = 0; k < 4; k++) {
+            A[0 * 4 + k] = u1x * P1[8 + k] - P1[0 + k];
+            A[1 * 4 + k] = u1y * P1[8 + k] - P1[4 + k];
+            A[2 * 4 + k] = u2x * p.g12[8 + k] - p.g12[0 + k];
+            A[3 * 4 + k] = u2y * p.g12[8 + k] - p.g12[4 + k];
+        }
+        dlt_nullvec(A, X);
     }
-    dlt_nullvec(A, X);
     // Z/W < zThresholdMin || Z/W >= zThresholdMax -> outlier (:200-216)
     const bool out = (X[2] / X[3] < p.zmin || X[2] / X[3] >= p.zmax);
     p.mask[i] = out ? 0 : 1;
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(kTriThreads) void triangulate_compact_kernel(TriPar
                                                                           int* hostCnt) {
     __shared__ int sBid;
     const int lane = threadIdx.x;
-    if (lane == 0) sBid = (int)(atomicAdd(lb.ctr, 1u) - lb.base);
+    if (lane == 0) sBid = lookback_block_id(lb);
     __syncthreads();
     const int bid = sBid;
     const int i = bid * kTriThreads + lane;

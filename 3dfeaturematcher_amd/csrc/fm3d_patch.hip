@@ -66,42 +66,16 @@ __global__ void frames_kernel(const double* __restrict__ pts, const double* __re
     F[15] = 1;
 }
 
-// 3x3 inverse transpose via the adjugate (one Newton step of the polar decomposition below)
-__device__ inline void inv_t3(const double A[9], double out[9]) {
-    const double c00 = A[4] * A[8] - A[5] * A[7];
-    const double c01 = A[5] * A[6] - A[3] * A[8];
-    const double c02 = A[3] * A[7] - A[4] * A[6];
-    const double c10 = A[2] * A[7] - A[1] * A[8];
-    const double c11 = A[0] * A[8] - A[2] * A[6];
-    const double c12 = A[1] * A[6] - A[0] * A[7];
-    const double c20 = A[1] * A[5] - A[2] * A[4];
-    const double c21 = A[2] * A[3] - A[0] * A[5];
-    const double c22 = A[0] * A[4] - A[1] * A[3];
-    const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
-    const double id = 1. / det;
-    out[0] = c00 * id;
-    out[1] = c01 * id;
-    out[2] = c02 * id;
-    out[3] = c10 * id;
-    out[4] = c11 * id;
-    out[5] = c12 * id;
-    out[6] = c20 * id;
-    out[7] = c21 * id;
-    out[8] = c22 * id;
-}
-
 // decomposeTransformation (tools.cpp:101-114) then cvProjectPoints2's Rodrigues: the R, t that
 // projectReferencePointsToImageWithFrame projects with.  cvRodrigues2 (matrix -> vector) first
-// replaces R by its nearest orthonormal matrix (polar factor, three Newton steps X <- (X + X^-T)/2).
+// replaces R by its nearest orthonormal matrix, U V^T of OpenCV 2.4's SVD (include/fm3d_cvsvd.h).
 __global__ void frame_camera_kernel(const double* __restrict__ frames, int P, double* __restrict__ RT) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
     const double* F = frames + 16 * (size_t)p;
-    double R[9] = {F[0], F[1], F[2], F[4], F[5], F[6], F[8], F[9], F[10]}, Y[9];
-    for (int it = 0; it < 3; it++) {
-        inv_t3(R, Y);
-        for (int k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
-    }
+    const double Rin[9] = {F[0], F[1], F[2], F[4], F[5], F[6], F[8], F[9], F[10]};
+    double R[9];
+    fm3d_cv::polar3(Rin, R);
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
     const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;

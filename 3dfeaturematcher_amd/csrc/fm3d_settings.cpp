@@ -171,6 +171,7 @@ extern "C" int fm3d_settings_default(fm3d_settings* s) {
     s->mserMinMargin = 0.003;
     s->mserEdgeBlurSize = 5;
     s->lmReduction = 0;  // pixel-order sums (the reference's)
+    s->dltSolver = 0;    // OpenCV 2.4 cvSVD (the reference's)
     return FM3D_OK;
 }
 
@@ -292,6 +293,7 @@ extern "C" int fm3d_settings_load(const char* path, fm3d_settings* s) {
     get_i(kv, "Fm3d.strictNanExit", &s->strictNanExit);
     get_i(kv, "Fm3d.lmWaves", &s->lmWaves);
     get_i(kv, "Fm3d.lmReduction", &s->lmReduction);
+    get_i(kv, "Fm3d.dltSolver", &s->dltSolver);
     return FM3D_OK;
 }
 

@@ -87,7 +87,16 @@ def parse():
                     help="descriptor kind of the synthetic pair (orb: 256-bit, Hamming; BASELINE C3 with "
                          "--keypoints 10000 --seed 102 --nndr 0.8 --ray 32|64)")
     ap.add_argument("--nndr", type=float, default=None)
+    ap.add_argument("--desc-dtype", choices=("u8", "f32"), default="u8",
+                    help="SIFT rows as u8, or as the float cv::Mat rows the reference's knnMatch receives "
+                         "(descriptorsmatcher.cpp:114-117; checked and packed to u8 on the device)")
+    ap.add_argument("--io", choices=("resident", "host"), default="resident",
+                    help="C2: resident -- inputs uploaded once, steps on HBM-resident inputs; host -- every step "
+                         "one frame pair's descriptors and keypoints from host memory and its matches and "
+                         "inlier points back to host memory")
     ap.add_argument("--lm-waves", type=int, default=0)
+    ap.add_argument("--lm-tree", action="store_true",
+                    help="settings.lmReduction = 1: the opt-in tree-reduction LM (fails the parity gate; A/B only)")
     ap.add_argument("--mode", choices=("stream", "resident"), default="stream",
                     help="stream (C4 headline): every step a frame pair from host memory to host memory, "
                          "--inflight pairs in flight; resident: inputs uploaded once, one step in flight")
@@ -111,6 +120,12 @@ def parse():
         os.path.join(ROOT, "profiles", "r02_pmc_c4.json")),
                     help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()
+
+
+def desc_rows(args, a):
+    """the descriptor rows as the caller hands them (--desc-dtype): u8, or SIFT's float cv::Mat rows"""
+    return a.astype(np.float32) if getattr(args, "desc_dtype", "u8") == "f32" and a.dtype == np.uint8 and \
+        args.desc != "orb" else a
 
 
 def records_digest(rec_bytes: bytes) -> str:
@@ -162,6 +177,7 @@ def c4_settings(fm3d, pair, args):
     s.pixelsRay = args.ray
     s.pyramids = args.levels
     s.lmWaves = args.lm_waves
+    s.lmReduction = 1 if getattr(args, "lm_tree", False) else 0
     return s
 
 
@@ -203,7 +219,7 @@ def run_c4_stream(args):
             pipes[j].link(pipes[i + nl - 1])
     binary = args.desc == "orb"
     bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(nf)]
-    inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+    inputs = (desc_rows(args, pair.desc1), desc_rows(args, pair.desc2), pair.kp1, pair.kp2, pair.img1, pair.img2)
 
     def stream_run(n_steps, timed):
         """n_steps frame pairs through the pipeline; returns per-pair (kept, stats, latency s, digest)."""
@@ -287,7 +303,8 @@ def run_c4_stream(args):
         },
     })
     kp_k = wl["keypoints"] // 1000
-    desc = (f"C4: {kp_k}k SIFT-128 (u8) keypoints per {wl['width']}x{wl['height']} frame pair, full pipeline, "
+    rows = "float" if getattr(args, "desc_dtype", "u8") == "f32" else "u8"
+    desc = (f"C4: {kp_k}k SIFT-128 ({rows}) keypoints per {wl['width']}x{wl['height']} frame pair, full pipeline, "
             f"pixelsRay {args.ray}, pyramids {args.levels}") if args.desc == "sift" else (
             f"C3-like: {kp_k}k ORB-256 (Hamming) keypoints per {wl['width']}x{wl['height']} frame pair, NNDR "
             f"{args.nndr}, full pipeline, pixelsRay {args.ray}, pyramids {args.levels}")
@@ -323,8 +340,14 @@ def run_c4_stream(args):
         "input_keypoints_per_s": wl["keypoints"] / frame_s,
         "roofline": roof,
         "cpu_baseline": cpu,
-        "stages_ms": {k: last_st[k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "lm_ms", "total_ms")},
-        "h2d_pyramids_ms": last_st["pyramid_ms"],
+        # stage costs from the resident run (one pair in flight); in the stream every stage's HIP events
+        # also take the time its launches wait behind the other pairs' LM launches
+        "stages_ms": {k: rstats[-1][k] for k in ("match_ms", "nndr_ms", "triangulate_ms", "lm_ms", "total_ms")},
+        "stages_note": ("stages_ms: the device-resident run's last step (one pair in flight: stage costs; nndr_ms "
+                        "is folded into match_ms); stages_ms_queued_and_run: the stream's last pair, whose stage "
+                        "events also span the time its launches queue behind the other pairs' LM launches"),
+        "stages_ms_queued_and_run": {k: last_st[k] for k in ("match_ms", "triangulate_ms", "pyramid_ms", "lm_ms",
+                                                              "total_ms")},
         "counts": {k: last_st[k] for k in ("queries", "matches", "inliers", "kept")},
         "lm_profile": lm_profile(rstats[-1]["lm"]),
         "lm_profile_overlapped": lm_profile(last_st["lm"]),
@@ -377,7 +400,7 @@ def run_mgpu(args, workload):
     mg = fm3d.MultiGPU(s, devices=list(range(n)), shares=n)
     mg.set_g12(pair.g12)
     binary = args.desc == "orb"
-    inputs = (pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+    inputs = (desc_rows(args, pair.desc1), desc_rows(args, pair.desc2), pair.kp1, pair.kp2, pair.img1, pair.img2)
     bufs = [np.zeros(len(pair.desc1), dtype=fm3d.RECORD) for _ in range(2)]  # the last two waits' records
 
     def stream_run(n_steps, mg=mg):
@@ -401,6 +424,9 @@ def run_mgpu(args, workload):
     t0 = time.perf_counter()
     res, last_rec = stream_run(args.steps)
     elapsed = time.perf_counter() - t0
+    # one pair alone after the stream (untimed): its stage events are stage costs, not time queued
+    # behind the other pairs' LM launches
+    iso_st = stream_run(1)[0][0][1]
     mg.close()
     kept_total = sum(r[0] for r in res)
     value = kept_total / elapsed
@@ -472,7 +498,11 @@ def run_mgpu(args, workload):
             "avg_launch_ms": frame_s * 1e3,
         },
         "cpu_baseline": None,
-        "stages_ms": {k: last_st[k] for k in ("match_ms", "lm_ms", "total_ms", "pyramid_ms")},
+        "stages_ms": {k: iso_st[k] for k in ("match_ms", "lm_ms", "total_ms", "pyramid_ms")},
+        "stages_ms_queued_and_run": {k: last_st[k] for k in ("match_ms", "lm_ms", "total_ms", "pyramid_ms")},
+        "stages_note": ("stages_ms: one frame pair alone after the timed stream (device 0's stage events: stage "
+                        "costs); stages_ms_queued_and_run: the stream's last pair, whose events also span the time "
+                        "its launches and copies wait behind the other pairs' LM launches"),
         "counts": {k: last_st[k] for k in ("queries", "matches", "inliers", "kept")},
         "setup_s": {"synthetic_generation": round(t_gen, 2)},
         "records_sha256": digests[0] if len(digests) == 1 else digests,
@@ -523,7 +553,8 @@ def run_torchrun_stream(args, workload):
     s = c4_settings(fm3d, pair, args)
     n = len(pair.desc1)
     qidx = shard.query_blocks(n, world, rank)
-    inputs = (pair.desc1[qidx], pair.desc2, pair.kp1[qidx], pair.kp2, pair.img1, pair.img2)
+    inputs = (desc_rows(args, pair.desc1[qidx]), desc_rows(args, pair.desc2), pair.kp1[qidx], pair.kp2, pair.img1,
+              pair.img2)
     nl = max(1, args.lm_pairs)
     nf = max(1, args.inflight) * nl
     streams = [torch.cuda.Stream(device=dev) for _ in range(nf)]
@@ -642,7 +673,9 @@ def run_torchrun_stream(args, workload):
                 "avg_launch_ms": frame_s * 1e3,
             },
             "cpu_baseline": None,
-            "stages_ms": {k: last_st[k] for k in ("match_ms", "lm_ms", "total_ms", "pyramid_ms")},
+            "stages_ms_queued_and_run": {k: last_st[k] for k in ("match_ms", "lm_ms", "total_ms", "pyramid_ms")},
+            "stages_note": ("rank 0's last pair of the stream: its stage events also span the time its launches "
+                            "and copies wait behind the other pairs' LM launches"),
             "counts_rank0": {k: last_st[k] for k in ("queries", "matches", "inliers", "kept")},
             "kept_per_frame_pair": int(len(merged)),
             "setup_s": {"synthetic_generation": round(t_gen, 2)},
@@ -847,16 +880,22 @@ def run_c2(args):
     s = fm3d.Settings.default()
     s.set_camera(pair.cam)
     s.nndrEpsilon = args.nndr
+    # the rows as the caller hands them: u8, or the float rows of the reference's cv::Mat
+    d1, d2 = ((pair.desc1, pair.desc2) if args.desc_dtype == "u8"
+              else (pair.desc1.astype(np.float32), pair.desc2.astype(np.float32)))
+    host_io = args.io == "host"
     # a serving loop: `inflight` contexts (one HIP stream each) with the pair resident, a frame pair
     # submitted on one while the previous ones run (fm3d_pipeline_submit_dlt / wait_dlt); the
-    # synchronous step (run_dlt, one host wait per pair) is timed beside it
+    # synchronous step (run_dlt, one host wait per pair) is timed beside it.  --io host: every step
+    # also stages the pair from host memory (fm3d_pipeline_upload without images: C2 needs none) and
+    # downloads its matches and inlier points
     nf = max(1, args.inflight)
     ctxs = [fm3d.Context(s) for _ in range(nf)]
     pipes = []
     for ctx in ctxs:
         fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
         pipe = fm3d.Pipeline(ctx)
-        pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+        pipe.upload(d1, d2, pair.kp1, pair.kp2, None, None)
         pipes.append(pipe)
     for _ in range(args.warmup):
         for pipe in pipes:
@@ -874,24 +913,29 @@ def run_c2(args):
     t_sub = [0.0] * nf
     busy = [False] * nf
     total = 0
+
+    def finish(k):
+        n, st = pipes[k].wait_dlt()
+        if host_io:  # the pair's matches and inlier points to host memory
+            pipes[k].dlt_results(st["matches"], st["inliers"])
+        lat.append(time.perf_counter() - t_sub[k])
+        stats.append(st)
+        return n
+
     t0 = time.perf_counter()
     for i in range(args.steps):
         k = i % nf
         if busy[k]:
-            n, st = pipes[k].wait_dlt()
-            lat.append(time.perf_counter() - t_sub[k])
-            total += n
-            stats.append(st)
+            total += finish(k)
         t_sub[k] = time.perf_counter()
+        if host_io:
+            pipes[k].upload(d1, d2, pair.kp1, pair.kp2, None, None)
         pipes[k].submit_dlt()
         busy[k] = True
     for j in range(args.steps, args.steps + nf):
         k = j % nf
         if busy[k]:
-            n, st = pipes[k].wait_dlt()
-            lat.append(time.perf_counter() - t_sub[k])
-            total += n
-            stats.append(st)
+            total += finish(k)
             busy[k] = False
     elapsed = time.perf_counter() - t0
     last = sync_stats[-1]
@@ -921,13 +965,21 @@ def run_c2(args):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8 (exact int32 distances), f64 triangulation",
         "data": "synthetic (ray-cast facet scene, seeded; 3dfeaturematcher_amd/synth.py)",
-        "config": {"workload": f"C2: {wl['keypoints'] // 1000}k SIFT-128 (u8) keypoints per {wl['width']}x{wl['height']} "
+        "config": {"workload": f"C2: {wl['keypoints'] // 1000}k SIFT-128 ({'float' if args.desc_dtype == 'f32' else 'u8'}) "
+                               f"keypoints per {wl['width']}x{wl['height']} "
                                f"frame pair, knnMatch k=2 + NNDR {args.nndr} + DLT triangulation",
                    "keypoints_per_frame": wl["keypoints"], "parallelism": "1 GPU",
-                   "timed": f"K frame pairs through match -> NNDR -> compaction -> DLT -> compaction on "
-                            f"HBM-resident inputs, {nf} contexts (HIP streams) in flight, every pair's counts read "
-                            f"back (page-locked) before its context takes the next; synchronous_ms_per_step: one "
-                            f"pair at a time"},
+                   "descriptor_rows": ("float32 (the reference's cv::Mat of SIFT rows; integer-valued, checked "
+                                       "and packed to u8 on the device)" if args.desc_dtype == "f32" else "u8"),
+                   "io": args.io,
+                   "timed": (f"K frame pairs, each from host memory to host memory: descriptors + keypoints "
+                             f"staged (pinned, H2D{', device integer check + u8 pack' if args.desc_dtype == 'f32' else ''}), "
+                             f"match -> NNDR -> compaction -> DLT -> compaction, matches + inlier points D2H; "
+                             f"{nf} contexts (HIP streams) in flight" if host_io else
+                             f"K frame pairs through match -> NNDR -> compaction -> DLT -> compaction on "
+                             f"HBM-resident inputs, {nf} contexts (HIP streams) in flight, every pair's counts read "
+                             f"back (page-locked) before its context takes the next") +
+                            "; synchronous_ms_per_step: one resident pair at a time"},
         "roofline": {"kernel": "match stage (row constants + knn2_i8_kernel + part merge + NNDR), HIP events",
                      "bound": "mfma", "compute": "int8 MFMA (v_mfma_i32_32x32x32_i8) + VALU top-2 epilogue",
                      "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TOP/s", "frac": achieved / INT8_PEAK_TOPS,

@@ -121,6 +121,11 @@ typedef struct fm3d_settings {
        ORC_LM_TREE | ORC_LM_GRAM mode, but the normals leave the reference's by more than 1e-4 on a
        share of the points, profiles/r05_full_parity.json) */
     int lmReduction;
+    /* The DLT's null-vector solver (not a reference key; Fm3d.dltSolver in the settings file):
+       0 = OpenCV 2.4's cvTriangulatePoints -- the 6 x 4 system and JacobiSVD, include/fm3d_cvsvd.h --
+       the default, the parity contract; 1 = the 4-row system and a round-robin Jacobi of rounds 1-5
+       (opt-in; its points leave OpenCV's in the last bits) */
+    int dltSolver;
 } fm3d_settings;
 
 #define FM3D_FEAT_SURF 0
@@ -450,7 +455,13 @@ int fm3d_compute(fm3d_ctx *ctx, const uint8_t *img, int width, int height, const
                  fm3d_keypoint *kout, int32_t *kept, int *nOut, void *desc);
 
 /* ---------------- the whole hot path, device resident ---------------- */
-/* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding). */
+/* Stage inputs in HBM (H2D once).  queryOffset is added to queryIdx (sharding).
+   type FM3D_DESC_F32 (the float cv::Mat rows knnMatch receives, descriptorsmatcher.cpp:114-117): the
+   rows go to the device as they are and a kernel checks them; rows that hold integers in [0, 255]
+   (SIFT) are packed to u8 on the device and take the exact u8 matcher (same ranking and distances),
+   others the float matchers.  This choice costs the call one wait for its own copies.
+   img1 = img2 = NULL: no images (C2's match + DLT needs none; the context keeps earlier ones, and
+   the full path fails without any). */
 int fm3d_pipeline_upload(fm3d_ctx *ctx, const void *descA, int nA, const void *descB, int nB, int dim, int type,
                          const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, const uint8_t *img1,
                          const uint8_t *img2, int width, int height, int queryOffset);
@@ -517,7 +528,12 @@ int fm3d_records_download(fm3d_ctx *ctx, const fm3d_record *recordsDev, int n, f
    (ncclCommInitAll, ncclAllGather, queued behind each device's records); the host merge returns the
    records in query order, byte-identical to fm3d_pipeline_run of the whole frame pair.  devices may
    be NULL (0..ndev-1); FM3D_ERR_INVALID when a device index is not visible (fewer GPUs than asked
-   for) or repeats; FM3D_ERR_UNSUPPORTED when RCCL (librccl.so.1) cannot be loaded. */
+   for) or repeats; FM3D_ERR_UNSUPPORTED when RCCL (librccl.so.1) cannot be loaded.
+   Memory pre-flight: fm3d_mgpu_create checks every device's free memory (hipMemGetInfo) for the LM
+   slabs of its four context sets, and the first upload / submit of a larger frame pair for the
+   per-pair buffers and exchange slots, before anything grows: too little is FM3D_ERR_NOMEM with the
+   shortfall in the error text (fm3d_mgpu_last_error(NULL) after a failed create), never an
+   allocation failure in the middle of a run.  The merge is linear (blocks in order, no sort). */
 typedef struct fm3d_mgpu fm3d_mgpu;
 /* the GPUs visible to this process (hipGetDeviceCount; 0 when HIP finds none): what a multi-GPU
    host checks before fm3d_mgpu_create, without loading another runtime (bench.py --gpus N) */

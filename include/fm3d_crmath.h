@@ -275,4 +275,40 @@ FM3D_HD double fm3d_exp_cr(double x)
     return ldexp(fm3d_dd_round(e), (int)k);
 }
 
+/* hypot(x, y), the function OpenCV 2.4's JacobiSVDImpl_ forms each rotation with
+   (include/fm3d_cvsvd.h).  x^2 + y^2 in double-double (exact products, one double-double add:
+   relative error below 2^-104), r = sqrt of its high part (correctly rounded), one Newton correction
+   (s - r^2) / 2r from the double-double residual, rounded once: correctly rounded unless the exact
+   value lies within ~2^-50 ulp of a rounding boundary (tests/test_crmath.py: every case of its
+   random and hard-case sets equals mpmath's).  |y| <= 2^-60 |x| returns |x|, which is the correctly
+   rounded value there. */
+FM3D_HD double fm3d_hypot_cr(double x, double y)
+{
+    double ax = fabs(x), ay = fabs(y), t, r, c;
+    int e = 0;
+    fm3d_dd s, d;
+    if (ax == INFINITY || ay == INFINITY) return INFINITY;
+    if (ax != ax || ay != ay) return ax + ay;
+    if (ax < ay) {
+        t = ax;
+        ax = ay;
+        ay = t;
+    }
+    if (ay <= ax * 0x1p-60) return ax;
+    if (ax > 0x1p+500) {
+        ax *= 0x1p-600;
+        ay *= 0x1p-600;
+        e = 600;
+    } else if (ax < 0x1p-500) {
+        ax *= 0x1p+600;
+        ay *= 0x1p+600;
+        e = -600;
+    }
+    s = fm3d_dd_add(fm3d_two_prod(ax, ax), fm3d_two_prod(ay, ay));
+    r = sqrt(s.hi);
+    d = fm3d_dd_sub(s, fm3d_two_prod(r, r));
+    c = d.hi / (2.0 * r);
+    return e ? ldexp(r + c, e) : r + c;
+}
+
 #endif /* FM3D_CRMATH_H */

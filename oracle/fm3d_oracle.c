@@ -190,7 +190,239 @@ ORC_API void orc_rodrigues_v2m(const double r[3], double R[9])
     }
 }
 
-/* 3x3 inverse transpose via adjugate (for the polar iteration below) */
+/* ------------------------------------------------------------------ */
+/* OpenCV 2.4's SVD (core/src/lapack.cpp), where the hot path calls it  */
+/* ------------------------------------------------------------------ */
+/* cvTriangulatePoints' null vector (singlecameratriangulator.cpp:186) and cvRodrigues2's
+   orthonormalisation of R (decomposeTransformation, tools.cpp:110) both run cvSVD -> cv::SVD::compute
+   -> _SVDcompute -> JacobiSVD(double) = JacobiSVDImpl_<double>(..., minval = DBL_MIN,
+   eps = 10 DBL_EPSILON), restated below from OpenCV 2.4.9's published source.
+
+   Geometry switches (measurement only: tools/dlt_parity.py):
+     ORC_GEOM_DLT_LEGACY   the DLT of rounds 1-5: the 4-row system (no x P.row1 - y P.row0 rows), a
+                           one-sided Jacobi in round-robin pair order with its own rotation formulas
+                           and a 1e-15 threshold;
+     ORC_GEOM_POLAR_NEWTON the polar factor of rounds 1-5: three Newton steps X <- (X + X^-T) / 2;
+     ORC_GEOM_SVD_LANES    JacobiSVDImpl_'s dot product and rotated norms in VBLAS<double>'s two SSE2
+                           lanes (VBLAS::dot / givensx, the accumulation order of the OpenCV releases
+                           that kept W in _Tp) instead of 2.4.9's scalar double loops;
+     ORC_GEOM_LIBM_HYPOT   libm's hypot for the rotation instead of fm3d_hypot_cr (the product's). */
+enum { ORC_GEOM_DLT_LEGACY = 1, ORC_GEOM_POLAR_NEWTON = 2, ORC_GEOM_SVD_LANES = 4, ORC_GEOM_LIBM_HYPOT = 8 };
+static int orc_geom_mode = 0;
+ORC_API void orc_set_geometry_mode(int mode) { orc_geom_mode = mode; }
+ORC_API int orc_get_geometry_mode(void) { return orc_geom_mode; }
+
+#define ORC_SVD_MAXN 8
+#define ORC_SVD_MAXM 8
+
+/* cv::RNG (core.hpp): state = (uint64)(unsigned)state * CV_RNG_COEFF + (unsigned)(state >> 32) */
+static unsigned orc_cv_rng_next(uint64_t *state)
+{
+    *state = (uint64_t)(unsigned)*state * 4164903690U + (unsigned)(*state >> 32);
+    return (unsigned)*state;
+}
+
+/* VBLAS<double>::dot under SSE2: lanes (k, k+1) and (k+2, k+3) per step of 4, lane sums added
+   pairwise, the low lane first; returns the elements consumed (0 when n < 4) */
+static int orc_vblas_dot(const double *a, const double *b, int n, double *result)
+{
+    double s0[2] = {0, 0}, s1[2] = {0, 0};
+    int k = 0;
+    if (n < 4) return 0;
+    for (; k <= n - 4; k += 4) {
+        s0[0] = s0[0] + a[k] * b[k];
+        s0[1] = s0[1] + a[k + 1] * b[k + 1];
+        s1[0] = s1[0] + a[k + 2] * b[k + 2];
+        s1[1] = s1[1] + a[k + 3] * b[k + 3];
+    }
+    s0[0] = s0[0] + s1[0];
+    s0[1] = s0[1] + s1[1];
+    *result = s0[0] + s0[1];
+    return k;
+}
+
+/* VBLAS<double>::givensx under SSE2: the rotation two lanes at a time, the squared norms of the
+   rotated rows per lane, the lanes added at the end */
+static int orc_vblas_givensx(double *a, double *b, int n, double c, double s, double *anorm, double *bnorm)
+{
+    double sa[2] = {0, 0}, sb[2] = {0, 0};
+    int k = 0, l;
+    for (; k <= n - 2; k += 2)
+        for (l = 0; l < 2; l++) {
+            double t0 = a[k + l] * c + b[k + l] * s;
+            double t1 = b[k + l] * c - a[k + l] * s;
+            a[k + l] = t0;
+            b[k + l] = t1;
+            sa[l] = sa[l] + t0 * t0;
+            sb[l] = sb[l] + t1 * t1;
+        }
+    *anorm = sa[0] + sa[1];
+    *bnorm = sb[0] + sb[1];
+    return k;
+}
+
+/* JacobiSVDImpl_<double>(At, astep, _W, Vt, vstep, m, n, n1, DBL_MIN, 10 DBL_EPSILON): At holds the n
+   columns of A as rows of m (strides in elements); on return its first n1 rows are the left singular
+   vectors, _W the singular values in descending order, Vt's rows the right singular vectors. */
+static void orc_cv_jacobi_svd(double *At, int astep, double *_W, double *Vt, int vstep, int m, int n, int n1)
+{
+    const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
+    const int lanes = (orc_geom_mode & ORC_GEOM_SVD_LANES) != 0;
+    double W[ORC_SVD_MAXN], c, s, sd;
+    int i, j, k, iter, max_iter = m > 30 ? m : 30;
+    uint64_t rng = 0x12345678;
+
+    for (i = 0; i < n; i++) {
+        for (k = 0, sd = 0; k < m; k++) {
+            double t = At[i * astep + k];
+            sd += t * t;
+        }
+        W[i] = sd;
+        if (Vt) {
+            for (k = 0; k < n; k++) Vt[i * vstep + k] = 0;
+            Vt[i * vstep + i] = 1;
+        }
+    }
+
+    for (iter = 0; iter < max_iter; iter++) {
+        int changed = 0;
+        for (i = 0; i < n - 1; i++)
+            for (j = i + 1; j < n; j++) {
+                double *Ai = At + i * astep, *Aj = At + j * astep;
+                double a = W[i], p = 0, b = W[j], beta, gamma;
+                k = lanes ? orc_vblas_dot(Ai, Aj, m, &p) : 0;
+                for (; k < m; k++) p += Ai[k] * Aj[k];
+                if (fabs(p) <= eps * sqrt(a * b)) continue;
+                p *= 2;
+                beta = a - b;
+                gamma = (orc_geom_mode & ORC_GEOM_LIBM_HYPOT) ? hypot(p, beta) : fm3d_hypot_cr(p, beta);
+                if (beta < 0) {
+                    double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                a = b = 0;
+                k = lanes ? orc_vblas_givensx(Ai, Aj, m, c, s, &a, &b) : 0;
+                for (; k < m; k++) {
+                    double t0 = c * Ai[k] + s * Aj[k];
+                    double t1 = -s * Ai[k] + c * Aj[k];
+                    Ai[k] = t0;
+                    Aj[k] = t1;
+                    a += t0 * t0;
+                    b += t1 * t1;
+                }
+                W[i] = a;
+                W[j] = b;
+                changed = 1;
+                if (Vt) {
+                    /* VBLAS<double>::givens (SSE2, two lanes: Vi c + Vj s, Vj c - Vi s) and the
+                       scalar tail give the scalar loop's bits: no FMA, and -(s Vi) + c Vj is
+                       c Vj - s Vi exactly */
+                    double *Vi = Vt + i * vstep, *Vj = Vt + j * vstep;
+                    for (k = 0; k < n; k++) {
+                        double t0 = c * Vi[k] + s * Vj[k];
+                        double t1 = -s * Vi[k] + c * Vj[k];
+                        Vi[k] = t0;
+                        Vj[k] = t1;
+                    }
+                }
+            }
+        if (!changed) break;
+    }
+
+    for (i = 0; i < n; i++) {
+        for (k = 0, sd = 0; k < m; k++) {
+            double t = At[i * astep + k];
+            sd += t * t;
+        }
+        W[i] = sqrt(sd);
+    }
+
+    for (i = 0; i < n - 1; i++) {
+        j = i;
+        for (k = i + 1; k < n; k++)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            double t = W[i];
+            W[i] = W[j];
+            W[j] = t;
+            if (Vt) {
+                for (k = 0; k < m; k++) {
+                    t = At[i * astep + k];
+                    At[i * astep + k] = At[j * astep + k];
+                    At[j * astep + k] = t;
+                }
+                for (k = 0; k < n; k++) {
+                    t = Vt[i * vstep + k];
+                    Vt[i * vstep + k] = Vt[j * vstep + k];
+                    Vt[j * vstep + k] = t;
+                }
+            }
+        }
+    }
+
+    for (i = 0; i < n; i++) _W[i] = W[i];
+    if (!Vt) return;
+
+    for (i = 0; i < n1; i++) {
+        sd = i < n ? W[i] : 0;
+        while (sd <= minval) {
+            /* a zero singular value: a random +-1/m vector, twice orthogonalised against the
+               previous left vectors and l1-normalised */
+            const double val0 = 1. / m;
+            for (k = 0; k < m; k++) At[i * astep + k] = (orc_cv_rng_next(&rng) & 256) != 0 ? val0 : -val0;
+            for (iter = 0; iter < 2; iter++)
+                for (j = 0; j < i; j++) {
+                    double asum = 0;
+                    sd = 0;
+                    for (k = 0; k < m; k++) sd += At[i * astep + k] * At[j * astep + k];
+                    for (k = 0; k < m; k++) {
+                        double t = At[i * astep + k] - sd * At[j * astep + k];
+                        At[i * astep + k] = t;
+                        asum += fabs(t);
+                    }
+                    asum = asum ? 1 / asum : 0;
+                    for (k = 0; k < m; k++) At[i * astep + k] *= asum;
+                }
+            sd = 0;
+            for (k = 0; k < m; k++) {
+                double t = At[i * astep + k];
+                sd += t * t;
+            }
+            sd = sqrt(sd);
+        }
+        s = 1 / sd;
+        for (k = 0; k < m; k++) At[i * astep + k] *= s;
+    }
+}
+
+/* cv::SVD::compute (_SVDcompute) of an m x n row-major double matrix with m >= n and no FULL_UV:
+   temp_a = A^T, JacobiSVD(temp_a, m, n, n1 = n); w (n), u (m x n, may be NULL) = temp_u^T,
+   vt (n x n) = temp_v */
+static void orc_cv_svd(const double *A, int m, int n, double *w, double *u, double *vt)
+{
+    double At[ORC_SVD_MAXN * ORC_SVD_MAXM];
+    int i, k;
+    for (i = 0; i < n; i++)
+        for (k = 0; k < m; k++) At[i * m + k] = A[k * n + i];
+    orc_cv_jacobi_svd(At, m, w, vt, n, m, n, n);
+    if (u)
+        for (k = 0; k < m; k++)
+            for (i = 0; i < n; i++) u[k * n + i] = At[i * m + k];
+}
+
+/* elementwise SVD entry for the tests (tests/test_cvsvd.py): A (m x n, m >= n, n, m <= 8) -> w, u, vt */
+ORC_API int orc_cv_svd_eval(const double *A, int m, int n, double *w, double *u, double *vt)
+{
+    if (m < n || n < 1 || m > ORC_SVD_MAXM || n > ORC_SVD_MAXN) return -1;
+    orc_cv_svd(A, m, n, w, u, vt);
+    return 0;
+}
+
+/* 3x3 inverse transpose via adjugate (the legacy Newton polar iteration, ORC_GEOM_POLAR_NEWTON) */
 static void orc_inv_t3(const double A[9], double out[9])
 {
     double c00 = A[4] * A[8] - A[5] * A[7];
@@ -210,27 +442,48 @@ static void orc_inv_t3(const double A[9], double out[9])
     out[6] = c20 * id; out[7] = c21 * id; out[8] = c22 * id;
 }
 
-/* cvRodrigues2 matrix -> vector.  OpenCV first replaces R by U*V^T of its SVD
-   (nearest orthonormal matrix); we compute the same polar factor with three
-   Newton steps X <- (X + X^-T)/2 (deterministic; equal to the SVD route within
-   a few ulp for the near-orthonormal inputs this path sees). */
-ORC_API void orc_rodrigues_m2v(const double Rin[9], double r[3])
+/* cvRodrigues2's orthonormalisation of a 3x3 R (OpenCV 2.4 calib3d/src/calibration.cpp):
+   cvSVD(R, W, U, V, CV_SVD_MODIFY_A + CV_SVD_U_T + CV_SVD_V_T), then
+   cvGEMM(U, V, 1, 0, 0, R, CV_GEMM_A_T) = U V^T, which takes GEMMSingleMul's generic loop
+   (flags != 0): s = 0; s += U(i,k) Vt(k,j) for k = 0..2; s * alpha */
+ORC_API void orc_cv_polar3(const double R[9], double Rp[9])
 {
-    double R[9], Y[9];
-    double rx, ry, rz, s, c, theta;
-    int it, k;
-    memcpy(R, Rin, sizeof(R));
-    for (it = 0; it < 3; it++) {
-        orc_inv_t3(R, Y);
-        for (k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
+    int i, j, k;
+    if (orc_geom_mode & ORC_GEOM_POLAR_NEWTON) {
+        double Y[9];
+        memcpy(Rp, R, 9 * sizeof(double));
+        for (i = 0; i < 3; i++) {
+            orc_inv_t3(Rp, Y);
+            for (k = 0; k < 9; k++) Rp[k] = 0.5 * (Rp[k] + Y[k]);
+        }
+        return;
     }
+    {
+        double W[3], U[9], Vt[9];
+        orc_cv_svd(R, 3, 3, W, U, Vt);
+        for (i = 0; i < 3; i++)
+            for (j = 0; j < 3; j++) {
+                double s = 0;
+                for (k = 0; k < 3; k++) s += U[i * 3 + k] * Vt[k * 3 + j];
+                Rp[i * 3 + j] = s * 1.;
+            }
+    }
+}
+
+/* cvRodrigues2 matrix -> vector (OpenCV 2.4): R replaced by its polar factor U V^T (above), then
+   the rotation vector from its skew part and trace; acos from libm, or fm3d_acos (cr: 1) */
+static void orc_rodrigues_m2v_acos(const double Rin[9], double r[3], int detacos)
+{
+    double R[9];
+    double rx, ry, rz, s, c, theta;
+    orc_cv_polar3(Rin, R);
     rx = R[7] - R[5];
     ry = R[2] - R[6];
     rz = R[3] - R[1];
     s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
-    theta = acos(c);
+    theta = detacos ? fm3d_acos(c) : acos(c);
     if (s < 1e-5) {
         double t;
         if (c > 0)
@@ -252,6 +505,11 @@ ORC_API void orc_rodrigues_m2v(const double Rin[9], double r[3])
         rx *= vth; ry *= vth; rz *= vth;
     }
     r[0] = rx; r[1] = ry; r[2] = rz;
+}
+
+ORC_API void orc_rodrigues_m2v(const double Rin[9], double r[3])
+{
+    orc_rodrigues_m2v_acos(Rin, r, 0);
 }
 
 /* composeTransformation, tools.cpp:87-99 */
@@ -342,7 +600,8 @@ ORC_API void orc_camera2_from_g12(const double g12[16], double R2[9], double t2[
 /* ------------------------------------------------------------------ */
 /* DLT triangulation (a4, a5)                                          */
 /* ------------------------------------------------------------------ */
-/* one Jacobi rotation of columns (p, q) of A (and V) unless they are orthogonal to 1e-15 */
+/* ORC_GEOM_DLT_LEGACY (rounds 1-5): one Jacobi rotation of columns (p, q) of the 4x4 A (and V)
+   unless they are orthogonal to 1e-15 */
 static int orc_jacobi_pair(double A[16], double V[16], int p, int q)
 {
     double alpha = 0, beta = 0, gamma = 0;
@@ -372,13 +631,9 @@ static int orc_jacobi_pair(double A[16], double V[16], int p, int q)
     return 0;
 }
 
-/* Null vector of the 4x4 DLT system: one-sided (Hestenes) Jacobi SVD in the round-robin
-   (tournament) pair order -- (0,1)+(2,3), (0,2)+(1,3), (0,3)+(1,2): the two rotations of a step
-   touch disjoint columns, so they are independent and the GPU runs them side by side (half the
-   dependent chain of the cyclic order, round 5) -- up to 30 sweeps.  OpenCV's cvSVD (JacobiSVD) is
-   not reproducible bit for bit; the null vector agrees with numpy.linalg.svd to ~1e-12
-   (tests/golden). */
-static void orc_dlt_nullvec(double A[16], double v[4])
+/* ORC_GEOM_DLT_LEGACY: null vector of the 4-row system by the round-robin one-sided Jacobi
+   ((0,1)+(2,3), (0,2)+(1,3), (0,3)+(1,2), up to 30 sweeps), the smallest column norm's V column */
+static void orc_dlt_nullvec_legacy(double A[16], double v[4])
 {
     static const int PQ[6][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {0, 3}, {1, 2}};
     double V[16];
@@ -403,25 +658,46 @@ static void orc_dlt_nullvec(double A[16], double v[4])
     for (i = 0; i < 4; i++) v[i] = V[i * 4 + best];
 }
 
-/* cv::triangulatePoints (OpenCV 2.4 cvTriangulatePoints) for one pair of
-   undistorted points, P1 = [I|0], P2 = first 3 rows of g12
-   (singlecameratriangulator.cpp:179-186). Returns homogeneous X (4). */
+/* cv::triangulatePoints (OpenCV 2.4 cvTriangulatePoints, calib3d/src/triangulate.cpp) for one pair of
+   undistorted points, P1 = [I|0], P2 = the first 3 rows of g12 (singlecameratriangulator.cpp:179-186):
+   the 6 x 4 matrA, per view j rows 3j..3j+2 = x P.row2 - P.row0, y P.row2 - P.row1,
+   x P.row1 - y P.row0; cvSVD(matrA, matrW, 0, matrV, CV_SVD_V_T); X = matrV's row 3 (the right singular
+   vector of the smallest singular value after JacobiSVD's descending sort).  Returns homogeneous X. */
 ORC_API void orc_triangulate1(const double g12[16], const double u1[2], const double u2[2], double X[4])
 {
-    double A[16], P1[12], P2[12];
+    double P1[12], P2[12];
     int j, k;
     for (k = 0; k < 12; k++) P1[k] = (k == 0 || k == 5 || k == 10) ? 1. : 0.;
     for (k = 0; k < 12; k++) P2[k] = g12[k];
-    for (j = 0; j < 2; j++) {
-        const double *P = j == 0 ? P1 : P2;
-        double x = j == 0 ? u1[0] : u2[0];
-        double y = j == 0 ? u1[1] : u2[1];
-        for (k = 0; k < 4; k++) {
-            A[(j * 2 + 0) * 4 + k] = x * P[8 + k] - P[0 + k];
-            A[(j * 2 + 1) * 4 + k] = y * P[8 + k] - P[4 + k];
+    if (orc_geom_mode & ORC_GEOM_DLT_LEGACY) {
+        double A[16];
+        for (j = 0; j < 2; j++) {
+            const double *P = j == 0 ? P1 : P2;
+            double x = j == 0 ? u1[0] : u2[0];
+            double y = j == 0 ? u1[1] : u2[1];
+            for (k = 0; k < 4; k++) {
+                A[(j * 2 + 0) * 4 + k] = x * P[8 + k] - P[0 + k];
+                A[(j * 2 + 1) * 4 + k] = y * P[8 + k] - P[4 + k];
+            }
         }
+        orc_dlt_nullvec_legacy(A, X);
+        return;
     }
-    orc_dlt_nullvec(A, X);
+    {
+        double A[24], W[4], Vt[16];
+        for (j = 0; j < 2; j++) {
+            const double *P = j == 0 ? P1 : P2;
+            double x = j == 0 ? u1[0] : u2[0];
+            double y = j == 0 ? u1[1] : u2[1];
+            for (k = 0; k < 4; k++) {
+                A[(j * 3 + 0) * 4 + k] = x * P[8 + k] - P[0 + k];
+                A[(j * 3 + 1) * 4 + k] = y * P[8 + k] - P[4 + k];
+                A[(j * 3 + 2) * 4 + k] = x * P[4 + k] - y * P[0 + k];
+            }
+        }
+        orc_cv_svd(A, 6, 4, W, NULL, Vt);
+        for (k = 0; k < 4; k++) X[k] = Vt[3 * 4 + k];
+    }
 }
 
 /* setKeypoints (:145-171) + triangulate (:173-230).
@@ -736,13 +1012,15 @@ static double orc_fexp(int mode, double x)
     return (mode & ORC_DET_1ULP) ? fm3d_exp(x) : fm3d_exp_cr(x);
 }
 /* the four transcendentals elementwise in a mode (tests/test_crmath.py pins the correctly rounded
-   ones against mpmath): fn 0 sin(x), 1 cos(x), 2 atan2(x, y), 3 exp(x) */
+   ones against mpmath): fn 0 sin(x), 1 cos(x), 2 atan2(x, y), 3 exp(x), 4 hypot(x, y) (DETMATH:
+   fm3d_hypot_cr, the SVD's; else libm) */
 ORC_API void orc_math_eval(int fn, int mode, const double *x, const double *y, int n, double *out)
 {
     int i;
     for (i = 0; i < n; i++)
         out[i] = fn == 0 ? orc_fsin(mode, x[i]) : fn == 1 ? orc_fcos(mode, x[i])
-               : fn == 2 ? orc_fatan2(mode, x[i], y[i]) : orc_fexp(mode, x[i]);
+               : fn == 2 ? orc_fatan2(mode, x[i], y[i]) : fn == 3 ? orc_fexp(mode, x[i])
+               : (mode & ORC_LM_DETMATH) ? fm3d_hypot_cr(x[i], y[i]) : hypot(x[i], y[i]);
 }
 
 static void orc_sph2car(int mode, double phi, double theta, double n[3])
@@ -1785,11 +2063,12 @@ ORC_API int orc_circular_neighborhoods(const double *points, const double *norma
 }
 
 /* cvRodrigues2 round trip of decomposeTransformation + cvProjectPoints2, with libm (mode 0) or
-   the deterministic transcendentals (mode ORC_LM_DETMATH; acos(c) = atan2(sqrt((1-c)(1+c)), c)). */
+   the deterministic transcendentals (mode ORC_LM_DETMATH; acos(c) = atan2(sqrt((1-c)(1+c)), c)).
+   Both orthonormalise R by OpenCV's SVD (orc_cv_polar3). */
 static void orc_frame_camera(const double F[16], int mode, double R2[9], double t2[3])
 {
-    double R[9], Y[9], r[3], rx, ry, rz, s, c, theta;
-    int it, k;
+    double R[9], r[3], rx, ry, rz, theta;
+    int k;
     R[0] = F[0]; R[1] = F[1]; R[2] = F[2];
     R[3] = F[4]; R[4] = F[5]; R[5] = F[6];
     R[6] = F[8]; R[7] = F[9]; R[8] = F[10];
@@ -1799,38 +2078,8 @@ static void orc_frame_camera(const double F[16], int mode, double R2[9], double 
         orc_rodrigues_v2m(r, R2);
         return;
     }
-    /* orc_rodrigues_m2v with fm3d_acos */
-    for (it = 0; it < 3; it++) {
-        orc_inv_t3(R, Y);
-        for (k = 0; k < 9; k++) R[k] = 0.5 * (R[k] + Y[k]);
-    }
-    rx = R[7] - R[5];
-    ry = R[2] - R[6];
-    rz = R[3] - R[1];
-    s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
-    c = (R[0] + R[4] + R[8] - 1) * 0.5;
-    c = c > 1. ? 1. : c < -1. ? -1. : c;
-    theta = fm3d_acos(c);
-    if (s < 1e-5) {
-        double t;
-        if (c > 0)
-            rx = ry = rz = 0;
-        else {
-            t = (R[0] + 1) * 0.5;
-            rx = sqrt(t > 0. ? t : 0.);
-            t = (R[4] + 1) * 0.5;
-            ry = sqrt(t > 0. ? t : 0.) * (R[1] < 0 ? -1. : 1.);
-            t = (R[8] + 1) * 0.5;
-            rz = sqrt(t > 0. ? t : 0.) * (R[2] < 0 ? -1. : 1.);
-            if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
-            theta /= sqrt(rx * rx + ry * ry + rz * rz);
-            rx *= theta; ry *= theta; rz *= theta;
-        }
-    } else {
-        double vth = 1 / (2 * s);
-        vth *= theta;
-        rx *= vth; ry *= vth; rz *= vth;
-    }
+    orc_rodrigues_m2v_acos(R, r, 1);
+    rx = r[0]; ry = r[1]; rz = r[2];
     /* orc_rodrigues_v2m with fm3d_cos / fm3d_sin */
     theta = sqrt(rx * rx + ry * ry + rz * rz);
     if (theta < DBL_EPSILON) {

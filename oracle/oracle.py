@@ -31,10 +31,10 @@ def tree_stats(reset=False):
     return out
 
 def math_eval(fn, x, y=None, mode=DETMATH):
-    """orc_math_eval: fn "sin", "cos", "exp" of x, or "atan2" of (x, y) = atan2(x, y), elementwise,
+    """orc_math_eval: fn "sin", "cos", "exp" of x, or "atan2" / "hypot" of (x, y), elementwise,
     in an oracle mode (DETMATH: include/fm3d_crmath.h's correctly rounded functions; DETMATH |
     DET_1ULP: fm3d_detmath.h's; 0: libm)."""
-    f = {"sin": 0, "cos": 1, "atan2": 2, "exp": 3}[fn]
+    f = {"sin": 0, "cos": 1, "atan2": 2, "exp": 3, "hypot": 4}[fn]
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = x if y is None else np.ascontiguousarray(y, dtype=np.float64)
     out = np.empty_like(x)
@@ -89,6 +89,53 @@ def camera2_from_g12(g12):
     t2 = np.zeros(3)
     lib().orc_camera2_from_g12(_p(_f64(np.asarray(g12).ravel())), _p(R2), _p(t2))
     return R2.reshape(3, 3), t2
+
+
+# orc_set_geometry_mode switches (fm3d_oracle.c ORC_GEOM_*; measurement only, tools/dlt_parity.py):
+# the rounds 1-5 DLT (4-row system, round-robin Jacobi), the rounds 1-5 Newton polar factor,
+# JacobiSVDImpl_'s SSE2 two-lane dot / givensx accumulation, libm's hypot in the SVD rotation
+GEOM_DLT_LEGACY, GEOM_POLAR_NEWTON, GEOM_SVD_LANES, GEOM_LIBM_HYPOT = 1, 2, 4, 8
+
+
+def set_geometry_mode(mode: int) -> int:
+    """set the oracle's geometry mode (0 = OpenCV 2.4's cvSVD everywhere, the product contract);
+    returns the previous mode"""
+    prev = int(lib().orc_get_geometry_mode())
+    lib().orc_set_geometry_mode(ctypes.c_int(mode))
+    return prev
+
+
+class geometry_mode:
+    """with orc.geometry_mode(orc.GEOM_DLT_LEGACY): ... -- restores the previous mode"""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = set_geometry_mode(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_geometry_mode(self.prev)
+
+
+def cv_svd(A):
+    """cv::SVD::compute of an m x n (m >= n, both <= 8) double matrix as OpenCV 2.4's JacobiSVD does it:
+    w (n, descending), u (m x n), vt (n x n)"""
+    A = _f64(A)
+    m, n = A.shape
+    w, u, vt = np.zeros(n), np.zeros((m, n)), np.zeros((n, n))
+    rc = lib().orc_cv_svd_eval(_p(A), ctypes.c_int(m), ctypes.c_int(n), _p(w), _p(u), _p(vt))
+    if rc != 0:
+        raise ValueError("orc_cv_svd_eval: m >= n, n, m <= 8")
+    return w, u, vt
+
+
+def cv_polar3(R):
+    """cvRodrigues2's orthonormalisation U V^T of a 3 x 3 matrix"""
+    out = np.zeros(9)
+    lib().orc_cv_polar3(_p(_f64(np.asarray(R).ravel())), _p(out))
+    return out.reshape(3, 3)
 
 
 def rodrigues_v2m(r):

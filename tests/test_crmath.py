@@ -89,3 +89,28 @@ def test_libm_differs_somewhere(orc):
     x = np.random.default_rng(4).uniform(-4, 4, 20000)
     d = sum(int((orc.math_eval(f, x, mode=orc.STRICT) != orc.math_eval(f, x)).sum()) for f in ("sin", "cos"))
     print(f"libm sin/cos differ from the correctly rounded value on {d} of {2 * len(x)} inputs")
+
+
+def test_hypot_correctly_rounded(orc):
+    """fm3d_hypot_cr -- the rotation's hypot in OpenCV's JacobiSVDImpl_ (include/fm3d_cvsvd.h, the DLT
+    and the polar factor) -- is mpmath's sqrt(x^2 + y^2) rounded to nearest, over random pairs of
+    mixed magnitudes (the DLT's p and beta span many decades), equal pairs, zeros, the 2^-60 cut,
+    scaled extremes and non-finite values; glibc's hypot here is not correctly rounded everywhere."""
+    rng = np.random.default_rng(6)
+    n = 6000
+    x = rng.normal(size=n) * 10.0 ** rng.uniform(-12, 12, n)
+    y = rng.normal(size=n) * 10.0 ** rng.uniform(-12, 12, n)
+    hard = np.array([[3.0, 4.0], [1.0, 1.0], [0.0, 0.0], [-0.0, 5.0], [1.0, 2.0 ** -61], [1.0, 2.0 ** -59],
+                     [1e300, 1e300], [1e-300, 3e-300], [5e-324, 5e-324], [1.5e308, 1.5e308], [2.0 ** 500, 1.0]])
+    x = np.concatenate([x, hard[:, 0]])
+    y = np.concatenate([y, hard[:, 1]])
+    got = orc.math_eval("hypot", x, y)
+    with mpmath.workprec(300):
+        ref = np.array([float(mpmath.sqrt(mpmath.mpf(a) ** 2 + mpmath.mpf(b) ** 2)) for a, b in zip(x, y)])
+    bad = _mismatch(got, ref)
+    assert bad.size == 0, [(x[i], y[i], got[i], ref[i]) for i in bad[:5]]
+    inf, nan = float("inf"), float("nan")
+    sp = orc.math_eval("hypot", np.array([inf, nan, -inf, nan]), np.array([nan, inf, 1.0, 1.0]))
+    assert sp[0] == inf and sp[1] == inf and sp[2] == inf and np.isnan(sp[3])
+    libm = orc.math_eval("hypot", x[:n], y[:n], mode=orc.STRICT)
+    print(f"libm hypot differs from the correctly rounded value on {int((libm != got[:n]).sum())} of {n} pairs")

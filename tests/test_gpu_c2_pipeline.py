@@ -188,3 +188,99 @@ def test_pipeline_ncc_bitwise(fm3d, orc, synth):
                                     bound=(s.boundWidth, s.boundHeight), zmax=s.zThresholdMax)
     assert np.array_equal(sc[sel], rs) and np.array_equal(b[sel], rb) and np.array_equal(nb[sel], rn, equal_nan=True)
     assert (b >= 0).mean() > 0.3
+
+
+def test_pipeline_float_sift_rows_packed_on_device(fm3d, orc, synth):
+    """VERDICT r05 item 2: SIFT rows as the reference hands them to knnMatch (float cv::Mat,
+    descriptorsmatcher.cpp:114-117).  fm3d_pipeline_submit with float32 rows: the device checks them
+    (integers in [0, 255]) and packs them to u8, so the survivor records equal the u8 rows' byte for
+    byte and the oracle's matches; rows with one non-integer element take the float kernels and
+    equal the oracle's float (FLANN-order) matching; upload without images runs C2's path."""
+    pair = synth.make_frame_pair(4000, seed=31)
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon = 0.55
+    s.pixelsRay, s.pyramids = 12, 2
+    ctx = fm3d.Context(s)
+    try:
+        fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
+        pipe = fm3d.Pipeline(ctx)
+        out = {}
+        for kind in ("u8", "f32"):
+            d1 = pair.desc1 if kind == "u8" else pair.desc1.astype(np.float32)
+            d2 = pair.desc2 if kind == "u8" else pair.desc2.astype(np.float32)
+            pipe.submit(d1, d2, pair.kp1, pair.kp2, pair.img1, pair.img2)
+            rec, st = pipe.wait()
+            out[kind] = (rec.copy(), st)
+        assert len(out["u8"][0]) > 100 and out["u8"][0].tobytes() == out["f32"][0].tobytes()
+        q, t, dist = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+        assert out["f32"][1]["matches"] == len(q)
+        # C2's front half from float rows, staged without images
+        pipe.upload(pair.desc1.astype(np.float32), pair.desc2.astype(np.float32), pair.kp1, pair.kp2, None, None)
+        P, st = pipe.run_dlt()
+        m, pts, _ = pipe.dlt_results(st["matches"], st["inliers"])
+        opts, _ = orc.triangulate(pair.cam, pair.g12, s.zThresholdMin, s.zThresholdMax, pair.kp1, pair.kp2, q, t)
+        assert np.array_equal(m["queryIdx"], q) and np.array_equal(m["trainIdx"], t)
+        assert np.array_equal(m["distance"], dist) and np.array_equal(pts, opts)
+        # one element off the integers: the float path (FLANN's L2 order), against the oracle's F32 scan
+        f1 = pair.desc1.astype(np.float32)
+        f2 = pair.desc2.astype(np.float32)
+        f2[17, 5] += 0.25
+        pipe.upload(f1, f2, pair.kp1, pair.kp2, None, None)
+        P, st = pipe.run_dlt()
+        m, pts, _ = pipe.dlt_results(st["matches"], st["inliers"])
+        qf, tf, df = orc.match_nndr(f1, f2, orc.F32, 0.55, oracle_threads())
+        assert np.array_equal(m["queryIdx"], qf) and np.array_equal(m["trainIdx"], tf)
+        assert np.array_equal(m["distance"], df)
+    finally:
+        ctx.close()
+
+
+def test_pipeline_no_images_full_path_fails_cleanly(fm3d, synth):
+    """a context staged without images runs C2's front half; the full path refuses (no pyramids)"""
+    pair = synth.make_frame_pair(1500, seed=32)
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    ctx = fm3d.Context(s)
+    try:
+        fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(pair.desc1, pair.desc2, pair.kp1, pair.kp2, None, None)
+        P, _ = pipe.run_dlt()
+        assert P > 0
+        with pytest.raises(fm3d.Fm3dError):
+            pipe.run()
+    finally:
+        ctx.close()
+
+
+def test_lookback_epoch_wrap_and_counter_reset(fm3d, orc, synth, monkeypatch):
+    """the fused compactions' look-back.  Each launch takes block indices
+    0 .. n-1 from a counter its last block resets (no host-side base), and the 32-bit launch tag
+    skips 0 (the zeroed status words' "not yet") when it wraps.  A context started 3 tags before the
+    wrap runs C2's front half eight times across it, alternating two pairs: every result equals the
+    oracle's."""
+    pairs = [synth.make_frame_pair(3000, seed=41), synth.make_frame_pair(9000, seed=42)]
+    s = fm3d.Settings.default()
+    s.set_camera(pairs[0].cam)
+    s.nndrEpsilon = 0.55
+    ref = []
+    for fp in pairs:
+        q, t, _ = orc.match_nndr(fp.desc1, fp.desc2, orc.U8, 0.55, oracle_threads())
+        pts, _ = orc.triangulate(fp.cam, fp.g12, s.zThresholdMin, s.zThresholdMax, fp.kp1, fp.kp2, q, t)
+        ref.append((q, pts))
+    monkeypatch.setenv("FM3D_DEBUG_LB_EPOCH", str(2 ** 32 - 3))
+    ctx = fm3d.Context(s)
+    monkeypatch.delenv("FM3D_DEBUG_LB_EPOCH")
+    try:
+        fm3d.SingleCameraTriangulator(ctx).set_g12(pairs[0].g12)
+        pipe = fm3d.Pipeline(ctx)
+        for i in range(8):  # two look-back launches per step: the tag wraps in the second step
+            fp = pairs[i % 2]
+            pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, None, None)
+            P, st = pipe.run_dlt()
+            m, pts, _ = pipe.dlt_results(st["matches"], st["inliers"])
+            q, opts = ref[i % 2]
+            assert np.array_equal(m["queryIdx"], q) and np.array_equal(pts, opts), i
+    finally:
+        ctx.close()

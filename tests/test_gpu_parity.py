@@ -213,6 +213,26 @@ def test_triangulate_bitwise(fm3d, orc, ctx, pair):
     assert 0 < len(pts) <= len(m)
 
 
+def test_triangulate_legacy_solver_bitwise(fm3d, orc, pair):
+    """dltSolver = 1 (opt-in): the 4-row system and round-robin Jacobi of rounds 1-5, bit for bit the
+    oracle's GEOM_DLT_LEGACY mode; the default (cvTriangulatePoints' 6 x 4 JacobiSVD) differs from it"""
+    c = fm3d.Context(_settings(fm3d, pair.cam, pixelsRay=16, dltSolver=1))
+    try:
+        dm = fm3d.DescriptorsMatcher(c)
+        m = dm.compareWithNNDR(0.55, pair.desc1, pair.desc2)
+        sct = fm3d.SingleCameraTriangulator(c)
+        sct.set_g12(pair.g12)
+        sct.setKeypoints(pair.kp1, pair.kp2, m)
+        pts, mask = sct.triangulate()
+    finally:
+        c.close()
+    with orc.geometry_mode(orc.GEOM_DLT_LEGACY):
+        pto, masko = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, m["queryIdx"], m["trainIdx"])
+    assert np.array_equal(mask, masko) and np.array_equal(pts, pto)
+    ptn, maskn = orc.triangulate(pair.cam, pair.g12, 1.5, 2.4, pair.kp1, pair.kp2, m["queryIdx"], m["trainIdx"])
+    assert np.array_equal(maskn, mask) and not np.array_equal(ptn, pts)
+
+
 def test_pyramid_bitwise(fm3d, orc, ctx, pair):
     no = fm3d.NormalOptimizer(ctx)
     no.setImages(pair.img1, pair.img2)

@@ -62,12 +62,21 @@ def test_rodrigues_roundtrip(orc):
 
 
 def test_dlt_vs_numpy_svd(orc):
+    """cvTriangulatePoints' 6 x 4 system through the oracle's JacobiSVD against numpy.linalg.svd of the
+    same system; the legacy 4-row solver (GEOM_DLT_LEGACY, dltSolver 1) against numpy on its 4 rows"""
     g = load("dlt.npz")
     cam = Cam(g["cam"])
     pts, mask = orc.triangulate(cam, g["g12"], 1.5, 2.4, g["kp1"], g["kp2"], g["q"], g["t"])
     assert np.array_equal(mask, g["mask"])
     rel = np.abs(pts - g["pts"]) / np.maximum(1.0, np.abs(g["pts"]))
     assert rel.max() < 1e-9
+    with orc.geometry_mode(orc.GEOM_DLT_LEGACY):
+        pts4, mask4 = orc.triangulate(cam, g["g12"], 1.5, 2.4, g["kp1"], g["kp2"], g["q"], g["t"])
+    assert np.array_equal(mask4, g["mask4"])
+    assert (np.abs(pts4 - g["pts4"]) / np.maximum(1.0, np.abs(g["pts4"]))).max() < 1e-9
+    # the third row of each view (x P.row1 - y P.row0) reweights the least-squares problem: the two
+    # systems' points differ far beyond rounding wherever the keypoints are not exactly consistent
+    assert (np.abs(pts4 - pts) / np.maximum(1.0, np.abs(pts))).max() > 1e-7
 
 
 def test_pyrdown_vs_scipy(orc):

@@ -216,3 +216,34 @@ def test_merge_shares_cpp_on_fabricated_buffers(fm3d):
         fm3d.merge_shares([bad, bad[:0]], 100, 32)
     with pytest.raises(ValueError):
         shard.merge_gathered_shares(np.zeros((2, 3), dtype=np.uint8), np.zeros(2), 10)
+
+
+def _oracle_records(orc, fm3d, fp, rows, ray=8, levels=1):
+    """the oracle's survivor records (fm3d_record) of the query rows `rows` of fp against all of frame
+    B, with local query indices (position in rows)"""
+    q, t, d = orc.match_nndr(fp.desc1[rows], fp.desc2, orc.U8, 0.55, 8)
+    pts, mask = orc.triangulate(fp.cam, fp.g12, 1.5, 2.4, fp.kp1[rows], fp.kp2, q, t)
+    R2, t2 = orc.camera2_from_g12(fp.g12)
+    ref = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, levels, pts, ray, mode=orc.DETMATH, nthreads=8)
+    ok = ref["status"] == 0
+    rec = np.zeros(int(ok.sum()), dtype=fm3d.RECORD)
+    rec["queryIdx"] = q[mask][ok]
+    rec["trainIdx"] = t[mask][ok]
+    rec["distance"] = d[mask][ok]
+    rec["point"] = pts[ok]
+    rec["normal"] = ref["normals"][ok]
+    return rec
+
+
+def test_eight_shares_of_30k_queries_merge_to_the_whole_run(fm3d, orc, synth):
+    """a 30k-query frame pair split into 8 shares of 512-query blocks by
+    fm3d_share_queries (the C ABI's block-cyclic partition), each share's survivor records computed
+    alone (the oracle's path: knn + NNDR against all of frame B, DLT, LM), merged by fm3d_merge_shares
+    (the linear block merge of fm3d_mgpu): byte-equal to the records of the whole pair in one run."""
+    fp = synth.make_frame_pair(30_000, seed=51)
+    n = len(fp.desc1)
+    whole = _oracle_records(orc, fm3d, fp, np.arange(n))
+    parts = [_oracle_records(orc, fm3d, fp, fm3d.share_queries(n, 8, s, 512)) for s in range(8)]
+    assert len(whole) > 10_000 and all(len(p) > 0 for p in parts)
+    merged = fm3d.merge_shares(parts, n, 512)
+    assert merged.tobytes() == whole.tobytes()
