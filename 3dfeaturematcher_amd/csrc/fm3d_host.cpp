@@ -100,6 +100,7 @@ struct fm3d_ctx {
     int w = 0, h = 0;
     std::vector<int> lw, lh;
     std::vector<DevBuf> pyr1, pyr2;
+    int pyrGuardW = -1, pyrGuardH = -1, pyrGuardLevels = -1;  // the geometry whose guards are zero
     DevBuf lvlDesc;
     // circle offsets of pixelsRay
     DevBuf offsets;
@@ -832,21 +833,26 @@ int run_lm_multi(fm3d_ctx* c, const LMSrc* src, int nProb, fm3d_lm_stats* stats,
         const char* sf = getenv("FM3D_LM_SAFE");  // test switch: the guarded pass forms only
         p.safe = sf ? atoi(sf) : 0;
     }
-    // the counters (incl. the overflow word) are reset for every call, also for P == 0
-    HIPCHK(c, hipMemsetAsync(c->lmStat.p, 0, 256, c->stream));
-    for (int j = 0; j < nProb; j++) HIPCHK(c, hipMemsetAsync(src[j].c->pcnt.as<char>() + 16, 0, 16, c->stream));
-    if (Ptot > 0) {
-        HIPCHK(c, hipEventRecord(e0, c->stream));
-        HIPCHK(c, hipMemsetAsync(c->lmQueue.p, 0, 64 * sizeof(int), c->stream));
-        HIPCHK(c, hipMemsetAsync(c->lmStat.as<unsigned long long>() + 20, 0xff, 8, c->stream));  // min start
+    // the counters (incl. the overflow word) are reset for every call, also for P == 0; with points,
+    // the queue, the min-start word and every problem's statuses / info / nfev too -- one kernel
+    {
+        fm3d::LMReset rz{};
+        rz.stat = c->lmStat.as<unsigned long long>();
+        rz.queue = Ptot > 0 ? c->lmQueue.as<int>() : nullptr;
+        rz.nProb = nProb;
         for (int j = 0; j < nProb; j++) {
             fm3d_ctx* q = src[j].c;
-            const int P = src[j].P;
-            if (P <= 0) continue;
-            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)q->lmStatus.p, fm3d::kLMRunning, P, c->stream));
-            HIPCHK(c, hipMemsetAsync(q->lmInfo.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
-            HIPCHK(c, hipMemsetAsync(q->lmNfev.p, 0, (size_t)P * 8 * sizeof(int), c->stream));
+            rz.pcnt16[j] = q->pcnt.as<int>() + 4;
+            rz.status[j] = q->lmStatus.as<int>();
+            rz.info[j] = q->lmInfo.as<int>();
+            rz.nfev[j] = q->lmNfev.as<int>();
+            rz.P[j] = Ptot > 0 && src[j].P > 0 ? src[j].P : 0;
         }
+        if (Ptot > 0) HIPCHK(c, hipEventRecord(e0, c->stream));
+        fm3d::launch_lm_reset(rz, c->stream);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (Ptot > 0) {
         // one launch: every slot runs its point through all levels, coarsest first
         // (optimize_pyramid :225-241)
         // through the runtime's launch by address (not a call through a cast function pointer, which
@@ -890,15 +896,29 @@ int set_images_impl(fm3d_ctx* c, const uint8_t* img1, const uint8_t* img2, int w
         c->lw[L] = (c->lw[L - 1] + 1) / 2;
         c->lh[L] = (c->lh[L - 1] + 1) / 2;
     }
+    // the zero guards: cleared when a level's buffer is new or the image size changed, not per frame
+    // pair -- nothing but the guard clearing writes past a level's w x h pixels, so they stay zero
+    // (each clear is a fill kernel, which in a stream of frame pairs waits for CUs behind the other
+    // pairs' LM launches)
+    bool fresh = c->pyrGuardW != width || c->pyrGuardH != height || c->pyrGuardLevels != levels;
     for (int L = 0; L <= levels; L++) {
         size_t bytes = (size_t)c->lw[L] * c->lh[L] + kGuard(c->lw[L]);
+        void* p1 = c->pyr1[L].p;
+        void* p2 = c->pyr2[L].p;
         HIPCHK(c, c->pyr1[L].ensure(bytes));
         HIPCHK(c, c->pyr2[L].ensure(bytes));
-        // level 0 is overwritten by the copy below: only its zero guard needs clearing
-        const size_t skip = L == 0 ? (size_t)width * height : 0;
-        HIPCHK(c, hipMemsetAsync((char*)c->pyr1[L].p + skip, 0, bytes - skip, c->stream));
-        HIPCHK(c, hipMemsetAsync((char*)c->pyr2[L].p + skip, 0, bytes - skip, c->stream));
+        fresh |= c->pyr1[L].p != p1 || c->pyr2[L].p != p2;
     }
+    for (int L = 0; fresh && L <= levels; L++) {
+        // a level's pixels are overwritten (level 0 by the copy below, the others by pyrDown): the
+        // guard past them is what needs clearing
+        const size_t img = (size_t)c->lw[L] * c->lh[L];
+        HIPCHK(c, hipMemsetAsync((char*)c->pyr1[L].p + img, 0, c->pyr1[L].bytes - img, c->stream));
+        HIPCHK(c, hipMemsetAsync((char*)c->pyr2[L].p + img, 0, c->pyr2[L].bytes - img, c->stream));
+    }
+    c->pyrGuardW = width;
+    c->pyrGuardH = height;
+    c->pyrGuardLevels = levels;
     const size_t wh = (size_t)width * height;
     HIPCHK(c, c->hImg.ensure(2 * wh));
     for (int y = 0; y < height; y++) {

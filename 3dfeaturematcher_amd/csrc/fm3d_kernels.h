@@ -320,6 +320,22 @@ struct TriParams {
 };
 void launch_triangulate(const TriParams& p, hipStream_t s);
 
+// The LM launch's resets in one kernel (it replaced eleven fill launches per launch: each a blit
+// kernel that, in a stream of frame pairs, waits for CUs behind the other pairs' LM launches):
+// the launch counters (stat: 32 words, word 20 = ~0, the minimum start), the work queue, and per
+// problem its pair counters (pcnt + 16 bytes), its statuses (kLMRunning) and lmdif info / nfev.
+struct LMReset {
+    unsigned long long* stat;
+    int* queue;  // 64 ints, or null (no points)
+    int nProb;
+    int* pcnt16[kLMMaxProblems];  // 4 ints each
+    int* status[kLMMaxProblems];
+    int* info[kLMMaxProblems];
+    int* nfev[kLMMaxProblems];
+    int P[kLMMaxProblems];  // the problems' point bounds (0: only the counters)
+};
+void launch_lm_reset(const LMReset& r, hipStream_t s);
+
 // ---------------- stable compaction fused into its producer (decoupled look-back) ----------------
 // One launch produces the items and compacts them in order: each block counts its kept items,
 // publishes the count, and adds up its predecessors' (their inclusive prefix as soon as one is

@@ -153,6 +153,22 @@ __global__ __launch_bounds__(kTriThreads) void triangulate_compact_kernel(TriPar
     }
 }
 
+// ---------------- the LM launch's resets (LMReset) ----------------
+__global__ void lm_reset_kernel(LMReset r, int maxP) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 32) r.stat[t] = t == 20 ? ~0ull : 0ull;
+    if (r.queue && t < 64) r.queue[t] = 0;
+    for (int j = 0; j < r.nProb; j++) {
+        if (t < 4) r.pcnt16[j][t] = 0;
+        if (t < r.P[j]) r.status[j][t] = kLMRunning;
+        if (t < 8 * r.P[j]) {
+            r.info[j][t] = 0;
+            r.nfev[j][t] = 0;
+        }
+    }
+    (void)maxP;
+}
+
 // ---------------- cv::pyrDown (8U) ----------------
 __device__ inline int reflect101(int q, int len) {
     if (len == 1) return 0;
@@ -449,6 +465,13 @@ void launch_triangulate_compact(const TriParams& p, double* out, int* srcIdx, in
                                 hipStream_t s, int* hostCnt) {
     triangulate_compact_kernel<<<triangulate_compact_blocks(p.K), kTriThreads, 0, s>>>(p, out, srcIdx, count, lb,
                                                                                       hostCnt);
+}
+
+void launch_lm_reset(const LMReset& r, hipStream_t s) {
+    int maxP = 0;
+    for (int j = 0; j < r.nProb; j++) maxP = r.P[j] > maxP ? r.P[j] : maxP;
+    const long n = 8L * maxP > 64 ? 8L * maxP : 64;
+    lm_reset_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(r, maxP);
 }
 
 void launch_pyrdown(const uint8_t* src, int w, int h, uint8_t* dst, hipStream_t s) {

@@ -116,7 +116,7 @@ def parse():
     ap.add_argument("--dump-records", type=str, default="",
                     help="torchrun C5: rank 0 saves the last step's merged survivor records (.npy)")
     ap.add_argument("--pmc-json", type=str, default=next(
-        (p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_c4.json") for r in (5, 4, 3, 2)) if os.path.exists(p)),
+        (p for p in (os.path.join(ROOT, "profiles", f"r0{r}_pmc_c4.json") for r in (6, 5, 4, 3, 2)) if os.path.exists(p)),
         os.path.join(ROOT, "profiles", "r02_pmc_c4.json")),
                     help="rocprofv3 PMC summary of the same command (HBM bytes per LM launch)")
     return ap.parse_args()

@@ -200,6 +200,11 @@ typedef struct fm3d_lm_stats {
     int64_t queue_empty_ticks;
 } fm3d_lm_stats;
 
+/* match_ms: row constants + knn + NNDR with its compaction (NNDR is fused into the match's last
+   launch, so nndr_ms is always 0); triangulate_ms: DLT + inlier compaction.  Both are 0 when the step
+   recorded no stage events (FM3D_STAGE_EVENTS=0).  In a stream of frame pairs the stage events of a
+   pair also span the time its launches wait behind other pairs' work on the GPU: stage costs come from
+   a pair run alone. */
 typedef struct fm3d_pipeline_stats {
     int64_t queries, trains, matches, inliers, kept;
     double match_ms, nndr_ms, triangulate_ms, pyramid_ms, lm_ms, total_ms; /* HIP events */

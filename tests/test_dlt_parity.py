@@ -1,0 +1,100 @@
+"""What the rounds 1-5 geometry stand-ins did, pinned two
+ways.  CPU only (the oracle):
+
+  * the per-match arrays tools/dlt_parity.py saved (tests/golden/dlt_parity_c4.npz) reproduce every
+    count of the committed table (profiles/r06_dlt_parity.json): the C4 frame pair's DLT with
+    OpenCV 2.4's cvTriangulatePoints / JacobiSVD and cvRodrigues2's SVD polar factor (the contract
+    since round 6) against the 4-row round-robin Jacobi DLT and the Newton polar factor of rounds 1-5,
+    over every match and inlier, through the LM (DETMATH);
+  * a pinned subset -- the 16 largest normal moves, 16 status changes, 32 seeded inliers -- re-run
+    through the oracle with the OpenCV geometry gives the saved statuses and normals bit for bit.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import oracle_threads
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIXTURE = os.path.join(ROOT, "tests", "golden", "dlt_parity_c4.npz")
+TABLE = os.path.join(ROOT, "profiles", "r06_dlt_parity.json")
+
+pytestmark = pytest.mark.skipif(not (os.path.exists(FIXTURE) and os.path.exists(TABLE)),
+                                reason="tools/dlt_parity.py has not been run")
+
+
+class Cam:
+    def __init__(self, arr):
+        self.fx, self.fy, self.cx, self.cy = arr[:4]
+        self.k = tuple(arr[4:9])
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return np.load(FIXTURE, allow_pickle=False)
+
+
+@pytest.fixture(scope="module")
+def table():
+    with open(TABLE) as f:
+        return json.load(f)
+
+
+def _counts(s_new, s_oth, d):
+    both = (s_new >= 0) & (s_oth >= 0)
+    sb, so, dk = s_new[both], s_oth[both], d[both & (s_new == 0) & (s_oth == 0)]
+    return {
+        "points": int(both.sum()),
+        "status_changed": int((sb != so).sum()),
+        "keep_drop_changed": int(((sb == 0) != (so == 0)).sum()),
+        "kept_both": int(((sb == 0) & (so == 0)).sum()),
+        "normals_bit_equal": int((dk == 0).sum()),
+        "beyond_1e-4": int((dk > 1e-4).sum()),
+        "max": float(dk.max()),
+        "inlier_only_opencv": int(((s_new >= 0) & (s_oth < 0)).sum()),
+        "inlier_only_other": int(((s_new < 0) & (s_oth >= 0)).sum()),
+        "survivors_opencv": int((s_new == 0).sum()),
+        "survivors_other": int((s_oth == 0).sum()),
+    }
+
+
+def test_table_is_the_saved_data(fx, table):
+    c = _counts(fx["status_opencv"].astype(int), fx["status_legacy"].astype(int), fx["dn_legacy"])
+    t = table["points"]["legacy_both_vs_opencv_lm"]
+    for k, v in c.items():
+        assert t[k] == v, k
+    for name in ("legacy_dlt", "legacy_polar"):
+        key = f"status_{name}"
+        if key in fx.files:
+            c = _counts(fx["status_opencv"].astype(int), fx[key].astype(int), fx[f"dn_{name}"])
+            ta = table["attribution"][f"{name}_vs_opencv_lm"]
+            for k, v in c.items():
+                assert ta[k] == v, (name, k)
+
+
+def test_stand_ins_moved_the_results(table):
+    """The stand-ins were not harmless: the 4-row DLT moves the points by ~4e-7 relative (median)
+    and the LM, which decides its steps at rounding-noise level, turns that into normals beyond the
+    north_star's 1e-4 on most kept points and into keep/drop changes; the SVD itself is OpenCV's up
+    to last-bit variants (SSE2 lane sums, libm's hypot), and numpy's SVD of the same 6 x 4 system
+    agrees to 1e-13."""
+    p = table["points"]
+    assert p["opencv_vs_numpy_svd_6x4"]["max_rel"] < 1e-12 and p["opencv_vs_numpy_svd_6x4"]["mask_changed"] == 0
+    assert p["legacy_dlt_vs_opencv"]["median_rel"] > 1e-8
+    assert p["legacy_polar_vs_opencv"]["points_bit_equal"] == p["legacy_polar_vs_opencv"]["inliers"]
+    assert 0 < p["legacy_polar_vs_opencv"]["R2_max_abs_diff"] < 1e-14
+    for v in ("sse2_lanes_vs_opencv", "libm_hypot_vs_opencv"):
+        assert p[v]["max_rel"] < 1e-13 and p[v]["mask_changed"] == 0
+    lm = p["legacy_both_vs_opencv_lm"]
+    assert lm["keep_drop_changed"] > 0 and lm["beyond_1e-4"] > lm["kept_both"] // 2
+
+
+def test_pinned_subset_reruns_bitwise(orc, fx):
+    cam = Cam(fx["cam"])
+    r = orc.optimize_normals(cam, fx["R2"], fx["t2"], fx["img1"], fx["img2"], 3, fx["pin_points"], 64,
+                             mode=orc.DETMATH, nthreads=oracle_threads())
+    assert np.array_equal(r["status"], fx["pin_status"])
+    ok = r["status"] == 0
+    assert np.array_equal(r["normals"][ok], fx["pin_normals"][ok])

@@ -15,7 +15,8 @@ max-abs difference of the normals.  The points where STRICT and DETMATH differ a
 re-run with libm for ONE transcendental at a time (sin, cos, atan2, exp) to attribute the
 difference.
 
-Writes profiles/r05_full_parity.json (the tables) and tests/golden/full_parity_c4.npz (per-point
+Writes profiles/r06_full_parity.json (the tables; round 5's, over the rounds 1-5 DLT, stay in
+profiles/r05_full_parity.json) and tests/golden/full_parity_c4.npz (per-point
 statuses and differences, plus the inputs and expected outputs of a small pinned subset that
 tests/test_full_parity.py re-runs through the oracle).
 
@@ -75,7 +76,7 @@ def diff(base, other):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=len(os.sched_getaffinity(0)))
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05_full_parity.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r06_full_parity.json"))
     ap.add_argument("--fixture", default=os.path.join(ROOT, "tests", "golden", "full_parity_c4.npz"))
     ap.add_argument("--limit", type=int, default=0, help="first N inliers only (a dry run)")
     args = ap.parse_args()
@@ -156,6 +157,7 @@ def main():
         pin_status_detmath=base["status"][pin], pin_status_strict=strict["status"][pin],
         pin_status_tree=tree["status"][pin],
         R2=R2, t2=t2, img1=fp.img1, img2=fp.img2,
+        records_sha256=np.array(mff.load_fixture("c4")["records_sha256"]) if not args.limit else np.array(""),
         cam=np.array([fp.cam.fx, fp.cam.fy, fp.cam.cx, fp.cam.cy, *fp.cam.k]),
     )
     print(f"-> {args.out}, {args.fixture} ({time.time() - t0:.0f} s)")
