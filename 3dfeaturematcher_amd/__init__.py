@@ -1033,7 +1033,8 @@ class MultiGPU:
         rc = lib().fm3d_mgpu_create(ctypes.byref(settings), self.ndev, _ptr(devs, ctypes.c_int32), self.shares, block,
                                     ctypes.byref(self._h))
         if rc != FM3D_OK:
-            raise Fm3dError(rc, "fm3d_mgpu_create failed (no HIP devices / RCCL?)")
+            why = (lib().fm3d_mgpu_last_error(None) or b"").decode(errors="replace")
+            raise Fm3dError(rc, "fm3d_mgpu_create failed" + (f": {why}" if why else " (no HIP devices / RCCL?)"))
         self.n_queries = 0
 
     def check(self, rc):

@@ -30,6 +30,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -205,6 +206,8 @@ int preflight(fm3d_mgpu* m, int64_t nB, int dim, int type, int width, int height
         size_t freeB = 0, totalB = 0;
         MHIP(m, hipSetDevice(m->devices[d]));
         MHIP(m, hipMemGetInfo(&freeB, &totalB));
+        // test hook (tests/test_gpu_parity.py): pretend the device has at most this much free
+        if (const char* lim = getenv("FM3D_DEBUG_FREE_MB")) freeB = std::min(freeB, (size_t)strtoull(lim, nullptr, 0) << 20);
         const size_t grow = need - m->memChecked[d];
         if (grow + ((size_t)256 << 20) > freeB)
             return mfail(m, FM3D_ERR_NOMEM, "device " + std::to_string(m->devices[d]) + ": " +

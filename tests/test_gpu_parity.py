@@ -1246,6 +1246,45 @@ def test_mgpu_more_devices_than_visible_fails(fm3d, pair):
     assert e.value.code == fm3d.ERR_INVALID
 
 
+def test_mgpu_memory_preflight_nomem(fm3d, synth, monkeypatch):
+    """fm3d_mgpu pre-flights device memory before anything grows.  With the device
+    pretending to have 1 GiB free (FM3D_DEBUG_FREE_MB), creation fails cleanly with FM3D_ERR_NOMEM
+    and the shortfall in fm3d_mgpu_last_error(NULL) (four context sets' LM slabs do not fit); a
+    created one given 300 MiB refuses a 20k-keypoint pair's buffers at upload, before staging; with
+    the real free memory the same object then takes the pair, and its records equal
+    fm3d_pipeline_run's."""
+    fp = synth.make_frame_pair(20_000, seed=61)
+    s = _settings(fm3d, fp.cam, pixelsRay=64, pyramids=3)
+    monkeypatch.setenv("FM3D_DEBUG_FREE_MB", "1024")
+    with pytest.raises(fm3d.Fm3dError) as e:
+        fm3d.MultiGPU(s, devices=[0])
+    assert e.value.code == fm3d.ERR_NOMEM
+    assert "MiB more needed" in str(e.value), str(e.value)
+    monkeypatch.delenv("FM3D_DEBUG_FREE_MB")
+    mg = fm3d.MultiGPU(s, devices=[0])
+    try:
+        mg.set_g12(fp.g12)
+        monkeypatch.setenv("FM3D_DEBUG_FREE_MB", "300")
+        with pytest.raises(fm3d.Fm3dError) as e:
+            mg.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        assert e.value.code == fm3d.ERR_NOMEM and "MiB more needed" in str(e.value)
+        monkeypatch.delenv("FM3D_DEBUG_FREE_MB")
+        mg.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        rec, _ = mg.run()
+    finally:
+        mg.close()
+    ctx = fm3d.Context(s)
+    try:
+        fm3d.SingleCameraTriangulator(ctx).set_g12(fp.g12)
+        pipe = fm3d.Pipeline(ctx)
+        pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        n, _ = pipe.run()
+        ref = pipe.records(n)
+    finally:
+        ctx.close()
+    assert rec.tobytes() == ref.tobytes() and len(rec) > 1000
+
+
 def test_bench_gpus_more_than_visible_exits_nonzero():
     """`bench.py --gpus N` with fewer than N GPUs visible exits non-zero with a clear
     message, never a one-GPU line labelled otherwise."""
