@@ -341,13 +341,8 @@ int upload_pinned(fm3d_ctx* c, DevBuf& dst, HostBuf& h, const void* src, size_t 
     HIPCHK(c, dst.ensure(bytes));
     if (!bytes) return FM3D_OK;
     HIPCHK(c, h.ensure(bytes));
-    constexpr size_t kPiece = (size_t)1 << 20;
-    const size_t piece = bytes >= 4 * kPiece ? kPiece : bytes;
-    for (size_t o = 0; o < bytes; o += piece) {
-        const size_t n = std::min(piece, bytes - o);
-        std::memcpy((char*)h.p + o, (const char*)src + o, n);
-        HIPCHK(c, hipMemcpyAsync((char*)dst.p + o, (char*)h.p + o, n, hipMemcpyHostToDevice, c->stream));
-    }
+    std::memcpy(h.p, src, bytes);
+    HIPCHK(c, hipMemcpyAsync(dst.p, h.p, bytes, hipMemcpyHostToDevice, c->stream));
     return FM3D_OK;
 }
 
