@@ -775,13 +775,13 @@ def test_c4_sift100k_full_pipeline(fm3d, orc, synth):
       * NNDR: every one of the 100k queries (the oracle's NNDR on the GPU's knn lists);
       * DLT: all matches, inlier mask and points bit-exact;
       * records: every survivor's (queryIdx, trainIdx, distance, point) equal to its match / point;
-      * the whole result: the generated inputs' digests equal the fixture's, then ALL 36,151
-        survivor records byte for byte against the oracle's DETMATH run over all 71,223 inliers
+      * the whole result: the generated inputs' digests equal the fixture's, then ALL 36,143
+        survivor records byte for byte against the oracle's DETMATH run over all 71,238 inliers
         (tests/golden/full_c4.npz, made by tests/golden/make_full_fixtures.py in the container);
       * LM vs libm (STRICT) on a seeded random 128-point sample: the same statuses, and each kept
         point's |n - n_libm| exactly the one tools/full_parity.py measured for it over the whole
         set (tests/golden/full_parity_c4.npz, DESIGN.md §4: with the correctly rounded
-        transcendentals every one of the 36,151 kept normals is within 1e-4 of libm's, not a
+        transcendentals every one of the 36,143 kept normals is within 1e-4 of libm's, not a
         sampled 99 %)."""
     mod, fx = full_fixture("c4")
     fp = synth.make_frame_pair(100_000, 640, 480, seed=7)
@@ -818,7 +818,7 @@ def test_c4_sift100k_full_pipeline(fm3d, orc, synth):
     assert (np.diff(rec["queryIdx"]) > 0).all() and np.array_equal(q[mask][pos], rec["queryIdx"])
     assert np.array_equal(rec["trainIdx"], t[mask][pos]) and np.array_equal(rec["distance"], d[mask][pos])
     assert np.array_equal(rec["point"], pts[pos])
-    # EVERY survivor record (all 71,223 inliers through the LM) byte for byte against the oracle's
+    # EVERY survivor record (all 71,238 inliers through the LM) byte for byte against the oracle's
     # DETMATH run of the whole frame pair (tests/golden/full_c4.npz)
     assert n == len(fx["records"]) and tuple(fx["counts"]) == (100_000, stats["matches"], stats["inliers"], n)
     assert rec.tobytes() == fx["records"].tobytes()
@@ -855,7 +855,7 @@ def test_c5_1m_keypoints_query_blocks(fm3d, orc, synth):
     """BASELINE configs[4] (C5) on one GPU: one 1M-keypoint frame pair (640x480, sub-pixel
     keypoints; pixelsRay 64, pyramids 3) run whole and as the 4 block-cyclic
     shares of a 4-GPU run (bench.py --gpus 4): the merged share records are byte-identical to
-    the whole run.  Every 10th 4,096-query block (102,400 queries, 36,449 survivors) against the
+    the whole run.  Every 10th 4,096-query block (102,400 queries, 36,455 survivors) against the
     committed oracle run over all 1M train rows (tests/golden/full_c5sub.npz),
     record for record; and a seeded 2,000-query sample through the oracle here (match, NNDR, DLT, LM
     in DETMATH mode): the whole run's records of those queries are exactly the oracle's survivors."""
@@ -868,7 +868,7 @@ def test_c5_1m_keypoints_query_blocks(fm3d, orc, synth):
     full = shard.run_shard(fp, s, 0, n)
     qsel = mod.subset_queries(mod.WORKLOADS["c5sub"], n)
     sub10 = full[np.isin(full["queryIdx"], qsel)]
-    assert len(sub10) == len(fx["records"]) == 36_449 and sub10.tobytes() == fx["records"].tobytes()
+    assert len(sub10) == len(fx["records"]) == 36_455 and sub10.tobytes() == fx["records"].tobytes()
     parts = [shard.run_shard_queries(fp, s, shard.query_blocks(n, 4, r)) for r in range(4)]
     merged = np.concatenate(parts)
     merged = merged[np.argsort(merged["queryIdx"], kind="stable")]

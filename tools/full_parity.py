@@ -1,7 +1,7 @@
 """Full-set LM parity measurements on the C4 frame pair.
 
 CPU only, oracle only (test infrastructure; no GPU).  Over EVERY DLT inlier of the C4 frame pair
-(100k SIFT-128, 640x480, seed 7, pixelsRay 64, pyramids 3; 71,223 inliers) the LM is run by the
+(100k SIFT-128, 640x480, seed 7, pixelsRay 64, pyramids 3; 71,238 inliers) the LM is run by the
 oracle (oracle/fm3d_oracle.c) in
 
   * DETMATH            -- the GPU contract (the records of tests/golden/full_c4.npz);
