@@ -25,6 +25,10 @@
 // queued behind the records.
 // RCCL is loaded with dlopen on first use, so libfm3d.so itself does not depend on it (a process
 // that also loads PyTorch's bundled RCCL keeps one copy per user).
+// Test mode FM3D_DEBUG_MGPU_ALIAS=1: a device may be listed more than once (eight "devices" on one
+// GPU), so the N-device plan, per-device submit threads, memory pre-flight and merge run on a
+// one-GPU box.  RCCL refuses a device twice, so in that mode the all-gather is restated as the same
+// copies on the device streams (each destination stream waits for every source's records).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -132,6 +136,8 @@ struct fm3d_mgpu {
     std::vector<std::vector<fm3d_point2f>> kpA;     // per device: its gathered keypoints
     std::vector<fm3d_record> mergeTmp;              // the devices' records before the merge
     std::vector<size_t> memChecked;                 // per device: the memory need last pre-flighted
+    bool alias = false;                             // a device listed twice (FM3D_DEBUG_MGPU_ALIAS)
+    hipEvent_t aliasEv[kSets][16] = {};             // alias mode: each device's records queued
     bool staged = false;                            // fm3d_mgpu_pipeline_upload ran (set 0)
     bool pending[kSets] = {};
     bool gathered[kSets] = {};                      // the set's all-gather is queued
@@ -196,26 +202,33 @@ int64_t merge_blocks(const fm3d_record* recs, const int64_t* off, int lists, int
 // `need` grows monotonically; only the growth since the last check must fit in the free memory.
 int preflight(fm3d_mgpu* m, int64_t nB, int dim, int type, int width, int height, int64_t capDev) {
     if (m->memChecked.size() != (size_t)m->ndev) m->memChecked.assign(m->ndev, 0);
+    std::vector<size_t> need(m->ndev);
     for (int d = 0; d < m->ndev; d++) {
         const int64_t nAd = m->idx.empty() ? 0 : (int64_t)m->idx[d].size();
         size_t per = 0;
         int r = fm3d_internal_memory_need(m->ctx[0][d], nAd, nB, dim, type, width, height, &per);
         if (r) return mfail(m, r, std::string("memory estimate: ") + fm3d_last_error(m->ctx[0][d]));
-        const size_t need = kSets * (per + (size_t)capDev * sizeof(fm3d_record) * (1 + m->ndev));
-        if (need <= m->memChecked[d]) continue;
+        need[d] = kSets * (per + (size_t)capDev * sizeof(fm3d_record) * (1 + m->ndev));
+    }
+    // per physical device (several entries in alias mode): the growth of its entries' needs
+    for (int d = 0; d < m->ndev; d++) {
+        if (std::find(m->devices.begin(), m->devices.end(), m->devices[d]) - m->devices.begin() != d) continue;
+        size_t grow = 0;
+        for (int e = d; e < m->ndev; e++)
+            if (m->devices[e] == m->devices[d] && need[e] > m->memChecked[e]) grow += need[e] - m->memChecked[e];
+        if (!grow) continue;
         size_t freeB = 0, totalB = 0;
         MHIP(m, hipSetDevice(m->devices[d]));
         MHIP(m, hipMemGetInfo(&freeB, &totalB));
         // test hook (tests/test_gpu_parity.py): pretend the device has at most this much free
         if (const char* lim = getenv("FM3D_DEBUG_FREE_MB")) freeB = std::min(freeB, (size_t)strtoull(lim, nullptr, 0) << 20);
-        const size_t grow = need - m->memChecked[d];
         if (grow + ((size_t)256 << 20) > freeB)
             return mfail(m, FM3D_ERR_NOMEM, "device " + std::to_string(m->devices[d]) + ": " +
                                                 std::to_string(grow >> 20) + " MiB more needed for " +
                                                 std::to_string(kSets) + " context sets (LM slabs + frame-pair "
                                                 "buffers), " + std::to_string(freeB >> 20) + " MiB free");
-        m->memChecked[d] = need;
     }
+    for (int d = 0; d < m->ndev; d++) m->memChecked[d] = std::max(m->memChecked[d], need[d]);
     return FM3D_OK;
 }
 
@@ -262,6 +275,24 @@ void gather_device(fm3d_mgpu* m, int d, const void* descA, size_t rb, const fm3d
 // the collectives of set k, queued on every device's pipeline stream behind its records
 int queue_allgather(fm3d_mgpu* m, int k) {
     const size_t slot = (size_t)m->capDev * sizeof(fm3d_record);
+    if (m->alias) {  // test mode: the all-gather's result by copies on the one GPU's streams
+        for (int e = 0; e < m->ndev; e++) {
+            MHIP(m, hipSetDevice(m->devices[e]));
+            MHIP(m, hipEventRecord(m->aliasEv[k][e], fm3d_internal_stream(m->ctx[k][e])));
+        }
+        for (int d = 0; d < m->ndev; d++) {
+            hipStream_t st = fm3d_internal_stream(m->ctx[k][d]);
+            MHIP(m, hipSetDevice(m->devices[d]));
+            for (int e = 0; e < m->ndev; e++) {
+                MHIP(m, hipStreamWaitEvent(st, m->aliasEv[k][e], 0));
+                MHIP(m, hipMemcpyAsync(m->cntRecv[k][d] + e, fm3d_internal_kept_dev(m->ctx[k][e]), sizeof(int32_t),
+                                       hipMemcpyDeviceToDevice, st));
+                MHIP(m, hipMemcpyAsync((char*)m->recv[k][d] + (size_t)e * slot, m->send[k][e], slot,
+                                       hipMemcpyDeviceToDevice, st));
+            }
+        }
+        return FM3D_OK;
+    }
     RcclGroup g;
     ncclResult_t r = g.start();
     if (r != ncclSuccess) return mfail(m, FM3D_ERR_HIP, std::string("ncclGroupStart: ") + rccl().errStr(r));
@@ -410,6 +441,8 @@ int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int s
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    const char* aliasEnv = getenv("FM3D_DEBUG_MGPU_ALIAS");
+    const bool allowAlias = aliasEnv && aliasEnv[0] == '1';
     fm3d_mgpu* m = new fm3d_mgpu();
     m->s = *s;
     m->ndev = ndev;
@@ -417,13 +450,15 @@ int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int s
     m->block = block ? block : kDefaultBlock;
     for (int d = 0; d < ndev; d++) {
         const int dev = devices ? devices[d] : d;
-        if (dev < 0 || dev >= count || std::count(m->devices.begin(), m->devices.end(), dev)) {
+        const bool twice = std::count(m->devices.begin(), m->devices.end(), dev) != 0;
+        if (dev < 0 || dev >= count || (twice && !allowAlias)) {
             delete m;
             return FM3D_ERR_INVALID;  // fewer devices visible than asked for, or a device twice
         }
+        m->alias |= twice;
         m->devices.push_back(dev);
     }
-    if (!rccl().load()) {
+    if (!m->alias && !rccl().load()) {
         m->err = rccl().err;
         fm3d_mgpu_destroy(m);
         return FM3D_ERR_UNSUPPORTED;
@@ -446,10 +481,21 @@ int fm3d_mgpu_create(const fm3d_settings* s, int ndev, const int* devices, int s
             return r;
         }
     }
-    m->comms.assign(ndev, nullptr);
-    if (rccl().commInitAll(m->comms.data(), ndev, m->devices.data()) != ncclSuccess) {
-        fm3d_mgpu_destroy(m);
-        return FM3D_ERR_HIP;
+    if (m->alias) {
+        for (int k = 0; k < kSets; k++)
+            for (int d = 0; d < ndev; d++)
+                if (hipSetDevice(m->devices[d]) != hipSuccess ||
+                    hipEventCreateWithFlags(&m->aliasEv[k][d], hipEventDisableTiming) != hipSuccess) {
+                    create_error() = "hipEventCreate failed";
+                    fm3d_mgpu_destroy(m);
+                    return FM3D_ERR_HIP;
+                }
+    } else {
+        m->comms.assign(ndev, nullptr);
+        if (rccl().commInitAll(m->comms.data(), ndev, m->devices.data()) != ncclSuccess) {
+            fm3d_mgpu_destroy(m);
+            return FM3D_ERR_HIP;
+        }
     }
     m->rowsA.resize(ndev);
     m->kpA.resize(ndev);
@@ -465,6 +511,9 @@ void fm3d_mgpu_destroy(fm3d_mgpu* m) {
     free_buffers(m);
     for (auto c : m->comms)
         if (c) rccl().commDestroy(c);
+    for (int k = 0; k < kSets; k++)
+        for (int d = 0; d < m->ndev; d++)
+            if (m->aliasEv[k][d]) hipEventDestroy(m->aliasEv[k][d]);
     for (int k = 0; k < kSets; k++)
         for (int d = 0; d < m->ndev; d++) fm3d_ctx_destroy(m->ctx[k][d]);
     delete m;

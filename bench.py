@@ -106,6 +106,9 @@ def parse():
                     help="frame pairs per LM launch in the stream mode (2-4: fm3d_pipeline_link)")
     ap.add_argument("--mgpu", action="store_true",
                     help="the one-process multi-GPU path (fm3d_mgpu, C5) also at --gpus 1 (its reference point)")
+    ap.add_argument("--alias-devices", action="store_true",
+                    help="diagnostic, not a bench line: --gpus N --mgpu with device 0 listed N times "
+                         "(fm3d_mgpu's test mode FM3D_DEBUG_MGPU_ALIAS): the N-device host path on one GPU")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the C5 byte-identity check against one GPU")
@@ -380,7 +383,10 @@ def run_mgpu(args, workload):
     fm3d = importlib.import_module("3dfeaturematcher_amd")
     n = args.gpus
     vis = fm3d.device_count()
-    if vis < n:
+    alias = bool(getattr(args, "alias_devices", False))
+    if alias:
+        os.environ["FM3D_DEBUG_MGPU_ALIAS"] = "1"
+    if vis < (1 if alias else n):
         print(f"bench.py --gpus {n}: only {vis} GPU(s) visible", file=sys.stderr, flush=True)
         raise SystemExit(2)
     if workload != "c5":
@@ -397,7 +403,7 @@ def run_mgpu(args, workload):
     t_gen = time.time() - t_gen
     s = c4_settings(fm3d, pair, args)
     torch_at_create = "torch" in sys.modules
-    mg = fm3d.MultiGPU(s, devices=list(range(n)), shares=n)
+    mg = fm3d.MultiGPU(s, devices=[0] * n if alias else list(range(n)), shares=n)
     mg.set_g12(pair.g12)
     binary = args.desc == "orb"
     inputs = (desc_rows(args, pair.desc1), desc_rows(args, pair.desc2), pair.kp1, pair.kp2, pair.img1, pair.img2)
@@ -513,6 +519,15 @@ def run_mgpu(args, workload):
     out.update(verify_against_fixture(args, wl, "c5", pair, last_rec))
     if len(digests) != 1:
         out["verified"] = False
+    if alias:
+        out["alias_devices"] = {
+            "note": (f"diagnostic, not a scaling point: device 0 listed {n} times (FM3D_DEBUG_MGPU_ALIAS=1), so "
+                     f"all {n} shares, their {4 * n} context sets and {n} concurrent LM launches share ONE GPU and "
+                     f"the all-gather is restated as device copies; value / value_one_gpu is the {n}-way host "
+                     f"path's cost on one GPU"),
+            "value_over_one_device": value / out["value_one_gpu"]}
+        out["efficiency"] = None
+        out["n_gpus"] = 1
     emit(out, args)
 
 

@@ -1235,6 +1235,45 @@ def test_mgpu_submit_wait_stream_equals_run(fm3d, synth):
         assert mst["kept"] == k and mst["inliers"] == st["inliers"]
 
 
+def test_mgpu_eight_aliased_devices_equal_run(fm3d, synth, monkeypatch):
+    """The 8-device code of fm3d_mgpu on a one-GPU box. In test mode FM3D_DEBUG_MGPU_ALIAS=1 device 0
+    may be listed eight times. Each entry runs as its own device: its own four context sets, its
+    host submit thread, its block-cyclic share of the queries (12 shares of 512-query blocks) and its
+    memory pre-flight (summed per physical GPU). The all-gather becomes the same copies on the
+    streams, since RCCL refuses a device twice. Both fm3d_mgpu_pipeline_run and the submit / wait
+    stream merge the eight lists into records byte-identical to one fm3d_pipeline_run of the whole
+    pair. Without the variable, a repeated device is refused."""
+    fp = synth.make_frame_pair(9000, seed=33)
+    s = _settings(fm3d, fp.cam, pixelsRay=12, pyramids=1)
+    ctx, pipe = _pipe_ctx(fm3d, s, fp.g12)
+    try:
+        pipe.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        k, st = pipe.run()
+        full = pipe.records(k)
+    finally:
+        ctx.close()
+    with pytest.raises(fm3d.Fm3dError) as e:
+        fm3d.MultiGPU(s, devices=[0, 0])
+    assert e.value.code == fm3d.ERR_INVALID
+    monkeypatch.setenv("FM3D_DEBUG_MGPU_ALIAS", "1")
+    mg = fm3d.MultiGPU(s, devices=[0] * 8, shares=12, block=512)
+    try:
+        mg.set_g12(fp.g12)
+        mg.upload(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        outs = [mg.run()]
+        for i in range(6):
+            if i >= 4:
+                outs.append(mg.wait())
+            mg.submit(fp.desc1, fp.desc2, fp.kp1, fp.kp2, fp.img1, fp.img2)
+        outs += [mg.wait() for _ in range(4)]
+    finally:
+        mg.close()
+    assert k > 50 and len(outs) == 7
+    for rec, mst in outs:
+        assert rec.tobytes() == full.tobytes()
+        assert mst["kept"] == k and mst["inliers"] == st["inliers"] and mst["queries"] == 9000
+
+
 def test_mgpu_more_devices_than_visible_fails(fm3d, pair):
     """fm3d_mgpu_create over more devices than the box has: FM3D_ERR_INVALID, never a silent
     one-GPU run (bench.py --gpus N relies on it)."""
