@@ -3,8 +3,9 @@ C4 frame pair: DETMATH, the GPU contract, against STRICT, libm's transcendentals
 opt-in tree-reduction mode DETMATH|TREE|GRAM), pinned two ways.  CPU only (the oracle):
 
   * the per-point arrays the tool saved (tests/golden/full_parity_c4.npz) reproduce every count of
-    the committed table (profiles/r05_full_parity.json), so the figures DESIGN.md quotes are the
-    data's;
+    the committed table (profiles/r06_full_parity.json: the round-6 geometry, OpenCV's SVD; round
+    5's table over the rounds 1-5 DLT stays in profiles/r05_full_parity.json), so the figures
+    DESIGN.md quotes are the data's;
   * a pinned subset -- the 16 largest STRICT moves, the 16 largest tree moves and 32 seeded points --
     re-run through the oracle in all three modes gives the saved statuses and normals bit for bit.
 """
@@ -18,7 +19,7 @@ from conftest import oracle_threads
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIXTURE = os.path.join(ROOT, "tests", "golden", "full_parity_c4.npz")
-TABLE = os.path.join(ROOT, "profiles", "r05_full_parity.json")
+TABLE = os.path.join(ROOT, "profiles", "r06_full_parity.json")
 TREE, GRAM = 64, 128  # oracle/fm3d_oracle.c ORC_LM_TREE / ORC_LM_GRAM
 
 pytestmark = pytest.mark.skipif(not (os.path.exists(FIXTURE) and os.path.exists(TABLE)),
@@ -62,31 +63,36 @@ def test_table_is_the_saved_data(fx, table, other, key):
     c = _counts(fx["status_detmath"], fx[f"status_{other}"], fx[f"dn_{other}"])
     for k, v in c.items():
         assert table[key][k] == v, (key, k)
-    assert table["inliers"] == len(fx["status_detmath"]) == 71223
+    assert table["inliers"] == len(fx["status_detmath"]) == 71238
 
 
 def test_strict_vs_detmath_bar(table):
     """The GPU contract (DETMATH: correctly rounded sin / cos / atan2 / exp, include/fm3d_crmath.h)
-    against libm on all 71,223 C4 inliers (DESIGN.md §4 quotes the table): the same status on every
-    point, every kept normal within 1e-4 -- in fact within 1e-15, 35,808 of 36,151 bit for bit.  The
-    345 points that differ at all differ through libm's sin, cos and atan2 (not correctly rounded
-    on every argument here), not exp (the attribution runs)."""
+    against libm on all 71,238 C4 inliers (DESIGN.md §4 quotes the table): the same status on every
+    point; 35,786 of the 36,143 kept normals bit for bit, 36,141 within 1e-4.  The two others move
+    by up to 4.4e-3, and re-running them with libm's sin alone reproduces STRICT on both: glibc's
+    sin is not correctly rounded on every argument, and lmdif's 30-eps decisions turn one ulp into
+    a different path.  Of the 357 points that differ at all, libm's sin, cos and atan2 each
+    reproduce STRICT on some, exp on almost none."""
     t = table["strict_vs_detmath"]
     assert t["status_changed"] == 0 and t["keep_drop_changed"] == 0
-    assert t["beyond_1e-4"] == 0 and t["frac_within_1e-4"] == 1.0 and t["max"] < 1e-15
+    assert t["kept_both"] == 36143 and t["normals_bit_equal"] == 35786
+    assert t["beyond_1e-4"] == 2 and t["max"] < 1e-2
     a = table["attribution"]
-    assert a["points_differing_at_all"] == 345 and a["large_points"] == 0
-    assert a["sample:exp"]["vs_strict"]["normals_bit_equal"] == 0  # libm's exp alone explains none
+    assert a["points_differing_at_all"] == 357 and a["large_points"] == 2
+    assert a["large:sin"]["vs_strict"]["normals_bit_equal"] == 2  # libm's sin explains both large moves
+    assert a["large:exp"]["vs_strict"]["normals_bit_equal"] == 0
+    assert a["sample:exp"]["vs_strict"]["normals_bit_equal"] <= 1
     assert a["sample:sin+cos"]["vs_strict"]["normals_bit_equal"] > a["sample:sin"]["vs_strict"]["normals_bit_equal"]
 
 
 def test_tree_mode_gate_fails(table):
     """VERDICT r04 item 1's gate for the tree-reduction mode (DETMATH | TREE | GRAM against the
-    default order, all 71,223 inliers): it asks for identical statuses and every kept normal within
-    1e-4.  22 points change keep/drop and 7,507 of the 36,140 kept by both move past 1e-4 (median
+    default order, all 71,238 inliers): it asks for identical statuses and every kept normal within
+    1e-4.  9 points change keep/drop and 7,529 of the 36,139 kept by both move past 1e-4 (median
     3e-14), so the mode stays opt-in."""
     t = table["tree_gram_vs_detmath"]
-    assert t["keep_drop_changed"] == 22 and t["beyond_1e-4"] == 7507 and t["kept_both"] == 36140
+    assert t["keep_drop_changed"] == 9 and t["beyond_1e-4"] == 7529 and t["kept_both"] == 36139
 
 
 def test_pinned_subset_reruns_bitwise(orc, fx):

@@ -73,6 +73,63 @@ def diff(base, other):
     }
 
 
+def attribute(run, pts, base, strict, d_strict):
+    """libm for one function at a time, on the points where STRICT and DETMATH differ by more than 1e-9
+    or in status ("large"), and on 2,000 seeded points among those that differ at all (a status, or
+    the normal of a point both keep)"""
+    anyd = (base["status"] != strict["status"]) | (d_strict != 0)
+    large = np.flatnonzero((base["status"] != strict["status"]) | (d_strict > 1e-9))
+    rng0 = np.random.default_rng(11)
+    some = np.flatnonzero(anyd)
+    some = np.sort(rng0.choice(some, min(2000, len(some)), replace=False)) if len(some) else some
+    attribution = {"points_differing_at_all": int(anyd.sum()), "large_points": int(len(large)),
+                   "sample_points": int(len(some))}
+    for tag, sel in (("large", large), ("sample", some)):
+        if not len(sel):
+            continue
+        sub = pts[sel]
+        bsub = {k: base[k][sel] for k in ("status", "normals", "nfev")}
+        ssub = {k: strict[k][sel] for k in ("status", "normals", "nfev")}
+        for name, bit in list(LIBM.items()) + [("sin+cos", LIBM["sin"] | LIBM["cos"])]:
+            r = run(orc.DETMATH | bit, sub)
+            attribution[f"{tag}:{name}"] = {"vs_detmath": diff(bsub, r)[1], "vs_strict": diff(ssub, r)[1]}
+    return attribution
+
+
+def attribution_only(args, fp, wl, pts, R2, t2, t0):
+    """the attribution again from the saved per-point arrays: DETMATH and STRICT re-run on the chosen
+    points only (they are deterministic), then the libm variants"""
+    fx = np.load(args.fixture, allow_pickle=False)
+    sb, ss, d_strict = fx["status_detmath"].astype(np.int32), fx["status_strict"].astype(np.int32), fx["dn_strict"]
+    assert len(sb) == len(pts)
+
+    def run(mode, P):
+        t = time.time()
+        r = orc.optimize_normals(fp.cam, R2, t2, fp.img1, fp.img2, wl["levels"], P, wl["ray"], mode=mode,
+                                 nthreads=args.threads)
+        print(f"  mode {mode}: {len(P)} points ({time.time() - t:.0f} s)", flush=True)
+        return r
+
+    anyd = (sb != ss) | (d_strict != 0)
+    cand = np.flatnonzero(anyd)
+    rb, rs = run(orc.DETMATH, pts[cand]), run(orc.STRICT, pts[cand])
+    assert np.array_equal(rb["status"], sb[cand]) and np.array_equal(rs["status"], ss[cand])
+    nb = np.zeros((len(pts), 3))
+    ns = np.zeros((len(pts), 3))
+    nb[cand], ns[cand] = rb["normals"], rs["normals"]
+    fb = np.ones((len(pts), 8), dtype=np.int32)
+    base = dict(status=sb, normals=nb, nfev=fb)
+    strict = dict(status=ss, normals=ns, nfev=fb)
+    attribution = attribute(lambda mode, P: run(mode, P), pts, base, strict, d_strict)
+    with open(args.out) as f:
+        out = json.load(f)
+    out["attribution"] = attribution
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(attribution, indent=1)[:3000])
+    print(f"-> {args.out} ({time.time() - t0:.0f} s)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=len(os.sched_getaffinity(0)))
@@ -81,6 +138,8 @@ def main():
     ap.add_argument("--limit", type=int, default=0, help="first N inliers only (a dry run)")
     ap.add_argument("--reuse-base", action="store_true",
                     help="take the DETMATH run from full_c4.npz + dlt_parity_c4.npz instead of running it")
+    ap.add_argument("--attribution-only", action="store_true",
+                    help="redo only the attribution runs, from the per-point arrays of --fixture and the table of --out")
     args = ap.parse_args()
     wl = mff.WORKLOADS["c4"]
     t0 = time.time()
@@ -100,6 +159,8 @@ def main():
         print(f"  mode {mode}: {int((r['status'] == 0).sum())} kept ({r['seconds']:.0f} s)", flush=True)
         return r
 
+    if args.attribution_only:
+        return attribution_only(args, fp, wl, pts, R2, t2, t0)
     dlt_par = os.path.join(ROOT, "tests", "golden", "dlt_parity_c4.npz")
     if args.reuse_base and not args.limit and os.path.exists(dlt_par):
         # the DETMATH run over every inlier is tools/dlt_parity.py's (its per-match statuses and the
@@ -124,24 +185,7 @@ def main():
     d_tree, t_tree = diff(base, tree)
     _, t_tree_strict = diff(strict, tree)
 
-    # attribution: libm for one function at a time, on the points where STRICT and DETMATH differ by
-    # more than 1e-9 or in status ("large"), and on 2,000 seeded points among those that differ at all
-    anyd = (base["status"] != strict["status"]) | (np.abs(base["normals"] - strict["normals"]).max(axis=1) != 0)
-    large = np.flatnonzero((base["status"] != strict["status"]) | (d_strict > 1e-9))
-    rng0 = np.random.default_rng(11)
-    some = np.flatnonzero(anyd)
-    some = np.sort(rng0.choice(some, min(2000, len(some)), replace=False)) if len(some) else some
-    attribution = {"points_differing_at_all": int(anyd.sum()), "large_points": int(len(large)),
-                   "sample_points": int(len(some))}
-    for tag, sel in (("large", large), ("sample", some)):
-        if not len(sel):
-            continue
-        sub = pts[sel]
-        bsub = {k: base[k][sel] for k in ("status", "normals", "nfev")}
-        ssub = {k: strict[k][sel] for k in ("status", "normals", "nfev")}
-        for name, bit in list(LIBM.items()) + [("sin+cos", LIBM["sin"] | LIBM["cos"])]:
-            r = run(orc.DETMATH | bit, sub)
-            attribution[f"{tag}:{name}"] = {"vs_detmath": diff(bsub, r)[1], "vs_strict": diff(ssub, r)[1]}
+    attribution = attribute(run, pts, base, strict, d_strict)
 
     # the pinned subset: the 16 largest STRICT moves, the 16 largest tree moves, 32 seeded random
     rng = np.random.default_rng(5)
