@@ -334,9 +334,9 @@ int staging_wait(fm3d_ctx* c) {
     return FM3D_OK;
 }
 
-// bytes from a host array to a device buffer through the pinned staging buffer h
-// Large arrays go in 1 MiB pieces: the host copies piece k + 1 into the staging buffer while the DMA
-// engine moves piece k, so the two overlap instead of adding up (C2's float rows from host memory)
+// bytes from a host array to a device buffer through the pinned staging buffer h: one memcpy, one
+// DMA copy (1 MiB pieces issued as they were copied, and the memcpy split over host threads, were
+// both slower on the C2 and C4 lines)
 int upload_pinned(fm3d_ctx* c, DevBuf& dst, HostBuf& h, const void* src, size_t bytes) {
     HIPCHK(c, dst.ensure(bytes));
     if (!bytes) return FM3D_OK;
