@@ -43,7 +43,7 @@ EXPORTS = (
     "fm3d_mgpu_pipeline_upload", "fm3d_mgpu_pipeline_run", "fm3d_share_queries", "fm3d_merge_shares",
     "fm3d_plane_to_image2", "fm3d_pipeline_submit", "fm3d_pipeline_wait",
     "fm3d_mgpu_submit", "fm3d_mgpu_wait", "fm3d_pipeline_link", "fm3d_freak_compute", "fm3d_freak_set_pairs",
-    "fm3d_mser_detect", "fm3d_mser_detect_batch", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt",
+    "fm3d_mser_detect", "fm3d_mser_detect_batch", "fm3d_mser_regions", "fm3d_pipeline_submit_dlt", "fm3d_pipeline_submit_dlt_pair",
     "fm3d_pipeline_submit_ncc", "fm3d_pipeline_wait_ncc", "fm3d_pipeline_wait_dlt", "fm3d_device_count",
 )
 
@@ -936,6 +936,18 @@ class Pipeline:
     def submit_dlt(self) -> None:
         """fm3d_pipeline_submit_dlt: C2's path queued on the context stream (returns at once)"""
         self.ctx.check(lib().fm3d_pipeline_submit_dlt(self.ctx.handle))
+
+    def submit_dlt_pair(self, desc_a, desc_b, kp1, kp2, binary=False, query_offset=0) -> None:
+        """fm3d_pipeline_submit_dlt_pair: stage a pair from host memory (no images) and queue C2's path,
+        with no host wait (float rows are checked on the device; wait_dlt redoes non-integer ones)"""
+        a = np.ascontiguousarray(desc_a)
+        b = np.ascontiguousarray(desc_b)
+        k1 = np.ascontiguousarray(kp1, dtype=np.float32)
+        k2 = np.ascontiguousarray(kp2, dtype=np.float32)
+        self.n_queries = a.shape[0]
+        self.ctx.check(lib().fm3d_pipeline_submit_dlt_pair(self.ctx.handle, _vp(a), a.shape[0], _vp(b), b.shape[0],
+                                                           a.shape[1], _desc_type(a, binary), _vp(k1), _vp(k2),
+                                                           query_offset))
 
     def wait_dlt(self):
         """fm3d_pipeline_wait_dlt: (n_inliers, stats dict) of the submitted front half"""

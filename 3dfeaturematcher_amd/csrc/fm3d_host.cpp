@@ -110,6 +110,7 @@ struct fm3d_ctx {
     DevBuf partIdx, partKey;  // per-part top-2 lists of the split matchers
     DevBuf A8, B8;            // binary rows unpacked to int8 for the MFMA matcher; u8 rows packed from floats
     DevBuf u8Flag;            // launch_f32_pack_u8's "not integer-valued" flag
+    bool specU8 = false;      // the staged float rows went to the u8 matcher before their flag was read
     // SURF detection / description
     DevBuf sfImg, sfSum, sfDet, sfTr, sfLayers, sfMids, sfCand, sfCount, sfSortTmp, sfFlag, sfPos, sfKp, sfKin, sfSrc,
         sfDesc, sfDW, sfAng;
@@ -361,10 +362,11 @@ void pad_u8(uint8_t* o, const uint8_t* x, int n, int dim, int dimPad) {
 // orders every later use); returns the effective kernel type
 // (waitStaging false: the caller waited for the staging buffers already, stage_pipeline)
 int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
-                      int* effType, int* dimPad, bool waitStaging = true) {
+                      int* effType, int* dimPad, bool waitStaging = true, bool speculate = false) {
     if (dim <= 0 || nA < 0 || nB < 0) return fail(c, FM3D_ERR_INVALID, "bad descriptor shape");
     int r;
     if (waitStaging && (r = staging_wait(c))) return r;
+    c->specU8 = false;
     int t = type;
     if (type == FM3D_DESC_F32 && ((dim + 127) / 128) * 128 <= 256) {
         // float rows as the reference hands them to knnMatch (descriptorsmatcher.cpp:114-117): to the
@@ -385,7 +387,19 @@ int stage_descriptors(fm3d_ctx* c, const void* descA, int nA, const void* descB,
         fm3d::launch_f32_pack_u8(c->A.as<float>(), nA, c->B.as<float>(), nB, dim, dp, c->A8.as<uint8_t>(),
                                  c->B8.as<uint8_t>(), c->u8Flag.as<int>(), c->stream);
         HIPCHK(c, hipGetLastError());
+        *c->hFlag.as<int>() = -1;  // "not arrived" (the previous pair's copies into it have run: staging_wait)
         HIPCHK(c, hipMemcpyAsync(c->hFlag.p, c->u8Flag.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        if (speculate) {
+            // no host wait (fm3d_pipeline_submit_dlt_pair): the u8 matcher runs on the packed rows, and
+            // the wait re-runs the front half on the float rows if the flag then says they were not
+            // integers (redo_float_front)
+            std::swap(c->A, c->A8);
+            std::swap(c->B, c->B8);
+            *dimPad = dp;
+            *effType = FM3D_DESC_U8;
+            c->specU8 = true;
+            return FM3D_OK;
+        }
         HIPCHK(c, hipEventRecord(c->evStage, c->stream));
         HIPCHK(c, hipEventSynchronize(c->evStage));
         if (*c->hFlag.as<int>() == 0) {
@@ -2018,13 +2032,13 @@ namespace {
 // descriptors, keypoints, both images and their pyramids (a6, normaloptimizer.cpp:206-221)
 int stage_pipeline(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim, int type,
                    const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, const uint8_t* img1, const uint8_t* img2,
-                   int width, int height, int queryOffset) {
+                   int width, int height, int queryOffset, bool speculate = false) {
     if (!kpts1 || !kpts2) return fail(c, FM3D_ERR_INVALID, "null argument");
     int t, dp, r;
     // the previous pair's copies out of the staging buffers have run: one wait, then every H2D of
     // this pair is queued without another (the call returns before they execute)
     if ((r = staging_wait(c))) return r;
-    if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp, false))) return r;
+    if ((r = stage_descriptors(c, descA, nA, descB, nB, dim, type, &t, &dp, false, speculate))) return r;
     if ((r = upload_pinned(c, c->kp1, c->hK1, kpts1, (size_t)nA * sizeof(fm3d_point2f)))) return r;
     if ((r = upload_pinned(c, c->kp2, c->hK2, kpts2, (size_t)nB * sizeof(fm3d_point2f)))) return r;
     if (img1 || img2) {
@@ -2396,10 +2410,10 @@ int fm3d_internal_prepare(fm3d_ctx* c) {  // the device count buffer, before a c
 
 extern "C" {
 
-int fm3d_pipeline_submit_dlt(fm3d_ctx* c) {
-    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
-    PENDING_CHECK(c);
-    hipSetDevice(c->device);
+}  // extern "C"
+namespace {
+// the staged pair's front half with its counts written to page-locked memory by the DLT kernel
+int queue_front_counts(fm3d_ctx* c) {
     int r;
     HIPCHK(c, c->hSmall.ensure(sizeof(PipeSmall)));
     PipeSmall* hs = c->hSmall.as<PipeSmall>();
@@ -2411,6 +2425,51 @@ int fm3d_pipeline_submit_dlt(fm3d_ctx* c) {
     c->frontHostCnt = nullptr;
     if (r) return r;
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    return FM3D_OK;
+}
+
+// after a speculative front half (stage_descriptors' speculate): when the pack kernel flagged an
+// element that is not an integer in [0, 255], the float rows (still on the device) go through the
+// float matchers and the front half runs again, as the non-speculative staging would have run it
+int redo_float_front(fm3d_ctx* c) {
+    if (!c->specU8) return FM3D_OK;
+    c->specU8 = false;
+    const int flag = *c->hFlag.as<int>();
+    if (flag == 0) return FM3D_OK;
+    if (flag < 0) return fail(c, FM3D_ERR_HIP, "the float rows' flag never arrived");
+    std::swap(c->A, c->A8);
+    std::swap(c->B, c->B8);
+    c->stType = FM3D_DESC_F32;
+    c->stDimPad = c->stDim;
+    int r;
+    if ((r = queue_front_counts(c))) return r;
+    HIPCHK(c, hipEventSynchronize(c->ev[1]));
+    return FM3D_OK;
+}
+}  // namespace
+extern "C" {
+
+int fm3d_pipeline_submit_dlt(fm3d_ctx* c) {
+    if (!c || !c->staged) return fail(c, FM3D_ERR_INVALID, "fm3d_pipeline_upload not called");
+    PENDING_CHECK(c);
+    hipSetDevice(c->device);
+    int r;
+    if ((r = queue_front_counts(c))) return r;
+    c->pending = true;
+    c->pendingDlt = true;
+    return FM3D_OK;
+}
+
+int fm3d_pipeline_submit_dlt_pair(fm3d_ctx* c, const void* descA, int nA, const void* descB, int nB, int dim,
+                                  int type, const fm3d_point2f* kpts1, const fm3d_point2f* kpts2, int queryOffset) {
+    if (!c) return FM3D_ERR_INVALID;
+    PENDING_CHECK(c);
+    hipSetDevice(c->device);
+    int r;
+    if ((r = stage_pipeline(c, descA, nA, descB, nB, dim, type, kpts1, kpts2, nullptr, nullptr, 0, 0, queryOffset,
+                            true)))
+        return r;
+    if ((r = queue_front_counts(c))) return r;
     c->pending = true;
     c->pendingDlt = true;
     return FM3D_OK;
@@ -2424,6 +2483,8 @@ int fm3d_pipeline_wait_dlt(fm3d_ctx* c, int* nInliers, fm3d_pipeline_stats* stat
     c->pending = false;
     c->pendingDlt = false;
     HIPCHK(c, hipEventSynchronize(ev[1]));
+    int r;
+    if ((r = redo_float_front(c))) return r;
     const PipeSmall* hs = c->hSmall.as<PipeSmall>();
     const int K = hs->cnt[0], P = hs->cnt[1];
     c->stK = K;

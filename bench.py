@@ -902,8 +902,8 @@ def run_c2(args):
     # a serving loop: `inflight` contexts (one HIP stream each) with the pair resident, a frame pair
     # submitted on one while the previous ones run (fm3d_pipeline_submit_dlt / wait_dlt); the
     # synchronous step (run_dlt, one host wait per pair) is timed beside it.  --io host: every step
-    # also stages the pair from host memory (fm3d_pipeline_upload without images: C2 needs none) and
-    # downloads its matches and inlier points
+    # also stages the pair from host memory (fm3d_pipeline_submit_dlt_pair: staging and the front half
+    # queued without a host wait; C2 needs no images) and downloads its matches and inlier points
     nf = max(1, args.inflight)
     ctxs = [fm3d.Context(s) for _ in range(nf)]
     pipes = []
@@ -943,9 +943,10 @@ def run_c2(args):
         if busy[k]:
             total += finish(k)
         t_sub[k] = time.perf_counter()
-        if host_io:
-            pipes[k].upload(d1, d2, pair.kp1, pair.kp2, None, None)
-        pipes[k].submit_dlt()
+        if host_io:  # staged and queued with no host wait (fm3d_pipeline_submit_dlt_pair)
+            pipes[k].submit_dlt_pair(d1, d2, pair.kp1, pair.kp2)
+        else:
+            pipes[k].submit_dlt()
         busy[k] = True
     for j in range(args.steps, args.steps + nf):
         k = j % nf
@@ -988,7 +989,8 @@ def run_c2(args):
                                        "and packed to u8 on the device)" if args.desc_dtype == "f32" else "u8"),
                    "io": args.io,
                    "timed": (f"K frame pairs, each from host memory to host memory: descriptors + keypoints "
-                             f"staged (pinned, H2D{', device integer check + u8 pack' if args.desc_dtype == 'f32' else ''}), "
+                             f"staged (pinned, H2D{', device integer check + u8 pack' if args.desc_dtype == 'f32' else ''}; "
+                             f"fm3d_pipeline_submit_dlt_pair, no host wait), "
                              f"match -> NNDR -> compaction -> DLT -> compaction, matches + inlier points D2H; "
                              f"{nf} contexts (HIP streams) in flight" if host_io else
                              f"K frame pairs through match -> NNDR -> compaction -> DLT -> compaction on "

@@ -505,6 +505,14 @@ int fm3d_pipeline_run_dlt(fm3d_ctx *ctx, int *nInliers, fm3d_pipeline_stats *sta
    fm3d_pipeline_run_dlt.  Until the wait the other pipeline calls on the context fail. */
 int fm3d_pipeline_submit_dlt(fm3d_ctx *ctx);
 int fm3d_pipeline_wait_dlt(fm3d_ctx *ctx, int *nInliers, fm3d_pipeline_stats *stats);
+/* fm3d_pipeline_upload (no images) + fm3d_pipeline_submit_dlt in one call that never waits for the
+   device: a serving loop of C2 from host memory overlaps one context's staging copy with another's
+   DMA.  Float rows (FM3D_DESC_F32) are packed on the device and matched as u8 rows before their
+   "integer-valued" flag is read; fm3d_pipeline_wait_dlt reads it and, for rows that are not, runs the
+   front half again on the float rows, so the results are always those of fm3d_pipeline_upload +
+   fm3d_pipeline_run_dlt.  The arrays are copied before it returns.  (Round 6.) */
+int fm3d_pipeline_submit_dlt_pair(fm3d_ctx *ctx, const void *descA, int nA, const void *descB, int nB, int dim,
+                                  int type, const fm3d_point2f *kpts1, const fm3d_point2f *kpts2, int queryOffset);
 /* after fm3d_pipeline_run(_dlt): the compacted matches (K), the inlier points (P x 3 doubles, the
    z-filtered triangulation in match order) and each point's match index (P); any may be NULL */
 int fm3d_pipeline_dlt_download(fm3d_ctx *ctx, fm3d_dmatch *matches, double *points, int32_t *matchIdx);

@@ -236,6 +236,62 @@ def test_pipeline_float_sift_rows_packed_on_device(fm3d, orc, synth):
         ctx.close()
 
 
+def test_submit_dlt_pair_equals_upload_and_run_dlt(fm3d, orc, synth):
+    """fm3d_pipeline_submit_dlt_pair (C2 from host memory without a host wait; bench.py --workload
+    c2 --io host): u8 rows, integer float rows (packed on the device and matched as u8 before their
+    flag is read) and float rows with one non-integer element (wait_dlt reads the flag and runs
+    the front half again on the float rows), on two contexts in flight, interleaved.  Each pair's
+    matches and points equal fm3d_pipeline_upload + run_dlt of the same rows, and the oracle's."""
+    pair = synth.make_frame_pair(4000, seed=35)
+    s = fm3d.Settings.default()
+    s.set_camera(pair.cam)
+    s.nndrEpsilon = 0.55
+    f1 = pair.desc1.astype(np.float32)
+    f2 = pair.desc2.astype(np.float32)
+    g2 = f2.copy()
+    g2[23, 7] += 0.5
+    cases = {"u8": (pair.desc1, pair.desc2), "f32": (f1, f2), "f32_frac": (f1, g2)}
+    ctxs = [fm3d.Context(s) for _ in range(2)]
+    try:
+        pipes = []
+        for ctx in ctxs:
+            fm3d.SingleCameraTriangulator(ctx).set_g12(pair.g12)
+            pipes.append(fm3d.Pipeline(ctx))
+        ref = {}
+        for name, (a, b) in cases.items():
+            pipes[0].upload(a, b, pair.kp1, pair.kp2, None, None)
+            P, st = pipes[0].run_dlt()
+            m, pts, src = pipes[0].dlt_results(st["matches"], st["inliers"])
+            ref[name] = (m.copy(), pts.copy(), src.copy())
+        order = ["f32", "f32_frac", "u8", "f32_frac", "f32", "u8", "f32", "f32_frac"]
+        pend = [None, None]
+        got = []
+        for i, name in enumerate(order + [None, None]):
+            k = i % 2
+            if pend[k] is not None:
+                P, st = pipes[k].wait_dlt()
+                m, pts, src = pipes[k].dlt_results(st["matches"], st["inliers"])
+                got.append((pend[k], m.copy(), pts.copy(), src.copy()))
+                pend[k] = None
+            if name is not None:
+                a, b = cases[name]
+                pipes[k].submit_dlt_pair(a, b, pair.kp1, pair.kp2)
+                pend[k] = name
+        assert len(got) == len(order)
+        for name, m, pts, src in got:
+            rm, rp, rs = ref[name]
+            assert m.tobytes() == rm.tobytes() and pts.tobytes() == rp.tobytes() and src.tobytes() == rs.tobytes(), name
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    q, t, dist = orc.match_nndr(pair.desc1, pair.desc2, orc.U8, 0.55, oracle_threads())
+    assert np.array_equal(ref["f32"][0]["queryIdx"], q) and np.array_equal(ref["f32"][0]["distance"], dist)
+    qf, tf, df = orc.match_nndr(f1, g2, orc.F32, 0.55, oracle_threads())
+    assert np.array_equal(ref["f32_frac"][0]["queryIdx"], qf) and np.array_equal(ref["f32_frac"][0]["trainIdx"], tf)
+    assert np.array_equal(ref["f32_frac"][0]["distance"], df)
+    assert len(ref["u8"][1]) > 1000
+
+
 def test_pipeline_no_images_full_path_fails_cleanly(fm3d, synth):
     """a context staged without images runs C2's front half; the full path refuses (no pyramids)"""
     pair = synth.make_frame_pair(1500, seed=32)
