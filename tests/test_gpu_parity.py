@@ -233,6 +233,43 @@ def test_triangulate_legacy_solver_bitwise(fm3d, orc, pair):
     assert np.array_equal(maskn, mask) and not np.array_equal(ptn, pts)
 
 
+def test_triangulate_degenerate_systems_bitwise(fm3d, orc, pair):
+    """OpenCV's JacobiSVD where its branches matter: DLT systems with zero and repeated singular
+    values. Cases: a pure rotation (t = 0, so the 6 x 4 system has a zero column), the same keypoint
+    in both views, both keypoints at the principal point, keypoints far outside the frame, and
+    repeated matches. With the z filter opened wide, every point and mask bit equals the oracle's
+    (NaN included)."""
+    rng = np.random.default_rng(41)
+    n = 512
+    kp1 = np.ascontiguousarray(rng.uniform(0, 640, (n, 2)).astype(np.float32))
+    kp2 = np.ascontiguousarray(rng.uniform(0, 480, (n, 2)).astype(np.float32))
+    cx, cy = pair.cam.cx, pair.cam.cy
+    kp2[:64] = kp1[:64]                                 # the same pixel in both views
+    kp1[64:96] = kp2[64:96] = (np.float32(cx), np.float32(cy))  # the principal point
+    kp1[96:128] *= np.float32(1e4)                      # far outside the frame
+    kp2[128:160] = np.float32(-3e5)
+    m = np.zeros(n + 64, dtype=fm3d.DMATCH)
+    m["queryIdx"][:n] = np.arange(n)
+    m["trainIdx"][:n] = np.arange(n)
+    m["queryIdx"][n:] = 7                               # repeated matches
+    m["trainIdx"][n:] = 9
+    g_rot = np.array(pair.g12, dtype=np.float64).copy()
+    g_rot[:3, 3] = 0.0
+    c = fm3d.Context(_settings(fm3d, pair.cam, pixelsRay=16, zThresholdMin=-1e300, zThresholdMax=1e300))
+    try:
+        for g in (np.asarray(pair.g12, dtype=np.float64), g_rot):
+            sct = fm3d.SingleCameraTriangulator(c)
+            sct.set_g12(g)
+            sct.setKeypoints(kp1, kp2, m)
+            pts, mask = sct.triangulate()
+            pto, masko = orc.triangulate(pair.cam, g, -1e300, 1e300, kp1, kp2, m["queryIdx"], m["trainIdx"])
+            assert np.array_equal(mask, masko)
+            assert np.array_equal(pts, pto, equal_nan=True)
+            assert mask.sum() > n // 2
+    finally:
+        c.close()
+
+
 def test_pyramid_bitwise(fm3d, orc, ctx, pair):
     no = fm3d.NormalOptimizer(ctx)
     no.setImages(pair.img1, pair.img2)
